@@ -1,0 +1,624 @@
+// oracle/az_oracle.cpp -- TEST INFRASTRUCTURE ONLY.
+//
+// CPU restatement of the reference self-play hot path in "Mode S" (SURVEY.md
+// Appendix A): GomokuState rules/features/hash, ParallelMCTS sequential simulation
+// (numThreads=1, setDeterministicMode(true)), TranspositionTable, Dirichlet noise,
+// and the SelfPlayManager::playSingleGame move loop.  Only tests/, bench.py's
+// cpu_baseline leg and __graft_entry__.smoke() may load it, and only as the checker.
+// It is pinned against golden vectors produced by the patched reference
+// (oracle/build_ref.sh -> oracle/_ref/ref_harness -> tests/golden/).
+//
+// Every function cites the reference lines (paths relative to the reference root)
+// it restates.  fp32 arithmetic is written in the reference's evaluation order;
+// compile WITHOUT FMA contraction (-ffp-contract=off), as the reference is built.
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <limits>
+#include <random>
+#include <sstream>
+#include <string>
+#include <unordered_map>
+#include <unordered_set>
+#include <vector>
+
+namespace {
+
+uint32_t fbits(float f) { uint32_t u; std::memcpy(&u, &f, 4); return u; }
+
+uint64_t splitmix64(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ULL;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBULL;
+    return x ^ (x >> 31);
+}
+
+enum GameResult { ONGOING = 0, DRAW = 1, WIN_P1 = 2, WIN_P2 = 3 };   // igamestate.h:26-31
+
+// ---------------------------------------------------------------------------
+// Zobrist keys: ZobristHash(bs, 2 piece types, 2 players, seed)
+// (src/core/zobrist_hash.cpp:9-36): mt19937_64(seed); piece[p][pos] then player[p].
+struct Zobrist {
+    std::vector<uint64_t> piece;   // [2][A]
+    uint64_t player[2];
+    Zobrist(int A, unsigned seed) : piece(2 * A) {
+        std::mt19937_64 rng(seed);
+        for (int p = 0; p < 2; ++p)
+            for (int a = 0; a < A; ++a) piece[p * A + a] = rng();
+        player[0] = rng(); player[1] = rng();
+    }
+};
+
+// ---------------------------------------------------------------------------
+// GomokuState (src/games/gomoku/gomoku_state.cpp), standard rules (no Renju/Omok/pro-long).
+struct State {
+    int bs, A;
+    std::vector<int8_t> cell;      // 0 empty, 1 black, 2 white
+    int player = 1;                // current_player, BLACK=1 moves first (:20)
+    std::vector<int> history;      // move_history (:718)
+    int stones = 0;
+    bool fresh = true;             // unordered_set never grown yet
+    const Zobrist* z;
+    State(int bs_, const Zobrist* z_) : bs(bs_), A(bs_ * bs_), cell(bs_ * bs_, 0), z(z_) {}
+
+    // count_direction (gomoku_rules.cpp:98-115)
+    int count_dir(int x, int y, int dx, int dy, int p) const {
+        int c = 0;
+        while (x >= 0 && x < bs && y >= 0 && y < bs && cell[x * bs + y] == p) { ++c; x += dx; y += dy; }
+        return c;
+    }
+    // check_line_for_five (gomoku_rules.cpp:62-96): BLACK needs exactly 5, WHITE >= 5.
+    bool five_at(int a, int p) const {
+        if (cell[a] != p) return false;
+        int x = a / bs, y = a % bs;
+        static const int D[4][2] = {{0, 1}, {1, 0}, {1, 1}, {1, -1}};
+        for (auto& d : D) {
+            int len = count_dir(x, y, d[0], d[1], p) + count_dir(x, y, -d[0], -d[1], p) - 1;
+            if (p == 1 ? len == 5 : len >= 5) return true;
+        }
+        return false;
+    }
+    // refresh_winner_cache (gomoku_state.cpp:477-489): full-board scan, BLACK first.
+    int winner() const {
+        for (int p : {1, 2})
+            for (int a = 0; a < A; ++a)
+                if (cell[a] == p && five_at(a, p)) return p;
+        return 0;
+    }
+    // is_terminal (:491-504) / getGameResult (:189-201)
+    GameResult result() const {
+        int w = winner();
+        if (w == 1) return WIN_P1;
+        if (w == 2) return WIN_P2;
+        if (stones >= A) return DRAW;   // is_stalemate: no empty cell (:506-521)
+        return ONGOING;
+    }
+    bool terminal() const { return result() != ONGOING; }
+    // get_valid_moves (:531-578): iteration order of the cached unordered_set<int>.
+    // A fresh state's first query grows the set from one bucket (libstdc++ 11
+    // prime rehash policy); every later refresh clears and re-inserts ascending into
+    // a table with > A buckets, which iterates in strictly descending order.
+    std::vector<int> legal() const {
+        std::vector<int> out;
+        if (fresh) {
+            std::unordered_set<int> s;
+            for (int a = 0; a < A; ++a) if (!cell[a]) s.insert(a);
+            out.assign(s.begin(), s.end());
+        } else {
+            for (int a = A - 1; a >= 0; --a) if (!cell[a]) out.push_back(a);
+        }
+        return out;
+    }
+    // make_move (:681-722)
+    void play(int a) {
+        cell[a] = (int8_t)player;
+        player = 3 - player;
+        history.push_back(a);
+        ++stones;
+        fresh = false;
+    }
+    // compute_hash_signature (:620-656)
+    uint64_t hash() const {
+        uint64_t h = 0;
+        for (int a = 0; a < A; ++a) {
+            if (cell[a] == 1) h ^= z->piece[a];
+            else if (cell[a] == 2) h ^= z->piece[A + a];
+        }
+        return h ^ z->player[player - 1];
+    }
+    // getEnhancedTensorRepresentation (:207-258, to_tensor :811-840, get_previous_moves :852-869)
+    void planes(float* out) const {   // [11][bs][bs]
+        std::fill(out, out + 11 * A, 0.0f);
+        int me = player, opp = 3 - player;
+        for (int a = 0; a < A; ++a) {
+            if (cell[a] == me) out[a] = 1.0f;
+            else if (cell[a] == opp) out[A + a] = 1.0f;
+        }
+        if (player == 1) for (int a = 0; a < A; ++a) out[2 * A + a] = 1.0f;
+        for (int pl : {1, 2}) {   // BLACK list -> planes 3..5, WHITE list -> 6..8
+            int found = 0;
+            int n = (int)history.size();
+            for (int i = n - 1; i >= 0 && found < 3; --i) {
+                int mp = ((n - i) % 2 == 1) ? player : 3 - player;   // reference's parity rule (:860)
+                if (mp == pl) { out[(pl == 1 ? 3 : 6) * A + found * A + history[i]] = 1.0f; ++found; }
+            }
+        }
+        for (int x = 0; x < bs; ++x)
+            for (int y = 0; y < bs; ++y) {
+                out[9 * A + x * bs + y] = (float)x / (bs - 1);
+                out[10 * A + x * bs + y] = (float)y / (bs - 1);
+            }
+    }
+};
+
+// ---------------------------------------------------------------------------
+// Evaluators
+struct Evaluator {
+    virtual ~Evaluator() {}
+    virtual void eval(int game, const State& s, std::vector<float>& policy, float& value) = 0;
+    long calls = 0;
+};
+
+// HashEvaluator (same definition as oracle/ref_harness.cpp hash_eval)
+struct HashEval : Evaluator {
+    void eval(int, const State& s, std::vector<float>& p, float& v) override {
+        ++calls;
+        uint64_t key = splitmix64(s.hash() ^ 0x5A17C0DEULL);
+        for (int i = 0; i < 6; ++i) {
+            int m = (i < (int)s.history.size()) ? s.history[s.history.size() - 1 - i] : -1;
+            key = splitmix64(key + (uint64_t)(uint32_t)(m + 2));
+        }
+        p.assign(s.A, 0.0f);
+        for (int a = 0; a < s.A; ++a) {
+            uint64_t r = splitmix64(key ^ ((uint64_t)(a + 1) * 0x9E3779B97F4A7C15ULL));
+            p[a] = (float)(uint32_t)(r >> 40) * (1.0f / 16777216.0f);
+        }
+        uint64_t rv = splitmix64(key ^ 0x76A1ULL);
+        v = ((float)(int32_t)(uint32_t)(rv >> 40) - 8388608.0f) * (1.0f / 8388608.0f);
+    }
+};
+
+// RandomPolicyNetwork (src/nn/random_policy_network.cpp:9-24,93-138), one instance per game.
+struct RandomEval : Evaluator {
+    std::vector<std::mt19937> rng;
+    RandomEval(int games, unsigned seed) { for (int g = 0; g < games; ++g) rng.emplace_back(seed + g); }
+    void eval(int game, const State& s, std::vector<float>& p, float& v) override {
+        ++calls;
+        std::uniform_real_distribution<float> dist(0.0f, 1.0f);
+        p.assign(s.A, 0.001f);
+        float sum = 0.0f;
+        auto legal = s.legal();
+        for (int m : legal) { p[m] = dist(rng[game]); sum += p[m]; }
+        if (sum > 0.0f) for (int i = 0; i < s.A; ++i) p[i] /= sum;
+        else if (!legal.empty()) { float u = 1.0f / (float)legal.size(); for (int m : legal) p[m] = u; }
+        std::uniform_real_distribution<float> vd(-0.1f, 0.1f);
+        v = vd(rng[game]);
+    }
+};
+
+// Network evaluator through a user callback: planes -> raw logits [A] + value; the
+// softmax of TorchNeuralNetwork::predictBatch (torch_neural_network.cpp:296-316) is
+// applied here.  Replay evaluator: the callback returns final (post-softmax) policy.
+typedef int (*az_eval_cb)(void* user, int game, const float* planes, int n_planes, int A,
+                          float* policy_out, float* value_out);
+struct CallbackEval : Evaluator {
+    az_eval_cb cb; void* user; bool softmax;
+    std::vector<float> buf;
+    CallbackEval(az_eval_cb c, void* u, bool sm) : cb(c), user(u), softmax(sm) {}
+    void eval(int game, const State& s, std::vector<float>& p, float& v) override {
+        ++calls;
+        buf.resize(11 * s.A);
+        s.planes(buf.data());
+        p.assign(s.A, 0.0f);
+        if (cb(user, game, buf.data(), 11, s.A, p.data(), &v) != 0) { std::fprintf(stderr, "eval cb failed\n"); std::abort(); }
+        if (softmax) {
+            float mx = *std::max_element(p.begin(), p.end());
+            float sum = 0.0f;
+            for (auto& x : p) { x = std::exp(x - mx); sum += x; }
+            if (sum > 0.0f) for (auto& x : p) x /= sum;
+        }
+    }
+};
+
+// ---------------------------------------------------------------------------
+// TranspositionTable (src/mcts/transposition_table.cpp:44-191, 405-439) with the
+// wall-clock age clause treated as never firing (ages < cacheEntryMaxAge = 60 s):
+// replacement of an occupied slot happens iff its visitCount < minVisits (5).
+struct TT {
+    struct E { uint64_t hash; std::vector<float> policy; float value; int visits; };
+    uint64_t mask;
+    std::unordered_map<uint64_t, E> slots;
+    long lookups = 0, hits = 0;
+    explicit TT(int log2) : mask((1ULL << log2) - 1) {}
+    bool lookup(uint64_t h, std::vector<float>& p, float& v) {
+        ++lookups;
+        auto it = slots.find(h & mask);
+        if (it != slots.end() && it->second.hash == h) {
+            p = it->second.policy; v = it->second.value; ++it->second.visits; ++hits;
+            return true;
+        }
+        return false;
+    }
+    void store(uint64_t h, const std::vector<float>& p, float v) {
+        auto it = slots.find(h & mask);
+        if (it != slots.end()) {
+            if (it->second.hash == h) { ++it->second.visits; return; }
+            if (it->second.visits >= 5) return;   // collision, kept
+        }
+        E& e = slots[h & mask];
+        e.hash = h; e.policy = p; e.value = v; e.visits = 1;
+    }
+};
+
+// ---------------------------------------------------------------------------
+// MCTSNode (include/alphazero/mcts/mcts_node.h:29-275) as a flat arena.
+struct Node {
+    int N = 0; float W = 0.0f; int VL = 0; float P = 0.0f;
+    int action = -1, parent = -1, first = -1, nchild = 0;
+    bool expanded = false, terminal = false;
+    GameResult result = ONGOING;
+};
+
+struct Cfg {
+    int bs = 9, sims = 100, max_moves = 1 << 30, vl = 3, noise_each_search = 0, temp_drop = 30;
+    float cpuct = 1.5f, fpu = 0.0f, alpha = 0.03f, eps = 0.25f, t_init = 1.0f, t_final = 0.0f;
+    unsigned noise_seed = 42, zobrist_seed = 12345;
+    int tt_log2 = 20;
+};
+
+float convert_value(GameResult r, int player) {   // parallel_mcts.cpp:973-985
+    switch (r) {
+        case WIN_P1: return player == 1 ? 1.0f : -1.0f;
+        case WIN_P2: return player == 2 ? 1.0f : -1.0f;
+        default: return 0.0f;
+    }
+}
+
+struct Search {
+    const Cfg& cfg;
+    int game;
+    Evaluator* ev;
+    TT tt;
+    std::vector<Node> nodes;
+    int root = 0;
+    State rootState;
+    std::mt19937 rng;
+    Search(const Cfg& c, int g, Evaluator* e, const Zobrist* z)
+        : cfg(c), game(g), ev(e), tt(c.tt_log2), rootState(c.bs, z), rng(c.noise_seed) {
+        nodes.emplace_back();     // root (parallel_mcts.cpp:68), parent = none
+        nodes.reserve(1 << 16);
+    }
+
+    void add_vl(Node& n) { n.N += cfg.vl; n.VL += cfg.vl; n.W = n.W - (float)cfg.vl; }      // mcts_node.cpp:168-181
+    void remove_vl(Node& n) { n.N -= cfg.vl; n.VL -= cfg.vl; n.W = n.W + (float)cfg.vl; }   // mcts_node.cpp:183-196
+
+    // getPuctScore (mcts_node.cpp:61-119); `depth` of the node being selected FROM
+    // relative to the current root decides the sign rule (:88-93).
+    float puct(const Node& c, const Node& parentNode, int parentDepth, int parentVisits) const {
+        int visits = c.N;
+        if (visits == 0) return std::numeric_limits<float>::max();
+        float q = 0.0f;
+        int act = visits - c.VL;
+        if (act > 0) q = c.W / (float)act;
+        else q = 0.0f;
+        if (parentDepth >= 1) {                 // parent && parent->parent
+            bool flip = (parentDepth == 1);     // nodePlayer = parent->parent->parent ? cp : 3-cp
+            if (flip) q = -q;
+        }
+        if (parentDepth >= 0 && act <= 0 && cfg.fpu > 0.0f) {   // c has a parent always
+            int pa = parentNode.N - parentNode.VL;
+            if (pa > 0) q = parentNode.W / (float)pa - cfg.fpu;
+            else q = -cfg.fpu;
+        }
+        float sq = std::sqrt((float)parentVisits);
+        float u = cfg.cpuct * c.P * sq / (1.0f + (float)visits);
+        float div = 0.0f;
+        if (visits < 5) div = 0.05f * (float)(5 - visits);
+        return q + u + div;
+    }
+
+    // expandNodeWithPolicy (parallel_mcts.cpp:681-745)
+    void expand(int ni, const State& s, const std::vector<float>& policy) {
+        if (nodes[ni].expanded || nodes[ni].terminal) return;
+        std::vector<int> legal = s.legal();
+        if (legal.empty()) {
+            nodes[ni].terminal = true; nodes[ni].result = s.result(); nodes[ni].expanded = true;
+            return;
+        }
+        float sum = 0.0f;
+        std::vector<float> lp(legal.size(), 0.0f);
+        for (size_t i = 0; i < legal.size(); ++i) {
+            int a = legal[i];
+            if (a >= 0 && a < (int)policy.size()) { lp[i] = policy[a]; sum += lp[i]; }
+        }
+        if (sum > 0.0f) for (auto& x : lp) x /= sum;
+        else { float u = 1.0f / (float)legal.size(); for (auto& x : lp) x = u; }
+        int first = (int)nodes.size();
+        for (size_t i = 0; i < legal.size(); ++i) {
+            Node c; c.P = lp[i]; c.action = legal[i]; c.parent = ni;
+            nodes.push_back(c);
+        }
+        nodes[ni].first = first; nodes[ni].nchild = (int)legal.size(); nodes[ni].expanded = true;
+    }
+
+    // evaluateState (parallel_mcts.cpp:835-917), direct-NN branch (Mode S)
+    void evaluate(const State& s, std::vector<float>& p, float& v) {
+        if (s.terminal()) {
+            v = convert_value(s.result(), s.player);
+            p.assign(s.A, 1.0f / (float)s.A);
+            return;
+        }
+        if (tt.lookup(s.hash(), p, v)) return;
+        ev->eval(game, s, p, v);
+    }
+
+    // expandNode (parallel_mcts.cpp:636-679)
+    void expand_node(int ni, const State& s) {
+        if (nodes[ni].expanded || nodes[ni].terminal) return;
+        if (s.legal().empty()) {
+            nodes[ni].terminal = true; nodes[ni].result = s.result(); nodes[ni].expanded = true;
+            return;
+        }
+        std::vector<float> p; float v;
+        if (!tt.lookup(s.hash(), p, v)) { evaluate(s, p, v); tt.store(s.hash(), p, v); }
+        expand(ni, s, p);
+    }
+
+    // runSingleSimulation (parallel_mcts.cpp:276-380) with selectLeafWithPath (:456-535)
+    // and selectChildPuct (:537-563), backpropagate(node, value, path) (:782-833).
+    void simulate() {
+        State s = rootState;
+        std::vector<int> path;
+        int ni = root;
+        add_vl(nodes[ni]);
+        path.push_back(ni);
+        int depth = 0;
+        while (nodes[ni].expanded && !nodes[ni].terminal && depth < 1000) {
+            const Node& n = nodes[ni];
+            int pv = n.N;
+            float best = -std::numeric_limits<float>::max();
+            int bc = -1;
+            for (int i = 0; i < n.nchild; ++i) {
+                float sc = puct(nodes[n.first + i], n, depth, pv);
+                if (sc > best) { best = sc; bc = n.first + i; }
+            }
+            if (bc < 0) break;
+            s.play(nodes[bc].action);
+            path.push_back(bc);
+            ni = bc;
+            ++depth;
+        }
+        for (int pi : path) add_vl(nodes[pi]);
+        float value = 0.0f;
+        Node& leaf = nodes[ni];
+        if (leaf.terminal) {
+            value = convert_value(leaf.result, s.player);
+        } else if (s.terminal()) {
+            value = convert_value(s.result(), s.player);
+            leaf.terminal = true; leaf.result = s.result();
+        } else {
+            std::vector<float> p;
+            if (tt.lookup(s.hash(), p, value)) {
+                expand(ni, s, p);
+            } else if (nodes[ni].expanded) {
+                value = nodes[ni].N == 0 ? 0.0f : nodes[ni].W / (float)nodes[ni].N;
+            } else {
+                evaluate(s, p, value);
+                tt.store(s.hash(), p, value);
+                expand(ni, s, p);
+            }
+        }
+        float v = value;
+        for (auto it = path.rbegin(); it != path.rend(); ++it) {
+            Node& n = nodes[*it];
+            remove_vl(n);
+            n.N += 1;
+            n.W = n.W + v;
+            v = -v;
+        }
+    }
+
+    // addDirichletNoise (parallel_mcts.cpp:1110-1171)
+    void add_noise(float alpha, float eps) {
+        if (!nodes[root].expanded) expand_node(root, rootState);
+        Node& r = nodes[root];
+        if (r.nchild == 0) return;
+        std::vector<float> noise(r.nchild);
+        std::gamma_distribution<float> gamma(alpha, 1.0f);
+        float sum = 0.0f;
+        for (int i = 0; i < r.nchild; ++i) { noise[i] = std::max(1e-10f, gamma(rng)); sum += noise[i]; }
+        if (sum <= 0.0f) { sum = 1.0f; for (auto& x : noise) x = 1.0f / (float)noise.size(); }
+        for (auto& x : noise) x /= sum;
+        for (int i = 0; i < r.nchild; ++i) {
+            Node& c = nodes[r.first + i];
+            c.P = (1.0f - eps) * c.P + eps * noise[i];
+        }
+    }
+
+    // search (parallel_mcts.cpp:142-274), Mode S
+    void search() {
+        Node& r = nodes[root];
+        if (!r.expanded && !rootState.terminal()) {
+            std::vector<float> p; float v;
+            evaluate(rootState, p, v);
+            tt.store(rootState.hash(), p, v);
+            expand(root, rootState, p);
+        }
+        if (cfg.noise_each_search && nodes[root].expanded) add_noise(cfg.alpha, cfg.eps);
+        for (int i = 0; i < cfg.sims; ++i) simulate();
+    }
+
+    // getVisitCountDistribution (mcts_node.cpp:289-322)
+    std::vector<float> probs(float T) const {
+        const Node& r = nodes[root];
+        std::vector<float> d(r.nchild, 0.0f);
+        if (!r.expanded || r.nchild == 0) return {};
+        float total = 0.0f;
+        std::vector<float> c(r.nchild);
+        for (int i = 0; i < r.nchild; ++i) {
+            c[i] = std::pow((float)nodes[r.first + i].N, 1.0f / std::max(0.01f, T));
+            total += c[i];
+        }
+        if (total > 0.0f) for (int i = 0; i < r.nchild; ++i) d[i] = c[i] / total;
+        else { float u = 1.0f / (float)r.nchild; for (auto& x : d) x = u; }
+        return d;
+    }
+
+    // selectAction (parallel_mcts.cpp:987-1047) with useBatchInference (deterministic)
+    int select_action(bool training, float T) {
+        if (!nodes[root].expanded) search();
+        const Node& r = nodes[root];
+        if (r.terminal || r.nchild == 0) {
+            auto l = rootState.legal();
+            return l.empty() ? -1 : l[0];
+        }
+        if (training && T > 0.0f) {
+            auto d = probs(T);
+            int bi = (int)(std::max_element(d.begin(), d.end()) - d.begin());
+            return nodes[r.first + bi].action;
+        }
+        int mx = 0;
+        for (int i = 0; i < r.nchild; ++i) mx = std::max(mx, nodes[r.first + i].N);
+        for (int i = 0; i < r.nchild; ++i) if (nodes[r.first + i].N == mx) return nodes[r.first + i].action;
+        return -1;
+    }
+
+    float root_value() const {   // getRootValue (:1057-1063) -> MCTSNode::getValue (mcts_node.h:80-85)
+        const Node& r = nodes[root];
+        if (r.nchild == 0) return 0.0f;
+        return r.N == 0 ? 0.0f : r.W / (float)r.N;
+    }
+
+    // updateWithMove (parallel_mcts.cpp:1065-1108)
+    void apply(int action) {
+        const Node& r = nodes[root];
+        int child = -1;
+        for (int i = 0; i < r.nchild; ++i) if (nodes[r.first + i].action == action) { child = r.first + i; break; }
+        rootState.play(action);
+        if (child >= 0) { root = child; nodes[child].parent = -1; }
+        else { nodes.emplace_back(); root = (int)nodes.size() - 1; }
+    }
+
+    void dump_children(std::ostringstream& o) const {
+        const Node& r = nodes[root];
+        o << "[";
+        for (int i = 0; i < r.nchild; ++i) {
+            const Node& c = nodes[r.first + i];
+            o << (i ? "," : "") << "[" << c.action << "," << c.N << "," << c.VL << "," << fbits(c.W) << "," << fbits(c.P) << "]";
+        }
+        o << "]";
+    }
+};
+
+char* dup(const std::string& s) {
+    char* p = (char*)std::malloc(s.size() + 1);
+    std::memcpy(p, s.c_str(), s.size() + 1);
+    return p;
+}
+
+}  // namespace
+
+extern "C" {
+
+struct az_oracle_cfg {
+    int bs, sims, max_moves, vl, noise_each_search, temp_drop, tt_log2, eval_kind;   // eval: 0 hash, 1 random, 2 net cb, 3 replay cb
+    float cpuct, fpu, alpha, eps, t_init, t_final;
+    unsigned noise_seed, zobrist_seed, eval_seed;
+    int n_games;
+};
+
+void az_oracle_free(char* p) { std::free(p); }
+
+// Plays cfg->n_games independent games (game g uses noise seed noise_seed + g when
+// n_games > 1 is driven with per-game seeds by the caller: here all games share
+// cfg->noise_seed unless seed_stride != 0).  Output: JSON identical in structure to
+// oracle/ref_harness `game` mode, one document per game in a JSON array.
+char* az_oracle_play(const az_oracle_cfg* c, int seed_stride, az_eval_cb cb, void* user) {
+    Cfg cfg;
+    cfg.bs = c->bs; cfg.sims = c->sims; cfg.max_moves = c->max_moves; cfg.vl = c->vl;
+    cfg.noise_each_search = c->noise_each_search; cfg.temp_drop = c->temp_drop; cfg.tt_log2 = c->tt_log2;
+    cfg.cpuct = c->cpuct; cfg.fpu = c->fpu; cfg.alpha = c->alpha; cfg.eps = c->eps;
+    cfg.t_init = c->t_init; cfg.t_final = c->t_final;
+    cfg.zobrist_seed = c->zobrist_seed;
+    Zobrist z(cfg.bs * cfg.bs, cfg.zobrist_seed);
+    std::ostringstream o;
+    o << "[";
+    HashEval he; RandomEval re(c->n_games, c->eval_seed);
+    CallbackEval ne(cb, user, c->eval_kind == 2);
+    Evaluator* ev = c->eval_kind == 0 ? (Evaluator*)&he : c->eval_kind == 1 ? (Evaluator*)&re : (Evaluator*)&ne;
+    for (int g = 0; g < c->n_games; ++g) {
+        Cfg gc = cfg;
+        gc.noise_seed = c->noise_seed + (unsigned)(seed_stride * g);
+        Search m(gc, g, ev, &z);
+        State st(cfg.bs, &z);       // SelfPlayManager's own state (self_play_manager.cpp:157)
+        long evals0 = ev->calls;
+        m.add_noise(cfg.alpha, cfg.eps);
+        if (g) o << ",";
+        o << "{\"mode\":\"game\",\"bs\":" << cfg.bs << ",\"sims\":" << cfg.sims << ",\"init_root\":";
+        m.dump_children(o);
+        o << ",\"moves\":[";
+        int move = 0;
+        while (!st.terminal() && move < cfg.max_moves) {
+            m.search();
+            float T = move >= cfg.temp_drop ? cfg.t_final : cfg.t_init;
+            auto probs = m.probs(T);
+            std::ostringstream kids; m.dump_children(kids);
+            const Node& r = m.nodes[m.root];
+            int rN = r.N, rVL = r.VL; uint32_t rW = fbits(r.W);
+            int action = m.select_action(true, T);
+            float value = m.root_value();
+            if (move) o << ",";
+            o << "{\"ply\":" << move << ",\"root\":[" << rN << "," << rVL << "," << rW << "],\"children\":" << kids.str()
+              << ",\"probs\":[";
+            for (size_t i = 0; i < probs.size(); ++i) o << (i ? "," : "") << fbits(probs[i]);
+            o << "],\"action\":" << action << ",\"value\":" << fbits(value) << ",\"tt_lookups\":" << m.tt.lookups
+              << ",\"tt_hits\":" << m.tt.hits << ",\"evals\":" << (ev->calls - evals0) << "}";
+            st.play(action);
+            m.apply(action);
+            if (move % 2 == 0) m.add_noise(cfg.alpha, cfg.eps);
+            ++move;
+        }
+        GameResult res = st.result();
+        o << "],\"terminal\":" << (res != ONGOING ? 1 : 0) << ",\"result\":" << (int)res << "}";
+    }
+    o << "]";
+    return dup(o.str());
+}
+
+// Feature planes / hash / terminal / legal order for a move sequence (tests/golden positions).
+int az_oracle_position(int bs, unsigned zobrist_seed, const int* moves, int n, float* planes_out,
+                       uint64_t* hash_out, int* result_out, int* legal_out, int* n_legal) {
+    Zobrist z(bs * bs, zobrist_seed);
+    State s(bs, &z);
+    for (int i = 0; i < n; ++i) s.play(moves[i]);
+    if (planes_out) s.planes(planes_out);
+    if (hash_out) *hash_out = s.hash();
+    if (result_out) *result_out = (int)s.result();
+    if (legal_out) { auto l = s.legal(); std::copy(l.begin(), l.end(), legal_out); *n_legal = (int)l.size(); }
+    return 0;
+}
+
+// Initial-root child order of a fresh GomokuState.
+int az_oracle_fresh_order(int bs, int* out) {
+    std::unordered_set<int> s;
+    for (int a = 0; a < bs * bs; ++a) s.insert(a);
+    int i = 0;
+    for (int a : s) out[i++] = a;
+    return i;
+}
+
+// libstdc++ gamma_distribution<float>(alpha, 1) draws on mt19937(seed), one fresh
+// distribution object per call (parallel_mcts.cpp:1137).
+int az_oracle_gamma(unsigned seed, float alpha, int calls, int n, float* out) {
+    std::mt19937 rng(seed);
+    for (int c = 0; c < calls; ++c) {
+        std::gamma_distribution<float> g(alpha, 1.0f);
+        for (int i = 0; i < n; ++i) out[c * n + i] = g(rng);
+    }
+    return 0;
+}
+
+}  // extern "C"
