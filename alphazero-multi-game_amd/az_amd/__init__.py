@@ -1,0 +1,315 @@
+"""az_amd -- host-side Python mirror of the reference's self-play plugin surface,
+over the C-ABI of libaz_hip.so (include/az_engine.h).
+
+Reference surfaces mirrored (paths relative to the reference root):
+  HipNeuralNetwork  alphazero::nn::NeuralNetwork  (include/alphazero/nn/neural_network.h:20-132):
+                    predict(planes) / predictBatch(planes) with TorchNeuralNetwork::predictBatch
+                    semantics (softmax over A, value [B]) (src/nn/torch_neural_network.cpp:224-363)
+  ParallelMCTS      alphazero::mcts::ParallelMCTS (include/alphazero/mcts/parallel_mcts.h:131-201),
+                    one tree per game, G games per device handle: search(), selectAction(),
+                    getActionProbabilities(), getRootValue(), updateWithMove(), addDirichletNoise()
+  SelfPlayManager   alphazero::selfplay::SelfPlayManager (src/selfplay/self_play_manager.cpp:47-240):
+                    generateGames() with the playSingleGame move loop and temperature schedule.
+"""
+import ctypes
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from ._lib import (AZ_EVAL_HASH, AZ_EVAL_NET, AZ_EVAL_RANDOM, AZ_PREC_BF16, AZ_PREC_BF16X3, AZ_PREC_F32, AzError,
+                   NetDesc, SearchCfg, SelfPlayCfg, check, lib)
+
+__all__ = ["Engine", "HipNeuralNetwork", "ParallelMCTS", "SelfPlayManager", "GameRecord", "MoveData", "AzError",
+           "AZ_PREC_F32", "AZ_PREC_BF16X3", "AZ_PREC_BF16", "AZ_EVAL_NET", "AZ_EVAL_HASH", "AZ_EVAL_RANDOM",
+           "gomoku_net_desc"]
+
+_f = ctypes.POINTER(ctypes.c_float)
+_i = ctypes.POINTER(ctypes.c_int)
+
+
+def _fp(a):
+    return a.ctypes.data_as(_f)
+
+
+def _ip(a):
+    return a.ctypes.data_as(_i)
+
+
+class Engine:
+    """One HIP device (az_engine_create).  Raises if no GPU is present."""
+
+    def __init__(self, device=0):
+        h = ctypes.c_void_p()
+        check(lib().az_engine_create(device, ctypes.byref(h)))
+        self.h = h
+
+    @property
+    def device_name(self):
+        buf = ctypes.create_string_buffer(256)
+        check(lib().az_engine_device_name(self.h, buf, 256))
+        return buf.value.decode()
+
+    def close(self):
+        if self.h:
+            lib().az_engine_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def gomoku_net_desc(board_size=15, channels=256, blocks=20, precision=AZ_PREC_F32, max_batch=256, residual=1,
+                    conv_bias=0, in_planes=11, head_channels=32, pool=8, fc_hidden=256):
+    """Residual policy/value net of BASELINE.json (C2: 6x64, C3: 20x256) for Gomoku."""
+    return NetDesc(board_size, in_planes, channels, blocks, board_size * board_size, head_channels, pool, fc_hidden,
+                   residual, conv_bias, precision, max_batch)
+
+
+class HipNeuralNetwork:
+    """NeuralNetwork plugin on the MI355X ConvNet kernels."""
+
+    def __init__(self, engine, desc):
+        self.engine = engine
+        self.desc = desc
+        h = ctypes.c_void_p()
+        check(lib().az_net_create(engine.h, ctypes.byref(desc), ctypes.byref(h)))
+        self.h = h
+        n = ctypes.c_size_t()
+        check(lib().az_net_num_params(self.h, ctypes.byref(n)))
+        self.num_params = n.value
+
+    def load_weights(self, blob):
+        blob = np.ascontiguousarray(blob, dtype=np.float32).reshape(-1)
+        check(lib().az_net_load_weights(self.h, _fp(blob), blob.size))
+
+    def init_random(self, seed):
+        check(lib().az_net_init_random(self.h, seed))
+
+    def set_precision(self, precision):
+        check(lib().az_net_set_precision(self.h, precision))
+        self.desc.precision = precision
+
+    def forward(self, planes):
+        """planes [B, C_in, H, W] fp32 -> (logits [B, A], value [B])."""
+        x = np.ascontiguousarray(planes, dtype=np.float32)
+        B = x.shape[0]
+        A = self.desc.action_size
+        lo = np.zeros((B, A), np.float32)
+        v = np.zeros(B, np.float32)
+        check(lib().az_net_forward(self.h, _fp(x), B, _fp(lo), _fp(v)))
+        return lo, v
+
+    def predictBatch(self, planes):
+        """TorchNeuralNetwork::predictBatch semantics: (softmax policy [B, A], value [B])."""
+        x = np.ascontiguousarray(planes, dtype=np.float32)
+        B = x.shape[0]
+        A = self.desc.action_size
+        p = np.zeros((B, A), np.float32)
+        v = np.zeros(B, np.float32)
+        check(lib().az_net_predict_batch(self.h, _fp(x), B, _fp(p), _fp(v)))
+        return p, v
+
+    def predict(self, planes):
+        p, v = self.predictBatch(np.asarray(planes, np.float32)[None])
+        return p[0], float(v[0])
+
+    def getBatchSize(self):
+        return self.desc.max_batch
+
+    def isGpuAvailable(self):
+        return True
+
+    def close(self):
+        if self.h:
+            lib().az_net_destroy(self.h)
+            self.h = None
+
+
+class ParallelMCTS:
+    """G independent ParallelMCTS trees (Mode S semantics, setDeterministicMode) on one device."""
+
+    def __init__(self, engine, n_games=1, board_size=15, num_simulations=800, c_puct=1.5, fpu_reduction=0.0,
+                 virtual_loss=3, evaluator=AZ_EVAL_HASH, net=None, eval_seed=7, zobrist_seed=12345, noise_seed=42,
+                 noise_seed_stride=0, use_dirichlet_each_search=False, dirichlet_alpha=0.03, dirichlet_eps=0.25,
+                 tt_log2=20, node_capacity=0, prior_ring=0):
+        self.G = n_games
+        self.bs = board_size
+        self.A = board_size * board_size
+        cfg = SearchCfg(n_games, board_size, num_simulations, c_puct, fpu_reduction, virtual_loss, evaluator,
+                        eval_seed, zobrist_seed, noise_seed, noise_seed_stride, int(use_dirichlet_each_search),
+                        dirichlet_alpha, dirichlet_eps, tt_log2, node_capacity, prior_ring)
+        self.cfg = cfg
+        h = ctypes.c_void_p()
+        check(lib().az_search_create(engine.h, net.h if net is not None else None, ctypes.byref(cfg), ctypes.byref(h)))
+        self.h = h
+        self.engine, self.net = engine, net
+
+    def newGames(self, games=None):
+        games = np.arange(self.G, dtype=np.int32) if games is None else np.asarray(games, np.int32)
+        check(lib().az_search_new_games(self.h, _ip(games), games.size))
+
+    def addDirichletNoise(self, alpha=0.03, epsilon=0.25, mask=None):
+        if mask is None:
+            check(lib().az_search_add_noise(self.h, alpha, epsilon))
+        else:
+            m = np.ascontiguousarray(mask, dtype=np.uint8)
+            check(lib().az_search_add_noise_masked(self.h, alpha, epsilon,
+                                                   m.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))))
+
+    def search(self):
+        check(lib().az_search_run(self.h))
+
+    def select(self, is_training=True, temperature=1.0):
+        """(actions [G], root values [G], probs [G][A] child order, child actions [G][A], n_children [G])."""
+        G, A = self.G, self.A
+        act = np.zeros(G, np.int32)
+        val = np.zeros(G, np.float32)
+        probs = np.zeros((G, A), np.float32)
+        cact = np.zeros((G, A), np.int32)
+        nch = np.zeros(G, np.int32)
+        check(lib().az_search_select(self.h, int(is_training), temperature, _ip(act), _fp(val), _fp(probs), _ip(cact),
+                                     _ip(nch)))
+        return act, val, probs, cact, nch
+
+    def selectAction(self, isTraining=False, temperature=1.0):
+        return self.select(isTraining, temperature)[0]
+
+    def getActionProbabilities(self, temperature=1.0):
+        _, _, probs, _, nch = self.select(True, temperature)
+        return [probs[g, :nch[g]].copy() for g in range(self.G)]
+
+    def getRootValue(self):
+        return self.select(True, 1.0)[1]
+
+    def updateWithMove(self, actions):
+        a = np.ascontiguousarray(actions, dtype=np.int32).reshape(self.G)
+        term = np.zeros(self.G, np.int32)
+        res = np.zeros(self.G, np.int32)
+        check(lib().az_search_apply(self.h, _ip(a), _ip(term), _ip(res)))
+        return term, res
+
+    def rootChildren(self, game):
+        A = self.A
+        act = np.zeros(A, np.int32)
+        N = np.zeros(A, np.int32)
+        VL = np.zeros(A, np.int32)
+        W = np.zeros(A, np.float32)
+        Pp = np.zeros(A, np.float32)
+        n = ctypes.c_int()
+        check(lib().az_search_root_children(self.h, game, _ip(act), _ip(N), _ip(VL), _fp(W), _fp(Pp), ctypes.byref(n)))
+        k = n.value
+        return act[:k], N[:k], VL[:k], W[:k], Pp[:k]
+
+    def rootNode(self, game):
+        N = ctypes.c_int()
+        VL = ctypes.c_int()
+        W = ctypes.c_float()
+        check(lib().az_search_root_node(self.h, game, ctypes.byref(N), ctypes.byref(VL), ctypes.byref(W)))
+        return N.value, VL.value, W.value
+
+    def counters(self, game):
+        out = (ctypes.c_int64 * 5)()
+        check(lib().az_search_counters(self.h, game, out))
+        return dict(zip(("evals", "tt_lookups", "tt_hits", "sims", "nodes"), list(out)))
+
+    def enableEvalLog(self, game, capacity):
+        check(lib().az_search_enable_eval_log(self.h, game, capacity))
+
+    def readEvalLog(self, capacity):
+        A = self.A
+        pol = np.zeros((capacity, A), np.float32)
+        val = np.zeros(capacity, np.float32)
+        planes = np.zeros((capacity, 11, self.bs, self.bs), np.float32)
+        n = ctypes.c_int()
+        check(lib().az_search_read_eval_log(self.h, _fp(pol), _fp(val), _fp(planes), ctypes.byref(n)))
+        k = n.value
+        return pol[:k], val[:k], planes[:k]
+
+    def selfplayStep(self, temp_drop_move=30, t_init=1.0, t_final=0.0, restart_finished=True):
+        cfg = SelfPlayCfg(temp_drop_move, t_init, t_final, int(restart_finished))
+        moves = ctypes.c_int64(0)
+        evals = ctypes.c_int64(0)
+        check(lib().az_selfplay_step(self.h, ctypes.byref(cfg), ctypes.byref(moves), ctypes.byref(evals)))
+        return moves.value, evals.value
+
+    def close(self):
+        if self.h:
+            lib().az_search_destroy(self.h)
+            self.h = None
+
+
+@dataclass
+class MoveData:
+    """include/alphazero/selfplay/game_record.h:21-33 (policy in CHILD order, not action-indexed)."""
+    action: int
+    policy: list
+    value: float
+    thinking_time_ms: int = 0
+
+
+@dataclass
+class GameRecord:
+    board_size: int
+    moves: list = field(default_factory=list)
+    result: int = 0
+
+
+class SelfPlayManager:
+    """SelfPlayManager::generateGames over G device-resident games (playSingleGame loop,
+    self_play_manager.cpp:151-234): initial noise, search, T = initial until
+    temperatureDropMove then final, selectAction(true, T), record, makeMove +
+    updateWithMove, noise after every even ply."""
+
+    def __init__(self, engine, net=None, numGames=1, numSimulations=800, board_size=15, evaluator=None, **mcts_kw):
+        ev = evaluator if evaluator is not None else (AZ_EVAL_NET if net is not None else AZ_EVAL_HASH)
+        self.mcts = ParallelMCTS(engine, n_games=numGames, board_size=board_size, num_simulations=numSimulations,
+                                 evaluator=ev, net=net, **mcts_kw)
+        self.numGames = numGames
+        self.dirichletAlpha, self.dirichletEpsilon = 0.03, 0.25
+        self.initialTemperature, self.temperatureDropMove, self.finalTemperature = 1.0, 30, 0.0
+        self.progressCallback = None
+
+    def setExplorationParams(self, dirichletAlpha, dirichletEpsilon, initialTemperature, temperatureDropMove,
+                             finalTemperature):
+        self.dirichletAlpha, self.dirichletEpsilon = dirichletAlpha, dirichletEpsilon
+        self.initialTemperature, self.temperatureDropMove = initialTemperature, temperatureDropMove
+        self.finalTemperature = finalTemperature
+
+    def setProgressCallback(self, cb):
+        self.progressCallback = cb
+
+    def getTemperature(self, moveNum):
+        return self.finalTemperature if moveNum >= self.temperatureDropMove else self.initialTemperature
+
+    def generateGames(self, max_moves=1 << 30, on_move=None):
+        m = self.mcts
+        G = self.numGames
+        m.newGames()
+        m.addDirichletNoise(self.dirichletAlpha, self.dirichletEpsilon)
+        records = [GameRecord(m.bs) for _ in range(G)]
+        live = np.ones(G, bool)
+        move = 0
+        while live.any() and move < max_moves:
+            m.search()
+            T = self.getTemperature(move)
+            act, val, probs, cact, nch = m.select(True, T)
+            if on_move is not None:
+                on_move(move, m)
+            for g in range(G):
+                if live[g]:
+                    records[g].moves.append(MoveData(int(act[g]), probs[g, :nch[g]].tolist(), float(val[g])))
+                    if self.progressCallback:
+                        self.progressCallback(g, move, G, move * G)
+            act = np.where(live, act, -1).astype(np.int32)
+            term, res = m.updateWithMove(act)
+            for g in range(G):
+                if live[g] and term[g]:
+                    records[g].result = int(res[g])
+                    live[g] = False
+            if move % 2 == 0:
+                m.addDirichletNoise(self.dirichletAlpha, self.dirichletEpsilon)
+            move += 1
+        return records

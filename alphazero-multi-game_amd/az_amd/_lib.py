@@ -1,0 +1,91 @@
+"""ctypes binding of include/az_engine.h (libaz_hip.so, built in-tree).
+
+Loading fails loudly if the library is missing; there is no CPU fallback."""
+import ctypes
+import os
+
+PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(PKG, "build", "libaz_hip.so")
+
+c_int, c_float, c_size_t, c_uint32, c_uint64, c_int64 = (ctypes.c_int, ctypes.c_float, ctypes.c_size_t,
+                                                          ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int64)
+P = ctypes.POINTER
+vp = ctypes.c_void_p
+
+AZ_PREC_F32, AZ_PREC_BF16X3, AZ_PREC_BF16 = 0, 1, 2
+AZ_EVAL_NET, AZ_EVAL_HASH, AZ_EVAL_RANDOM = 0, 1, 2
+
+
+class NetDesc(ctypes.Structure):
+    _fields_ = [(n, c_int) for n in ("board_size", "in_planes", "channels", "blocks", "action_size", "head_channels",
+                                     "pool", "fc_hidden", "residual", "conv_bias", "precision", "max_batch")]
+
+
+class SearchCfg(ctypes.Structure):
+    _fields_ = [("n_games", c_int), ("board_size", c_int), ("num_simulations", c_int), ("c_puct", c_float),
+                ("fpu_reduction", c_float), ("virtual_loss", c_int), ("eval_kind", c_int), ("eval_seed", c_uint32),
+                ("zobrist_seed", c_uint32), ("noise_seed", c_uint32), ("noise_seed_stride", c_int),
+                ("use_dirichlet_each_search", c_int), ("dirichlet_alpha", c_float), ("dirichlet_eps", c_float),
+                ("tt_log2", c_int), ("node_capacity", c_int), ("prior_ring", c_int)]
+
+
+class SelfPlayCfg(ctypes.Structure):
+    _fields_ = [("temp_drop_move", c_int), ("t_init", c_float), ("t_final", c_float), ("restart_finished", c_int)]
+
+
+EXPORTS = {
+    "az_last_error": (ctypes.c_char_p, []),
+    "az_engine_create": (c_int, [c_int, P(vp)]),
+    "az_engine_destroy": (None, [vp]),
+    "az_engine_device_name": (c_int, [vp, ctypes.c_char_p, c_int]),
+    "az_net_create": (c_int, [vp, P(NetDesc), P(vp)]),
+    "az_net_destroy": (None, [vp]),
+    "az_net_num_params": (c_int, [vp, P(c_size_t)]),
+    "az_net_load_weights": (c_int, [vp, P(c_float), c_size_t]),
+    "az_net_init_random": (c_int, [vp, c_uint64]),
+    "az_net_set_precision": (c_int, [vp, c_int]),
+    "az_net_forward": (c_int, [vp, P(c_float), c_int, P(c_float), P(c_float)]),
+    "az_net_predict_batch": (c_int, [vp, P(c_float), c_int, P(c_float), P(c_float)]),
+    "az_search_create": (c_int, [vp, vp, P(SearchCfg), P(vp)]),
+    "az_search_destroy": (None, [vp]),
+    "az_search_new_games": (c_int, [vp, P(c_int), c_int]),
+    "az_search_add_noise": (c_int, [vp, c_float, c_float]),
+    "az_search_add_noise_masked": (c_int, [vp, c_float, c_float, P(ctypes.c_uint8)]),
+    "az_search_run": (c_int, [vp]),
+    "az_search_select": (c_int, [vp, c_int, c_float, P(c_int), P(c_float), P(c_float), P(c_int), P(c_int)]),
+    "az_search_apply": (c_int, [vp, P(c_int), P(c_int), P(c_int)]),
+    "az_search_root_children": (c_int, [vp, c_int, P(c_int), P(c_int), P(c_int), P(c_float), P(c_float), P(c_int)]),
+    "az_search_root_node": (c_int, [vp, c_int, P(c_int), P(c_int), P(c_float)]),
+    "az_search_counters": (c_int, [vp, c_int, P(c_int64)]),
+    "az_search_enable_eval_log": (c_int, [vp, c_int, c_int]),
+    "az_search_read_eval_log": (c_int, [vp, P(c_float), P(c_float), P(c_float), P(c_int)]),
+    "az_selfplay_step": (c_int, [vp, P(SelfPlayCfg), P(c_int64), P(c_int64)]),
+}
+
+_lib = None
+
+
+def lib():
+    """Load libaz_hip.so and bind every entry point declared in include/az_engine.h."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"libaz_hip.so not built ({LIB_PATH}); run __graft_entry__.build() / make -C "
+                               f"alphazero-multi-game_amd")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in EXPORTS.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+class AzError(RuntimeError):
+    pass
+
+
+def check(rc):
+    if rc != 0:
+        raise AzError(f"az error {rc}: {lib().az_last_error().decode()}")
+    return rc

@@ -1,0 +1,917 @@
+// engine.hip -- host runtime behind include/az_engine.h (libaz_hip.so).
+//
+// Owns device memory, streams and launches; no exceptions cross the C-ABI.
+// The product path never falls back to the CPU: without a HIP device every entry
+// point fails with AZ_ERR_HIP.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <random>
+#include <string>
+#include <unordered_set>
+#include <vector>
+
+#include "../../include/az_engine.h"
+#include "net.h"
+#include "tree.h"
+
+// kernels (tree_kernels.hip)
+__global__ void k_select(TreeDev t, int mode);
+__global__ void k_scan(TreeDev t);
+__global__ void k_expand_backup(TreeDev t, int mode);
+__global__ void k_select_action(TreeDev t, int training, float temperature, int* actions, float* values, float* probs,
+                                int* child_actions, int* nchild);
+__global__ void k_apply(TreeDev t, const int* actions, int* terminal, int* result);
+__global__ void k_compact(TreeDev t, Nodes dst, int* src_of);
+__global__ void k_noise(TreeDev t, const float* noise, const uint8_t* mask, float eps);
+__global__ void k_new_games(TreeDev t, const int* games, int n, uint32_t eval_seed);
+__global__ void k_tt_clear(TreeDev t, const int* games, int n);
+__global__ void k_root_children(TreeDev t, int g, int* act, int* N, int* VL, float* W, float* P, int* n, int* rootinfo,
+                                float* rootW);
+void az_conv_bf16_launch(const ConvBf16Args& a, bool split, hipStream_t st);
+void az_launch_split_bf16(const float* in, uint16_t* hi, uint16_t* lo, size_t n, const int* m_limit, int rows_per_sample,
+                          int C, hipStream_t st);
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+#define HIPCHK(x)                                                                            \
+    do {                                                                                     \
+        hipError_t e_ = (x);                                                                 \
+        if (e_ != hipSuccess) return fail(AZ_ERR_HIP, "%s: %s (%s:%d)", #x, hipGetErrorString(e_), __FILE__, __LINE__); \
+    } while (0)
+
+template <class T>
+int dalloc(T** p, size_t n) {
+    if (n == 0) n = 1;
+    hipError_t e = hipMalloc((void**)p, n * sizeof(T));
+    if (e != hipSuccess) return fail(AZ_ERR_OOM, "hipMalloc(%zu bytes): %s", n * sizeof(T), hipGetErrorString(e));
+    return 0;
+}
+#define DALLOC(p, n) do { int r_ = dalloc(&(p), (n)); if (r_) return r_; } while (0)
+
+uint64_t splitmix64(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ULL;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBULL;
+    return x ^ (x >> 31);
+}
+
+}  // namespace
+
+// ===========================================================================
+struct az_engine {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    hipDeviceProp_t prop{};
+    std::mutex mu;
+};
+
+struct Layer {            // one implicit-GEMM layer, BN folded
+    float* W = nullptr;   // [N][K] fp32
+    uint16_t* Whi = nullptr; uint16_t* Wlo = nullptr;   // bf16 split copies (3x3 trunk)
+    float* b = nullptr;   // [N]
+    int N = 0, K = 0, Kpad = 0, taps = 1, C = 0;
+};
+
+struct az_net {
+    az_engine* e = nullptr;
+    az_net_desc d{};
+    int cin_pad = 16;
+    int HW = 0, P2 = 0;
+    size_t nparams = 0;
+    Layer in, pconv, vconv, pfc, vfc1, vfc2;
+    std::vector<Layer> blk;   // 2 per block
+    // activations (max_batch samples)
+    float *x0 = nullptr, *h0 = nullptr, *h1 = nullptr, *t = nullptr, *pool = nullptr;
+    uint16_t *hh[2] = {nullptr, nullptr}, *hl[2] = {nullptr, nullptr}, *th = nullptr, *tl = nullptr;
+    float *pp = nullptr, *vp = nullptr, *v1 = nullptr, *logits = nullptr, *value = nullptr, *soft = nullptr;
+    float* in_nchw = nullptr;
+    int* d_nb = nullptr;
+    bool loaded = false;
+    std::mutex mu;
+};
+
+// ---------------------------------------------------------------- network
+namespace {
+
+struct ParamCursor {
+    const float* p; size_t off = 0;
+    const float* take(size_t n) { const float* r = p + off; off += n; return r; }
+};
+
+size_t count_params(const az_net_desc& d) {
+    const size_t F = d.channels, Ci = d.in_planes, HC = d.head_channels, PP = (size_t)d.pool * d.pool;
+    size_t n = 0;
+    auto conv = [&](size_t co, size_t ci, size_t k) { n += co * ci * k * k + (d.conv_bias ? co : 0) + 4 * co; };
+    conv(F, Ci, 3);
+    for (int i = 0; i < d.blocks; ++i) { conv(F, F, 3); conv(F, F, 3); }
+    conv(HC, F, 1);
+    n += (size_t)d.action_size * HC * PP + d.action_size;
+    conv(HC, F, 1);
+    n += (size_t)d.fc_hidden * HC * PP + d.fc_hidden;
+    n += (size_t)d.fc_hidden + 1;
+    return n;
+}
+
+uint16_t f2bf(float f) {   // round to nearest even
+    uint32_t u; std::memcpy(&u, &f, 4);
+    if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40);
+    u += 0x7fffu + ((u >> 16) & 1u);
+    return (uint16_t)(u >> 16);
+}
+float bf2f(uint16_t h) { uint32_t u = (uint32_t)h << 16; float f; std::memcpy(&f, &u, 4); return f; }
+
+// conv + BN (eval) -> folded [co][tap*cpad + c] weights and bias
+void fold_conv(ParamCursor& pc, int co, int ci, int k, int cpad, bool has_bias, std::vector<float>& W, std::vector<float>& b) {
+    const float* w = pc.take((size_t)co * ci * k * k);
+    const float* cb = has_bias ? pc.take(co) : nullptr;
+    const float* g = pc.take(co);
+    const float* be = pc.take(co);
+    const float* mu = pc.take(co);
+    const float* var = pc.take(co);
+    const int taps = k * k;
+    W.assign((size_t)co * taps * cpad, 0.0f);
+    b.assign(co, 0.0f);
+    for (int o = 0; o < co; ++o) {
+        const float scale = g[o] / std::sqrt(var[o] + 1e-5f);
+        b[o] = ((cb ? cb[o] : 0.0f) - mu[o]) * scale + be[o];
+        for (int c = 0; c < ci; ++c)
+            for (int t = 0; t < taps; ++t) W[((size_t)o * taps + t) * cpad + c] = w[((size_t)o * ci + c) * taps + t] * scale;
+    }
+}
+
+int upload_layer(Layer& L, const std::vector<float>& W, const std::vector<float>& b, int N, int K, int taps, int C,
+                 bool split) {
+    L.N = N; L.K = K; L.Kpad = (K + 31) / 32 * 32; L.taps = taps; L.C = C;
+    if (!L.W) { DALLOC(L.W, W.size()); DALLOC(L.b, b.size()); }
+    HIPCHK(hipMemcpy(L.W, W.data(), W.size() * 4, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(L.b, b.data(), b.size() * 4, hipMemcpyHostToDevice));
+    if (split) {
+        std::vector<uint16_t> hi(W.size()), lo(W.size());
+        for (size_t i = 0; i < W.size(); ++i) { hi[i] = f2bf(W[i]); lo[i] = f2bf(W[i] - bf2f(hi[i])); }
+        if (!L.Whi) { DALLOC(L.Whi, W.size()); DALLOC(L.Wlo, W.size()); }
+        HIPCHK(hipMemcpy(L.Whi, hi.data(), hi.size() * 2, hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(L.Wlo, lo.data(), lo.size() * 2, hipMemcpyHostToDevice));
+    }
+    return 0;
+}
+
+int net_load(az_net* n, const float* blob) {
+    const az_net_desc& d = n->d;
+    ParamCursor pc{blob};
+    const int F = d.channels, HC = d.head_channels, PP = d.pool * d.pool;
+    std::vector<float> W, b;
+    const bool split = F % 32 == 0;
+    fold_conv(pc, F, d.in_planes, 3, n->cin_pad, d.conv_bias, W, b);
+    if (int r = upload_layer(n->in, W, b, F, 9 * n->cin_pad, 9, n->cin_pad, false)) return r;
+    n->blk.resize(2 * d.blocks);
+    for (int i = 0; i < 2 * d.blocks; ++i) {
+        fold_conv(pc, F, F, 3, F, d.conv_bias, W, b);
+        if (int r = upload_layer(n->blk[i], W, b, F, 9 * F, 9, F, split)) return r;
+    }
+    // policy head: 1x1 conv + BN, FC over the flattened (c, y, x) pooled map
+    fold_conv(pc, HC, F, 1, F, d.conv_bias, W, b);
+    if (int r = upload_layer(n->pconv, W, b, HC, F, 1, F, false)) return r;
+    auto fc_perm = [&](int out, int hc, int pp, std::vector<float>& Wt, std::vector<float>& bt) {
+        // torch flattens NCHW (index c*pp + px); our pooled head map is [px][c].
+        const float* w = pc.take((size_t)out * hc * pp);
+        const float* bb = pc.take(out);
+        Wt.assign((size_t)out * hc * pp, 0.0f);
+        for (int o = 0; o < out; ++o)
+            for (int c = 0; c < hc; ++c)
+                for (int px = 0; px < pp; ++px) Wt[((size_t)o * pp + px) * hc + c] = w[((size_t)o * hc + c) * pp + px];
+        bt.assign(bb, bb + out);
+    };
+    fc_perm(d.action_size, HC, PP, W, b);
+    if (int r = upload_layer(n->pfc, W, b, d.action_size, HC * PP, 1, HC * PP, false)) return r;
+    fold_conv(pc, HC, F, 1, F, d.conv_bias, W, b);
+    if (int r = upload_layer(n->vconv, W, b, HC, F, 1, F, false)) return r;
+    fc_perm(d.fc_hidden, HC, PP, W, b);
+    if (int r = upload_layer(n->vfc1, W, b, d.fc_hidden, HC * PP, 1, HC * PP, false)) return r;
+    {
+        const float* w = pc.take(d.fc_hidden);
+        const float* bb = pc.take(1);
+        W.assign(w, w + d.fc_hidden);
+        b.assign(bb, bb + 1);
+        if (int r = upload_layer(n->vfc2, W, b, 1, d.fc_hidden, 1, d.fc_hidden, false)) return r;
+    }
+    if (pc.off != n->nparams) return fail(AZ_ERR_ARG, "parameter blob size mismatch (%zu vs %zu)", pc.off, n->nparams);
+    n->loaded = true;
+    return 0;
+}
+
+GemmArgs gemm_args(const Layer& L, const float* A, int lda, float* C, int ldc, const float* res, int M, int H, int W,
+                   const int* m_limit, int rows_per_sample) {
+    GemmArgs p{};
+    p.A = A; p.lda = lda; p.B = L.W; p.ldb = L.K; p.C = C; p.ldc = ldc; p.bias = L.b; p.res = res;
+    p.M = M; p.N = L.N; p.K = L.K; p.Kpad = L.Kpad; p.taps = L.taps; p.Cch = L.C; p.H = H; p.W = W;
+    p.m_limit = m_limit; p.rows_per_sample = rows_per_sample;
+    return p;
+}
+
+// Forward of B samples (B = capacity; *nb = active samples, device side) from the
+// NHWC16 input x0 -> logits [B][A], value [B].
+int net_forward(az_net* n, const float* x0, int B, const int* nb, float* logits, float* value, hipStream_t st) {
+    const az_net_desc& d = n->d;
+    const int H = d.board_size, W = d.board_size, HW = n->HW, F = d.channels, P = d.pool, PP = n->P2;
+    const int rows = B * HW;
+    const int prec = d.precision;
+    const bool bf = (prec == AZ_PREC_BF16X3 || prec == AZ_PREC_BF16) && F % 32 == 0;
+    az_launch_gemm_f32(gemm_args(n->in, x0, n->cin_pad, n->h0, F, nullptr, rows, H, W, nb, HW), ACT_RELU, false, st);
+    float* h = n->h0;
+    float* other = n->h1;
+    if (!bf) {
+        for (int i = 0; i < d.blocks; ++i) {
+            az_launch_gemm_f32(gemm_args(n->blk[2 * i], h, F, n->t, F, nullptr, rows, H, W, nb, HW), ACT_RELU, false, st);
+            az_launch_gemm_f32(gemm_args(n->blk[2 * i + 1], n->t, F, other, F, d.residual ? h : nullptr, rows, H, W, nb, HW),
+                               ACT_RELU, d.residual != 0, st);
+            std::swap(h, other);
+        }
+    } else {
+        const bool split = prec == AZ_PREC_BF16X3;
+        az_launch_split_bf16(h, n->hh[0], split ? n->hl[0] : nullptr, (size_t)rows * F, nb, HW, F, st);
+        int cur = 0;
+        for (int i = 0; i < d.blocks; ++i) {
+            const Layer& L1 = n->blk[2 * i];
+            const Layer& L2 = n->blk[2 * i + 1];
+            ConvBf16Args a{};
+            a.Ahi = n->hh[cur]; a.Alo = split ? n->hl[cur] : nullptr;
+            a.Bhi = L1.Whi; a.Blo = split ? L1.Wlo : nullptr;
+            a.Chi = n->th; a.Clo = split ? n->tl : nullptr; a.Cf = nullptr;
+            a.bias = L1.b; a.Rhi = nullptr; a.Rlo = nullptr;
+            a.M = rows; a.N = F; a.C = F; a.H = H; a.W = W; a.m_limit = nb; a.rows_per_sample = HW; a.relu = 1;
+            az_conv_bf16_launch(a, split, st);
+            ConvBf16Args b2 = a;
+            b2.Ahi = n->th; b2.Alo = split ? n->tl : nullptr;
+            b2.Bhi = L2.Whi; b2.Blo = split ? L2.Wlo : nullptr;
+            b2.Chi = n->hh[cur ^ 1]; b2.Clo = split ? n->hl[cur ^ 1] : nullptr;
+            b2.bias = L2.b;
+            b2.Rhi = d.residual ? n->hh[cur] : nullptr; b2.Rlo = d.residual && split ? n->hl[cur] : nullptr;
+            b2.Cf = (i == d.blocks - 1) ? other : nullptr;
+            az_conv_bf16_launch(b2, split, st);
+            cur ^= 1;
+        }
+        if (d.blocks > 0) h = other;
+    }
+    az_launch_pool(h, n->pool, B, H, W, F, P, nb, st);
+    az_launch_gemm_f32(gemm_args(n->pconv, n->pool, F, n->pp, d.head_channels, nullptr, B * PP, 1, 1, nb, PP), ACT_RELU, false, st);
+    az_launch_gemm_f32(gemm_args(n->vconv, n->pool, F, n->vp, d.head_channels, nullptr, B * PP, 1, 1, nb, PP), ACT_RELU, false, st);
+    const int HK = d.head_channels * PP;
+    az_launch_gemm_f32(gemm_args(n->pfc, n->pp, HK, logits, d.action_size, nullptr, B, 1, 1, nb, 1), ACT_NONE, false, st);
+    az_launch_gemm_f32(gemm_args(n->vfc1, n->vp, HK, n->v1, d.fc_hidden, nullptr, B, 1, 1, nb, 1), ACT_RELU, false, st);
+    az_launch_gemm_f32(gemm_args(n->vfc2, n->v1, d.fc_hidden, value, 1, nullptr, B, 1, 1, nb, 1), ACT_TANH, false, st);
+    HIPCHK(hipGetLastError());
+    return 0;
+}
+
+}  // namespace
+
+// ===========================================================================
+struct az_search {
+    az_engine* e = nullptr;
+    az_net* net = nullptr;
+    az_search_cfg c{};
+    TreeDev t{};
+    Nodes arena[2]{};
+    int cur = 0;
+    int* d_src_of = nullptr;
+    float* d_batch = nullptr;       // gathered NHWC16 planes [G][A][16]
+    float* d_logits = nullptr; float* d_value = nullptr;
+    float* d_noise = nullptr; uint8_t* d_mask = nullptr;
+    int* d_actions = nullptr; float* d_values = nullptr; float* d_probs = nullptr; int* d_cact = nullptr; int* d_nch = nullptr;
+    int* d_term = nullptr; int* d_res = nullptr; int* d_games = nullptr;
+    float* d_temps = nullptr;
+    // host mirrors
+    std::vector<int> stones, active, fresh, ply, expanded;
+    std::vector<std::mt19937> rng;
+    std::vector<float> h_noise; std::vector<uint8_t> h_mask;
+    std::mutex mu;
+};
+
+namespace {
+
+int check_err(az_search* s) {
+    int err = 0;
+    HIPCHK(hipMemcpyAsync(&err, s->t.err, 4, hipMemcpyDeviceToHost, s->e->stream));
+    HIPCHK(hipStreamSynchronize(s->e->stream));
+    if (err) return fail(AZ_ERR_CAPACITY, "device capacity exceeded (flags 0x%x: 1 node pool, 2 path, 4 prior ring)", err);
+    return 0;
+}
+
+// One batched step over all games: select -> (network) -> expand/backup.
+int search_step(az_search* s, int mode) {
+    hipStream_t st = s->e->stream;
+    const int G = s->c.n_games;
+    s->t.nd = s->arena[s->cur];
+    hipLaunchKernelGGL(k_select, dim3(G), dim3(64), 0, st, s->t, mode);
+    if (s->c.eval_kind == AZ_EVAL_NET) {
+        hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, st, s->t);
+        az_launch_gather_planes(s->t.planes, s->d_batch, s->t.eval_games, s->t.n_eval, s->t.A * 16, G, st);
+        if (int r = net_forward(s->net, s->d_batch, G, s->t.n_eval, s->d_logits, s->d_value, st)) return r;
+    }
+    hipLaunchKernelGGL(k_expand_backup, dim3(G), dim3(64), 0, st, s->t, mode);
+    HIPCHK(hipGetLastError());
+    return 0;
+}
+
+int search_noise(az_search* s, float alpha, float eps, const uint8_t* mask) {
+    const int G = s->c.n_games, A = s->t.A;
+    if (int r = search_step(s, MODE_ROOT_NOISE)) return r;
+    // addDirichletNoise draws (parallel_mcts.cpp:1136-1156): libstdc++ gamma on the host,
+    // one fresh gamma_distribution per call on the game's mt19937.
+    bool any = false;
+    for (int g = 0; g < G; ++g) {
+        s->h_mask[g] = 0;
+        if (!s->active[g] || (mask && !mask[g])) continue;
+        const int nc = s->fresh[g] ? A : A - s->stones[g];
+        if (nc <= 0) continue;
+        float* nz = s->h_noise.data() + (size_t)g * A;
+        std::gamma_distribution<float> gamma(alpha, 1.0f);
+        float sum = 0.0f;
+        for (int i = 0; i < nc; ++i) { nz[i] = std::max(1e-10f, gamma(s->rng[g])); sum += nz[i]; }
+        if (sum <= 0.0f) { sum = 1.0f; for (int i = 0; i < nc; ++i) nz[i] = 1.0f / (float)nc; }
+        for (int i = 0; i < nc; ++i) nz[i] /= sum;
+        s->h_mask[g] = 1;
+        any = true;
+    }
+    if (!any) return 0;
+    hipStream_t st = s->e->stream;
+    HIPCHK(hipMemcpyAsync(s->d_noise, s->h_noise.data(), (size_t)G * A * 4, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(s->d_mask, s->h_mask.data(), G, hipMemcpyHostToDevice, st));
+    s->t.nd = s->arena[s->cur];
+    hipLaunchKernelGGL(k_noise, dim3(G), dim3(64), 0, st, s->t, s->d_noise, s->d_mask, eps);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(st));
+    return 0;
+}
+
+int search_run(az_search* s) {
+    if (int r = search_step(s, MODE_ROOT_SEARCH)) return r;
+    if (s->c.use_dirichlet_each_search)
+        if (int r = search_noise(s, s->c.dirichlet_alpha, s->c.dirichlet_eps, nullptr)) return r;
+    for (int i = 0; i < s->c.num_simulations; ++i)
+        if (int r = search_step(s, MODE_SIM)) return r;
+    return check_err(s);
+}
+
+int search_new_games(az_search* s, const int* games, int n) {
+    if (n <= 0) return 0;
+    hipStream_t st = s->e->stream;
+    for (int i = 0; i < n; ++i)
+        if (games[i] < 0 || games[i] >= s->c.n_games) return fail(AZ_ERR_ARG, "game index %d out of range", games[i]);
+    HIPCHK(hipMemcpyAsync(s->d_games, games, n * 4, hipMemcpyHostToDevice, st));
+    s->t.nd = s->arena[s->cur];
+    hipLaunchKernelGGL(k_new_games, dim3(n), dim3(64), 0, st, s->t, s->d_games, n, s->c.eval_seed);
+    hipLaunchKernelGGL(k_tt_clear, dim3(64, n), dim3(256), 0, st, s->t, s->d_games, n);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(st));
+    for (int i = 0; i < n; ++i) {
+        const int g = games[i];
+        s->stones[g] = 0; s->active[g] = 1; s->fresh[g] = 1; s->ply[g] = 0;
+        s->rng[g].seed(s->c.noise_seed + (uint32_t)(s->c.noise_seed_stride * g));
+    }
+    return 0;
+}
+
+int search_select(az_search* s, int training, const float* temps_host, float T, int* actions, float* values, float* probs,
+                  int* cact, int* nch) {
+    hipStream_t st = s->e->stream;
+    const int G = s->c.n_games, A = s->t.A;
+    s->t.nd = s->arena[s->cur];
+    if (!temps_host) {
+        hipLaunchKernelGGL(k_select_action, dim3(G), dim3(64), 0, st, s->t, training, T, s->d_actions, s->d_values,
+                           s->d_probs, s->d_cact, s->d_nch);
+    } else {
+        // per-game temperature: one launch per distinct T (the schedule has two values)
+        std::vector<float> ts(temps_host, temps_host + G);
+        std::vector<float> uniq = ts;
+        std::sort(uniq.begin(), uniq.end());
+        uniq.erase(std::unique(uniq.begin(), uniq.end()), uniq.end());
+        std::vector<int> sel(G);
+        std::vector<int> act_all(G, -1);
+        std::vector<float> val_all(G, 0.0f);
+        std::vector<int> nch_all(G, 0);
+        for (float u : uniq) {
+            hipLaunchKernelGGL(k_select_action, dim3(G), dim3(64), 0, st, s->t, training, u, s->d_actions, s->d_values,
+                               s->d_probs, s->d_cact, s->d_nch);
+            std::vector<int> a(G); std::vector<float> v(G); std::vector<int> nc(G);
+            HIPCHK(hipMemcpyAsync(a.data(), s->d_actions, G * 4, hipMemcpyDeviceToHost, st));
+            HIPCHK(hipMemcpyAsync(v.data(), s->d_values, G * 4, hipMemcpyDeviceToHost, st));
+            HIPCHK(hipMemcpyAsync(nc.data(), s->d_nch, G * 4, hipMemcpyDeviceToHost, st));
+            HIPCHK(hipStreamSynchronize(st));
+            for (int g = 0; g < G; ++g)
+                if (ts[g] == u) { act_all[g] = a[g]; val_all[g] = v[g]; nch_all[g] = nc[g]; }
+        }
+        if (actions) std::copy(act_all.begin(), act_all.end(), actions);
+        if (values) std::copy(val_all.begin(), val_all.end(), values);
+        if (nch) std::copy(nch_all.begin(), nch_all.end(), nch);
+        HIPCHK(hipMemcpyAsync(s->d_actions, act_all.data(), G * 4, hipMemcpyHostToDevice, st));
+        HIPCHK(hipStreamSynchronize(st));
+        (void)probs; (void)cact;
+        return 0;
+    }
+    HIPCHK(hipGetLastError());
+    if (actions) HIPCHK(hipMemcpyAsync(actions, s->d_actions, G * 4, hipMemcpyDeviceToHost, st));
+    if (values) HIPCHK(hipMemcpyAsync(values, s->d_values, G * 4, hipMemcpyDeviceToHost, st));
+    if (probs) HIPCHK(hipMemcpyAsync(probs, s->d_probs, (size_t)G * A * 4, hipMemcpyDeviceToHost, st));
+    if (cact) HIPCHK(hipMemcpyAsync(cact, s->d_cact, (size_t)G * A * 4, hipMemcpyDeviceToHost, st));
+    if (nch) HIPCHK(hipMemcpyAsync(nch, s->d_nch, G * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    return 0;
+}
+
+// makeMove + updateWithMove (device), then subtree compaction into the other arena.
+int search_apply_dev(az_search* s, int* terminal, int* result) {
+    hipStream_t st = s->e->stream;
+    const int G = s->c.n_games;
+    s->t.nd = s->arena[s->cur];
+    std::vector<int> acts(G);
+    HIPCHK(hipMemcpyAsync(acts.data(), s->d_actions, G * 4, hipMemcpyDeviceToHost, st));
+    hipLaunchKernelGGL(k_apply, dim3(G), dim3(64), 0, st, s->t, s->d_actions, s->d_term, s->d_res);
+    hipLaunchKernelGGL(k_compact, dim3(G), dim3(64), 0, st, s->t, s->arena[s->cur ^ 1], s->d_src_of);
+    HIPCHK(hipGetLastError());
+    s->cur ^= 1;
+    s->t.nd = s->arena[s->cur];
+    std::vector<int> term(G), res(G);
+    HIPCHK(hipMemcpyAsync(term.data(), s->d_term, G * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(res.data(), s->d_res, G * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    for (int g = 0; g < G; ++g) {
+        if (s->active[g] && acts[g] >= 0) {
+            s->stones[g] += 1; s->ply[g] += 1; s->fresh[g] = 0;
+            if (term[g]) s->active[g] = 0;
+        }
+    }
+    if (terminal) std::copy(term.begin(), term.end(), terminal);
+    if (result) std::copy(res.begin(), res.end(), result);
+    return check_err(s);
+}
+
+}  // namespace
+
+// ===========================================================================
+extern "C" {
+
+const char* az_last_error(void) { return g_err.c_str(); }
+
+int az_engine_create(int device, az_engine** out) {
+    if (!out) return fail(AZ_ERR_ARG, "null out");
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess || n <= 0) return fail(AZ_ERR_HIP, "no HIP device available (hipGetDeviceCount: %s)", hipGetErrorString(e));
+    if (device < 0 || device >= n) return fail(AZ_ERR_ARG, "device %d out of range (%d devices)", device, n);
+    auto* en = new az_engine();
+    en->device = device;
+    hipError_t r = hipSetDevice(device);
+    if (r == hipSuccess) r = hipGetDeviceProperties(&en->prop, device);
+    if (r == hipSuccess) r = hipStreamCreateWithFlags(&en->stream, hipStreamNonBlocking);
+    if (r != hipSuccess) { delete en; return fail(AZ_ERR_HIP, "device init: %s", hipGetErrorString(r)); }
+    *out = en;
+    return 0;
+}
+
+void az_engine_destroy(az_engine* e) {
+    if (!e) return;
+    hipSetDevice(e->device);
+    if (e->stream) hipStreamDestroy(e->stream);
+    delete e;
+}
+
+int az_engine_device_name(az_engine* e, char* buf, int len) {
+    if (!e || !buf || len <= 0) return fail(AZ_ERR_ARG, "bad args");
+    snprintf(buf, len, "%s (%s)", e->prop.name, e->prop.gcnArchName);
+    return 0;
+}
+
+// ------------------------------------------------------------------ net
+int az_net_create(az_engine* e, const az_net_desc* d, az_net** out) {
+    if (!e || !d || !out) return fail(AZ_ERR_ARG, "null argument");
+    if (d->board_size < 2 || d->board_size * d->board_size > AZ_MAXA || d->in_planes < 1 || d->in_planes > 16 ||
+        d->channels < 4 || d->channels % 4 || d->blocks < 0 || d->action_size < 1 || d->action_size > 4096 ||
+        d->head_channels < 1 || d->head_channels % 4 || d->pool < 1 || d->fc_hidden < 1 || d->fc_hidden % 4 ||
+        d->max_batch < 1)
+        return fail(AZ_ERR_ARG, "unsupported network description");
+    std::lock_guard<std::mutex> lk(e->mu);
+    HIPCHK(hipSetDevice(e->device));
+    auto* n = new az_net();
+    n->e = e;
+    n->d = *d;
+    n->HW = d->board_size * d->board_size;
+    n->P2 = d->pool * d->pool;
+    n->nparams = count_params(*d);
+    const size_t B = d->max_batch, rows = B * n->HW, F = d->channels;
+    int r = 0;
+    auto A_ = [&](float** p, size_t cnt) { if (!r) r = dalloc(p, cnt); };
+    auto H_ = [&](uint16_t** p, size_t cnt) { if (!r) r = dalloc(p, cnt); };
+    A_(&n->x0, rows * n->cin_pad);
+    A_(&n->h0, rows * F); A_(&n->h1, rows * F); A_(&n->t, rows * F);
+    if (F % 32 == 0) {
+        H_(&n->hh[0], rows * F); H_(&n->hh[1], rows * F); H_(&n->hl[0], rows * F); H_(&n->hl[1], rows * F);
+        H_(&n->th, rows * F); H_(&n->tl, rows * F);
+    }
+    A_(&n->pool, B * n->P2 * F);
+    A_(&n->pp, B * n->P2 * d->head_channels); A_(&n->vp, B * n->P2 * d->head_channels);
+    A_(&n->v1, B * d->fc_hidden);
+    A_(&n->logits, B * d->action_size); A_(&n->value, B); A_(&n->soft, B * d->action_size);
+    A_(&n->in_nchw, B * d->in_planes * n->HW);
+    if (!r) r = dalloc(&n->d_nb, 1);
+    if (r) { az_net_destroy(n); return r; }
+    *out = n;
+    return 0;
+}
+
+void az_net_destroy(az_net* n) {
+    if (!n) return;
+    hipSetDevice(n->e->device);
+    auto F = [](void* p) { if (p) hipFree(p); };
+    std::vector<Layer*> ls = {&n->in, &n->pconv, &n->vconv, &n->pfc, &n->vfc1, &n->vfc2};
+    for (auto& l : n->blk) ls.push_back(&l);
+    for (Layer* l : ls) { F(l->W); F(l->b); F(l->Whi); F(l->Wlo); }
+    for (void* p : {(void*)n->x0, (void*)n->h0, (void*)n->h1, (void*)n->t, (void*)n->pool, (void*)n->pp, (void*)n->vp,
+                    (void*)n->v1, (void*)n->logits, (void*)n->value, (void*)n->soft, (void*)n->in_nchw, (void*)n->d_nb,
+                    (void*)n->hh[0], (void*)n->hh[1], (void*)n->hl[0], (void*)n->hl[1], (void*)n->th, (void*)n->tl})
+        F(p);
+    delete n;
+}
+
+int az_net_num_params(az_net* n, size_t* count) {
+    if (!n || !count) return fail(AZ_ERR_ARG, "null argument");
+    *count = n->nparams;
+    return 0;
+}
+
+int az_net_load_weights(az_net* n, const float* blob, size_t count) {
+    if (!n || !blob) return fail(AZ_ERR_ARG, "null argument");
+    if (count != n->nparams) return fail(AZ_ERR_ARG, "expected %zu parameters, got %zu", n->nparams, count);
+    std::lock_guard<std::mutex> lk(n->mu);
+    HIPCHK(hipSetDevice(n->e->device));
+    return net_load(n, blob);
+}
+
+// Counter-based init; tests/nn_weights.py restates it in numpy (same fp32 ops).
+int az_net_init_random(az_net* n, uint64_t seed) {
+    if (!n) return fail(AZ_ERR_ARG, "null net");
+    const az_net_desc& d = n->d;
+    std::vector<float> blob(n->nparams);
+    size_t off = 0;
+    int tensor = 0;
+    auto fill = [&](size_t cnt, int kind, int fan_in) {
+        // kind: 0 weight U(-1,1)/sqrt(fan_in); 1 bias U(-1,1)/sqrt(fan_in); 2 bn gamma 1+0.1u;
+        //       3 bn beta 0.1u; 4 bn mean 0.1u; 5 bn var 1+0.25(u+1)
+        const float bound = 1.0f / std::sqrt((float)fan_in);
+        for (size_t i = 0; i < cnt; ++i) {
+            const uint64_t r = splitmix64(seed ^ ((uint64_t)tensor << 40) ^ (uint64_t)i);
+            const float u = (float)(int32_t)(r >> 40) * (1.0f / 8388608.0f) - 1.0f;
+            float v;
+            switch (kind) {
+                case 0: case 1: v = u * bound; break;
+                case 2: v = 1.0f + 0.1f * u; break;
+                case 3: case 4: v = 0.1f * u; break;
+                default: v = 1.0f + 0.25f * (u + 1.0f); break;
+            }
+            blob[off + i] = v;
+        }
+        off += cnt;
+        ++tensor;
+    };
+    const int F = d.channels, HC = d.head_channels, PP = d.pool * d.pool;
+    auto conv = [&](int co, int ci, int k) {
+        fill((size_t)co * ci * k * k, 0, ci * k * k);
+        if (d.conv_bias) fill(co, 1, ci * k * k);
+        fill(co, 2, 1); fill(co, 3, 1); fill(co, 4, 1); fill(co, 5, 1);
+    };
+    conv(F, d.in_planes, 3);
+    for (int i = 0; i < d.blocks; ++i) { conv(F, F, 3); conv(F, F, 3); }
+    conv(HC, F, 1);
+    fill((size_t)d.action_size * HC * PP, 0, HC * PP); fill(d.action_size, 1, HC * PP);
+    conv(HC, F, 1);
+    fill((size_t)d.fc_hidden * HC * PP, 0, HC * PP); fill(d.fc_hidden, 1, HC * PP);
+    fill(d.fc_hidden, 0, d.fc_hidden); fill(1, 1, d.fc_hidden);
+    if (off != n->nparams) return fail(AZ_ERR_STATE, "init size mismatch");
+    return az_net_load_weights(n, blob.data(), blob.size());
+}
+
+int az_net_set_precision(az_net* n, int precision) {
+    if (!n || precision < 0 || precision > 2) return fail(AZ_ERR_ARG, "bad precision");
+    if (precision != AZ_PREC_F32 && n->d.channels % 32) return fail(AZ_ERR_ARG, "bf16 trunk needs channels %% 32 == 0");
+    n->d.precision = precision;
+    return 0;
+}
+
+static int net_host_forward(az_net* n, const float* planes, int B, float* logits, float* value, bool soft) {
+    if (!n || !planes || B < 1 || B > n->d.max_batch) return fail(AZ_ERR_ARG, "bad batch (1..%d)", n ? n->d.max_batch : 0);
+    if (!n->loaded) return fail(AZ_ERR_STATE, "weights not loaded");
+    std::lock_guard<std::mutex> lk(n->mu);
+    HIPCHK(hipSetDevice(n->e->device));
+    hipStream_t st = n->e->stream;
+    const int A = n->d.action_size;
+    HIPCHK(hipMemcpyAsync(n->in_nchw, planes, (size_t)B * n->d.in_planes * n->HW * 4, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(n->d_nb, &B, 4, hipMemcpyHostToDevice, st));
+    az_launch_pack_input(n->in_nchw, n->x0, B, n->d.in_planes, n->HW, n->cin_pad, st);
+    if (int r = net_forward(n, n->x0, B, n->d_nb, n->logits, n->value, st)) return r;
+    const float* pol = n->logits;
+    if (soft) { az_launch_softmax_rows(n->logits, n->soft, B, A, st); pol = n->soft; }
+    HIPCHK(hipGetLastError());
+    if (logits) HIPCHK(hipMemcpyAsync(logits, pol, (size_t)B * A * 4, hipMemcpyDeviceToHost, st));
+    if (value) HIPCHK(hipMemcpyAsync(value, n->value, (size_t)B * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    return 0;
+}
+
+int az_net_forward(az_net* n, const float* planes, int B, float* logits, float* value) {
+    return net_host_forward(n, planes, B, logits, value, false);
+}
+
+int az_net_predict_batch(az_net* n, const float* planes, int B, float* policy, float* value) {
+    return net_host_forward(n, planes, B, policy, value, true);
+}
+
+// ------------------------------------------------------------------ search
+int az_search_create(az_engine* e, az_net* net, const az_search_cfg* c, az_search** out) {
+    if (!e || !c || !out) return fail(AZ_ERR_ARG, "null argument");
+    const int bs = c->board_size, A = bs * bs, G = c->n_games;
+    if (bs < 3 || A > AZ_MAXA || G < 1 || c->num_simulations < 0 || c->virtual_loss < 0 || c->tt_log2 < 4 ||
+        c->tt_log2 > 24 || c->eval_kind < 0 || c->eval_kind > 2)
+        return fail(AZ_ERR_ARG, "unsupported search configuration");
+    if (c->eval_kind == AZ_EVAL_NET) {
+        if (!net) return fail(AZ_ERR_ARG, "AZ_EVAL_NET needs a network");
+        if (net->d.board_size != bs || net->d.action_size != A || net->d.in_planes != 11)
+            return fail(AZ_ERR_ARG, "network shape does not match the board");
+        if (net->d.max_batch < G) return fail(AZ_ERR_ARG, "network max_batch %d < n_games %d", net->d.max_batch, G);
+        if (!net->loaded) return fail(AZ_ERR_STATE, "network weights not loaded");
+    }
+    std::lock_guard<std::mutex> lk(e->mu);
+    HIPCHK(hipSetDevice(e->device));
+    auto* s = new az_search();
+    s->e = e; s->net = net; s->c = *c;
+    const int ncap = c->node_capacity > 0 ? c->node_capacity : 3 * std::max(64, c->num_simulations) * A + 8 * A + 64;
+    const int ring = c->prior_ring > 0 ? c->prior_ring : std::max(1 << 16, 12 * std::max(64, c->num_simulations) * A);
+    s->c.node_capacity = ncap; s->c.prior_ring = ring;
+    TreeDev& t = s->t;
+    t.G = G; t.bs = bs; t.A = A; t.ncap = ncap; t.vl = c->virtual_loss; t.cpuct = c->c_puct; t.fpu = c->fpu_reduction;
+    t.eval_kind = c->eval_kind; t.tt_slots = 1 << c->tt_log2; t.tt_mask = (uint64_t)t.tt_slots - 1; t.ring = ring;
+    t.log_game = -1; t.log_cap = 0;
+    const size_t NG = (size_t)G * ncap;
+    int r = 0;
+#define SA(p, n) do { if (!r) r = dalloc(&(p), (size_t)(n)); } while (0)
+    for (int k = 0; k < 2; ++k) {
+        Nodes& nd = s->arena[k];
+        SA(nd.N, NG); SA(nd.W, NG); SA(nd.VL, NG); SA(nd.P, NG); SA(nd.first, NG); SA(nd.act, NG); SA(nd.cnt, NG);
+        SA(nd.flag, NG);
+    }
+    SA(t.atop, G); SA(t.rboard, (size_t)G * A); SA(t.rhist, G * 6); SA(t.rplayer, G); SA(t.rstones, G); SA(t.rply, G);
+    SA(t.rhash, G); SA(t.rfresh, G); SA(t.rnode, G); SA(t.active, G); SA(t.gresult, G);
+    SA(t.path, (size_t)G * AZ_DMAX); SA(t.plen, G); SA(t.lstatus, G); SA(t.lvalue, G); SA(t.lhash, G); SA(t.ttstore, G);
+    SA(t.ttref, G); SA(t.tthslot, G); SA(t.need_eval, G); SA(t.eval_slot, G); SA(t.eval_games, G); SA(t.n_eval, 1);
+    SA(t.planes, (size_t)G * A * 16);
+    SA(t.tt_hash, (size_t)G * t.tt_slots); SA(t.tt_visits, (size_t)G * t.tt_slots); SA(t.tt_value, (size_t)G * t.tt_slots);
+    SA(t.tt_ref, (size_t)G * t.tt_slots);
+    SA(t.ring_buf, (size_t)G * ring); SA(t.ring_cur, G); SA(t.cnt, (size_t)G * AZ_NCNT);
+    if (!r) r = hipMemset(t.cnt, 0, (size_t)G * AZ_NCNT * 8) == hipSuccess ? 0 : fail(AZ_ERR_HIP, "memset");
+    uint64_t* zp = nullptr; uint64_t* zpl = nullptr; int* fo = nullptr;
+    SA(zp, 2 * A); SA(zpl, 2); SA(fo, A);
+    if (c->eval_kind == AZ_EVAL_RANDOM) SA(t.mt, (size_t)G * 625);
+    SA(t.err, 1);
+    SA(s->d_src_of, NG);
+    if (c->eval_kind == AZ_EVAL_NET) { SA(s->d_batch, (size_t)G * A * 16); SA(s->d_logits, (size_t)G * A); SA(s->d_value, G); }
+    SA(s->d_noise, (size_t)G * A); SA(s->d_mask, G); SA(s->d_actions, G); SA(s->d_values, G); SA(s->d_probs, (size_t)G * A);
+    SA(s->d_cact, (size_t)G * A); SA(s->d_nch, G); SA(s->d_term, G); SA(s->d_res, G); SA(s->d_games, G); SA(s->d_temps, G);
+#undef SA
+    if (r) { az_search_destroy(s); return r; }
+    t.zpiece = zp; t.zplayer = zpl; t.fresh_order = fo;
+    t.net_logits = s->d_logits; t.net_value = s->d_value;
+    // Zobrist keys: ZobristHash(bs, 2, 2, seed) (src/core/zobrist_hash.cpp:9-36)
+    {
+        std::mt19937_64 rng(c->zobrist_seed);
+        std::vector<uint64_t> keys(2 * A + 2);
+        for (auto& k : keys) k = rng();
+        HIPCHK(hipMemcpy(zp, keys.data(), 2 * A * 8, hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(zpl, keys.data() + 2 * A, 16, hipMemcpyHostToDevice));
+    }
+    // First-query legal order of a fresh GomokuState: libstdc++ unordered_set growth
+    {
+        std::unordered_set<int> set;
+        for (int a = 0; a < A; ++a) set.insert(a);
+        std::vector<int> order(set.begin(), set.end());
+        HIPCHK(hipMemcpy(fo, order.data(), A * 4, hipMemcpyHostToDevice));
+    }
+    HIPCHK(hipMemset(t.err, 0, 4));
+    HIPCHK(hipMemset(t.active, 0, G * 4));
+    s->stones.assign(G, 0); s->active.assign(G, 0); s->fresh.assign(G, 1); s->ply.assign(G, 0); s->expanded.assign(G, 0);
+    s->rng.resize(G);
+    s->h_noise.assign((size_t)G * A, 0.0f);
+    s->h_mask.assign(G, 0);
+    *out = s;
+    return 0;
+}
+
+void az_search_destroy(az_search* s) {
+    if (!s) return;
+    hipSetDevice(s->e->device);
+    auto F = [](const void* p) { if (p) hipFree((void*)p); };
+    for (auto& nd : s->arena) { F(nd.N); F(nd.W); F(nd.VL); F(nd.P); F(nd.first); F(nd.act); F(nd.cnt); F(nd.flag); }
+    TreeDev& t = s->t;
+    for (const void* p : {(const void*)t.atop, (const void*)t.rboard, (const void*)t.rhist, (const void*)t.rplayer,
+                          (const void*)t.rstones, (const void*)t.rply, (const void*)t.rhash, (const void*)t.rfresh,
+                          (const void*)t.rnode, (const void*)t.active, (const void*)t.gresult, (const void*)t.path,
+                          (const void*)t.plen, (const void*)t.lstatus, (const void*)t.lvalue, (const void*)t.lhash,
+                          (const void*)t.ttstore, (const void*)t.ttref, (const void*)t.tthslot, (const void*)t.need_eval,
+                          (const void*)t.eval_slot, (const void*)t.eval_games, (const void*)t.n_eval, (const void*)t.planes,
+                          (const void*)t.tt_hash, (const void*)t.tt_visits, (const void*)t.tt_value, (const void*)t.tt_ref,
+                          (const void*)t.ring_buf, (const void*)t.ring_cur, (const void*)t.cnt, (const void*)t.zpiece,
+                          (const void*)t.zplayer, (const void*)t.fresh_order, (const void*)t.mt, (const void*)t.err,
+                          (const void*)t.log_pol, (const void*)t.log_val, (const void*)t.log_planes, (const void*)t.log_n,
+                          (const void*)s->d_src_of, (const void*)s->d_batch, (const void*)s->d_logits,
+                          (const void*)s->d_value, (const void*)s->d_noise, (const void*)s->d_mask, (const void*)s->d_actions,
+                          (const void*)s->d_values, (const void*)s->d_probs, (const void*)s->d_cact, (const void*)s->d_nch,
+                          (const void*)s->d_term, (const void*)s->d_res, (const void*)s->d_games, (const void*)s->d_temps})
+        F(p);
+    delete s;
+}
+
+int az_search_new_games(az_search* s, const int* games, int n) {
+    if (!s || (!games && n)) return fail(AZ_ERR_ARG, "null argument");
+    std::lock_guard<std::mutex> lk(s->mu);
+    HIPCHK(hipSetDevice(s->e->device));
+    return search_new_games(s, games, n);
+}
+
+int az_search_add_noise(az_search* s, float alpha, float eps) {
+    if (!s) return fail(AZ_ERR_ARG, "null search");
+    std::lock_guard<std::mutex> lk(s->mu);
+    HIPCHK(hipSetDevice(s->e->device));
+    return search_noise(s, alpha, eps, nullptr);
+}
+
+int az_search_add_noise_masked(az_search* s, float alpha, float eps, const uint8_t* mask) {
+    if (!s || !mask) return fail(AZ_ERR_ARG, "null argument");
+    std::lock_guard<std::mutex> lk(s->mu);
+    HIPCHK(hipSetDevice(s->e->device));
+    return search_noise(s, alpha, eps, mask);
+}
+
+int az_search_run(az_search* s) {
+    if (!s) return fail(AZ_ERR_ARG, "null search");
+    std::lock_guard<std::mutex> lk(s->mu);
+    HIPCHK(hipSetDevice(s->e->device));
+    return search_run(s);
+}
+
+int az_search_select(az_search* s, int training, float temperature, int* actions, float* root_values, float* probs,
+                     int* children_actions, int* n_children) {
+    if (!s) return fail(AZ_ERR_ARG, "null search");
+    std::lock_guard<std::mutex> lk(s->mu);
+    HIPCHK(hipSetDevice(s->e->device));
+    return search_select(s, training, nullptr, temperature, actions, root_values, probs, children_actions, n_children);
+}
+
+int az_search_apply(az_search* s, const int* actions, int* terminal, int* result) {
+    if (!s || !actions) return fail(AZ_ERR_ARG, "null argument");
+    std::lock_guard<std::mutex> lk(s->mu);
+    HIPCHK(hipSetDevice(s->e->device));
+    const int G = s->c.n_games, A = s->t.A;
+    for (int g = 0; g < G; ++g)
+        if (actions[g] >= A) return fail(AZ_ERR_ARG, "action %d out of range for game %d", actions[g], g);
+    HIPCHK(hipMemcpyAsync(s->d_actions, actions, G * 4, hipMemcpyHostToDevice, s->e->stream));
+    return search_apply_dev(s, terminal, result);
+}
+
+int az_search_root_children(az_search* s, int game, int* actions, int* N, int* VL, float* W, float* P, int* n_children) {
+    if (!s || game < 0 || game >= s->c.n_games || !n_children) return fail(AZ_ERR_ARG, "bad argument");
+    std::lock_guard<std::mutex> lk(s->mu);
+    HIPCHK(hipSetDevice(s->e->device));
+    hipStream_t st = s->e->stream;
+    const int A = s->t.A;
+    int *da, *dN, *dVL, *dn, *dri; float *dW, *dP, *drw;
+    DALLOC(da, A); DALLOC(dN, A); DALLOC(dVL, A); DALLOC(dn, 1); DALLOC(dri, 2); DALLOC(dW, A); DALLOC(dP, A); DALLOC(drw, 1);
+    s->t.nd = s->arena[s->cur];
+    hipLaunchKernelGGL(k_root_children, dim3(1), dim3(256), 0, st, s->t, game, da, dN, dVL, dW, dP, dn, dri, drw);
+    int n = 0;
+    HIPCHK(hipMemcpyAsync(&n, dn, 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    if (actions) HIPCHK(hipMemcpy(actions, da, n * 4, hipMemcpyDeviceToHost));
+    if (N) HIPCHK(hipMemcpy(N, dN, n * 4, hipMemcpyDeviceToHost));
+    if (VL) HIPCHK(hipMemcpy(VL, dVL, n * 4, hipMemcpyDeviceToHost));
+    if (W) HIPCHK(hipMemcpy(W, dW, n * 4, hipMemcpyDeviceToHost));
+    if (P) HIPCHK(hipMemcpy(P, dP, n * 4, hipMemcpyDeviceToHost));
+    *n_children = n;
+    for (void* p : {(void*)da, (void*)dN, (void*)dVL, (void*)dn, (void*)dri, (void*)dW, (void*)dP, (void*)drw}) hipFree(p);
+    return 0;
+}
+
+int az_search_root_node(az_search* s, int game, int* N, int* VL, float* W) {
+    if (!s || game < 0 || game >= s->c.n_games) return fail(AZ_ERR_ARG, "bad argument");
+    std::lock_guard<std::mutex> lk(s->mu);
+    HIPCHK(hipSetDevice(s->e->device));
+    int root = 0;
+    HIPCHK(hipMemcpy(&root, s->t.rnode + game, 4, hipMemcpyDeviceToHost));
+    const size_t off = (size_t)game * s->t.ncap + root;
+    const Nodes& nd = s->arena[s->cur];
+    if (N) HIPCHK(hipMemcpy(N, nd.N + off, 4, hipMemcpyDeviceToHost));
+    if (VL) HIPCHK(hipMemcpy(VL, nd.VL + off, 4, hipMemcpyDeviceToHost));
+    if (W) HIPCHK(hipMemcpy(W, nd.W + off, 4, hipMemcpyDeviceToHost));
+    return 0;
+}
+
+int az_search_counters(az_search* s, int game, int64_t* out5) {
+    if (!s || game < 0 || game >= s->c.n_games || !out5) return fail(AZ_ERR_ARG, "bad argument");
+    std::lock_guard<std::mutex> lk(s->mu);
+    HIPCHK(hipSetDevice(s->e->device));
+    long long c[AZ_NCNT];
+    HIPCHK(hipMemcpy(c, s->t.cnt + (size_t)game * AZ_NCNT, sizeof c, hipMemcpyDeviceToHost));
+    for (int i = 0; i < 5; ++i) out5[i] = c[i];
+    return 0;
+}
+
+int az_search_enable_eval_log(az_search* s, int game, int capacity) {
+    if (!s || game < 0 || game >= s->c.n_games || capacity < 1) return fail(AZ_ERR_ARG, "bad argument");
+    std::lock_guard<std::mutex> lk(s->mu);
+    HIPCHK(hipSetDevice(s->e->device));
+    TreeDev& t = s->t;
+    if (t.log_pol) { hipFree(t.log_pol); hipFree(t.log_val); hipFree(t.log_planes); hipFree(t.log_n); }
+    t.log_pol = nullptr; t.log_val = nullptr; t.log_planes = nullptr; t.log_n = nullptr;
+    DALLOC(t.log_pol, (size_t)capacity * t.A); DALLOC(t.log_val, capacity); DALLOC(t.log_planes, (size_t)capacity * 11 * t.A);
+    DALLOC(t.log_n, 1);
+    HIPCHK(hipMemset(t.log_n, 0, 4));
+    t.log_game = game; t.log_cap = capacity;
+    return 0;
+}
+
+int az_search_read_eval_log(az_search* s, float* policy, float* value, float* planes, int* count) {
+    if (!s || !count) return fail(AZ_ERR_ARG, "bad argument");
+    std::lock_guard<std::mutex> lk(s->mu);
+    HIPCHK(hipSetDevice(s->e->device));
+    TreeDev& t = s->t;
+    if (!t.log_pol) { *count = 0; return 0; }
+    int n = 0;
+    HIPCHK(hipMemcpy(&n, t.log_n, 4, hipMemcpyDeviceToHost));
+    if (policy) HIPCHK(hipMemcpy(policy, t.log_pol, (size_t)n * t.A * 4, hipMemcpyDeviceToHost));
+    if (value) HIPCHK(hipMemcpy(value, t.log_val, (size_t)n * 4, hipMemcpyDeviceToHost));
+    if (planes) HIPCHK(hipMemcpy(planes, t.log_planes, (size_t)n * 11 * t.A * 4, hipMemcpyDeviceToHost));
+    *count = n;
+    return 0;
+}
+
+// One playSingleGame move for every active game (self_play_manager.cpp:187-216).
+int az_selfplay_step(az_search* s, const az_selfplay_cfg* cfg, int64_t* moves_done, int64_t* evals_done) {
+    if (!s || !cfg) return fail(AZ_ERR_ARG, "null argument");
+    std::lock_guard<std::mutex> lk(s->mu);
+    HIPCHK(hipSetDevice(s->e->device));
+    const int G = s->c.n_games;
+    std::vector<long long> c0((size_t)G * AZ_NCNT), c1((size_t)G * AZ_NCNT);
+    if (evals_done) HIPCHK(hipMemcpy(c0.data(), s->t.cnt, c0.size() * 8, hipMemcpyDeviceToHost));
+    if (int r = search_run(s)) return r;
+    std::vector<float> temps(G);
+    std::vector<int> was_active = s->active;
+    std::vector<int> ply0 = s->ply;
+    for (int g = 0; g < G; ++g) temps[g] = s->ply[g] >= cfg->temp_drop_move ? cfg->t_final : cfg->t_init;
+    std::vector<int> actions(G);
+    if (int r = search_select(s, 1, temps.data(), 0.0f, actions.data(), nullptr, nullptr, nullptr, nullptr)) return r;
+    std::vector<int> term(G), res(G);
+    if (int r = search_apply_dev(s, term.data(), res.data())) return r;
+    int64_t moves = 0;
+    std::vector<uint8_t> noise_mask(G, 0);
+    for (int g = 0; g < G; ++g) {
+        if (!was_active[g] || actions[g] < 0) continue;
+        ++moves;
+        if (ply0[g] % 2 == 0) noise_mask[g] = 1;
+    }
+    if (int r = search_noise(s, s->c.dirichlet_alpha, s->c.dirichlet_eps, noise_mask.data())) return r;
+    if (cfg->restart_finished) {
+        std::vector<int> fin;
+        for (int g = 0; g < G; ++g) if (!s->active[g]) fin.push_back(g);
+        if (!fin.empty()) {
+            if (int r = search_new_games(s, fin.data(), (int)fin.size())) return r;
+            std::vector<uint8_t> m(G, 0);
+            for (int g : fin) m[g] = 1;
+            if (int r = search_noise(s, s->c.dirichlet_alpha, s->c.dirichlet_eps, m.data())) return r;
+        }
+    }
+    if (moves_done) *moves_done += moves;
+    if (evals_done) {
+        HIPCHK(hipMemcpy(c1.data(), s->t.cnt, c1.size() * 8, hipMemcpyDeviceToHost));
+        long long ev = 0;
+        for (int g = 0; g < G; ++g) ev += c1[(size_t)g * AZ_NCNT + CNT_EVALS_TOTAL] - c0[(size_t)g * AZ_NCNT + CNT_EVALS_TOTAL];
+        *evals_done += ev;
+    }
+    return 0;
+}
+
+}  // extern "C"

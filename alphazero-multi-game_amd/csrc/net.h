@@ -1,0 +1,40 @@
+// net.h -- launch interface of the ConvNet kernels (net_kernels.hip, conv_bf16.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+enum { ACT_NONE = 0, ACT_RELU = 1, ACT_TANH = 2 };
+
+// out[m][n] = act( sum_k A(m,k) * B[n][k] + bias[n] (+ res[m][n]) ),  k = tap*C + c
+struct GemmArgs {
+    const float* A; int lda;        // activations, row-major [rows][lda] (NHWC for convs)
+    const float* B; int ldb;        // weights [N][ldb], BN folded
+    float* C; int ldc;              // output [rows][ldc]
+    const float* bias;              // [N] or null
+    const float* res;               // residual [rows][ldc] or null
+    int M, N, K, Kpad;              // K = taps*C, Kpad = K rounded up to the k-tile
+    int taps, Cch;                  // 9 (3x3, pad 1) or 1; channels per tap
+    int H, W;                       // spatial size of one sample (taps == 9)
+    const int* m_limit;             // device: active samples (leaf batch) or null
+    int rows_per_sample;            // rows of one sample (H*W, P*P or 1)
+};
+
+// bf16 trunk conv: activations stored as bf16 hi (+ lo) planes, NHWC.
+struct ConvBf16Args {
+    const uint16_t* Ahi; const uint16_t* Alo;   // [rows][C] bf16 (Alo null for plain bf16)
+    const uint16_t* Bhi; const uint16_t* Blo;   // [N][9*C] bf16
+    uint16_t* Chi; uint16_t* Clo;               // outputs (split for the next layer)
+    float* Cf;                                  // optional fp32 output [rows][N]
+    const float* bias;
+    const uint16_t* Rhi; const uint16_t* Rlo;   // residual (split) or null
+    int M, N, C, H, W;
+    const int* m_limit; int rows_per_sample;
+    int relu;
+};
+
+void az_launch_gemm_f32(const GemmArgs& p, int act, bool res, hipStream_t st);
+void az_launch_pool(const float* in, float* out, int B, int H, int W, int C, int P, const int* m_limit, hipStream_t st);
+void az_launch_pack_input(const float* in, float* out, int B, int Cin, int HW, int Cp, hipStream_t st);
+void az_launch_gather_planes(const float* src, float* dst, const int* eval_games, const int* n_eval, int per, int maxB,
+                             hipStream_t st);
+void az_launch_softmax_rows(const float* logits, float* out, int B, int A, hipStream_t st);

@@ -1,0 +1,262 @@
+// net_kernels.hip -- ConvNet forward for the leaf batch (gfx950).
+//
+// Every layer of the policy/value net is one implicit
+// GEMM  out[m][n] = act( sum_k A(m,k) * Wt[n][k] + bias[n] (+ res[m][n]) )
+//   3x3 conv : m = pixel (b, y, x) of an NHWC activation, k = (tap, c), A gathered
+//              from the 3x3 neighbourhood (zero padding), BN folded into Wt/bias
+//   1x1 conv : taps = 1 over pooled pixels;  FC : taps = 1 over samples.
+// Kernels here:
+//   gemm_f32   f32-input MFMA (v_mfma_f32_32x32x2_f32): exact f32 products, the
+//              AZ_PREC_F32 path and the head layers of every precision.
+//   (bf16 MFMA trunk kernels live in conv_bf16.hip.)
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "net.h"
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+namespace {
+
+template <int ACT>
+__device__ __forceinline__ float activate(float v) {
+    if (ACT == ACT_RELU) return v > 0.0f ? v : 0.0f;
+    if (ACT == ACT_TANH) return tanhf(v);
+    return v;
+}
+
+}  // namespace
+
+// Block tile BM x BN (BM = 128), BK = 32, 256 threads = 2x2 waves, wave tile
+// (BM/2) x (BN/2) of 32x32 MFMA tiles.  LDS holds A and B transposed ([k][m] with
+// row stride BM+1 / BN+1, conflict-free for the transposed writes and for the
+// MFMA operand reads), double buffered; global loads are register staged.
+template <int BN, int ACT, bool RES>
+__global__ __launch_bounds__(256) void gemm_f32(GemmArgs p) {
+    constexpr int BM = 128, BK = 32;
+    constexpr int LDA = BM + 1, LDB = BN + 1;
+    constexpr int TM = BM / 2, TN = BN / 2;
+    constexpr int MT = TM / 32, NT = TN / 32;
+    constexpr int BROWS = BN / 32;   // B rows loaded per thread (BN*8 float4 / 256 threads)
+    __shared__ float As[2][BK * LDA];
+    __shared__ float Bs[2][BK * LDB];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, wave = tid >> 6;
+    const int wm = wave >> 1, wn = wave & 1;
+    const int nbm = (p.M + BM - 1) / BM;
+    const int bid = blockIdx.x;
+    const int bm = bid % nbm, bn = bid / nbm;
+    const int m0 = bm * BM, n0 = bn * BN;
+    // device-side leaf batch: rows beyond n_eval * rows_per_sample are skipped
+    const int Mact = p.m_limit ? min(p.M, *p.m_limit * p.rows_per_sample) : p.M;
+    if (m0 >= Mact) return;
+
+    // Per-thread A rows: m = tid/8 + 32*i, float4 column kq = tid%8.
+    const int kq = tid & 7;
+    const int r0 = tid >> 3;
+    int arow_b[4], arow_y[4], arow_x[4];
+    bool arow_ok[4];
+    for (int i = 0; i < 4; ++i) {
+        const int m = m0 + r0 + 32 * i;
+        arow_ok[i] = m < Mact;
+        const int pix = p.H * p.W;
+        const int b = m / pix, r = m % pix;
+        arow_b[i] = b; arow_y[i] = r / p.W; arow_x[i] = r % p.W;
+    }
+    const int K = p.K;           // taps * C
+    const int nk = (p.Kpad + BK - 1) / BK;
+
+    float4 ra[4], rb[BROWS];
+    auto load_stage = [&](int kt) {
+        const int k = kt * BK + kq * 4;
+        int tap = 0, c = k;
+        if (p.taps == 9) { tap = k / p.Cch; c = k - tap * p.Cch; }
+        const int dy = tap / 3 - 1, dx = tap % 3 - 1;
+        for (int i = 0; i < 4; ++i) {
+            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (arow_ok[i] && k < K) {
+                const float* src = nullptr;
+                if (p.taps == 9) {
+                    const int y = arow_y[i] + dy, x = arow_x[i] + dx;
+                    if (y >= 0 && y < p.H && x >= 0 && x < p.W)
+                        src = p.A + ((size_t)(arow_b[i] * p.H + y) * p.W + x) * p.lda + c;
+                } else {
+                    src = p.A + (size_t)(m0 + r0 + 32 * i) * p.lda + c;
+                }
+                if (src) v = *reinterpret_cast<const float4*>(src);
+            }
+            ra[i] = v;
+        }
+        for (int i = 0; i < BROWS; ++i) {
+            const int n = n0 + r0 + 32 * i;
+            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (n < p.N && k < K) v = *reinterpret_cast<const float4*>(p.B + (size_t)n * p.ldb + k);
+            rb[i] = v;
+        }
+    };
+    auto store_stage = [&](int buf) {
+        float* as = As[buf];
+        float* bs = Bs[buf];
+        for (int i = 0; i < 4; ++i) {
+            const int m = r0 + 32 * i;
+            as[(kq * 4 + 0) * LDA + m] = ra[i].x;
+            as[(kq * 4 + 1) * LDA + m] = ra[i].y;
+            as[(kq * 4 + 2) * LDA + m] = ra[i].z;
+            as[(kq * 4 + 3) * LDA + m] = ra[i].w;
+        }
+        for (int i = 0; i < BROWS; ++i) {
+            const int n = r0 + 32 * i;
+            bs[(kq * 4 + 0) * LDB + n] = rb[i].x;
+            bs[(kq * 4 + 1) * LDB + n] = rb[i].y;
+            bs[(kq * 4 + 2) * LDB + n] = rb[i].z;
+            bs[(kq * 4 + 3) * LDB + n] = rb[i].w;
+        }
+    };
+
+    floatx16 acc[MT][NT];
+    for (int i = 0; i < MT; ++i)
+        for (int j = 0; j < NT; ++j)
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
+
+    load_stage(0);
+    store_stage(0);
+    __syncthreads();
+    const int kh = lane >> 5, l32 = lane & 31;
+    for (int kt = 0; kt < nk; ++kt) {
+        const int buf = kt & 1;
+        if (kt + 1 < nk) load_stage(kt + 1);
+        const float* as = As[buf];
+        const float* bs = Bs[buf];
+#pragma unroll 4
+        for (int kk = 0; kk < BK / 2; ++kk) {
+            float a[MT], b[NT];
+            for (int i = 0; i < MT; ++i) a[i] = as[(kk * 2 + kh) * LDA + wm * TM + i * 32 + l32];
+            for (int j = 0; j < NT; ++j) b[j] = bs[(kk * 2 + kh) * LDB + wn * TN + j * 32 + l32];
+            for (int i = 0; i < MT; ++i)
+                for (int j = 0; j < NT; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[j], acc[i][j], 0, 0, 0);
+        }
+        if (kt + 1 < nk) {
+            store_stage(buf ^ 1);
+        }
+        __syncthreads();
+    }
+
+    // Epilogue: C/D map col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5).
+    for (int i = 0; i < MT; ++i)
+        for (int j = 0; j < NT; ++j) {
+            const int n = n0 + wn * TN + j * 32 + l32;
+            if (n >= p.N) continue;
+            const float bias = p.bias ? p.bias[n] : 0.0f;
+            for (int r = 0; r < 16; ++r) {
+                const int m = m0 + wm * TM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * kh;
+                if (m >= Mact) continue;
+                float v = acc[i][j][r] + bias;
+                if (RES) v += p.res[(size_t)m * p.ldc + n];
+                p.C[(size_t)m * p.ldc + n] = activate<ACT>(v);
+            }
+        }
+}
+
+// adaptive_avg_pool2d(x, (P, P)) on NHWC: out[b][oy][ox][c]
+__global__ void k_adaptive_pool(const float* in, float* out, int B, int H, int W, int C, int P, const int* m_limit) {
+    const int idx = blockIdx.x;           // b * P*P + oy*P + ox
+    const int b = idx / (P * P);
+    if (m_limit && b >= *m_limit) return;
+    const int o = idx % (P * P);
+    const int oy = o / P, ox = o % P;
+    const int y0 = (oy * H) / P, y1 = ((oy + 1) * H + P - 1) / P;
+    const int x0 = (ox * W) / P, x1 = ((ox + 1) * W + P - 1) / P;
+    const float kh = (float)(y1 - y0), kw = (float)(x1 - x0);
+    for (int c = threadIdx.x; c < C; c += blockDim.x) {
+        float s = 0.0f;
+        for (int y = y0; y < y1; ++y)
+            for (int x = x0; x < x1; ++x) s += in[((size_t)(b * H + y) * W + x) * C + c];
+        out[(size_t)idx * C + c] = s / kh / kw;
+    }
+}
+
+// NCHW planes [B][Cin][H*W] -> NHWC [B][H*W][Cp] (zero-padded channels)
+__global__ void k_pack_input(const float* in, float* out, int B, int Cin, int HW, int Cp) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const size_t total = (size_t)B * HW * Cp;
+    if (i >= total) return;
+    const int c = (int)(i % Cp);
+    const size_t bp = i / Cp;
+    const int px = (int)(bp % HW);
+    const int b = (int)(bp / HW);
+    out[i] = c < Cin ? in[((size_t)b * Cin + c) * HW + px] : 0.0f;
+}
+
+// Gather the staged per-game planes of the leaves that need the network into a
+// dense batch: dst[s] = src[eval_games[s]].
+__global__ void k_gather_planes(const float* src, float* dst, const int* eval_games, const int* n_eval, int per) {
+    const int s = blockIdx.y;
+    if (s >= *n_eval) return;
+    const int g = eval_games[s];
+    const float4* a = reinterpret_cast<const float4*>(src + (size_t)g * per);
+    float4* b = reinterpret_cast<float4*>(dst + (size_t)s * per);
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < per / 4; i += gridDim.x * blockDim.x) b[i] = a[i];
+}
+
+// softmax over A per row (predictBatch semantics; host-facing az_net_predict_batch)
+__global__ void k_softmax_rows(const float* logits, float* out, int A) {
+    const int b = blockIdx.x;
+    __shared__ float e[1024];
+    __shared__ float s_sum, s_max;
+    if (threadIdx.x == 0) {
+        float mx = -3.402823466e38f;
+        for (int a = 0; a < A; ++a) mx = fmaxf(mx, logits[(size_t)b * A + a]);
+        s_max = mx;
+    }
+    __syncthreads();
+    for (int a = threadIdx.x; a < A; a += blockDim.x) e[a] = expf(logits[(size_t)b * A + a] - s_max);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float s = 0.0f;
+        for (int a = 0; a < A; ++a) s += e[a];
+        s_sum = s;
+    }
+    __syncthreads();
+    for (int a = threadIdx.x; a < A; a += blockDim.x) out[(size_t)b * A + a] = s_sum > 0.0f ? e[a] / s_sum : e[a];
+}
+
+// ---------------------------------------------------------------------------
+template <int BN, int ACT, bool RES>
+static void launch_f32(const GemmArgs& p, hipStream_t st) {
+    const int nbm = (p.M + 127) / 128, nbn = (p.N + BN - 1) / BN;
+    hipLaunchKernelGGL((gemm_f32<BN, ACT, RES>), dim3(nbm * nbn), dim3(256), 0, st, p);
+}
+
+void az_launch_gemm_f32(const GemmArgs& p, int act, bool res, hipStream_t st) {
+    const bool small = p.N <= 64;
+    if (small) {
+        if (res) { if (act == ACT_RELU) launch_f32<64, ACT_RELU, true>(p, st); else launch_f32<64, ACT_NONE, true>(p, st); }
+        else if (act == ACT_RELU) launch_f32<64, ACT_RELU, false>(p, st);
+        else if (act == ACT_TANH) launch_f32<64, ACT_TANH, false>(p, st);
+        else launch_f32<64, ACT_NONE, false>(p, st);
+    } else {
+        if (res) { if (act == ACT_RELU) launch_f32<128, ACT_RELU, true>(p, st); else launch_f32<128, ACT_NONE, true>(p, st); }
+        else if (act == ACT_RELU) launch_f32<128, ACT_RELU, false>(p, st);
+        else if (act == ACT_TANH) launch_f32<128, ACT_TANH, false>(p, st);
+        else launch_f32<128, ACT_NONE, false>(p, st);
+    }
+}
+
+void az_launch_pool(const float* in, float* out, int B, int H, int W, int C, int P, const int* m_limit, hipStream_t st) {
+    hipLaunchKernelGGL(k_adaptive_pool, dim3(B * P * P), dim3(C < 256 ? 64 : 256), 0, st, in, out, B, H, W, C, P, m_limit);
+}
+
+void az_launch_pack_input(const float* in, float* out, int B, int Cin, int HW, int Cp, hipStream_t st) {
+    const size_t total = (size_t)B * HW * Cp;
+    hipLaunchKernelGGL(k_pack_input, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, in, out, B, Cin, HW, Cp);
+}
+
+void az_launch_gather_planes(const float* src, float* dst, const int* eval_games, const int* n_eval, int per, int maxB,
+                             hipStream_t st) {
+    hipLaunchKernelGGL(k_gather_planes, dim3(4, maxB), dim3(256), 0, st, src, dst, eval_games, n_eval, per);
+}
+
+void az_launch_softmax_rows(const float* logits, float* out, int B, int A, hipStream_t st) {
+    hipLaunchKernelGGL(k_softmax_rows, dim3(B), dim3(256), 0, st, logits, out, A);
+}

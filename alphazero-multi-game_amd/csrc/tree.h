@@ -1,0 +1,52 @@
+// tree.h -- device-side data layout of the batched search (G independent games).
+//
+// Flat structure-of-arrays node pool per game (two arenas, compacted after every
+// committed move), per-game root state, per-step scratch, a direct-mapped
+// transposition-table emulation per game and a prior ring that keeps the children
+// priors of every TT entry alive for later hits.  See DESIGN.md "Data layout in HBM".
+#pragma once
+#include <stdint.h>
+
+#define AZ_MAXA 361          // largest action space handled on device (19x19)
+#define AZ_DMAX 96           // longest selection path (root + 95 plies); overflow => AZ_ERR_CAPACITY
+#define AZ_NCNT 8            // per-game counters
+
+enum { ST_NONE = 0, ST_TERMINAL = 1, ST_TTHIT = 2, ST_EVAL = 3, ST_EXPANDED = 4 };
+enum { MODE_SIM = 0, MODE_ROOT_NOISE = 1, MODE_ROOT_SEARCH = 2 };
+enum { FL_EXPANDED = 1, FL_TERMINAL = 2 };   // result (GameResult) in bits 2..3
+enum { CNT_EVALS = 0, CNT_LOOKUPS = 1, CNT_HITS = 2, CNT_SIMS = 3, CNT_NODES = 4, CNT_EVALS_TOTAL = 5 };  // [5] survives new games
+enum { ERR_NODES = 1, ERR_PATH = 2, ERR_RING = 4, ERR_BATCH = 8 };
+
+struct Nodes {          // one arena: [G][ncap]
+    int* N; float* W; int* VL; float* P; int* first; int16_t* act; int16_t* cnt; uint8_t* flag;
+};
+
+struct TreeDev {
+    int G, bs, A, ncap;
+    int vl; float cpuct, fpu;
+    int eval_kind;
+    uint64_t tt_mask; int tt_slots;
+    int ring;
+    Nodes nd;                    // current arena
+    int* atop;                   // [G] next free node in the current arena
+    uint8_t* rboard;             // [G][A]   root board, 0 empty 1 black 2 white
+    int* rhist;                  // [G][6]   last moves, [0] most recent, -1 none
+    int* rplayer; int* rstones; int* rply; uint64_t* rhash; int* rfresh; int* rnode;
+    int* active;                 // [G] game searching (not finished)
+    int* gresult;                // [G] GameResult of the root state
+    int* path; int* plen;        // [G][AZ_DMAX], [G]
+    int* lstatus; float* lvalue; uint64_t* lhash; int* ttstore; uint64_t* ttref; int* tthslot;
+    int* need_eval; int* eval_slot; int* eval_games; int* n_eval;
+    float* planes;               // [G][A][16] NHWC, channels 11..15 zero (NET)
+    uint64_t* tt_hash; int* tt_visits; float* tt_value; uint64_t* tt_ref;   // [G][slots]
+    float* ring_buf; uint64_t* ring_cur;                                     // [G][ring], [G]
+    long long* cnt;              // [G][AZ_NCNT]
+    const uint64_t* zpiece;      // [2][A]
+    const uint64_t* zplayer;     // [2]
+    const int* fresh_order;      // [A] first-query legal order of a fresh state
+    uint32_t* mt;                // [G][625] mt19937 state + index (RANDOM evaluator)
+    int* err;                    // [1] sticky error bits
+    const float* net_logits;     // [B][A] (NET) raw policy logits, by eval slot
+    const float* net_value;      // [B]
+    int log_game, log_cap; float* log_pol; float* log_val; float* log_planes; int* log_n;
+};

@@ -1,0 +1,783 @@
+// tree_kernels.hip -- HIP kernels of the batched PUCT search (gfx950).
+//
+// One wavefront (64 lanes) per game.  Every fp32 operation that feeds the tree
+// statistics is written in the reference's evaluation order and this file is
+// compiled with -ffp-contract=off (no FMA contraction) and IEEE division/sqrt, so
+// results are bit-identical to the reference CPU search:
+//   k_select         ParallelMCTS::selectLeafWithPath + selectChildPuct + VL
+//                    (src/mcts/parallel_mcts.cpp:456-563; mcts_node.cpp:61-119,168-196),
+//                    leaf state (GomokuState::make_move, gomoku_state.cpp:681-722),
+//                    terminal test (gomoku_rules.cpp:39-115), Zobrist hash (:620-656),
+//                    TT lookup (transposition_table.cpp:44-84), feature planes (:207-258)
+//   k_scan           deterministic compaction of the leaves that need the network
+//   k_expand_backup  evaluator output -> softmax (torch_neural_network.cpp:296-316),
+//                    TT store (:128-191), expandNodeWithPolicy (parallel_mcts.cpp:681-745),
+//                    backpropagate(node, value, path) (:782-833)
+//   k_select_action  getVisitCountDistribution (mcts_node.cpp:289-322), selectAction
+//                    (parallel_mcts.cpp:987-1047), getRootValue (:1057-1063)
+//   k_apply          makeMove + updateWithMove (parallel_mcts.cpp:1065-1108)
+//   k_compact        subtree reuse: BFS copy of the new root's subtree into the other arena
+//   k_noise          Dirichlet mix of addDirichletNoise (parallel_mcts.cpp:1158-1166)
+#include <hip/hip_runtime.h>
+#include <float.h>
+#include <limits.h>
+#include "tree.h"
+
+namespace {
+
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ULL;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBULL;
+    return x ^ (x >> 31);
+}
+
+__device__ __forceinline__ int wave_sum(int v) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+    return v;
+}
+
+// inclusive prefix sum across the wave
+__device__ __forceinline__ int wave_incl_scan(int v, int lane) {
+    for (int o = 1; o < 64; o <<= 1) {
+        int t = __shfl_up(v, o);
+        if (lane >= o) v += t;
+    }
+    return v;
+}
+
+// GameResult (include/alphazero/core/igamestate.h:26-31)
+enum { R_ONGOING = 0, R_DRAW = 1, R_WIN1 = 2, R_WIN2 = 3 };
+
+// ParallelMCTS::convertToValue (parallel_mcts.cpp:973-985)
+__device__ __forceinline__ float convert_value(int result, int player) {
+    if (result == R_WIN1) return player == 1 ? 1.0f : -1.0f;
+    if (result == R_WIN2) return player == 2 ? 1.0f : -1.0f;
+    return 0.0f;
+}
+
+// count_direction / check_line_for_five (gomoku_rules.cpp:62-115): run through cell a.
+__device__ int five_at(const uint8_t* board, int bs, int a, int p) {
+    int x0 = a / bs, y0 = a % bs;
+    const int D[4][2] = {{0, 1}, {1, 0}, {1, 1}, {1, -1}};
+    for (int d = 0; d < 4; ++d) {
+        int len = -1;
+        for (int s = -1; s <= 1; s += 2) {
+            int x = x0, y = y0;
+            while (x >= 0 && x < bs && y >= 0 && y < bs && board[x * bs + y] == p) {
+                ++len; x += s * D[d][0]; y += s * D[d][1];
+            }
+        }
+        if (p == 1 ? len == 5 : len >= 5) return 1;
+    }
+    return 0;
+}
+
+// getPuctScore (mcts_node.cpp:61-119).  parentDepth: depth of the node being selected
+// FROM (root = 0); the reference negates Q exactly when that node is at depth 1 (:88-93).
+__device__ __forceinline__ float puct_score(int visits, float W, int VL, float P, int parentDepth, int pN, int pVL,
+                                            float pW, float cpuct, float fpu, float sqrtPV) {
+    if (visits == 0) return FLT_MAX;
+    float q = 0.0f;
+    int act = visits - VL;
+    if (act > 0) q = W / (float)act;
+    if (parentDepth == 1) q = -q;
+    if (act <= 0 && fpu > 0.0f) {
+        int pa = pN - pVL;
+        q = pa > 0 ? pW / (float)pa - fpu : -fpu;
+    }
+    float u = cpuct * P * sqrtPV / (1.0f + (float)visits);
+    float div = 0.0f;
+    if (visits < 5) div = 0.05f * (float)(5 - visits);
+    return q + u + div;
+}
+
+// HashEvaluator key (oracle/ref_harness.cpp hash_eval)
+__device__ uint64_t hash_eval_key(uint64_t zhash, const int* hist6) {
+    uint64_t key = splitmix64(zhash ^ 0x5A17C0DEULL);
+    for (int i = 0; i < 6; ++i) key = splitmix64(key + (uint64_t)(uint32_t)(hist6[i] + 2));
+    return key;
+}
+__device__ __forceinline__ float hash_eval_p(uint64_t key, int a) {
+    uint64_t r = splitmix64(key ^ ((uint64_t)(a + 1) * 0x9E3779B97F4A7C15ULL));
+    return (float)(uint32_t)(r >> 40) * (1.0f / 16777216.0f);
+}
+__device__ __forceinline__ float hash_eval_v(uint64_t key) {
+    uint64_t rv = splitmix64(key ^ 0x76A1ULL);
+    return ((float)(int32_t)(uint32_t)(rv >> 40) - 8388608.0f) * (1.0f / 8388608.0f);
+}
+
+// std::mt19937 (libstdc++ _M_gen_rand / operator()) for RandomPolicyNetwork.
+__device__ uint32_t mt_next(uint32_t* st) {
+    uint32_t* x = st;
+    uint32_t& p = st[624];
+    if (p >= 624) {
+        const uint32_t up = 0x80000000u, lo = 0x7fffffffu;
+        for (int k = 0; k < 624 - 397; ++k) {
+            uint32_t y = (x[k] & up) | (x[k + 1] & lo);
+            x[k] = x[k + 397] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+        }
+        for (int k = 624 - 397; k < 623; ++k) {
+            uint32_t y = (x[k] & up) | (x[k + 1] & lo);
+            x[k] = x[k + (397 - 624)] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+        }
+        uint32_t y = (x[623] & up) | (x[0] & lo);
+        x[623] = x[396] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+        p = 0;
+    }
+    uint32_t z = x[p++];
+    z ^= (z >> 11) & 0xffffffffu;
+    z ^= (z << 7) & 0x9d2c5680u;
+    z ^= (z << 15) & 0xefc60000u;
+    z ^= (z >> 18);
+    return z;
+}
+// uniform_real_distribution<float>(a, b) over generate_canonical<float, 24>
+__device__ float mt_uniform(uint32_t* st, float a, float b) {
+    float c = (float)mt_next(st) / 4294967296.0f;
+    if (c >= 1.0f) c = __uint_as_float(0x3F7FFFFFu);   // nextafter(1, 0)
+    return (c * (b - a)) + a;
+}
+
+struct GamePtrs {
+    int* N; float* W; int* VL; float* P; int* first; int16_t* act; int16_t* cnt; uint8_t* flag;
+};
+__device__ __forceinline__ GamePtrs game_nodes(const Nodes& nd, size_t base) {
+    GamePtrs p;
+    p.N = nd.N + base; p.W = nd.W + base; p.VL = nd.VL + base; p.P = nd.P + base;
+    p.first = nd.first + base; p.act = nd.act + base; p.cnt = nd.cnt + base; p.flag = nd.flag + base;
+    return p;
+}
+
+// Leaf state = root state + path moves.  Fills the LDS board, returns side to move,
+// stone count, Zobrist hash and the last six moves (most recent first).
+__device__ void build_leaf(const TreeDev& t, int g, int lane, const GamePtrs& nd, const int* spath, int depth,
+                           uint8_t* board, int* hist6, int& player, int& stones, uint64_t& hash) {
+    const int A = t.A;
+    const uint8_t* rb = t.rboard + (size_t)g * A;
+    for (int a = lane; a < A; a += 64) board[a] = rb[a];
+    __syncthreads();
+    int p = t.rplayer[g];
+    uint64_t h = t.rhash[g];
+    const int p0 = p;
+    if (lane == 0) {
+        for (int i = 1; i <= depth; ++i) {
+            int a = nd.act[spath[i]];
+            board[a] = (uint8_t)p;
+            h ^= t.zpiece[(size_t)(p - 1) * A + a];
+            p = 3 - p;
+        }
+    }
+    __syncthreads();
+    p = __shfl(p, 0);
+    h = __shfl(h, 0);
+    h ^= t.zplayer[p0 - 1] ^ t.zplayer[p - 1];
+    player = p;
+    stones = t.rstones[g] + depth;
+    hash = h;
+    for (int i = 0; i < 6; ++i) {
+        if (i < depth) hist6[i] = nd.act[spath[depth - i]];
+        else hist6[i] = t.rhist[g * 6 + (i - depth)];
+    }
+}
+
+// getEnhancedTensorRepresentation (gomoku_state.cpp:207-258) in NHWC with 16 channels.
+__device__ void write_planes(const TreeDev& t, int g, int lane, const uint8_t* board, const int* hist6, int player) {
+    const int A = t.A, bs = t.bs;
+    // history plane per slot: the reference's get_previous_moves parity rule (:852-869)
+    // puts h0,h2,h4 into the "BLACK" planes 3..5 when BLACK is to move, else 6..8.
+    int hp[6];
+    for (int i = 0; i < 6; ++i) {
+        bool evenSlot = (i % 2) == 0;
+        int base = (player == 1) == evenSlot ? 3 : 6;
+        hp[i] = base + i / 2;
+    }
+    float4* out = reinterpret_cast<float4*>(t.planes + (size_t)g * A * 16);
+    const float inv = 1.0f / 1.0f;
+    (void)inv;
+    for (int a = lane; a < A; a += 64) {
+        float c[16];
+        for (int k = 0; k < 16; ++k) c[k] = 0.0f;
+        int v = board[a];
+        if (v == player) c[0] = 1.0f;
+        else if (v == 3 - player) c[1] = 1.0f;
+        if (player == 1) c[2] = 1.0f;
+        for (int i = 0; i < 6; ++i)
+            if (hist6[i] == a) c[hp[i]] = 1.0f;
+        int x = a / bs, y = a % bs;
+        c[9] = (float)x / (float)(bs - 1);
+        c[10] = (float)y / (float)(bs - 1);
+        for (int k = 0; k < 4; ++k) out[(size_t)a * 4 + k] = make_float4(c[4 * k], c[4 * k + 1], c[4 * k + 2], c[4 * k + 3]);
+    }
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// K1: selection + virtual loss + leaf classification (+ planes for the network).
+__global__ __launch_bounds__(64) void k_select(TreeDev t, int mode) {
+    const int g = blockIdx.x;
+    const int lane = threadIdx.x;
+    __shared__ uint8_t board[AZ_MAXA];
+    __shared__ int spath[AZ_DMAX];
+    if (g >= t.G) return;
+    if (!t.active[g]) {
+        if (lane == 0) { t.lstatus[g] = ST_NONE; t.need_eval[g] = 0; }
+        return;
+    }
+    const size_t base = (size_t)g * t.ncap;
+    GamePtrs nd = game_nodes(t.nd, base);
+    long long* cnt = t.cnt + (size_t)g * AZ_NCNT;
+    const int root = t.rnode[g];
+    int depth = 0;
+    int node = root;
+    int status = ST_NONE;
+    float value = 0.0f;
+
+    if (mode != MODE_SIM) {
+        // Root expansion: expandNode (noise) / search() root branch.
+        uint8_t f = nd.flag[root];
+        if ((f & (FL_EXPANDED | FL_TERMINAL)) || t.gresult[g] != R_ONGOING) {
+            if (lane == 0) { t.lstatus[g] = ST_NONE; t.need_eval[g] = 0; }
+            return;
+        }
+        if (lane == 0) spath[0] = root;
+    } else {
+        // selectLeafWithPath: VL on the root, then PUCT descent.
+        int rN = nd.N[root], rVL = nd.VL[root];
+        float rW = nd.W[root];
+        rN += t.vl; rVL += t.vl; rW = rW - (float)t.vl;           // addVirtualLoss (root, first)
+        if (lane == 0) spath[0] = root;
+        while (true) {
+            uint8_t f = nd.flag[node];
+            if (!(f & FL_EXPANDED) || (f & FL_TERMINAL) || depth >= 1000) break;
+            int pN, pVL; float pW;
+            if (node == root) { pN = rN; pVL = rVL; pW = rW; }
+            else { pN = nd.N[node]; pVL = nd.VL[node]; pW = nd.W[node]; }
+            const int fc = nd.first[node], nc = nd.cnt[node];
+            const float sq = sqrtf((float)pN);
+            float best = -FLT_MAX;
+            int bi = INT_MAX;
+            for (int i = lane; i < nc; i += 64) {
+                const int c = fc + i;
+                float s = puct_score(nd.N[c], nd.W[c], nd.VL[c], nd.P[c], depth, pN, pVL, pW, t.cpuct, t.fpu, sq);
+                if (s > best) { best = s; bi = i; }
+            }
+            for (int o = 32; o > 0; o >>= 1) {
+                float ob = __shfl_xor(best, o);
+                int oi = __shfl_xor(bi, o);
+                if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
+            }
+            if (bi == INT_MAX) break;
+            if (depth + 1 >= AZ_DMAX) { if (lane == 0) atomicOr(t.err, ERR_PATH); break; }
+            node = fc + bi;
+            ++depth;
+            if (lane == 0) spath[depth] = node;
+        }
+        // addVirtualLoss on every path node, root a second time (parallel_mcts.cpp:293-295)
+        if (lane == 0) {
+            rN += t.vl; rVL += t.vl; rW = rW - (float)t.vl;
+            nd.N[root] = rN; nd.VL[root] = rVL; nd.W[root] = rW;
+        }
+        __syncthreads();
+        for (int i = 1 + lane; i <= depth; i += 64) {
+            const int n = spath[i];
+            nd.N[n] += t.vl; nd.VL[n] += t.vl; nd.W[n] = nd.W[n] - (float)t.vl;
+        }
+    }
+    __syncthreads();
+
+    int hist6[6];
+    int player, stones;
+    uint64_t hash;
+    build_leaf(t, g, lane, nd, spath, depth, board, hist6, player, stones, hash);
+    const int leaf = node;
+    int store = 0;
+    uint64_t ref = 0;
+    int hslot = 0;
+
+    if (mode == MODE_SIM) {
+        uint8_t f = nd.flag[leaf];
+        int result = R_ONGOING;
+        if (f & FL_TERMINAL) {
+            status = ST_TERMINAL;
+            value = convert_value((f >> 2) & 3, player);
+        } else {
+            if (depth > 0) {
+                const int a = nd.act[leaf];
+                if (five_at(board, t.bs, a, 3 - player)) result = (3 - player) == 1 ? R_WIN1 : R_WIN2;
+                else if (stones >= t.A) result = R_DRAW;
+            } else {
+                result = t.gresult[g];
+            }
+            if (result != R_ONGOING) {
+                status = ST_TERMINAL;
+                value = convert_value(result, player);
+                if (lane == 0) nd.flag[leaf] = (uint8_t)(f | FL_TERMINAL | (result << 2));
+            } else if (f & FL_EXPANDED) {
+                status = ST_EXPANDED;   // depth cap only (reference: node->getValue())
+            }
+        }
+    } else if (stones >= t.A) {
+        // expandNode: no legal moves -> terminal (parallel_mcts.cpp:646-654)
+        if (lane == 0) {
+            nd.flag[leaf] = (uint8_t)(nd.flag[leaf] | FL_TERMINAL | FL_EXPANDED | (R_DRAW << 2));
+            t.lstatus[g] = ST_NONE; t.need_eval[g] = 0;
+        }
+        return;
+    }
+
+    if (status == ST_NONE) {
+        // Transposition table (direct-mapped emulation, transposition_table.cpp:44-191)
+        const size_t tb = (size_t)g * t.tt_slots;
+        hslot = (int)(hash & t.tt_mask);
+        const int vis = t.tt_visits[tb + hslot];
+        const bool hit = vis > 0 && t.tt_hash[tb + hslot] == hash;
+        if (hit) {
+            status = ST_TTHIT;
+            value = t.tt_value[tb + hslot];
+            ref = t.tt_ref[tb + hslot];
+            if (lane == 0) {
+                t.tt_visits[tb + hslot] = vis + (mode == MODE_ROOT_SEARCH ? 2 : 1);
+                cnt[CNT_LOOKUPS] += 1;
+                cnt[CNT_HITS] += 1;
+            }
+        } else {
+            status = ST_EVAL;
+            store = (vis == 0 || vis < 5) ? 1 : 0;     // empty slot, or shouldReplace (visits < 5)
+            if (lane == 0) cnt[CNT_LOOKUPS] += (mode == MODE_ROOT_SEARCH ? 1 : 2);
+            write_planes(t, g, lane, board, hist6, player);
+        }
+    }
+    if (lane == 0) {
+        t.lstatus[g] = status;
+        t.lvalue[g] = value;
+        t.lhash[g] = hash;
+        t.ttstore[g] = store;
+        t.ttref[g] = ref;
+        t.tthslot[g] = hslot;
+        t.plen[g] = depth + 1;
+        t.need_eval[g] = (status == ST_EVAL && t.eval_kind == 0) ? 1 : 0;
+    }
+    for (int i = lane; i <= depth; i += 64) t.path[(size_t)g * AZ_DMAX + i] = spath[i];
+}
+
+// K2: deterministic compaction of the leaves that need the network (one block).
+__global__ __launch_bounds__(1024) void k_scan(TreeDev t) {
+    __shared__ int part[1024];
+    const int tid = threadIdx.x;
+    const int per = (t.G + 1023) / 1024;
+    const int b0 = tid * per;
+    int s = 0;
+    for (int i = 0; i < per; ++i) { int g = b0 + i; if (g < t.G) s += t.need_eval[g]; }
+    part[tid] = s;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {
+        int v = tid >= o ? part[tid - o] : 0;
+        __syncthreads();
+        part[tid] += v;
+        __syncthreads();
+    }
+    int off = part[tid] - s;
+    for (int i = 0; i < per; ++i) {
+        int g = b0 + i;
+        if (g < t.G) {
+            if (t.need_eval[g]) { t.eval_slot[g] = off; t.eval_games[off] = g; ++off; }
+            else t.eval_slot[g] = -1;
+        }
+    }
+    if (tid == 1023) *t.n_eval = part[1023];
+}
+
+// K3: evaluator output -> TT store -> expansion -> backup.
+__global__ __launch_bounds__(64) void k_expand_backup(TreeDev t, int mode) {
+    const int g = blockIdx.x;
+    const int lane = threadIdx.x;
+    __shared__ uint8_t board[AZ_MAXA];
+    __shared__ int spath[AZ_DMAX];
+    __shared__ float pol[AZ_MAXA];
+    __shared__ int legal[AZ_MAXA];
+    __shared__ float lp[AZ_MAXA];
+    __shared__ float s_scalar[2];
+    if (g >= t.G) return;
+    const int status = t.lstatus[g];
+    if (status == ST_NONE) return;
+    const size_t base = (size_t)g * t.ncap;
+    GamePtrs nd = game_nodes(t.nd, base);
+    long long* cnt = t.cnt + (size_t)g * AZ_NCNT;
+    const int A = t.A;
+    const int plen = t.plen[g];
+    const int depth = plen - 1;
+    for (int i = lane; i < plen; i += 64) spath[i] = t.path[(size_t)g * AZ_DMAX + i];
+    __syncthreads();
+    const int leaf = spath[depth];
+    int hist6[6]; int player, stones; uint64_t hash;
+    build_leaf(t, g, lane, nd, spath, depth, board, hist6, player, stones, hash);
+    float value = t.lvalue[g];
+
+    if (status == ST_EVAL || status == ST_TTHIT) {
+        // legal moves in child order (gomoku_state.cpp:531-578)
+        int n = 0;
+        const bool fresh = (depth == 0) && t.rfresh[g];
+        if (fresh) {
+            for (int i = lane; i < A; i += 64) legal[i] = t.fresh_order[i];
+            n = A - t.rstones[g];   // fresh root is the empty board
+        } else {
+            for (int c0 = 0; c0 < A; c0 += 64) {
+                const int a = A - 1 - (c0 + lane);
+                const bool e = a >= 0 && board[a] == 0;
+                const unsigned long long m = __ballot(e);
+                const int pos = n + __popcll(m & ((1ULL << lane) - 1ULL));
+                if (e) legal[pos] = a;
+                n += __popcll(m);
+            }
+        }
+        __syncthreads();
+        if (status == ST_EVAL) {
+            if (lane == 0) { cnt[CNT_EVALS] += 1; cnt[CNT_EVALS_TOTAL] += 1; }
+            if (t.eval_kind == 0) {
+                const int slot = t.eval_slot[g];
+                const float* lg = t.net_logits + (size_t)slot * A;
+                float mx = -FLT_MAX;
+                for (int a = lane; a < A; a += 64) { float v = lg[a]; pol[a] = v; mx = fmaxf(mx, v); }
+                mx = wave_max(mx);
+                __syncthreads();
+                for (int a = lane; a < A; a += 64) pol[a] = expf(pol[a] - mx);
+                __syncthreads();
+                if (lane == 0) {
+                    float sum = 0.0f;
+                    for (int a = 0; a < A; ++a) sum += pol[a];
+                    s_scalar[0] = sum;
+                }
+                __syncthreads();
+                const float sum = s_scalar[0];
+                if (sum > 0.0f) for (int a = lane; a < A; a += 64) pol[a] = pol[a] / sum;
+                value = t.net_value[slot];
+            } else if (t.eval_kind == 1) {
+                const uint64_t key = hash_eval_key(hash, hist6);
+                for (int a = lane; a < A; a += 64) pol[a] = hash_eval_p(key, a);
+                value = hash_eval_v(key);
+            } else {
+                uint32_t* st = t.mt + (size_t)g * 625;
+                for (int a = lane; a < A; a += 64) pol[a] = 0.001f;
+                __syncthreads();
+                if (lane == 0) {
+                    float sum = 0.0f;
+                    for (int i = 0; i < n; ++i) { float u = mt_uniform(st, 0.0f, 1.0f); pol[legal[i]] = u; sum += u; }
+                    s_scalar[0] = sum;
+                    s_scalar[1] = mt_uniform(st, -0.1f, 0.1f);
+                }
+                __syncthreads();
+                const float sum = s_scalar[0];
+                if (sum > 0.0f) for (int a = lane; a < A; a += 64) pol[a] = pol[a] / sum;
+                value = s_scalar[1];
+            }
+            __syncthreads();
+            if (g == t.log_game && t.log_pol) {
+                const int k = *t.log_n;
+                if (k < t.log_cap) {
+                    for (int a = lane; a < A; a += 64) t.log_pol[(size_t)k * A + a] = pol[a];
+                    if (t.log_planes) {
+                        const float* src = t.planes + (size_t)g * A * 16;
+                        for (int a = lane; a < A; a += 64)
+                            for (int c = 0; c < 11; ++c) t.log_planes[((size_t)k * 11 + c) * A + a] = src[(size_t)a * 16 + c];
+                    }
+                    if (lane == 0) { t.log_val[k] = value; *t.log_n = k + 1; }
+                }
+            }
+            // expandNodeWithPolicy: gather, sequential sum, renormalise (parallel_mcts.cpp:702-724)
+            for (int i = lane; i < n; i += 64) lp[i] = pol[legal[i]];
+            __syncthreads();
+            if (lane == 0) {
+                float sum = 0.0f;
+                for (int i = 0; i < n; ++i) sum += lp[i];
+                s_scalar[0] = sum;
+            }
+            __syncthreads();
+            const float ps = s_scalar[0];
+            if (ps > 0.0f) for (int i = lane; i < n; i += 64) lp[i] = lp[i] / ps;
+            else { const float u = 1.0f / (float)n; for (int i = lane; i < n; i += 64) lp[i] = u; }
+        } else {
+            // transposition hit: the stored priors are exactly the renormalised gather of
+            // the cached policy over the same legal set (same position => same order).
+            const uint64_t cur = t.ring_cur[g];
+            if (cur - t.ttref[g] > (uint64_t)t.ring) { if (lane == 0) atomicOr(t.err, ERR_RING); return; }
+            const float* rb = t.ring_buf + (size_t)g * t.ring;
+            for (int i = lane; i < n; i += 64) lp[i] = rb[(t.ttref[g] + i) % (uint64_t)t.ring];
+        }
+        __syncthreads();
+        // TT store (new entry) + prior ring
+        if (status == ST_EVAL && t.ttstore[g]) {
+            const uint64_t cur = t.ring_cur[g];
+            float* rb = t.ring_buf + (size_t)g * t.ring;
+            for (int i = lane; i < n; i += 64) rb[(cur + i) % (uint64_t)t.ring] = lp[i];
+            if (lane == 0) {
+                const size_t tb = (size_t)g * t.tt_slots + t.tthslot[g];
+                t.tt_hash[tb] = hash; t.tt_visits[tb] = 1; t.tt_value[tb] = value; t.tt_ref[tb] = cur;
+                t.ring_cur[g] = cur + (uint64_t)n;
+            }
+        }
+        // create children (include/alphazero/mcts/mcts_node.h: N=W=VL=0, prior, action)
+        int first = 0;
+        if (lane == 0) {
+            first = t.atop[g];
+            if (first + n > t.ncap) { atomicOr(t.err, ERR_NODES); first = -1; }
+            else t.atop[g] = first + n;
+        }
+        first = __shfl(first, 0);
+        if (first < 0) return;
+        for (int i = lane; i < n; i += 64) {
+            const int c = first + i;
+            nd.N[c] = 0; nd.W[c] = 0.0f; nd.VL[c] = 0; nd.P[c] = lp[i];
+            nd.first[c] = -1; nd.act[c] = (int16_t)legal[i]; nd.cnt[c] = 0; nd.flag[c] = 0;
+        }
+        if (lane == 0) {
+            nd.first[leaf] = first; nd.cnt[leaf] = (int16_t)n; nd.flag[leaf] = (uint8_t)(nd.flag[leaf] | FL_EXPANDED);
+            cnt[CNT_NODES] = first + n;
+        }
+    } else if (status == ST_EXPANDED) {
+        value = nd.N[leaf] == 0 ? 0.0f : nd.W[leaf] / (float)nd.N[leaf];
+    }
+
+    if (mode == MODE_SIM && lane == 0) {
+        // backpropagate(node, value, searchPath) (parallel_mcts.cpp:782-833)
+        float v = value;
+        for (int i = depth; i >= 0; --i) {
+            const int nn = spath[i];
+            int N = nd.N[nn], VL = nd.VL[nn];
+            float W = nd.W[nn];
+            N -= t.vl; VL -= t.vl; W = W + (float)t.vl;   // removeVirtualLoss
+            N += 1;
+            W = W + v;
+            v = -v;
+            nd.N[nn] = N; nd.VL[nn] = VL; nd.W[nn] = W;
+        }
+        cnt[CNT_SIMS] += 1;
+    }
+}
+
+// K4: visit distribution, action choice and root value per game.
+__global__ __launch_bounds__(64) void k_select_action(TreeDev t, int training, float temperature, int* actions,
+                                                      float* values, float* probs, int* child_actions, int* nchild) {
+    const int g = blockIdx.x;
+    const int lane = threadIdx.x;
+    __shared__ float c[AZ_MAXA];
+    if (g >= t.G) return;
+    const int A = t.A;
+    if (!t.active[g]) {
+        if (lane == 0) { actions[g] = -1; values[g] = 0.0f; nchild[g] = 0; }
+        return;
+    }
+    GamePtrs nd = game_nodes(t.nd, (size_t)g * t.ncap);
+    const int root = t.rnode[g];
+    const int fc = nd.first[root], nc = nd.cnt[root];
+    const uint8_t f = nd.flag[root];
+    if ((f & FL_TERMINAL) || nc == 0) {
+        if (lane == 0) {
+            // first legal move of the root state (parallel_mcts.cpp:994-1004)
+            int a = -1;
+            const uint8_t* rb = t.rboard + (size_t)g * A;
+            if (t.rfresh[g]) a = t.fresh_order[0];
+            else for (int x = A - 1; x >= 0; --x) if (rb[x] == 0) { a = x; break; }
+            actions[g] = a; values[g] = 0.0f; nchild[g] = 0;
+        }
+        return;
+    }
+    const float ex = 1.0f / fmaxf(0.01f, temperature);
+    for (int i = lane; i < nc; i += 64) {
+        const float Nf = (float)nd.N[fc + i];
+        float v;
+        if (ex == 1.0f) v = Nf;                                // pow(x, 1) == x exactly
+        else v = (float)pow((double)Nf, (double)ex);
+        c[i] = v;
+        child_actions[(size_t)g * A + i] = nd.act[fc + i];
+    }
+    __syncthreads();
+    if (lane == 0) {
+        float total = 0.0f;
+        for (int i = 0; i < nc; ++i) total += c[i];
+        float* pr = probs + (size_t)g * A;
+        if (total > 0.0f) for (int i = 0; i < nc; ++i) pr[i] = c[i] / total;
+        else { const float u = 1.0f / (float)nc; for (int i = 0; i < nc; ++i) pr[i] = u; }
+        int bi = 0;
+        if (training && temperature > 0.0f) {
+            for (int i = 1; i < nc; ++i) if (pr[bi] < pr[i]) bi = i;      // std::max_element
+        } else {
+            int mx = 0;
+            for (int i = 0; i < nc; ++i) mx = max(mx, nd.N[fc + i]);
+            for (int i = 0; i < nc; ++i) if (nd.N[fc + i] == mx) { bi = i; break; }
+        }
+        actions[g] = nd.act[fc + bi];
+        const int rN = nd.N[root];
+        values[g] = rN == 0 ? 0.0f : nd.W[root] / (float)rN;
+        nchild[g] = nc;
+    }
+}
+
+// K5: makeMove + updateWithMove; terminal test of the new root (game loop condition).
+__global__ __launch_bounds__(64) void k_apply(TreeDev t, const int* actions, int* terminal, int* result) {
+    const int g = blockIdx.x;
+    const int lane = threadIdx.x;
+    __shared__ uint8_t board[AZ_MAXA];
+    if (g >= t.G) return;
+    const int a = actions[g];
+    const int A = t.A;
+    if (!t.active[g] || a < 0 || a >= A) {
+        if (lane == 0) { terminal[g] = t.active[g] ? 0 : 1; result[g] = t.gresult[g]; }
+        return;
+    }
+    GamePtrs nd = game_nodes(t.nd, (size_t)g * t.ncap);
+    uint8_t* rb = t.rboard + (size_t)g * A;
+    const int p = t.rplayer[g];
+    for (int i = lane; i < A; i += 64) board[i] = rb[i];
+    __syncthreads();
+    if (lane == 0) {
+        board[a] = (uint8_t)p;
+        rb[a] = (uint8_t)p;
+        const int np = 3 - p;
+        t.rhash[g] = t.rhash[g] ^ t.zpiece[(size_t)(p - 1) * A + a] ^ t.zplayer[p - 1] ^ t.zplayer[np - 1];
+        int* h = t.rhist + g * 6;
+        for (int i = 5; i > 0; --i) h[i] = h[i - 1];
+        h[0] = a;
+        t.rplayer[g] = np;
+        const int stones = t.rstones[g] + 1;
+        t.rstones[g] = stones;
+        t.rply[g] += 1;
+        t.rfresh[g] = 0;
+        int res = R_ONGOING;
+        if (five_at(board, t.bs, a, p)) res = p == 1 ? R_WIN1 : R_WIN2;
+        else if (stones >= A) res = R_DRAW;
+        t.gresult[g] = res;
+        if (res != R_ONGOING) t.active[g] = 0;
+        terminal[g] = res != R_ONGOING;
+        result[g] = res;
+        // subtree reuse
+        const int root = t.rnode[g];
+        const int fc = nd.first[root], nc = nd.cnt[root];
+        int child = -1;
+        for (int i = 0; i < nc; ++i) if (nd.act[fc + i] == a) { child = fc + i; break; }
+        if (child < 0) {
+            child = t.atop[g];
+            if (child + 1 > t.ncap) { atomicOr(t.err, ERR_NODES); child = 0; }
+            else t.atop[g] = child + 1;
+            nd.N[child] = 0; nd.W[child] = 0.0f; nd.VL[child] = 0; nd.P[child] = 0.0f;
+            nd.first[child] = -1; nd.act[child] = -1; nd.cnt[child] = 0; nd.flag[child] = 0;
+        }
+        t.rnode[g] = child;
+    }
+}
+
+// K6: copy the subtree of the (new) root into the other arena, breadth first.
+__global__ __launch_bounds__(64) void k_compact(TreeDev t, Nodes dst, int* src_of) {
+    const int g = blockIdx.x;
+    const int lane = threadIdx.x;
+    if (g >= t.G) return;
+    const size_t base = (size_t)g * t.ncap;
+    GamePtrs s = game_nodes(t.nd, base);
+    GamePtrs d = game_nodes(dst, base);
+    int* so = src_of + base;
+    const int root = t.rnode[g];
+    if (lane == 0) {
+        d.N[0] = s.N[root]; d.W[0] = s.W[root]; d.VL[0] = s.VL[root]; d.P[0] = s.P[root];
+        d.act[0] = s.act[root]; d.cnt[0] = s.cnt[root]; d.flag[0] = s.flag[root]; d.first[0] = -1;
+        so[0] = root;
+    }
+    __syncthreads();
+    int j = 0, top = 1;
+    while (j < top) {
+        const int k = j + lane;
+        const bool valid = k < top;
+        const int sn = valid ? so[k] : 0;
+        const int nc = valid ? (int)s.cnt[sn] : 0;
+        const int incl = wave_incl_scan(nc, lane);
+        const int tot = __shfl(incl, 63);
+        const int nf = top + incl - nc;
+        if (valid) d.first[k] = nc ? nf : -1;
+        const int fsrc = valid && nc ? s.first[sn] : 0;
+        const int m = min(64, top - j);
+        for (int e = 0; e < m; ++e) {
+            const int ce = __shfl(nc, e);
+            if (ce == 0) continue;
+            const int fs = __shfl(fsrc, e);
+            const int fd = __shfl(nf, e);
+            if (fd + ce > t.ncap) { if (lane == 0) atomicOr(t.err, ERR_NODES); return; }
+            for (int i = lane; i < ce; i += 64) {
+                const int a = fs + i, b = fd + i;
+                d.N[b] = s.N[a]; d.W[b] = s.W[a]; d.VL[b] = s.VL[a]; d.P[b] = s.P[a];
+                d.act[b] = s.act[a]; d.cnt[b] = s.cnt[a]; d.flag[b] = s.flag[a]; d.first[b] = -1;
+                so[b] = a;
+            }
+        }
+        __syncthreads();
+        j += m;
+        top += tot;
+    }
+    if (lane == 0) { t.rnode[g] = 0; t.atop[g] = top; }
+}
+
+// K7: Dirichlet mix on the root children (noise already normalised on the host).
+__global__ __launch_bounds__(64) void k_noise(TreeDev t, const float* noise, const uint8_t* mask, float eps) {
+    const int g = blockIdx.x;
+    const int lane = threadIdx.x;
+    if (g >= t.G || !mask[g]) return;
+    GamePtrs nd = game_nodes(t.nd, (size_t)g * t.ncap);
+    const int root = t.rnode[g];
+    const int fc = nd.first[root], nc = nd.cnt[root];
+    const float* nz = noise + (size_t)g * t.A;
+    for (int i = lane; i < nc; i += 64) {
+        const float old = nd.P[fc + i];
+        nd.P[fc + i] = (1.0f - eps) * old + eps * nz[i];
+    }
+}
+
+// K8: fresh games (empty board, new tree; TT visits cleared by the caller).
+__global__ __launch_bounds__(64) void k_new_games(TreeDev t, const int* games, int n, uint32_t eval_seed) {
+    const int idx = blockIdx.x;
+    const int lane = threadIdx.x;
+    if (idx >= n) return;
+    const int g = games[idx];
+    uint8_t* rb = t.rboard + (size_t)g * t.A;
+    for (int i = lane; i < t.A; i += 64) rb[i] = 0;
+    GamePtrs nd = game_nodes(t.nd, (size_t)g * t.ncap);
+    long long* cnt = t.cnt + (size_t)g * AZ_NCNT;
+    if (lane < CNT_EVALS_TOTAL) cnt[lane] = 0;
+    if (lane < 6) t.rhist[g * 6 + lane] = -1;
+    if (lane == 0) {
+        t.rplayer[g] = 1; t.rstones[g] = 0; t.rply[g] = 0; t.rhash[g] = t.zplayer[0]; t.rfresh[g] = 1;
+        t.rnode[g] = 0; t.atop[g] = 1; t.active[g] = 1; t.gresult[g] = R_ONGOING; t.ring_cur[g] = 0;
+        nd.N[0] = 0; nd.W[0] = 0.0f; nd.VL[0] = 0; nd.P[0] = 0.0f; nd.first[0] = -1; nd.act[0] = -1;
+        nd.cnt[0] = 0; nd.flag[0] = 0;
+        if (t.mt) {
+            // std::mt19937(seed + g) seeding (libstdc++ mersenne_twister_engine::seed)
+            uint32_t* st = t.mt + (size_t)g * 625;
+            st[0] = eval_seed + (uint32_t)g;
+            for (int i = 1; i < 624; ++i) st[i] = 1812433253u * (st[i - 1] ^ (st[i - 1] >> 30)) + (uint32_t)i;
+            st[624] = 624;
+        }
+    }
+}
+
+// TT clear for the listed games (visits == 0 marks an empty slot).
+__global__ void k_tt_clear(TreeDev t, const int* games, int n) {
+    const int idx = blockIdx.y;
+    if (idx >= n) return;
+    int* v = t.tt_visits + (size_t)games[idx] * t.tt_slots;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < t.tt_slots; i += gridDim.x * blockDim.x) v[i] = 0;
+}
+
+// Root children readback helper (tests / records).
+__global__ void k_root_children(TreeDev t, int g, int* act, int* N, int* VL, float* W, float* P, int* n, int* rootinfo,
+                                float* rootW) {
+    GamePtrs nd = game_nodes(t.nd, (size_t)g * t.ncap);
+    const int root = t.rnode[g];
+    const int fc = nd.first[root], nc = nd.cnt[root];
+    for (int i = threadIdx.x; i < nc; i += blockDim.x) {
+        act[i] = nd.act[fc + i]; N[i] = nd.N[fc + i]; VL[i] = nd.VL[fc + i]; W[i] = nd.W[fc + i]; P[i] = nd.P[fc + i];
+    }
+    if (threadIdx.x == 0) { *n = nc; rootinfo[0] = nd.N[root]; rootinfo[1] = nd.VL[root]; *rootW = nd.W[root]; }
+}

@@ -1,0 +1,166 @@
+/*
+ * az_engine.h -- C-ABI of the MI355X-native self-play engine (libaz_hip.so).
+ *
+ * This is the drop-in boundary for the reference's self-play hot path
+ * (src/selfplay + src/mcts + src/nn of cosmosapjw-quantum/alphazero-multi-game).
+ * Plain pointers and sizes only; no exceptions cross it.  Every entry point
+ * returns 0 on success and a negative az_status otherwise; az_last_error()
+ * gives a thread-local message.  The caller owns every host buffer (the engine
+ * copies in and out); the engine owns all device memory.  Calls on one handle
+ * are serialised internally, so the reference's multi-threaded callers stay legal.
+ *
+ * Reference interfaces replaced (paths relative to the reference root):
+ *   az_net_*      alphazero::nn::NeuralNetwork plugin
+ *                 (include/alphazero/nn/neural_network.h:20-132),
+ *                 TorchNeuralNetwork::predictBatch (src/nn/torch_neural_network.cpp:224-363)
+ *   az_search_*   alphazero::mcts::ParallelMCTS, one tree per game, G games per handle
+ *                 (include/alphazero/mcts/parallel_mcts.h:131-201)
+ *   az_selfplay_* alphazero::selfplay::SelfPlayManager::generateGames / playSingleGame
+ *                 (src/selfplay/self_play_manager.cpp:47-234)
+ */
+#ifndef AZ_ENGINE_H
+#define AZ_ENGINE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum az_status {
+    AZ_OK = 0,
+    AZ_ERR_ARG = -1,       /* invalid argument / shape */
+    AZ_ERR_HIP = -2,       /* HIP runtime error (device missing, launch failure) */
+    AZ_ERR_OOM = -3,       /* device allocation failed */
+    AZ_ERR_CAPACITY = -4,  /* node pool / prior ring / batch capacity exceeded */
+    AZ_ERR_STATE = -5      /* call not valid in the current state */
+};
+
+typedef struct az_engine az_engine;
+typedef struct az_net az_net;
+typedef struct az_search az_search;
+
+/* ---------------------------------------------------------------- engine */
+const char* az_last_error(void);
+int az_engine_create(int device, az_engine** out);   /* hipSetDevice(device); fails loudly without a GPU */
+void az_engine_destroy(az_engine* e);
+int az_engine_device_name(az_engine* e, char* buf, int len);
+
+/* ------------------------------------------------------- NeuralNetwork */
+/* Residual policy/value ConvNet of SURVEY.md CS5 / §8(a) a27:
+ *   input 3x3 conv C_in->F (+BN, ReLU); `blocks` x {3x3 conv, BN, ReLU, 3x3 conv, BN,
+ *   (+skip if residual), ReLU}; adaptive avg-pool to pool x pool; policy head
+ *   1x1 conv F->head_ch + BN + ReLU + FC -> A logits; value head 1x1 conv F->head_ch +
+ *   BN + ReLU + FC -> fc_hidden + ReLU + FC -> 1 + tanh.
+ *   residual=1,conv_bias=1 : SimplifiedModel (python/simple_export.py:12-66)
+ *   residual=0,conv_bias=0 : exporter fallback (python/scripts/simple_export.py:40-96)  */
+enum az_precision {
+    AZ_PREC_F32 = 0,    /* fp32 operands, f32-input MFMA (exact f32 products)              */
+    AZ_PREC_BF16X3 = 1, /* fp32 split into bf16 hi+lo, 3 bf16 MFMAs per product (~2^-16)   */
+    AZ_PREC_BF16 = 2    /* plain bf16 operands, fp32 accumulate (throughput only)          */
+};
+typedef struct az_net_desc {
+    int board_size;     /* H = W */
+    int in_planes;      /* 11 for Gomoku (gomoku_state.cpp:207-258) */
+    int channels;       /* F */
+    int blocks;
+    int action_size;    /* A */
+    int head_channels;  /* 32 */
+    int pool;           /* 8: adaptive_avg_pool2d target */
+    int fc_hidden;      /* 256 */
+    int residual;       /* 1: relu(x + block(x)) */
+    int conv_bias;      /* 1: convolutions carry a bias */
+    int precision;      /* az_precision for the 3x3 trunk */
+    int max_batch;      /* largest B passed to az_net_* (device buffers sized for it) */
+} az_net_desc;
+
+int az_net_create(az_engine* e, const az_net_desc* desc, az_net** out);
+void az_net_destroy(az_net* n);
+/* Number of floats of the canonical parameter blob (torch state_dict order, BN in
+ * eval form: weight, bias, running_mean, running_var per BN). */
+int az_net_num_params(az_net* n, size_t* count);
+int az_net_load_weights(az_net* n, const float* blob, size_t count);
+/* Counter-based deterministic init (SplitMix64), identical to tests' generator. */
+int az_net_init_random(az_net* n, uint64_t seed);
+int az_net_set_precision(az_net* n, int precision);
+/* planes: host fp32 NCHW [B][in_planes][H][W].  logits [B][A] raw, value [B] (tanh). */
+int az_net_forward(az_net* n, const float* planes, int B, float* logits, float* value);
+/* predictBatch semantics: policy = softmax over A (max-subtracted, sequential fp32 sum,
+ * torch_neural_network.cpp:296-316), value [B]. */
+int az_net_predict_batch(az_net* n, const float* planes, int B, float* policy, float* value);
+
+/* ---------------------------------------------------------------- search */
+enum az_eval_kind {
+    AZ_EVAL_NET = 0,    /* the ConvNet above (az_search_create's `net`) */
+    AZ_EVAL_HASH = 1,   /* HashEvaluator (oracle/ref_harness.cpp hash_eval), tests */
+    AZ_EVAL_RANDOM = 2  /* RandomPolicyNetwork(seed + game) semantics (random_policy_network.cpp) */
+};
+typedef struct az_search_cfg {
+    int n_games;          /* G: independent games (trees) on this device */
+    int board_size;       /* Gomoku bs (standard rules: no Renju/Omok/pro-long) */
+    int num_simulations;  /* MCTSConfig::numSimulations */
+    float c_puct;         /* 1.5 */
+    float fpu_reduction;  /* 0.0 */
+    int virtual_loss;     /* 3 */
+    int eval_kind;        /* az_eval_kind */
+    uint32_t eval_seed;   /* RandomPolicyNetwork seed (game g uses eval_seed + g) */
+    uint32_t zobrist_seed;/* ZobristHash seed (reference patch P2 uses 12345) */
+    uint32_t noise_seed;  /* ParallelMCTS rng_ seed; setDeterministicMode => 42 */
+    int noise_seed_stride;/* game g uses noise_seed + g*stride (0: every game seeded 42) */
+    int use_dirichlet_each_search; /* MCTSConfig::useDirichletNoise */
+    float dirichlet_alpha;/* 0.03 */
+    float dirichlet_eps;  /* 0.25 */
+    int tt_log2;          /* TranspositionTable slots = 2^tt_log2 per game (reference: 20) */
+    int node_capacity;    /* per-game node pool (0: auto = sims*A + 4*A) */
+    int prior_ring;       /* per-game prior ring floats for TT hits (0: auto) */
+} az_search_cfg;
+
+int az_search_create(az_engine* e, az_net* net, const az_search_cfg* cfg, az_search** out);
+void az_search_destroy(az_search* s);
+/* Start fresh games (empty board, new tree and TT) for the listed game slots. */
+int az_search_new_games(az_search* s, const int* games, int n);
+/* ParallelMCTS::addDirichletNoise(alpha, eps) for every non-terminal game; expands
+ * roots first (expandNode semantics).  Gamma draws: host libstdc++ per game. */
+int az_search_add_noise(az_search* s, float alpha, float eps);
+/* Like az_search_add_noise but only for games with mask[g] != 0. */
+int az_search_add_noise_masked(az_search* s, float alpha, float eps, const uint8_t* mask);
+/* ParallelMCTS::search() for every active (non-terminal) game. */
+int az_search_run(az_search* s);
+/* getActionProbabilities(T) + selectAction(isTraining, T) + getRootValue() for every
+ * game.  probs: [G][A] in CHILD order (n_children[g] valid entries), children_actions
+ * [G][A]; actions[g] = -1 for finished games. */
+int az_search_select(az_search* s, int training, float temperature, int* actions, float* root_values,
+                     float* probs, int* children_actions, int* n_children);
+/* state.makeMove(a) + updateWithMove(a) for every game with actions[g] >= 0;
+ * terminal[g] / result[g] (GameResult: 0 ongoing, 1 draw, 2 P1 win, 3 P2 win). */
+int az_search_apply(az_search* s, const int* actions, int* terminal, int* result);
+/* Root children statistics of one game, child order (raw N, VL, W, P). */
+int az_search_root_children(az_search* s, int game, int* actions, int* N, int* VL, float* W, float* P,
+                            int* n_children);
+/* Root node's own N, VL, W. */
+int az_search_root_node(az_search* s, int game, int* N, int* VL, float* W);
+/* Counters per game: [0] evals, [1] tt_lookups, [2] tt_hits, [3] simulations, [4] nodes used. */
+int az_search_counters(az_search* s, int game, int64_t* out5);
+/* Evaluation log (tests): every evaluation of game `game` appends (policy[A] post-softmax,
+ * value) in evaluation order; planes too when planes != 0.  Capacity in evaluations. */
+int az_search_enable_eval_log(az_search* s, int game, int capacity);
+int az_search_read_eval_log(az_search* s, float* policy, float* value, float* planes, int* count);
+
+/* ------------------------------------------------------------- self-play */
+/* One SelfPlayManager::playSingleGame move for every active game: search, temperature
+ * schedule (T = ply < temp_drop ? t_init : t_final), selectAction(true, T), record,
+ * makeMove/updateWithMove, noise after even plies.  Finished games restart when
+ * restart != 0.  moves_done/evals_done accumulate the positions and NN evaluations. */
+typedef struct az_selfplay_cfg {
+    int temp_drop_move;   /* 30 */
+    float t_init;         /* 1.0 */
+    float t_final;        /* 0.0 */
+    int restart_finished; /* throughput mode: start a new game in a finished slot */
+} az_selfplay_cfg;
+int az_selfplay_step(az_search* s, const az_selfplay_cfg* cfg, int64_t* moves_done, int64_t* evals_done);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* AZ_ENGINE_H */

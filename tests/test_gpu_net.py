@@ -1,0 +1,120 @@
+"""GPU parity of the HIP ConvNet (through the C-ABI) against the fp32 PyTorch-CPU
+restatement (oracle/net_oracle.py), itself pinned to the reference's Python classes
+(tests/test_nn_golden.py).
+
+Tolerance (BASELINE.json north_star): |logit - ref| <= 1e-4 and |value - ref| <= 1e-4
+for the parity precisions (AZ_PREC_F32, AZ_PREC_BF16X3).  Plain bf16 is a throughput
+variant and only gets a loose sanity bound."""
+import numpy as np
+import pytest
+
+TOL = 1e-4
+
+
+@pytest.fixture(scope="module")
+def engine():
+    import az_amd
+    return az_amd.Engine(0)
+
+
+def _planes(B, bs, seed):
+    """Feature planes of random legal positions (0/1 stone planes, coords), like the search emits."""
+    import az_oracle as O
+    rng = np.random.default_rng(seed)
+    out = np.zeros((B, 11, bs, bs), np.float32)
+    for b in range(B):
+        k = int(rng.integers(0, bs * bs // 3))
+        moves = rng.permutation(bs * bs)[:k].tolist()
+        out[b] = O.position(bs, moves)[0]
+    return out
+
+
+CASES = [  # (board, channels, blocks, residual, conv_bias, B)
+    (15, 64, 6, 1, 0, 16),     # C2 net
+    (15, 256, 20, 1, 0, 8),    # C3 net
+    (15, 32, 3, 0, 0, 5),      # exporter fallback (plain stack)
+    (8, 16, 2, 1, 1, 3),       # SimplifiedModel shape (pool 8x8 = identity)
+    (9, 64, 2, 1, 0, 130),     # ragged batch (> one 128-row tile of samples)
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("prec", ["f32", "bf16x3"])
+@pytest.mark.parametrize("case", CASES, ids=[str(c) for c in CASES])
+def test_gpu_net_matches_fp32_reference(engine, case, prec):
+    import az_amd
+    import net_oracle
+    bs, ch, blocks, res, bias, B = case
+    p = {"f32": az_amd.AZ_PREC_F32, "bf16x3": az_amd.AZ_PREC_BF16X3}[prec]
+    if p != az_amd.AZ_PREC_F32 and ch % 32:
+        pytest.skip("bf16 trunk needs channels % 32 == 0")
+    desc = az_amd.gomoku_net_desc(board_size=bs, channels=ch, blocks=blocks, residual=res, conv_bias=bias,
+                                  precision=p, max_batch=B)
+    net = az_amd.HipNeuralNetwork(engine, desc)
+    blob = net_oracle.init_blob(desc, seed=11)
+    net.load_weights(blob)
+    x = _planes(B, bs, seed=1)
+    lo, v = net.forward(x)
+    rl, rv = net_oracle.forward(desc, blob, x)
+    err_l = float(np.abs(lo - rl).max())
+    err_v = float(np.abs(v - rv).max())
+    print(f"{case} {prec}: max|dlogit|={err_l:.3e} (|logit|max {np.abs(rl).max():.3f}) max|dvalue|={err_v:.3e}")
+    assert err_l <= TOL and err_v <= TOL
+    # predictBatch semantics: softmax over A
+    pp, pv = net.predictBatch(x)
+    assert np.abs(pp - net_oracle.softmax_policy(rl)).max() <= 1e-5
+    assert np.array_equal(pv, v)
+    net.close()
+
+
+@pytest.mark.gpu
+def test_gpu_net_bf16_sanity(engine):
+    import az_amd
+    import net_oracle
+    desc = az_amd.gomoku_net_desc(board_size=15, channels=64, blocks=6, precision=az_amd.AZ_PREC_BF16, max_batch=8)
+    net = az_amd.HipNeuralNetwork(engine, desc)
+    blob = net_oracle.init_blob(desc, seed=11)
+    net.load_weights(blob)
+    x = _planes(8, 15, seed=2)
+    lo, v = net.forward(x)
+    rl, rv = net_oracle.forward(desc, blob, x)
+    print("bf16 max|dlogit|", np.abs(lo - rl).max(), "max|dvalue|", np.abs(v - rv).max())
+    assert np.abs(lo - rl).max() < 5e-2 * max(1.0, np.abs(rl).max())
+    net.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("prec", [0, 1])
+def test_gpu_net_batch_position_independent(engine, prec):
+    """A sample's output does not depend on its position or batch-mates (bitwise)."""
+    import az_amd
+    import net_oracle
+    desc = az_amd.gomoku_net_desc(board_size=15, channels=64, blocks=2, precision=prec, max_batch=40)
+    net = az_amd.HipNeuralNetwork(engine, desc)
+    net.load_weights(net_oracle.init_blob(desc, seed=5))
+    x = _planes(40, 15, seed=3)
+    lo, v = net.forward(x)
+    perm = np.random.default_rng(0).permutation(40)
+    lo2, v2 = net.forward(x[perm])
+    assert np.array_equal(lo2, lo[perm]) and np.array_equal(v2, v[perm])
+    lo3, v3 = net.forward(x[7:9])
+    assert np.array_equal(lo3, lo[7:9]) and np.array_equal(v3, v[7:9])
+    net.close()
+
+
+@pytest.mark.gpu
+def test_gpu_net_init_random_matches_numpy(engine):
+    """az_net_init_random == oracle/net_oracle.init_blob (same counter-based generator)."""
+    import az_amd
+    import net_oracle
+    desc = az_amd.gomoku_net_desc(board_size=9, channels=32, blocks=1, max_batch=4)
+    a = az_amd.HipNeuralNetwork(engine, desc)
+    a.init_random(77)
+    b = az_amd.HipNeuralNetwork(engine, desc)
+    b.load_weights(net_oracle.init_blob(desc, seed=77))
+    x = _planes(4, 9, seed=4)
+    la, va = a.forward(x)
+    lb, vb = b.forward(x)
+    assert np.array_equal(la, lb) and np.array_equal(va, vb)
+    a.close()
+    b.close()
