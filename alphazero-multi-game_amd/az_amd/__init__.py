@@ -116,6 +116,17 @@ class HipNeuralNetwork:
         p, v = self.predictBatch(np.asarray(planes, np.float32)[None])
         return p[0], float(v[0])
 
+    def profile(self, enable=True):
+        check(lib().az_net_profile(self.h, int(enable)))
+
+    def profile_read(self):
+        """(trunk milliseconds, trunk conv launches, forwards) since profile(True)."""
+        ms = ctypes.c_double()
+        la = ctypes.c_int64()
+        fw = ctypes.c_int64()
+        check(lib().az_net_profile_read(self.h, ctypes.byref(ms), ctypes.byref(la), ctypes.byref(fw)))
+        return ms.value, la.value, fw.value
+
     def getBatchSize(self):
         return self.desc.max_batch
 

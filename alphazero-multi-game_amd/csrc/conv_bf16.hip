@@ -60,6 +60,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_bf16(ConvBf16Args p) {
     const int q = tid & 3;
     int rb_[2], ry[2], rx[2];
     bool rok[2];
+#pragma unroll
     for (int j = 0; j < 2; ++j) {
         const int m = m0 + (tid >> 2) + 64 * j;
         rok[j] = m < Mact;
@@ -72,6 +73,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_bf16(ConvBf16Args p) {
         const int tap = kt / cpt;
         const int c0 = (kt - tap * cpt) * BK + q * 8;
         const int dy = tap / 3 - 1, dx = tap % 3 - 1;
+#pragma unroll
         for (int j = 0; j < 2; ++j) {
             uint4 vh = make_uint4(0, 0, 0, 0), vl = make_uint4(0, 0, 0, 0);
             const int y = ry[j] + dy, x = rx[j] + dx;
@@ -93,6 +95,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_bf16(ConvBf16Args p) {
     };
     auto lstore = [&](int buf) {
         uint8_t* base = lds + buf * NOP * TILE;
+#pragma unroll
         for (int j = 0; j < 2; ++j) {
             const int row = (tid >> 2) + 64 * j;
             const int off = row * ROWB + 16 * (q ^ swz(row));
@@ -106,7 +109,9 @@ __global__ __launch_bounds__(256, 2) void conv3x3_bf16(ConvBf16Args p) {
     };
 
     floatx4 acc[4][4];
+#pragma unroll
     for (int i = 0; i < 4; ++i)
+#pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
 
     gload(0);
@@ -118,19 +123,23 @@ __global__ __launch_bounds__(256, 2) void conv3x3_bf16(ConvBf16Args p) {
         if (kt + 1 < nk) gload(kt + 1);
         const uint8_t* base = lds + buf * NOP * TILE;
         bf16x8 ah[4], bh[4], al[4], bl[4];
+#pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int row = wm * 64 + i * 16 + fr;
             const int off = row * ROWB + 16 * (fh ^ swz(row));
             ah[i] = *reinterpret_cast<const bf16x8*>(base + 0 * TILE + off);
             if (SPLIT) al[i] = *reinterpret_cast<const bf16x8*>(base + 2 * TILE + off);
         }
+#pragma unroll
         for (int j = 0; j < 4; ++j) {
             const int row = wn * 64 + j * 16 + fr;
             const int off = row * ROWB + 16 * (fh ^ swz(row));
             bh[j] = *reinterpret_cast<const bf16x8*>(base + 1 * TILE + off);
             if (SPLIT) bl[j] = *reinterpret_cast<const bf16x8*>(base + 3 * TILE + off);
         }
+#pragma unroll
         for (int i = 0; i < 4; ++i)
+#pragma unroll
             for (int j = 0; j < 4; ++j) {
                 if (SPLIT) {
                     acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
@@ -143,22 +152,26 @@ __global__ __launch_bounds__(256, 2) void conv3x3_bf16(ConvBf16Args p) {
     }
 
     // epilogue: C/D map col = lane&15, row = 4*(lane>>4) + r
+#pragma unroll
     for (int i = 0; i < 4; ++i)
+#pragma unroll
         for (int j = 0; j < 4; ++j) {
             const int n = n0 + wn * 64 + j * 16 + fr;
-            if (n >= p.N) continue;
-            const float bias = p.bias[n];
+            const bool nok = n < p.N;
+            const float bias = nok ? p.bias[n] : 0.0f;
+#pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int m = m0 + wm * 64 + i * 16 + 4 * fh + r;
-                if (m >= Mact) continue;
-                const size_t o = (size_t)m * p.N + n;
-                float v = acc[i][j][r] + bias;
-                if (p.Rhi) v += bf2f(p.Rhi[o]) + (SPLIT ? bf2f(p.Rlo[o]) : 0.0f);
-                if (p.relu) v = v > 0.0f ? v : 0.0f;
-                const uint16_t hi = f2bf(v);
-                p.Chi[o] = hi;
-                if (SPLIT) p.Clo[o] = f2bf(v - bf2f(hi));
-                if (p.Cf) p.Cf[o] = v;
+                if (nok && m < Mact) {
+                    const size_t o = (size_t)m * p.N + n;
+                    float v = acc[i][j][r] + bias;
+                    if (p.Rhi) v += bf2f(p.Rhi[o]) + (SPLIT ? bf2f(p.Rlo[o]) : 0.0f);
+                    if (p.relu) v = v > 0.0f ? v : 0.0f;
+                    const uint16_t hi = f2bf(v);
+                    p.Chi[o] = hi;
+                    if (SPLIT) p.Clo[o] = f2bf(v - bf2f(hi));
+                    if (p.Cf) p.Cf[o] = v;
+                }
             }
         }
 }

@@ -105,6 +105,11 @@ struct az_net {
     float* in_nchw = nullptr;
     int* d_nb = nullptr;
     bool loaded = false;
+    // profiling: HIP events bracketing the 3x3 trunk of every forward (on the launch stream)
+    bool prof = false;
+    std::vector<hipEvent_t> evpool;
+    size_t evused = 0;
+    long long prof_launches = 0, prof_forwards = 0;
     std::mutex mu;
 };
 
@@ -237,6 +242,19 @@ int net_forward(az_net* n, const float* x0, int B, const int* nb, float* logits,
     az_launch_gemm_f32(gemm_args(n->in, x0, n->cin_pad, n->h0, F, nullptr, rows, H, W, nb, HW), ACT_RELU, false, st);
     float* h = n->h0;
     float* other = n->h1;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    if (n->prof && d.blocks > 0) {
+        while (n->evpool.size() < n->evused + 2) {
+            hipEvent_t ev;
+            HIPCHK(hipEventCreate(&ev));
+            n->evpool.push_back(ev);
+        }
+        ev0 = n->evpool[n->evused]; ev1 = n->evpool[n->evused + 1];
+        n->evused += 2;
+        HIPCHK(hipEventRecord(ev0, st));
+        n->prof_launches += 2 * d.blocks;
+        n->prof_forwards += 1;
+    }
     if (!bf) {
         for (int i = 0; i < d.blocks; ++i) {
             az_launch_gemm_f32(gemm_args(n->blk[2 * i], h, F, n->t, F, nullptr, rows, H, W, nb, HW), ACT_RELU, false, st);
@@ -270,6 +288,7 @@ int net_forward(az_net* n, const float* x0, int B, const int* nb, float* logits,
         }
         if (d.blocks > 0) h = other;
     }
+    if (ev1) HIPCHK(hipEventRecord(ev1, st));
     az_launch_pool(h, n->pool, B, H, W, F, P, nb, st);
     az_launch_gemm_f32(gemm_args(n->pconv, n->pool, F, n->pp, d.head_channels, nullptr, B * PP, 1, 1, nb, PP), ACT_RELU, false, st);
     az_launch_gemm_f32(gemm_args(n->vconv, n->pool, F, n->vp, d.head_channels, nullptr, B * PP, 1, 1, nb, PP), ACT_RELU, false, st);
@@ -324,7 +343,11 @@ int search_step(az_search* s, int mode) {
     if (s->c.eval_kind == AZ_EVAL_NET) {
         hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, st, s->t);
         az_launch_gather_planes(s->t.planes, s->d_batch, s->t.eval_games, s->t.n_eval, s->t.A * 16, G, st);
-        if (int r = net_forward(s->net, s->d_batch, G, s->t.n_eval, s->d_logits, s->d_value, st)) return r;
+        const bool prof = s->net->prof;
+        if (mode != MODE_SIM) s->net->prof = false;   // time only the simulation batches
+        int r = net_forward(s->net, s->d_batch, G, s->t.n_eval, s->d_logits, s->d_value, st);
+        s->net->prof = prof;
+        if (r) return r;
     }
     hipLaunchKernelGGL(k_expand_backup, dim3(G), dim3(64), 0, st, s->t, mode);
     HIPCHK(hipGetLastError());
@@ -632,6 +655,31 @@ static int net_host_forward(az_net* n, const float* planes, int B, float* logits
     if (logits) HIPCHK(hipMemcpyAsync(logits, pol, (size_t)B * A * 4, hipMemcpyDeviceToHost, st));
     if (value) HIPCHK(hipMemcpyAsync(value, n->value, (size_t)B * 4, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
+    return 0;
+}
+
+int az_net_profile(az_net* n, int enable) {
+    if (!n) return fail(AZ_ERR_ARG, "null net");
+    std::lock_guard<std::mutex> lk(n->mu);
+    n->prof = enable != 0;
+    n->evused = 0; n->prof_launches = 0; n->prof_forwards = 0;
+    return 0;
+}
+
+int az_net_profile_read(az_net* n, double* trunk_ms, int64_t* trunk_launches, int64_t* forwards) {
+    if (!n) return fail(AZ_ERR_ARG, "null net");
+    std::lock_guard<std::mutex> lk(n->mu);
+    HIPCHK(hipSetDevice(n->e->device));
+    HIPCHK(hipStreamSynchronize(n->e->stream));
+    double ms = 0.0;
+    for (size_t i = 0; i + 1 < n->evused; i += 2) {
+        float t = 0.0f;
+        HIPCHK(hipEventElapsedTime(&t, n->evpool[i], n->evpool[i + 1]));
+        ms += t;
+    }
+    if (trunk_ms) *trunk_ms = ms;
+    if (trunk_launches) *trunk_launches = n->prof_launches;
+    if (forwards) *forwards = n->prof_forwards;
     return 0;
 }
 

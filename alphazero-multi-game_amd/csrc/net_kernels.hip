@@ -56,6 +56,7 @@ __global__ __launch_bounds__(256) void gemm_f32(GemmArgs p) {
     const int r0 = tid >> 3;
     int arow_b[4], arow_y[4], arow_x[4];
     bool arow_ok[4];
+#pragma unroll
     for (int i = 0; i < 4; ++i) {
         const int m = m0 + r0 + 32 * i;
         arow_ok[i] = m < Mact;
@@ -72,6 +73,7 @@ __global__ __launch_bounds__(256) void gemm_f32(GemmArgs p) {
         int tap = 0, c = k;
         if (p.taps == 9) { tap = k / p.Cch; c = k - tap * p.Cch; }
         const int dy = tap / 3 - 1, dx = tap % 3 - 1;
+#pragma unroll
         for (int i = 0; i < 4; ++i) {
             float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
             if (arow_ok[i] && k < K) {
@@ -87,6 +89,7 @@ __global__ __launch_bounds__(256) void gemm_f32(GemmArgs p) {
             }
             ra[i] = v;
         }
+#pragma unroll
         for (int i = 0; i < BROWS; ++i) {
             const int n = n0 + r0 + 32 * i;
             float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -97,6 +100,7 @@ __global__ __launch_bounds__(256) void gemm_f32(GemmArgs p) {
     auto store_stage = [&](int buf) {
         float* as = As[buf];
         float* bs = Bs[buf];
+#pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int m = r0 + 32 * i;
             as[(kq * 4 + 0) * LDA + m] = ra[i].x;
@@ -104,6 +108,7 @@ __global__ __launch_bounds__(256) void gemm_f32(GemmArgs p) {
             as[(kq * 4 + 2) * LDA + m] = ra[i].z;
             as[(kq * 4 + 3) * LDA + m] = ra[i].w;
         }
+#pragma unroll
         for (int i = 0; i < BROWS; ++i) {
             const int n = r0 + 32 * i;
             bs[(kq * 4 + 0) * LDB + n] = rb[i].x;
@@ -114,8 +119,11 @@ __global__ __launch_bounds__(256) void gemm_f32(GemmArgs p) {
     };
 
     floatx16 acc[MT][NT];
+#pragma unroll
     for (int i = 0; i < MT; ++i)
+#pragma unroll
         for (int j = 0; j < NT; ++j)
+#pragma unroll
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
 
     load_stage(0);
@@ -130,9 +138,13 @@ __global__ __launch_bounds__(256) void gemm_f32(GemmArgs p) {
 #pragma unroll 4
         for (int kk = 0; kk < BK / 2; ++kk) {
             float a[MT], b[NT];
+#pragma unroll
             for (int i = 0; i < MT; ++i) a[i] = as[(kk * 2 + kh) * LDA + wm * TM + i * 32 + l32];
+#pragma unroll
             for (int j = 0; j < NT; ++j) b[j] = bs[(kk * 2 + kh) * LDB + wn * TN + j * 32 + l32];
+#pragma unroll
             for (int i = 0; i < MT; ++i)
+#pragma unroll
                 for (int j = 0; j < NT; ++j)
                     acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[j], acc[i][j], 0, 0, 0);
         }
@@ -143,17 +155,21 @@ __global__ __launch_bounds__(256) void gemm_f32(GemmArgs p) {
     }
 
     // Epilogue: C/D map col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5).
+#pragma unroll
     for (int i = 0; i < MT; ++i)
+#pragma unroll
         for (int j = 0; j < NT; ++j) {
             const int n = n0 + wn * TN + j * 32 + l32;
-            if (n >= p.N) continue;
-            const float bias = p.bias ? p.bias[n] : 0.0f;
+            const bool nok = n < p.N;
+            const float bias = (nok && p.bias) ? p.bias[n] : 0.0f;
+#pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int m = m0 + wm * TM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * kh;
-                if (m >= Mact) continue;
-                float v = acc[i][j][r] + bias;
-                if (RES) v += p.res[(size_t)m * p.ldc + n];
-                p.C[(size_t)m * p.ldc + n] = activate<ACT>(v);
+                if (nok && m < Mact) {
+                    float v = acc[i][j][r] + bias;
+                    if (RES) v += p.res[(size_t)m * p.ldc + n];
+                    p.C[(size_t)m * p.ldc + n] = activate<ACT>(v);
+                }
             }
         }
 }

@@ -1,0 +1,181 @@
+#!/usr/bin/env python3
+"""bench.py -- self-play positions/s (+ NN evals/s) at 800 sims/move on MI355X.
+
+Workload (BASELINE.json configs[2], "C3"): Gomoku 15x15, 20-block x 256-filter residual
+policy/value net, 2048 concurrent games per GPU, 800 simulations per move, the
+reference's playSingleGame loop (Dirichlet noise, temperature schedule, subtree
+reuse, per-game transposition table).  One step = one committed move of every game
+(800 batched simulations: PUCT select -> leaf batch through the ConvNet -> expand /
+backup).  Games shard across ranks with no data-path collective (weak scaling:
+2048 games per GPU); RCCL only broadcasts the weights and reduces counters.
+
+Synthetic data: games start from the empty board; weights are random-init of the
+named architecture (counter-based generator, identical on every rank).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for _p in (os.path.join(ROOT, "alphazero-multi-game_amd"), os.path.join(ROOT, "oracle")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import numpy as np  # noqa: E402
+
+METRIC = "self-play positions/sec (+ NN evals/sec) at 800 sims/move, 1/2/4/8 GPU"
+PEAK_TFLOPS = {"bf16x3": 2500.0, "bf16": 2500.0, "f32": 157.3}   # dense MFMA peaks, MI355X_MICROARCH.md
+PREC = {"f32": 0, "bf16x3": 1, "bf16": 2}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--games", type=int, default=2048, help="games per GPU")
+    ap.add_argument("--sims", type=int, default=800)
+    ap.add_argument("--board", type=int, default=15)
+    ap.add_argument("--channels", type=int, default=256)
+    ap.add_argument("--blocks", type=int, default=20)
+    ap.add_argument("--precision", default="bf16x3", choices=list(PREC))
+    ap.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU oracle on rank 0 at N=1")
+    ap.add_argument("--cpu-moves", type=int, default=1)
+    ap.add_argument("--seed", type=int, default=1234)
+    return ap.parse_args()
+
+
+def cpu_baseline(desc, blob, board, sims, moves):
+    """The CPU restatement (oracle/, Mode S, one game) with the fp32 PyTorch-CPU network
+    evaluating one state per call, as the reference's ParallelMCTS::evaluateState does."""
+    import torch
+    import az_oracle as O
+    import net_oracle
+    model = net_oracle.Model(desc, blob)
+    calls = [0]
+
+    def ev(game, planes):
+        calls[0] += 1
+        lo, v = model(planes[None])
+        return lo[0], float(v[0])
+
+    ev(0, np.zeros((11, board, board), np.float32))   # warm-up
+    calls[0] = 0
+    t0 = time.perf_counter()
+    O.play(bs=board, sims=sims, max_moves=moves, eval_kind=O.EVAL_NET, evaluator=ev)
+    dt = time.perf_counter() - t0
+    return {"value": moves / dt, "unit": "positions/s", "cores": torch.get_num_threads(), "kind": "port",
+            "evals_per_s": calls[0] / dt,
+            "sample": f"1 game x {moves} move(s) x {sims} sims, Gomoku {board}x{board}, {desc.blocks}b x "
+                      f"{desc.channels}f fp32 net on PyTorch-CPU (B=1 per evaluation), oracle/ Mode S search; "
+                      f"{calls[0]} evaluations in {dt:.1f} s"}
+
+
+def main():
+    a = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", init_method="env://")
+
+    import az_amd
+    import net_oracle
+    eng = az_amd.Engine(local)
+    desc = az_amd.gomoku_net_desc(board_size=a.board, channels=a.channels, blocks=a.blocks,
+                                  precision=PREC[a.precision], max_batch=a.games)
+    net = az_amd.HipNeuralNetwork(eng, desc)
+    blob = None
+    if dist is None:
+        net.init_random(a.seed)
+    else:
+        import torch
+        t = torch.empty(net.num_params, dtype=torch.float32, device=f"cuda:{local}")
+        if rank == 0:
+            blob = net_oracle.init_blob(desc, a.seed)
+            t.copy_(torch.from_numpy(blob))
+        dist.broadcast(t, src=0)           # RCCL over xGMI: one weight version
+        blob = t.cpu().numpy()
+        net.load_weights(blob)
+    m = az_amd.ParallelMCTS(eng, n_games=a.games, board_size=a.board, num_simulations=a.sims,
+                            evaluator=az_amd.AZ_EVAL_NET, net=net, noise_seed=42 + rank * a.games,
+                            noise_seed_stride=1)
+    m.newGames()
+    m.addDirichletNoise(0.03, 0.25)
+    for _ in range(a.warmup):
+        m.selfplayStep()
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+    barrier()
+    net.profile(True)
+    t0 = time.perf_counter()
+    moves = evals = 0
+    for _ in range(a.steps):
+        mv, ev = m.selfplayStep()
+        moves += mv
+        evals += ev
+    elapsed = time.perf_counter() - t0     # selfplayStep returns after a stream sync
+    barrier()
+    trunk_ms, launches, forwards = net.profile_read()
+
+    if dist is not None:
+        import torch
+        x = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(x, op=dist.ReduceOp.MAX)
+        elapsed = float(x.item())
+        c = torch.tensor([moves, evals], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(c, op=dist.ReduceOp.SUM)
+        moves, evals = int(c[0].item()), int(c[1].item())
+
+    if rank == 0:
+        HW = a.board * a.board
+        conv_flops_per_eval = 2 * a.blocks * 2.0 * 9 * a.channels * a.channels * HW
+        local_evals = evals // max(1, world)
+        per_launch_flops = local_evals * conv_flops_per_eval / max(1, launches)
+        per_launch_ms = trunk_ms / max(1, launches)
+        achieved = per_launch_flops / (per_launch_ms * 1e-3) / 1e12 if launches else 0.0
+        peak = PEAK_TFLOPS[a.precision]
+        out = {
+            "metric": METRIC,
+            "value": moves / elapsed,
+            "unit": "positions/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": 1e3 * elapsed / a.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": a.precision,
+            "data": "synthetic: self-play from empty boards, counter-based random-init weights of the named net",
+            "config": {"workload": f"C3 Gomoku {a.board}x{a.board}, {a.blocks}b x {a.channels}f ResNet, "
+                                   f"{a.sims} sims/move", "games_per_gpu": a.games, "global_games": a.games * world,
+                       "sims_per_move": a.sims, "board": a.board, "blocks": a.blocks, "channels": a.channels,
+                       "parallelism": f"game-shard x{world}"},
+            "nn_evals_per_s": evals / elapsed,
+            "roofline": {"kernel": f"conv3x3_{a.precision} (trunk)", "bound": "mfma", "achieved": achieved,
+                         "peak": peak, "unit": "TFLOP/s", "frac": achieved / peak, "traffic": None,
+                         "launches": launches, "avg_launch_ms": per_launch_ms,
+                         "flops_per_launch": per_launch_flops},
+        }
+        if a.cpu_baseline and world == 1:
+            if blob is None:
+                blob = net_oracle.init_blob(desc, a.seed)
+            out["cpu_baseline"] = cpu_baseline(desc, blob, a.board, a.sims, a.cpu_moves)
+        else:
+            out["cpu_baseline"] = None
+        print(json.dumps(out))
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

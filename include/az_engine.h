@@ -86,6 +86,10 @@ int az_net_init_random(az_net* n, uint64_t seed);
 int az_net_set_precision(az_net* n, int precision);
 /* planes: host fp32 NCHW [B][in_planes][H][W].  logits [B][A] raw, value [B] (tanh). */
 int az_net_forward(az_net* n, const float* planes, int B, float* logits, float* value);
+/* Profiling: HIP events bracket the 3x3 trunk (2*blocks conv launches) of every
+ * simulation-batch forward on the engine stream.  read returns the summed trunk time. */
+int az_net_profile(az_net* n, int enable);
+int az_net_profile_read(az_net* n, double* trunk_ms, int64_t* trunk_launches, int64_t* forwards);
 /* predictBatch semantics: policy = softmax over A (max-subtracted, sequential fp32 sum,
  * torch_neural_network.cpp:296-316), value [B]. */
 int az_net_predict_batch(az_net* n, const float* planes, int B, float* policy, float* value);

@@ -127,3 +127,35 @@ def softmax_policy(logits):
             s = np.float32(s + v)
         out[b] = e / s if s > 0 else e
     return out
+
+
+class Model:
+    """Cached fp32 CPU model (weights unpacked once) for repeated single-state evaluations."""
+
+    def __init__(self, desc, blob):
+        self.desc = desc
+        self.p = unpack(desc, blob)
+
+    def __call__(self, planes):
+        d, p = self.desc, self.p
+        x = torch.from_numpy(np.ascontiguousarray(planes, np.float32))
+
+        def conv_bn(x, conv, bn, pad):
+            x = F.conv2d(x, p[conv + ".weight"], p.get(conv + ".bias"), padding=pad)
+            return F.batch_norm(x, p[bn + ".running_mean"], p[bn + ".running_var"], p[bn + ".weight"],
+                                p[bn + ".bias"], training=False, eps=1e-5)
+
+        with torch.no_grad():
+            x = torch.relu(conv_bn(x, "input_conv", "input_bn", 1))
+            for i in range(d.blocks):
+                r = x
+                y = torch.relu(conv_bn(x, f"blocks.{i}.0", f"blocks.{i}.1", 1))
+                y = conv_bn(y, f"blocks.{i}.3", f"blocks.{i}.4", 1)
+                x = torch.relu(y + r) if d.residual else torch.relu(y)
+            x = F.adaptive_avg_pool2d(x, (d.pool, d.pool))
+            pol = torch.relu(conv_bn(x, "policy_conv", "policy_bn", 0)).reshape(x.shape[0], -1)
+            pol = F.linear(pol, p["policy_fc.weight"], p["policy_fc.bias"])
+            v = torch.relu(conv_bn(x, "value_conv", "value_bn", 0)).reshape(x.shape[0], -1)
+            v = torch.relu(F.linear(v, p["value_fc1.weight"], p["value_fc1.bias"]))
+            v = torch.tanh(F.linear(v, p["value_fc2.weight"], p["value_fc2.bias"]))
+        return pol.numpy(), v.reshape(-1).numpy()
