@@ -1,0 +1,69 @@
+"""Full hot path with the ConvNet evaluator: device feature planes -> HIP ConvNet ->
+softmax -> TT/expand/backup.  The engine logs every evaluation of one game; the CPU
+restatement replays those (policy, value) outputs and must reproduce the device
+search bit for bit, and must have asked for exactly the logged feature planes.
+The logged network outputs are separately checked against the fp32 reference
+network (tolerance 1e-4, BASELINE.json north_star)."""
+import numpy as np
+import pytest
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("prec", [0, 1])
+@pytest.mark.parametrize("logged", [0, 3])
+def test_gpu_net_selfplay_matches_oracle_replay(prec, logged):
+    import az_amd
+    import az_oracle as O
+    import net_oracle
+    bs, sims, G, moves = 9, 48, 4, 6
+    eng = az_amd.Engine(0)
+    desc = az_amd.gomoku_net_desc(board_size=bs, channels=32, blocks=2, precision=prec, max_batch=G)
+    net = az_amd.HipNeuralNetwork(eng, desc)
+    blob = net_oracle.init_blob(desc, seed=9)
+    net.load_weights(blob)
+    m = az_amd.ParallelMCTS(eng, n_games=G, board_size=bs, num_simulations=sims, evaluator=az_amd.AZ_EVAL_NET,
+                            net=net, noise_seed=42, noise_seed_stride=1)
+    cap = (sims + 2) * (moves + 1)
+    m.enableEvalLog(logged, cap)
+    m.newGames()
+    m.addDirichletNoise(0.03, 0.25)
+    dev = []
+    for ply in range(moves):
+        m.search()
+        T = 1.0 if ply < 30 else 0.0
+        act, val, probs, cact, nch = m.select(True, T)
+        a, N, VL, W, P = m.rootChildren(logged)
+        dev.append(dict(action=int(act[logged]), value=float(val[logged]), N=N.tolist(), VL=VL.tolist(),
+                        W=W.view(np.uint32).tolist(), P=P.view(np.uint32).tolist(),
+                        probs=probs[logged, :nch[logged]].view(np.uint32).tolist()))
+        term, _ = m.updateWithMove(act)
+        if ply % 2 == 0:
+            m.addDirichletNoise(0.03, 0.25)
+        if term[logged]:
+            break
+    pol, valv, planes = m.readEvalLog(cap)
+    assert len(pol) > sims
+
+    k = [0]
+
+    def replay(game, x):
+        i = k[0]
+        k[0] += 1
+        assert np.array_equal(x, planes[i]), f"feature planes differ at evaluation {i}"
+        return pol[i], float(valv[i])
+
+    ref = O.play(bs=bs, sims=sims, max_moves=len(dev), eval_kind=O.EVAL_REPLAY, evaluator=replay,
+                 noise_seed=42 + logged)[0]
+    assert k[0] == len(pol)
+    for ply, (d, r) in enumerate(zip(dev, ref["moves"])):
+        kids = r["children"]
+        assert d["N"] == [c[1] for c in kids] and d["VL"] == [c[2] for c in kids], ply
+        assert d["W"] == [c[3] for c in kids] and d["P"] == [c[4] for c in kids], ply
+        assert d["probs"] == r["probs"] and d["action"] == r["action"], ply
+        assert np.float32(d["value"]).view(np.uint32) == r["value"], ply
+    # the logged network outputs against the fp32 reference network
+    rl, rv = net_oracle.forward(desc, blob, planes)
+    assert np.abs(valv - rv).max() <= 1e-4
+    assert np.abs(pol - net_oracle.softmax_policy(rl)).max() <= 1e-4
+    m.close()
+    net.close()
