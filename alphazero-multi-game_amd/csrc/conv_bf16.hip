@@ -19,6 +19,7 @@
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float floatx4 __attribute__((ext_vector_type(4)));
+typedef float floatx16 __attribute__((ext_vector_type(16)));
 
 namespace {
 
@@ -197,4 +198,655 @@ void az_conv_bf16_launch(const ConvBf16Args& a, bool split, hipStream_t st) {
 void az_launch_split_bf16(const float* in, uint16_t* hi, uint16_t* lo, size_t n, const int* m_limit, int rows_per_sample,
                           int C, hipStream_t st) {
     hipLaunchKernelGGL(k_split_bf16, dim3(2048), dim3(256), 0, st, in, hi, lo, n, m_limit, rows_per_sample, C);
+}
+
+// ===========================================================================
+// v2: block tile BM pixels x BN channels, 8 waves (WM x WN), BK = 32.  Operand tiles
+// move HBM/L2 -> LDS by global_load_lds_dwordx4 (LDS-DMA, per-lane source address
+// = the im2col gather, zero page for the board edge) into a STAGES-deep ring; each
+// wave issues its share of the 16-row pieces and retires them with a counted
+// s_waitcnt vmcnt before one raw s_barrier per k-step (the loads of k-steps kt+1 ..
+// kt+STAGES-1 stay in flight across it).  LDS images are linear rows of 64 B; the
+// chunk swizzle is applied to the SOURCE address (glds writes lane-linear).  The
+// epilogue stages the fp32 tile through LDS and stores 16-byte vectors.
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) const void g_void_t;
+
+template <bool SPLIT, int BM, int BN, int WM, int WN, int STAGES>
+__global__ __launch_bounds__(WM * WN * 64, 1) void conv3x3_v2(ConvBf16Args p) {
+    constexpr int NT = WM * WN * 64, NW = WM * WN;
+    constexpr int ROWB = 64;                          // 32 bf16 per row
+    constexpr int NPL = SPLIT ? 2 : 1;                // hi (+ lo) planes
+    constexpr int A_BYTES = BM * ROWB, B_BYTES = BN * ROWB;
+    constexpr int STAGE = NPL * (A_BYTES + B_BYTES);
+    constexpr int EPI_LD = BN + 4;                    // fp32 row stride of the epilogue tile
+    constexpr int EPI = BM * EPI_LD * 4;
+    constexpr int LDS = STAGES * STAGE > EPI ? STAGES * STAGE : EPI;
+    constexpr int A_INS = BM / 16, B_INS = BN / 16;   // 1 KiB pieces per plane
+    constexpr int INS = NPL * (A_INS + B_INS);
+    constexpr int PW = INS / NW;                      // pieces per wave per k-step
+    static_assert(INS % NW == 0, "pieces must split evenly over waves");
+    constexpr int TM = BM / WM, TN = BN / WN;         // wave tile
+    constexpr int FM = TM / 16, FN = TN / 16;         // 16x16 MFMA tiles per wave
+    __shared__ __attribute__((aligned(16))) uint8_t lds[LDS];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, wave = tid >> 6;
+    const int wm = wave / WN, wn = wave % WN;
+    const int nbm = (p.M + BM - 1) / BM;
+    const int bm = blockIdx.x % nbm, bn = blockIdx.x / nbm;
+    const int m0 = bm * BM, n0 = bn * BN;
+    const int Mact = p.m_limit ? min(p.M, *p.m_limit * p.rows_per_sample) : p.M;
+    if (m0 >= Mact) return;
+    const int C = p.C, H = p.H, W = p.W, HW = H * W, K = 9 * C;
+    const int cpt = C / 32, nk = 9 * cpt;
+
+    // Per-lane source description of this wave's PW pieces (same rows every k-step).
+    const uint16_t* src_base[PW];     // A: sample base; B: weight row base
+    int src_y[PW], src_x[PW];         // A: pixel coords (-1000: row out of range)
+    bool isA[PW];
+    int lds_off[PW];                  // wave-uniform LDS offset of the piece inside a stage
+    int chunk[PW];                    // logical 16-byte chunk this lane fetches
+#pragma unroll
+    for (int j = 0; j < PW; ++j) {
+        const int q = wave + NW * j;
+        const int row_in_piece = lane >> 2, phys = lane & 3;
+        if (q < NPL * A_INS) {
+            const int plane = q / A_INS, rb = q % A_INS;
+            const int row = rb * 16 + row_in_piece;
+            const int m = m0 + row;
+            isA[j] = true;
+            lds_off[j] = plane * A_BYTES + rb * 1024;
+            chunk[j] = phys ^ swz(row);
+            const uint16_t* base = plane ? p.Alo : p.Ahi;
+            if (m < Mact) {
+                const int b = m / HW, r = m - b * HW;
+                src_base[j] = base + (size_t)b * HW * C;
+                src_y[j] = r / W; src_x[j] = r - (r / W) * W;
+            } else {
+                src_base[j] = base; src_y[j] = -1000; src_x[j] = -1000;
+            }
+        } else {
+            const int qq = q - NPL * A_INS;
+            const int plane = qq / B_INS, rb = qq % B_INS;
+            const int row = rb * 16 + row_in_piece;
+            const int n = n0 + row;
+            isA[j] = false;
+            lds_off[j] = NPL * A_BYTES + plane * B_BYTES + rb * 1024;
+            chunk[j] = phys ^ swz(row);
+            const uint16_t* base = plane ? p.Blo : p.Bhi;
+            src_base[j] = n < p.N ? base + (size_t)n * K : nullptr;
+            src_y[j] = 0; src_x[j] = 0;
+        }
+    }
+    auto issue = [&](int kt) {
+        const int tap = kt / cpt;
+        const int c0 = (kt - tap * cpt) * 32;
+        const int dy = tap / 3 - 1, dx = tap % 3 - 1;
+        uint8_t* stage = lds + (kt % STAGES) * STAGE;
+#pragma unroll
+        for (int j = 0; j < PW; ++j) {
+            const uint16_t* src;
+            if (isA[j]) {
+                const int y = src_y[j] + dy, x = src_x[j] + dx;
+                src = (y >= 0 && y < H && x >= 0 && x < W) ? src_base[j] + ((size_t)(y * W + x) * C + c0 + chunk[j] * 8)
+                                                           : p.zero + chunk[j] * 8;
+            } else {
+                src = src_base[j] ? src_base[j] + (size_t)kt * 32 + chunk[j] * 8 : p.zero + chunk[j] * 8;
+            }
+            __builtin_amdgcn_global_load_lds((g_void_t*)src, (lds_void_t*)(stage + lds_off[j]), 16, 0, 0);
+        }
+    };
+
+    floatx4 acc[FM][FN];
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+    for (int s = 0; s < STAGES - 1; ++s)
+        if (s < nk) issue(s);
+    const int fr = lane & 15, fh = lane >> 4;
+    for (int kt = 0; kt < nk; ++kt) {
+        // retire this wave's pieces of k-step kt, leaving later k-steps in flight
+        if (kt + STAGES - 2 < nk) {
+            if constexpr (STAGES == 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PW) : "memory");
+            else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PW * (STAGES - 2)) : "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        if (kt + STAGES - 1 < nk) issue(kt + STAGES - 1);
+        const uint8_t* st = lds + (kt % STAGES) * STAGE;
+        bf16x8 ah[FM], al[FM], bh[FN], bl[FN];
+#pragma unroll
+        for (int i = 0; i < FM; ++i) {
+            const int row = wm * TM + i * 16 + fr;
+            const int off = row * ROWB + 16 * (fh ^ swz(row));
+            ah[i] = *reinterpret_cast<const bf16x8*>(st + off);
+            if (SPLIT) al[i] = *reinterpret_cast<const bf16x8*>(st + A_BYTES + off);
+        }
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+            const int row = wn * TN + j * 16 + fr;
+            const int off = row * ROWB + 16 * (fh ^ swz(row));
+            bh[j] = *reinterpret_cast<const bf16x8*>(st + NPL * A_BYTES + off);
+            if (SPLIT) bl[j] = *reinterpret_cast<const bf16x8*>(st + NPL * A_BYTES + B_BYTES + off);
+        }
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+            for (int j = 0; j < FN; ++j) {
+                if (SPLIT) {
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+                }
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+            }
+    }
+    // epilogue: fp32 tile through LDS (ring is free once every wave passed its last read)
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __syncthreads();
+    float* ep = reinterpret_cast<float*>(lds);
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                ep[(wm * TM + i * 16 + 4 * fh + r) * EPI_LD + wn * TN + j * 16 + fr] = acc[i][j][r];
+    __syncthreads();
+    constexpr int VPR = BN / 8;                        // 8-channel vectors per row
+    for (int v = tid; v < BM * VPR; v += NT) {
+        const int row = v / VPR, cv = (v % VPR) * 8;
+        const int m = m0 + row, n = n0 + cv;
+        if (m >= Mact || n >= p.N) continue;
+        const float4 x0 = *reinterpret_cast<const float4*>(ep + row * EPI_LD + cv);
+        const float4 x1 = *reinterpret_cast<const float4*>(ep + row * EPI_LD + cv + 4);
+        float o[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+        const size_t g = (size_t)m * p.N + n;
+        const float4 b0 = *reinterpret_cast<const float4*>(p.bias + n);
+        const float4 b1 = *reinterpret_cast<const float4*>(p.bias + n + 4);
+        const float bb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+        uint16_t rh[8], rl[8];
+        if (p.Rhi) {
+            *reinterpret_cast<uint4*>(rh) = *reinterpret_cast<const uint4*>(p.Rhi + g);
+            if (SPLIT) *reinterpret_cast<uint4*>(rl) = *reinterpret_cast<const uint4*>(p.Rlo + g);
+        }
+        uint16_t oh[8], ol[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            float val = o[e] + bb[e];
+            if (p.Rhi) val += bf2f(rh[e]) + (SPLIT ? bf2f(rl[e]) : 0.0f);
+            if (p.relu) val = val > 0.0f ? val : 0.0f;
+            o[e] = val;
+            oh[e] = f2bf(val);
+            if (SPLIT) ol[e] = f2bf(val - bf2f(oh[e]));
+        }
+        *reinterpret_cast<uint4*>(p.Chi + g) = *reinterpret_cast<const uint4*>(oh);
+        if (SPLIT) *reinterpret_cast<uint4*>(p.Clo + g) = *reinterpret_cast<const uint4*>(ol);
+        if (p.Cf) {
+            *reinterpret_cast<float4*>(p.Cf + g) = make_float4(o[0], o[1], o[2], o[3]);
+            *reinterpret_cast<float4*>(p.Cf + g + 4) = make_float4(o[4], o[5], o[6], o[7]);
+        }
+    }
+}
+
+// ===========================================================================
+// v3: v2's glds ring + fragment double buffering.  The wait/barrier that publishes
+// k-step kt+1 sits in the MIDDLE of k-step kt's MFMAs; the ds_reads of kt+1's
+// fragments (second register set) and the glds issue of k-step kt+3 follow it and
+// overlap the second half of kt's MFMAs, so neither LDS latency nor the barrier
+// exposes a bubble at the step boundary.
+template <bool SPLIT, int BM, int BN, int WM, int WN>
+__global__ __launch_bounds__(WM * WN * 64, 1) void conv3x3_v3(ConvBf16Args p) {
+    constexpr int STAGES = 3;
+    constexpr int NT = WM * WN * 64, NW = WM * WN;
+    constexpr int ROWB = 64;
+    constexpr int NPL = SPLIT ? 2 : 1;
+    constexpr int A_BYTES = BM * ROWB, B_BYTES = BN * ROWB;
+    constexpr int STAGE = NPL * (A_BYTES + B_BYTES);
+    constexpr int EPI_LD = BN + 4;
+    constexpr int EPI = BM * EPI_LD * 4;
+    constexpr int LDS = STAGES * STAGE > EPI ? STAGES * STAGE : EPI;
+    constexpr int A_INS = BM / 16, B_INS = BN / 16;
+    constexpr int INS = NPL * (A_INS + B_INS);
+    constexpr int PW = INS / NW;
+    static_assert(INS % NW == 0, "pieces must split evenly over waves");
+    constexpr int TM = BM / WM, TN = BN / WN;
+    constexpr int FM = TM / 16, FN = TN / 16;
+    static_assert(FM % 2 == 0, "two MFMA halves");
+    __shared__ __attribute__((aligned(16))) uint8_t lds[LDS];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, wave = tid >> 6;
+    const int wm = wave / WN, wn = wave % WN;
+    const int nbm = (p.M + BM - 1) / BM;
+    const int bm = blockIdx.x % nbm, bn = blockIdx.x / nbm;
+    const int m0 = bm * BM, n0 = bn * BN;
+    const int Mact = p.m_limit ? min(p.M, *p.m_limit * p.rows_per_sample) : p.M;
+    if (m0 >= Mact) return;
+    const int C = p.C, H = p.H, W = p.W, HW = H * W, K = 9 * C;
+    const int cpt = C / 32, nk = 9 * cpt;
+
+    const uint16_t* src_base[PW];
+    int src_y[PW], src_x[PW];
+    bool isA[PW];
+    int lds_off[PW];
+    int chunk[PW];
+#pragma unroll
+    for (int j = 0; j < PW; ++j) {
+        const int q = wave + NW * j;
+        const int row_in_piece = lane >> 2, phys = lane & 3;
+        if (q < NPL * A_INS) {
+            const int plane = q / A_INS, rb = q % A_INS;
+            const int row = rb * 16 + row_in_piece;
+            const int m = m0 + row;
+            isA[j] = true;
+            lds_off[j] = plane * A_BYTES + rb * 1024;
+            chunk[j] = phys ^ swz(row);
+            const uint16_t* base = plane ? p.Alo : p.Ahi;
+            if (m < Mact) {
+                const int b = m / HW, r = m - b * HW;
+                src_base[j] = base + (size_t)b * HW * C;
+                src_y[j] = r / W; src_x[j] = r - (r / W) * W;
+            } else {
+                src_base[j] = base; src_y[j] = -1000; src_x[j] = -1000;
+            }
+        } else {
+            const int qq = q - NPL * A_INS;
+            const int plane = qq / B_INS, rb = qq % B_INS;
+            const int row = rb * 16 + row_in_piece;
+            const int n = n0 + row;
+            isA[j] = false;
+            lds_off[j] = NPL * A_BYTES + plane * B_BYTES + rb * 1024;
+            chunk[j] = phys ^ swz(row);
+            const uint16_t* base = plane ? p.Blo : p.Bhi;
+            src_base[j] = n < p.N ? base + (size_t)n * K : nullptr;
+            src_y[j] = 0; src_x[j] = 0;
+        }
+    }
+    auto issue = [&](int kt) {
+        const int tap = kt / cpt;
+        const int c0 = (kt - tap * cpt) * 32;
+        const int dy = tap / 3 - 1, dx = tap % 3 - 1;
+        uint8_t* stage = lds + (kt % STAGES) * STAGE;
+#pragma unroll
+        for (int j = 0; j < PW; ++j) {
+            const uint16_t* src;
+            if (isA[j]) {
+                const int y = src_y[j] + dy, x = src_x[j] + dx;
+                src = (y >= 0 && y < H && x >= 0 && x < W) ? src_base[j] + ((size_t)(y * W + x) * C + c0 + chunk[j] * 8)
+                                                           : p.zero + chunk[j] * 8;
+            } else {
+                src = src_base[j] ? src_base[j] + (size_t)kt * 32 + chunk[j] * 8 : p.zero + chunk[j] * 8;
+            }
+            __builtin_amdgcn_global_load_lds((g_void_t*)src, (lds_void_t*)(stage + lds_off[j]), 16, 0, 0);
+        }
+    };
+    const int fr = lane & 15, fh = lane >> 4;
+    auto read_frags = [&](int kt, bf16x8 (&ah)[FM], bf16x8 (&al)[FM], bf16x8 (&bh)[FN], bf16x8 (&bl)[FN]) {
+        const uint8_t* st = lds + (kt % STAGES) * STAGE;
+#pragma unroll
+        for (int i = 0; i < FM; ++i) {
+            const int row = wm * TM + i * 16 + fr;
+            const int off = row * ROWB + 16 * (fh ^ swz(row));
+            ah[i] = *reinterpret_cast<const bf16x8*>(st + off);
+            if (SPLIT) al[i] = *reinterpret_cast<const bf16x8*>(st + A_BYTES + off);
+        }
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+            const int row = wn * TN + j * 16 + fr;
+            const int off = row * ROWB + 16 * (fh ^ swz(row));
+            bh[j] = *reinterpret_cast<const bf16x8*>(st + NPL * A_BYTES + off);
+            if (SPLIT) bl[j] = *reinterpret_cast<const bf16x8*>(st + NPL * A_BYTES + B_BYTES + off);
+        }
+    };
+    floatx4 acc[FM][FN];
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+    auto mfma_rows = [&](int i0, int i1, const bf16x8 (&ah)[FM], const bf16x8 (&al)[FM], const bf16x8 (&bh)[FN],
+                         const bf16x8 (&bl)[FN]) {
+#pragma unroll
+        for (int i = 0; i < FM; ++i) {
+            if (i < i0 || i >= i1) continue;
+#pragma unroll
+            for (int j = 0; j < FN; ++j) {
+                if (SPLIT) {
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+                }
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+            }
+        }
+    };
+    // one k-step: first half of the MFMAs, publish k+1 (wait + barrier), issue k+3,
+    // read k+1's fragments, second half.
+    auto step = [&](int kt, const bf16x8 (&ch)[FM], const bf16x8 (&cl)[FM], const bf16x8 (&dh)[FN],
+                    const bf16x8 (&dl)[FN], bf16x8 (&nah)[FM], bf16x8 (&nal)[FM], bf16x8 (&nbh)[FN], bf16x8 (&nbl)[FN]) {
+        mfma_rows(0, FM / 2, ch, cl, dh, dl);
+        if (kt + 1 < nk) {
+            if (kt + 2 < nk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PW) : "memory");
+            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __builtin_amdgcn_sched_barrier(0);
+            __builtin_amdgcn_s_barrier();
+            __builtin_amdgcn_sched_barrier(0);
+            if (kt + 3 < nk) issue(kt + 3);
+            read_frags(kt + 1, nah, nal, nbh, nbl);
+        }
+        mfma_rows(FM / 2, FM, ch, cl, dh, dl);
+    };
+
+    bf16x8 a0h[FM], a0l[FM], b0h[FN], b0l[FN], a1h[FM], a1l[FM], b1h[FN], b1l[FN];
+#pragma unroll
+    for (int s = 0; s < STAGES; ++s)
+        if (s < nk) issue(s);
+    if (nk > 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PW) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    read_frags(0, a0h, a0l, b0h, b0l);
+    for (int kt = 0; kt < nk; kt += 2) {
+        step(kt, a0h, a0l, b0h, b0l, a1h, a1l, b1h, b1l);
+        if (kt + 1 < nk) step(kt + 1, a1h, a1l, b1h, b1l, a0h, a0l, b0h, b0l);
+    }
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __syncthreads();
+    float* ep = reinterpret_cast<float*>(lds);
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                ep[(wm * TM + i * 16 + 4 * fh + r) * EPI_LD + wn * TN + j * 16 + fr] = acc[i][j][r];
+    __syncthreads();
+    constexpr int VPR = BN / 8;
+    for (int v = tid; v < BM * VPR; v += NT) {
+        const int row = v / VPR, cv = (v % VPR) * 8;
+        const int m = m0 + row, n = n0 + cv;
+        if (m >= Mact || n >= p.N) continue;
+        const float4 x0 = *reinterpret_cast<const float4*>(ep + row * EPI_LD + cv);
+        const float4 x1 = *reinterpret_cast<const float4*>(ep + row * EPI_LD + cv + 4);
+        float o[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+        const size_t g = (size_t)m * p.N + n;
+        const float4 b0 = *reinterpret_cast<const float4*>(p.bias + n);
+        const float4 b1 = *reinterpret_cast<const float4*>(p.bias + n + 4);
+        const float bb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+        uint16_t rh[8], rl[8];
+        if (p.Rhi) {
+            *reinterpret_cast<uint4*>(rh) = *reinterpret_cast<const uint4*>(p.Rhi + g);
+            if (SPLIT) *reinterpret_cast<uint4*>(rl) = *reinterpret_cast<const uint4*>(p.Rlo + g);
+        }
+        uint16_t oh[8], ol[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            float val = o[e] + bb[e];
+            if (p.Rhi) val += bf2f(rh[e]) + (SPLIT ? bf2f(rl[e]) : 0.0f);
+            if (p.relu) val = val > 0.0f ? val : 0.0f;
+            o[e] = val;
+            oh[e] = f2bf(val);
+            if (SPLIT) ol[e] = f2bf(val - bf2f(oh[e]));
+        }
+        *reinterpret_cast<uint4*>(p.Chi + g) = *reinterpret_cast<const uint4*>(oh);
+        if (SPLIT) *reinterpret_cast<uint4*>(p.Clo + g) = *reinterpret_cast<const uint4*>(ol);
+        if (p.Cf) {
+            *reinterpret_cast<float4*>(p.Cf + g) = make_float4(o[0], o[1], o[2], o[3]);
+            *reinterpret_cast<float4*>(p.Cf + g + 4) = make_float4(o[4], o[5], o[6], o[7]);
+        }
+    }
+}
+
+// ===========================================================================
+// v4 (bf16x3): board-halo implicit GEMM.  A block owns TWO boards x 128 output
+// channels.  For every 16-channel chunk the zero-padded 17x17 input halo of both
+// boards is DMA'd (global_load_lds) into LDS once and read by all nine taps as
+// row-shifted windows: outputs live on a 15x17 grid (two dead columns) so that the
+// tap (dy,dx) operand of 32 consecutive outputs is 32 consecutive halo rows
+// (row shift (dy+1)*17 + (dx+1)).  Activation traffic drops ~9x and each weight
+// byte feeds two boards.  LDS images are chunk-major ([16-byte chunk][row]), which
+// keeps every ds_read_b128 lane group on 16 distinct bank slots for ANY row shift.
+// Pipeline: A halo double-buffered per chunk, weights for one tap row (3 taps) per
+// step in a 3-slot ring, counted vmcnt + one barrier per step.  MFMA 32x32x16 bf16.
+constexpr int V4_HROWS = 320;                 // 17*17 = 289 halo rows, padded to 5 x 64
+template <int BNT>
+__global__ __launch_bounds__(512, 1) void conv3x3_v4(ConvBf16Args p) {
+    constexpr int NPL = 2;                    // hi, lo
+    constexpr int BOARDS = 2;
+    constexpr int A_PLANE = 2 * V4_HROWS * 16;             // one board, one plane, 16 channels: 10 KB
+    constexpr int A_BUF = BOARDS * NPL * A_PLANE;          // 40 KB
+    constexpr int B_TAP = NPL * 2 * BNT * 16;              // one tap, both planes: 8 KB (BNT=128)
+    constexpr int B_STAGE = 3 * B_TAP;                     // one tap row: 24 KB
+    constexpr int LDS_MAIN = 2 * A_BUF + 3 * B_STAGE;      // 152 KB
+    constexpr int EP_LD = BNT + 4;
+    constexpr int LDS_EPI = 256 * EP_LD * 4;
+    constexpr int LDS = LDS_MAIN > LDS_EPI ? LDS_MAIN : LDS_EPI;
+    constexpr int PA = (BOARDS * NPL * 2 * (V4_HROWS / 64)) / 8;   // A pieces per wave per chunk (5)
+    constexpr int PB = (3 * NPL * 2 * (BNT / 64)) / 8;             // B pieces per wave per step (3)
+    static_assert((BOARDS * NPL * 2 * (V4_HROWS / 64)) % 8 == 0 && (3 * NPL * 2 * (BNT / 64)) % 8 == 0, "pieces");
+    constexpr int WN = BNT / 64;              // waves along N (2 for 128 channels)
+    constexpr int WM = 8 / WN;                // waves along M (4): 512 output rows / WM
+    constexpr int TM = 512 / WM;              // 128 rows per wave
+    constexpr int FM = TM / 32, FN = 2;       // 32x32 tiles per wave
+    __shared__ __attribute__((aligned(16))) uint8_t lds[LDS];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave / WN, wn = wave % WN;
+    const int nsplit = p.N / BNT;
+    const int pair = blockIdx.x / nsplit, nb = blockIdx.x % nsplit;
+    const int n0 = nb * BNT;
+    const int nboards = p.m_limit ? *p.m_limit : p.M / (p.H * p.W);
+    const int b0 = pair * BOARDS;
+    if (b0 >= nboards) return;
+    const int C = p.C, HW = p.H * p.W, K = 9 * C;   // 15x15 boards (H = W = 15)
+    const int NCH = C / 16, NS = NCH * 3;
+
+    // A pieces of this wave: index q = wave + 8*j over (board, plane, chunk, rowblock)
+    const uint16_t* a_src[PA];   // pixel base (channel 0) or null for padding rows
+    int a_ch[PA];
+    int a_off[PA];
+#pragma unroll
+    for (int j = 0; j < PA; ++j) {
+        const int q = wave + 8 * j;
+        const int rb = q % 5, ch = (q / 5) % 2, plane = (q / 10) % 2, bd = q / 20;
+        const int hr = rb * 64 + lane;
+        const int Y = hr / 17, X = hr - Y * 17;
+        const int b = b0 + bd;
+        const bool ok = hr < 289 && Y >= 1 && Y <= 15 && X >= 1 && X <= 15 && b < nboards;
+        const uint16_t* base = plane ? p.Alo : p.Ahi;
+        a_src[j] = ok ? base + ((size_t)b * HW + (Y - 1) * 15 + (X - 1)) * C + ch * 8 : nullptr;
+        a_ch[j] = ch;
+        a_off[j] = (bd * NPL + plane) * A_PLANE + ch * (V4_HROWS * 16) + rb * 1024;
+    }
+    // B pieces: q over (tap 0..2, plane, chunk, rowblock)
+    const uint16_t* b_src[PB];
+    int b_off[PB];
+#pragma unroll
+    for (int j = 0; j < PB; ++j) {
+        const int q = wave + 8 * j;
+        const int RB = BNT / 64;
+        const int rb = q % RB, ch = (q / RB) % 2, plane = (q / (2 * RB)) % 2, t = q / (4 * RB);
+        const int n = n0 + rb * 64 + lane;
+        const uint16_t* base = plane ? p.Blo : p.Bhi;
+        b_src[j] = base + (size_t)n * K + t * C + ch * 8;        // + dyrow*3*C + chunk*16 at issue
+        b_off[j] = t * B_TAP + (plane * 2 + ch) * BNT * 16 + rb * 1024;
+    }
+    uint8_t* abuf = lds;
+    uint8_t* bbuf = lds + 2 * A_BUF;
+    auto issueA = [&](int c) {
+        uint8_t* dst = abuf + (c & 1) * A_BUF;
+#pragma unroll
+        for (int j = 0; j < PA; ++j) {
+            const uint16_t* src = a_src[j] ? a_src[j] + c * 16 : p.zero + a_ch[j] * 8;
+            __builtin_amdgcn_global_load_lds((g_void_t*)src, (lds_void_t*)(dst + a_off[j]), 16, 0, 0);
+        }
+    };
+    auto issueB = [&](int s) {
+        const int c = s / 3, r = s - c * 3;
+        uint8_t* dst = bbuf + (s % 3) * B_STAGE;
+#pragma unroll
+        for (int j = 0; j < PB; ++j) {
+            const uint16_t* src = b_src[j] + r * 3 * C + c * 16;
+            __builtin_amdgcn_global_load_lds((g_void_t*)src, (lds_void_t*)(dst + b_off[j]), 16, 0, 0);
+        }
+    };
+
+    floatx16 acc[FM][FN];
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.0f;
+
+    issueA(0);
+    issueB(0);
+    if (NS > 1) issueB(1);
+    const int l32 = lane & 31, lh = lane >> 5;
+    const int bd_w = (wm * TM) / 256;                       // board of this wave's rows
+    const int q0 = (wm * TM) % 256;                          // first output row (15x17 grid) of the wave
+    for (int s = 0; s < NS; ++s) {
+        const int c = s / 3, r = s - c * 3;
+        // retire B(s) (and A(c) at r == 0): later pieces stay in flight
+        const bool nextB = s + 1 < NS;
+        const bool aAfter = r >= 1 && c + 1 < NCH;
+        if (nextB && aAfter) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PA + PB) : "memory");
+        else if (nextB) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PB) : "memory");
+        else if (aAfter) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PA) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        if (s + 2 < NS) issueB(s + 2);
+        if (r == 0 && c + 1 < NCH) issueA(c + 1);
+        const uint8_t* ab = abuf + (c & 1) * A_BUF + bd_w * NPL * A_PLANE;
+        const uint8_t* bb = bbuf + (s % 3) * B_STAGE;
+#pragma unroll
+        for (int t = 0; t < 3; ++t) {
+            const int shift = r * 17 + t;                       // (dy+1)*17 + (dx+1)
+            bf16x8 ah[FM], al[FM], bh[FN], bl[FN];
+#pragma unroll
+            for (int i = 0; i < FM; ++i) {
+                const int hr = q0 + i * 32 + l32 + shift;
+                const int off = lh * (V4_HROWS * 16) + hr * 16;
+                ah[i] = *reinterpret_cast<const bf16x8*>(ab + off);
+                al[i] = *reinterpret_cast<const bf16x8*>(ab + A_PLANE + off);
+            }
+#pragma unroll
+            for (int j = 0; j < FN; ++j) {
+                const int n = wn * 64 + j * 32 + l32;
+                const int off = t * B_TAP + lh * BNT * 16 + n * 16;
+                bh[j] = *reinterpret_cast<const bf16x8*>(bb + off);
+                bl[j] = *reinterpret_cast<const bf16x8*>(bb + 2 * BNT * 16 + off);
+            }
+#pragma unroll
+            for (int i = 0; i < FM; ++i)
+#pragma unroll
+                for (int j = 0; j < FN; ++j) {
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+                }
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __syncthreads();
+    // epilogue, one board (256 grid rows) at a time through LDS
+    float* ep = reinterpret_cast<float*>(lds);
+    for (int bd = 0; bd < BOARDS; ++bd) {
+        if (bd_w == bd) {
+#pragma unroll
+            for (int i = 0; i < FM; ++i)
+#pragma unroll
+                for (int j = 0; j < FN; ++j)
+#pragma unroll
+                    for (int e = 0; e < 16; ++e) {
+                        const int row = q0 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * lh;
+                        ep[row * EP_LD + wn * 64 + j * 32 + l32] = acc[i][j][e];
+                    }
+        }
+        __syncthreads();
+        const int b = b0 + bd;
+        constexpr int VPR = BNT / 8;
+        if (b < nboards) {
+            for (int v = tid; v < 225 * VPR; v += 512) {
+                const int pix = v / VPR, cv = (v % VPR) * 8;
+                const int y = pix / 15, x = pix - y * 15;
+                const int row = y * 17 + x;
+                const float4 x0 = *reinterpret_cast<const float4*>(ep + row * EP_LD + cv);
+                const float4 x1 = *reinterpret_cast<const float4*>(ep + row * EP_LD + cv + 4);
+                float o[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+                const int n = n0 + cv;
+                const size_t g = ((size_t)b * HW + pix) * p.N + n;
+                const float4 c0v = *reinterpret_cast<const float4*>(p.bias + n);
+                const float4 c1v = *reinterpret_cast<const float4*>(p.bias + n + 4);
+                const float bb[8] = {c0v.x, c0v.y, c0v.z, c0v.w, c1v.x, c1v.y, c1v.z, c1v.w};
+                uint16_t rh[8], rl[8];
+                if (p.Rhi) {
+                    *reinterpret_cast<uint4*>(rh) = *reinterpret_cast<const uint4*>(p.Rhi + g);
+                    *reinterpret_cast<uint4*>(rl) = *reinterpret_cast<const uint4*>(p.Rlo + g);
+                }
+                uint16_t oh[8], ol[8];
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    float val = o[e] + bb[e];
+                    if (p.Rhi) val += bf2f(rh[e]) + bf2f(rl[e]);
+                    if (p.relu) val = val > 0.0f ? val : 0.0f;
+                    o[e] = val;
+                    oh[e] = f2bf(val);
+                    ol[e] = f2bf(val - bf2f(oh[e]));
+                }
+                *reinterpret_cast<uint4*>(p.Chi + g) = *reinterpret_cast<const uint4*>(oh);
+                *reinterpret_cast<uint4*>(p.Clo + g) = *reinterpret_cast<const uint4*>(ol);
+                if (p.Cf) {
+                    *reinterpret_cast<float4*>(p.Cf + g) = make_float4(o[0], o[1], o[2], o[3]);
+                    *reinterpret_cast<float4*>(p.Cf + g + 4) = make_float4(o[4], o[5], o[6], o[7]);
+                }
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// variant selector: 0 = v1 (128x128, register staged), 1 = v2 (glds ring), 2 = v3
+static int g_conv_variant = 3;
+void az_conv_set_variant(int v) { g_conv_variant = v; }
+
+void az_conv_bf16_launch_v(const ConvBf16Args& a, bool split, hipStream_t st) {
+    if (g_conv_variant == 3 && split && a.H == 15 && a.W == 15 && a.N % 128 == 0 && a.C % 16 == 0 &&
+        a.rows_per_sample == 225) {
+        const int boards = a.M / 225;
+        const int grid = (boards + 1) / 2 * (a.N / 128);
+        hipLaunchKernelGGL((conv3x3_v4<128>), dim3(grid), dim3(512), 0, st, a);
+        return;
+    }
+    if (g_conv_variant >= 2 && a.N % 256 == 0 && a.C % 32 == 0) {
+        const int nbm = (a.M + 127) / 128, nbn = a.N / 256;
+        if (split) hipLaunchKernelGGL((conv3x3_v3<true, 128, 256, 2, 4>), dim3(nbm * nbn), dim3(512), 0, st, a);
+        else hipLaunchKernelGGL((conv3x3_v3<false, 128, 256, 2, 4>), dim3(nbm * nbn), dim3(512), 0, st, a);
+        return;
+    }
+    if (g_conv_variant >= 2 && a.N == 64 && a.C % 32 == 0) {
+        const int nbm = (a.M + 255) / 256;
+        if (split) hipLaunchKernelGGL((conv3x3_v3<true, 256, 64, 4, 1>), dim3(nbm), dim3(256), 0, st, a);
+        else hipLaunchKernelGGL((conv3x3_v3<false, 256, 64, 4, 1>), dim3(nbm), dim3(256), 0, st, a);
+        return;
+    }
+    if (g_conv_variant >= 1 && a.N % 256 == 0 && a.C % 32 == 0) {
+        const int nbm = (a.M + 127) / 128, nbn = a.N / 256;
+        if (split) hipLaunchKernelGGL((conv3x3_v2<true, 128, 256, 2, 4, 3>), dim3(nbm * nbn), dim3(512), 0, st, a);
+        else hipLaunchKernelGGL((conv3x3_v2<false, 128, 256, 2, 4, 4>), dim3(nbm * nbn), dim3(512), 0, st, a);
+        return;
+    }
+    if (g_conv_variant >= 1 && a.N == 64 && a.C % 32 == 0) {
+        const int nbm = (a.M + 255) / 256;
+        if (split) hipLaunchKernelGGL((conv3x3_v2<true, 256, 64, 4, 1, 3>), dim3(nbm), dim3(256), 0, st, a);
+        else hipLaunchKernelGGL((conv3x3_v2<false, 256, 64, 4, 1, 4>), dim3(nbm), dim3(256), 0, st, a);
+        return;
+    }
+    az_conv_bf16_launch(a, split, st);
 }

@@ -9,6 +9,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <random>
@@ -33,7 +34,8 @@ __global__ void k_new_games(TreeDev t, const int* games, int n, uint32_t eval_se
 __global__ void k_tt_clear(TreeDev t, const int* games, int n);
 __global__ void k_root_children(TreeDev t, int g, int* act, int* N, int* VL, float* W, float* P, int* n, int* rootinfo,
                                 float* rootW);
-void az_conv_bf16_launch(const ConvBf16Args& a, bool split, hipStream_t st);
+void az_conv_bf16_launch_v(const ConvBf16Args& a, bool split, hipStream_t st);
+void az_conv_set_variant(int v);
 void az_launch_split_bf16(const float* in, uint16_t* hi, uint16_t* lo, size_t n, const int* m_limit, int rows_per_sample,
                           int C, hipStream_t st);
 
@@ -104,6 +106,7 @@ struct az_net {
     float *pp = nullptr, *vp = nullptr, *v1 = nullptr, *logits = nullptr, *value = nullptr, *soft = nullptr;
     float* in_nchw = nullptr;
     int* d_nb = nullptr;
+    uint16_t* zero = nullptr;   // 256 zero bytes: glds source for the board edge
     bool loaded = false;
     // profiling: HIP events bracketing the 3x3 trunk of every forward (on the launch stream)
     bool prof = false;
@@ -275,7 +278,8 @@ int net_forward(az_net* n, const float* x0, int B, const int* nb, float* logits,
             a.Chi = n->th; a.Clo = split ? n->tl : nullptr; a.Cf = nullptr;
             a.bias = L1.b; a.Rhi = nullptr; a.Rlo = nullptr;
             a.M = rows; a.N = F; a.C = F; a.H = H; a.W = W; a.m_limit = nb; a.rows_per_sample = HW; a.relu = 1;
-            az_conv_bf16_launch(a, split, st);
+            a.zero = n->zero;
+            az_conv_bf16_launch_v(a, split, st);
             ConvBf16Args b2 = a;
             b2.Ahi = n->th; b2.Alo = split ? n->tl : nullptr;
             b2.Bhi = L2.Whi; b2.Blo = split ? L2.Wlo : nullptr;
@@ -283,7 +287,7 @@ int net_forward(az_net* n, const float* x0, int B, const int* nb, float* logits,
             b2.bias = L2.b;
             b2.Rhi = d.residual ? n->hh[cur] : nullptr; b2.Rlo = d.residual && split ? n->hl[cur] : nullptr;
             b2.Cf = (i == d.blocks - 1) ? other : nullptr;
-            az_conv_bf16_launch(b2, split, st);
+            az_conv_bf16_launch_v(b2, split, st);
             cur ^= 1;
         }
         if (d.blocks > 0) h = other;
@@ -555,6 +559,9 @@ int az_net_create(az_engine* e, const az_net_desc* d, az_net** out) {
     A_(&n->logits, B * d->action_size); A_(&n->value, B); A_(&n->soft, B * d->action_size);
     A_(&n->in_nchw, B * d->in_planes * n->HW);
     if (!r) r = dalloc(&n->d_nb, 1);
+    if (!r) r = dalloc(&n->zero, 128);
+    if (!r && hipMemset(n->zero, 0, 256) != hipSuccess) r = fail(AZ_ERR_HIP, "memset");
+    if (const char* v = getenv("AZ_CONV_VARIANT")) az_conv_set_variant(atoi(v));
     if (r) { az_net_destroy(n); return r; }
     *out = n;
     return 0;
@@ -569,7 +576,8 @@ void az_net_destroy(az_net* n) {
     for (Layer* l : ls) { F(l->W); F(l->b); F(l->Whi); F(l->Wlo); }
     for (void* p : {(void*)n->x0, (void*)n->h0, (void*)n->h1, (void*)n->t, (void*)n->pool, (void*)n->pp, (void*)n->vp,
                     (void*)n->v1, (void*)n->logits, (void*)n->value, (void*)n->soft, (void*)n->in_nchw, (void*)n->d_nb,
-                    (void*)n->hh[0], (void*)n->hh[1], (void*)n->hl[0], (void*)n->hl[1], (void*)n->th, (void*)n->tl})
+                    (void*)n->hh[0], (void*)n->hh[1], (void*)n->hl[0], (void*)n->hl[1], (void*)n->th, (void*)n->tl,
+                    (void*)n->zero})
         F(p);
     delete n;
 }

@@ -30,6 +30,7 @@ struct ConvBf16Args {
     int M, N, C, H, W;
     const int* m_limit; int rows_per_sample;
     int relu;
+    const uint16_t* zero;                       // >= 64 zero bytes (padding source for glds)
 };
 
 void az_launch_gemm_f32(const GemmArgs& p, int act, bool res, hipStream_t st);
