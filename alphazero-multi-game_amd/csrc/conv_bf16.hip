@@ -15,6 +15,7 @@
 // loads, one barrier per k-step.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <type_traits>
 #include "net.h"
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -602,36 +603,71 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void conv3x3_v3(ConvBf16Args p) {
 }
 
 // ===========================================================================
-// v4 (bf16x3): board-halo implicit GEMM.  A block owns TWO boards x 128 output
-// channels.  For every 16-channel chunk the zero-padded 17x17 input halo of both
-// boards is DMA'd (global_load_lds) into LDS once and read by all nine taps as
-// row-shifted windows: outputs live on a 15x17 grid (two dead columns) so that the
-// tap (dy,dx) operand of 32 consecutive outputs is 32 consecutive halo rows
-// (row shift (dy+1)*17 + (dx+1)).  Activation traffic drops ~9x and each weight
-// byte feeds two boards.  LDS images are chunk-major ([16-byte chunk][row]), which
-// keeps every ds_read_b128 lane group on 16 distinct bank slots for ANY row shift.
-// Pipeline: A halo double-buffered per chunk, weights for one tap row (3 taps) per
-// step in a 3-slot ring, counted vmcnt + one barrier per step.  MFMA 32x32x16 bf16.
+// v4: board-halo implicit GEMM for 15x15 boards (all trunk precisions).
+// A block owns TWO boards x BNT output channels.  For every 16-channel chunk the
+// zero-padded 17x17 input halo of both boards is DMA'd (global_load_lds) into LDS
+// once and read by all nine taps as row-shifted windows: outputs live on a 15x17
+// grid (two dead columns) so the tap (dy,dx) operand of 32 consecutive outputs is 32
+// consecutive halo rows (shift (dy+1)*17 + (dx+1)).  Activation traffic drops ~9x and
+// each weight byte feeds two boards.  LDS images are chunk-major ([16-byte chunk]
+// [row]), which keeps every ds_read_b128 lane group on 16 distinct bank slots for ANY
+// row shift.  Pipeline: A halo double-buffered per chunk, weights of one tap row
+// (3 taps) per step in a 3-slot ring, counted vmcnt + one barrier per step.
+//   MODE 0: bf16x3 (hi/lo planes, 3 MFMAs);  1: bf16;  2: fp16 (reference useFp16)
 constexpr int V4_HROWS = 320;                 // 17*17 = 289 halo rows, padded to 5 x 64
-template <int BNT>
+
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ void wait_vm(int n) {      // s_waitcnt vmcnt(n), n wave-uniform
+    switch (n) {
+        case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+        case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+        case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+        case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+        case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+        case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+        case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+        case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
+        case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+        case 9: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
+        case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
+        case 11: asm volatile("s_waitcnt vmcnt(11)" ::: "memory"); break;
+        default: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+    }
+}
+
+template <int MODE>
+__device__ __forceinline__ float v4_load(uint16_t h) {
+    if (MODE == 2) { _Float16 x; __builtin_memcpy(&x, &h, 2); return (float)x; }
+    return bf2f(h);
+}
+template <int MODE>
+__device__ __forceinline__ uint16_t v4_store(float f) {
+    if (MODE == 2) { _Float16 x = (_Float16)f; uint16_t h; __builtin_memcpy(&h, &x, 2); return h; }
+    return f2bf(f);
+}
+
+template <int MODE, int BNT>
 __global__ __launch_bounds__(512, 1) void conv3x3_v4(ConvBf16Args p) {
-    constexpr int NPL = 2;                    // hi, lo
+    constexpr bool SPLIT = MODE == 0;
+    constexpr int NPL = SPLIT ? 2 : 1;
     constexpr int BOARDS = 2;
     constexpr int A_PLANE = 2 * V4_HROWS * 16;             // one board, one plane, 16 channels: 10 KB
-    constexpr int A_BUF = BOARDS * NPL * A_PLANE;          // 40 KB
-    constexpr int B_TAP = NPL * 2 * BNT * 16;              // one tap, both planes: 8 KB (BNT=128)
-    constexpr int B_STAGE = 3 * B_TAP;                     // one tap row: 24 KB
-    constexpr int LDS_MAIN = 2 * A_BUF + 3 * B_STAGE;      // 152 KB
+    constexpr int A_BUF = BOARDS * NPL * A_PLANE;
+    constexpr int B_TAP = NPL * 2 * BNT * 16;
+    constexpr int B_STAGE = 3 * B_TAP;
+    constexpr int LDS_MAIN = 2 * A_BUF + 3 * B_STAGE;
     constexpr int EP_LD = BNT + 4;
     constexpr int LDS_EPI = 256 * EP_LD * 4;
     constexpr int LDS = LDS_MAIN > LDS_EPI ? LDS_MAIN : LDS_EPI;
-    constexpr int PA = (BOARDS * NPL * 2 * (V4_HROWS / 64)) / 8;   // A pieces per wave per chunk (5)
-    constexpr int PB = (3 * NPL * 2 * (BNT / 64)) / 8;             // B pieces per wave per step (3)
-    static_assert((BOARDS * NPL * 2 * (V4_HROWS / 64)) % 8 == 0 && (3 * NPL * 2 * (BNT / 64)) % 8 == 0, "pieces");
-    constexpr int WN = BNT / 64;              // waves along N (2 for 128 channels)
-    constexpr int WM = 8 / WN;                // waves along M (4): 512 output rows / WM
-    constexpr int TM = 512 / WM;              // 128 rows per wave
-    constexpr int FM = TM / 32, FN = 2;       // 32x32 tiles per wave
+    constexpr int A_INS = BOARDS * NPL * 2 * (V4_HROWS / 64);   // 1 KiB pieces per A chunk
+    constexpr int B_INS = 3 * NPL * 2 * (BNT / 64);             // per step
+    constexpr int PAX = (A_INS + 7) / 8, PBX = (B_INS + 7) / 8;
+    constexpr int WN = BNT >= 128 ? BNT / 64 : 1;
+    constexpr int WM = 8 / WN;
+    constexpr int TM = 512 / WM;
+    constexpr int FM = TM / 32, FN = BNT / WN / 32;
+    typedef typename std::conditional<MODE == 2, f16x8, bf16x8>::type frag;
     __shared__ __attribute__((aligned(16))) uint8_t lds[LDS];
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -642,37 +678,35 @@ __global__ __launch_bounds__(512, 1) void conv3x3_v4(ConvBf16Args p) {
     const int nboards = p.m_limit ? *p.m_limit : p.M / (p.H * p.W);
     const int b0 = pair * BOARDS;
     if (b0 >= nboards) return;
-    const int C = p.C, HW = p.H * p.W, K = 9 * C;   // 15x15 boards (H = W = 15)
+    const int C = p.C, HW = p.H * p.W, K = 9 * C;
     const int NCH = C / 16, NS = NCH * 3;
+    const int PA = (A_INS - wave + 7) / 8, PB = (B_INS - wave + 7) / 8;   // this wave's pieces
 
-    // A pieces of this wave: index q = wave + 8*j over (board, plane, chunk, rowblock)
-    const uint16_t* a_src[PA];   // pixel base (channel 0) or null for padding rows
-    int a_ch[PA];
-    int a_off[PA];
+    const uint16_t* a_src[PAX];
+    int a_ch[PAX], a_off[PAX];
 #pragma unroll
-    for (int j = 0; j < PA; ++j) {
+    for (int j = 0; j < PAX; ++j) {
         const int q = wave + 8 * j;
-        const int rb = q % 5, ch = (q / 5) % 2, plane = (q / 10) % 2, bd = q / 20;
+        const int rb = q % 5, ch = (q / 5) % 2, plane = (q / 10) % NPL, bd = q / (10 * NPL);
         const int hr = rb * 64 + lane;
         const int Y = hr / 17, X = hr - Y * 17;
         const int b = b0 + bd;
-        const bool ok = hr < 289 && Y >= 1 && Y <= 15 && X >= 1 && X <= 15 && b < nboards;
+        const bool ok = q < A_INS && hr < 289 && Y >= 1 && Y <= 15 && X >= 1 && X <= 15 && b < nboards;
         const uint16_t* base = plane ? p.Alo : p.Ahi;
         a_src[j] = ok ? base + ((size_t)b * HW + (Y - 1) * 15 + (X - 1)) * C + ch * 8 : nullptr;
         a_ch[j] = ch;
         a_off[j] = (bd * NPL + plane) * A_PLANE + ch * (V4_HROWS * 16) + rb * 1024;
     }
-    // B pieces: q over (tap 0..2, plane, chunk, rowblock)
-    const uint16_t* b_src[PB];
-    int b_off[PB];
+    const uint16_t* b_src[PBX];
+    int b_off[PBX];
 #pragma unroll
-    for (int j = 0; j < PB; ++j) {
-        const int q = wave + 8 * j;
-        const int RB = BNT / 64;
-        const int rb = q % RB, ch = (q / RB) % 2, plane = (q / (2 * RB)) % 2, t = q / (4 * RB);
+    for (int j = 0; j < PBX; ++j) {
+        const int q = min(wave + 8 * j, B_INS - 1);
+        constexpr int RB = BNT / 64;
+        const int rb = q % RB, ch = (q / RB) % 2, plane = (q / (2 * RB)) % NPL, t = q / (2 * RB * NPL);
         const int n = n0 + rb * 64 + lane;
         const uint16_t* base = plane ? p.Blo : p.Bhi;
-        b_src[j] = base + (size_t)n * K + t * C + ch * 8;        // + dyrow*3*C + chunk*16 at issue
+        b_src[j] = base + (size_t)n * K + t * C + ch * 8;
         b_off[j] = t * B_TAP + (plane * 2 + ch) * BNT * 16 + rb * 1024;
     }
     uint8_t* abuf = lds;
@@ -680,7 +714,8 @@ __global__ __launch_bounds__(512, 1) void conv3x3_v4(ConvBf16Args p) {
     auto issueA = [&](int c) {
         uint8_t* dst = abuf + (c & 1) * A_BUF;
 #pragma unroll
-        for (int j = 0; j < PA; ++j) {
+        for (int j = 0; j < PAX; ++j) {
+            if (j >= PA) break;
             const uint16_t* src = a_src[j] ? a_src[j] + c * 16 : p.zero + a_ch[j] * 8;
             __builtin_amdgcn_global_load_lds((g_void_t*)src, (lds_void_t*)(dst + a_off[j]), 16, 0, 0);
         }
@@ -689,7 +724,8 @@ __global__ __launch_bounds__(512, 1) void conv3x3_v4(ConvBf16Args p) {
         const int c = s / 3, r = s - c * 3;
         uint8_t* dst = bbuf + (s % 3) * B_STAGE;
 #pragma unroll
-        for (int j = 0; j < PB; ++j) {
+        for (int j = 0; j < PBX; ++j) {
+            if (j >= PB) break;
             const uint16_t* src = b_src[j] + r * 3 * C + c * 16;
             __builtin_amdgcn_global_load_lds((g_void_t*)src, (lds_void_t*)(dst + b_off[j]), 16, 0, 0);
         }
@@ -707,17 +743,12 @@ __global__ __launch_bounds__(512, 1) void conv3x3_v4(ConvBf16Args p) {
     issueB(0);
     if (NS > 1) issueB(1);
     const int l32 = lane & 31, lh = lane >> 5;
-    const int bd_w = (wm * TM) / 256;                       // board of this wave's rows
-    const int q0 = (wm * TM) % 256;                          // first output row (15x17 grid) of the wave
+    const int bd_w = (wm * TM) / 256;
+    const int q0 = (wm * TM) % 256;
     for (int s = 0; s < NS; ++s) {
         const int c = s / 3, r = s - c * 3;
-        // retire B(s) (and A(c) at r == 0): later pieces stay in flight
-        const bool nextB = s + 1 < NS;
-        const bool aAfter = r >= 1 && c + 1 < NCH;
-        if (nextB && aAfter) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PA + PB) : "memory");
-        else if (nextB) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PB) : "memory");
-        else if (aAfter) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PA) : "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        // retire B(s) (and A(c) at r == 0); later pieces stay in flight
+        wait_vm((s + 1 < NS ? PB : 0) + ((r >= 1 && c + 1 < NCH) ? PA : 0));
         __builtin_amdgcn_sched_barrier(0);
         __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_sched_barrier(0);
@@ -727,35 +758,40 @@ __global__ __launch_bounds__(512, 1) void conv3x3_v4(ConvBf16Args p) {
         const uint8_t* bb = bbuf + (s % 3) * B_STAGE;
 #pragma unroll
         for (int t = 0; t < 3; ++t) {
-            const int shift = r * 17 + t;                       // (dy+1)*17 + (dx+1)
-            bf16x8 ah[FM], al[FM], bh[FN], bl[FN];
+            const int shift = r * 17 + t;
+            frag ah[FM], al[FM], bh[FN], bl[FN];
 #pragma unroll
             for (int i = 0; i < FM; ++i) {
                 const int hr = q0 + i * 32 + l32 + shift;
                 const int off = lh * (V4_HROWS * 16) + hr * 16;
-                ah[i] = *reinterpret_cast<const bf16x8*>(ab + off);
-                al[i] = *reinterpret_cast<const bf16x8*>(ab + A_PLANE + off);
+                ah[i] = *reinterpret_cast<const frag*>(ab + off);
+                if (SPLIT) al[i] = *reinterpret_cast<const frag*>(ab + A_PLANE + off);
             }
 #pragma unroll
             for (int j = 0; j < FN; ++j) {
-                const int n = wn * 64 + j * 32 + l32;
+                const int n = wn * (BNT / WN) + j * 32 + l32;
                 const int off = t * B_TAP + lh * BNT * 16 + n * 16;
-                bh[j] = *reinterpret_cast<const bf16x8*>(bb + off);
-                bl[j] = *reinterpret_cast<const bf16x8*>(bb + 2 * BNT * 16 + off);
+                bh[j] = *reinterpret_cast<const frag*>(bb + off);
+                if (SPLIT) bl[j] = *reinterpret_cast<const frag*>(bb + 2 * BNT * 16 + off);
             }
 #pragma unroll
             for (int i = 0; i < FM; ++i)
 #pragma unroll
                 for (int j = 0; j < FN; ++j) {
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+                    if constexpr (MODE == 2) {
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+                    } else {
+                        if (SPLIT) {
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+                        }
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+                    }
                 }
         }
     }
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __syncthreads();
-    // epilogue, one board (256 grid rows) at a time through LDS
     float* ep = reinterpret_cast<float*>(lds);
     for (int bd = 0; bd < BOARDS; ++bd) {
         if (bd_w == bd) {
@@ -766,7 +802,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_v4(ConvBf16Args p) {
 #pragma unroll
                     for (int e = 0; e < 16; ++e) {
                         const int row = q0 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * lh;
-                        ep[row * EP_LD + wn * 64 + j * 32 + l32] = acc[i][j][e];
+                        ep[row * EP_LD + wn * (BNT / WN) + j * 32 + l32] = acc[i][j][e];
                     }
         }
         __syncthreads();
@@ -786,22 +822,28 @@ __global__ __launch_bounds__(512, 1) void conv3x3_v4(ConvBf16Args p) {
                 const float4 c1v = *reinterpret_cast<const float4*>(p.bias + n + 4);
                 const float bb[8] = {c0v.x, c0v.y, c0v.z, c0v.w, c1v.x, c1v.y, c1v.z, c1v.w};
                 uint16_t rh[8], rl[8];
+                float rf[8];
+                if (p.Rf) {
+                    *reinterpret_cast<float4*>(rf) = *reinterpret_cast<const float4*>(p.Rf + g);
+                    *reinterpret_cast<float4*>(rf + 4) = *reinterpret_cast<const float4*>(p.Rf + g + 4);
+                }
                 if (p.Rhi) {
                     *reinterpret_cast<uint4*>(rh) = *reinterpret_cast<const uint4*>(p.Rhi + g);
-                    *reinterpret_cast<uint4*>(rl) = *reinterpret_cast<const uint4*>(p.Rlo + g);
+                    if (SPLIT) *reinterpret_cast<uint4*>(rl) = *reinterpret_cast<const uint4*>(p.Rlo + g);
                 }
                 uint16_t oh[8], ol[8];
 #pragma unroll
                 for (int e = 0; e < 8; ++e) {
                     float val = o[e] + bb[e];
-                    if (p.Rhi) val += bf2f(rh[e]) + bf2f(rl[e]);
+                    if (p.Rf) val += rf[e];
+                    else if (p.Rhi) val += v4_load<MODE>(rh[e]) + (SPLIT ? bf2f(rl[e]) : 0.0f);
                     if (p.relu) val = val > 0.0f ? val : 0.0f;
                     o[e] = val;
-                    oh[e] = f2bf(val);
-                    ol[e] = f2bf(val - bf2f(oh[e]));
+                    oh[e] = v4_store<MODE>(val);
+                    if (SPLIT) ol[e] = f2bf(val - bf2f(oh[e]));
                 }
                 *reinterpret_cast<uint4*>(p.Chi + g) = *reinterpret_cast<const uint4*>(oh);
-                *reinterpret_cast<uint4*>(p.Clo + g) = *reinterpret_cast<const uint4*>(ol);
+                if (SPLIT) *reinterpret_cast<uint4*>(p.Clo + g) = *reinterpret_cast<const uint4*>(ol);
                 if (p.Cf) {
                     *reinterpret_cast<float4*>(p.Cf + g) = make_float4(o[0], o[1], o[2], o[3]);
                     *reinterpret_cast<float4*>(p.Cf + g + 4) = make_float4(o[4], o[5], o[6], o[7]);
@@ -812,16 +854,43 @@ __global__ __launch_bounds__(512, 1) void conv3x3_v4(ConvBf16Args p) {
     }
 }
 
+// fp32 -> fp16 activations (first trunk input, AZ_PREC_FP16)
+__global__ void k_to_f16(const float* in, uint16_t* out, size_t n, const int* m_limit, int rows_per_sample, int C) {
+    size_t lim = n;
+    if (m_limit) lim = min(n, (size_t)(*m_limit) * rows_per_sample * C);
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < lim; i += (size_t)gridDim.x * blockDim.x)
+        out[i] = v4_store<2>(in[i]);
+}
+void az_launch_to_f16(const float* in, uint16_t* out, size_t n, const int* m_limit, int rows_per_sample, int C,
+                      hipStream_t st) {
+    hipLaunchKernelGGL(k_to_f16, dim3(2048), dim3(256), 0, st, in, out, n, m_limit, rows_per_sample, C);
+}
+
+// true when conv3x3_v4 handles this shape
+bool az_conv_v4_supported(int H, int W, int C, int N) { return H == 15 && W == 15 && C % 16 == 0 && N % 64 == 0; }
+
+void az_conv_v4_launch(const ConvBf16Args& a, int mode, hipStream_t st) {
+    const int boards = a.M / 225;
+    const int bnt = a.N % 128 == 0 ? 128 : 64;
+    const int grid = (boards + 1) / 2 * (a.N / bnt);
+    if (bnt == 128) {
+        if (mode == 0) hipLaunchKernelGGL((conv3x3_v4<0, 128>), dim3(grid), dim3(512), 0, st, a);
+        else if (mode == 1) hipLaunchKernelGGL((conv3x3_v4<1, 128>), dim3(grid), dim3(512), 0, st, a);
+        else hipLaunchKernelGGL((conv3x3_v4<2, 128>), dim3(grid), dim3(512), 0, st, a);
+    } else {
+        if (mode == 0) hipLaunchKernelGGL((conv3x3_v4<0, 64>), dim3(grid), dim3(512), 0, st, a);
+        else if (mode == 1) hipLaunchKernelGGL((conv3x3_v4<1, 64>), dim3(grid), dim3(512), 0, st, a);
+        else hipLaunchKernelGGL((conv3x3_v4<2, 64>), dim3(grid), dim3(512), 0, st, a);
+    }
+}
+
 // variant selector: 0 = v1 (128x128, register staged), 1 = v2 (glds ring), 2 = v3
 static int g_conv_variant = 3;
 void az_conv_set_variant(int v) { g_conv_variant = v; }
 
 void az_conv_bf16_launch_v(const ConvBf16Args& a, bool split, hipStream_t st) {
-    if (g_conv_variant == 3 && split && a.H == 15 && a.W == 15 && a.N % 128 == 0 && a.C % 16 == 0 &&
-        a.rows_per_sample == 225) {
-        const int boards = a.M / 225;
-        const int grid = (boards + 1) / 2 * (a.N / 128);
-        hipLaunchKernelGGL((conv3x3_v4<128>), dim3(grid), dim3(512), 0, st, a);
+    if (g_conv_variant == 3 && a.rows_per_sample == 225 && az_conv_v4_supported(a.H, a.W, a.C, a.N)) {
+        az_conv_v4_launch(a, split ? 0 : 1, st);
         return;
     }
     if (g_conv_variant >= 2 && a.N % 256 == 0 && a.C % 32 == 0) {

@@ -36,6 +36,10 @@ __global__ void k_root_children(TreeDev t, int g, int* act, int* N, int* VL, flo
                                 float* rootW);
 void az_conv_bf16_launch_v(const ConvBf16Args& a, bool split, hipStream_t st);
 void az_conv_set_variant(int v);
+bool az_conv_v4_supported(int H, int W, int C, int N);
+void az_conv_v4_launch(const ConvBf16Args& a, int mode, hipStream_t st);
+void az_launch_to_f16(const float* in, uint16_t* out, size_t n, const int* m_limit, int rows_per_sample, int C,
+                      hipStream_t st);
 void az_launch_split_bf16(const float* in, uint16_t* hi, uint16_t* lo, size_t n, const int* m_limit, int rows_per_sample,
                           int C, hipStream_t st);
 
@@ -88,6 +92,7 @@ struct az_engine {
 struct Layer {            // one implicit-GEMM layer, BN folded
     float* W = nullptr;   // [N][K] fp32
     uint16_t* Whi = nullptr; uint16_t* Wlo = nullptr;   // bf16 split copies (3x3 trunk)
+    uint16_t* Wh16 = nullptr;                           // fp16 copy (3x3 trunk, AZ_PREC_FP16)
     float* b = nullptr;   // [N]
     int N = 0, K = 0, Kpad = 0, taps = 1, C = 0;
 };
@@ -177,6 +182,10 @@ int upload_layer(Layer& L, const std::vector<float>& W, const std::vector<float>
         if (!L.Whi) { DALLOC(L.Whi, W.size()); DALLOC(L.Wlo, W.size()); }
         HIPCHK(hipMemcpy(L.Whi, hi.data(), hi.size() * 2, hipMemcpyHostToDevice));
         HIPCHK(hipMemcpy(L.Wlo, lo.data(), lo.size() * 2, hipMemcpyHostToDevice));
+        std::vector<uint16_t> h16(W.size());
+        for (size_t i = 0; i < W.size(); ++i) { _Float16 h = (_Float16)W[i]; std::memcpy(&h16[i], &h, 2); }
+        if (!L.Wh16) DALLOC(L.Wh16, W.size());
+        HIPCHK(hipMemcpy(L.Wh16, h16.data(), h16.size() * 2, hipMemcpyHostToDevice));
     }
     return 0;
 }
@@ -241,7 +250,8 @@ int net_forward(az_net* n, const float* x0, int B, const int* nb, float* logits,
     const int H = d.board_size, W = d.board_size, HW = n->HW, F = d.channels, P = d.pool, PP = n->P2;
     const int rows = B * HW;
     const int prec = d.precision;
-    const bool bf = (prec == AZ_PREC_BF16X3 || prec == AZ_PREC_BF16) && F % 32 == 0;
+    const bool bf = (prec == AZ_PREC_BF16X3 || prec == AZ_PREC_BF16 || prec == AZ_PREC_FP16) && F % 32 == 0;
+    const bool f16 = prec == AZ_PREC_FP16;
     az_launch_gemm_f32(gemm_args(n->in, x0, n->cin_pad, n->h0, F, nullptr, rows, H, W, nb, HW), ACT_RELU, false, st);
     float* h = n->h0;
     float* other = n->h1;
@@ -267,7 +277,8 @@ int net_forward(az_net* n, const float* x0, int B, const int* nb, float* logits,
         }
     } else {
         const bool split = prec == AZ_PREC_BF16X3;
-        az_launch_split_bf16(h, n->hh[0], split ? n->hl[0] : nullptr, (size_t)rows * F, nb, HW, F, st);
+        if (f16) az_launch_to_f16(h, n->hh[0], (size_t)rows * F, nb, HW, F, st);
+        else az_launch_split_bf16(h, n->hh[0], split ? n->hl[0] : nullptr, (size_t)rows * F, nb, HW, F, st);
         int cur = 0;
         for (int i = 0; i < d.blocks; ++i) {
             const Layer& L1 = n->blk[2 * i];
@@ -279,7 +290,9 @@ int net_forward(az_net* n, const float* x0, int B, const int* nb, float* logits,
             a.bias = L1.b; a.Rhi = nullptr; a.Rlo = nullptr;
             a.M = rows; a.N = F; a.C = F; a.H = H; a.W = W; a.m_limit = nb; a.rows_per_sample = HW; a.relu = 1;
             a.zero = n->zero;
-            az_conv_bf16_launch_v(a, split, st);
+            if (f16) a.Bhi = L1.Wh16;
+            if (f16) az_conv_v4_launch(a, 2, st);
+            else az_conv_bf16_launch_v(a, split, st);
             ConvBf16Args b2 = a;
             b2.Ahi = n->th; b2.Alo = split ? n->tl : nullptr;
             b2.Bhi = L2.Whi; b2.Blo = split ? L2.Wlo : nullptr;
@@ -287,10 +300,20 @@ int net_forward(az_net* n, const float* x0, int B, const int* nb, float* logits,
             b2.bias = L2.b;
             b2.Rhi = d.residual ? n->hh[cur] : nullptr; b2.Rlo = d.residual && split ? n->hl[cur] : nullptr;
             b2.Cf = (i == d.blocks - 1) ? other : nullptr;
-            az_conv_bf16_launch_v(b2, split, st);
+            if (f16) {
+                // fp16 conv operands, fp32 residual stream (an fp16 stream doubles the logit error)
+                b2.Bhi = L2.Wh16;
+                b2.Rhi = nullptr;
+                b2.Rf = d.residual ? h : nullptr;
+                b2.Cf = other;
+                az_conv_v4_launch(b2, 2, st);
+                std::swap(h, other);
+            } else {
+                az_conv_bf16_launch_v(b2, split, st);
+            }
             cur ^= 1;
         }
-        if (d.blocks > 0) h = other;
+        if (d.blocks > 0 && !f16) h = other;
     }
     if (ev1) HIPCHK(hipEventRecord(ev1, st));
     az_launch_pool(h, n->pool, B, H, W, F, P, nb, st);
@@ -528,6 +551,14 @@ int az_engine_device_name(az_engine* e, char* buf, int len) {
 }
 
 // ------------------------------------------------------------------ net
+static int check_precision(const az_net_desc& d, int precision) {
+    if (precision < 0 || precision > 3) return fail(AZ_ERR_ARG, "bad precision %d", precision);
+    if (precision != AZ_PREC_F32 && d.channels % 32) return fail(AZ_ERR_ARG, "bf16/fp16 trunk needs channels %% 32 == 0");
+    if (precision == AZ_PREC_FP16 && !az_conv_v4_supported(d.board_size, d.board_size, d.channels, d.channels))
+        return fail(AZ_ERR_ARG, "AZ_PREC_FP16 trunk needs 15x15 boards and channels %% 64 == 0");
+    return 0;
+}
+
 int az_net_create(az_engine* e, const az_net_desc* d, az_net** out) {
     if (!e || !d || !out) return fail(AZ_ERR_ARG, "null argument");
     if (d->board_size < 2 || d->board_size * d->board_size > AZ_MAXA || d->in_planes < 1 || d->in_planes > 16 ||
@@ -535,6 +566,7 @@ int az_net_create(az_engine* e, const az_net_desc* d, az_net** out) {
         d->head_channels < 1 || d->head_channels % 4 || d->pool < 1 || d->fc_hidden < 1 || d->fc_hidden % 4 ||
         d->max_batch < 1)
         return fail(AZ_ERR_ARG, "unsupported network description");
+    if (int r = check_precision(*d, d->precision)) return r;
     std::lock_guard<std::mutex> lk(e->mu);
     HIPCHK(hipSetDevice(e->device));
     auto* n = new az_net();
@@ -573,7 +605,7 @@ void az_net_destroy(az_net* n) {
     auto F = [](void* p) { if (p) hipFree(p); };
     std::vector<Layer*> ls = {&n->in, &n->pconv, &n->vconv, &n->pfc, &n->vfc1, &n->vfc2};
     for (auto& l : n->blk) ls.push_back(&l);
-    for (Layer* l : ls) { F(l->W); F(l->b); F(l->Whi); F(l->Wlo); }
+    for (Layer* l : ls) { F(l->W); F(l->b); F(l->Whi); F(l->Wlo); F(l->Wh16); }
     for (void* p : {(void*)n->x0, (void*)n->h0, (void*)n->h1, (void*)n->t, (void*)n->pool, (void*)n->pp, (void*)n->vp,
                     (void*)n->v1, (void*)n->logits, (void*)n->value, (void*)n->soft, (void*)n->in_nchw, (void*)n->d_nb,
                     (void*)n->hh[0], (void*)n->hh[1], (void*)n->hl[0], (void*)n->hl[1], (void*)n->th, (void*)n->tl,
@@ -640,8 +672,8 @@ int az_net_init_random(az_net* n, uint64_t seed) {
 }
 
 int az_net_set_precision(az_net* n, int precision) {
-    if (!n || precision < 0 || precision > 2) return fail(AZ_ERR_ARG, "bad precision");
-    if (precision != AZ_PREC_F32 && n->d.channels % 32) return fail(AZ_ERR_ARG, "bf16 trunk needs channels %% 32 == 0");
+    if (!n) return fail(AZ_ERR_ARG, "null net");
+    if (int r = check_precision(n->d, precision)) return r;
     n->d.precision = precision;
     return 0;
 }

@@ -27,6 +27,7 @@ struct ConvBf16Args {
     float* Cf;                                  // optional fp32 output [rows][N]
     const float* bias;
     const uint16_t* Rhi; const uint16_t* Rlo;   // residual (split) or null
+    const float* Rf;                            // fp32 residual [rows][N] (v4 only; AZ_PREC_FP16)
     int M, N, C, H, W;
     const int* m_limit; int rows_per_sample;
     int relu;

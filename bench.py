@@ -26,8 +26,8 @@ for _p in (os.path.join(ROOT, "alphazero-multi-game_amd"), os.path.join(ROOT, "o
 import numpy as np  # noqa: E402
 
 METRIC = "self-play positions/sec (+ NN evals/sec) at 800 sims/move, 1/2/4/8 GPU"
-PEAK_TFLOPS = {"bf16x3": 2500.0, "bf16": 2500.0, "f32": 157.3}   # dense MFMA peaks, MI355X_MICROARCH.md
-PREC = {"f32": 0, "bf16x3": 1, "bf16": 2}
+PEAK_TFLOPS = {"bf16x3": 2500.0, "bf16": 2500.0, "fp16": 2500.0, "f32": 157.3}   # dense MFMA peaks, MI355X_MICROARCH.md
+PREC = {"f32": 0, "bf16x3": 1, "bf16": 2, "fp16": 3}
 
 
 def parse():

@@ -58,7 +58,9 @@ int az_engine_device_name(az_engine* e, char* buf, int len);
 enum az_precision {
     AZ_PREC_F32 = 0,    /* fp32 operands, f32-input MFMA (exact f32 products)              */
     AZ_PREC_BF16X3 = 1, /* fp32 split into bf16 hi+lo, 3 bf16 MFMAs per product (~2^-16)   */
-    AZ_PREC_BF16 = 2    /* plain bf16 operands, fp32 accumulate (throughput only)          */
+    AZ_PREC_BF16 = 2,   /* plain bf16 operands, fp32 accumulate (throughput only)          */
+    AZ_PREC_FP16 = 3    /* fp16 operands, fp32 accumulate: TorchNeuralNetworkConfig::useFp16
+                           (include/alphazero/nn/torch_neural_network.h:29); 15x15, F%64==0   */
 };
 typedef struct az_net_desc {
     int board_size;     /* H = W */

@@ -39,15 +39,17 @@ CASES = [  # (board, channels, blocks, residual, conv_bias, B)
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("prec", ["f32", "bf16x3"])
+@pytest.mark.parametrize("prec", ["f32", "bf16x3", "fp16"])
 @pytest.mark.parametrize("case", CASES, ids=[str(c) for c in CASES])
 def test_gpu_net_matches_fp32_reference(engine, case, prec):
     import az_amd
     import net_oracle
     bs, ch, blocks, res, bias, B = case
-    p = {"f32": az_amd.AZ_PREC_F32, "bf16x3": az_amd.AZ_PREC_BF16X3}[prec]
+    p = {"f32": az_amd.AZ_PREC_F32, "bf16x3": az_amd.AZ_PREC_BF16X3, "fp16": az_amd.AZ_PREC_FP16}[prec]
     if p != az_amd.AZ_PREC_F32 and ch % 32:
         pytest.skip("bf16 trunk needs channels % 32 == 0")
+    if p == az_amd.AZ_PREC_FP16 and (bs != 15 or ch % 64):
+        pytest.skip("fp16 trunk: 15x15 boards, channels % 64 == 0")
     desc = az_amd.gomoku_net_desc(board_size=bs, channels=ch, blocks=blocks, residual=res, conv_bias=bias,
                                   precision=p, max_batch=B)
     net = az_amd.HipNeuralNetwork(engine, desc)
@@ -118,3 +120,24 @@ def test_gpu_net_init_random_matches_numpy(engine):
     assert np.array_equal(la, lb) and np.array_equal(va, vb)
     a.close()
     b.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("prec", ["bf16x3", "fp16"])
+def test_gpu_c3_net_error_over_many_positions(engine, prec):
+    """The C3 net (20 blocks x 256 filters) on 96 random positions: every logit and value
+    within 1e-4 of the fp32 reference (the bench precisions)."""
+    import az_amd
+    import net_oracle
+    p = {"bf16x3": az_amd.AZ_PREC_BF16X3, "fp16": az_amd.AZ_PREC_FP16}[prec]
+    desc = az_amd.gomoku_net_desc(board_size=15, channels=256, blocks=20, precision=p, max_batch=96)
+    net = az_amd.HipNeuralNetwork(engine, desc)
+    blob = net_oracle.init_blob(desc, seed=1234)      # bench.py's weights
+    net.load_weights(blob)
+    x = _planes(96, 15, seed=7)
+    lo, v = net.forward(x)
+    rl, rv = net_oracle.forward(desc, blob, x)
+    el, ev = float(np.abs(lo - rl).max()), float(np.abs(v - rv).max())
+    print(f"C3 {prec}: max|dlogit|={el:.3e} max|dvalue|={ev:.3e} (|logit|max {np.abs(rl).max():.3f})")
+    assert el <= TOL and ev <= TOL
+    net.close()
