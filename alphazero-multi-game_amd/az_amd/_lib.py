@@ -5,7 +5,7 @@ import ctypes
 import os
 
 PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG, "build", "libaz_hip.so")
+LIB_PATH = os.environ.get("AZ_HIP_LIB") or os.path.join(PKG, "build", "libaz_hip.so")  # override: diagnostic builds
 
 c_int, c_float, c_size_t, c_uint32, c_uint64, c_int64 = (ctypes.c_int, ctypes.c_float, ctypes.c_size_t,
                                                           ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int64)

@@ -647,7 +647,21 @@ __device__ __forceinline__ uint16_t v4_store(float f) {
     return f2bf(f);
 }
 
-template <int MODE, int BNT>
+#ifdef AZ_V4_STAMPS
+// diagnostic build only: per-block s_memrealtime (100 MHz) at start / end of main loop / end,
+// slot p.stamp (the engine numbers the trunk launches of a forward 0..2*blocks-1)
+constexpr int V4_SLOTS = 48, V4_MAXBLK = 4096;
+__device__ unsigned long long g_v4_stamps[V4_SLOTS * V4_MAXBLK * 4];
+#define V4_STAMP(k) do { if (threadIdx.x == 0 && blockIdx.x < V4_MAXBLK && p.stamp >= 0 && p.stamp < V4_SLOTS) \
+    g_v4_stamps[((size_t)p.stamp * V4_MAXBLK + blockIdx.x) * 4 + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+extern "C" int az_diag_v4_stamps(unsigned long long* out, int n) {
+    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_v4_stamps), sizeof(unsigned long long) * (size_t)n);
+}
+#else
+#define V4_STAMP(k) do { } while (0)
+#endif
+
+template <int MODE, int BNT, int SCHED>
 __global__ __launch_bounds__(512, 1) void conv3x3_v4(ConvBf16Args p) {
     constexpr bool SPLIT = MODE == 0;
     constexpr int NPL = SPLIT ? 2 : 1;
@@ -670,6 +684,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_v4(ConvBf16Args p) {
     typedef typename std::conditional<MODE == 2, f16x8, bf16x8>::type frag;
     __shared__ __attribute__((aligned(16))) uint8_t lds[LDS];
 
+    V4_STAMP(0);
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm = wave / WN, wn = wave % WN;
     const int nsplit = p.N / BNT;
@@ -756,10 +771,9 @@ __global__ __launch_bounds__(512, 1) void conv3x3_v4(ConvBf16Args p) {
         if (r == 0 && c + 1 < NCH) issueA(c + 1);
         const uint8_t* ab = abuf + (c & 1) * A_BUF + bd_w * NPL * A_PLANE;
         const uint8_t* bb = bbuf + (s % 3) * B_STAGE;
-#pragma unroll
-        for (int t = 0; t < 3; ++t) {
+        // fragments of tap t: A rows shifted by r*17 + t, B tap slot t
+        auto load = [&](int t, frag (&ah)[FM], frag (&al)[FM], frag (&bh)[FN], frag (&bl)[FN]) {
             const int shift = r * 17 + t;
-            frag ah[FM], al[FM], bh[FN], bl[FN];
 #pragma unroll
             for (int i = 0; i < FM; ++i) {
                 const int hr = q0 + i * 32 + l32 + shift;
@@ -774,6 +788,8 @@ __global__ __launch_bounds__(512, 1) void conv3x3_v4(ConvBf16Args p) {
                 bh[j] = *reinterpret_cast<const frag*>(bb + off);
                 if (SPLIT) bl[j] = *reinterpret_cast<const frag*>(bb + 2 * BNT * 16 + off);
             }
+        };
+        auto mma = [&](frag (&ah)[FM], frag (&al)[FM], frag (&bh)[FN], frag (&bl)[FN]) {
 #pragma unroll
             for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -788,10 +804,33 @@ __global__ __launch_bounds__(512, 1) void conv3x3_v4(ConvBf16Args p) {
                         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
                     }
                 }
+        };
+        if constexpr (SCHED == 0) {
+#pragma unroll
+            for (int t = 0; t < 3; ++t) {
+                frag ah[FM], al[FM], bh[FN], bl[FN];
+                load(t, ah, al, bh, bl);
+                mma(ah, al, bh, bl);
+            }
+        } else {
+            // register double buffer: tap t+1's fragments are in flight while tap t's MFMAs issue
+            frag ah0[FM], al0[FM], bh0[FN], bl0[FN], ah1[FM], al1[FM], bh1[FN], bl1[FN];
+            load(0, ah0, al0, bh0, bl0);
+            __builtin_amdgcn_sched_barrier(0);
+            load(1, ah1, al1, bh1, bl1);
+            __builtin_amdgcn_sched_barrier(0);
+            mma(ah0, al0, bh0, bl0);
+            __builtin_amdgcn_sched_barrier(0);
+            load(2, ah0, al0, bh0, bl0);
+            __builtin_amdgcn_sched_barrier(0);
+            mma(ah1, al1, bh1, bl1);
+            __builtin_amdgcn_sched_barrier(0);
+            mma(ah0, al0, bh0, bl0);
         }
     }
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __syncthreads();
+    V4_STAMP(1);
     float* ep = reinterpret_cast<float*>(lds);
     for (int bd = 0; bd < BOARDS; ++bd) {
         if (bd_w == bd) {
@@ -852,6 +891,354 @@ __global__ __launch_bounds__(512, 1) void conv3x3_v4(ConvBf16Args p) {
         }
         __syncthreads();
     }
+    V4_STAMP(2);
+}
+
+// ===========================================================================
+// v5: board-halo implicit GEMM for the single-plane trunk modes (AZ_PREC_FP16, AZ_PREC_BF16).
+// Activations live in a channel-blocked layout, [board][C/8][225 pixels][8 channels] 16-bit
+// ("g8"), and the weights in [C/16][9 taps][2][N][8]; every LDS-DMA piece (64 lanes x 16 B)
+// is then one contiguous KiB.  A block owns two boards x 128 output channels; per 16-channel
+// chunk the zero-padded 17x17 halo of both boards and the weights of all nine taps are staged
+// (2-deep ring, one barrier per chunk) and the next chunk's pieces are issued one per tap
+// between the MFMAs.  Fragment reads run one tap ahead (register double buffer, inline-asm
+// ds_read with explicit lgkmcnt: the compiler's own waits drain to zero).
+// The residual stream is kept at ~2^-19 relative precision without an fp32 copy: the
+// 16-bit value h (the next conv's input) plus an int8 remainder q, x = h + q/254 * ulp(h).
+// Blocks b and b+8 of the grid are the two channel halves of one board pair: same XCD
+// (round-robin dispatch), so the second half reads the halo from that XCD's L2.
+template <int MODE>
+struct Half16 {                                         // MODE 2: fp16, MODE 1: bf16
+    __device__ static float to_f(uint16_t h) {
+        if (MODE == 2) { _Float16 x; __builtin_memcpy(&x, &h, 2); return (float)x; }
+        return __uint_as_float((uint32_t)h << 16);
+    }
+    __device__ static uint16_t from_f(float f) {
+        if (MODE == 2) { _Float16 x = (_Float16)f; uint16_t h; __builtin_memcpy(&h, &x, 2); return h; }
+        uint32_t u = __float_as_uint(f);
+        u += 0x7fffu + ((u >> 16) & 1u);
+        return (uint16_t)(u >> 16);
+    }
+    // x -> (h, q): h = round(x), q = round((x - h) / u * 254) with u = 2^(frexp_exp(h) - MANT), the
+    // spacing of 16-bit values at h's binade (MANT = 11 fp16, 8 bf16); |q| <= 127 (clamped at
+    // subnormal h, where |x - h| < 2^-24 anyway).  A handful of VALU ops per element.
+    static constexpr int MANT = MODE == 2 ? 11 : 8;
+    __device__ static void split(float x, uint16_t& h, int8_t& q) {
+        h = from_f(x);
+        const float hf = to_f(h);
+        const int e = __builtin_amdgcn_frexp_expf(hf);
+        const float s = __builtin_rintf(__builtin_amdgcn_ldexpf((x - hf) * 254.0f, MANT - e));
+        q = (int8_t)(int)__builtin_amdgcn_fmed3f(s, -127.0f, 127.0f);
+    }
+    __device__ static float join(uint16_t h, int8_t q) {
+        const float hf = to_f(h);
+        const int e = __builtin_amdgcn_frexp_expf(hf);
+        return hf + __builtin_amdgcn_ldexpf((float)q * (1.0f / 254.0f), e - MANT);
+    }
+};
+
+__device__ __forceinline__ uint32_t lds_addr(const void* p) { return (uint32_t)(uintptr_t)p; }
+
+template <typename F>
+__device__ __forceinline__ void ds_rd(F& d, uint32_t addr) {
+    asm volatile("ds_read_b128 %0, %1" : "=v"(d) : "v"(addr) : "memory");
+}
+
+template <int N, typename F>
+__device__ __forceinline__ void lgkm_wait6(F (&a)[4], F (&b)[2]) {
+    // the fragments are in-out operands: every MFMA that reads them is ordered after the wait
+    asm volatile("s_waitcnt lgkmcnt(%6)"
+                 : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(b[0]), "+v"(b[1])
+                 : "i"(N));
+}
+
+template <int MODE>
+__global__ __launch_bounds__(512, 1) void conv3x3_v5(ConvBf16Args p) {
+    static_assert(MODE == 1 || MODE == 2, "v5: single-plane modes");
+    typedef Half16<MODE> H16;
+    constexpr int BNT = 128;
+    constexpr int BOARDS = 2;
+    constexpr int A_PLANE = 2 * V4_HROWS * 16;        // one board, 16 channels: [2 halves][320 rows][16 B]
+    constexpr int A_BUF = BOARDS * A_PLANE;            // 20 KB
+    constexpr int B_TAP = 2 * BNT * 16;                // [2 halves][BNT][16 B] = 4 KB
+    constexpr int B_BUF = 9 * B_TAP;                   // 36 KB
+    constexpr int LDS_MAIN = 2 * A_BUF + 2 * B_BUF;    // 112 KB
+    constexpr int SC = 64, SLD = SC + 4;               // epilogue: 64 staged columns per pass
+    constexpr int LDS_EPI = BOARDS * 256 * SLD * 4;    // 136 KB: [2 boards][256 grid rows][68]
+    constexpr int LDS_BIAS = (LDS_MAIN > LDS_EPI ? LDS_MAIN : LDS_EPI);   // + 128 fp32 biases
+    constexpr int LDS = LDS_BIAS + BNT * 4;
+    constexpr int A_INS = BOARDS * 2 * (V4_HROWS / 64);    // 20 pieces per chunk
+    constexpr int B_INS = 9 * 2 * (BNT / 64);              // 36 pieces per chunk
+    constexpr int PAX = (A_INS + 7) / 8, PBX = (B_INS + 7) / 8;
+    static_assert(PAX + PBX <= 9, "one DMA piece per tap");
+    constexpr int WN = 2, TM = 128;
+    constexpr int FM = 4, FN = 2;
+    typedef typename std::conditional<MODE == 2, f16x8, bf16x8>::type frag;
+    __shared__ __attribute__((aligned(16))) uint8_t lds[LDS];
+
+    V4_STAMP(0);
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave / WN, wn = wave % WN;
+    const int nsplit = p.N / BNT;
+    const int xcd = blockIdx.x % 8, slot = blockIdx.x / 8;
+    const int nb = slot % nsplit, pair = (slot / nsplit) * 8 + xcd;
+    const int n0 = nb * BNT;
+    const int nboards = p.m_limit ? *p.m_limit : p.M / (p.H * p.W);
+    const int b0 = pair * BOARDS;
+    if (b0 >= nboards) return;
+    float* sbias = reinterpret_cast<float*>(lds + LDS_BIAS);
+    if (tid < BNT) sbias[tid] = p.bias[n0 + tid];     // visible after the first chunk barrier
+    const int C = p.C, GI = C / 8, GO = p.N / 8;
+    const int NCH = C / 16;
+    const int PA = (A_INS - wave + 7) / 8, PB = (B_INS - wave + 7) / 8;
+
+    const uint16_t* a_src[PAX];
+    int a_ch[PAX], a_off[PAX];
+#pragma unroll
+    for (int j = 0; j < PAX; ++j) {
+        const int q = wave + 8 * j;
+        const int rb = q % 5, ch = (q / 5) % 2, bd = q / 10;
+        const int hr = rb * 64 + lane;
+        const int Y = hr / 17, X = hr - Y * 17;
+        const int b = b0 + bd;
+        const bool ok = q < A_INS && hr < 289 && Y >= 1 && Y <= 15 && X >= 1 && X <= 15 && b < nboards;
+        a_src[j] = ok ? p.Ahi + (((size_t)b * GI + ch) * 225 + (Y - 1) * 15 + (X - 1)) * 8 : nullptr;
+        a_ch[j] = ch;
+        a_off[j] = bd * A_PLANE + ch * (V4_HROWS * 16) + rb * 1024;
+    }
+    const uint16_t* b_src[PBX];
+    int b_off[PBX];
+#pragma unroll
+    for (int j = 0; j < PBX; ++j) {
+        const int q = min(wave + 8 * j, B_INS - 1);
+        constexpr int RB = BNT / 64;
+        const int rb = q % RB, ch = (q / RB) % 2, t = q / (2 * RB);
+        const int n = n0 + rb * 64 + lane;
+        b_src[j] = p.Bblk + ((size_t)(t * 2 + ch) * p.N + n) * 8;
+        b_off[j] = t * B_TAP + ch * BNT * 16 + rb * 1024;
+    }
+    uint8_t* abuf = lds;
+    uint8_t* bbuf = lds + 2 * A_BUF;
+    // one LDS-DMA piece: k < PAX -> activation piece k, else weight piece k - PAX
+    auto issue_piece = [&](int k, int c) {
+        if (k < PAX) {
+            if (k >= PA) return;
+            const uint16_t* src = a_src[k] ? a_src[k] + (size_t)c * (2 * 225 * 8) : p.zero + a_ch[k] * 8;
+            __builtin_amdgcn_global_load_lds((g_void_t*)src, (lds_void_t*)(abuf + (c & 1) * A_BUF + a_off[k]), 16, 0, 0);
+        } else {
+            const int j = k - PAX;
+            if (j >= PB) return;
+            __builtin_amdgcn_global_load_lds((g_void_t*)(b_src[j] + (size_t)c * 144 * p.N),
+                                             (lds_void_t*)(bbuf + (c & 1) * B_BUF + b_off[j]), 16, 0, 0);
+        }
+    };
+
+    floatx16 acc[FM][FN];
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.0f;
+
+#pragma unroll
+    for (int k = 0; k < PAX + PBX; ++k) issue_piece(k, 0);
+    const int l32 = lane & 31, lh = lane >> 5;
+    const int bd_w = (wm * TM) / 256;
+    const int q0 = (wm * TM) % 256;
+    const uint32_t a_lane = lds_addr(abuf) + bd_w * A_PLANE + lh * (V4_HROWS * 16) + (q0 + l32) * 16;
+    const uint32_t b_lane = lds_addr(bbuf) + lh * BNT * 16 + (wn * (BNT / WN) + l32) * 16;
+    for (int c = 0; c < NCH; ++c) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        const uint32_t ab = a_lane + (c & 1) * A_BUF;
+        const uint32_t bb = b_lane + (c & 1) * B_BUF;
+        auto load = [&](int tap, frag (&a)[FM], frag (&b)[FN]) {
+            const int shift = (tap / 3) * 17 + (tap % 3);
+#pragma unroll
+            for (int i = 0; i < FM; ++i) ds_rd(a[i], ab + (i * 32 + shift) * 16);
+#pragma unroll
+            for (int j = 0; j < FN; ++j) ds_rd(b[j], bb + tap * B_TAP + j * 32 * 16);
+        };
+        auto mma = [&](frag (&a)[FM], frag (&b)[FN], int tap) {
+#pragma unroll
+            for (int i = 0; i < FM; ++i) {
+#ifndef AZ_V5_NOLOAD
+                // next chunk's LDS-DMA pieces ride between this chunk's MFMAs, one per tap
+                if (i == FM / 2 && c + 1 < NCH && tap < PAX + PBX) {
+                    __builtin_amdgcn_sched_barrier(0);
+                    issue_piece(tap, c + 1);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+#endif
+#pragma unroll
+                for (int j = 0; j < FN; ++j) {
+#ifdef AZ_V5_NOMFMA
+                    acc[i][j][0] += (float)a[i][0] * (float)b[j][0];
+#else
+                    if constexpr (MODE == 2)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[i], b[j], acc[i][j], 0, 0, 0);
+                    else
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+#endif
+                }
+            }
+        };
+        frag a0[FM], b0[FN], a1[FM], b1[FN];
+        load(0, a0, b0);
+#pragma unroll
+        for (int tap = 0; tap < 9; ++tap) {
+            if (tap & 1) {
+                if (tap + 1 < 9) { load(tap + 1, a0, b0); lgkm_wait6<6>(a1, b1); }
+                else lgkm_wait6<0>(a1, b1);
+                mma(a1, b1, tap);
+            } else {
+                if (tap + 1 < 9) { load(tap + 1, a1, b1); lgkm_wait6<6>(a0, b0); }
+                else lgkm_wait6<0>(a0, b0);
+                mma(a0, b0, tap);
+            }
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __syncthreads();
+    V4_STAMP(1);
+
+    // epilogue in two column passes (acc[.][j], j = 0, 1), both boards at once: the staged
+    // fp32 tile is [2 boards][225 pixels][64 + 4], so the other pass's accumulators are the only
+    // ones live while a pass finishes.  Item v = tid + 512k -> (board, channel group, pixel),
+    // pixel fastest: a wave's 16-byte stores cover consecutive pixels of one group (contiguous in g8).
+    constexpr int ITEMS = BOARDS * (SC / 8) * 225;     // 3600
+    constexpr int ITER = (ITEMS + 511) / 512;          // 8
+    float* ep = reinterpret_cast<float*>(lds);
+    struct Res { uint4 h; uint2 q; };
+    // residual of item v in pass j (zero beyond the items / boards)
+    auto fetch = [&](int j, int v) {
+        Res r{};
+        const int pix = v % 225, t = v / 225, gl = t % 8, bd = t / 8;
+        const int b = b0 + bd;
+        if (v < ITEMS && b < nboards) {
+            const int n = n0 + (gl / 4) * 64 + j * 32 + (gl % 4) * 8;
+            const size_t e = (((size_t)b * GO + n / 8) * 225 + pix) * 8;
+            r.h = *reinterpret_cast<const uint4*>(p.Rhi + e);
+            r.q = *reinterpret_cast<const uint2*>(p.Rq + e);
+        }
+        return r;
+    };
+    // residual rows: pass 0's are fetched before its staging, pass 1's right after it, so both
+    // latencies hide behind staging / the previous pass's arithmetic
+    Res rr[FN][ITER];
+    if (p.Rhi) {
+#pragma unroll
+        for (int k = 0; k < ITER; ++k) rr[0][k] = fetch(0, tid + 512 * k);
+    }
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+        Res (&r)[ITER] = rr[j];
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                const int q = q0 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * lh;   // 15x17 grid row
+                ep[(bd_w * 256 + q) * SLD + wn * 32 + l32] = acc[i][j][e];
+            }
+        __syncthreads();
+        if (j + 1 < FN && p.Rhi) {
+#pragma unroll
+            for (int k = 0; k < ITER; ++k) rr[j + 1][k] = fetch(j + 1, tid + 512 * k);
+        }
+#pragma unroll
+        for (int k = 0; k < ITER; ++k) {
+            const int v = tid + 512 * k;
+            const int pix = v % 225, t = v / 225, gl = t % 8, bd = t / 8;
+            const int b = b0 + bd;
+            if (v < ITEMS && b < nboards) {
+                const int nl = (gl / 4) * 64 + j * 32 + (gl % 4) * 8, n = n0 + nl;
+                const float* src = ep + (bd * 256 + (pix / 15) * 17 + pix % 15) * SLD + gl * 8;
+                const float4 x0 = *reinterpret_cast<const float4*>(src);
+                const float4 x1 = *reinterpret_cast<const float4*>(src + 4);
+                const float4 c0v = *reinterpret_cast<const float4*>(sbias + nl);
+                const float4 c1v = *reinterpret_cast<const float4*>(sbias + nl + 4);
+                float o[8] = {x0.x + c0v.x, x0.y + c0v.y, x0.z + c0v.z, x0.w + c0v.w,
+                              x1.x + c1v.x, x1.y + c1v.y, x1.z + c1v.z, x1.w + c1v.w};
+                if (p.Rhi) {
+                    uint16_t hh[8];
+                    int8_t qq[8];
+                    *reinterpret_cast<uint4*>(hh) = r[k].h;
+                    *reinterpret_cast<uint2*>(qq) = r[k].q;
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) o[e] += H16::join(hh[e], qq[e]);
+                }
+                uint16_t oh[8];
+                int8_t oq[8];
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    if (p.relu) o[e] = o[e] > 0.0f ? o[e] : 0.0f;
+                    H16::split(o[e], oh[e], oq[e]);
+                }
+                const size_t e = (((size_t)b * GO + n / 8) * 225 + pix) * 8;
+                *reinterpret_cast<uint4*>(p.Chi + e) = *reinterpret_cast<const uint4*>(oh);
+                if (p.Cq) *reinterpret_cast<uint2*>(p.Cq + e) = *reinterpret_cast<const uint2*>(oq);
+                if (p.Cf) {                            // fp32 NHWC (the trunk output the pool reads)
+                    float* cf = p.Cf + ((size_t)b * 225 + pix) * p.N + n;
+                    *reinterpret_cast<float4*>(cf) = make_float4(o[0], o[1], o[2], o[3]);
+                    *reinterpret_cast<float4*>(cf + 4) = make_float4(o[4], o[5], o[6], o[7]);
+                }
+            }
+        }
+        __syncthreads();
+    }
+    V4_STAMP(2);
+}
+
+// fp32 NHWC [B*225][C] -> g8 16-bit + int8 remainder (the first trunk input and residual)
+template <int MODE>
+__global__ void k_to_g8(const float* in, uint16_t* hi, int8_t* q, int C, const int* m_limit, int maxB) {
+    const int G = C / 8;
+    const int B = m_limit ? min(*m_limit, maxB) : maxB;
+    const size_t total = (size_t)B * G * 225;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+        const int pix = (int)(i % 225);
+        const size_t bg = i / 225;
+        const int g = (int)(bg % G);
+        const size_t b = bg / G;
+        const float* src = in + (b * 225 + pix) * C + g * 8;
+        const float4 v0 = *reinterpret_cast<const float4*>(src);
+        const float4 v1 = *reinterpret_cast<const float4*>(src + 4);
+        const float f[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+        uint16_t h[8];
+        int8_t r[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) Half16<MODE>::split(f[e], h[e], r[e]);
+        *reinterpret_cast<uint4*>(hi + i * 8) = *reinterpret_cast<const uint4*>(h);
+        *reinterpret_cast<uint2*>(q + i * 8) = *reinterpret_cast<const uint2*>(r);
+    }
+}
+
+void az_launch_to_g8(const float* in, uint16_t* hi, int8_t* q, int C, const int* m_limit, int maxB, int mode,
+                     hipStream_t st) {
+    if (mode == 2) hipLaunchKernelGGL(k_to_g8<2>, dim3(2048), dim3(256), 0, st, in, hi, q, C, m_limit, maxB);
+    else hipLaunchKernelGGL(k_to_g8<1>, dim3(2048), dim3(256), 0, st, in, hi, q, C, m_limit, maxB);
+}
+
+// true when conv3x3_v5 handles this shape (15x15 boards, 16-channel chunks, 128-channel halves)
+bool az_conv_v5_supported(int H, int W, int C, int N) { return H == 15 && W == 15 && C % 16 == 0 && N % 128 == 0; }
+
+static int g_conv_flags = 0;
+// Variant bits for A/B measurement inside one process (tools/net_bench.py --flags); none defined now
+// (a residual L2 prefetch during the main loop measured 0.6% slower and was removed)
+extern "C" int az_diag_set_conv_flags(int flags) { g_conv_flags = flags; return 0; }
+
+void az_conv_v5_launch(const ConvBf16Args& a_in, int mode, hipStream_t st) {
+    ConvBf16Args a = a_in;
+    a.flags = g_conv_flags;
+    const int boards = a.M / 225;
+    const int pairs = (boards + 1) / 2;
+    const int nsplit = a.N / 128;
+    const int grid = (pairs + 7) / 8 * 8 * nsplit;     // XCD-aware pair/half mapping needs whole groups of 8
+    if (mode == 2) hipLaunchKernelGGL(conv3x3_v5<2>, dim3(grid), dim3(512), 0, st, a);
+    else hipLaunchKernelGGL(conv3x3_v5<1>, dim3(grid), dim3(512), 0, st, a);
 }
 
 // fp32 -> fp16 activations (first trunk input, AZ_PREC_FP16)
@@ -869,18 +1256,27 @@ void az_launch_to_f16(const float* in, uint16_t* out, size_t n, const int* m_lim
 // true when conv3x3_v4 handles this shape
 bool az_conv_v4_supported(int H, int W, int C, int N) { return H == 15 && W == 15 && C % 16 == 0 && N % 64 == 0; }
 
+static int g_v4_sched = 1;
+void az_conv_set_v4_sched(int v) { g_v4_sched = v; }
+
+template <int BNT, int SCHED>
+static void v4_launch(const ConvBf16Args& a, int mode, int grid, hipStream_t st) {
+    // bf16x3 keeps the single-buffered schedule: the double buffer spills at 256 VGPRs
+    if (mode == 0) hipLaunchKernelGGL((conv3x3_v4<0, BNT, 0>), dim3(grid), dim3(512), 0, st, a);
+    else if (mode == 1) hipLaunchKernelGGL((conv3x3_v4<1, BNT, SCHED>), dim3(grid), dim3(512), 0, st, a);
+    else hipLaunchKernelGGL((conv3x3_v4<2, BNT, SCHED>), dim3(grid), dim3(512), 0, st, a);
+}
+
 void az_conv_v4_launch(const ConvBf16Args& a, int mode, hipStream_t st) {
     const int boards = a.M / 225;
     const int bnt = a.N % 128 == 0 ? 128 : 64;
     const int grid = (boards + 1) / 2 * (a.N / bnt);
     if (bnt == 128) {
-        if (mode == 0) hipLaunchKernelGGL((conv3x3_v4<0, 128>), dim3(grid), dim3(512), 0, st, a);
-        else if (mode == 1) hipLaunchKernelGGL((conv3x3_v4<1, 128>), dim3(grid), dim3(512), 0, st, a);
-        else hipLaunchKernelGGL((conv3x3_v4<2, 128>), dim3(grid), dim3(512), 0, st, a);
+        if (g_v4_sched) v4_launch<128, 1>(a, mode, grid, st);
+        else v4_launch<128, 0>(a, mode, grid, st);
     } else {
-        if (mode == 0) hipLaunchKernelGGL((conv3x3_v4<0, 64>), dim3(grid), dim3(512), 0, st, a);
-        else if (mode == 1) hipLaunchKernelGGL((conv3x3_v4<1, 64>), dim3(grid), dim3(512), 0, st, a);
-        else hipLaunchKernelGGL((conv3x3_v4<2, 64>), dim3(grid), dim3(512), 0, st, a);
+        if (g_v4_sched) v4_launch<64, 1>(a, mode, grid, st);
+        else v4_launch<64, 0>(a, mode, grid, st);
     }
 }
 

@@ -38,6 +38,11 @@ void az_conv_bf16_launch_v(const ConvBf16Args& a, bool split, hipStream_t st);
 void az_conv_set_variant(int v);
 bool az_conv_v4_supported(int H, int W, int C, int N);
 void az_conv_v4_launch(const ConvBf16Args& a, int mode, hipStream_t st);
+void az_conv_set_v4_sched(int v);
+bool az_conv_v5_supported(int H, int W, int C, int N);
+void az_conv_v5_launch(const ConvBf16Args& a, int mode, hipStream_t st);
+void az_launch_to_g8(const float* in, uint16_t* hi, int8_t* q, int C, const int* m_limit, int maxB, int mode,
+                     hipStream_t st);
 void az_launch_to_f16(const float* in, uint16_t* out, size_t n, const int* m_limit, int rows_per_sample, int C,
                       hipStream_t st);
 void az_launch_split_bf16(const float* in, uint16_t* hi, uint16_t* lo, size_t n, const int* m_limit, int rows_per_sample,
@@ -93,6 +98,7 @@ struct Layer {            // one implicit-GEMM layer, BN folded
     float* W = nullptr;   // [N][K] fp32
     uint16_t* Whi = nullptr; uint16_t* Wlo = nullptr;   // bf16 split copies (3x3 trunk)
     uint16_t* Wh16 = nullptr;                           // fp16 copy (3x3 trunk, AZ_PREC_FP16)
+    uint16_t* Wbk_bf = nullptr; uint16_t* Wbk_h = nullptr;  // chunk-blocked bf16 / fp16 copies (v5 conv)
     float* b = nullptr;   // [N]
     int N = 0, K = 0, Kpad = 0, taps = 1, C = 0;
 };
@@ -186,6 +192,20 @@ int upload_layer(Layer& L, const std::vector<float>& W, const std::vector<float>
         for (size_t i = 0; i < W.size(); ++i) { _Float16 h = (_Float16)W[i]; std::memcpy(&h16[i], &h, 2); }
         if (!L.Wh16) DALLOC(L.Wh16, W.size());
         HIPCHK(hipMemcpy(L.Wh16, h16.data(), h16.size() * 2, hipMemcpyHostToDevice));
+        if (taps == 9 && C % 16 == 0) {
+            // [N][9][C] -> [C/16][9][2][N][8]: one 64-row piece of a chunk/tap/half is 1 KiB contiguous
+            std::vector<uint16_t> bb(W.size()), bh(W.size());
+            for (int o = 0; o < N; ++o)
+                for (int t = 0; t < 9; ++t)
+                    for (int c = 0; c < C; ++c) {
+                        const size_t src = ((size_t)o * 9 + t) * C + c;
+                        const size_t dst = ((((size_t)(c / 16) * 9 + t) * 2 + (c / 8) % 2) * N + o) * 8 + c % 8;
+                        bb[dst] = hi[src]; bh[dst] = h16[src];
+                    }
+            if (!L.Wbk_bf) { DALLOC(L.Wbk_bf, W.size()); DALLOC(L.Wbk_h, W.size()); }
+            HIPCHK(hipMemcpy(L.Wbk_bf, bb.data(), bb.size() * 2, hipMemcpyHostToDevice));
+            HIPCHK(hipMemcpy(L.Wbk_h, bh.data(), bh.size() * 2, hipMemcpyHostToDevice));
+        }
     }
     return 0;
 }
@@ -277,6 +297,37 @@ int net_forward(az_net* n, const float* x0, int B, const int* nb, float* logits,
         }
     } else {
         const bool split = prec == AZ_PREC_BF16X3;
+        if (!split && az_conv_v5_supported(H, W, F, F)) {
+            // g8 layout, v5 conv; the int8 remainder planes live in the (otherwise idle) bf16 lo buffers
+            const int mode = f16 ? 2 : 1;
+            int8_t* hq[2] = {reinterpret_cast<int8_t*>(n->hl[0]), reinterpret_cast<int8_t*>(n->hl[1])};
+            az_launch_to_g8(h, n->hh[0], hq[0], F, nb, B, mode, st);
+            int cur = 0;
+            for (int i = 0; i < d.blocks; ++i) {
+                const Layer& L1 = n->blk[2 * i];
+                const Layer& L2 = n->blk[2 * i + 1];
+                ConvBf16Args a{};
+                a.Ahi = n->hh[cur];
+                a.Bblk = f16 ? L1.Wbk_h : L1.Wbk_bf;
+                a.Chi = n->th;
+                a.bias = L1.b;
+                a.M = rows; a.N = F; a.C = F; a.H = H; a.W = W; a.m_limit = nb; a.rows_per_sample = HW; a.relu = 1;
+                a.zero = n->zero;
+                a.stamp = 2 * i;
+                az_conv_v5_launch(a, mode, st);
+                ConvBf16Args b2 = a;
+                b2.stamp = 2 * i + 1;
+                b2.Ahi = n->th;
+                b2.Bblk = f16 ? L2.Wbk_h : L2.Wbk_bf;
+                b2.Chi = n->hh[cur ^ 1]; b2.Cq = hq[cur ^ 1];
+                b2.bias = L2.b;
+                if (d.residual) { b2.Rhi = n->hh[cur]; b2.Rq = hq[cur]; }
+                b2.Cf = (i == d.blocks - 1) ? other : nullptr;
+                az_conv_v5_launch(b2, mode, st);
+                cur ^= 1;
+            }
+            if (d.blocks > 0) h = other;
+        } else {
         if (f16) az_launch_to_f16(h, n->hh[0], (size_t)rows * F, nb, HW, F, st);
         else az_launch_split_bf16(h, n->hh[0], split ? n->hl[0] : nullptr, (size_t)rows * F, nb, HW, F, st);
         int cur = 0;
@@ -290,6 +341,8 @@ int net_forward(az_net* n, const float* x0, int B, const int* nb, float* logits,
             a.bias = L1.b; a.Rhi = nullptr; a.Rlo = nullptr;
             a.M = rows; a.N = F; a.C = F; a.H = H; a.W = W; a.m_limit = nb; a.rows_per_sample = HW; a.relu = 1;
             a.zero = n->zero;
+            a.stamp = 2 * i;
+            a.Bblk = f16 ? L1.Wbk_h : L1.Wbk_bf;
             if (f16) a.Bhi = L1.Wh16;
             if (f16) az_conv_v4_launch(a, 2, st);
             else az_conv_bf16_launch_v(a, split, st);
@@ -298,6 +351,8 @@ int net_forward(az_net* n, const float* x0, int B, const int* nb, float* logits,
             b2.Bhi = L2.Whi; b2.Blo = split ? L2.Wlo : nullptr;
             b2.Chi = n->hh[cur ^ 1]; b2.Clo = split ? n->hl[cur ^ 1] : nullptr;
             b2.bias = L2.b;
+            b2.stamp = 2 * i + 1;
+            b2.Bblk = f16 ? L2.Wbk_h : L2.Wbk_bf;
             b2.Rhi = d.residual ? n->hh[cur] : nullptr; b2.Rlo = d.residual && split ? n->hl[cur] : nullptr;
             b2.Cf = (i == d.blocks - 1) ? other : nullptr;
             if (f16) {
@@ -314,6 +369,7 @@ int net_forward(az_net* n, const float* x0, int B, const int* nb, float* logits,
             cur ^= 1;
         }
         if (d.blocks > 0 && !f16) h = other;
+        }
     }
     if (ev1) HIPCHK(hipEventRecord(ev1, st));
     az_launch_pool(h, n->pool, B, H, W, F, P, nb, st);
@@ -594,6 +650,7 @@ int az_net_create(az_engine* e, const az_net_desc* d, az_net** out) {
     if (!r) r = dalloc(&n->zero, 128);
     if (!r && hipMemset(n->zero, 0, 256) != hipSuccess) r = fail(AZ_ERR_HIP, "memset");
     if (const char* v = getenv("AZ_CONV_VARIANT")) az_conv_set_variant(atoi(v));
+    if (const char* v = getenv("AZ_V4_SCHED")) az_conv_set_v4_sched(atoi(v));
     if (r) { az_net_destroy(n); return r; }
     *out = n;
     return 0;
@@ -605,7 +662,7 @@ void az_net_destroy(az_net* n) {
     auto F = [](void* p) { if (p) hipFree(p); };
     std::vector<Layer*> ls = {&n->in, &n->pconv, &n->vconv, &n->pfc, &n->vfc1, &n->vfc2};
     for (auto& l : n->blk) ls.push_back(&l);
-    for (Layer* l : ls) { F(l->W); F(l->b); F(l->Whi); F(l->Wlo); F(l->Wh16); }
+    for (Layer* l : ls) { F(l->W); F(l->b); F(l->Whi); F(l->Wlo); F(l->Wh16); F(l->Wbk_bf); F(l->Wbk_h); }
     for (void* p : {(void*)n->x0, (void*)n->h0, (void*)n->h1, (void*)n->t, (void*)n->pool, (void*)n->pp, (void*)n->vp,
                     (void*)n->v1, (void*)n->logits, (void*)n->value, (void*)n->soft, (void*)n->in_nchw, (void*)n->d_nb,
                     (void*)n->hh[0], (void*)n->hh[1], (void*)n->hl[0], (void*)n->hl[1], (void*)n->th, (void*)n->tl,

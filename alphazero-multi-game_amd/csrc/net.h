@@ -23,15 +23,19 @@ struct GemmArgs {
 struct ConvBf16Args {
     const uint16_t* Ahi; const uint16_t* Alo;   // [rows][C] bf16 (Alo null for plain bf16)
     const uint16_t* Bhi; const uint16_t* Blo;   // [N][9*C] bf16
+    const uint16_t* Bblk;                       // chunk-blocked [C/16][9][2][N][8] (v5; same type as Ahi)
     uint16_t* Chi; uint16_t* Clo;               // outputs (split for the next layer)
     float* Cf;                                  // optional fp32 output [rows][N]
     const float* bias;
     const uint16_t* Rhi; const uint16_t* Rlo;   // residual (split) or null
-    const float* Rf;                            // fp32 residual [rows][N] (v4 only; AZ_PREC_FP16)
+    const float* Rf;                            // fp32 residual [rows][N] (v4 only)
+    const int8_t* Rq; int8_t* Cq;               // v5: int8 remainders of the g8 residual / output
     int M, N, C, H, W;
     const int* m_limit; int rows_per_sample;
     int relu;
     const uint16_t* zero;                       // >= 64 zero bytes (padding source for glds)
+    int stamp;                                  // diagnostic builds: launch slot for phase stamps
+    int flags;                                  // kernel variant bits (az_diag_set_conv_flags; A/B tests)
 };
 
 void az_launch_gemm_f32(const GemmArgs& p, int act, bool res, hipStream_t st);

@@ -1,0 +1,70 @@
+#!/usr/bin/env python3
+"""Trunk-conv microbenchmark: C3 net (15x15, 20 blocks x 256 filters) forward at batch B.
+Prints the average trunk-conv launch time (HIP events on the engine stream) and the
+algorithmic TFLOP/s (2*9*C*C*225 FLOP per board per conv).  Used for kernel iteration and
+for rocprofv3 PMC passes (the conv kernel is the only MFMA kernel of note)."""
+import argparse
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "alphazero-multi-game_amd"))
+import az_amd  # noqa: E402
+
+PREC = {"f32": az_amd.AZ_PREC_F32, "bf16x3": az_amd.AZ_PREC_BF16X3, "bf16": az_amd.AZ_PREC_BF16,
+        "fp16": az_amd.AZ_PREC_FP16}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--precision", default="fp16", choices=list(PREC))
+    ap.add_argument("--batch", type=int, default=2048)
+    ap.add_argument("--channels", type=int, default=256)
+    ap.add_argument("--blocks", type=int, default=20)
+    ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--flags", default="", help="comma list of conv variant flag sets to A/B (alternating rounds)")
+    ap.add_argument("--rounds", type=int, default=4)
+    a = ap.parse_args()
+    eng = az_amd.Engine(int(os.environ.get("LOCAL_RANK", 0)))
+    desc = az_amd.gomoku_net_desc(board_size=15, channels=a.channels, blocks=a.blocks,
+                                  precision=PREC[a.precision], max_batch=a.batch)
+    net = az_amd.HipNeuralNetwork(eng, desc)
+    net.init_random(1234)
+    x = (np.random.default_rng(0).random((a.batch, 11, 15, 15)) < 0.2).astype(np.float32)
+    net.forward(x)
+    if a.flags:
+        from az_amd import _lib
+        sets = [int(f, 0) for f in a.flags.split(",")]
+        res = {f: [] for f in sets}
+        flops = a.batch * 2 * 9 * a.channels * a.channels * 225
+        for _ in range(a.rounds):
+            for f in sets:
+                _lib.lib().az_diag_set_conv_flags(f)
+                net.forward(x)
+                net.profile(True)
+                for _ in range(a.iters):
+                    net.forward(x)
+                ms, launches, _ = net.profile_read()
+                res[f].append(ms / launches)
+        for f in sets:
+            v = np.array(res[f])
+            print(f"{a.precision} flags={f:#x}: trunk {np.median(v):.4f} ms/launch (min {v.min():.4f} max {v.max():.4f}), "
+                  f"{flops / np.median(v) / 1e9:.1f} TFLOP/s")
+        return
+    net.profile(True)
+    t0 = time.perf_counter()
+    for _ in range(a.iters):
+        net.forward(x)
+    wall = (time.perf_counter() - t0) / a.iters
+    ms, launches, fw = net.profile_read()
+    per = ms / launches
+    flops = a.batch * 2 * 9 * a.channels * a.channels * 225
+    print(f"{a.precision} B={a.batch}: trunk {per:.4f} ms/launch, {flops / per / 1e9:.1f} TFLOP/s algorithmic, "
+          f"forward wall {wall * 1e3:.2f} ms (incl. H2D/D2H)")
+
+
+if __name__ == "__main__":
+    main()
