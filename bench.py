@@ -168,6 +168,9 @@ def main():
                          "launches": launches, "avg_launch_ms": per_launch_ms,
                          "flops_per_launch": per_launch_flops},
         }
+        tr = pmc_traffic(a, per_launch_flops / (conv_flops_per_eval / (2 * a.blocks)) if launches else 0)
+        if tr:
+            out["roofline"].update(tr)
         if a.cpu_baseline and world == 1:
             if blob is None:
                 blob = net_oracle.init_blob(desc, a.seed)
@@ -177,6 +180,29 @@ def main():
         print(json.dumps(out))
     if dist is not None:
         dist.destroy_process_group()
+
+
+def pmc_traffic(a, boards_per_launch):
+    """HBM bytes per trunk launch from the committed rocprofv3 PMC summary of the same kernel
+    (profiles/*_trunk_pmc.json: FETCH_SIZE x2 per the gfx950 correction + WRITE_SIZE, measured at
+    B boards per launch), scaled to this run's average boards per launch.  None if no summary
+    matches the precision / net."""
+    import glob
+    best = None
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_trunk_pmc.json"))):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        if (d.get("precision"), d.get("board"), d.get("channels"), d.get("blocks")) == \
+                (a.precision, a.board, a.channels, a.blocks):
+            best = (f, d)
+    if best is None or boards_per_launch <= 0:
+        return None
+    f, d = best
+    scale = boards_per_launch / d["boards_per_launch"]
+    return {"traffic": d["hbm_bytes_per_launch"] * scale, "traffic_unit": "bytes/launch",
+            "traffic_source": os.path.relpath(f, ROOT) + f" (PMC at B={d['boards_per_launch']}, scaled x{scale:.4f})"}
 
 
 if __name__ == "__main__":
