@@ -1066,7 +1066,8 @@ __global__ __launch_bounds__(512, 1) void conv3x3_v5(ConvBf16Args p) {
 #pragma unroll
             for (int i = 0; i < FM; ++i) {
 #ifndef AZ_V5_NOLOAD
-                // next chunk's LDS-DMA pieces ride between this chunk's MFMAs, one per tap
+                // next chunk's LDS-DMA pieces ride between this chunk's MFMAs, one per tap (two per
+                // tap early in the chunk, or staggered between SIMD-mate waves, measured no better)
                 if (i == FM / 2 && c + 1 < NCH && tap < PAX + PBX) {
                     __builtin_amdgcn_sched_barrier(0);
                     issue_piece(tap, c + 1);
@@ -1212,7 +1213,7 @@ __global__ void k_to_g8(const float* in, uint16_t* hi, int8_t* q, int C, const i
 #pragma unroll
         for (int e = 0; e < 8; ++e) Half16<MODE>::split(f[e], h[e], r[e]);
         *reinterpret_cast<uint4*>(hi + i * 8) = *reinterpret_cast<const uint4*>(h);
-        *reinterpret_cast<uint2*>(q + i * 8) = *reinterpret_cast<const uint2*>(r);
+        if (q) *reinterpret_cast<uint2*>(q + i * 8) = *reinterpret_cast<const uint2*>(r);
     }
 }
 
@@ -1220,6 +1221,46 @@ void az_launch_to_g8(const float* in, uint16_t* hi, int8_t* q, int C, const int*
                      hipStream_t st) {
     if (mode == 2) hipLaunchKernelGGL(k_to_g8<2>, dim3(2048), dim3(256), 0, st, in, hi, q, C, m_limit, maxB);
     else hipLaunchKernelGGL(k_to_g8<1>, dim3(2048), dim3(256), 0, st, in, hi, q, C, m_limit, maxB);
+}
+
+// adaptive_avg_pool2d(x, (P, P)) of a 15x15 g8 trunk output (16-bit + int8 remainder) -> fp32 NHWC
+// [B][P*P][C]; one thread per (board, 8-channel group, output cell), same summation order as
+// k_adaptive_pool (rows, then columns; sum / kh / kw)
+template <int MODE>
+__global__ void k_pool_g8(const uint16_t* hi, const int8_t* q, float* out, int C, int P, const int* m_limit, int maxB) {
+    const int G = C / 8, PP = P * P;
+    const int B = m_limit ? min(*m_limit, maxB) : maxB;
+    const size_t total = (size_t)B * G * PP;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+        const int o = (int)(i % PP);
+        const size_t bg = i / PP;
+        const int g = (int)(bg % G);
+        const size_t b = bg / G;
+        const int oy = o / P, ox = o % P;
+        const int y0 = (oy * 15) / P, y1 = ((oy + 1) * 15 + P - 1) / P;
+        const int x0 = (ox * 15) / P, x1 = ((ox + 1) * 15 + P - 1) / P;
+        float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        for (int y = y0; y < y1; ++y)
+            for (int x = x0; x < x1; ++x) {
+                const size_t e = ((b * G + g) * 225 + y * 15 + x) * 8;
+                uint16_t h[8];
+                int8_t r[8];
+                *reinterpret_cast<uint4*>(h) = *reinterpret_cast<const uint4*>(hi + e);
+                *reinterpret_cast<uint2*>(r) = *reinterpret_cast<const uint2*>(q + e);
+#pragma unroll
+                for (int k = 0; k < 8; ++k) s[k] += Half16<MODE>::join(h[k], r[k]);
+            }
+        const float kh = (float)(y1 - y0), kw = (float)(x1 - x0);
+        float* dst = out + (b * PP + o) * C + g * 8;
+        *reinterpret_cast<float4*>(dst) = make_float4(s[0] / kh / kw, s[1] / kh / kw, s[2] / kh / kw, s[3] / kh / kw);
+        *reinterpret_cast<float4*>(dst + 4) = make_float4(s[4] / kh / kw, s[5] / kh / kw, s[6] / kh / kw, s[7] / kh / kw);
+    }
+}
+
+void az_launch_pool_g8(const uint16_t* hi, const int8_t* q, float* out, int B, int C, int P, const int* m_limit, int mode,
+                       hipStream_t st) {
+    if (mode == 2) hipLaunchKernelGGL(k_pool_g8<2>, dim3(4096), dim3(256), 0, st, hi, q, out, C, P, m_limit, B);
+    else hipLaunchKernelGGL(k_pool_g8<1>, dim3(4096), dim3(256), 0, st, hi, q, out, C, P, m_limit, B);
 }
 
 // true when conv3x3_v5 handles this shape (15x15 boards, 16-channel chunks, 128-channel halves)

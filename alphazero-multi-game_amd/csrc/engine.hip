@@ -43,6 +43,8 @@ bool az_conv_v5_supported(int H, int W, int C, int N);
 void az_conv_v5_launch(const ConvBf16Args& a, int mode, hipStream_t st);
 void az_launch_to_g8(const float* in, uint16_t* hi, int8_t* q, int C, const int* m_limit, int maxB, int mode,
                      hipStream_t st);
+void az_launch_pool_g8(const uint16_t* hi, const int8_t* q, float* out, int B, int C, int P, const int* m_limit, int mode,
+                       hipStream_t st);
 void az_launch_to_f16(const float* in, uint16_t* out, size_t n, const int* m_limit, int rows_per_sample, int C,
                       hipStream_t st);
 void az_launch_split_bf16(const float* in, uint16_t* hi, uint16_t* lo, size_t n, const int* m_limit, int rows_per_sample,
@@ -115,6 +117,7 @@ struct az_net {
     float *x0 = nullptr, *h0 = nullptr, *h1 = nullptr, *t = nullptr, *pool = nullptr;
     uint16_t *hh[2] = {nullptr, nullptr}, *hl[2] = {nullptr, nullptr}, *th = nullptr, *tl = nullptr;
     float *pp = nullptr, *vp = nullptr, *v1 = nullptr, *logits = nullptr, *value = nullptr, *soft = nullptr;
+    float* ws = nullptr;                                // split-K workspace of the FC layers
     float* in_nchw = nullptr;
     int* d_nb = nullptr;
     uint16_t* zero = nullptr;   // 256 zero bytes: glds source for the board edge
@@ -217,7 +220,7 @@ int net_load(az_net* n, const float* blob) {
     std::vector<float> W, b;
     const bool split = F % 32 == 0;
     fold_conv(pc, F, d.in_planes, 3, n->cin_pad, d.conv_bias, W, b);
-    if (int r = upload_layer(n->in, W, b, F, 9 * n->cin_pad, 9, n->cin_pad, false)) return r;
+    if (int r = upload_layer(n->in, W, b, F, 9 * n->cin_pad, 9, n->cin_pad, F % 32 == 0)) return r;  // 16-bit copies: g8 input conv
     n->blk.resize(2 * d.blocks);
     for (int i = 0; i < 2 * d.blocks; ++i) {
         fold_conv(pc, F, F, 3, F, d.conv_bias, W, b);
@@ -263,6 +266,14 @@ GemmArgs gemm_args(const Layer& L, const float* A, int lda, float* C, int ldc, c
     return p;
 }
 
+// K slices for an FC layer of B rows: enough blocks to cover the chip, slices of >= 256 K
+static int fc_splits(int B, int K) {
+    const int tiles = (B + 127) / 128 * 2;
+    int s = 1;
+    while (s < 16 && tiles * s < 512 && K / (2 * s) >= 256) s *= 2;
+    return s;
+}
+
 // Forward of B samples (B = capacity; *nb = active samples, device side) from the
 // NHWC16 input x0 -> logits [B][A], value [B].
 int net_forward(az_net* n, const float* x0, int B, const int* nb, float* logits, float* value, hipStream_t st) {
@@ -272,7 +283,26 @@ int net_forward(az_net* n, const float* x0, int B, const int* nb, float* logits,
     const int prec = d.precision;
     const bool bf = (prec == AZ_PREC_BF16X3 || prec == AZ_PREC_BF16 || prec == AZ_PREC_FP16) && F % 32 == 0;
     const bool f16 = prec == AZ_PREC_FP16;
-    az_launch_gemm_f32(gemm_args(n->in, x0, n->cin_pad, n->h0, F, nullptr, rows, H, W, nb, HW), ACT_RELU, false, st);
+    // g8 path (v5 conv, fp16/bf16): input conv, trunk and pool all on 16-bit channel-blocked rows
+    const bool g8 = bf && prec != AZ_PREC_BF16X3 && az_conv_v5_supported(H, W, F, F) && n->cin_pad == 16 &&
+                    n->in.Wbk_h != nullptr;
+    const int mode = f16 ? 2 : 1;
+    int8_t* hq[2] = {reinterpret_cast<int8_t*>(n->hl[0]), reinterpret_cast<int8_t*>(n->hl[1])};
+    if (g8) {
+        // input planes -> g8 16-bit (0/1 planes are exact), then the input conv as a one-chunk v5 conv
+        az_launch_to_g8(x0, n->th, nullptr, n->cin_pad, nb, B, mode, st);
+        ConvBf16Args a{};
+        a.Ahi = n->th;
+        a.Bblk = f16 ? n->in.Wbk_h : n->in.Wbk_bf;
+        a.Chi = n->hh[0]; a.Cq = hq[0];
+        a.bias = n->in.b;
+        a.M = rows; a.N = F; a.C = n->cin_pad; a.H = H; a.W = W; a.m_limit = nb; a.rows_per_sample = HW; a.relu = 1;
+        a.zero = n->zero;
+        a.stamp = -1;
+        az_conv_v5_launch(a, mode, st);
+    } else {
+        az_launch_gemm_f32(gemm_args(n->in, x0, n->cin_pad, n->h0, F, nullptr, rows, H, W, nb, HW), ACT_RELU, false, st);
+    }
     float* h = n->h0;
     float* other = n->h1;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -297,11 +327,8 @@ int net_forward(az_net* n, const float* x0, int B, const int* nb, float* logits,
         }
     } else {
         const bool split = prec == AZ_PREC_BF16X3;
-        if (!split && az_conv_v5_supported(H, W, F, F)) {
+        if (g8) {
             // g8 layout, v5 conv; the int8 remainder planes live in the (otherwise idle) bf16 lo buffers
-            const int mode = f16 ? 2 : 1;
-            int8_t* hq[2] = {reinterpret_cast<int8_t*>(n->hl[0]), reinterpret_cast<int8_t*>(n->hl[1])};
-            az_launch_to_g8(h, n->hh[0], hq[0], F, nb, B, mode, st);
             int cur = 0;
             for (int i = 0; i < d.blocks; ++i) {
                 const Layer& L1 = n->blk[2 * i];
@@ -322,11 +349,12 @@ int net_forward(az_net* n, const float* x0, int B, const int* nb, float* logits,
                 b2.Chi = n->hh[cur ^ 1]; b2.Cq = hq[cur ^ 1];
                 b2.bias = L2.b;
                 if (d.residual) { b2.Rhi = n->hh[cur]; b2.Rq = hq[cur]; }
-                b2.Cf = (i == d.blocks - 1) ? other : nullptr;
                 az_conv_v5_launch(b2, mode, st);
                 cur ^= 1;
             }
-            if (d.blocks > 0) h = other;
+            if (ev1) HIPCHK(hipEventRecord(ev1, st));
+            ev1 = nullptr;
+            az_launch_pool_g8(n->hh[cur], hq[cur], n->pool, B, F, P, nb, mode, st);
         } else {
         if (f16) az_launch_to_f16(h, n->hh[0], (size_t)rows * F, nb, HW, F, st);
         else az_launch_split_bf16(h, n->hh[0], split ? n->hl[0] : nullptr, (size_t)rows * F, nb, HW, F, st);
@@ -372,12 +400,17 @@ int net_forward(az_net* n, const float* x0, int B, const int* nb, float* logits,
         }
     }
     if (ev1) HIPCHK(hipEventRecord(ev1, st));
-    az_launch_pool(h, n->pool, B, H, W, F, P, nb, st);
+    if (!g8) az_launch_pool(h, n->pool, B, H, W, F, P, nb, st);
     az_launch_gemm_f32(gemm_args(n->pconv, n->pool, F, n->pp, d.head_channels, nullptr, B * PP, 1, 1, nb, PP), ACT_RELU, false, st);
     az_launch_gemm_f32(gemm_args(n->vconv, n->pool, F, n->vp, d.head_channels, nullptr, B * PP, 1, 1, nb, PP), ACT_RELU, false, st);
     const int HK = d.head_channels * PP;
-    az_launch_gemm_f32(gemm_args(n->pfc, n->pp, HK, logits, d.action_size, nullptr, B, 1, 1, nb, 1), ACT_NONE, false, st);
-    az_launch_gemm_f32(gemm_args(n->vfc1, n->vp, HK, n->v1, d.fc_hidden, nullptr, B, 1, 1, nb, 1), ACT_RELU, false, st);
+    // FC layers: few rows, long K -> split-K over the workspace (deterministic reduction)
+    GemmArgs pf = gemm_args(n->pfc, n->pp, HK, logits, d.action_size, nullptr, B, 1, 1, nb, 1);
+    GemmArgs v1 = gemm_args(n->vfc1, n->vp, HK, n->v1, d.fc_hidden, nullptr, B, 1, 1, nb, 1);
+    const int splits = fc_splits(B, HK);
+    if (splits > 1) { pf.part = v1.part = n->ws; pf.splits = v1.splits = splits; }
+    az_launch_gemm_f32(pf, ACT_NONE, false, st);
+    az_launch_gemm_f32(v1, ACT_RELU, false, st);
     az_launch_gemm_f32(gemm_args(n->vfc2, n->v1, d.fc_hidden, value, 1, nullptr, B, 1, 1, nb, 1), ACT_TANH, false, st);
     HIPCHK(hipGetLastError());
     return 0;
@@ -644,6 +677,7 @@ int az_net_create(az_engine* e, const az_net_desc* d, az_net** out) {
     A_(&n->pool, B * n->P2 * F);
     A_(&n->pp, B * n->P2 * d->head_channels); A_(&n->vp, B * n->P2 * d->head_channels);
     A_(&n->v1, B * d->fc_hidden);
+    A_(&n->ws, (size_t)B * std::max(d->action_size, d->fc_hidden) * 16);
     A_(&n->logits, B * d->action_size); A_(&n->value, B); A_(&n->soft, B * d->action_size);
     A_(&n->in_nchw, B * d->in_planes * n->HW);
     if (!r) r = dalloc(&n->d_nb, 1);
@@ -664,7 +698,7 @@ void az_net_destroy(az_net* n) {
     for (auto& l : n->blk) ls.push_back(&l);
     for (Layer* l : ls) { F(l->W); F(l->b); F(l->Whi); F(l->Wlo); F(l->Wh16); F(l->Wbk_bf); F(l->Wbk_h); }
     for (void* p : {(void*)n->x0, (void*)n->h0, (void*)n->h1, (void*)n->t, (void*)n->pool, (void*)n->pp, (void*)n->vp,
-                    (void*)n->v1, (void*)n->logits, (void*)n->value, (void*)n->soft, (void*)n->in_nchw, (void*)n->d_nb,
+                    (void*)n->v1, (void*)n->ws, (void*)n->logits, (void*)n->value, (void*)n->soft, (void*)n->in_nchw, (void*)n->d_nb,
                     (void*)n->hh[0], (void*)n->hh[1], (void*)n->hl[0], (void*)n->hl[1], (void*)n->th, (void*)n->tl,
                     (void*)n->zero})
         F(p);

@@ -17,6 +17,8 @@ struct GemmArgs {
     int H, W;                       // spatial size of one sample (taps == 9)
     const int* m_limit;             // device: active samples (leaf batch) or null
     int rows_per_sample;            // rows of one sample (H*W, P*P or 1)
+    float* part;                    // split-K workspace [splits][M][N] (FC layers) or null
+    int splits;                     // K slices when part != null
 };
 
 // bf16 trunk conv: activations stored as bf16 hi (+ lo) planes, NHWC.

@@ -65,7 +65,11 @@ __global__ __launch_bounds__(256) void gemm_f32(GemmArgs p) {
         arow_b[i] = b; arow_y[i] = r / p.W; arow_x[i] = r % p.W;
     }
     const int K = p.K;           // taps * C
-    const int nk = (p.Kpad + BK - 1) / BK;
+    const int nk_all = (p.Kpad + BK - 1) / BK;
+    // split-K (FC layers at small M): this block accumulates k-tiles [kt0, kt0 + nk)
+    const int kper = p.part ? (nk_all + p.splits - 1) / p.splits : nk_all;
+    const int kt0 = p.part ? blockIdx.y * kper : 0;
+    const int nk = max(0, min(nk_all - kt0, kper));
 
     float4 ra[4], rb[BROWS];
     auto load_stage = [&](int kt) {
@@ -126,13 +130,13 @@ __global__ __launch_bounds__(256) void gemm_f32(GemmArgs p) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
 
-    load_stage(0);
+    if (nk > 0) load_stage(kt0);
     store_stage(0);
     __syncthreads();
     const int kh = lane >> 5, l32 = lane & 31;
     for (int kt = 0; kt < nk; ++kt) {
         const int buf = kt & 1;
-        if (kt + 1 < nk) load_stage(kt + 1);
+        if (kt + 1 < nk) load_stage(kt0 + kt + 1);
         const float* as = As[buf];
         const float* bs = Bs[buf];
 #pragma unroll 4
@@ -155,6 +159,21 @@ __global__ __launch_bounds__(256) void gemm_f32(GemmArgs p) {
     }
 
     // Epilogue: C/D map col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5).
+    if (p.part) {                // raw partial sums; k_splitk_reduce adds bias + activation
+        float* part = p.part + (size_t)blockIdx.y * p.M * p.N;
+#pragma unroll
+        for (int i = 0; i < MT; ++i)
+#pragma unroll
+            for (int j = 0; j < NT; ++j) {
+                const int n = n0 + wn * TN + j * 32 + l32;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int m = m0 + wm * TM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * kh;
+                    if (n < p.N && m < Mact) part[(size_t)m * p.N + n] = acc[i][j][r];
+                }
+            }
+        return;
+    }
 #pragma unroll
     for (int i = 0; i < MT; ++i)
 #pragma unroll
@@ -237,11 +256,32 @@ __global__ void k_softmax_rows(const float* logits, float* out, int A) {
     for (int a = threadIdx.x; a < A; a += blockDim.x) out[(size_t)b * A + a] = s_sum > 0.0f ? e[a] / s_sum : e[a];
 }
 
+// split-K reduction: C = act(sum_s part[s] + bias), slices summed in order (deterministic)
+template <int ACT>
+__global__ void k_splitk_reduce(GemmArgs p) {
+    const int Mact = p.m_limit ? min(p.M, *p.m_limit * p.rows_per_sample) : p.M;
+    const size_t total = (size_t)Mact * p.N;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+        const int m = (int)(i / p.N), n = (int)(i % p.N);
+        float v = 0.0f;
+        for (int s = 0; s < p.splits; ++s) v += p.part[((size_t)s * p.M + m) * p.N + n];
+        if (p.bias) v += p.bias[n];
+        p.C[(size_t)m * p.ldc + n] = activate<ACT>(v);
+    }
+}
+
 // ---------------------------------------------------------------------------
 template <int BN, int ACT, bool RES>
 static void launch_f32(const GemmArgs& p, hipStream_t st) {
     const int nbm = (p.M + 127) / 128, nbn = (p.N + BN - 1) / BN;
-    hipLaunchKernelGGL((gemm_f32<BN, ACT, RES>), dim3(nbm * nbn), dim3(256), 0, st, p);
+    if (p.part && !RES) {
+        hipLaunchKernelGGL((gemm_f32<BN, ACT, RES>), dim3(nbm * nbn, p.splits), dim3(256), 0, st, p);
+        hipLaunchKernelGGL(k_splitk_reduce<ACT>, dim3(1024), dim3(256), 0, st, p);
+        return;
+    }
+    GemmArgs q = p;
+    q.part = nullptr;
+    hipLaunchKernelGGL((gemm_f32<BN, ACT, RES>), dim3(nbm * nbn), dim3(256), 0, st, q);
 }
 
 void az_launch_gemm_f32(const GemmArgs& p, int act, bool res, hipStream_t st) {
