@@ -17,7 +17,7 @@ from dataclasses import dataclass, field
 import numpy as np
 
 from ._lib import (AZ_EVAL_HASH, AZ_EVAL_NET, AZ_EVAL_RANDOM, AZ_PREC_BF16, AZ_PREC_BF16X3, AZ_PREC_F32, AZ_PREC_FP16, AzError,
-                   NetDesc, SearchCfg, SelfPlayCfg, check, lib)
+                   GAME_SINK, PROGRESS_FN, NetDesc, SearchCfg, SelfPlayCfg, check, lib)
 
 __all__ = ["Engine", "HipNeuralNetwork", "ParallelMCTS", "SelfPlayManager", "GameRecord", "MoveData", "AzError",
            "AZ_PREC_F32", "AZ_PREC_BF16X3", "AZ_PREC_BF16", "AZ_PREC_FP16", "AZ_EVAL_NET", "AZ_EVAL_HASH", "AZ_EVAL_RANDOM",
@@ -254,11 +254,13 @@ class ParallelMCTS:
 
 @dataclass
 class MoveData:
-    """include/alphazero/selfplay/game_record.h:21-33 (policy in CHILD order, not action-indexed)."""
+    """include/alphazero/selfplay/game_record.h:21-33 (policy in CHILD order, not action-indexed;
+    child_actions holds the matching actions, an extension the reference does not record)."""
     action: int
     policy: list
     value: float
     thinking_time_ms: int = 0
+    child_actions: list = field(default_factory=list)
 
 
 @dataclass
@@ -266,6 +268,7 @@ class GameRecord:
     board_size: int
     moves: list = field(default_factory=list)
     result: int = 0
+    game_id: int = -1
 
 
 class SelfPlayManager:
@@ -295,7 +298,36 @@ class SelfPlayManager:
     def getTemperature(self, moveNum):
         return self.finalTemperature if moveNum >= self.temperatureDropMove else self.initialTemperature
 
-    def generateGames(self, max_moves=1 << 30, on_move=None):
+    def generateGames(self, totalGames=None, max_moves=0, abort=None):
+        """SelfPlayManager::generateGames through the engine's device driver (az_selfplay_run):
+        totalGames games (default numGames) on the handle's slots; returns GameRecords by game id."""
+        total = self.numGames if totalGames is None else int(totalGames)
+        recs = [None] * total
+
+        def sink(_user, gid, bs, n, moves, result):
+            r = GameRecord(bs, result=int(result), game_id=int(gid))
+            for i in range(n):
+                mv = moves[i]
+                k = mv.n_children
+                r.moves.append(MoveData(int(mv.action), [float(mv.policy[j]) for j in range(k)], float(mv.value),
+                                        int(mv.thinking_time_ms), [int(mv.child_actions[j]) for j in range(k)]))
+            recs[gid] = r
+
+        def progress(_user, gid, move, tg, tm):
+            if self.progressCallback:
+                self.progressCallback(int(gid), int(move), int(tg), int(tm))
+
+        cfg = SelfPlayCfg(self.temperatureDropMove, self.initialTemperature, self.finalTemperature, 0)
+        flag = ctypes.c_int(0) if abort is None else abort
+        cb_sink, cb_prog = GAME_SINK(sink), PROGRESS_FN(progress)
+        check(lib().az_selfplay_run(self.mcts.h, ctypes.byref(cfg), total, int(max_moves), cb_sink, cb_prog, None,
+                                    ctypes.byref(flag)))
+        return recs
+
+    def generateGamesStepwise(self, max_moves=1 << 30, on_move=None):
+        """The playSingleGame loop driven from the host through the per-call C-ABI (search /
+        select / apply / noise), all numGames games in lock step -- the cross-check for
+        generateGames."""
         m = self.mcts
         G = self.numGames
         m.newGames()
@@ -311,7 +343,8 @@ class SelfPlayManager:
                 on_move(move, m)
             for g in range(G):
                 if live[g]:
-                    records[g].moves.append(MoveData(int(act[g]), probs[g, :nch[g]].tolist(), float(val[g])))
+                    records[g].moves.append(MoveData(int(act[g]), probs[g, :nch[g]].tolist(), float(val[g]), 0,
+                                                     cact[g, :nch[g]].tolist()))
                     if self.progressCallback:
                         self.progressCallback(g, move, G, move * G)
             act = np.where(live, act, -1).astype(np.int32)

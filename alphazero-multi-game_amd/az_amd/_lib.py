@@ -33,6 +33,14 @@ class SelfPlayCfg(ctypes.Structure):
     _fields_ = [("temp_drop_move", c_int), ("t_init", c_float), ("t_final", c_float), ("restart_finished", c_int)]
 
 
+class MoveRec(ctypes.Structure):
+    _fields_ = [("action", c_int), ("value", c_float), ("n_children", c_int), ("policy", P(c_float)),
+                ("child_actions", P(c_int)), ("thinking_time_ms", c_int64)]
+
+
+GAME_SINK = ctypes.CFUNCTYPE(None, vp, c_int, c_int, c_int, P(MoveRec), c_int)
+PROGRESS_FN = ctypes.CFUNCTYPE(None, vp, c_int, c_int, c_int, c_int64)
+
 EXPORTS = {
     "az_last_error": (ctypes.c_char_p, []),
     "az_engine_create": (c_int, [c_int, P(vp)]),
@@ -62,6 +70,7 @@ EXPORTS = {
     "az_search_enable_eval_log": (c_int, [vp, c_int, c_int]),
     "az_search_read_eval_log": (c_int, [vp, P(c_float), P(c_float), P(c_float), P(c_int)]),
     "az_selfplay_step": (c_int, [vp, P(SelfPlayCfg), P(c_int64), P(c_int64)]),
+    "az_selfplay_run": (c_int, [vp, P(SelfPlayCfg), c_int, c_int, GAME_SINK, PROGRESS_FN, vp, P(c_int)]),
 }
 
 _lib = None

@@ -12,6 +12,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
+#include <chrono>
 #include <random>
 #include <string>
 #include <unordered_set>
@@ -25,12 +26,12 @@
 __global__ void k_select(TreeDev t, int mode);
 __global__ void k_scan(TreeDev t);
 __global__ void k_expand_backup(TreeDev t, int mode);
-__global__ void k_select_action(TreeDev t, int training, float temperature, int* actions, float* values, float* probs,
+__global__ void k_select_action(TreeDev t, int training, float temperature, const float* temps, int* actions, float* values, float* probs,
                                 int* child_actions, int* nchild);
 __global__ void k_apply(TreeDev t, const int* actions, int* terminal, int* result);
 __global__ void k_compact(TreeDev t, Nodes dst, int* src_of);
 __global__ void k_noise(TreeDev t, const float* noise, const uint8_t* mask, float eps);
-__global__ void k_new_games(TreeDev t, const int* games, int n, uint32_t eval_seed);
+__global__ void k_new_games(TreeDev t, const int* games, const int* seed_ids, int n, uint32_t eval_seed);
 __global__ void k_tt_clear(TreeDev t, const int* games, int n);
 __global__ void k_root_children(TreeDev t, int g, int* act, int* N, int* VL, float* W, float* P, int* n, int* rootinfo,
                                 float* rootW);
@@ -431,7 +432,7 @@ struct az_search {
     float* d_logits = nullptr; float* d_value = nullptr;
     float* d_noise = nullptr; uint8_t* d_mask = nullptr;
     int* d_actions = nullptr; float* d_values = nullptr; float* d_probs = nullptr; int* d_cact = nullptr; int* d_nch = nullptr;
-    int* d_term = nullptr; int* d_res = nullptr; int* d_games = nullptr;
+    int* d_term = nullptr; int* d_res = nullptr; int* d_games = nullptr; int* d_seed_ids = nullptr;
     float* d_temps = nullptr;
     // host mirrors
     std::vector<int> stones, active, fresh, ply, expanded;
@@ -510,21 +511,27 @@ int search_run(az_search* s) {
     return check_err(s);
 }
 
-int search_new_games(az_search* s, const int* games, int n) {
+// (Re)start the listed slots with fresh games.  seed_ids (optional) give each game its own
+// stream id for the evaluator / noise seeds (default: the slot index), so a game's record
+// does not depend on which slot plays it.
+int search_new_games(az_search* s, const int* games, int n, const int* seed_ids = nullptr) {
     if (n <= 0) return 0;
     hipStream_t st = s->e->stream;
     for (int i = 0; i < n; ++i)
         if (games[i] < 0 || games[i] >= s->c.n_games) return fail(AZ_ERR_ARG, "game index %d out of range", games[i]);
     HIPCHK(hipMemcpyAsync(s->d_games, games, n * 4, hipMemcpyHostToDevice, st));
+    if (seed_ids) HIPCHK(hipMemcpyAsync(s->d_seed_ids, seed_ids, n * 4, hipMemcpyHostToDevice, st));
     s->t.nd = s->arena[s->cur];
-    hipLaunchKernelGGL(k_new_games, dim3(n), dim3(64), 0, st, s->t, s->d_games, n, s->c.eval_seed);
+    hipLaunchKernelGGL(k_new_games, dim3(n), dim3(64), 0, st, s->t, s->d_games, seed_ids ? s->d_seed_ids : nullptr, n,
+                       s->c.eval_seed);
     hipLaunchKernelGGL(k_tt_clear, dim3(64, n), dim3(256), 0, st, s->t, s->d_games, n);
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(st));
     for (int i = 0; i < n; ++i) {
         const int g = games[i];
         s->stones[g] = 0; s->active[g] = 1; s->fresh[g] = 1; s->ply[g] = 0;
-        s->rng[g].seed(s->c.noise_seed + (uint32_t)(s->c.noise_seed_stride * g));
+        const int id = seed_ids ? seed_ids[i] : g;
+        s->rng[g].seed(s->c.noise_seed + (uint32_t)(s->c.noise_seed_stride * id));
     }
     return 0;
 }
@@ -534,38 +541,9 @@ int search_select(az_search* s, int training, const float* temps_host, float T, 
     hipStream_t st = s->e->stream;
     const int G = s->c.n_games, A = s->t.A;
     s->t.nd = s->arena[s->cur];
-    if (!temps_host) {
-        hipLaunchKernelGGL(k_select_action, dim3(G), dim3(64), 0, st, s->t, training, T, s->d_actions, s->d_values,
-                           s->d_probs, s->d_cact, s->d_nch);
-    } else {
-        // per-game temperature: one launch per distinct T (the schedule has two values)
-        std::vector<float> ts(temps_host, temps_host + G);
-        std::vector<float> uniq = ts;
-        std::sort(uniq.begin(), uniq.end());
-        uniq.erase(std::unique(uniq.begin(), uniq.end()), uniq.end());
-        std::vector<int> sel(G);
-        std::vector<int> act_all(G, -1);
-        std::vector<float> val_all(G, 0.0f);
-        std::vector<int> nch_all(G, 0);
-        for (float u : uniq) {
-            hipLaunchKernelGGL(k_select_action, dim3(G), dim3(64), 0, st, s->t, training, u, s->d_actions, s->d_values,
-                               s->d_probs, s->d_cact, s->d_nch);
-            std::vector<int> a(G); std::vector<float> v(G); std::vector<int> nc(G);
-            HIPCHK(hipMemcpyAsync(a.data(), s->d_actions, G * 4, hipMemcpyDeviceToHost, st));
-            HIPCHK(hipMemcpyAsync(v.data(), s->d_values, G * 4, hipMemcpyDeviceToHost, st));
-            HIPCHK(hipMemcpyAsync(nc.data(), s->d_nch, G * 4, hipMemcpyDeviceToHost, st));
-            HIPCHK(hipStreamSynchronize(st));
-            for (int g = 0; g < G; ++g)
-                if (ts[g] == u) { act_all[g] = a[g]; val_all[g] = v[g]; nch_all[g] = nc[g]; }
-        }
-        if (actions) std::copy(act_all.begin(), act_all.end(), actions);
-        if (values) std::copy(val_all.begin(), val_all.end(), values);
-        if (nch) std::copy(nch_all.begin(), nch_all.end(), nch);
-        HIPCHK(hipMemcpyAsync(s->d_actions, act_all.data(), G * 4, hipMemcpyHostToDevice, st));
-        HIPCHK(hipStreamSynchronize(st));
-        (void)probs; (void)cact;
-        return 0;
-    }
+    if (temps_host) HIPCHK(hipMemcpyAsync(s->d_temps, temps_host, G * 4, hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(k_select_action, dim3(G), dim3(64), 0, st, s->t, training, T, temps_host ? s->d_temps : nullptr,
+                       s->d_actions, s->d_values, s->d_probs, s->d_cact, s->d_nch);
     HIPCHK(hipGetLastError());
     if (actions) HIPCHK(hipMemcpyAsync(actions, s->d_actions, G * 4, hipMemcpyDeviceToHost, st));
     if (values) HIPCHK(hipMemcpyAsync(values, s->d_values, G * 4, hipMemcpyDeviceToHost, st));
@@ -871,7 +849,7 @@ int az_search_create(az_engine* e, az_net* net, const az_search_cfg* c, az_searc
     SA(s->d_src_of, NG);
     if (c->eval_kind == AZ_EVAL_NET) { SA(s->d_batch, (size_t)G * A * 16); SA(s->d_logits, (size_t)G * A); SA(s->d_value, G); }
     SA(s->d_noise, (size_t)G * A); SA(s->d_mask, G); SA(s->d_actions, G); SA(s->d_values, G); SA(s->d_probs, (size_t)G * A);
-    SA(s->d_cact, (size_t)G * A); SA(s->d_nch, G); SA(s->d_term, G); SA(s->d_res, G); SA(s->d_games, G); SA(s->d_temps, G);
+    SA(s->d_cact, (size_t)G * A); SA(s->d_nch, G); SA(s->d_term, G); SA(s->d_res, G); SA(s->d_games, G); SA(s->d_seed_ids, G); SA(s->d_temps, G);
 #undef SA
     if (r) { az_search_destroy(s); return r; }
     t.zpiece = zp; t.zplayer = zpl; t.fresh_order = fo;
@@ -920,7 +898,7 @@ void az_search_destroy(az_search* s) {
                           (const void*)s->d_src_of, (const void*)s->d_batch, (const void*)s->d_logits,
                           (const void*)s->d_value, (const void*)s->d_noise, (const void*)s->d_mask, (const void*)s->d_actions,
                           (const void*)s->d_values, (const void*)s->d_probs, (const void*)s->d_cact, (const void*)s->d_nch,
-                          (const void*)s->d_term, (const void*)s->d_res, (const void*)s->d_games, (const void*)s->d_temps})
+                          (const void*)s->d_term, (const void*)s->d_res, (const void*)s->d_games, (const void*)s->d_seed_ids, (const void*)s->d_temps})
         F(p);
     delete s;
 }
@@ -1090,6 +1068,96 @@ int az_selfplay_step(az_search* s, const az_selfplay_cfg* cfg, int64_t* moves_do
         for (int g = 0; g < G; ++g) ev += c1[(size_t)g * AZ_NCNT + CNT_EVALS_TOTAL] - c0[(size_t)g * AZ_NCNT + CNT_EVALS_TOTAL];
         *evals_done += ev;
     }
+    return 0;
+}
+
+int az_selfplay_run(az_search* s, const az_selfplay_cfg* cfg, int total_games, int max_moves, az_game_sink sink,
+                    az_progress_fn progress, void* user, const volatile int* abort_flag) {
+    if (!s || !cfg || total_games < 0) return fail(AZ_ERR_ARG, "bad argument");
+    std::lock_guard<std::mutex> lk(s->mu);
+    HIPCHK(hipSetDevice(s->e->device));
+    hipStream_t st = s->e->stream;
+    const int G = s->c.n_games, A = s->t.A;
+    struct Rec {
+        std::vector<az_move_rec> moves;
+        std::vector<std::vector<float>> pol;
+        std::vector<std::vector<int>> cact;
+    };
+    std::vector<Rec> rec(G);
+    std::vector<int> game_of(G, -1);
+    int next = 0;
+    int64_t total_moves = 0;
+    // every slot idle, then the first min(G, total) games
+    std::fill(s->active.begin(), s->active.end(), 0);
+    HIPCHK(hipMemsetAsync(s->t.active, 0, (size_t)G * sizeof(int), st));
+    auto start = [&](const std::vector<int>& slots) -> int {
+        if (slots.empty()) return 0;
+        std::vector<int> ids(slots.size());
+        std::vector<uint8_t> mask(G, 0);
+        for (size_t i = 0; i < slots.size(); ++i) {
+            ids[i] = next++;
+            game_of[slots[i]] = ids[i];
+            rec[slots[i]] = Rec{};
+            mask[slots[i]] = 1;
+        }
+        if (int r = search_new_games(s, slots.data(), (int)slots.size(), ids.data())) return r;
+        return search_noise(s, s->c.dirichlet_alpha, s->c.dirichlet_eps, mask.data());   // :184
+    };
+    std::vector<int> first;
+    for (int g = 0; g < G && g < total_games; ++g) first.push_back(g);
+    if (int r = start(first)) return r;
+    std::vector<float> temps(G), values(G), probs((size_t)G * A);
+    std::vector<int> actions(G), cact((size_t)G * A), nch(G), term(G), res(G);
+    for (;;) {
+        bool any = false;
+        for (int g = 0; g < G; ++g) any |= s->active[g] != 0;
+        if (!any || (abort_flag && *abort_flag)) break;
+        const auto t0 = std::chrono::steady_clock::now();
+        if (int r = search_run(s)) return r;
+        for (int g = 0; g < G; ++g) temps[g] = s->ply[g] >= cfg->temp_drop_move ? cfg->t_final : cfg->t_init;  // :236-240
+        if (int r = search_select(s, 1, temps.data(), 0.0f, actions.data(), values.data(), probs.data(), cact.data(),
+                                  nch.data()))
+            return r;
+        const int64_t ms = std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::steady_clock::now() - t0).count();
+        std::vector<int> was_active = s->active, ply0 = s->ply;
+        for (int g = 0; g < G; ++g) {
+            if (!was_active[g] || actions[g] < 0) continue;
+            Rec& R = rec[g];
+            R.pol.emplace_back(probs.begin() + (size_t)g * A, probs.begin() + (size_t)g * A + nch[g]);
+            R.cact.emplace_back(cact.begin() + (size_t)g * A, cact.begin() + (size_t)g * A + nch[g]);
+            R.moves.push_back(az_move_rec{actions[g], values[g], nch[g], nullptr, nullptr, ms});
+            ++total_moves;
+            if (progress) progress(user, game_of[g], ply0[g], total_games, total_moves);
+        }
+        if (int r = search_apply_dev(s, term.data(), res.data())) return r;
+        std::vector<uint8_t> noise(G, 0);
+        std::vector<int> done, restart;
+        for (int g = 0; g < G; ++g) {
+            if (!was_active[g]) continue;
+            const bool fin = !s->active[g] || (max_moves > 0 && s->ply[g] >= max_moves);
+            if (!fin) {
+                if (ply0[g] % 2 == 0) noise[g] = 1;                                            // :209-211
+                continue;
+            }
+            done.push_back(g);
+        }
+        if (int r = search_noise(s, s->c.dirichlet_alpha, s->c.dirichlet_eps, noise.data())) return r;
+        for (int g : done) {
+            Rec& R = rec[g];
+            for (size_t i = 0; i < R.moves.size(); ++i) { R.moves[i].policy = R.pol[i].data(); R.moves[i].child_actions = R.cact[i].data(); }
+            const int result = s->active[g] ? 0 : res[g];
+            if (s->active[g]) {                     // cut at max_moves: park the slot
+                s->active[g] = 0;
+                HIPCHK(hipMemsetAsync(s->t.active + g, 0, sizeof(int), st));
+            }
+            if (sink) sink(user, game_of[g], s->c.board_size, (int)R.moves.size(), R.moves.data(), result);
+            rec[g] = Rec{};
+            game_of[g] = -1;
+            if (next + (int)restart.size() < total_games) restart.push_back(g);
+        }
+        if (int r = start(restart)) return r;
+    }
+    HIPCHK(hipStreamSynchronize(st));
     return 0;
 }
 

@@ -562,9 +562,11 @@ __global__ __launch_bounds__(64) void k_expand_backup(TreeDev t, int mode) {
 }
 
 // K4: visit distribution, action choice and root value per game.
-__global__ __launch_bounds__(64) void k_select_action(TreeDev t, int training, float temperature, int* actions,
-                                                      float* values, float* probs, int* child_actions, int* nchild) {
+__global__ __launch_bounds__(64) void k_select_action(TreeDev t, int training, float temperature, const float* temps,
+                                                      int* actions, float* values, float* probs, int* child_actions,
+                                                      int* nchild) {
     const int g = blockIdx.x;
+    if (temps && g < t.G) temperature = temps[g];         // per-game schedule (self-play driver)
     const int lane = threadIdx.x;
     __shared__ float c[AZ_MAXA];
     if (g >= t.G) return;
@@ -736,7 +738,8 @@ __global__ __launch_bounds__(64) void k_noise(TreeDev t, const float* noise, con
 }
 
 // K8: fresh games (empty board, new tree; TT visits cleared by the caller).
-__global__ __launch_bounds__(64) void k_new_games(TreeDev t, const int* games, int n, uint32_t eval_seed) {
+__global__ __launch_bounds__(64) void k_new_games(TreeDev t, const int* games, const int* seed_ids, int n,
+                                                  uint32_t eval_seed) {
     const int idx = blockIdx.x;
     const int lane = threadIdx.x;
     if (idx >= n) return;
@@ -755,7 +758,7 @@ __global__ __launch_bounds__(64) void k_new_games(TreeDev t, const int* games, i
         if (t.mt) {
             // std::mt19937(seed + g) seeding (libstdc++ mersenne_twister_engine::seed)
             uint32_t* st = t.mt + (size_t)g * 625;
-            st[0] = eval_seed + (uint32_t)g;
+            st[0] = eval_seed + (uint32_t)(seed_ids ? seed_ids[idx] : g);
             for (int i = 1; i < 624; ++i) st[i] = 1812433253u * (st[i - 1] ^ (st[i - 1] >> 30)) + (uint32_t)i;
             st[624] = 624;
         }

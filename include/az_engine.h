@@ -166,6 +166,35 @@ typedef struct az_selfplay_cfg {
 } az_selfplay_cfg;
 int az_selfplay_step(az_search* s, const az_selfplay_cfg* cfg, int64_t* moves_done, int64_t* evals_done);
 
+/* One committed move of a finished game: selfplay::MoveData (include/alphazero/selfplay/
+ * game_record.h:21-33).  policy[] is the visit distribution in CHILD order (as the reference
+ * records it, NaN entries at T = 0 included), child_actions[] the matching actions. */
+typedef struct az_move_rec {
+    int action;
+    float value;
+    int n_children;
+    const float* policy;
+    const int* child_actions;
+    int64_t thinking_time_ms;
+} az_move_rec;
+
+/* Receives every finished game once, on the calling thread between device steps; the arrays
+ * are valid only during the call.  result: core::GameResult (0 ONGOING, 1 DRAW, 2 WIN_PLAYER1,
+ * 3 WIN_PLAYER2; ONGOING for a game cut at max_moves). */
+typedef void (*az_game_sink)(void* user, int game_id, int board_size, int n_moves, const az_move_rec* moves,
+                             int result);
+/* SelfPlayManager progress callback (gameId, moveNum, totalGames, totalMoves),
+ * self_play_manager.cpp:198-203; called once per recorded move. */
+typedef void (*az_progress_fn)(void* user, int game_id, int move_num, int total_games, int64_t total_moves);
+
+/* SelfPlayManager::generateGames (self_play_manager.cpp:47-114 + playSingleGame :151-234):
+ * plays total_games games, game ids 0..total_games-1, on the handle's n_games device slots
+ * (a finished slot takes the next id; each game's evaluator/noise streams are seeded by its id,
+ * so records do not depend on n_games).  max_moves <= 0: play to the end.  abort (optional) is
+ * polled between moves (setAbort).  Returns 0 or an error code. */
+int az_selfplay_run(az_search* s, const az_selfplay_cfg* cfg, int total_games, int max_moves, az_game_sink sink,
+                    az_progress_fn progress, void* user, const volatile int* abort_flag);
+
 #ifdef __cplusplus
 }
 #endif

@@ -118,3 +118,36 @@ def test_gpu_small_tt_forces_replacement(engine):
         play_and_compare(m, refs, 1, 12)
     finally:
         m.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("slots", [3, 8])
+def test_gpu_selfplay_run_matches_oracle(engine, slots):
+    """az_selfplay_run (the SelfPlayManager::generateGames device driver): 8 games on `slots`
+    device slots (finished slots take the next game id) give, game by game, the oracle's
+    playSingleGame records -- actions, child-order visit distributions and root values bit for
+    bit, results -- independent of the slot count."""
+    import az_amd
+    import az_oracle as O
+    total, bs, sims, max_moves = 8, 7, 64, 30
+    refs = O.play(seed_stride=1, bs=bs, sims=sims, max_moves=max_moves, eval_kind=O.EVAL_RANDOM, eval_seed=5,
+                  n_games=total)
+    mgr = az_amd.SelfPlayManager(engine, numGames=slots, numSimulations=sims, board_size=bs,
+                                 evaluator=az_amd.AZ_EVAL_RANDOM, eval_seed=5, noise_seed=42, noise_seed_stride=1)
+    seen = []
+    mgr.setProgressCallback(lambda gid, mv, tg, tm: seen.append((gid, mv, tg, tm)))
+    try:
+        recs = mgr.generateGames(totalGames=total, max_moves=max_moves)
+    finally:
+        mgr.mcts.close()
+    assert [r.game_id for r in recs] == list(range(total))
+    for g, (rec, ref) in enumerate(zip(recs, refs)):
+        assert len(rec.moves) == len(ref["moves"]), g
+        for ply, (mv, rm) in enumerate(zip(rec.moves, ref["moves"])):
+            assert mv.action == rm["action"], (g, ply)
+            assert bits(mv.policy) == rm["probs"], (g, ply)
+            assert bits([mv.value])[0] == rm["value"], (g, ply)
+            assert len(mv.child_actions) == len(mv.policy)
+        assert rec.result == (ref["result"] if ref["terminal"] else 0), g
+    assert len(seen) == sum(len(r.moves) for r in recs)
+    assert seen[-1][2] == total and seen[-1][3] == len(seen)
