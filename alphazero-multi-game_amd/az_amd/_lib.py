@@ -13,7 +13,7 @@ P = ctypes.POINTER
 vp = ctypes.c_void_p
 
 AZ_PREC_F32, AZ_PREC_BF16X3, AZ_PREC_BF16, AZ_PREC_FP16 = 0, 1, 2, 3
-AZ_EVAL_NET, AZ_EVAL_HASH, AZ_EVAL_RANDOM = 0, 1, 2
+AZ_EVAL_NET, AZ_EVAL_HASH, AZ_EVAL_RANDOM, AZ_EVAL_UNIFORM = 0, 1, 2, 3
 
 
 class NetDesc(ctypes.Structure):

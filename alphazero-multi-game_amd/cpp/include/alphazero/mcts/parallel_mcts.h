@@ -1,0 +1,130 @@
+// alphazero/mcts/parallel_mcts.h -- ParallelMCTS of the host API on the MI355X engine.
+// One tree (one az_search game slot) per object; search() runs the Mode S simulations of
+// parallel_mcts.cpp:276-380 on the device, bit-exact with the reference
+// for the hash / random / uniform evaluators.  Selection is always the deterministic
+// (batch-inference) rule SelfPlayManager forces (selectAction: argmax of the visit
+// distribution, first max); numThreads / batch settings are accepted and ignored (the device
+// runs one simulation per game per step, Mode S).
+#pragma once
+#include <atomic>
+#include <functional>
+#include <memory>
+#include <string>
+#include <tuple>
+#include <vector>
+
+#include "alphazero/core/igamestate.h"
+#include "alphazero/mcts/transposition_table.h"
+#include "alphazero/nn/neural_network.h"
+#include "az_engine.h"
+
+namespace alphazero {
+namespace mcts {
+
+enum class MCTSNodeSelection { UCB, PUCT, PROGRESSIVE_BIAS, RAVE };
+enum class MCTSSearchMode { SERIAL, PARALLEL, BATCHED };
+
+struct MCTSConfig {
+    int numThreads = 1;
+    int numSimulations = 800;
+    float cPuct = 1.5f;
+    float fpuReduction = 0.0f;
+    int virtualLoss = 3;
+    int maxSearchDepth = 1000;
+    bool useDirichletNoise = false;
+    float dirichletAlpha = 0.03f;
+    float dirichletEpsilon = 0.25f;
+    bool useBatchInference = false;
+    bool useTemporalDifference = false;
+    float tdLambda = 0.8f;
+    bool useProgressiveWidening = false;
+    int minVisitsForWidening = 10;
+    float progressiveWideningBase = 2.0f;
+    float progressiveWideningExponent = 0.5f;
+    MCTSNodeSelection selectionStrategy = MCTSNodeSelection::PUCT;
+    int maxRetries = 3;
+    int transpositionTableSize = 1048576;
+    uint64_t cacheEntryMaxAge = 60000;
+    bool useFmapCache = false;
+    int batchSize = 16;
+    bool useBatchedMCTS = false;
+    int batchTimeoutMs = 5;
+    MCTSSearchMode searchMode = MCTSSearchMode::PARALLEL;
+    bool pinThreads = false;
+    bool deterministic = false;
+    int cacheSize = 2097152;
+};
+
+struct MCTSStats {
+    std::atomic<size_t> nodesCreated{0}, nodesExpanded{0}, nodesTotalVisits{0}, simulationCount{0};
+    std::atomic<size_t> evaluationCalls{0}, cacheHits{0}, cacheMisses{0}, batchedEvaluations{0}, totalBatches{0};
+};
+
+// The device evaluator a NeuralNetwork* maps to: HipNeuralNetwork -> AZ_EVAL_NET,
+// RandomPolicyNetwork(seed) -> AZ_EVAL_RANDOM, nullptr -> AZ_EVAL_UNIFORM; any other class is
+// refused (std::invalid_argument) -- there is no host-evaluated path.
+struct DeviceEvaluator {
+    int kind;
+    unsigned seed;
+    az_net* net;
+    az_engine* engine;
+};
+DeviceEvaluator deviceEvaluator(nn::NeuralNetwork* nn);
+
+class ParallelMCTS {
+ public:
+    ParallelMCTS(const core::IGameState& rootState, nn::NeuralNetwork* nn = nullptr, TranspositionTable* tt = nullptr,
+                 int numThreads = 1, int numSimulations = 800, float cPuct = 1.5f, float fpuReduction = 0.0f,
+                 int virtualLoss = 3);
+    ParallelMCTS(const core::IGameState& rootState, const MCTSConfig& config, nn::NeuralNetwork* nn = nullptr,
+                 TranspositionTable* tt = nullptr);
+    ~ParallelMCTS();
+    ParallelMCTS(const ParallelMCTS&) = delete;
+    ParallelMCTS& operator=(const ParallelMCTS&) = delete;
+
+    void search();
+    int selectAction(bool isTraining = false, float temperature = 1.0f);
+    std::vector<float> getActionProbabilities(float temperature = 1.0f) const;   // child order
+    std::vector<int> getChildActions() const;                                    // matching actions
+    float getRootValue() const;
+    void updateWithMove(int action);
+    void addDirichletNoise(float alpha = 0.03f, float epsilon = 0.25f);
+
+    void setNumThreads(int n) { config_.numThreads = n; }
+    void setNumSimulations(int n);
+    void setCPuct(float c);
+    void setFpuReduction(float f);
+    void setVirtualLoss(int v);
+    void setNeuralNetwork(nn::NeuralNetwork* nn);
+    void setTranspositionTable(TranspositionTable* tt);
+    void setSelectionStrategy(MCTSNodeSelection s) { config_.selectionStrategy = s; }
+    void setConfig(const MCTSConfig& config);
+    void enableBatchedMCTS(bool enable) { config_.useBatchedMCTS = enable; }
+    void setBatchSize(int b) { config_.batchSize = b; }
+    void setBatchTimeout(int ms) { config_.batchTimeoutMs = ms; }
+    void setDeterministicMode(bool enable);
+    void setDebugMode(bool enable) { debug_ = enable; }
+    void setProgressCallback(std::function<void(int, int)> cb) { progress_ = std::move(cb); }
+    void printSearchStats() const;
+    std::string getSearchInfo() const;
+    void printSearchPath(int action) const;
+    size_t getMemoryUsage() const;
+    std::vector<std::tuple<int, int, float, float>> analyzePosition(int topN = 10) const;   // (action, N, Q, P)
+    const MCTSStats& getStats() const { return stats_; }
+    az_search* handle() const { return s_; }
+
+ private:
+    void rebuild();           // (re)create the device search for the current config / root
+    MCTSConfig config_;
+    nn::NeuralNetwork* nn_;
+    TranspositionTable* tt_;
+    std::unique_ptr<core::IGameState> root_;
+    az_search* s_ = nullptr;
+    MCTSStats stats_;
+    bool debug_ = false;
+    bool searched_ = false;
+    std::function<void(int, int)> progress_;
+};
+
+}  // namespace mcts
+}  // namespace alphazero

@@ -1,0 +1,67 @@
+// alphazero/nn/hip_neural_network.h -- NeuralNetwork backed by the MI355X ConvNet
+// (az_net_* in include/az_engine.h).  predictBatch has TorchNeuralNetwork::predictBatch
+// semantics (torch_neural_network.cpp:224-363): policy = softmax over A, value [B].
+#pragma once
+#include <mutex>
+
+#include "alphazero/nn/neural_network.h"
+#include "az_engine.h"
+
+namespace alphazero {
+namespace nn {
+
+// One engine per HIP device, shared by every handle of the process (device = LOCAL_RANK or 0
+// unless given).
+az_engine* engineForDevice(int device = -1);
+
+struct NetShape {
+    int boardSize = 15, inPlanes = 11, channels = 256, blocks = 20, actionSize = 225;
+    int headChannels = 32, pool = 8, fcHidden = 256, residual = 1, convBias = 0;
+    int precision = AZ_PREC_FP16, maxBatch = 2048;
+};
+
+class HipNeuralNetwork : public NeuralNetwork {
+ public:
+    HipNeuralNetwork(const NetShape& shape, int device = -1);
+    ~HipNeuralNetwork() override;
+    HipNeuralNetwork(const HipNeuralNetwork&) = delete;
+    HipNeuralNetwork& operator=(const HipNeuralNetwork&) = delete;
+
+    void loadWeights(const std::vector<float>& blob);   // torch state_dict order, no num_batches_tracked
+    void initRandom(uint64_t seed);                      // counter-based init (oracle/net_oracle.init_blob)
+    void setPrecision(int precision);
+    // .azw file: "AZW1", 12 int32 NetShape fields, uint64 count, float32[count]
+    static std::unique_ptr<HipNeuralNetwork> load(const std::string& path, int device = -1);
+    void save(const std::string& path) const;
+
+    std::pair<std::vector<float>, float> predict(const core::IGameState& state) override;
+    void predictBatch(const std::vector<std::reference_wrapper<const core::IGameState>>& states,
+                      std::vector<std::vector<float>>& policies, std::vector<float>& values) override;
+    std::future<std::pair<std::vector<float>, float>> predictAsync(const core::IGameState& state) override;
+    bool isGpuAvailable() const override { return true; }
+    std::string getDeviceInfo() const override;
+    float getInferenceTimeMs() const override { return lastMs_; }
+    int getBatchSize() const override { return shape_.maxBatch; }
+    std::string getModelInfo() const override;
+    size_t getModelSizeBytes() const override { return params_ * sizeof(float); }
+    void benchmark(int numIterations = 100, int batchSize = 16) override;
+    void enableDebugMode(bool enable) override { debug_ = enable; }
+    void printModelSummary() const override;
+
+    az_net* handle() const { return net_; }
+    az_engine* engine() const { return eng_; }
+    const NetShape& shape() const { return shape_; }
+
+ private:
+    NetShape shape_;
+    az_engine* eng_ = nullptr;
+    az_net* net_ = nullptr;
+    size_t params_ = 0;
+    std::vector<float> blob_;
+    float lastMs_ = 0.0f;
+    bool debug_ = false;
+    std::mutex mu_;
+};
+
+}  // namespace nn
+}  // namespace alphazero

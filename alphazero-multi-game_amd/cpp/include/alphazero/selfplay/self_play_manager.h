@@ -1,0 +1,64 @@
+// alphazero/selfplay/self_play_manager.h -- SelfPlayManager of the host API.  generateGames
+// runs every game on the MI355X engine through az_selfplay_run (many games per device step,
+// the playSingleGame loop of self_play_manager.cpp:151-240 per game) instead of a host thread
+// pool; records, progress callbacks, saved files and counters keep the reference's meaning.
+#pragma once
+#include <atomic>
+#include <functional>
+#include <string>
+#include <vector>
+
+#include "alphazero/mcts/parallel_mcts.h"
+#include "alphazero/nn/neural_network.h"
+#include "alphazero/selfplay/game_record.h"
+
+namespace alphazero {
+namespace selfplay {
+
+class SelfPlayManager {
+ public:
+    // numThreads is kept for the signature; concurrency is the device slot count
+    // (setConcurrentGames, default min(numGames, 2048)).
+    SelfPlayManager(nn::NeuralNetwork* neuralNetwork, int numGames = 100, int numSimulations = 800,
+                    int numThreads = 4);
+    ~SelfPlayManager();
+
+    std::vector<GameRecord> generateGames(core::GameType gameType, int boardSize = 0, bool useVariantRules = false);
+    void setExplorationParams(float dirichletAlpha = 0.03f, float dirichletEpsilon = 0.25f,
+                              float initialTemperature = 1.0f, int temperatureDropMove = 30,
+                              float finalTemperature = 0.0f);
+    void setProgressCallback(std::function<void(int, int, int, int)> callback) { progress_ = std::move(callback); }
+    void setBatchConfig(int batchSize, int batchTimeoutMs) { batchSize_ = batchSize; batchTimeoutMs_ = batchTimeoutMs; }
+    void setSaveGames(bool saveGames, const std::string& outputDir = "games");
+    void setAbort(bool abort) { abort_ = abort ? 1 : 0; }
+    bool isRunning() const { return running_; }
+    void setMctsConfig(const mcts::MCTSConfig& config);
+    int getCompletedGamesCount() const { return completed_; }
+    int getTotalMovesCount() const { return totalMoves_; }
+    float getTemperature(int moveNum) const { return moveNum >= tempDrop_ ? tFinal_ : tInit_; }
+
+    // engine extensions
+    void setConcurrentGames(int n) { slots_ = n; }
+    void setMaxMoves(int n) { maxMoves_ = n; }
+    void setSeeds(unsigned noiseSeed, int noiseSeedStride) { noiseSeed_ = noiseSeed; noiseStride_ = noiseSeedStride; }
+
+ private:
+    nn::NeuralNetwork* nn_;
+    int numGames_, numSimulations_, numThreads_;
+    float alpha_ = 0.03f, eps_ = 0.25f, tInit_ = 1.0f, tFinal_ = 0.0f;
+    int tempDrop_ = 30;
+    int batchSize_ = 16, batchTimeoutMs_ = 5;
+    bool save_ = false;
+    std::string outDir_ = "games";
+    mcts::MCTSConfig mcts_;
+    std::function<void(int, int, int, int)> progress_;
+    volatile int abort_ = 0;
+    std::atomic<bool> running_{false};
+    std::atomic<int> completed_{0}, totalMoves_{0};
+    int slots_ = 0, maxMoves_ = 0;
+    unsigned noiseSeed_ = 42;
+    int noiseStride_ = 1;
+};
+
+}  // namespace selfplay
+}  // namespace alphazero

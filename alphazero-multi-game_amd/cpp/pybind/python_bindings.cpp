@@ -1,0 +1,285 @@
+// _alphazero_cpp: the reference's Python module surface (src/pybind/python_bindings.cpp:26-458)
+// over the MI355X host API.  The GIL is released around search / generateGames / predict /
+// predictBatch / benchmark and re-acquired for the progress callback, as in the reference.
+// Not bound: the LibTorch module classes (DDWRandWire, SEBlock, ...) and Dataset (out of scope).
+#include <pybind11/functional.h>
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include "alphazero/games/gomoku/gomoku_state.h"
+#include "alphazero/mcts/parallel_mcts.h"
+#include "alphazero/nn/hip_neural_network.h"
+#include "alphazero/nn/random_policy_network.h"
+#include "alphazero/selfplay/game_record.h"
+#include "alphazero/selfplay/self_play_manager.h"
+
+namespace py = pybind11;
+using namespace alphazero;
+
+static std::vector<std::reference_wrapper<const core::IGameState>> stateRefs(const py::list& states) {
+    std::vector<std::reference_wrapper<const core::IGameState>> v;
+    for (auto h : states) v.push_back(std::cref(h.cast<const core::IGameState&>()));
+    return v;
+}
+
+PYBIND11_MODULE(_alphazero_cpp, m) {
+    m.doc() = "AlphaZero multi-game engine, MI355X (HIP) backend";
+
+    py::enum_<core::GameType>(m, "GameType")
+        .value("GOMOKU", core::GameType::GOMOKU).value("CHESS", core::GameType::CHESS).value("GO", core::GameType::GO)
+        .export_values();
+    py::enum_<core::GameResult>(m, "GameResult")
+        .value("ONGOING", core::GameResult::ONGOING).value("DRAW", core::GameResult::DRAW)
+        .value("WIN_PLAYER1", core::GameResult::WIN_PLAYER1).value("WIN_PLAYER2", core::GameResult::WIN_PLAYER2)
+        .export_values();
+    py::enum_<mcts::MCTSNodeSelection>(m, "MCTSNodeSelection")
+        .value("UCB", mcts::MCTSNodeSelection::UCB).value("PUCT", mcts::MCTSNodeSelection::PUCT)
+        .value("PROGRESSIVE_BIAS", mcts::MCTSNodeSelection::PROGRESSIVE_BIAS).value("RAVE", mcts::MCTSNodeSelection::RAVE)
+        .export_values();
+    py::enum_<mcts::MCTSSearchMode>(m, "MCTSSearchMode")
+        .value("SERIAL", mcts::MCTSSearchMode::SERIAL).value("PARALLEL", mcts::MCTSSearchMode::PARALLEL)
+        .value("BATCHED", mcts::MCTSSearchMode::BATCHED)
+        .export_values();
+
+    py::class_<core::IGameState>(m, "IGameState")
+        .def("getLegalMoves", &core::IGameState::getLegalMoves)
+        .def("isLegalMove", &core::IGameState::isLegalMove)
+        .def("makeMove", &core::IGameState::makeMove)
+        .def("undoMove", &core::IGameState::undoMove)
+        .def("isTerminal", &core::IGameState::isTerminal)
+        .def("getGameResult", &core::IGameState::getGameResult)
+        .def("getCurrentPlayer", &core::IGameState::getCurrentPlayer)
+        .def("getBoardSize", &core::IGameState::getBoardSize)
+        .def("getActionSpaceSize", &core::IGameState::getActionSpaceSize)
+        .def("getTensorRepresentation", &core::IGameState::getTensorRepresentation)
+        .def("getEnhancedTensorRepresentation", &core::IGameState::getEnhancedTensorRepresentation)
+        .def("getHash", &core::IGameState::getHash)
+        .def("actionToString", &core::IGameState::actionToString)
+        .def("stringToAction", &core::IGameState::stringToAction)
+        .def("toString", &core::IGameState::toString)
+        .def("getMoveHistory", &core::IGameState::getMoveHistory)
+        .def("getGameType", &core::IGameState::getGameType)
+        .def("clone", [](const core::IGameState& s) { return s.clone(); });
+
+    py::class_<gomoku::GomokuState, core::IGameState>(m, "GomokuState")
+        .def(py::init<int, bool, bool, int, bool>(), py::arg("board_size") = 15, py::arg("use_renju") = false,
+             py::arg("use_omok") = false, py::arg("seed") = 0, py::arg("use_pro_long_opening") = false)
+        .def("is_occupied", &gomoku::GomokuState::is_occupied)
+        .def("get_board", &gomoku::GomokuState::get_board);
+
+    m.def("createGameState", &core::createGameState, py::arg("type"), py::arg("boardSize") = 0,
+          py::arg("variantRules") = false);
+
+    py::class_<nn::NeuralNetwork>(m, "NeuralNetwork")
+        .def("predict", [](nn::NeuralNetwork& self, const core::IGameState& s) {
+            py::gil_scoped_release release;
+            return self.predict(s);
+        })
+        .def("predictBatch", [](nn::NeuralNetwork& self, const py::list& states) {
+            auto refs = stateRefs(states);
+            std::vector<std::vector<float>> p;
+            std::vector<float> v;
+            {
+                py::gil_scoped_release release;
+                self.predictBatch(refs, p, v);
+            }
+            return py::make_tuple(p, v);
+        })
+        .def("predictBatch", [](nn::NeuralNetwork& self, const py::list& states, py::list policies, py::list values) {
+            // reference signature: output lists filled in place
+            auto refs = stateRefs(states);
+            std::vector<std::vector<float>> p;
+            std::vector<float> v;
+            {
+                py::gil_scoped_release release;
+                self.predictBatch(refs, p, v);
+            }
+            policies.attr("clear")();
+            values.attr("clear")();
+            for (auto& x : p) policies.append(py::cast(x));
+            for (float x : v) values.append(x);
+        })
+        .def("isGpuAvailable", &nn::NeuralNetwork::isGpuAvailable)
+        .def("getDeviceInfo", &nn::NeuralNetwork::getDeviceInfo)
+        .def("getInferenceTimeMs", &nn::NeuralNetwork::getInferenceTimeMs)
+        .def("getBatchSize", &nn::NeuralNetwork::getBatchSize)
+        .def("getModelInfo", &nn::NeuralNetwork::getModelInfo)
+        .def("getModelSizeBytes", &nn::NeuralNetwork::getModelSizeBytes)
+        .def("benchmark", [](nn::NeuralNetwork& self, int n, int b) {
+            py::gil_scoped_release release;
+            self.benchmark(n, b);
+        }, py::arg("numIterations") = 100, py::arg("batchSize") = 16)
+        .def("enableDebugMode", &nn::NeuralNetwork::enableDebugMode)
+        .def("is_gil_safe", [](nn::NeuralNetwork&) { return true; });
+
+    py::class_<nn::HipNeuralNetwork, nn::NeuralNetwork>(m, "HipNeuralNetwork")
+        .def(py::init([](int boardSize, int channels, int blocks, int inPlanes, int precision, int maxBatch,
+                         int residual, int convBias, int device) {
+                 nn::NetShape s;
+                 s.boardSize = boardSize; s.channels = channels; s.blocks = blocks; s.inPlanes = inPlanes;
+                 s.actionSize = boardSize * boardSize; s.precision = precision; s.maxBatch = maxBatch;
+                 s.residual = residual; s.convBias = convBias;
+                 return std::make_unique<nn::HipNeuralNetwork>(s, device);
+             }),
+             py::arg("boardSize") = 15, py::arg("channels") = 256, py::arg("blocks") = 20, py::arg("inPlanes") = 11,
+             py::arg("precision") = (int)AZ_PREC_FP16, py::arg("maxBatch") = 2048, py::arg("residual") = 1,
+             py::arg("convBias") = 0, py::arg("device") = -1)
+        .def("loadWeights", [](nn::HipNeuralNetwork& self, py::array_t<float, py::array::c_style | py::array::forcecast> a) {
+            std::vector<float> blob(a.data(), a.data() + a.size());
+            self.loadWeights(blob);
+        })
+        .def("initRandom", &nn::HipNeuralNetwork::initRandom)
+        .def("setPrecision", &nn::HipNeuralNetwork::setPrecision)
+        .def("save", &nn::HipNeuralNetwork::save)
+        .def_static("load", &nn::HipNeuralNetwork::load, py::arg("path"), py::arg("device") = -1);
+
+    py::class_<nn::RandomPolicyNetwork, nn::NeuralNetwork>(m, "RandomPolicyNetwork")
+        .def(py::init<core::GameType, int, unsigned int>(), py::arg("gameType"), py::arg("boardSize") = 0,
+             py::arg("seed") = 0);
+
+    m.def("createNeuralNetwork", &nn::NeuralNetwork::create, py::arg("modelPath"), py::arg("gameType"),
+          py::arg("boardSize") = 0, py::arg("useGpu") = true);
+
+    py::class_<mcts::MCTSConfig>(m, "MCTSConfig")
+        .def(py::init<>())
+        .def_readwrite("numThreads", &mcts::MCTSConfig::numThreads)
+        .def_readwrite("numSimulations", &mcts::MCTSConfig::numSimulations)
+        .def_readwrite("cPuct", &mcts::MCTSConfig::cPuct)
+        .def_readwrite("fpuReduction", &mcts::MCTSConfig::fpuReduction)
+        .def_readwrite("virtualLoss", &mcts::MCTSConfig::virtualLoss)
+        .def_readwrite("maxSearchDepth", &mcts::MCTSConfig::maxSearchDepth)
+        .def_readwrite("useDirichletNoise", &mcts::MCTSConfig::useDirichletNoise)
+        .def_readwrite("dirichletAlpha", &mcts::MCTSConfig::dirichletAlpha)
+        .def_readwrite("dirichletEpsilon", &mcts::MCTSConfig::dirichletEpsilon)
+        .def_readwrite("useBatchInference", &mcts::MCTSConfig::useBatchInference)
+        .def_readwrite("useTemporalDifference", &mcts::MCTSConfig::useTemporalDifference)
+        .def_readwrite("tdLambda", &mcts::MCTSConfig::tdLambda)
+        .def_readwrite("useProgressiveWidening", &mcts::MCTSConfig::useProgressiveWidening)
+        .def_readwrite("minVisitsForWidening", &mcts::MCTSConfig::minVisitsForWidening)
+        .def_readwrite("progressiveWideningBase", &mcts::MCTSConfig::progressiveWideningBase)
+        .def_readwrite("progressiveWideningExponent", &mcts::MCTSConfig::progressiveWideningExponent)
+        .def_readwrite("selectionStrategy", &mcts::MCTSConfig::selectionStrategy)
+        .def_readwrite("batchSize", &mcts::MCTSConfig::batchSize)
+        .def_readwrite("useBatchedMCTS", &mcts::MCTSConfig::useBatchedMCTS)
+        .def_readwrite("batchTimeoutMs", &mcts::MCTSConfig::batchTimeoutMs)
+        .def_readwrite("searchMode", &mcts::MCTSConfig::searchMode)
+        .def_readwrite("transpositionTableSize", &mcts::MCTSConfig::transpositionTableSize);
+
+    py::class_<mcts::MCTSStats>(m, "MCTSStats")
+        .def_property_readonly("nodesCreated", [](const mcts::MCTSStats& s) { return s.nodesCreated.load(); })
+        .def_property_readonly("nodesExpanded", [](const mcts::MCTSStats& s) { return s.nodesExpanded.load(); })
+        .def_property_readonly("nodesTotalVisits", [](const mcts::MCTSStats& s) { return s.nodesTotalVisits.load(); })
+        .def_property_readonly("simulationCount", [](const mcts::MCTSStats& s) { return s.simulationCount.load(); })
+        .def_property_readonly("evaluationCalls", [](const mcts::MCTSStats& s) { return s.evaluationCalls.load(); })
+        .def_property_readonly("cacheHits", [](const mcts::MCTSStats& s) { return s.cacheHits.load(); })
+        .def_property_readonly("cacheMisses", [](const mcts::MCTSStats& s) { return s.cacheMisses.load(); })
+        .def_property_readonly("batchedEvaluations", [](const mcts::MCTSStats& s) { return s.batchedEvaluations.load(); })
+        .def_property_readonly("totalBatches", [](const mcts::MCTSStats& s) { return s.totalBatches.load(); });
+
+    py::class_<mcts::TranspositionTable>(m, "TranspositionTable")
+        .def(py::init<size_t, size_t>(), py::arg("size") = 1048576, py::arg("numShards") = 1024)
+        .def("getSize", &mcts::TranspositionTable::getSize)
+        .def("getHitRate", &mcts::TranspositionTable::getHitRate)
+        .def("getLookups", &mcts::TranspositionTable::getLookups)
+        .def("getHits", &mcts::TranspositionTable::getHits)
+        .def("getEntryCount", &mcts::TranspositionTable::getEntryCount)
+        .def("getMemoryUsageBytes", &mcts::TranspositionTable::getMemoryUsageBytes)
+        .def("clear", &mcts::TranspositionTable::clear)
+        .def("resize", &mcts::TranspositionTable::resize);
+
+    py::class_<mcts::ParallelMCTS>(m, "ParallelMCTS")
+        .def(py::init<const core::IGameState&, nn::NeuralNetwork*, mcts::TranspositionTable*, int, int, float, float, int>(),
+             py::arg("rootState"), py::arg("nn") = nullptr, py::arg("tt") = nullptr, py::arg("numThreads") = 1,
+             py::arg("numSimulations") = 800, py::arg("cPuct") = 1.5f, py::arg("fpuReduction") = 0.0f,
+             py::arg("virtualLoss") = 3, py::keep_alive<1, 3>(), py::keep_alive<1, 4>())
+        .def(py::init<const core::IGameState&, const mcts::MCTSConfig&, nn::NeuralNetwork*, mcts::TranspositionTable*>(),
+             py::arg("rootState"), py::arg("config"), py::arg("nn") = nullptr, py::arg("tt") = nullptr,
+             py::keep_alive<1, 4>(), py::keep_alive<1, 5>())
+        .def("search", [](mcts::ParallelMCTS& self) {
+            py::gil_scoped_release release;
+            self.search();
+        })
+        .def("selectAction", &mcts::ParallelMCTS::selectAction, py::arg("isTraining") = false, py::arg("temperature") = 1.0f)
+        .def("getActionProbabilities", &mcts::ParallelMCTS::getActionProbabilities, py::arg("temperature") = 1.0f)
+        .def("getChildActions", &mcts::ParallelMCTS::getChildActions)
+        .def("getRootValue", &mcts::ParallelMCTS::getRootValue)
+        .def("updateWithMove", &mcts::ParallelMCTS::updateWithMove)
+        .def("addDirichletNoise", &mcts::ParallelMCTS::addDirichletNoise, py::arg("alpha") = 0.03f,
+             py::arg("epsilon") = 0.25f)
+        .def("setNumThreads", &mcts::ParallelMCTS::setNumThreads)
+        .def("setNumSimulations", &mcts::ParallelMCTS::setNumSimulations)
+        .def("setCPuct", &mcts::ParallelMCTS::setCPuct)
+        .def("setFpuReduction", &mcts::ParallelMCTS::setFpuReduction)
+        .def("setVirtualLoss", &mcts::ParallelMCTS::setVirtualLoss)
+        .def("setNeuralNetwork", &mcts::ParallelMCTS::setNeuralNetwork, py::keep_alive<1, 2>())
+        .def("setTranspositionTable", &mcts::ParallelMCTS::setTranspositionTable, py::keep_alive<1, 2>())
+        .def("setSelectionStrategy", &mcts::ParallelMCTS::setSelectionStrategy)
+        .def("setConfig", &mcts::ParallelMCTS::setConfig)
+        .def("enableBatchedMCTS", &mcts::ParallelMCTS::enableBatchedMCTS)
+        .def("setBatchSize", &mcts::ParallelMCTS::setBatchSize)
+        .def("setBatchTimeout", &mcts::ParallelMCTS::setBatchTimeout)
+        .def("setDeterministicMode", &mcts::ParallelMCTS::setDeterministicMode)
+        .def("setDebugMode", &mcts::ParallelMCTS::setDebugMode)
+        .def("printSearchStats", &mcts::ParallelMCTS::printSearchStats)
+        .def("getSearchInfo", &mcts::ParallelMCTS::getSearchInfo)
+        .def("printSearchPath", &mcts::ParallelMCTS::printSearchPath)
+        .def("getMemoryUsage", &mcts::ParallelMCTS::getMemoryUsage)
+        .def("analyzePosition", &mcts::ParallelMCTS::analyzePosition, py::arg("topN") = 10)
+        .def("getStats", &mcts::ParallelMCTS::getStats, py::return_value_policy::reference_internal);
+
+    py::class_<selfplay::MoveData>(m, "MoveData")
+        .def(py::init<>())
+        .def_readwrite("action", &selfplay::MoveData::action)
+        .def_readwrite("policy", &selfplay::MoveData::policy)
+        .def_readwrite("value", &selfplay::MoveData::value)
+        .def_readwrite("thinking_time_ms", &selfplay::MoveData::thinking_time_ms)
+        .def("toJson", &selfplay::MoveData::toJson)
+        .def_static("fromJson", &selfplay::MoveData::fromJson);
+
+    py::class_<selfplay::GameRecord>(m, "GameRecord")
+        .def(py::init<core::GameType, int, bool>(), py::arg("gameType"), py::arg("boardSize"),
+             py::arg("useVariantRules") = false)
+        .def("addMove", &selfplay::GameRecord::addMove)
+        .def("setResult", &selfplay::GameRecord::setResult)
+        .def("getMetadata", &selfplay::GameRecord::getMetadata)
+        .def("getMoves", &selfplay::GameRecord::getMoves)
+        .def("getResult", &selfplay::GameRecord::getResult)
+        .def("toJson", &selfplay::GameRecord::toJson)
+        .def("saveToFile", &selfplay::GameRecord::saveToFile)
+        .def("setTimestamp", [](selfplay::GameRecord& r, int64_t unix_seconds) {
+            r.setTimestamp(std::chrono::system_clock::from_time_t((std::time_t)unix_seconds));
+        })
+        .def_static("fromJson", &selfplay::GameRecord::fromJson)
+        .def_static("loadFromFile", &selfplay::GameRecord::loadFromFile);
+    m.def("jsonNumber", &selfplay::jsonNumber);
+
+    py::class_<selfplay::SelfPlayManager>(m, "SelfPlayManager")
+        .def(py::init<nn::NeuralNetwork*, int, int, int>(), py::arg("neuralNetwork"), py::arg("numGames") = 100,
+             py::arg("numSimulations") = 800, py::arg("numThreads") = 4, py::keep_alive<1, 2>())
+        .def("generateGames", [](selfplay::SelfPlayManager& self, core::GameType t, int bs, bool variant) {
+            py::gil_scoped_release release;
+            return self.generateGames(t, bs, variant);
+        }, py::arg("gameType"), py::arg("boardSize") = 0, py::arg("useVariantRules") = false)
+        .def("setExplorationParams", &selfplay::SelfPlayManager::setExplorationParams,
+             py::arg("dirichletAlpha") = 0.03f, py::arg("dirichletEpsilon") = 0.25f,
+             py::arg("initialTemperature") = 1.0f, py::arg("temperatureDropMove") = 30,
+             py::arg("finalTemperature") = 0.0f)
+        .def("setProgressCallback", [](selfplay::SelfPlayManager& self, std::function<void(int, int, int, int)> cb) {
+            self.setProgressCallback([cb](int g, int mv, int tg, int tm) {
+                py::gil_scoped_acquire acquire;
+                cb(g, mv, tg, tm);
+            });
+        })
+        .def("setBatchConfig", &selfplay::SelfPlayManager::setBatchConfig)
+        .def("setSaveGames", &selfplay::SelfPlayManager::setSaveGames, py::arg("saveGames"),
+             py::arg("outputDir") = "games")
+        .def("setAbort", &selfplay::SelfPlayManager::setAbort)
+        .def("isRunning", &selfplay::SelfPlayManager::isRunning)
+        .def("setMctsConfig", &selfplay::SelfPlayManager::setMctsConfig)
+        .def("getCompletedGamesCount", &selfplay::SelfPlayManager::getCompletedGamesCount)
+        .def("getTotalMovesCount", &selfplay::SelfPlayManager::getTotalMovesCount)
+        .def("setConcurrentGames", &selfplay::SelfPlayManager::setConcurrentGames)
+        .def("setMaxMoves", &selfplay::SelfPlayManager::setMaxMoves)
+        .def("setSeeds", &selfplay::SelfPlayManager::setSeeds);
+}

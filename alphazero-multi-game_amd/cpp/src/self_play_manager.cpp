@@ -1,0 +1,122 @@
+// SelfPlayManager of the host API: generateGames = az_selfplay_run over device game slots.
+#include "alphazero/selfplay/self_play_manager.h"
+
+#include <chrono>
+#include <ctime>
+#include <filesystem>
+#include <iomanip>
+#include <iostream>
+#include <sstream>
+
+#include "alphazero/games/gomoku/gomoku_state.h"
+
+namespace alphazero {
+namespace selfplay {
+
+SelfPlayManager::SelfPlayManager(nn::NeuralNetwork* nn, int numGames, int numSimulations, int numThreads)
+    : nn_(nn), numGames_(numGames), numSimulations_(numSimulations), numThreads_(numThreads) {}
+
+SelfPlayManager::~SelfPlayManager() { abort_ = 1; }
+
+void SelfPlayManager::setExplorationParams(float a, float e, float ti, int drop, float tf) {
+    alpha_ = a; eps_ = e; tInit_ = ti; tempDrop_ = drop; tFinal_ = tf;
+}
+
+void SelfPlayManager::setSaveGames(bool s, const std::string& dir) { save_ = s; outDir_ = dir; }
+
+void SelfPlayManager::setMctsConfig(const mcts::MCTSConfig& c) {
+    mcts_ = c;
+    if (c.useBatchedMCTS) { batchSize_ = c.batchSize; batchTimeoutMs_ = c.batchTimeoutMs; }
+}
+
+namespace {
+struct RunCtx {
+    SelfPlayManager* self;
+    std::vector<GameRecord>* records;
+    core::GameType type;
+    bool variant;
+    bool save;
+    std::string dir;
+    std::function<void(int, int, int, int)>* progress;
+    std::atomic<int>* completed;
+    std::atomic<int>* totalMoves;
+    std::vector<char>* done;
+};
+
+void sink(void* user, int gid, int bs, int n, const az_move_rec* moves, int result) {
+    auto* c = static_cast<RunCtx*>(user);
+    GameRecord rec(c->type, bs, c->variant);
+    for (int i = 0; i < n; ++i)
+        rec.addMove(moves[i].action, std::vector<float>(moves[i].policy, moves[i].policy + moves[i].n_children),
+                    moves[i].value, moves[i].thinking_time_ms);
+    rec.setResult((core::GameResult)result);
+    if (c->save) {   // <dir>/<id:03>_<YYYYmmdd_HHMMSS>.json (self_play_manager.cpp:220-229)
+        const std::time_t t = std::time(nullptr);
+        std::tm tm{};
+        localtime_r(&t, &tm);
+        std::ostringstream f;
+        f << c->dir << "/" << std::setfill('0') << std::setw(3) << gid << "_" << std::put_time(&tm, "%Y%m%d_%H%M%S")
+          << ".json";
+        rec.saveToFile(f.str());
+    }
+    (*c->records)[gid] = std::move(rec);
+    (*c->done)[gid] = 1;
+    c->completed->fetch_add(1);
+}
+
+void progress(void* user, int gid, int move, int total_games, int64_t /*total_moves*/) {
+    auto* c = static_cast<RunCtx*>(user);
+    const int tm = c->totalMoves->fetch_add(1);
+    if (*c->progress) (*c->progress)(gid, move, total_games, tm);
+}
+}  // namespace
+
+std::vector<GameRecord> SelfPlayManager::generateGames(core::GameType type, int boardSize, bool variant) {
+    if (type != core::GameType::GOMOKU) throw std::invalid_argument("generateGames: Gomoku only (Go/Chess: row f2)");
+    if (variant) throw std::invalid_argument("generateGames: variant rules are not supported");
+    running_ = true;
+    abort_ = 0;
+    completed_ = 0;
+    totalMoves_ = 0;
+    const int bs = boardSize > 0 ? boardSize : 15;
+    if (save_) std::filesystem::create_directories(outDir_);
+    std::vector<GameRecord> records(numGames_, GameRecord(type, bs, variant));
+    std::vector<char> done(numGames_, 0);
+    try {
+        const mcts::DeviceEvaluator ev = mcts::deviceEvaluator(nn_);
+        az_search_cfg c{};
+        c.n_games = slots_ > 0 ? slots_ : std::min(std::max(numGames_, 1), 2048);
+        c.board_size = bs;
+        c.num_simulations = numSimulations_;
+        c.c_puct = mcts_.cPuct > 0.0f ? mcts_.cPuct : 1.5f;       // :177-178
+        c.fpu_reduction = mcts_.fpuReduction >= 0.0f ? mcts_.fpuReduction : 0.1f;
+        c.virtual_loss = mcts_.virtualLoss;
+        c.eval_kind = ev.kind;
+        c.eval_seed = ev.seed;
+        c.zobrist_seed = 12345u;
+        c.noise_seed = noiseSeed_;
+        c.noise_seed_stride = noiseStride_;
+        c.use_dirichlet_each_search = mcts_.useDirichletNoise ? 1 : 0;
+        c.dirichlet_alpha = alpha_;
+        c.dirichlet_eps = eps_;
+        c.tt_log2 = 20;                                            // TranspositionTable tt(1048576), :159
+        az_search* s = nullptr;
+        if (az_search_create(ev.engine, ev.net, &c, &s)) throw std::runtime_error(az_last_error());
+        az_selfplay_cfg sc{tempDrop_, tInit_, tFinal_, 0};
+        RunCtx ctx{this, &records, type, variant, save_, outDir_, &progress_, &completed_, &totalMoves_, &done};
+        const int rc = az_selfplay_run(s, &sc, numGames_, maxMoves_, sink, progress, &ctx, &abort_);
+        az_search_destroy(s);
+        if (rc) throw std::runtime_error(az_last_error());
+    } catch (...) {
+        running_ = false;
+        throw;
+    }
+    running_ = false;
+    std::vector<GameRecord> out;   // finished games in game-id order (all of them unless aborted)
+    for (int g = 0; g < numGames_; ++g)
+        if (done[g]) out.push_back(std::move(records[g]));
+    return out;
+}
+
+}  // namespace selfplay
+}  // namespace alphazero

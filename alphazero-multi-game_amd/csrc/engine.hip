@@ -805,7 +805,7 @@ int az_search_create(az_engine* e, az_net* net, const az_search_cfg* c, az_searc
     if (!e || !c || !out) return fail(AZ_ERR_ARG, "null argument");
     const int bs = c->board_size, A = bs * bs, G = c->n_games;
     if (bs < 3 || A > AZ_MAXA || G < 1 || c->num_simulations < 0 || c->virtual_loss < 0 || c->tt_log2 < 4 ||
-        c->tt_log2 > 24 || c->eval_kind < 0 || c->eval_kind > 2)
+        c->tt_log2 > 24 || c->eval_kind < 0 || c->eval_kind > 3)
         return fail(AZ_ERR_ARG, "unsupported search configuration");
     if (c->eval_kind == AZ_EVAL_NET) {
         if (!net) return fail(AZ_ERR_ARG, "AZ_EVAL_NET needs a network");

@@ -458,6 +458,13 @@ __global__ __launch_bounds__(64) void k_expand_backup(TreeDev t, int mode) {
                 const float sum = s_scalar[0];
                 if (sum > 0.0f) for (int a = lane; a < A; a += 64) pol[a] = pol[a] / sum;
                 value = t.net_value[slot];
+            } else if (t.eval_kind == 3) {
+                // no network: 1/|legal| on the legal actions, value 0 (parallel_mcts.cpp:903-916)
+                const float u = n > 0 ? 1.0f / (float)n : 0.0f;
+                for (int a = lane; a < A; a += 64) pol[a] = 0.0f;
+                __syncthreads();
+                for (int i = lane; i < n; i += 64) pol[legal[i]] = u;
+                value = 0.0f;
             } else if (t.eval_kind == 1) {
                 const uint64_t key = hash_eval_key(hash, hist6);
                 for (int a = lane; a < A; a += 64) pol[a] = hash_eval_p(key, a);

@@ -100,7 +100,8 @@ int az_net_predict_batch(az_net* n, const float* planes, int B, float* policy, f
 enum az_eval_kind {
     AZ_EVAL_NET = 0,    /* the ConvNet above (az_search_create's `net`) */
     AZ_EVAL_HASH = 1,   /* HashEvaluator (oracle/ref_harness.cpp hash_eval), tests */
-    AZ_EVAL_RANDOM = 2  /* RandomPolicyNetwork(seed + game) semantics (random_policy_network.cpp) */
+    AZ_EVAL_RANDOM = 2, /* RandomPolicyNetwork(seed + game) semantics (random_policy_network.cpp) */
+    AZ_EVAL_UNIFORM = 3 /* no network: ParallelMCTS::evaluateState fallback (parallel_mcts.cpp:903-916) */
 };
 typedef struct az_search_cfg {
     int n_games;          /* G: independent games (trees) on this device */

@@ -199,6 +199,21 @@ struct RandomEval : Evaluator {
     }
 };
 
+// No network: ParallelMCTS::evaluateState's fallback (src/mcts/parallel_mcts.cpp:903-916),
+// 1/|legal| on the legal actions, value 0.
+struct UniformEval : Evaluator {
+    void eval(int, const State& s, std::vector<float>& p, float& v) override {
+        ++calls;
+        p.assign(s.A, 0.0f);
+        auto legal = s.legal();
+        if (!legal.empty()) {
+            const float u = 1.0f / (float)legal.size();
+            for (int m : legal) p[m] = u;
+        }
+        v = 0.0f;
+    }
+};
+
 // Network evaluator through a user callback: planes -> raw logits [A] + value; the
 // softmax of TorchNeuralNetwork::predictBatch (torch_neural_network.cpp:296-316) is
 // applied here.  Replay evaluator: the callback returns final (post-softmax) policy.
@@ -524,7 +539,7 @@ char* dup(const std::string& s) {
 extern "C" {
 
 struct az_oracle_cfg {
-    int bs, sims, max_moves, vl, noise_each_search, temp_drop, tt_log2, eval_kind;   // eval: 0 hash, 1 random, 2 net cb, 3 replay cb
+    int bs, sims, max_moves, vl, noise_each_search, temp_drop, tt_log2, eval_kind;   // eval: 0 hash, 1 random, 2 net cb, 3 replay cb, 4 uniform
     float cpuct, fpu, alpha, eps, t_init, t_final;
     unsigned noise_seed, zobrist_seed, eval_seed;
     int n_games;
@@ -548,7 +563,9 @@ char* az_oracle_play(const az_oracle_cfg* c, int seed_stride, az_eval_cb cb, voi
     o << "[";
     HashEval he; RandomEval re(c->n_games, c->eval_seed);
     CallbackEval ne(cb, user, c->eval_kind == 2);
-    Evaluator* ev = c->eval_kind == 0 ? (Evaluator*)&he : c->eval_kind == 1 ? (Evaluator*)&re : (Evaluator*)&ne;
+    UniformEval ue;
+    Evaluator* ev = c->eval_kind == 0 ? (Evaluator*)&he : c->eval_kind == 1 ? (Evaluator*)&re
+                  : c->eval_kind == 4 ? (Evaluator*)&ue : (Evaluator*)&ne;
     for (int g = 0; g < c->n_games; ++g) {
         Cfg gc = cfg;
         gc.noise_seed = c->noise_seed + (unsigned)(seed_stride * g);

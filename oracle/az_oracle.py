@@ -15,7 +15,7 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "_build", "liboracle.so")
 
-EVAL_HASH, EVAL_RANDOM, EVAL_NET, EVAL_REPLAY = 0, 1, 2, 3
+EVAL_HASH, EVAL_RANDOM, EVAL_NET, EVAL_REPLAY, EVAL_UNIFORM = 0, 1, 2, 3, 4
 
 # int cb(void* user, int game, const float* planes, int n_planes, int A, float* policy, float* value)
 EVAL_CB = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_float),

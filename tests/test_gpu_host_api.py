@@ -1,0 +1,122 @@
+"""The C++ host API (_alphazero_cpp) on the GPU: ParallelMCTS / SelfPlayManager /
+HipNeuralNetwork reproduce the reference's own golden games and the oracle bit for bit,
+through the same classes and methods a reference user calls."""
+import gzip
+import json
+import os
+
+import numpy as np
+import pytest
+
+az = pytest.importorskip("_alphazero_cpp", reason="build the host module: make -C alphazero-multi-game_amd")
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def bits(a):
+    return np.asarray(a, np.float32).view(np.uint32).tolist()
+
+
+def host_play(m, moves, n=None):
+    """SelfPlayManager::playSingleGame's loop (self_play_manager.cpp:184-215) on a ParallelMCTS."""
+    m.addDirichletNoise(0.03, 0.25)
+    out = []
+    for ply in range(len(moves) if n is None else n):
+        m.search()
+        T = 1.0 if ply < 30 else 0.0
+        probs = m.getActionProbabilities(T)
+        act = m.selectAction(True, T)
+        val = m.getRootValue()
+        out.append((act, bits(probs), bits([val])[0]))
+        m.updateWithMove(act)
+        if ply % 2 == 0:
+            m.addDirichletNoise(0.03, 0.25)
+    return out
+
+
+@pytest.mark.gpu
+def test_host_parallel_mcts_random_policy_matches_reference_golden():
+    """RandomPolicyNetwork(seed) game of the patched reference (7x7, 200 sims) through
+    ParallelMCTS(GomokuState, RandomPolicyNetwork)."""
+    games = json.load(gzip.open(os.path.join(GOLD, "ref_games.json.gz"), "rt"))
+    ref = next(g for g in games if g["case"][3] == "random")
+    bs, sims, _, _, seed, _, cp, fpu = ref["case"]
+    net = az.RandomPolicyNetwork(az.GameType.GOMOKU, bs, seed)
+    m = az.ParallelMCTS(az.GomokuState(bs), net, None, 1, sims, cp, fpu, 3)
+    got = host_play(m, ref["moves"])
+    for ply, (g, r) in enumerate(zip(got, ref["moves"])):
+        assert g == (r["action"], r["probs"], r["value"]), ply
+
+
+@pytest.mark.gpu
+def test_host_parallel_mcts_without_network_matches_oracle():
+    """nn = nullptr: evaluateState's uniform fallback (parallel_mcts.cpp:903-916)."""
+    import az_oracle as O
+    ref = O.play(bs=9, sims=100, max_moves=12, eval_kind=O.EVAL_UNIFORM)[0]
+    cfg = az.MCTSConfig()
+    cfg.numSimulations = 100
+    tt = az.TranspositionTable(1 << 20)
+    m = az.ParallelMCTS(az.GomokuState(9), cfg, None, tt)
+    got = host_play(m, ref["moves"])
+    for ply, (g, r) in enumerate(zip(got, ref["moves"])):
+        assert g == (r["action"], r["probs"], r["value"]), ply
+    assert tt.getLookups() == ref["moves"][-1]["tt_lookups"] and tt.getHits() == ref["moves"][-1]["tt_hits"]
+    top = m.analyzePosition(3)
+    assert len(top) <= 3 and all(len(t) == 4 for t in top)
+
+
+@pytest.mark.gpu
+def test_host_selfplay_manager_matches_oracle(tmp_path):
+    """SelfPlayManager.generateGames (device driver, 3 slots for 6 games) == the oracle's
+    playSingleGame records; saved files load back identical."""
+    import az_oracle as O
+    total, bs, sims, max_moves = 6, 7, 64, 30
+    refs = O.play(seed_stride=1, bs=bs, sims=sims, max_moves=max_moves, eval_kind=O.EVAL_RANDOM, eval_seed=5,
+                  n_games=total)
+    net = az.RandomPolicyNetwork(az.GameType.GOMOKU, bs, 5)
+    mgr = az.SelfPlayManager(net, total, sims, 4)
+    mgr.setConcurrentGames(3)
+    mgr.setMaxMoves(max_moves)
+    mgr.setSeeds(42, 1)
+    mgr.setSaveGames(True, str(tmp_path))
+    calls = []
+    mgr.setProgressCallback(lambda g, mv, tg, tm: calls.append((g, mv, tg, tm)))
+    recs = mgr.generateGames(az.GameType.GOMOKU, bs, False)
+    assert len(recs) == total and mgr.getCompletedGamesCount() == total and not mgr.isRunning()
+    for g, (rec, ref) in enumerate(zip(recs, refs)):
+        mv = rec.getMoves()
+        assert len(mv) == len(ref["moves"]), g
+        for ply, (m, r) in enumerate(zip(mv, ref["moves"])):
+            assert (m.action, bits(m.policy), bits([m.value])[0]) == (r["action"], r["probs"], r["value"]), (g, ply)
+        assert int(rec.getResult()) == (ref["result"] if ref["terminal"] else 0)
+    assert len(calls) == mgr.getTotalMovesCount() == sum(len(r["moves"]) for r in refs)
+    files = sorted(os.listdir(tmp_path))
+    assert len(files) == total and files[0].startswith("000_")
+    back = az.GameRecord.loadFromFile(str(tmp_path / files[0]))
+    assert [m.action for m in back.getMoves()] == [m.action for m in recs[0].getMoves()]
+
+
+@pytest.mark.gpu
+def test_host_hip_network_predict_batch_matches_torch():
+    """HipNeuralNetwork.predictBatch (planes built from GomokuState) == softmax of the fp32
+    restatement, <= 1e-4 (north_star tolerance) at f32 precision."""
+    import net_oracle
+    import az_amd
+    net = az.HipNeuralNetwork(boardSize=15, channels=64, blocks=2, precision=0, maxBatch=8)
+    desc = az_amd.gomoku_net_desc(board_size=15, channels=64, blocks=2, max_batch=8)
+    blob = net_oracle.init_blob(desc, seed=9)
+    net.loadWeights(blob)
+    states = []
+    rng = np.random.default_rng(2)
+    for i in range(5):
+        s = az.GomokuState(15)
+        for _ in range(i * 7):
+            s.makeMove(int(rng.choice(s.getLegalMoves())))
+        states.append(s)
+    pol, val = net.predictBatch(states)
+    x = np.stack([np.asarray(s.getEnhancedTensorRepresentation(), np.float32) for s in states])
+    rl, rv = net_oracle.forward(desc, blob, x)
+    assert np.abs(np.asarray(pol) - net_oracle.softmax_policy(rl)).max() <= 1e-4
+    assert np.abs(np.asarray(val) - rv).max() <= 1e-4
+    p1, v1 = net.predict(states[3])
+    assert np.allclose(p1, pol[3]) and abs(v1 - val[3]) < 1e-6
+    assert net.isGpuAvailable() and net.getBatchSize() == 8 and "MI355X" in net.getDeviceInfo()

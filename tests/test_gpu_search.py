@@ -89,16 +89,18 @@ def test_gpu_search_matches_reference_golden(engine, idx):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("bs,sims,games,ev", [(9, 64, 16, "hash"), (7, 96, 8, "random"), (15, 128, 6, "hash")])
+@pytest.mark.parametrize("bs,sims,games,ev", [(9, 64, 16, "hash"), (7, 96, 8, "random"), (15, 128, 6, "hash"),
+                                              (9, 100, 4, "uniform")])
 def test_gpu_multigame_matches_oracle(engine, bs, sims, games, ev):
-    """G independent games with per-game noise seeds (42 + g) and evaluator seeds."""
+    """G independent games with per-game noise seeds (42 + g) and evaluator seeds; "uniform" is
+    ParallelMCTS without a network (parallel_mcts.cpp:903-916)."""
     import az_amd
     import az_oracle as O
-    kind = O.EVAL_HASH if ev == "hash" else O.EVAL_RANDOM
+    kind = {"hash": O.EVAL_HASH, "random": O.EVAL_RANDOM, "uniform": O.EVAL_UNIFORM}[ev]
+    dev = {"hash": az_amd.AZ_EVAL_HASH, "random": az_amd.AZ_EVAL_RANDOM, "uniform": az_amd.AZ_EVAL_UNIFORM}[ev]
     max_moves = 40
     refs = O.play(seed_stride=1, bs=bs, sims=sims, max_moves=max_moves, eval_kind=kind, eval_seed=5, n_games=games)
-    m = az_amd.ParallelMCTS(engine, n_games=games, board_size=bs, num_simulations=sims,
-                            evaluator=az_amd.AZ_EVAL_HASH if ev == "hash" else az_amd.AZ_EVAL_RANDOM, eval_seed=5,
+    m = az_amd.ParallelMCTS(engine, n_games=games, board_size=bs, num_simulations=sims, evaluator=dev, eval_seed=5,
                             noise_seed=42, noise_seed_stride=1)
     try:
         play_and_compare(m, refs, games, max_moves)
