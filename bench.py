@@ -93,21 +93,18 @@ def main():
     desc = az_amd.gomoku_net_desc(board_size=a.board, channels=a.channels, blocks=a.blocks,
                                   precision=PREC[a.precision], max_batch=a.games)
     net = az_amd.HipNeuralNetwork(eng, desc)
+    from az_amd import dist as azdist
     blob = None
     if dist is None:
         net.init_random(a.seed)
     else:
-        import torch
-        t = torch.empty(net.num_params, dtype=torch.float32, device=f"cuda:{local}")
-        if rank == 0:
-            blob = net_oracle.init_blob(desc, a.seed)
-            t.copy_(torch.from_numpy(blob))
-        dist.broadcast(t, src=0)           # RCCL over xGMI: one weight version
-        blob = t.cpu().numpy()
+        blob = net_oracle.init_blob(desc, a.seed) if rank == 0 else None
+        blob = azdist.broadcast_weights(dist, blob, net.num_params, f"cuda:{local}")   # RCCL over xGMI, once
         net.load_weights(blob)
+    sh = azdist.shard(rank, a.games)       # global game ids / seeds of this rank
     m = az_amd.ParallelMCTS(eng, n_games=a.games, board_size=a.board, num_simulations=a.sims,
-                            evaluator=az_amd.AZ_EVAL_NET, net=net, noise_seed=42 + rank * a.games,
-                            noise_seed_stride=1)
+                            evaluator=az_amd.AZ_EVAL_NET, net=net, noise_seed=sh["noise_seed"],
+                            noise_seed_stride=sh["noise_seed_stride"])
     m.newGames()
     m.addDirichletNoise(0.03, 0.25)
     for _ in range(a.warmup):
@@ -129,13 +126,7 @@ def main():
     trunk_ms, launches, forwards = net.profile_read()
 
     if dist is not None:
-        import torch
-        x = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
-        dist.all_reduce(x, op=dist.ReduceOp.MAX)
-        elapsed = float(x.item())
-        c = torch.tensor([moves, evals], dtype=torch.float64, device=f"cuda:{local}")
-        dist.all_reduce(c, op=dist.ReduceOp.SUM)
-        moves, evals = int(c[0].item()), int(c[1].item())
+        elapsed, (moves, evals) = azdist.reduce_counters(dist, elapsed, [moves, evals], f"cuda:{local}")
 
     if rank == 0:
         HW = a.board * a.board

@@ -153,3 +153,28 @@ def test_gpu_selfplay_run_matches_oracle(engine, slots):
         assert rec.result == (ref["result"] if ref["terminal"] else 0), g
     assert len(seen) == sum(len(r.moves) for r in recs)
     assert seen[-1][2] == total and seen[-1][3] == len(seen)
+
+
+@pytest.mark.gpu
+def test_gpu_sharded_selfplay_independent_of_rank_count(engine):
+    """Two "ranks" (az_amd.dist.shard seeds, 3 games each) play exactly the records a single
+    device produces for the same 6 global game ids."""
+    import az_amd
+    from az_amd import dist as azdist
+    bs, sims, max_moves = 7, 48, 20
+
+    def run(n, sh):
+        mgr = az_amd.SelfPlayManager(engine, numGames=n, numSimulations=sims, board_size=bs,
+                                     evaluator=az_amd.AZ_EVAL_RANDOM, eval_seed=sh["eval_seed"],
+                                     noise_seed=sh["noise_seed"], noise_seed_stride=sh["noise_seed_stride"])
+        try:
+            return mgr.generateGames(totalGames=n, max_moves=max_moves)
+        finally:
+            mgr.mcts.close()
+
+    one = run(6, azdist.shard(0, 6, eval_seed=5))
+    two = run(3, azdist.shard(0, 3, eval_seed=5)) + run(3, azdist.shard(1, 3, eval_seed=5))
+    for g, (a, b) in enumerate(zip(one, two)):
+        assert [(m.action, bits(m.policy), bits([m.value])[0]) for m in a.moves] == \
+               [(m.action, bits(m.policy), bits([m.value])[0]) for m in b.moves], g
+        assert a.result == b.result
