@@ -436,6 +436,12 @@ struct az_search {
     float* d_temps = nullptr;
     // host mirrors
     std::vector<int> stones, active, fresh, ply, expanded;
+    // az_search_profile
+    bool prof = false;
+    std::vector<hipEvent_t> evpool;
+    size_t evused = 0;
+    int64_t prof_steps = 0;
+    std::vector<long long> prof_cnt0;
     std::vector<std::mt19937> rng;
     std::vector<float> h_noise; std::vector<uint8_t> h_mask;
     std::mutex mu;
@@ -452,11 +458,24 @@ int check_err(az_search* s) {
 }
 
 // One batched step over all games: select -> (network) -> expand/backup.
+// tree-kernel timing (az_search_profile): events around K1 and K3 of simulation steps
+static hipEvent_t prof_event(az_search* s) {
+    if (s->evused >= s->evpool.size()) {
+        hipEvent_t ev;
+        if (hipEventCreate(&ev) != hipSuccess) return nullptr;
+        s->evpool.push_back(ev);
+    }
+    return s->evpool[s->evused++];
+}
+
 int search_step(az_search* s, int mode) {
     hipStream_t st = s->e->stream;
     const int G = s->c.n_games;
     s->t.nd = s->arena[s->cur];
+    const bool prof = s->prof && mode == MODE_SIM;
+    if (prof) HIPCHK(hipEventRecord(prof_event(s), st));
     hipLaunchKernelGGL(k_select, dim3(G), dim3(64), 0, st, s->t, mode);
+    if (prof) HIPCHK(hipEventRecord(prof_event(s), st));
     if (s->c.eval_kind == AZ_EVAL_NET) {
         hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, st, s->t);
         az_launch_gather_planes(s->t.planes, s->d_batch, s->t.eval_games, s->t.n_eval, s->t.A * 16, G, st);
@@ -466,7 +485,9 @@ int search_step(az_search* s, int mode) {
         s->net->prof = prof;
         if (r) return r;
     }
+    if (prof) HIPCHK(hipEventRecord(prof_event(s), st));
     hipLaunchKernelGGL(k_expand_backup, dim3(G), dim3(64), 0, st, s->t, mode);
+    if (prof) { HIPCHK(hipEventRecord(prof_event(s), st)); s->prof_steps += 1; }
     HIPCHK(hipGetLastError());
     return 0;
 }
@@ -880,6 +901,7 @@ int az_search_create(az_engine* e, az_net* net, const az_search_cfg* c, az_searc
 }
 
 void az_search_destroy(az_search* s) {
+    if (s) for (hipEvent_t ev : s->evpool) (void)hipEventDestroy(ev);
     if (!s) return;
     hipSetDevice(s->e->device);
     auto F = [](const void* p) { if (p) hipFree((void*)p); };
@@ -1158,6 +1180,50 @@ int az_selfplay_run(az_search* s, const az_selfplay_cfg* cfg, int total_games, i
         if (int r = start(restart)) return r;
     }
     HIPCHK(hipStreamSynchronize(st));
+    return 0;
+}
+
+int az_search_profile(az_search* s, int enable) {
+    if (!s) return fail(AZ_ERR_ARG, "null search");
+    std::lock_guard<std::mutex> lk(s->mu);
+    HIPCHK(hipSetDevice(s->e->device));
+    HIPCHK(hipStreamSynchronize(s->e->stream));
+    s->prof = enable != 0;
+    s->evused = 0;
+    s->prof_steps = 0;
+    s->prof_cnt0.assign((size_t)s->c.n_games * AZ_NCNT, 0);
+    HIPCHK(hipMemcpy(s->prof_cnt0.data(), s->t.cnt, s->prof_cnt0.size() * 8, hipMemcpyDeviceToHost));
+    return 0;
+}
+
+int az_search_profile_read(az_search* s, double* select_ms, double* expand_ms, int64_t* sim_steps,
+                           int64_t* select_bytes, int64_t* expand_bytes) {
+    if (!s) return fail(AZ_ERR_ARG, "null search");
+    std::lock_guard<std::mutex> lk(s->mu);
+    HIPCHK(hipSetDevice(s->e->device));
+    HIPCHK(hipStreamSynchronize(s->e->stream));
+    double sel = 0.0, exp = 0.0;
+    for (size_t i = 0; i + 3 < s->evused; i += 4) {
+        float a = 0.0f, b = 0.0f;
+        HIPCHK(hipEventElapsedTime(&a, s->evpool[i], s->evpool[i + 1]));
+        HIPCHK(hipEventElapsedTime(&b, s->evpool[i + 2], s->evpool[i + 3]));
+        sel += a;
+        exp += b;
+    }
+    std::vector<long long> c((size_t)s->c.n_games * AZ_NCNT);
+    HIPCHK(hipMemcpy(c.data(), s->t.cnt, c.size() * 8, hipMemcpyDeviceToHost));
+    long long bs = 0, be = 0;
+    for (int g = 0; g < s->c.n_games; ++g) {
+        const size_t o = (size_t)g * AZ_NCNT;
+        const long long* c0 = s->prof_cnt0.empty() ? nullptr : s->prof_cnt0.data() + o;
+        bs += c[o + CNT_BYTES_SEL] - (c0 ? c0[CNT_BYTES_SEL] : 0);
+        be += c[o + CNT_BYTES_EXP] - (c0 ? c0[CNT_BYTES_EXP] : 0);
+    }
+    if (select_ms) *select_ms = sel;
+    if (expand_ms) *expand_ms = exp;
+    if (sim_steps) *sim_steps = s->prof_steps;
+    if (select_bytes) *select_bytes = bs;
+    if (expand_bytes) *expand_bytes = be;
     return 0;
 }
 

@@ -14,7 +14,8 @@
 enum { ST_NONE = 0, ST_TERMINAL = 1, ST_TTHIT = 2, ST_EVAL = 3, ST_EXPANDED = 4 };
 enum { MODE_SIM = 0, MODE_ROOT_NOISE = 1, MODE_ROOT_SEARCH = 2 };
 enum { FL_EXPANDED = 1, FL_TERMINAL = 2 };   // result (GameResult) in bits 2..3
-enum { CNT_EVALS = 0, CNT_LOOKUPS = 1, CNT_HITS = 2, CNT_SIMS = 3, CNT_NODES = 4, CNT_EVALS_TOTAL = 5 };  // [5] survives new games
+enum { CNT_EVALS = 0, CNT_LOOKUPS = 1, CNT_HITS = 2, CNT_SIMS = 3, CNT_NODES = 4, CNT_EVALS_TOTAL = 5,
+       CNT_BYTES_SEL = 6, CNT_BYTES_EXP = 7 };   // [5..7] survive new games; 6/7: algorithmic HBM bytes of K1 / K3
 enum { ERR_NODES = 1, ERR_PATH = 2, ERR_RING = 4, ERR_BATCH = 8 };
 
 struct Nodes {          // one arena: [G][ncap]

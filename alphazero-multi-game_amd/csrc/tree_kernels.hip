@@ -238,6 +238,7 @@ __global__ __launch_bounds__(64) void k_select(TreeDev t, int mode) {
     int node = root;
     int status = ST_NONE;
     float value = 0.0f;
+    long long scanned = 0;       // child records read by the PUCT scans (16 B each: N, W, VL, P)
 
     if (mode != MODE_SIM) {
         // Root expansion: expandNode (noise) / search() root branch.
@@ -260,6 +261,7 @@ __global__ __launch_bounds__(64) void k_select(TreeDev t, int mode) {
             if (node == root) { pN = rN; pVL = rVL; pW = rW; }
             else { pN = nd.N[node]; pVL = nd.VL[node]; pW = nd.W[node]; }
             const int fc = nd.first[node], nc = nd.cnt[node];
+            scanned += nc;
             const float sq = sqrtf((float)pN);
             float best = -FLT_MAX;
             int bi = INT_MAX;
@@ -365,6 +367,15 @@ __global__ __launch_bounds__(64) void k_select(TreeDev t, int mode) {
         t.need_eval[g] = (status == ST_EVAL && t.eval_kind == 0) ? 1 : 0;
     }
     for (int i = lane; i <= depth; i += 64) t.path[(size_t)g * AZ_DMAX + i] = spath[i];
+    if (lane == 0 && mode == MODE_SIM) {
+        // algorithmic bytes: child scans, node headers (first/cnt/flag/act 9 B) and VL read-modify-
+        // write (12 B + 12 B) along the path, root board, TT probe (12 B, +20 on a hit), planes
+        // (64 B per cell, fp32 NHWC16) when the leaf goes to the network, path record
+        long long b = scanned * 16 + (long long)(depth + 1) * (9 + 24 + 4) + t.A + 12;
+        if (status == ST_TTHIT) b += 20;
+        if (status == ST_EVAL) b += 64LL * t.A;
+        cnt[CNT_BYTES_SEL] += b;
+    }
 }
 
 // K2: deterministic compaction of the leaves that need the network (one block).
@@ -419,6 +430,9 @@ __global__ __launch_bounds__(64) void k_expand_backup(TreeDev t, int mode) {
     int hist6[6]; int player, stones; uint64_t hash;
     build_leaf(t, g, lane, nd, spath, depth, board, hist6, player, stones, hash);
     float value = t.lvalue[g];
+    // algorithmic bytes: path (4 + 2 B per level), root board, then below: policy / TT / ring,
+    // new child records (25 B), VL-removal + backup read-modify-write (24 B per path node)
+    long long kb = (long long)plen * 6 + A;
 
     if (status == ST_EVAL || status == ST_TTHIT) {
         // legal moves in child order (gomoku_state.cpp:531-578)
@@ -547,6 +561,7 @@ __global__ __launch_bounds__(64) void k_expand_backup(TreeDev t, int mode) {
             nd.first[leaf] = first; nd.cnt[leaf] = (int16_t)n; nd.flag[leaf] = (uint8_t)(nd.flag[leaf] | FL_EXPANDED);
             cnt[CNT_NODES] = first + n;
         }
+        kb += 25LL * n + 7 + 4LL * n + (status == ST_EVAL ? 4LL * A + 4 + 24 : 0);
     } else if (status == ST_EXPANDED) {
         value = nd.N[leaf] == 0 ? 0.0f : nd.W[leaf] / (float)nd.N[leaf];
     }
@@ -565,7 +580,9 @@ __global__ __launch_bounds__(64) void k_expand_backup(TreeDev t, int mode) {
             nd.N[nn] = N; nd.VL[nn] = VL; nd.W[nn] = W;
         }
         cnt[CNT_SIMS] += 1;
+        kb += 24LL * plen;
     }
+    if (lane == 0 && mode == MODE_SIM) cnt[CNT_BYTES_EXP] += kb;
 }
 
 // K4: visit distribution, action choice and root value per game.

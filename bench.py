@@ -115,6 +115,7 @@ def main():
             dist.barrier()
     barrier()
     net.profile(True)
+    m.profile(True)
     t0 = time.perf_counter()
     moves = evals = 0
     for _ in range(a.steps):
@@ -124,6 +125,7 @@ def main():
     elapsed = time.perf_counter() - t0     # selfplayStep returns after a stream sync
     barrier()
     trunk_ms, launches, forwards = net.profile_read()
+    tree = m.profile_read()
 
     if dist is not None:
         elapsed, (moves, evals) = azdist.reduce_counters(dist, elapsed, [moves, evals], f"cuda:{local}")
@@ -159,6 +161,17 @@ def main():
                          "launches": launches, "avg_launch_ms": per_launch_ms,
                          "flops_per_launch": per_launch_flops},
         }
+        steps = max(1, tree["sim_steps"])
+        out["tree_kernels"] = {
+            name: {"avg_launch_us": 1e3 * tree[f"{k}_ms"] / steps,
+                   "bytes_per_launch": tree[f"{k}_bytes"] / steps,
+                   "GB_per_s": tree[f"{k}_bytes"] / max(1e-12, 1e-3 * tree[f"{k}_ms"]) / 1e9,
+                   "frac_of_hbm_peak": tree[f"{k}_bytes"] / max(1e-12, 1e-3 * tree[f"{k}_ms"]) / 8.0e12}
+            for name, k in (("k_select", "select"), ("k_expand_backup", "expand"))}
+        out["tree_kernels"]["note"] = ("rank-0 HIP events around each kernel of every simulation step; algorithmic "
+                                       "bytes counted by the kernels (child records scanned, path VL/backup "
+                                       "read-modify-writes, new nodes, leaf planes); latency-bound (one wave per game, "
+                                       "dependent tree levels), peak 8 TB/s")
         tr = pmc_traffic(a, per_launch_flops / (conv_flops_per_eval / (2 * a.blocks)) if launches else 0)
         if tr:
             out["roofline"].update(tr)

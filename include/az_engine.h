@@ -149,6 +149,13 @@ int az_search_root_children(az_search* s, int game, int* actions, int* N, int* V
 int az_search_root_node(az_search* s, int game, int* N, int* VL, float* W);
 /* Counters per game: [0] evals, [1] tt_lookups, [2] tt_hits, [3] simulations, [4] nodes used. */
 int az_search_counters(az_search* s, int game, int64_t* out5);
+/* Tree-kernel profiling: enable resets; read returns the summed GPU time of K1 (selection +
+ * VL + leaf planes) and K3 (expansion + backup) over the simulation steps since enable (HIP
+ * events on the engine stream), the number of such steps, and the algorithmic HBM bytes the
+ * kernels moved (child records scanned, path updates, new nodes, planes; counted per game). */
+int az_search_profile(az_search* s, int enable);
+int az_search_profile_read(az_search* s, double* select_ms, double* expand_ms, int64_t* sim_steps,
+                           int64_t* select_bytes, int64_t* expand_bytes);
 /* Evaluation log (tests): every evaluation of game `game` appends (policy[A] post-softmax,
  * value) in evaluation order; planes too when planes != 0.  Capacity in evaluations. */
 int az_search_enable_eval_log(az_search* s, int game, int capacity);
