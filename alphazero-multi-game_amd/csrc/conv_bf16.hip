@@ -651,9 +651,10 @@ __device__ __forceinline__ uint16_t v4_store(float f) {
 // diagnostic build only: per-block s_memrealtime (100 MHz) at start / end of main loop / end,
 // slot p.stamp (the engine numbers the trunk launches of a forward 0..2*blocks-1)
 constexpr int V4_SLOTS = 48, V4_MAXBLK = 4096;
-__device__ unsigned long long g_v4_stamps[V4_SLOTS * V4_MAXBLK * 4];
-#define V4_STAMP(k) do { if (threadIdx.x == 0 && blockIdx.x < V4_MAXBLK && p.stamp >= 0 && p.stamp < V4_SLOTS) \
-    g_v4_stamps[((size_t)p.stamp * V4_MAXBLK + blockIdx.x) * 4 + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+__device__ unsigned long long g_v4_stamps[V4_SLOTS * V4_MAXBLK * 8];
+#define V4_STAMP(k) do { if (threadIdx.x == 0 && blockIdx.x < V4_MAXBLK && p.stamp >= 0 && p.stamp < V4_SLOTS) { \
+    g_v4_stamps[((size_t)p.stamp * V4_MAXBLK + blockIdx.x) * 8 + (k)] = __builtin_amdgcn_s_memrealtime(); \
+    if ((k) < 2) g_v4_stamps[((size_t)p.stamp * V4_MAXBLK + blockIdx.x) * 8 + 5 + (k)] = __builtin_amdgcn_s_memtime(); } } while (0)
 extern "C" int az_diag_v4_stamps(unsigned long long* out, int n) {
     return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_v4_stamps), sizeof(unsigned long long) * (size_t)n);
 }
@@ -952,7 +953,7 @@ __device__ __forceinline__ void lgkm_wait6(F (&a)[4], F (&b)[2]) {
                  : "i"(N));
 }
 
-template <int MODE>
+template <int MODE, int DW, int PPT_ = 0>
 __global__ __launch_bounds__(512, 1) void conv3x3_v5(ConvBf16Args p) {
     static_assert(MODE == 1 || MODE == 2, "v5: single-plane modes");
     typedef Half16<MODE> H16;
@@ -969,8 +970,11 @@ __global__ __launch_bounds__(512, 1) void conv3x3_v5(ConvBf16Args p) {
     constexpr int LDS = LDS_BIAS + BNT * 4;
     constexpr int A_INS = BOARDS * 2 * (V4_HROWS / 64);    // 20 pieces per chunk
     constexpr int B_INS = 9 * 2 * (BNT / 64);              // 36 pieces per chunk
-    constexpr int PAX = (A_INS + 7) / 8, PBX = (B_INS + 7) / 8;
-    static_assert(PAX + PBX <= 9, "one DMA piece per tap");
+    // DW waves issue the DMA pieces (all 8, or only the first wave of each SIMD pair, which
+    // otherwise idles at the chunk barrier); PPT pieces per tap between the MFMAs
+    constexpr int PAX = (A_INS + DW - 1) / DW, PBX = (B_INS + DW - 1) / DW;
+    constexpr int PPT = PPT_ ? PPT_ : (PAX + PBX + 8) / 9;   // PPT_ = 2 with DW = 8: all pieces in taps 0-3
+    static_assert(PPT <= 2, "at most two DMA pieces per tap");
     constexpr int WN = 2, TM = 128;
     constexpr int FM = 4, FN = 2;
     typedef typename std::conditional<MODE == 2, f16x8, bf16x8>::type frag;
@@ -990,31 +994,31 @@ __global__ __launch_bounds__(512, 1) void conv3x3_v5(ConvBf16Args p) {
     if (tid < BNT) sbias[tid] = p.bias[n0 + tid];     // visible after the first chunk barrier
     const int C = p.C, GI = C / 8, GO = p.N / 8;
     const int NCH = C / 16;
-    const int PA = (A_INS - wave + 7) / 8, PB = (B_INS - wave + 7) / 8;
+    const int PA = wave < DW ? (A_INS - wave + DW - 1) / DW : 0, PB = wave < DW ? (B_INS - wave + DW - 1) / DW : 0;
 
-    const uint16_t* a_src[PAX];
-    int a_ch[PAX], a_off[PAX];
+    // per-piece source element offsets (32-bit: < 2^31 elements) and LDS destinations;
+    // a_el < 0 marks a padding row (read from the zero page)
+    int a_el[PAX], a_ch[PAX], a_off[PAX];
 #pragma unroll
     for (int j = 0; j < PAX; ++j) {
-        const int q = wave + 8 * j;
+        const int q = wave + DW * j;
         const int rb = q % 5, ch = (q / 5) % 2, bd = q / 10;
         const int hr = rb * 64 + lane;
         const int Y = hr / 17, X = hr - Y * 17;
         const int b = b0 + bd;
         const bool ok = q < A_INS && hr < 289 && Y >= 1 && Y <= 15 && X >= 1 && X <= 15 && b < nboards;
-        a_src[j] = ok ? p.Ahi + (((size_t)b * GI + ch) * 225 + (Y - 1) * 15 + (X - 1)) * 8 : nullptr;
+        a_el[j] = ok ? (int)((((size_t)b * GI + ch) * 225 + (Y - 1) * 15 + (X - 1)) * 8) : -1;
         a_ch[j] = ch;
         a_off[j] = bd * A_PLANE + ch * (V4_HROWS * 16) + rb * 1024;
     }
-    const uint16_t* b_src[PBX];
-    int b_off[PBX];
+    int b_el[PBX], b_off[PBX];
 #pragma unroll
     for (int j = 0; j < PBX; ++j) {
-        const int q = min(wave + 8 * j, B_INS - 1);
+        const int q = min(wave + DW * j, B_INS - 1);
         constexpr int RB = BNT / 64;
         const int rb = q % RB, ch = (q / RB) % 2, t = q / (2 * RB);
         const int n = n0 + rb * 64 + lane;
-        b_src[j] = p.Bblk + ((size_t)(t * 2 + ch) * p.N + n) * 8;
+        b_el[j] = ((t * 2 + ch) * p.N + n) * 8;
         b_off[j] = t * B_TAP + ch * BNT * 16 + rb * 1024;
     }
     uint8_t* abuf = lds;
@@ -1023,12 +1027,12 @@ __global__ __launch_bounds__(512, 1) void conv3x3_v5(ConvBf16Args p) {
     auto issue_piece = [&](int k, int c) {
         if (k < PAX) {
             if (k >= PA) return;
-            const uint16_t* src = a_src[k] ? a_src[k] + (size_t)c * (2 * 225 * 8) : p.zero + a_ch[k] * 8;
+            const uint16_t* src = a_el[k] >= 0 ? p.Ahi + a_el[k] + (size_t)c * (2 * 225 * 8) : p.zero + a_ch[k] * 8;
             __builtin_amdgcn_global_load_lds((g_void_t*)src, (lds_void_t*)(abuf + (c & 1) * A_BUF + a_off[k]), 16, 0, 0);
         } else {
             const int j = k - PAX;
             if (j >= PB) return;
-            __builtin_amdgcn_global_load_lds((g_void_t*)(b_src[j] + (size_t)c * 144 * p.N),
+            __builtin_amdgcn_global_load_lds((g_void_t*)(p.Bblk + b_el[j] + (size_t)c * 144 * p.N),
                                              (lds_void_t*)(bbuf + (c & 1) * B_BUF + b_off[j]), 16, 0, 0);
         }
     };
@@ -1048,11 +1052,20 @@ __global__ __launch_bounds__(512, 1) void conv3x3_v5(ConvBf16Args p) {
     const int q0 = (wm * TM) % 256;
     const uint32_t a_lane = lds_addr(abuf) + bd_w * A_PLANE + lh * (V4_HROWS * 16) + (q0 + l32) * 16;
     const uint32_t b_lane = lds_addr(bbuf) + lh * BNT * 16 + (wn * (BNT / WN) + l32) * 16;
+#ifdef AZ_V4_STAMPS
+    unsigned long long t_wait = 0, t_issue = 0;
+#endif
     for (int c = 0; c < NCH; ++c) {
+#ifdef AZ_V4_STAMPS
+        const unsigned long long tw0 = __builtin_amdgcn_s_memtime();
+#endif
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __builtin_amdgcn_sched_barrier(0);
         __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_sched_barrier(0);
+#ifdef AZ_V4_STAMPS
+        t_wait += __builtin_amdgcn_s_memtime() - tw0;
+#endif
         const uint32_t ab = a_lane + (c & 1) * A_BUF;
         const uint32_t bb = b_lane + (c & 1) * B_BUF;
         auto load = [&](int tap, frag (&a)[FM], frag (&b)[FN]) {
@@ -1068,9 +1081,16 @@ __global__ __launch_bounds__(512, 1) void conv3x3_v5(ConvBf16Args p) {
 #ifndef AZ_V5_NOLOAD
                 // next chunk's LDS-DMA pieces ride between this chunk's MFMAs, one per tap (two per
                 // tap early in the chunk, or staggered between SIMD-mate waves, measured no better)
-                if (i == FM / 2 && c + 1 < NCH && tap < PAX + PBX) {
+                const int pk = tap * PPT + (PPT == 1 ? 0 : i / 2);
+                if ((PPT == 1 ? i == FM / 2 : (i & 1)) && c + 1 < NCH && pk < PAX + PBX) {
                     __builtin_amdgcn_sched_barrier(0);
-                    issue_piece(tap, c + 1);
+#ifdef AZ_V4_STAMPS
+                    const unsigned long long ti0 = __builtin_amdgcn_s_memtime();
+#endif
+                    issue_piece(pk, c + 1);
+#ifdef AZ_V4_STAMPS
+                    t_issue += __builtin_amdgcn_s_memtime() - ti0;
+#endif
                     __builtin_amdgcn_sched_barrier(0);
                 }
 #endif
@@ -1105,6 +1125,12 @@ __global__ __launch_bounds__(512, 1) void conv3x3_v5(ConvBf16Args p) {
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __syncthreads();
     V4_STAMP(1);
+#ifdef AZ_V4_STAMPS
+    if (threadIdx.x == 0 && blockIdx.x < V4_MAXBLK && p.stamp >= 0 && p.stamp < V4_SLOTS)
+        g_v4_stamps[((size_t)p.stamp * V4_MAXBLK + blockIdx.x) * 8 + 3] = t_wait;   // shader cycles in wait+barrier
+    if (threadIdx.x == 0 && blockIdx.x < V4_MAXBLK && p.stamp >= 0 && p.stamp < V4_SLOTS)
+        g_v4_stamps[((size_t)p.stamp * V4_MAXBLK + blockIdx.x) * 8 + 4] = t_issue;
+#endif
 
     // epilogue in two column passes (acc[.][j], j = 0, 1), both boards at once: the staged
     // fp32 tile is [2 boards][225 pixels][64 + 4], so the other pass's accumulators are the only
@@ -1193,6 +1219,308 @@ __global__ __launch_bounds__(512, 1) void conv3x3_v5(ConvBf16Args p) {
     V4_STAMP(2);
 }
 
+// ===========================================================================
+// v6: the v5 board-halo conv on v_mfma_f32_16x16x32_{f16,bf16}.  The 16x16x32 shape draws less
+// power than 32x32x16 for the same FLOPs, and this kernel is power-bound (the chip holds
+// ~1.8 GHz under v5; a bare-loop microbenchmark, tools/microbench/mfma_shape.hip, runs
+// 16x16x32 at ~2.0 GHz vs ~1.6 GHz).  K = 32 per MFMA = one tap x 32 channels, so a chunk is
+// 32 channels: the halo of both boards (40 KB) is double-buffered per chunk and the weights run
+// through a 3-deep ring of tap rows (3 taps x 8 KB), one barrier per tap row.  A wave owns 128
+// rows x 64 columns as 8 x 4 tiles of 16x16 (128 accumulators).  Fragments of the next tap are
+// read while the current tap's MFMAs issue: B(t+1) first, then the low / high halves of A(t+1)
+// as soon as the matching half of tap t has issued.  DMA pieces (weights of tap row s+2, and at
+// the first row of a chunk the halo of the next chunk) ride between MFMAs.
+template <int OFF, typename F>
+__device__ __forceinline__ void ds_rd_off(F& d, uint32_t addr) {
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(d) : "v"(addr), "i"(OFF) : "memory");
+}
+template <int I, int N, typename Fn>
+__device__ __forceinline__ void static_for(Fn&& f) {
+    if constexpr (I < N) {
+        f(std::integral_constant<int, I>{});
+        static_for<I + 1, N>(f);
+    }
+}
+
+#define AZ_LGKM_WAIT(N, X)                                                                        \
+    asm volatile("s_waitcnt lgkmcnt(" #N ")" : "+v"(X[0]), "+v"(X[1]), "+v"(X[2]), "+v"(X[3]))
+
+template <int MODE>
+__global__ __launch_bounds__(512, 1) void conv3x3_v6(ConvBf16Args p) {
+    static_assert(MODE == 1 || MODE == 2, "v6: single-plane modes");
+    typedef Half16<MODE> H16;
+    constexpr int BNT = 128, BOARDS = 2, KG = 4;
+    constexpr int A_PLANE = KG * V4_HROWS * 16;          // one board, 32 channels: [4 groups][320 rows][16 B]
+    constexpr int A_BUF = BOARDS * A_PLANE;              // 40 KB
+    constexpr int B_TAP = KG * BNT * 16;                 // 8 KB
+    constexpr int B_STAGE = 3 * B_TAP;                   // one tap row, 24 KB
+    constexpr int LDS_MAIN = 2 * A_BUF + 3 * B_STAGE;    // 152 KB
+    constexpr int SC = 64, SLD = SC + 4;
+    constexpr int LDS_EPI = BOARDS * 256 * SLD * 4;      // 136 KB
+    constexpr int LDS_BIAS = LDS_MAIN > LDS_EPI ? LDS_MAIN : LDS_EPI;
+    constexpr int LDS = LDS_BIAS + BNT * 4;
+    constexpr int A_INS = BOARDS * KG * (V4_HROWS / 64); // 40 pieces per chunk
+    constexpr int B_INS = 3 * KG * (BNT / 64);           // 24 pieces per tap row
+    constexpr int PA = A_INS / 8, PB = B_INS / 8;        // 5 / 3 per wave
+    static_assert(A_INS % 8 == 0 && B_INS % 8 == 0 && PA + PB <= 9, "piece schedule");
+    constexpr int WN = 2, TM = 128, FM = 8, FN = 4;
+    typedef typename std::conditional<MODE == 2, f16x8, bf16x8>::type frag;
+    typedef float f32x4v __attribute__((ext_vector_type(4)));
+    __shared__ __attribute__((aligned(16))) uint8_t lds[LDS];
+
+    V4_STAMP(0);
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: keeps piece offsets in SGPRs
+    const int wm = wave / WN, wn = wave % WN;
+    const int nsplit = p.N / BNT;
+    const int xcd = blockIdx.x % 8, slot = blockIdx.x / 8;
+    const int nb = slot % nsplit, pair = (slot / nsplit) * 8 + xcd;
+    const int n0 = nb * BNT;
+    const int nboards = p.m_limit ? *p.m_limit : p.M / (p.H * p.W);
+    const int b0 = pair * BOARDS;
+    if (b0 >= nboards) return;
+    float* sbias = reinterpret_cast<float*>(lds + LDS_BIAS);
+    if (tid < BNT) sbias[tid] = p.bias[n0 + tid];
+    const int C = p.C, GI = C / 8, GO = p.N / 8;
+    const int NCH = C / 32, NS = NCH * 3;
+
+    // DMA through buffer descriptors: one 32-bit VGPR offset per piece; padding halo rows use an
+    // offset past the end of the activation buffer, which the range check turns into zeros
+    // (a range-checked LDS-DMA load is dropped, not zero-filled, so padding rows read the zeroed
+    // tail AZ_ACT_TAIL behind the activation buffer; the per-chunk step keeps them inside it)
+    const uint32_t a_bytes = (uint32_t)((size_t)p.M * C * 2), b_bytes = (uint32_t)((size_t)9 * C * p.N * 2);
+    const __amdgpu_buffer_rsrc_t rsA =
+        __builtin_amdgcn_make_buffer_rsrc((void*)p.Ahi, (short)0, (int)(a_bytes + AZ_ACT_TAIL * 2), 0x00020000);
+    const __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc((void*)p.Bblk, (short)0, (int)b_bytes, 0x00020000);
+    const uint32_t PAD = a_bytes;
+    uint32_t a_vo[PA];
+    int a_off[PA];
+#pragma unroll
+    for (int j = 0; j < PA; ++j) {
+        const int q = wave + 8 * j;
+        const int rb = q % 5, g = (q / 5) % KG, bd = q / (5 * KG);
+        const int hr = rb * 64 + lane;
+        const int Y = hr / 17, X = hr - Y * 17;
+        const int b = b0 + bd;
+        const bool ok = hr < 289 && Y >= 1 && Y <= 15 && X >= 1 && X <= 15 && b < nboards;
+        a_vo[j] = ok ? (uint32_t)((((size_t)b * GI + g) * 225 + (Y - 1) * 15 + (X - 1)) * 16) : PAD;
+        a_off[j] = bd * A_PLANE + g * (V4_HROWS * 16) + rb * 1024;
+    }
+    int b_bo[PB], b_off[PB];   // wave-uniform byte offsets; the lane adds lane * 16
+#pragma unroll
+    for (int j = 0; j < PB; ++j) {
+        const int q = wave + 8 * j;
+        const int rb = q % 2, g = (q / 2) % KG, t = q / (2 * KG);
+        b_bo[j] = ((((g >> 1) * 9 + t) * 2 + (g & 1)) * p.N + n0 + rb * 64) * 16;
+        b_off[j] = t * B_TAP + g * BNT * 16 + rb * 1024;
+    }
+    const uint32_t lane16 = lane * 16;
+    uint8_t* abuf = lds;
+    uint8_t* bbuf = lds + 2 * A_BUF;
+    auto issueA = [&](int j, int c) {
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (lds_void_t*)(abuf + (c & 1) * A_BUF + a_off[j]), 16,
+                                                 (int)(a_vo[j] + (uint32_t)c * (KG * 225 * 16)), 0, 0, 0);
+    };
+    auto issueB = [&](int j, int s) {
+        const int c = s / 3, r = s - 3 * c;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, (lds_void_t*)(bbuf + (s % 3) * B_STAGE + b_off[j]), 16,
+                                                 (int)(lane16 + (uint32_t)(b_bo[j] + (36 * c + 6 * r) * p.N * 16)), 0, 0, 0);
+    };
+
+    f32x4v acc[FM][FN];
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = f32x4v{0.0f, 0.0f, 0.0f, 0.0f};
+
+    // prologue: halo of chunk 0, weights of tap rows 0 and 1
+#pragma unroll
+    for (int j = 0; j < PA; ++j) issueA(j, 0);
+#pragma unroll
+    for (int j = 0; j < PB; ++j) issueB(j, 0);
+    if (NS > 1) {
+#pragma unroll
+        for (int j = 0; j < PB; ++j) issueB(j, 1);
+    }
+    const int bd_w = (wm * TM) / 256, q0 = (wm * TM) % 256;
+    const int l16 = lane & 15, lg = lane >> 4;
+    const uint32_t a_lane = lds_addr(abuf) + bd_w * A_PLANE + lg * (V4_HROWS * 16) + (q0 + l16) * 16;
+    const uint32_t b_lane = lds_addr(bbuf) + lg * (BNT * 16) + (wn * 64 + l16) * 16;
+    for (int s = 0; s < NS; ++s) {
+        const int c = s / 3, r = s - 3 * c;
+        // retire B(s) (and A(c) at r == 0): pieces issued after B(s) may stay in flight
+        auto issued = [&](int u) {          // pieces this wave issued during tap row u
+            return (u + 2 < NS ? PB : 0) + ((u % 3) == 0 && u / 3 + 1 < NCH ? PA : 0);
+        };
+        int allow;
+        if (s == 0) allow = NS > 1 ? PB : 0;
+        else allow = issued(s - 1) + (s >= 2 && ((s - 2) % 3) == 0 && (s - 2) / 3 + 1 < NCH ? PA : 0);
+        wait_vm(allow);
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        const uint32_t ab = a_lane + (c & 1) * A_BUF;
+        const uint32_t bb = b_lane + (s % 3) * B_STAGE;
+        const int npieces = (s + 2 < NS ? PB : 0) + (r == 0 && c + 1 < NCH ? PA : 0);
+        // piece k of this row: weights of row s+2 first, then the next chunk's halo
+        auto piece = [&](int k) {
+            if (k >= npieces) return;
+            if (s + 2 < NS) {
+                if (k < PB) { issueB(k, s + 2); return; }
+                k -= PB;
+            }
+            issueA(k, c + 1);
+        };
+        frag alo[4], ahi[4], bc[4], bn[4];
+        const uint32_t abr = ab + r * (17 * 16);       // tap row r: halo rows shifted by 17 r
+        // fragment reads with compile-time LDS offsets (one base VGPR per operand)
+        auto loadA = [&](frag (&a)[4], auto tc, auto hc) {
+            constexpr int t = decltype(tc)::value, half = decltype(hc)::value;
+            static_for<0, 4>([&](auto ic) {
+                constexpr int i = decltype(ic)::value;
+                ds_rd_off<((half * 4 + i) * 16 + t) * 16>(a[i], abr);
+            });
+        };
+        auto loadB = [&](frag (&b)[4], auto tc) {
+            constexpr int t = decltype(tc)::value;
+            static_for<0, FN>([&](auto jc) {
+                constexpr int j = decltype(jc)::value;
+                ds_rd_off<t * B_TAP + j * 16 * 16>(b[j], bb);
+            });
+        };
+        using I0 = std::integral_constant<int, 0>;
+        using I1 = std::integral_constant<int, 1>;
+        using I2 = std::integral_constant<int, 2>;
+        auto mma = [&](const frag (&a)[4], const frag (&b)[4], int half, int t) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                // DMA slots per tap: before rows 0 and 2 of the low half, row 0 of the high half
+                if ((half == 0 && (i == 0 || i == 2)) || (half == 1 && i == 0)) {
+                    __builtin_amdgcn_sched_barrier(0);
+                    piece(t * 3 + (half == 0 ? (i >> 1) : 2));
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+#pragma unroll
+                for (int j = 0; j < FN; ++j) {
+                    if constexpr (MODE == 2)
+                        acc[half * 4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[i], b[j], acc[half * 4 + i][j], 0, 0, 0);
+                    else
+                        acc[half * 4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[half * 4 + i][j], 0, 0, 0);
+                }
+            }
+        };
+        loadA(alo, I0{}, I0{});
+        loadA(ahi, I0{}, I1{});
+        loadB(bc, I0{});
+        // tap 0
+        loadB(bn, I1{});
+        AZ_LGKM_WAIT(4, alo); AZ_LGKM_WAIT(4, bc);
+        mma(alo, bc, 0, 0);
+        loadA(alo, I1{}, I0{});
+        AZ_LGKM_WAIT(8, ahi);
+        mma(ahi, bc, 1, 0);
+        loadA(ahi, I1{}, I1{});
+        // tap 1 (bn holds B(1))
+        loadB(bc, I2{});
+        AZ_LGKM_WAIT(8, alo); AZ_LGKM_WAIT(8, bn);
+        mma(alo, bn, 0, 1);
+        loadA(alo, I2{}, I0{});
+        AZ_LGKM_WAIT(8, ahi);
+        mma(ahi, bn, 1, 1);
+        loadA(ahi, I2{}, I1{});
+        // tap 2 (bc holds B(2))
+        AZ_LGKM_WAIT(4, alo); AZ_LGKM_WAIT(4, bc);
+        mma(alo, bc, 0, 2);
+        AZ_LGKM_WAIT(0, ahi);
+        mma(ahi, bc, 1, 2);
+    }
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __syncthreads();
+    V4_STAMP(1);
+
+    // epilogue (as v5): two 64-column passes over both boards, staged [2][256][68] fp32
+    constexpr int ITEMS = BOARDS * (SC / 8) * 225;
+    constexpr int ITER = (ITEMS + 511) / 512;
+    float* ep = reinterpret_cast<float*>(lds);
+    struct Res { uint4 h; uint2 q; };
+    auto fetch = [&](int pp, int v) {
+        Res rr{};
+        const int pix = v % 225, t = v / 225, gl = t % 8, bd = t / 8;
+        const int b = b0 + bd;
+        if (v < ITEMS && b < nboards) {
+            const int n = n0 + (gl / 4) * 64 + pp * 32 + (gl % 4) * 8;
+            const size_t e = (((size_t)b * GO + n / 8) * 225 + pix) * 8;
+            rr.h = *reinterpret_cast<const uint4*>(p.Rhi + e);
+            rr.q = *reinterpret_cast<const uint2*>(p.Rq + e);
+        }
+        return rr;
+    };
+    Res rq[2][ITER];
+    if (p.Rhi) {
+#pragma unroll
+        for (int k = 0; k < ITER; ++k) rq[0][k] = fetch(0, tid + 512 * k);
+    }
+#pragma unroll
+    for (int pp = 0; pp < 2; ++pp) {
+        Res (&rres)[ITER] = rq[pp];
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+            for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int row = q0 + i * 16 + lg * 4 + e;            // 15x17 grid row of the board
+                    ep[(bd_w * 256 + row) * SLD + wn * 32 + jj * 16 + l16] = acc[i][2 * pp + jj][e];
+                }
+        __syncthreads();
+        if (pp == 0 && p.Rhi) {
+#pragma unroll
+            for (int k = 0; k < ITER; ++k) rq[1][k] = fetch(1, tid + 512 * k);
+        }
+#pragma unroll
+        for (int k = 0; k < ITER; ++k) {
+            const int v = tid + 512 * k;
+            const int pix = v % 225, t = v / 225, gl = t % 8, bd = t / 8;
+            const int b = b0 + bd;
+            if (v < ITEMS && b < nboards) {
+                const int nl = (gl / 4) * 64 + pp * 32 + (gl % 4) * 8, n = n0 + nl;
+                const float* src = ep + (bd * 256 + (pix / 15) * 17 + pix % 15) * SLD + gl * 8;
+                const float4 x0 = *reinterpret_cast<const float4*>(src);
+                const float4 x1 = *reinterpret_cast<const float4*>(src + 4);
+                const float4 c0v = *reinterpret_cast<const float4*>(sbias + nl);
+                const float4 c1v = *reinterpret_cast<const float4*>(sbias + nl + 4);
+                float o[8] = {x0.x + c0v.x, x0.y + c0v.y, x0.z + c0v.z, x0.w + c0v.w,
+                              x1.x + c1v.x, x1.y + c1v.y, x1.z + c1v.z, x1.w + c1v.w};
+                if (p.Rhi) {
+                    uint16_t hh[8];
+                    int8_t qq[8];
+                    *reinterpret_cast<uint4*>(hh) = rres[k].h;
+                    *reinterpret_cast<uint2*>(qq) = rres[k].q;
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) o[e] += H16::join(hh[e], qq[e]);
+                }
+                uint16_t oh[8];
+                int8_t oq[8];
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    if (p.relu) o[e] = o[e] > 0.0f ? o[e] : 0.0f;
+                    H16::split(o[e], oh[e], oq[e]);
+                }
+                const size_t e = (((size_t)b * GO + n / 8) * 225 + pix) * 8;
+                *reinterpret_cast<uint4*>(p.Chi + e) = *reinterpret_cast<const uint4*>(oh);
+                if (p.Cq) *reinterpret_cast<uint2*>(p.Cq + e) = *reinterpret_cast<const uint2*>(oq);
+                if (p.Cf) {
+                    float* cf = p.Cf + ((size_t)b * 225 + pix) * p.N + n;
+                    *reinterpret_cast<float4*>(cf) = make_float4(o[0], o[1], o[2], o[3]);
+                    *reinterpret_cast<float4*>(cf + 4) = make_float4(o[4], o[5], o[6], o[7]);
+                }
+            }
+        }
+        __syncthreads();
+    }
+    V4_STAMP(2);
+}
+
 // fp32 NHWC [B*225][C] -> g8 16-bit + int8 remainder (the first trunk input and residual)
 template <int MODE>
 __global__ void k_to_g8(const float* in, uint16_t* hi, int8_t* q, int C, const int* m_limit, int maxB) {
@@ -1266,7 +1594,7 @@ void az_launch_pool_g8(const uint16_t* hi, const int8_t* q, float* out, int B, i
 // true when conv3x3_v5 handles this shape (15x15 boards, 16-channel chunks, 128-channel halves)
 bool az_conv_v5_supported(int H, int W, int C, int N) { return H == 15 && W == 15 && C % 16 == 0 && N % 128 == 0; }
 
-static int g_conv_flags = 0;
+static int g_conv_flags = 4;   // bit 2: v6 (16x16x32) where supported
 // Variant bits for A/B measurement inside one process (tools/net_bench.py --flags); none defined now
 // (a residual L2 prefetch during the main loop measured 0.6% slower and was removed)
 extern "C" int az_diag_set_conv_flags(int flags) { g_conv_flags = flags; return 0; }
@@ -1274,12 +1602,28 @@ extern "C" int az_diag_set_conv_flags(int flags) { g_conv_flags = flags; return 
 void az_conv_v5_launch(const ConvBf16Args& a_in, int mode, hipStream_t st) {
     ConvBf16Args a = a_in;
     a.flags = g_conv_flags;
+    // v6 (16x16x32): the padding offset walks NCH * 14400 B into the zeroed tail
+    if ((g_conv_flags & 4) && a.C % 32 == 0 && (size_t)a.M * a.C * 2 < ((size_t)1 << 30) &&
+        (size_t)(a.C / 32) * 4 * 225 * 16 + 16 <= AZ_ACT_TAIL * 2) {
+        const int pairs = (a.M / 225 + 1) / 2;
+        const int grid = (pairs + 7) / 8 * 8 * (a.N / 128);
+        if (mode == 2) hipLaunchKernelGGL(conv3x3_v6<2>, dim3(grid), dim3(512), 0, st, a);
+        else hipLaunchKernelGGL(conv3x3_v6<1>, dim3(grid), dim3(512), 0, st, a);
+        return;
+    }
     const int boards = a.M / 225;
     const int pairs = (boards + 1) / 2;
     const int nsplit = a.N / 128;
     const int grid = (pairs + 7) / 8 * 8 * nsplit;     // XCD-aware pair/half mapping needs whole groups of 8
-    if (mode == 2) hipLaunchKernelGGL(conv3x3_v5<2>, dim3(grid), dim3(512), 0, st, a);
-    else hipLaunchKernelGGL(conv3x3_v5<1>, dim3(grid), dim3(512), 0, st, a);
+    const bool dw4 = (g_conv_flags & 1) != 0;
+    if (mode == 2) {
+        if (g_conv_flags & 2) hipLaunchKernelGGL((conv3x3_v5<2, 8, 2>), dim3(grid), dim3(512), 0, st, a);
+        else if (dw4) hipLaunchKernelGGL((conv3x3_v5<2, 4>), dim3(grid), dim3(512), 0, st, a);
+        else hipLaunchKernelGGL((conv3x3_v5<2, 8>), dim3(grid), dim3(512), 0, st, a);
+    } else {
+        if (dw4) hipLaunchKernelGGL((conv3x3_v5<1, 4>), dim3(grid), dim3(512), 0, st, a);
+        else hipLaunchKernelGGL((conv3x3_v5<1, 8>), dim3(grid), dim3(512), 0, st, a);
+    }
 }
 
 // fp32 -> fp16 activations (first trunk input, AZ_PREC_FP16)

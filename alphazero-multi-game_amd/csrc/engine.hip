@@ -40,6 +40,7 @@ void az_conv_set_variant(int v);
 bool az_conv_v4_supported(int H, int W, int C, int N);
 void az_conv_v4_launch(const ConvBf16Args& a, int mode, hipStream_t st);
 void az_conv_set_v4_sched(int v);
+extern "C" int az_diag_set_conv_flags(int flags);
 bool az_conv_v5_supported(int H, int W, int C, int N);
 void az_conv_v5_launch(const ConvBf16Args& a, int mode, hipStream_t st);
 void az_launch_to_g8(const float* in, uint16_t* hi, int8_t* q, int C, const int* m_limit, int maxB, int mode,
@@ -666,7 +667,12 @@ int az_net_create(az_engine* e, const az_net_desc* d, az_net** out) {
     const size_t B = d->max_batch, rows = B * n->HW, F = d->channels;
     int r = 0;
     auto A_ = [&](float** p, size_t cnt) { if (!r) r = dalloc(p, cnt); };
-    auto H_ = [&](uint16_t** p, size_t cnt) { if (!r) r = dalloc(p, cnt); };
+    // 16-bit activation planes carry a zeroed tail (AZ_ACT_TAIL elements): the v6 conv points the
+    // DMA of halo padding rows there
+    auto H_ = [&](uint16_t** p, size_t cnt) {
+        if (!r) r = dalloc(p, cnt + AZ_ACT_TAIL);
+        if (!r && hipMemset(*p + cnt, 0, AZ_ACT_TAIL * 2) != hipSuccess) r = fail(AZ_ERR_HIP, "hipMemset");
+    };
     A_(&n->x0, rows * n->cin_pad);
     A_(&n->h0, rows * F); A_(&n->h1, rows * F); A_(&n->t, rows * F);
     if (F % 32 == 0) {
@@ -684,6 +690,7 @@ int az_net_create(az_engine* e, const az_net_desc* d, az_net** out) {
     if (!r && hipMemset(n->zero, 0, 256) != hipSuccess) r = fail(AZ_ERR_HIP, "memset");
     if (const char* v = getenv("AZ_CONV_VARIANT")) az_conv_set_variant(atoi(v));
     if (const char* v = getenv("AZ_V4_SCHED")) az_conv_set_v4_sched(atoi(v));
+    if (const char* v = getenv("AZ_CONV_FLAGS")) az_diag_set_conv_flags(atoi(v));
     if (r) { az_net_destroy(n); return r; }
     *out = n;
     return 0;

@@ -22,6 +22,9 @@ struct GemmArgs {
 };
 
 // bf16 trunk conv: activations stored as bf16 hi (+ lo) planes, NHWC.
+// zeroed tail after every 16-bit activation buffer (elements): the v6 conv's padding source
+constexpr size_t AZ_ACT_TAIL = 65536;
+
 struct ConvBf16Args {
     const uint16_t* Ahi; const uint16_t* Alo;   // [rows][C] bf16 (Alo null for plain bf16)
     const uint16_t* Bhi; const uint16_t* Blo;   // [N][9*C] bf16

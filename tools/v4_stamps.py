@@ -29,20 +29,24 @@ for _ in range(3):
     net.forward(x)
 nblk = a.batch // 2 * 2
 SLOTS, MAXBLK = 48, 4096
-buf = (ctypes.c_ulonglong * (SLOTS * MAXBLK * 4))()
-assert _lib.lib().az_diag_v4_stamps(buf, SLOTS * MAXBLK * 4) == 0
-allst = np.frombuffer(buf, np.uint64).reshape(SLOTS, MAXBLK, 4)[:, :nblk, :3].astype(np.int64)
+buf = (ctypes.c_ulonglong * (SLOTS * MAXBLK * 8))()
+assert _lib.lib().az_diag_v4_stamps(buf, SLOTS * MAXBLK * 8) == 0
+allst4 = np.frombuffer(buf, np.uint64).reshape(SLOTS, MAXBLK, 8)[:, :nblk, :].astype(np.int64)
+allst = allst4[:, :, :3]
 rows = []
 for slot in range(40):
     st = allst[slot]
     if st[:, 0].max() == 0:
         continue
     st = (st - st[:, 0].min()) * 10                  # ns
-    rows.append((slot, st[:, 2].max() / 1e3, (st[:, 1] - st[:, 0]).mean() / 1e3, (st[:, 2] - st[:, 1]).mean() / 1e3))
+    rows.append((slot, st[:, 2].max() / 1e3, (st[:, 1] - st[:, 0]).mean() / 1e3, (st[:, 2] - st[:, 1]).mean() / 1e3,
+                 allst4[slot, :, 3].mean(), allst4[slot, :, 4].mean(),
+                 ((allst4[slot, :, 6] - allst4[slot, :, 5]) / np.maximum(1, allst4[slot, :, 1] - allst4[slot, :, 0])).mean() * 0.1))
 print(f"{a.precision}: launches stamped {len(rows)}")
 for name, sel in (("conv1 (even)", [r for r in rows if r[0] % 2 == 0 and r[0] < 38]),
                   ("conv2 (odd) ", [r for r in rows if r[0] % 2 == 1 and r[0] < 39]),
                   ("last launch ", rows[-1:])):
     if sel:
-        sp, mn, ep = (np.mean([r[i] for r in sel]) for i in (1, 2, 3))
-        print(f"  {name}: span {sp:7.1f} us   main/block {mn:6.2f} us   epilogue/block {ep:6.2f} us   (n={len(sel)})")
+        sp, mn, ep, wt, it, ck = (np.mean([r[i] for r in sel]) for i in (1, 2, 3, 4, 5, 6))
+        print(f"  {name}: span {sp:7.1f} us   main/block {mn:6.2f} us   epilogue/block {ep:6.2f} us   "
+              f"wave0 wait+barrier {wt:7.0f} cyc  DMA issue {it:7.0f} cyc  clock {ck:.2f} GHz  (n={len(sel)})")
