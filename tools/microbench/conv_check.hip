@@ -1,4 +1,4 @@
-// v5 vs v6 on the same random g8 activations / blocked weights (one conv, residual on):
+// v5 vs v6 (or the variant named by argv[2] as conv flags, e.g. 12 = v7) on the same random g8 activations / blocked weights (one conv, residual on):
 // reports max |diff| of the 16-bit outputs and where the mismatches are.
 #include "../../alphazero-multi-game_amd/csrc/conv_bf16.hip"
 #include <cstdio>
@@ -6,7 +6,7 @@
 #include <vector>
 
 int main(int argc, char** argv) {
-    const int B = argc > 1 ? atoi(argv[1]) : 64, C = 256, N = 256, HW = 225;
+    const int B = argc > 1 ? atoi(argv[1]) : 64, FL = argc > 2 ? atoi(argv[2]) : 4, C = 256, N = 256, HW = 225;
     const size_t act = (size_t)B * HW * C;
     std::vector<uint16_t> hA(act + AZ_ACT_TAIL, 0), hR(act + AZ_ACT_TAIL, 0), hW((size_t)9 * C * N);
     std::vector<int8_t> hQ(act, 0);
@@ -29,7 +29,7 @@ int main(int argc, char** argv) {
     az_diag_set_conv_flags(0);
     az_conv_v5_launch(a, 2, 0);
     a.Chi = dO6; a.Cq = dQ6;
-    az_diag_set_conv_flags(4);
+    az_diag_set_conv_flags(FL);
     az_conv_v5_launch(a, 2, 0);
     hipDeviceSynchronize();
     std::vector<uint16_t> o5(act), o6(act);
