@@ -1293,6 +1293,23 @@ __global__ __launch_bounds__(512, 1) void conv3x3_v6(ConvBf16Args p) {
         __builtin_amdgcn_make_buffer_rsrc((void*)p.Ahi, (short)0, (int)(a_bytes + AZ_ACT_TAIL * 2), 0x00020000);
     const __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc((void*)p.Bblk, (short)0, (int)b_bytes, 0x00020000);
     const uint32_t PAD = a_bytes;
+#ifdef AZ_V6_DIAG
+    // timing-only variants (tools/net_bench.py --flags): 16/32 = zero-record B/A descriptor (loads
+    // dropped by the range check, instruction stream unchanged); 64/128 = B/A pieces not issued
+    const __amdgpu_buffer_rsrc_t rsA_d =
+        __builtin_amdgcn_make_buffer_rsrc((void*)p.Ahi, (short)0, (p.flags & 32) ? 0 : (int)(a_bytes + AZ_ACT_TAIL * 2), 0x00020000);
+    const __amdgpu_buffer_rsrc_t rsB_d =
+        __builtin_amdgcn_make_buffer_rsrc((void*)p.Bblk, (short)0, (p.flags & 16) ? 0 : (int)b_bytes, 0x00020000);
+#define AZ_RSA rsA_d
+#define AZ_RSB rsB_d
+#define AZ_SKIP_A if (p.flags & 128) return;
+#define AZ_SKIP_B if (p.flags & 64) return;
+#else
+#define AZ_RSA rsA
+#define AZ_RSB rsB
+#define AZ_SKIP_A
+#define AZ_SKIP_B
+#endif
     uint32_t a_vo[PA];
     int a_off[PA];
 #pragma unroll
@@ -1318,12 +1335,14 @@ __global__ __launch_bounds__(512, 1) void conv3x3_v6(ConvBf16Args p) {
     uint8_t* abuf = lds;
     uint8_t* bbuf = lds + 2 * A_BUF;
     auto issueA = [&](int j, int c) {
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (lds_void_t*)(abuf + (c & 1) * A_BUF + a_off[j]), 16,
+        AZ_SKIP_A
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(AZ_RSA, (lds_void_t*)(abuf + (c & 1) * A_BUF + a_off[j]), 16,
                                                  (int)(a_vo[j] + (uint32_t)c * (KG * 225 * 16)), 0, 0, 0);
     };
     auto issueB = [&](int j, int s) {
         const int c = s / 3, r = s - 3 * c;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, (lds_void_t*)(bbuf + (s % 3) * B_STAGE + b_off[j]), 16,
+        AZ_SKIP_B
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(AZ_RSB, (lds_void_t*)(bbuf + (s % 3) * B_STAGE + b_off[j]), 16,
                                                  (int)(lane16 + (uint32_t)(b_bo[j] + (36 * c + 6 * r) * p.N * 16)), 0, 0, 0);
     };
 
@@ -1520,6 +1539,11 @@ __global__ __launch_bounds__(512, 1) void conv3x3_v6(ConvBf16Args p) {
     }
     V4_STAMP(2);
 }
+
+#undef AZ_RSA
+#undef AZ_RSB
+#undef AZ_SKIP_A
+#undef AZ_SKIP_B
 
 // fp32 NHWC [B*225][C] -> g8 16-bit + int8 remainder (the first trunk input and residual)
 template <int MODE>
