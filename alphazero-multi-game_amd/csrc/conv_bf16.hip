@@ -1245,24 +1245,42 @@ __device__ __forceinline__ void static_for(Fn&& f) {
 #define AZ_LGKM_WAIT(N, X)                                                                        \
     asm volatile("s_waitcnt lgkmcnt(" #N ")" : "+v"(X[0]), "+v"(X[1]), "+v"(X[2]), "+v"(X[3]))
 
-template <int MODE>
+// Board geometry of conv3x3_v6 for an HB x HB board: outputs on an HB x (HB+2) grid (two dead
+// columns) so tap (dy, dx) of 16 consecutive outputs is 16 consecutive rows of the zero-padded
+// (HB+2)^2 halo; a board's grid is padded to 128 / 256 / 512 rows and a 512-row block tile holds
+// BOARDS boards (15: 2 boards, 88% live rows; 19: 1 board, 71%; 8 / 9: 4 boards; 13: 2 boards).
+template <int HB>
+struct G8Geom {
+    static constexpr int WG = HB + 2;                       // grid / halo row width
+    static constexpr int HALO = WG * WG;                    // halo rows per board
+    static constexpr int HROWS = (HALO + 63) / 64 * 64;     // padded to whole 1 KiB DMA pieces
+    static constexpr int HP = HROWS / 64;                   // pieces per (board, 8-channel group)
+    static constexpr int OUTR = HB * WG;                    // grid rows per board
+    static constexpr int OUTP = OUTR <= 128 ? 128 : OUTR <= 256 ? 256 : 512;
+    static constexpr int BOARDS = 512 / OUTP;
+    static constexpr int HW = HB * HB;
+    static_assert(OUTR <= 512, "board too large for a 512-row tile");
+};
+
+template <int MODE, int HB = 15>
 __global__ __launch_bounds__(512, 1) void conv3x3_v6(ConvBf16Args p) {
     static_assert(MODE == 1 || MODE == 2, "v6: single-plane modes");
     typedef Half16<MODE> H16;
-    constexpr int BNT = 128, BOARDS = 2, KG = 4;
-    constexpr int A_PLANE = KG * V4_HROWS * 16;          // one board, 32 channels: [4 groups][320 rows][16 B]
-    constexpr int A_BUF = BOARDS * A_PLANE;              // 40 KB
+    typedef G8Geom<HB> GM;
+    constexpr int BNT = 128, BOARDS = GM::BOARDS, KG = 4, WG = GM::WG, HW = GM::HW, OUTP = GM::OUTP;
+    constexpr int A_PLANE = KG * GM::HROWS * 16;         // one board, 32 channels: [4 groups][halo rows][16 B]
+    constexpr int A_BUF = BOARDS * A_PLANE;              // 40 KB at 15x15
     constexpr int B_TAP = KG * BNT * 16;                 // 8 KB
     constexpr int B_STAGE = 3 * B_TAP;                   // one tap row, 24 KB
     constexpr int LDS_MAIN = 2 * A_BUF + 3 * B_STAGE;    // 152 KB
     constexpr int SC = 64, SLD = SC + 4;
-    constexpr int LDS_EPI = BOARDS * 256 * SLD * 4;      // 136 KB
+    constexpr int LDS_EPI = BOARDS * OUTP * SLD * 4;     // 136 KB
     constexpr int LDS_BIAS = LDS_MAIN > LDS_EPI ? LDS_MAIN : LDS_EPI;
     constexpr int LDS = LDS_BIAS + BNT * 4;
-    constexpr int A_INS = BOARDS * KG * (V4_HROWS / 64); // 40 pieces per chunk
+    constexpr int A_INS = BOARDS * KG * GM::HP;          // 40 pieces per chunk at 15x15
     constexpr int B_INS = 3 * KG * (BNT / 64);           // 24 pieces per tap row
-    constexpr int PA = A_INS / 8, PB = B_INS / 8;        // 5 / 3 per wave
-    static_assert(A_INS % 8 == 0 && B_INS % 8 == 0 && PA + PB <= 9, "piece schedule");
+    constexpr int PA = (A_INS + 7) / 8, PB = B_INS / 8;  // 5 / 3 per wave at 15x15
+    static_assert(B_INS % 8 == 0 && PA + PB <= 9, "piece schedule");
     constexpr int WN = 2, TM = 128, FM = 8, FN = 4;
     typedef typename std::conditional<MODE == 2, f16x8, bf16x8>::type frag;
     typedef float f32x4v __attribute__((ext_vector_type(4)));
@@ -1288,7 +1306,8 @@ __global__ __launch_bounds__(512, 1) void conv3x3_v6(ConvBf16Args p) {
     // offset past the end of the activation buffer, which the range check turns into zeros
     // (a range-checked LDS-DMA load is dropped, not zero-filled, so padding rows read the zeroed
     // tail AZ_ACT_TAIL behind the activation buffer; the per-chunk step keeps them inside it)
-    const uint32_t a_bytes = (uint32_t)((size_t)p.M * C * 2), b_bytes = (uint32_t)((size_t)9 * C * p.N * 2);
+    // a_bytes: where the zeroed tail starts (the allocation's capacity, not this batch's rows)
+    const uint32_t a_bytes = (uint32_t)p.a_tail, b_bytes = (uint32_t)((size_t)9 * C * p.N * 2);
     const __amdgpu_buffer_rsrc_t rsA =
         __builtin_amdgcn_make_buffer_rsrc((void*)p.Ahi, (short)0, (int)(a_bytes + AZ_ACT_TAIL * 2), 0x00020000);
     const __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc((void*)p.Bblk, (short)0, (int)b_bytes, 0x00020000);
@@ -1315,13 +1334,13 @@ __global__ __launch_bounds__(512, 1) void conv3x3_v6(ConvBf16Args p) {
 #pragma unroll
     for (int j = 0; j < PA; ++j) {
         const int q = wave + 8 * j;
-        const int rb = q % 5, g = (q / 5) % KG, bd = q / (5 * KG);
+        const int rb = q % GM::HP, g = (q / GM::HP) % KG, bd = q / (GM::HP * KG);
         const int hr = rb * 64 + lane;
-        const int Y = hr / 17, X = hr - Y * 17;
+        const int Y = hr / WG, X = hr - Y * WG;
         const int b = b0 + bd;
-        const bool ok = hr < 289 && Y >= 1 && Y <= 15 && X >= 1 && X <= 15 && b < nboards;
-        a_vo[j] = ok ? (uint32_t)((((size_t)b * GI + g) * 225 + (Y - 1) * 15 + (X - 1)) * 16) : PAD;
-        a_off[j] = bd * A_PLANE + g * (V4_HROWS * 16) + rb * 1024;
+        const bool ok = hr < GM::HALO && Y >= 1 && Y <= HB && X >= 1 && X <= HB && b < nboards;
+        a_vo[j] = ok ? (uint32_t)((((size_t)b * GI + g) * HW + (Y - 1) * HB + (X - 1)) * 16) : PAD;
+        a_off[j] = bd * A_PLANE + g * (GM::HROWS * 16) + rb * 1024;
     }
     int b_bo[PB], b_off[PB];   // wave-uniform byte offsets; the lane adds lane * 16
 #pragma unroll
@@ -1335,9 +1354,10 @@ __global__ __launch_bounds__(512, 1) void conv3x3_v6(ConvBf16Args p) {
     uint8_t* abuf = lds;
     uint8_t* bbuf = lds + 2 * A_BUF;
     auto issueA = [&](int j, int c) {
+        if (A_INS % 8 != 0 && wave + 8 * j >= A_INS) return;   // wave-uniform
         AZ_SKIP_A
         __builtin_amdgcn_raw_ptr_buffer_load_lds(AZ_RSA, (lds_void_t*)(abuf + (c & 1) * A_BUF + a_off[j]), 16,
-                                                 (int)(a_vo[j] + (uint32_t)c * (KG * 225 * 16)), 0, 0, 0);
+                                                 (int)(a_vo[j] + (uint32_t)c * (KG * HW * 16)), 0, 0, 0);
     };
     auto issueB = [&](int j, int s) {
         const int c = s / 3, r = s - 3 * c;
@@ -1361,9 +1381,9 @@ __global__ __launch_bounds__(512, 1) void conv3x3_v6(ConvBf16Args p) {
 #pragma unroll
         for (int j = 0; j < PB; ++j) issueB(j, 1);
     }
-    const int bd_w = (wm * TM) / 256, q0 = (wm * TM) % 256;
+    const int bd_w = (wm * TM) / OUTP, q0 = (wm * TM) % OUTP;
     const int l16 = lane & 15, lg = lane >> 4;
-    const uint32_t a_lane = lds_addr(abuf) + bd_w * A_PLANE + lg * (V4_HROWS * 16) + (q0 + l16) * 16;
+    const uint32_t a_lane = lds_addr(abuf) + bd_w * A_PLANE + lg * (GM::HROWS * 16) + (q0 + l16) * 16;
     const uint32_t b_lane = lds_addr(bbuf) + lg * (BNT * 16) + (wn * 64 + l16) * 16;
     for (int s = 0; s < NS; ++s) {
         const int c = s / 3, r = s - 3 * c;
@@ -1391,7 +1411,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_v6(ConvBf16Args p) {
             issueA(k, c + 1);
         };
         frag alo[4], ahi[4], bc[4], bn[4];
-        const uint32_t abr = ab + r * (17 * 16);       // tap row r: halo rows shifted by 17 r
+        const uint32_t abr = ab + r * (WG * 16);       // tap row r: halo rows shifted by WG r
         // fragment reads with compile-time LDS offsets (one base VGPR per operand)
         auto loadA = [&](frag (&a)[4], auto tc, auto hc) {
             constexpr int t = decltype(tc)::value, half = decltype(hc)::value;
@@ -1457,18 +1477,18 @@ __global__ __launch_bounds__(512, 1) void conv3x3_v6(ConvBf16Args p) {
     __syncthreads();
     V4_STAMP(1);
 
-    // epilogue (as v5): two 64-column passes over both boards, staged [2][256][68] fp32
-    constexpr int ITEMS = BOARDS * (SC / 8) * 225;
+    // epilogue (as v5): two 64-column passes over the block's boards, staged [BOARDS][OUTP][68] fp32
+    constexpr int ITEMS = BOARDS * (SC / 8) * HW;
     constexpr int ITER = (ITEMS + 511) / 512;
     float* ep = reinterpret_cast<float*>(lds);
     struct Res { uint4 h; uint2 q; };
     auto fetch = [&](int pp, int v) {
         Res rr{};
-        const int pix = v % 225, t = v / 225, gl = t % 8, bd = t / 8;
+        const int pix = v % HW, t = v / HW, gl = t % 8, bd = t / 8;
         const int b = b0 + bd;
         if (v < ITEMS && b < nboards) {
             const int n = n0 + (gl / 4) * 64 + pp * 32 + (gl % 4) * 8;
-            const size_t e = (((size_t)b * GO + n / 8) * 225 + pix) * 8;
+            const size_t e = (((size_t)b * GO + n / 8) * HW + pix) * 8;
             rr.h = *reinterpret_cast<const uint4*>(p.Rhi + e);
             rr.q = *reinterpret_cast<const uint2*>(p.Rq + e);
         }
@@ -1488,8 +1508,8 @@ __global__ __launch_bounds__(512, 1) void conv3x3_v6(ConvBf16Args p) {
             for (int jj = 0; jj < 2; ++jj)
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
-                    const int row = q0 + i * 16 + lg * 4 + e;            // 15x17 grid row of the board
-                    ep[(bd_w * 256 + row) * SLD + wn * 32 + jj * 16 + l16] = acc[i][2 * pp + jj][e];
+                    const int row = q0 + i * 16 + lg * 4 + e;            // HB x WG grid row of the board
+                    ep[(bd_w * OUTP + row) * SLD + wn * 32 + jj * 16 + l16] = acc[i][2 * pp + jj][e];
                 }
         __syncthreads();
         if (pp == 0 && p.Rhi) {
@@ -1499,11 +1519,11 @@ __global__ __launch_bounds__(512, 1) void conv3x3_v6(ConvBf16Args p) {
 #pragma unroll
         for (int k = 0; k < ITER; ++k) {
             const int v = tid + 512 * k;
-            const int pix = v % 225, t = v / 225, gl = t % 8, bd = t / 8;
+            const int pix = v % HW, t = v / HW, gl = t % 8, bd = t / 8;
             const int b = b0 + bd;
             if (v < ITEMS && b < nboards) {
                 const int nl = (gl / 4) * 64 + pp * 32 + (gl % 4) * 8, n = n0 + nl;
-                const float* src = ep + (bd * 256 + (pix / 15) * 17 + pix % 15) * SLD + gl * 8;
+                const float* src = ep + (bd * OUTP + (pix / HB) * WG + pix % HB) * SLD + gl * 8;
                 const float4 x0 = *reinterpret_cast<const float4*>(src);
                 const float4 x1 = *reinterpret_cast<const float4*>(src + 4);
                 const float4 c0v = *reinterpret_cast<const float4*>(sbias + nl);
@@ -1525,11 +1545,11 @@ __global__ __launch_bounds__(512, 1) void conv3x3_v6(ConvBf16Args p) {
                     if (p.relu) o[e] = o[e] > 0.0f ? o[e] : 0.0f;
                     H16::split(o[e], oh[e], oq[e]);
                 }
-                const size_t e = (((size_t)b * GO + n / 8) * 225 + pix) * 8;
+                const size_t e = (((size_t)b * GO + n / 8) * HW + pix) * 8;
                 *reinterpret_cast<uint4*>(p.Chi + e) = *reinterpret_cast<const uint4*>(oh);
                 if (p.Cq) *reinterpret_cast<uint2*>(p.Cq + e) = *reinterpret_cast<const uint2*>(oq);
                 if (p.Cf) {
-                    float* cf = p.Cf + ((size_t)b * 225 + pix) * p.N + n;
+                    float* cf = p.Cf + ((size_t)b * HW + pix) * p.N + n;
                     *reinterpret_cast<float4*>(cf) = make_float4(o[0], o[1], o[2], o[3]);
                     *reinterpret_cast<float4*>(cf + 4) = make_float4(o[4], o[5], o[6], o[7]);
                 }
@@ -1545,18 +1565,18 @@ __global__ __launch_bounds__(512, 1) void conv3x3_v6(ConvBf16Args p) {
 #undef AZ_SKIP_A
 #undef AZ_SKIP_B
 
-// fp32 NHWC [B*225][C] -> g8 16-bit + int8 remainder (the first trunk input and residual)
+// fp32 NHWC [B*HW][C] -> g8 16-bit + int8 remainder (the first trunk input and residual)
 template <int MODE>
-__global__ void k_to_g8(const float* in, uint16_t* hi, int8_t* q, int C, const int* m_limit, int maxB) {
+__global__ void k_to_g8(const float* in, uint16_t* hi, int8_t* q, int C, int HW, const int* m_limit, int maxB) {
     const int G = C / 8;
     const int B = m_limit ? min(*m_limit, maxB) : maxB;
-    const size_t total = (size_t)B * G * 225;
+    const size_t total = (size_t)B * G * HW;
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
-        const int pix = (int)(i % 225);
-        const size_t bg = i / 225;
+        const int pix = (int)(i % HW);
+        const size_t bg = i / HW;
         const int g = (int)(bg % G);
         const size_t b = bg / G;
-        const float* src = in + (b * 225 + pix) * C + g * 8;
+        const float* src = in + (b * HW + pix) * C + g * 8;
         const float4 v0 = *reinterpret_cast<const float4*>(src);
         const float4 v1 = *reinterpret_cast<const float4*>(src + 4);
         const float f[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
@@ -1569,17 +1589,17 @@ __global__ void k_to_g8(const float* in, uint16_t* hi, int8_t* q, int C, const i
     }
 }
 
-void az_launch_to_g8(const float* in, uint16_t* hi, int8_t* q, int C, const int* m_limit, int maxB, int mode,
+void az_launch_to_g8(const float* in, uint16_t* hi, int8_t* q, int C, int HW, const int* m_limit, int maxB, int mode,
                      hipStream_t st) {
-    if (mode == 2) hipLaunchKernelGGL(k_to_g8<2>, dim3(2048), dim3(256), 0, st, in, hi, q, C, m_limit, maxB);
-    else hipLaunchKernelGGL(k_to_g8<1>, dim3(2048), dim3(256), 0, st, in, hi, q, C, m_limit, maxB);
+    if (mode == 2) hipLaunchKernelGGL(k_to_g8<2>, dim3(2048), dim3(256), 0, st, in, hi, q, C, HW, m_limit, maxB);
+    else hipLaunchKernelGGL(k_to_g8<1>, dim3(2048), dim3(256), 0, st, in, hi, q, C, HW, m_limit, maxB);
 }
 
-// adaptive_avg_pool2d(x, (P, P)) of a 15x15 g8 trunk output (16-bit + int8 remainder) -> fp32 NHWC
+// adaptive_avg_pool2d(x, (P, P)) of an H x H g8 trunk output (16-bit + int8 remainder) -> fp32 NHWC
 // [B][P*P][C]; one thread per (board, 8-channel group, output cell), same summation order as
 // k_adaptive_pool (rows, then columns; sum / kh / kw)
 template <int MODE>
-__global__ void k_pool_g8(const uint16_t* hi, const int8_t* q, float* out, int C, int P, const int* m_limit, int maxB) {
+__global__ void k_pool_g8(const uint16_t* hi, const int8_t* q, float* out, int C, int H, int P, const int* m_limit, int maxB) {
     const int G = C / 8, PP = P * P;
     const int B = m_limit ? min(*m_limit, maxB) : maxB;
     const size_t total = (size_t)B * G * PP;
@@ -1589,12 +1609,12 @@ __global__ void k_pool_g8(const uint16_t* hi, const int8_t* q, float* out, int C
         const int g = (int)(bg % G);
         const size_t b = bg / G;
         const int oy = o / P, ox = o % P;
-        const int y0 = (oy * 15) / P, y1 = ((oy + 1) * 15 + P - 1) / P;
-        const int x0 = (ox * 15) / P, x1 = ((ox + 1) * 15 + P - 1) / P;
+        const int y0 = (oy * H) / P, y1 = ((oy + 1) * H + P - 1) / P;
+        const int x0 = (ox * H) / P, x1 = ((ox + 1) * H + P - 1) / P;
         float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         for (int y = y0; y < y1; ++y)
             for (int x = x0; x < x1; ++x) {
-                const size_t e = ((b * G + g) * 225 + y * 15 + x) * 8;
+                const size_t e = ((b * G + g) * H * H + y * H + x) * 8;
                 uint16_t h[8];
                 int8_t r[8];
                 *reinterpret_cast<uint4*>(h) = *reinterpret_cast<const uint4*>(hi + e);
@@ -1609,31 +1629,55 @@ __global__ void k_pool_g8(const uint16_t* hi, const int8_t* q, float* out, int C
     }
 }
 
-void az_launch_pool_g8(const uint16_t* hi, const int8_t* q, float* out, int B, int C, int P, const int* m_limit, int mode,
-                       hipStream_t st) {
-    if (mode == 2) hipLaunchKernelGGL(k_pool_g8<2>, dim3(4096), dim3(256), 0, st, hi, q, out, C, P, m_limit, B);
-    else hipLaunchKernelGGL(k_pool_g8<1>, dim3(4096), dim3(256), 0, st, hi, q, out, C, P, m_limit, B);
+void az_launch_pool_g8(const uint16_t* hi, const int8_t* q, float* out, int B, int C, int H, int P, const int* m_limit,
+                       int mode, hipStream_t st) {
+    if (mode == 2) hipLaunchKernelGGL(k_pool_g8<2>, dim3(4096), dim3(256), 0, st, hi, q, out, C, H, P, m_limit, B);
+    else hipLaunchKernelGGL(k_pool_g8<1>, dim3(4096), dim3(256), 0, st, hi, q, out, C, H, P, m_limit, B);
 }
 
-// true when conv3x3_v5 handles this shape (15x15 boards, 16-channel chunks, 128-channel halves)
-bool az_conv_v5_supported(int H, int W, int C, int N) { return H == 15 && W == 15 && C % 16 == 0 && N % 128 == 0; }
+// true when the g8 trunk (conv3x3_v5 at 15x15 / conv3x3_v6) handles this shape: square boards with a
+// G8Geom instantiation, 128-channel output halves, 16-channel chunks (v5, 15x15) or 32 (v6)
+static bool g8_board(int H) { return H == 8 || H == 9 || H == 13 || H == 15 || H == 19; }
+bool az_conv_g8_supported(int H, int W, int C, int N) {
+    if (H != W || !g8_board(H) || N % 128 != 0 || C < 16) return false;
+    return H == 15 ? C % 16 == 0 : C % 32 == 0;
+}
 
-static int g_conv_flags = 4;   // bit 2: v6 (16x16x32) where supported
+static int g_conv_flags = 4;   // bit 2: v6 (16x16x32) at 15x15 (other boards always use v6)
 // Variant bits for A/B measurement inside one process (tools/net_bench.py --flags); none defined now
-// (a residual L2 prefetch during the main loop measured 0.6% slower and was removed)
+// (a residual L2 prefetch during the main loop measured 0.6% slower and was removed; a cross-row
+// fragment prefetch and a mid-row barrier variant measured 1.5-2% slower)
 extern "C" int az_diag_set_conv_flags(int flags) { g_conv_flags = flags; return 0; }
 
-void az_conv_v5_launch(const ConvBf16Args& a_in, int mode, hipStream_t st) {
+template <int HB>
+static void v6_launch(const ConvBf16Args& a, int mode, hipStream_t st) {
+    typedef G8Geom<HB> GM;
+    const int groups = (a.M / GM::HW + GM::BOARDS - 1) / GM::BOARDS;
+    const int grid = (groups + 7) / 8 * 8 * (a.N / 128);   // XCD-aware group/half mapping: whole groups of 8
+    if (mode == 2) hipLaunchKernelGGL((conv3x3_v6<2, HB>), dim3(grid), dim3(512), 0, st, a);
+    else hipLaunchKernelGGL((conv3x3_v6<1, HB>), dim3(grid), dim3(512), 0, st, a);
+}
+
+int az_conv_g8_launch(const ConvBf16Args& a_in, int mode, hipStream_t st) {
     ConvBf16Args a = a_in;
     a.flags = g_conv_flags;
-    // v6 (16x16x32): the padding offset walks NCH * 14400 B into the zeroed tail
-    if ((g_conv_flags & 4) && a.C % 32 == 0 && (size_t)a.M * a.C * 2 < ((size_t)1 << 30) &&
-        (size_t)(a.C / 32) * 4 * 225 * 16 + 16 <= AZ_ACT_TAIL * 2) {
-        const int pairs = (a.M / 225 + 1) / 2;
-        const int grid = (pairs + 7) / 8 * 8 * (a.N / 128);
-        if (mode == 2) hipLaunchKernelGGL(conv3x3_v6<2>, dim3(grid), dim3(512), 0, st, a);
-        else hipLaunchKernelGGL(conv3x3_v6<1>, dim3(grid), dim3(512), 0, st, a);
-        return;
+    if (a.H != a.W || !az_conv_g8_supported(a.H, a.W, a.C, a.N)) return -1;
+    const size_t HW = (size_t)a.H * a.W;
+    if (a.a_tail == 0) a.a_tail = (size_t)a.M * a.C * 2;
+    if (a.a_tail < (size_t)a.M * a.C * 2) return -1;
+    // v6: the padding offset walks (C/32) chunk steps of 4*HW*16 B into the zeroed tail, and the
+    // buffer descriptor's 32-bit range must cover the activations plus that tail
+    const bool v6_ok = a.C % 32 == 0 && a.a_tail + AZ_ACT_TAIL * 2 < ((size_t)1 << 31) &&
+                       (size_t)(a.C / 32) * 4 * HW * 16 + 16 <= AZ_ACT_TAIL * 2;
+    if (a.H != 15 || ((g_conv_flags & 4) && a.C % 32 == 0)) {
+        if (!v6_ok) return -1;
+        switch (a.H) {
+            case 8: v6_launch<8>(a, mode, st); return 0;
+            case 9: v6_launch<9>(a, mode, st); return 0;
+            case 13: v6_launch<13>(a, mode, st); return 0;
+            case 19: v6_launch<19>(a, mode, st); return 0;
+            default: v6_launch<15>(a, mode, st); return 0;
+        }
     }
     const int boards = a.M / 225;
     const int pairs = (boards + 1) / 2;
@@ -1648,6 +1692,7 @@ void az_conv_v5_launch(const ConvBf16Args& a_in, int mode, hipStream_t st) {
         if (dw4) hipLaunchKernelGGL((conv3x3_v5<1, 4>), dim3(grid), dim3(512), 0, st, a);
         else hipLaunchKernelGGL((conv3x3_v5<1, 8>), dim3(grid), dim3(512), 0, st, a);
     }
+    return 0;
 }
 
 // fp32 -> fp16 activations (first trunk input, AZ_PREC_FP16)

@@ -41,12 +41,12 @@ bool az_conv_v4_supported(int H, int W, int C, int N);
 void az_conv_v4_launch(const ConvBf16Args& a, int mode, hipStream_t st);
 void az_conv_set_v4_sched(int v);
 extern "C" int az_diag_set_conv_flags(int flags);
-bool az_conv_v5_supported(int H, int W, int C, int N);
-void az_conv_v5_launch(const ConvBf16Args& a, int mode, hipStream_t st);
-void az_launch_to_g8(const float* in, uint16_t* hi, int8_t* q, int C, const int* m_limit, int maxB, int mode,
+bool az_conv_g8_supported(int H, int W, int C, int N);
+int az_conv_g8_launch(const ConvBf16Args& a, int mode, hipStream_t st);
+void az_launch_to_g8(const float* in, uint16_t* hi, int8_t* q, int C, int HW, const int* m_limit, int maxB, int mode,
                      hipStream_t st);
-void az_launch_pool_g8(const uint16_t* hi, const int8_t* q, float* out, int B, int C, int P, const int* m_limit, int mode,
-                       hipStream_t st);
+void az_launch_pool_g8(const uint16_t* hi, const int8_t* q, float* out, int B, int C, int H, int P, const int* m_limit,
+                       int mode, hipStream_t st);
 void az_launch_to_f16(const float* in, uint16_t* out, size_t n, const int* m_limit, int rows_per_sample, int C,
                       hipStream_t st);
 void az_launch_split_bf16(const float* in, uint16_t* hi, uint16_t* lo, size_t n, const int* m_limit, int rows_per_sample,
@@ -112,6 +112,7 @@ struct az_net {
     az_net_desc d{};
     int cin_pad = 16;
     int HW = 0, P2 = 0;
+    size_t act_elems = 0;   // elements of every 16-bit activation buffer before its zeroed tail
     size_t nparams = 0;
     Layer in, pconv, vconv, pfc, vfc1, vfc2;
     std::vector<Layer> blk;   // 2 per block
@@ -285,23 +286,27 @@ int net_forward(az_net* n, const float* x0, int B, const int* nb, float* logits,
     const int prec = d.precision;
     const bool bf = (prec == AZ_PREC_BF16X3 || prec == AZ_PREC_BF16 || prec == AZ_PREC_FP16) && F % 32 == 0;
     const bool f16 = prec == AZ_PREC_FP16;
-    // g8 path (v5 conv, fp16/bf16): input conv, trunk and pool all on 16-bit channel-blocked rows
-    const bool g8 = bf && prec != AZ_PREC_BF16X3 && az_conv_v5_supported(H, W, F, F) && n->cin_pad == 16 &&
-                    n->in.Wbk_h != nullptr;
+    // g8 path (v5 / v6 conv, fp16/bf16): input conv, trunk and pool all on 16-bit channel-blocked rows
+    const bool g8 = bf && prec != AZ_PREC_BF16X3 && az_conv_g8_supported(H, W, F, F);
     const int mode = f16 ? 2 : 1;
     int8_t* hq[2] = {reinterpret_cast<int8_t*>(n->hl[0]), reinterpret_cast<int8_t*>(n->hl[1])};
-    if (g8) {
-        // input planes -> g8 16-bit (0/1 planes are exact), then the input conv as a one-chunk v5 conv
-        az_launch_to_g8(x0, n->th, nullptr, n->cin_pad, nb, B, mode, st);
+    if (g8 && n->in.Wbk_h != nullptr && az_conv_g8_supported(H, W, n->cin_pad, F)) {
+        // input planes -> g8 16-bit (0/1 planes are exact), then the input conv on the g8 kernel
+        az_launch_to_g8(x0, n->th, nullptr, n->cin_pad, HW, nb, B, mode, st);
         ConvBf16Args a{};
         a.Ahi = n->th;
         a.Bblk = f16 ? n->in.Wbk_h : n->in.Wbk_bf;
         a.Chi = n->hh[0]; a.Cq = hq[0];
         a.bias = n->in.b;
         a.M = rows; a.N = F; a.C = n->cin_pad; a.H = H; a.W = W; a.m_limit = nb; a.rows_per_sample = HW; a.relu = 1;
+        a.a_tail = n->act_elems * 2;          // th's zeroed tail sits behind its full capacity
         a.zero = n->zero;
         a.stamp = -1;
-        az_conv_v5_launch(a, mode, st);
+        if (az_conv_g8_launch(a, mode, st)) return fail(AZ_ERR_ARG, "g8 input conv: unsupported shape");
+    } else if (g8) {
+        // few input planes on a board v6 cannot take at 16 channels: f32 input conv, then to g8
+        az_launch_gemm_f32(gemm_args(n->in, x0, n->cin_pad, n->h0, F, nullptr, rows, H, W, nb, HW), ACT_RELU, false, st);
+        az_launch_to_g8(n->h0, n->hh[0], hq[0], F, HW, nb, B, mode, st);
     } else {
         az_launch_gemm_f32(gemm_args(n->in, x0, n->cin_pad, n->h0, F, nullptr, rows, H, W, nb, HW), ACT_RELU, false, st);
     }
@@ -341,9 +346,10 @@ int net_forward(az_net* n, const float* x0, int B, const int* nb, float* logits,
                 a.Chi = n->th;
                 a.bias = L1.b;
                 a.M = rows; a.N = F; a.C = F; a.H = H; a.W = W; a.m_limit = nb; a.rows_per_sample = HW; a.relu = 1;
+                a.a_tail = n->act_elems * 2;
                 a.zero = n->zero;
                 a.stamp = 2 * i;
-                az_conv_v5_launch(a, mode, st);
+                if (az_conv_g8_launch(a, mode, st)) return fail(AZ_ERR_ARG, "g8 trunk conv: unsupported shape");
                 ConvBf16Args b2 = a;
                 b2.stamp = 2 * i + 1;
                 b2.Ahi = n->th;
@@ -351,12 +357,12 @@ int net_forward(az_net* n, const float* x0, int B, const int* nb, float* logits,
                 b2.Chi = n->hh[cur ^ 1]; b2.Cq = hq[cur ^ 1];
                 b2.bias = L2.b;
                 if (d.residual) { b2.Rhi = n->hh[cur]; b2.Rq = hq[cur]; }
-                az_conv_v5_launch(b2, mode, st);
+                if (az_conv_g8_launch(b2, mode, st)) return fail(AZ_ERR_ARG, "g8 trunk conv: unsupported shape");
                 cur ^= 1;
             }
             if (ev1) HIPCHK(hipEventRecord(ev1, st));
             ev1 = nullptr;
-            az_launch_pool_g8(n->hh[cur], hq[cur], n->pool, B, F, P, nb, mode, st);
+            az_launch_pool_g8(n->hh[cur], hq[cur], n->pool, B, F, H, P, nb, mode, st);
         } else {
         if (f16) az_launch_to_f16(h, n->hh[0], (size_t)rows * F, nb, HW, F, st);
         else az_launch_split_bf16(h, n->hh[0], split ? n->hl[0] : nullptr, (size_t)rows * F, nb, HW, F, st);
@@ -643,15 +649,17 @@ int az_engine_device_name(az_engine* e, char* buf, int len) {
 static int check_precision(const az_net_desc& d, int precision) {
     if (precision < 0 || precision > 3) return fail(AZ_ERR_ARG, "bad precision %d", precision);
     if (precision != AZ_PREC_F32 && d.channels % 32) return fail(AZ_ERR_ARG, "bf16/fp16 trunk needs channels %% 32 == 0");
-    if (precision == AZ_PREC_FP16 && !az_conv_v4_supported(d.board_size, d.board_size, d.channels, d.channels))
-        return fail(AZ_ERR_ARG, "AZ_PREC_FP16 trunk needs 15x15 boards and channels %% 64 == 0");
+    if (precision == AZ_PREC_FP16 && !az_conv_v4_supported(d.board_size, d.board_size, d.channels, d.channels) &&
+        !az_conv_g8_supported(d.board_size, d.board_size, d.channels, d.channels))
+        return fail(AZ_ERR_ARG, "AZ_PREC_FP16 trunk needs 15x15 boards and channels %% 64 == 0, or an 8/9/13/15/19 board "
+                                "and channels %% 128 == 0");
     return 0;
 }
 
 int az_net_create(az_engine* e, const az_net_desc* d, az_net** out) {
     if (!e || !d || !out) return fail(AZ_ERR_ARG, "null argument");
-    if (d->board_size < 2 || d->board_size * d->board_size > AZ_MAXA || d->in_planes < 1 || d->in_planes > 16 ||
-        d->channels < 4 || d->channels % 4 || d->blocks < 0 || d->action_size < 1 || d->action_size > 4096 ||
+    if (d->board_size < 2 || d->board_size * d->board_size > AZ_MAXA || d->in_planes < 1 || d->in_planes > 128 ||
+        d->channels < 4 || d->channels % 4 || d->blocks < 0 || d->action_size < 1 || d->action_size > 8192 ||
         d->head_channels < 1 || d->head_channels % 4 || d->pool < 1 || d->fc_hidden < 1 || d->fc_hidden % 4 ||
         d->max_batch < 1)
         return fail(AZ_ERR_ARG, "unsupported network description");
@@ -663,8 +671,13 @@ int az_net_create(az_engine* e, const az_net_desc* d, az_net** out) {
     n->d = *d;
     n->HW = d->board_size * d->board_size;
     n->P2 = d->pool * d->pool;
+    // input channels padded to 16 (the search's plane records); more than 16 planes on a g8 board
+    // pad to 32 so the v6 conv takes the input layer as whole 32-channel chunks
+    n->cin_pad = (d->in_planes + 15) / 16 * 16;
+    if (n->cin_pad > 16 && d->channels % 128 == 0) n->cin_pad = (d->in_planes + 31) / 32 * 32;
     n->nparams = count_params(*d);
     const size_t B = d->max_batch, rows = B * n->HW, F = d->channels;
+    n->act_elems = rows * F;
     int r = 0;
     auto A_ = [&](float** p, size_t cnt) { if (!r) r = dalloc(p, cnt); };
     // 16-bit activation planes carry a zeroed tail (AZ_ACT_TAIL elements): the v6 conv points the

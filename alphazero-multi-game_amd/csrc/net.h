@@ -23,7 +23,7 @@ struct GemmArgs {
 
 // bf16 trunk conv: activations stored as bf16 hi (+ lo) planes, NHWC.
 // zeroed tail after every 16-bit activation buffer (elements): the v6 conv's padding source
-constexpr size_t AZ_ACT_TAIL = 65536;
+constexpr size_t AZ_ACT_TAIL = 262144;   // zeroed 16-bit elements behind every g8 activation buffer (512 KB)
 
 struct ConvBf16Args {
     const uint16_t* Ahi; const uint16_t* Alo;   // [rows][C] bf16 (Alo null for plain bf16)
@@ -36,6 +36,7 @@ struct ConvBf16Args {
     const float* Rf;                            // fp32 residual [rows][N] (v4 only)
     const int8_t* Rq; int8_t* Cq;               // v5: int8 remainders of the g8 residual / output
     int M, N, C, H, W;
+    size_t a_tail;                              // v6: byte offset of Ahi's zeroed tail (AZ_ACT_TAIL); 0 = M*C*2
     const int* m_limit; int rows_per_sample;
     int relu;
     const uint16_t* zero;                       // >= 64 zero bytes (padding source for glds)

@@ -141,3 +141,70 @@ def test_gpu_c3_net_error_over_many_positions(engine, prec):
     print(f"C3 {prec}: max|dlogit|={el:.3e} max|dvalue|={ev:.3e} (|logit|max {np.abs(rl).max():.3f})")
     assert el <= TOL and ev <= TOL
     net.close()
+
+
+G8_CASES = [  # (board, in_planes, action_size, channels, blocks, B): the g8 conv3x3_v6 board geometries
+    (19, 8, 362, 128, 2, 5),      # Go shape (C4: 8 planes, 361 + pass); 1 board per 512-row tile
+    (8, 111, 4672, 128, 2, 9),    # Chess shape (C5: 111 planes, 4672 moves); 4 boards per tile, v6 input conv
+    (9, 11, 81, 128, 2, 6),       # Gomoku 9x9 (C1 board)
+    (13, 11, 169, 256, 1, 3),     # Go 13x13
+    (15, 20, 225, 128, 1, 4),     # 15x15 with > 16 planes: the input conv runs on v6 (32-channel chunks)
+]
+
+
+def _rand_planes(B, ci, bs, seed, p=0.2):
+    rng = np.random.default_rng(seed)
+    return (rng.random((B, ci, bs, bs)) < p).astype(np.float32)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("prec", ["fp16", "bf16"])
+@pytest.mark.parametrize("case", G8_CASES, ids=[str(c) for c in G8_CASES])
+def test_gpu_g8_boards_match_fp32_reference(engine, case, prec):
+    """conv3x3_v6 on every board geometry it is instantiated for (8, 9, 13, 15, 19), through the
+    whole net against the fp32 reference: fp16 within the 1e-4 tolerance, bf16 a sanity bound."""
+    import az_amd
+    import net_oracle
+    bs, ci, A, ch, blocks, B = case
+    p = {"fp16": az_amd.AZ_PREC_FP16, "bf16": az_amd.AZ_PREC_BF16}[prec]
+    desc = az_amd.NetDesc(bs, ci, ch, blocks, A, 32, 8, 256, 1, 0, p, B)
+    net = az_amd.HipNeuralNetwork(engine, desc)
+    blob = net_oracle.init_blob(desc, seed=21)
+    net.load_weights(blob)
+    x = _rand_planes(B, ci, bs, seed=bs, p=0.05 if ci > 16 else 0.2)
+    lo, v = net.forward(x)
+    rl, rv = net_oracle.forward(desc, blob, x)
+    el, ev = float(np.abs(lo - rl).max()), float(np.abs(v - rv).max())
+    print(f"{case} {prec}: max|dlogit|={el:.3e} (|logit|max {np.abs(rl).max():.3f}) max|dvalue|={ev:.3e}")
+    if prec == "fp16":
+        assert el <= TOL and ev <= TOL
+    else:
+        assert el < 5e-2 * max(1.0, np.abs(rl).max()) and ev < 5e-2
+    # a sample's output does not depend on the batch it rides in (ragged tiles of BOARDS boards)
+    lo1, v1 = net.forward(x[B - 1:])
+    assert np.array_equal(lo1, lo[B - 1:]) and np.array_equal(v1, v[B - 1:])
+    net.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape", ["go19", "chess"])
+def test_gpu_c4_c5_nets_fp16_within_tolerance(engine, shape):
+    """The C4 (Go 19x19) and C5 (Chess 8x8x111 -> 4672) 20-block x 256-filter nets in fp16: every
+    logit and value within 1e-4 of the fp32 reference."""
+    import az_amd
+    import net_oracle
+    if shape == "go19":
+        desc = az_amd.NetDesc(19, 8, 256, 20, 362, 32, 8, 256, 1, 0, az_amd.AZ_PREC_FP16, 24)
+        x = _rand_planes(24, 8, 19, seed=3, p=0.3)
+    else:
+        desc = az_amd.NetDesc(8, 111, 256, 20, 4672, 32, 8, 256, 1, 0, az_amd.AZ_PREC_FP16, 48)
+        x = _rand_planes(48, 111, 8, seed=4, p=0.05)
+    net = az_amd.HipNeuralNetwork(engine, desc)
+    blob = net_oracle.init_blob(desc, seed=1234)
+    net.load_weights(blob)
+    lo, v = net.forward(x)
+    rl, rv = net_oracle.forward(desc, blob, x)
+    el, ev = float(np.abs(lo - rl).max()), float(np.abs(v - rv).max())
+    print(f"{shape} fp16: max|dlogit|={el:.3e} max|dvalue|={ev:.3e} (|logit|max {np.abs(rl).max():.3f})")
+    assert el <= TOL and ev <= TOL
+    net.close()

@@ -27,10 +27,10 @@ int main(int argc, char** argv) {
     a.Ahi = dA; a.Bblk = dW; a.Chi = dO5; a.Cq = dQ5; a.bias = db; a.Rhi = dR; a.Rq = dQ;
     a.M = B * HW; a.N = N; a.C = C; a.H = 15; a.W = 15; a.rows_per_sample = HW; a.relu = 1; a.zero = dZ; a.stamp = -1;
     az_diag_set_conv_flags(0);
-    az_conv_v5_launch(a, 2, 0);
+    az_conv_g8_launch(a, 2, 0);
     a.Chi = dO6; a.Cq = dQ6;
     az_diag_set_conv_flags(FL);
-    az_conv_v5_launch(a, 2, 0);
+    az_conv_g8_launch(a, 2, 0);
     hipDeviceSynchronize();
     std::vector<uint16_t> o5(act), o6(act);
     hipMemcpy(o5.data(), dO5, act * 2, hipMemcpyDeviceToHost); hipMemcpy(o6.data(), dO6, act * 2, hipMemcpyDeviceToHost);
