@@ -1,7 +1,7 @@
 // oracle/az_oracle.cpp -- TEST INFRASTRUCTURE ONLY.
 //
 // CPU restatement of the reference self-play hot path in "Mode S" (SURVEY.md
-// Appendix A): GomokuState rules/features/hash, ParallelMCTS sequential simulation
+// Appendix A): GomokuState and GoState rules/features/hash, ParallelMCTS sequential simulation
 // (numThreads=1, setDeterministicMode(true)), TranspositionTable, Dirichlet noise,
 // and the SelfPlayManager::playSingleGame move loop.  Only tests/, bench.py's
 // cpu_baseline leg and __graft_entry__.smoke() may load it, and only as the checker.
@@ -55,7 +55,9 @@ struct Zobrist {
 // ---------------------------------------------------------------------------
 // GomokuState (src/games/gomoku/gomoku_state.cpp), standard rules (no Renju/Omok/pro-long).
 struct State {
+    static constexpr int NPLANES = 11;
     int bs, A;
+    int NA() const { return A; }        // getActionSpaceSize
     std::vector<int8_t> cell;      // 0 empty, 1 black, 2 white
     int player = 1;                // current_player, BLACK=1 moves first (:20)
     std::vector<int> history;      // move_history (:718)
@@ -155,24 +157,232 @@ struct State {
 };
 
 // ---------------------------------------------------------------------------
+// GoState (src/games/go/go_state.cpp, go_rules.cpp) as created by GoState(bs, 7.5, true, true):
+// komi 7.5, Chinese (area) scoring, positional superko, pass = -1, action space bs*bs + 1.
+struct GoZobrist {
+    std::vector<uint64_t> piece;        // [2][A]  ZobristHash(bs, 2, 2, seed) (patch P6)
+    uint64_t player[2];
+    std::vector<uint64_t> ko;           // addFeature("ko_point", A + 1) (go_state.cpp:49)
+    uint64_t rules[2], komi[16];        // addFeature("rules", 2), addFeature("komi", 16)
+    GoZobrist(int A, unsigned seed) : piece(2 * A), ko(A + 1) {
+        std::mt19937_64 rng(seed);
+        for (int p = 0; p < 2; ++p)
+            for (int a = 0; a < A; ++a) piece[p * A + a] = rng();
+        player[0] = rng(); player[1] = rng();
+        // ZobristHash::addFeature (zobrist_hash.cpp:58-70): mt19937_64(std::hash<std::string>(name))
+        std::mt19937_64 rk(std::hash<std::string>{}("ko_point"));
+        for (int i = 0; i <= A; ++i) ko[i] = rk();
+        std::mt19937_64 rr(std::hash<std::string>{}("rules"));
+        for (auto& x : rules) x = rr();
+        std::mt19937_64 rm(std::hash<std::string>{}("komi"));
+        for (auto& x : komi) x = rm();
+    }
+};
+
+struct GoState {
+    static constexpr int NPLANES = 8;
+    int bs, A;
+    int NA() const { return A + 1; }                 // getActionSpaceSize (:330-332)
+    std::vector<int8_t> cell;                        // board_ (0 / 1 black / 2 white), pos = y*bs + x
+    int player = 1, ko = -1, passes = 0;
+    int captured[3] = {0, 0, 0};
+    std::vector<int> history;                        // move_history_ (passes as -1)
+    std::vector<uint64_t> poshist;                   // position_history_ (non-pass moves only)
+    const GoZobrist* z;
+    float komi = 7.5f;
+    GoState(int bs_, const GoZobrist* z_) : bs(bs_), A(bs_ * bs_), cell(bs_ * bs_, 0), z(z_) {}
+
+    // getAdjacentPositions (:800-816): up, right, down, left
+    int adj(int pos, int* out) const {
+        int x = pos % bs, y = pos / bs, n = 0;
+        if (y > 0) out[n++] = pos - bs;
+        if (x + 1 < bs) out[n++] = pos + 1;
+        if (y + 1 < bs) out[n++] = pos + bs;
+        if (x > 0) out[n++] = pos - 1;
+        return n;
+    }
+    // the group through `pos` on board b, and whether it has a liberty (go_rules.cpp:150-200)
+    bool group(const std::vector<int8_t>& b, int pos, std::vector<int>& stones, std::vector<char>& seen) const {
+        const int c = b[pos];
+        stones.clear();
+        stones.push_back(pos);
+        seen[pos] = 1;
+        bool lib = false;
+        for (size_t i = 0; i < stones.size(); ++i) {
+            int nb[4], k = adj(stones[i], nb);
+            for (int j = 0; j < k; ++j) {
+                if (b[nb[j]] == 0) lib = true;
+                else if (b[nb[j]] == c && !seen[nb[j]]) { seen[nb[j]] = 1; stones.push_back(nb[j]); }
+            }
+        }
+        return lib;
+    }
+    int count_libs(const std::vector<int8_t>& b, const std::vector<int>& stones) const {
+        std::vector<char> l(A, 0);
+        int n = 0;
+        for (int s : stones) {
+            int nb[4], k = adj(s, nb);
+            for (int j = 0; j < k; ++j) if (b[nb[j]] == 0 && !l[nb[j]]) { l[nb[j]] = 1; ++n; }
+        }
+        return n;
+    }
+    // remove every libertyless group of colour c (findGroups + captureGroup); returns the stones
+    std::vector<std::vector<int>> capture(std::vector<int8_t>& b, int c) const {
+        std::vector<std::vector<int>> caps;
+        std::vector<char> seen(A, 0);
+        std::vector<int> st;
+        for (int p = 0; p < A; ++p) {
+            if (b[p] != c || seen[p]) continue;
+            if (!group(b, p, st, seen)) caps.push_back(st);
+        }
+        for (auto& g : caps) for (int s : g) b[s] = 0;
+        return caps;
+    }
+    // GoRules::isSuicidalMove (go_rules.cpp:27-136)
+    bool suicidal(int a, int p) const {
+        if (cell[a] != 0) return true;
+        std::vector<int8_t> b = cell;
+        b[a] = (int8_t)p;
+        std::vector<char> seen(A, 0);
+        std::vector<int> st;
+        int nb[4], k = adj(a, nb);
+        for (int j = 0; j < k; ++j)
+            if (b[nb[j]] == 3 - p && !seen[nb[j]] && !group(b, nb[j], st, seen)) return false;
+        std::fill(seen.begin(), seen.end(), 0);
+        return !group(b, a, st, seen);
+    }
+    uint64_t board_hash(const std::vector<int8_t>& b) const {
+        uint64_t h = 0;
+        for (int a = 0; a < A; ++a) if (b[a]) h ^= z->piece[(b[a] - 1) * A + a];
+        return h;
+    }
+    // updateHash (:846-877): stones ^ player ^ ko feature ^ rules(Chinese = 1) ^ komi(int(komi*2) & 15)
+    uint64_t hash_of(const std::vector<int8_t>& b, int pl, int k) const {
+        uint64_t h = board_hash(b) ^ z->player[pl - 1];
+        if (k >= 0) h ^= z->ko[k % (A + 1)];
+        h ^= z->rules[1];
+        h ^= z->komi[((int)(komi * 2)) & 0xF];
+        return h;
+    }
+    uint64_t hash() const { return hash_of(cell, player, ko); }
+    // getLegalMoves (:116-160): pass first, then every valid point whose resulting position (same
+    // side to move, the old ko point) is not in position_history_
+    std::vector<int> legal() const {
+        std::vector<int> out{-1};
+        for (int a = 0; a < A; ++a) {
+            if (cell[a] != 0 || a == ko || suicidal(a, player)) continue;
+            std::vector<int8_t> b = cell;
+            b[a] = (int8_t)player;
+            capture(b, 3 - player);
+            uint64_t h = hash_of(b, player, ko);
+            if (std::find(poshist.begin(), poshist.end(), h) == poshist.end()) out.push_back(a);
+        }
+        return out;
+    }
+    // makeMove (:192-257)
+    void play(int a) {
+        if (a == -1) {
+            ++passes;
+            ko = -1;
+            history.push_back(a);
+        } else {
+            passes = 0;
+            cell[a] = (int8_t)player;
+            auto caps = capture(cell, 3 - player);
+            int n = 0;
+            for (auto& g : caps) n += (int)g.size();
+            ko = (caps.size() == 1 && caps[0].size() == 1) ? caps[0][0] : -1;
+            captured[player] += n;
+            history.push_back(a);
+            poshist.push_back(hash());
+        }
+        player = 3 - player;
+    }
+    // GoRules::getTerritoryOwnership + calculateScores (go_rules.cpp:211-361), Chinese rules
+    std::pair<float, float> score() const {
+        std::vector<int> terr(A, 0);
+        std::vector<char> vis(A, 0);
+        for (int p = 0; p < A; ++p) {
+            if (cell[p] != 0 || vis[p]) continue;
+            std::vector<int> reg{p};
+            vis[p] = 1;
+            bool tb = false, tw = false;
+            for (size_t i = 0; i < reg.size(); ++i) {
+                int nb[4], k = adj(reg[i], nb);
+                for (int j = 0; j < k; ++j) {
+                    int s = cell[nb[j]];
+                    if (s == 0) { if (!vis[nb[j]]) { vis[nb[j]] = 1; reg.push_back(nb[j]); } }
+                    else if (s == 1) tb = true;
+                    else tw = true;
+                }
+            }
+            int col = (tb && !tw) ? 1 : (tw && !tb) ? 2 : 0;
+            for (int r : reg) terr[r] = col;
+        }
+        for (int p = 0; p < A; ++p) if (cell[p]) terr[p] = cell[p];
+        float bsc = 0.0f, wsc = 0.0f;
+        for (int p = 0; p < A; ++p) {
+            if (terr[p] == 1) bsc += 1.0f;
+            else if (terr[p] == 2) wsc += 1.0f;
+        }
+        wsc += komi;
+        return {bsc, wsc};
+    }
+    GameResult result() const {                     // getGameResult (:295-312)
+        if (passes < 2) return ONGOING;
+        auto sc = score();
+        if (sc.first > sc.second) return WIN_P1;
+        if (sc.second > sc.first) return WIN_P2;
+        return DRAW;
+    }
+    bool terminal() const { return passes >= 2; }
+    // getEnhancedTensorRepresentation (:338-420): black, white, black-to-move, black / white group
+    // liberties min(1, libs/10), ko point, border distances x / y
+    void planes(float* out) const {
+        std::fill(out, out + 8 * A, 0.0f);
+        for (int a = 0; a < A; ++a) {
+            if (cell[a] == 1) out[a] = 1.0f;
+            else if (cell[a] == 2) out[A + a] = 1.0f;
+            out[2 * A + a] = player == 1 ? 1.0f : 0.0f;
+        }
+        std::vector<char> seen(A, 0);
+        std::vector<int> st;
+        for (int p = 0; p < A; ++p) {
+            if (!cell[p] || seen[p]) continue;
+            group(cell, p, st, seen);
+            float l = std::min(1.0f, (float)count_libs(cell, st) / 10.0f);
+            for (int s : st) out[(cell[p] == 1 ? 3 : 4) * A + s] = l;
+        }
+        if (ko >= 0) out[5 * A + ko] = 1.0f;
+        for (int y = 0; y < bs; ++y)
+            for (int x = 0; x < bs; ++x) {
+                out[6 * A + y * bs + x] = (float)std::min(x, bs - 1 - x) / (bs / 2);
+                out[7 * A + y * bs + x] = (float)std::min(y, bs - 1 - y) / (bs / 2);
+            }
+    }
+};
+
+// ---------------------------------------------------------------------------
 // Evaluators
+template <class S>
 struct Evaluator {
     virtual ~Evaluator() {}
-    virtual void eval(int game, const State& s, std::vector<float>& policy, float& value) = 0;
+    virtual void eval(int game, const S& s, std::vector<float>& policy, float& value) = 0;
     long calls = 0;
 };
 
 // HashEvaluator (same definition as oracle/ref_harness.cpp hash_eval)
-struct HashEval : Evaluator {
-    void eval(int, const State& s, std::vector<float>& p, float& v) override {
-        ++calls;
+template <class S>
+struct HashEval : Evaluator<S> {
+    void eval(int, const S& s, std::vector<float>& p, float& v) override {
+        ++this->calls;
         uint64_t key = splitmix64(s.hash() ^ 0x5A17C0DEULL);
         for (int i = 0; i < 6; ++i) {
             int m = (i < (int)s.history.size()) ? s.history[s.history.size() - 1 - i] : -1;
             key = splitmix64(key + (uint64_t)(uint32_t)(m + 2));
         }
-        p.assign(s.A, 0.0f);
-        for (int a = 0; a < s.A; ++a) {
+        p.assign(s.NA(), 0.0f);
+        for (int a = 0; a < s.NA(); ++a) {
             uint64_t r = splitmix64(key ^ ((uint64_t)(a + 1) * 0x9E3779B97F4A7C15ULL));
             p[a] = (float)(uint32_t)(r >> 40) * (1.0f / 16777216.0f);
         }
@@ -182,7 +392,7 @@ struct HashEval : Evaluator {
 };
 
 // RandomPolicyNetwork (src/nn/random_policy_network.cpp:9-24,93-138), one instance per game.
-struct RandomEval : Evaluator {
+struct RandomEval : Evaluator<State> {
     std::vector<std::mt19937> rng;
     RandomEval(int games, unsigned seed) { for (int g = 0; g < games; ++g) rng.emplace_back(seed + g); }
     void eval(int game, const State& s, std::vector<float>& p, float& v) override {
@@ -201,14 +411,15 @@ struct RandomEval : Evaluator {
 
 // No network: ParallelMCTS::evaluateState's fallback (src/mcts/parallel_mcts.cpp:903-916),
 // 1/|legal| on the legal actions, value 0.
-struct UniformEval : Evaluator {
-    void eval(int, const State& s, std::vector<float>& p, float& v) override {
-        ++calls;
-        p.assign(s.A, 0.0f);
+template <class S>
+struct UniformEval : Evaluator<S> {
+    void eval(int, const S& s, std::vector<float>& p, float& v) override {
+        ++this->calls;
+        p.assign(s.NA(), 0.0f);
         auto legal = s.legal();
         if (!legal.empty()) {
             const float u = 1.0f / (float)legal.size();
-            for (int m : legal) p[m] = u;
+            for (int m : legal) if (m >= 0 && m < (int)p.size()) p[m] = u;
         }
         v = 0.0f;
     }
@@ -219,16 +430,17 @@ struct UniformEval : Evaluator {
 // applied here.  Replay evaluator: the callback returns final (post-softmax) policy.
 typedef int (*az_eval_cb)(void* user, int game, const float* planes, int n_planes, int A,
                           float* policy_out, float* value_out);
-struct CallbackEval : Evaluator {
+template <class S>
+struct CallbackEval : Evaluator<S> {
     az_eval_cb cb; void* user; bool softmax;
     std::vector<float> buf;
     CallbackEval(az_eval_cb c, void* u, bool sm) : cb(c), user(u), softmax(sm) {}
-    void eval(int game, const State& s, std::vector<float>& p, float& v) override {
-        ++calls;
-        buf.resize(11 * s.A);
+    void eval(int game, const S& s, std::vector<float>& p, float& v) override {
+        ++this->calls;
+        buf.resize(S::NPLANES * s.A);
         s.planes(buf.data());
-        p.assign(s.A, 0.0f);
-        if (cb(user, game, buf.data(), 11, s.A, p.data(), &v) != 0) { std::fprintf(stderr, "eval cb failed\n"); std::abort(); }
+        p.assign(s.NA(), 0.0f);
+        if (cb(user, game, buf.data(), S::NPLANES, s.NA(), p.data(), &v) != 0) { std::fprintf(stderr, "eval cb failed\n"); std::abort(); }
         if (softmax) {
             float mx = *std::max_element(p.begin(), p.end());
             float sum = 0.0f;
@@ -292,16 +504,17 @@ float convert_value(GameResult r, int player) {   // parallel_mcts.cpp:973-985
     }
 }
 
+template <class State, class Zob>
 struct Search {
     const Cfg& cfg;
     int game;
-    Evaluator* ev;
+    Evaluator<State>* ev;
     TT tt;
     std::vector<Node> nodes;
     int root = 0;
     State rootState;
     std::mt19937 rng;
-    Search(const Cfg& c, int g, Evaluator* e, const Zobrist* z)
+    Search(const Cfg& c, int g, Evaluator<State>* e, const Zob* z)
         : cfg(c), game(g), ev(e), tt(c.tt_log2), rootState(c.bs, z), rng(c.noise_seed) {
         nodes.emplace_back();     // root (parallel_mcts.cpp:68), parent = none
         nodes.reserve(1 << 16);
@@ -363,7 +576,7 @@ struct Search {
     void evaluate(const State& s, std::vector<float>& p, float& v) {
         if (s.terminal()) {
             v = convert_value(s.result(), s.player);
-            p.assign(s.A, 1.0f / (float)s.A);
+            p.assign(s.NA(), 1.0f / (float)s.NA());
             return;
         }
         if (tt.lookup(s.hash(), p, v)) return;
@@ -543,34 +756,21 @@ struct az_oracle_cfg {
     float cpuct, fpu, alpha, eps, t_init, t_final;
     unsigned noise_seed, zobrist_seed, eval_seed;
     int n_games;
+    int game;                                                                         // 0 Gomoku, 1 Go
 };
 
 void az_oracle_free(char* p) { std::free(p); }
 
-// Plays cfg->n_games independent games (game g uses noise seed noise_seed + g when
-// n_games > 1 is driven with per-game seeds by the caller: here all games share
-// cfg->noise_seed unless seed_stride != 0).  Output: JSON identical in structure to
-// oracle/ref_harness `game` mode, one document per game in a JSON array.
-char* az_oracle_play(const az_oracle_cfg* c, int seed_stride, az_eval_cb cb, void* user) {
-    Cfg cfg;
-    cfg.bs = c->bs; cfg.sims = c->sims; cfg.max_moves = c->max_moves; cfg.vl = c->vl;
-    cfg.noise_each_search = c->noise_each_search; cfg.temp_drop = c->temp_drop; cfg.tt_log2 = c->tt_log2;
-    cfg.cpuct = c->cpuct; cfg.fpu = c->fpu; cfg.alpha = c->alpha; cfg.eps = c->eps;
-    cfg.t_init = c->t_init; cfg.t_final = c->t_final;
-    cfg.zobrist_seed = c->zobrist_seed;
-    Zobrist z(cfg.bs * cfg.bs, cfg.zobrist_seed);
-    std::ostringstream o;
-    o << "[";
-    HashEval he; RandomEval re(c->n_games, c->eval_seed);
-    CallbackEval ne(cb, user, c->eval_kind == 2);
-    UniformEval ue;
-    Evaluator* ev = c->eval_kind == 0 ? (Evaluator*)&he : c->eval_kind == 1 ? (Evaluator*)&re
-                  : c->eval_kind == 4 ? (Evaluator*)&ue : (Evaluator*)&ne;
+}  // extern "C"
+
+namespace {
+template <class S, class Z>
+void play_games(const az_oracle_cfg* c, const Cfg& cfg, const Z& z, Evaluator<S>* ev, int seed_stride, std::ostringstream& o) {
     for (int g = 0; g < c->n_games; ++g) {
         Cfg gc = cfg;
         gc.noise_seed = c->noise_seed + (unsigned)(seed_stride * g);
-        Search m(gc, g, ev, &z);
-        State st(cfg.bs, &z);       // SelfPlayManager's own state (self_play_manager.cpp:157)
+        Search<S, Z> m(gc, g, ev, &z);
+        S st(cfg.bs, &z);           // SelfPlayManager's own state (self_play_manager.cpp:157)
         long evals0 = ev->calls;
         m.add_noise(cfg.alpha, cfg.eps);
         if (g) o << ",";
@@ -601,6 +801,39 @@ char* az_oracle_play(const az_oracle_cfg* c, int seed_stride, az_eval_cb cb, voi
         GameResult res = st.result();
         o << "],\"terminal\":" << (res != ONGOING ? 1 : 0) << ",\"result\":" << (int)res << "}";
     }
+}
+}  // namespace
+
+extern "C" {
+
+// Plays cfg->n_games independent games (game g uses noise seed noise_seed + g * seed_stride).
+// Output: JSON identical in structure to oracle/ref_harness `game` mode, one document per game
+// in a JSON array.
+char* az_oracle_play(const az_oracle_cfg* c, int seed_stride, az_eval_cb cb, void* user) {
+    Cfg cfg;
+    cfg.bs = c->bs; cfg.sims = c->sims; cfg.max_moves = c->max_moves; cfg.vl = c->vl;
+    cfg.noise_each_search = c->noise_each_search; cfg.temp_drop = c->temp_drop; cfg.tt_log2 = c->tt_log2;
+    cfg.cpuct = c->cpuct; cfg.fpu = c->fpu; cfg.alpha = c->alpha; cfg.eps = c->eps;
+    cfg.t_init = c->t_init; cfg.t_final = c->t_final;
+    cfg.zobrist_seed = c->zobrist_seed;
+    std::ostringstream o;
+    o << "[";
+    if (c->game == 1) {
+        GoZobrist z(cfg.bs * cfg.bs, cfg.zobrist_seed);
+        HashEval<GoState> he; CallbackEval<GoState> ne(cb, user, c->eval_kind == 2); UniformEval<GoState> ue;
+        Evaluator<GoState>* ev = c->eval_kind == 0 ? (Evaluator<GoState>*)&he
+                               : c->eval_kind == 4 ? (Evaluator<GoState>*)&ue : (Evaluator<GoState>*)&ne;
+        if (c->eval_kind == 1) return nullptr;     // RandomPolicyNetwork is Gomoku-only here
+        play_games<GoState, GoZobrist>(c, cfg, z, ev, seed_stride, o);
+    } else {
+        Zobrist z(cfg.bs * cfg.bs, cfg.zobrist_seed);
+        HashEval<State> he; RandomEval re(c->n_games, c->eval_seed);
+        CallbackEval<State> ne(cb, user, c->eval_kind == 2);
+        UniformEval<State> ue;
+        Evaluator<State>* ev = c->eval_kind == 0 ? (Evaluator<State>*)&he : c->eval_kind == 1 ? (Evaluator<State>*)&re
+                             : c->eval_kind == 4 ? (Evaluator<State>*)&ue : (Evaluator<State>*)&ne;
+        play_games<State, Zobrist>(c, cfg, z, ev, seed_stride, o);
+    }
     o << "]";
     return dup(o.str());
 }
@@ -615,6 +848,23 @@ int az_oracle_position(int bs, unsigned zobrist_seed, const int* moves, int n, f
     if (hash_out) *hash_out = s.hash();
     if (result_out) *result_out = (int)s.result();
     if (legal_out) { auto l = s.legal(); std::copy(l.begin(), l.end(), legal_out); *n_legal = (int)l.size(); }
+    return 0;
+}
+
+// GoState after a move sequence: planes [8][A], hash, result, ko, legal order, board, score bits.
+int az_oracle_go_position(int bs, unsigned zobrist_seed, const int* moves, int n, float* planes_out,
+                          uint64_t* hash_out, int* result_out, int* ko_out, int* legal_out, int* n_legal,
+                          int* board_out, float* score_out) {
+    GoZobrist z(bs * bs, zobrist_seed);
+    GoState s(bs, &z);
+    for (int i = 0; i < n; ++i) s.play(moves[i]);
+    if (planes_out) s.planes(planes_out);
+    if (hash_out) *hash_out = s.hash();
+    if (result_out) *result_out = (int)s.result();
+    if (ko_out) *ko_out = s.ko;
+    if (legal_out) { auto l = s.legal(); std::copy(l.begin(), l.end(), legal_out); *n_legal = (int)l.size(); }
+    if (board_out) for (int a = 0; a < s.A; ++a) board_out[a] = s.cell[a];
+    if (score_out) { auto sc = s.score(); score_out[0] = sc.first; score_out[1] = sc.second; }
     return 0;
 }
 

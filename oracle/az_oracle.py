@@ -30,7 +30,9 @@ class OracleCfg(ctypes.Structure):
                 ("cpuct", ctypes.c_float), ("fpu", ctypes.c_float), ("alpha", ctypes.c_float),
                 ("eps", ctypes.c_float), ("t_init", ctypes.c_float), ("t_final", ctypes.c_float),
                 ("noise_seed", ctypes.c_uint), ("zobrist_seed", ctypes.c_uint), ("eval_seed", ctypes.c_uint),
-                ("n_games", ctypes.c_int)]
+                ("n_games", ctypes.c_int), ("game", ctypes.c_int)]
+
+GAME_GOMOKU, GAME_GO = 0, 1
 
 
 def build():
@@ -54,6 +56,11 @@ def lib():
                                          ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_uint64),
                                          ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int),
                                          ctypes.POINTER(ctypes.c_int)]
+        L.az_oracle_go_position.argtypes = [ctypes.c_int, ctypes.c_uint, ctypes.POINTER(ctypes.c_int), ctypes.c_int,
+                                            ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_uint64),
+                                            ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int),
+                                            ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int),
+                                            ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_float)]
         L.az_oracle_fresh_order.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
         L.az_oracle_gamma.argtypes = [ctypes.c_uint, ctypes.c_float, ctypes.c_int, ctypes.c_int,
                                       ctypes.POINTER(ctypes.c_float)]
@@ -63,23 +70,24 @@ def lib():
 
 def make_cfg(bs=9, sims=100, max_moves=1 << 30, eval_kind=EVAL_HASH, eval_seed=7, n_games=1,
              noise_each_search=0, cpuct=1.5, fpu=0.0, vl=3, alpha=0.03, eps=0.25, temp_drop=30,
-             t_init=1.0, t_final=0.0, noise_seed=42, zobrist_seed=12345, tt_log2=20):
+             t_init=1.0, t_final=0.0, noise_seed=42, zobrist_seed=12345, tt_log2=20, game=GAME_GOMOKU):
     return OracleCfg(bs, sims, max_moves, vl, noise_each_search, temp_drop, tt_log2, eval_kind,
-                     cpuct, fpu, alpha, eps, t_init, t_final, noise_seed, zobrist_seed, eval_seed, n_games)
+                     cpuct, fpu, alpha, eps, t_init, t_final, noise_seed, zobrist_seed, eval_seed, n_games, game)
 
 
 def play(seed_stride=0, evaluator=None, **kw):
     """Play games with the restated Mode S loop; returns a list of per-game dicts
     with the same structure as oracle/_ref/ref_harness `game` output.
 
-    evaluator(game, planes[11,bs,bs] float32) -> (policy[A] float32, value float)
+    evaluator(game, planes[n_planes,bs,bs] float32) -> (policy[A] float32, value float)
+    (11 planes / A = bs*bs for Gomoku, 8 planes / A = bs*bs + 1 for Go)
     is used for eval_kind EVAL_NET (raw logits; softmax applied as the reference)
     and EVAL_REPLAY (final policy)."""
     cfg = make_cfg(**kw)
 
     def _cb(user, game, planes, n_planes, A, pol, val):
         try:
-            bs = int(round(A ** 0.5))
+            bs = int(round((A - (1 if cfg.game == GAME_GO else 0)) ** 0.5))
             x = np.ctypeslib.as_array(planes, shape=(n_planes, bs, bs)).copy()
             p, v = evaluator(game, x)
             p = np.asarray(p, dtype=np.float32).reshape(-1)
@@ -92,6 +100,8 @@ def play(seed_stride=0, evaluator=None, **kw):
 
     cb = EVAL_CB(_cb)
     ptr = lib().az_oracle_play(ctypes.byref(cfg), seed_stride, cb, None)
+    if not ptr:
+        raise ValueError("az_oracle_play: unsupported configuration")
     try:
         s = ctypes.string_at(ptr).decode()
     finally:
@@ -112,6 +122,23 @@ def position(bs, moves, zobrist_seed=12345):
                              planes.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), ctypes.byref(h),
                              ctypes.byref(res), legal, ctypes.byref(nl))
     return planes.reshape(11, bs, bs), h.value, res.value, list(legal[:nl.value])
+
+
+def go_position(bs, moves, zobrist_seed=12345):
+    """GoState after `moves`: dict of planes[8,bs,bs], hash, result, ko, legal order, board, score."""
+    A = bs * bs
+    mv = (ctypes.c_int * max(1, len(moves)))(*moves)
+    planes = np.zeros(8 * A, dtype=np.float32)
+    h = ctypes.c_uint64(0)
+    res, ko, nl = ctypes.c_int(0), ctypes.c_int(0), ctypes.c_int(0)
+    legal = (ctypes.c_int * (A + 1))()
+    board = (ctypes.c_int * A)()
+    score = (ctypes.c_float * 2)()
+    lib().az_oracle_go_position(bs, zobrist_seed, mv, len(moves),
+                                planes.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), ctypes.byref(h),
+                                ctypes.byref(res), ctypes.byref(ko), legal, ctypes.byref(nl), board, score)
+    return {"planes": planes.reshape(8, bs, bs), "hash": h.value, "result": res.value, "ko": ko.value,
+            "legal": list(legal[:nl.value]), "board": list(board), "score": (score[0], score[1])}
 
 
 def fresh_order(bs):

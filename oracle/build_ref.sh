@@ -17,6 +17,7 @@
 #                              exists; fixed seed => deterministic Zobrist keys)
 #   P5 mcts_node.h:64 + parallel_mcts.cpp  std::mutex expansionMutex -> std::recursive_mutex
 #                              (removes the F3 self-deadlock; no arithmetic change)
+#   P6 go_state.cpp:21         zobrist_(GameType::GO,bs,2) -> zobrist_(bs, 2, 2, 12345u)  (as P2, for GoState)
 set -euo pipefail
 REF=${REF:-/root/reference}
 HERE=$(cd "$(dirname "$0")" && pwd)
@@ -28,11 +29,12 @@ fi
 mkdir -p "$OUT"
 TMP=$(mktemp -d /tmp/az_refbuild.XXXXXX)
 trap 'rm -rf "$TMP"' EXIT
-mkdir -p "$TMP/src/mcts" "$TMP/src/nn" "$TMP/src/games/gomoku" "$TMP/src/core"
+mkdir -p "$TMP/src/mcts" "$TMP/src/nn" "$TMP/src/games/gomoku" "$TMP/src/games/go" "$TMP/src/core"
 cp -r "$REF/include" "$TMP/include"
 cp "$REF"/src/mcts/{parallel_mcts,mcts_node,transposition_table,thread_pool}.cpp "$TMP/src/mcts/"
 cp "$REF"/src/nn/{batch_queue,random_policy_network}.cpp "$TMP/src/nn/"
 cp "$REF"/src/games/gomoku/{gomoku_state,gomoku_rules}.cpp "$TMP/src/games/gomoku/"
+cp "$REF"/src/games/go/{go_state,go_rules}.cpp "$TMP/src/games/go/"
 cp "$REF"/src/core/zobrist_hash.cpp "$TMP/src/core/"
 chmod -R u+w "$TMP"
 
@@ -42,6 +44,9 @@ grep -q 'this, i, numThreads, &completedSimulations' "$TMP/src/mcts/parallel_mct
 # P2
 sed -i '32s/zobrist_(core::GameType::GOMOKU, board_size, 2)/zobrist_(board_size, 2, 2, 12345u)/' "$TMP/src/games/gomoku/gomoku_state.cpp"
 grep -q 'zobrist_(board_size, 2, 2, 12345u)' "$TMP/src/games/gomoku/gomoku_state.cpp"
+# P6
+sed -i '21s/zobrist_(core::GameType::GO, board_size, 2)/zobrist_(board_size, 2, 2, 12345u)/' "$TMP/src/games/go/go_state.cpp"
+grep -q 'zobrist_(board_size, 2, 2, 12345u)' "$TMP/src/games/go/go_state.cpp"
 # P5
 sed -i '64s/std::mutex expansionMutex;/std::recursive_mutex expansionMutex;/' "$TMP/include/alphazero/mcts/mcts_node.h"
 grep -q 'std::recursive_mutex expansionMutex;' "$TMP/include/alphazero/mcts/mcts_node.h"
@@ -50,7 +55,7 @@ test "$(grep -c 'lock_guard<std::recursive_mutex> lock(.*expansionMutex)' "$TMP/
 
 CXXFLAGS="-std=c++17 -O2 -pthread -DLIBTORCH_OFF -I$TMP/include"
 OBJS=()
-for f in "$TMP"/src/mcts/*.cpp "$TMP"/src/nn/*.cpp "$TMP"/src/games/gomoku/*.cpp "$TMP"/src/core/*.cpp; do
+for f in "$TMP"/src/mcts/*.cpp "$TMP"/src/nn/*.cpp "$TMP"/src/games/gomoku/*.cpp "$TMP"/src/games/go/*.cpp "$TMP"/src/core/*.cpp; do
   o="$TMP/$(basename "$f" .cpp).o"
   g++ $CXXFLAGS -w -c "$f" -o "$o" &
   OBJS+=("$o")

@@ -14,6 +14,8 @@
 //             hash (:620-656), terminal/result (:477-529), legal-move order.
 //   gamma     libstdc++ gamma_distribution<float> draws on mt19937(42), as used
 //             by ParallelMCTS::addDirichletNoise (parallel_mcts.cpp:1136-1142).
+//   go_positions / go_game  the same for GoState(bs, komi 7.5, Chinese rules, superko)
+//             (src/games/go/go_state.cpp, go_rules.cpp; patch P6 seeds its Zobrist keys).
 //
 // Evaluators: the reference's own RandomPolicyNetwork(seed) (random_policy_network.cpp)
 // and HashEvaluator, a pure function of (Zobrist hash, last 6 moves) that the engine
@@ -56,6 +58,7 @@
 #include "alphazero/mcts/parallel_mcts.h"
 #include "alphazero/mcts/transposition_table.h"
 #include "alphazero/games/gomoku/gomoku_state.h"
+#include "alphazero/games/go/go_state.h"
 #include "alphazero/nn/random_policy_network.h"
 #undef private
 #undef protected
@@ -139,8 +142,10 @@ static void dump_node_children(std::ostream& o, const mcts::MCTSNode* n) {
 }
 
 static int run_game(int bs, int sims, int maxMoves, const std::string& evalKind, unsigned evalSeed,
-                    int noiseEachSearch, float cpuct, float fpu) {
-    auto state = std::make_unique<gomoku::GomokuState>(bs, false, false, 1, false);
+                    int noiseEachSearch, float cpuct, float fpu, bool go = false) {
+    std::unique_ptr<core::IGameState> state;
+    if (go) state = std::make_unique<go::GoState>(bs, 7.5f, true, true);
+    else state = std::make_unique<gomoku::GomokuState>(bs, false, false, 1, false);
     mcts::TranspositionTable tt(1048576);
     mcts::MCTSConfig cfg;
     cfg.numThreads = 1;
@@ -159,7 +164,7 @@ static int run_game(int bs, int sims, int maxMoves, const std::string& evalKind,
     const float alpha = 0.03f, eps = 0.25f;
     m.addDirichletNoise(alpha, eps);
     std::ostream& o = std::cout;
-    o << "{\"mode\":\"game\",\"bs\":" << bs << ",\"sims\":" << sims << ",\"eval\":\"" << evalKind
+    o << "{\"mode\":\"" << (go ? "go_game" : "game") << "\",\"bs\":" << bs << ",\"sims\":" << sims << ",\"eval\":\"" << evalKind
       << "\",\"eval_seed\":" << evalSeed << ",\"noise_each_search\":" << noiseEachSearch
       << ",\"cpuct_bits\":" << fbits(cpuct) << ",\"fpu_bits\":" << fbits(fpu)
       << ",\"init_root\":";
@@ -236,6 +241,52 @@ static int run_positions(int bs, int count, unsigned seed) {
     return 0;
 }
 
+// GoState positions: random legal play (passes included, weight 1/16) from the empty board.
+static int run_go_positions(int bs, int count, unsigned seed) {
+    std::mt19937 g(seed);
+    std::ostream& o = std::cout;
+    o << "{\"mode\":\"go_positions\",\"bs\":" << bs << ",\"positions\":[";
+    for (int k = 0; k < count; ++k) {
+        go::GoState s(bs, 7.5f, true, true);
+        int target = (int)(g() % (unsigned)(2 * bs * bs));
+        std::vector<int> moves;
+        while ((int)moves.size() < target && !s.isTerminal()) {
+            auto legal = s.getLegalMoves();
+            int a = (g() % 16 == 0) ? -1 : legal[1 + g() % (legal.size() - 1 > 0 ? legal.size() - 1 : 1)];
+            if (legal.size() == 1) a = -1;
+            s.makeMove(a);
+            moves.push_back(a);
+        }
+        auto planes = s.getEnhancedTensorRepresentation();
+        auto sc = s.calculateScore();
+        if (k) o << ",";
+        o << "{\"moves\":[";
+        for (size_t i = 0; i < moves.size(); ++i) o << (i ? "," : "") << moves[i];
+        o << "],\"hash\":\"" << s.getHash() << "\",\"terminal\":" << (s.isTerminal() ? 1 : 0)
+          << ",\"result\":" << (int)s.getGameResult() << ",\"player\":" << s.getCurrentPlayer()
+          << ",\"ko\":" << s.getKoPoint() << ",\"captured\":[" << s.getCapturedStones(1) << "," << s.getCapturedStones(2)
+          << "],\"score\":[" << fbits(sc.first) << "," << fbits(sc.second) << "],\"legal\":[";
+        auto legal = s.getLegalMoves();
+        for (size_t i = 0; i < legal.size(); ++i) o << (i ? "," : "") << legal[i];
+        o << "],\"board\":[";
+        for (int a = 0; a < bs * bs; ++a) o << (a ? "," : "") << s.getStone(a);
+        o << "],\"planes\":[";
+        bool first = true;
+        for (size_t p = 0; p < planes.size(); ++p)
+            for (int y = 0; y < bs; ++y)
+                for (int x = 0; x < bs; ++x) {
+                    float v = planes[p][y][x];
+                    if (v != 0.0f) {
+                        o << (first ? "" : ",") << "[" << (p * bs * bs + y * bs + x) << "," << fbits(v) << "]";
+                        first = false;
+                    }
+                }
+        o << "],\"nplanes\":" << planes.size() << "}";
+    }
+    o << "]}\n";
+    return 0;
+}
+
 static int run_gamma(float alpha, int n, int calls) {
     std::mt19937 rng(42);
     std::ostream& o = std::cout;
@@ -252,7 +303,7 @@ static int run_gamma(float alpha, int n, int calls) {
 }
 
 int main(int argc, char** argv) {
-    if (argc < 2) { std::fprintf(stderr, "usage: ref_harness game|positions|gamma ...\n"); return 2; }
+    if (argc < 2) { std::fprintf(stderr, "usage: ref_harness game|positions|gamma|go_positions|go_game ...\n"); return 2; }
     std::string mode = argv[1];
     auto I = [&](int i, int d) { return argc > i ? std::atoi(argv[i]) : d; };
     auto F = [&](int i, float d) { return argc > i ? (float)std::atof(argv[i]) : d; };
@@ -261,6 +312,10 @@ int main(int argc, char** argv) {
                         F(8, 1.5f), F(9, 0.0f));
     if (mode == "positions") return run_positions(I(2, 9), I(3, 16), (unsigned)I(4, 1));
     if (mode == "gamma") return run_gamma(F(2, 0.03f), I(3, 81), I(4, 4));
+    if (mode == "go_positions") return run_go_positions(I(2, 9), I(3, 16), (unsigned)I(4, 1));
+    if (mode == "go_game")
+        return run_game(I(2, 9), I(3, 100), I(4, 1000), argc > 5 ? argv[5] : "hash", (unsigned)I(6, 7), I(7, 0),
+                        F(8, 1.5f), F(9, 0.0f), true);
     std::fprintf(stderr, "unknown mode\n");
     return 2;
 }

@@ -3,7 +3,7 @@
 REFERENCE build (oracle/_ref/ref_harness, built by oracle/build_ref.sh from the
 sources under /root/reference).  Run from the repo root:
 
-    oracle/build_ref.sh && python3 tests/golden/gen_golden.py
+    oracle/build_ref.sh && python3 tests/golden/gen_golden.py [--only go]
 
 Fixtures are data only: the harness' JSON output (inputs = case parameters,
 outputs = per-move root statistics as raw fp32 bit patterns).
@@ -30,6 +30,16 @@ GAME_CASES = [
     (15, 800, 2, "hash", 5, 0, 1.5, 0.0),        # C3 shape: 15x15, 800 sims
 ]
 
+# GoState (9/13/19, komi 7.5, Chinese area scoring, positional superko), same tuple layout
+GO_GAME_CASES = [
+    (9, 100, 80, "hash", 3, 0, 1.5, 0.0),       # 75 plies: captures, ko, ends pass / pass (area scoring)
+    (9, 150, 40, "hash", 11, 0, 1.5, 0.0),
+    (9, 30, 1000, "hash", 7, 0, 1.5, 0.0),      # sims < children: every child once, pass first -> pass / pass
+    (9, 60, 30, "hash", 5, 1, 1.5, 0.25),       # useDirichletNoise per search + FPU
+    (13, 300, 8, "hash", 7, 0, 1.5, 0.0),
+    (19, 500, 2, "hash", 7, 0, 1.5, 0.0),       # C4 board
+]
+
 
 def run(*args):
     r = subprocess.run([HARNESS] + [str(a) for a in args], capture_output=True, text=True, timeout=900)
@@ -41,6 +51,19 @@ def run(*args):
 def main():
     if not os.path.exists(HARNESS):
         sys.exit("build oracle/_ref/ref_harness first (oracle/build_ref.sh)")
+    go = []
+    for c in GO_GAME_CASES:
+        d = run("go_game", *c)
+        d["case"] = list(c)
+        go.append(d)
+        print("go_game", c, "moves", len(d["moves"]), "result", d["result"])
+    with gzip.open(os.path.join(OUT, "ref_go_games.json.gz"), "wt") as f:
+        json.dump(go, f, separators=(",", ":"))
+    gp = {str(bs): run("go_positions", bs, n, seed) for bs, n, seed in [(9, 64, 1), (13, 24, 2), (19, 12, 3)]}
+    with gzip.open(os.path.join(OUT, "ref_go_positions.json.gz"), "wt") as f:
+        json.dump(gp, f, separators=(",", ":"))
+    if sys.argv[1:] == ["--only", "go"]:
+        return
     games = []
     for c in GAME_CASES:
         d = run("game", *c)

@@ -71,3 +71,55 @@ def test_oracle_gamma_matches_reference():
     calls = g["calls"]
     got = O.gamma_draws(42, alpha, len(calls), len(calls[0]))
     assert got.view(np.uint32).tolist() == calls
+
+
+# ---------------------------------------------------------------- Go
+GO_GAMES = _load("ref_go_games.json.gz")
+
+
+def _f32(b):
+    return float(np.array([b], dtype=np.uint32).view(np.float32)[0])
+
+
+@pytest.mark.parametrize("bs", [9, 13, 19])
+def test_oracle_go_positions_match_reference(bs):
+    """GoState restatement vs the reference GoState (go_state.cpp / go_rules.cpp): board after
+    captures, ko point, Zobrist hash (pieces, side, ko / rules / komi features), legal-move order
+    with suicide, ko and positional superko, area score, result and the 8 feature planes."""
+    pos = _load("ref_go_positions.json.gz")[str(bs)]
+    for k, p in enumerate(pos["positions"]):
+        g = O.go_position(bs, p["moves"])
+        assert g["board"] == p["board"], k
+        assert g["ko"] == p["ko"], k
+        assert str(g["hash"]) == p["hash"], k
+        assert g["legal"] == p["legal"], k
+        assert g["result"] == p["result"], k
+        assert [int(np.array([x], np.float32).view(np.uint32)[0]) for x in g["score"]] == p["score"], k
+        flat = g["planes"].reshape(-1)
+        ref = np.zeros_like(flat)
+        for i, bits in p["planes"]:
+            ref[i] = _f32(bits)
+        assert p["nplanes"] == 8
+        assert np.array_equal(flat.view(np.uint32), ref.view(np.uint32)), k
+
+
+def test_go_golden_covers_captures_ko_and_scoring():
+    pos = [p for v in _load("ref_go_positions.json.gz").values() for p in v["positions"]]
+    assert any(sum(p["captured"]) > 0 for p in pos)       # captures happened
+    assert any(p["ko"] >= 0 for p in pos)                  # a ko point is live
+    assert any(p["terminal"] for p in pos)                 # pass / pass, area scoring
+    assert any(len(p["legal"]) - 1 < sum(1 for c in p["board"] if c == 0) for p in pos)  # an empty point is illegal
+
+
+@pytest.mark.parametrize("idx", range(len(GO_GAMES)), ids=[str(g["case"]) for g in GO_GAMES])
+def test_oracle_go_game_matches_reference(idx):
+    ref = GO_GAMES[idx]
+    bs, sims, mm, ev, es, nes, cp, fpu = ref["case"]
+    got = O.play(bs=bs, sims=sims, max_moves=mm, eval_kind=O.EVAL_HASH, eval_seed=es, noise_each_search=nes,
+                 cpuct=cp, fpu=fpu, game=O.GAME_GO)[0]
+    assert got["init_root"] == ref["init_root"]
+    assert len(got["moves"]) == len(ref["moves"])
+    for a, b in zip(ref["moves"], got["moves"]):
+        for k in ("root", "children", "probs", "action", "value", "tt_lookups", "tt_hits", "evals"):
+            assert a[k] == b[k], (a["ply"], k)
+    assert got["result"] == ref["result"]

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
-"""Trunk-conv microbenchmark: C3 net (15x15, 20 blocks x 256 filters) forward at batch B.
-Prints the average trunk-conv launch time (HIP events on the engine stream) and the
-algorithmic TFLOP/s (2*9*C*C*225 FLOP per board per conv).  Used for kernel iteration and
+"""Trunk-conv microbenchmark: C3 net (15x15, 20 blocks x 256 filters) forward at batch B
+(--game go19 / chess: the C4 / C5 nets).  Prints the average trunk-conv launch time (HIP events
+on the engine stream) and the algorithmic TFLOP/s (2*9*C*C*H*W FLOP per board per conv).  Used for kernel iteration and
 for rocprofv3 PMC passes (the conv kernel is the only MFMA kernel of note)."""
 import argparse
 import os
@@ -14,6 +14,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "alphazero-multi-game_amd"))
 import az_amd  # noqa: E402
 
+GAMES = {"gomoku15": (15, 11, 225), "go19": (19, 8, 362), "chess": (8, 111, 4672)}   # board, planes, actions
 PREC = {"f32": az_amd.AZ_PREC_F32, "bf16x3": az_amd.AZ_PREC_BF16X3, "bf16": az_amd.AZ_PREC_BF16,
         "fp16": az_amd.AZ_PREC_FP16}
 
@@ -27,19 +28,20 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--flags", default="", help="comma list of conv variant flag sets to A/B (alternating rounds)")
     ap.add_argument("--rounds", type=int, default=4)
+    ap.add_argument("--game", default="gomoku15", choices=list(GAMES))
     a = ap.parse_args()
+    bs, planes, actions = GAMES[a.game]
     eng = az_amd.Engine(int(os.environ.get("LOCAL_RANK", 0)))
-    desc = az_amd.gomoku_net_desc(board_size=15, channels=a.channels, blocks=a.blocks,
-                                  precision=PREC[a.precision], max_batch=a.batch)
+    desc = az_amd.NetDesc(bs, planes, a.channels, a.blocks, actions, 32, 8, 256, 1, 0, PREC[a.precision], a.batch)
     net = az_amd.HipNeuralNetwork(eng, desc)
     net.init_random(1234)
-    x = (np.random.default_rng(0).random((a.batch, 11, 15, 15)) < 0.2).astype(np.float32)
+    x = (np.random.default_rng(0).random((a.batch, planes, bs, bs)) < (0.05 if planes > 16 else 0.2)).astype(np.float32)
     net.forward(x)
     if a.flags:
         from az_amd import _lib
         sets = [int(f, 0) for f in a.flags.split(",")]
         res = {f: [] for f in sets}
-        flops = a.batch * 2 * 9 * a.channels * a.channels * 225
+        flops = a.batch * 2 * 9 * a.channels * a.channels * bs * bs
         for _ in range(a.rounds):
             for f in sets:
                 _lib.lib().az_diag_set_conv_flags(f)
@@ -61,8 +63,8 @@ def main():
     wall = (time.perf_counter() - t0) / a.iters
     ms, launches, fw = net.profile_read()
     per = ms / launches
-    flops = a.batch * 2 * 9 * a.channels * a.channels * 225
-    print(f"{a.precision} B={a.batch}: trunk {per:.4f} ms/launch, {flops / per / 1e9:.1f} TFLOP/s algorithmic, "
+    flops = a.batch * 2 * 9 * a.channels * a.channels * bs * bs
+    print(f"{a.game} {a.precision} B={a.batch}: trunk {per:.4f} ms/launch, {flops / per / 1e9:.1f} TFLOP/s algorithmic, "
           f"forward wall {wall * 1e3:.2f} ms (incl. H2D/D2H)")
 
 
