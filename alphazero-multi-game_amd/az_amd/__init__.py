@@ -139,19 +139,26 @@ class HipNeuralNetwork:
             self.h = None
 
 
+AZ_GAME_GOMOKU, AZ_GAME_GO, AZ_ACTION_NONE = 0, 1, -2
+
+
 class ParallelMCTS:
     """G independent ParallelMCTS trees (Mode S semantics, setDeterministicMode) on one device."""
 
     def __init__(self, engine, n_games=1, board_size=15, num_simulations=800, c_puct=1.5, fpu_reduction=0.0,
                  virtual_loss=3, evaluator=AZ_EVAL_HASH, net=None, eval_seed=7, zobrist_seed=12345, noise_seed=42,
                  noise_seed_stride=0, use_dirichlet_each_search=False, dirichlet_alpha=0.03, dirichlet_eps=0.25,
-                 tt_log2=20, node_capacity=0, prior_ring=0):
+                 tt_log2=20, node_capacity=0, prior_ring=0, game=0):
+        """game: AZ_GAME_GOMOKU (0) or AZ_GAME_GO (1) -- GoState(bs 9/13/19, komi 7.5, Chinese rules,
+        superko); Go actions are -1 (pass) .. bs*bs-1 and finished games report AZ_ACTION_NONE."""
         self.G = n_games
         self.bs = board_size
-        self.A = board_size * board_size
+        self.game = game
+        self.A = board_size * board_size + (1 if game == AZ_GAME_GO else 0)     # action space
+        self.none = AZ_ACTION_NONE if game == AZ_GAME_GO else -1
         cfg = SearchCfg(n_games, board_size, num_simulations, c_puct, fpu_reduction, virtual_loss, evaluator,
                         eval_seed, zobrist_seed, noise_seed, noise_seed_stride, int(use_dirichlet_each_search),
-                        dirichlet_alpha, dirichlet_eps, tt_log2, node_capacity, prior_ring)
+                        dirichlet_alpha, dirichlet_eps, tt_log2, node_capacity, prior_ring, game)
         self.cfg = cfg
         h = ctypes.c_void_p()
         check(lib().az_search_create(engine.h, net.h if net is not None else None, ctypes.byref(cfg), ctypes.byref(h)))
@@ -233,7 +240,7 @@ class ParallelMCTS:
         A = self.A
         pol = np.zeros((capacity, A), np.float32)
         val = np.zeros(capacity, np.float32)
-        planes = np.zeros((capacity, 11, self.bs, self.bs), np.float32)
+        planes = np.zeros((capacity, 8 if self.game == AZ_GAME_GO else 11, self.bs, self.bs), np.float32)
         n = ctypes.c_int()
         check(lib().az_search_read_eval_log(self.h, _fp(pol), _fp(val), _fp(planes), ctypes.byref(n)))
         k = n.value

@@ -26,7 +26,7 @@ class SearchCfg(ctypes.Structure):
                 ("fpu_reduction", c_float), ("virtual_loss", c_int), ("eval_kind", c_int), ("eval_seed", c_uint32),
                 ("zobrist_seed", c_uint32), ("noise_seed", c_uint32), ("noise_seed_stride", c_int),
                 ("use_dirichlet_each_search", c_int), ("dirichlet_alpha", c_float), ("dirichlet_eps", c_float),
-                ("tt_log2", c_int), ("node_capacity", c_int), ("prior_ring", c_int)]
+                ("tt_log2", c_int), ("node_capacity", c_int), ("prior_ring", c_int), ("game", c_int)]
 
 
 class SelfPlayCfg(ctypes.Structure):

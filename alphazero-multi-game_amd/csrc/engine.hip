@@ -33,6 +33,7 @@ __global__ void k_compact(TreeDev t, Nodes dst, int* src_of);
 __global__ void k_noise(TreeDev t, const float* noise, const uint8_t* mask, float eps);
 __global__ void k_new_games(TreeDev t, const int* games, const int* seed_ids, int n, uint32_t eval_seed);
 __global__ void k_tt_clear(TreeDev t, const int* games, int n);
+__global__ void k_root_nchild(TreeDev t, int* out);
 __global__ void k_root_children(TreeDev t, int g, int* act, int* N, int* VL, float* W, float* P, int* n, int* rootinfo,
                                 float* rootW);
 void az_conv_bf16_launch_v(const ConvBf16Args& a, bool split, hipStream_t st);
@@ -500,17 +501,25 @@ int search_step(az_search* s, int mode) {
 }
 
 int search_noise(az_search* s, float alpha, float eps, const uint8_t* mask) {
-    const int G = s->c.n_games, A = s->t.A;
+    const int G = s->c.n_games, A = s->t.A, NA = s->t.NA;
     if (int r = search_step(s, MODE_ROOT_NOISE)) return r;
+    std::vector<int> nroot;
+    if (s->t.game == GAME_GO) {        // |children| of each root (legal moves incl. pass and superko)
+        nroot.resize(G);
+        s->t.nd = s->arena[s->cur];
+        hipLaunchKernelGGL(k_root_nchild, dim3((G + 255) / 256), dim3(256), 0, s->e->stream, s->t, s->d_nch);
+        HIPCHK(hipMemcpyAsync(nroot.data(), s->d_nch, G * 4, hipMemcpyDeviceToHost, s->e->stream));
+        HIPCHK(hipStreamSynchronize(s->e->stream));
+    }
     // addDirichletNoise draws (parallel_mcts.cpp:1136-1156): libstdc++ gamma on the host,
     // one fresh gamma_distribution per call on the game's mt19937.
     bool any = false;
     for (int g = 0; g < G; ++g) {
         s->h_mask[g] = 0;
         if (!s->active[g] || (mask && !mask[g])) continue;
-        const int nc = s->fresh[g] ? A : A - s->stones[g];
+        const int nc = !nroot.empty() ? nroot[g] : s->fresh[g] ? A : A - s->stones[g];
         if (nc <= 0) continue;
-        float* nz = s->h_noise.data() + (size_t)g * A;
+        float* nz = s->h_noise.data() + (size_t)g * NA;
         std::gamma_distribution<float> gamma(alpha, 1.0f);
         float sum = 0.0f;
         for (int i = 0; i < nc; ++i) { nz[i] = std::max(1e-10f, gamma(s->rng[g])); sum += nz[i]; }
@@ -521,7 +530,7 @@ int search_noise(az_search* s, float alpha, float eps, const uint8_t* mask) {
     }
     if (!any) return 0;
     hipStream_t st = s->e->stream;
-    HIPCHK(hipMemcpyAsync(s->d_noise, s->h_noise.data(), (size_t)G * A * 4, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(s->d_noise, s->h_noise.data(), (size_t)G * NA * 4, hipMemcpyHostToDevice, st));
     HIPCHK(hipMemcpyAsync(s->d_mask, s->h_mask.data(), G, hipMemcpyHostToDevice, st));
     s->t.nd = s->arena[s->cur];
     hipLaunchKernelGGL(k_noise, dim3(G), dim3(64), 0, st, s->t, s->d_noise, s->d_mask, eps);
@@ -567,7 +576,7 @@ int search_new_games(az_search* s, const int* games, int n, const int* seed_ids 
 int search_select(az_search* s, int training, const float* temps_host, float T, int* actions, float* values, float* probs,
                   int* cact, int* nch) {
     hipStream_t st = s->e->stream;
-    const int G = s->c.n_games, A = s->t.A;
+    const int G = s->c.n_games, A = s->t.NA;     // child-order arrays are [G][NA]
     s->t.nd = s->arena[s->cur];
     if (temps_host) HIPCHK(hipMemcpyAsync(s->d_temps, temps_host, G * 4, hipMemcpyHostToDevice, st));
     hipLaunchKernelGGL(k_select_action, dim3(G), dim3(64), 0, st, s->t, training, T, temps_host ? s->d_temps : nullptr,
@@ -599,7 +608,7 @@ int search_apply_dev(az_search* s, int* terminal, int* result) {
     HIPCHK(hipMemcpyAsync(res.data(), s->d_res, G * 4, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
     for (int g = 0; g < G; ++g) {
-        if (s->active[g] && acts[g] >= 0) {
+        if (s->active[g] && acts[g] >= (s->t.game == GAME_GO ? -1 : 0)) {
             s->stones[g] += 1; s->ply[g] += 1; s->fresh[g] = 0;
             if (term[g]) s->active[g] = 0;
         }
@@ -845,12 +854,18 @@ int az_net_predict_batch(az_net* n, const float* planes, int B, float* policy, f
 int az_search_create(az_engine* e, az_net* net, const az_search_cfg* c, az_search** out) {
     if (!e || !c || !out) return fail(AZ_ERR_ARG, "null argument");
     const int bs = c->board_size, A = bs * bs, G = c->n_games;
+    const bool go = c->game == AZ_GAME_GO;
+    const int NA = go ? A + 1 : A;
     if (bs < 3 || A > AZ_MAXA || G < 1 || c->num_simulations < 0 || c->virtual_loss < 0 || c->tt_log2 < 4 ||
-        c->tt_log2 > 24 || c->eval_kind < 0 || c->eval_kind > 3)
+        c->tt_log2 > 24 || c->eval_kind < 0 || c->eval_kind > 3 || (c->game != AZ_GAME_GOMOKU && !go))
         return fail(AZ_ERR_ARG, "unsupported search configuration");
+    if (go && bs != 9 && bs != 13 && bs != 19)
+        return fail(AZ_ERR_ARG, "Go board %d: GoState supports 9, 13 and 19 (go_state.cpp:24-26)", bs);
+    if (go && c->eval_kind == AZ_EVAL_RANDOM)
+        return fail(AZ_ERR_ARG, "AZ_EVAL_RANDOM (RandomPolicyNetwork) is Gomoku-only");
     if (c->eval_kind == AZ_EVAL_NET) {
         if (!net) return fail(AZ_ERR_ARG, "AZ_EVAL_NET needs a network");
-        if (net->d.board_size != bs || net->d.action_size != A || net->d.in_planes != 11)
+        if (net->d.board_size != bs || net->d.action_size != NA || net->d.in_planes != (go ? 8 : 11))
             return fail(AZ_ERR_ARG, "network shape does not match the board");
         if (net->d.max_batch < G) return fail(AZ_ERR_ARG, "network max_batch %d < n_games %d", net->d.max_batch, G);
         if (!net->loaded) return fail(AZ_ERR_STATE, "network weights not loaded");
@@ -859,11 +874,12 @@ int az_search_create(az_engine* e, az_net* net, const az_search_cfg* c, az_searc
     HIPCHK(hipSetDevice(e->device));
     auto* s = new az_search();
     s->e = e; s->net = net; s->c = *c;
-    const int ncap = c->node_capacity > 0 ? c->node_capacity : 3 * std::max(64, c->num_simulations) * A + 8 * A + 64;
-    const int ring = c->prior_ring > 0 ? c->prior_ring : std::max(1 << 16, 12 * std::max(64, c->num_simulations) * A);
+    const int ncap = c->node_capacity > 0 ? c->node_capacity : 3 * std::max(64, c->num_simulations) * NA + 8 * NA + 64;
+    const int ring = c->prior_ring > 0 ? c->prior_ring : std::max(1 << 16, 12 * std::max(64, c->num_simulations) * NA);
     s->c.node_capacity = ncap; s->c.prior_ring = ring;
     TreeDev& t = s->t;
-    t.G = G; t.bs = bs; t.A = A; t.ncap = ncap; t.vl = c->virtual_loss; t.cpuct = c->c_puct; t.fpu = c->fpu_reduction;
+    t.G = G; t.bs = bs; t.A = A; t.ncap = ncap; t.game = go ? GAME_GO : GAME_GOMOKU; t.NA = NA;
+    t.hmax = go ? 2048 : 0; t.vl = c->virtual_loss; t.cpuct = c->c_puct; t.fpu = c->fpu_reduction;
     t.eval_kind = c->eval_kind; t.tt_slots = 1 << c->tt_log2; t.tt_mask = (uint64_t)t.tt_slots - 1; t.ring = ring;
     t.log_game = -1; t.log_cap = 0;
     const size_t NG = (size_t)G * ncap;
@@ -876,6 +892,8 @@ int az_search_create(az_engine* e, az_net* net, const az_search_cfg* c, az_searc
     }
     SA(t.atop, G); SA(t.rboard, (size_t)G * A); SA(t.rhist, G * 6); SA(t.rplayer, G); SA(t.rstones, G); SA(t.rply, G);
     SA(t.rhash, G); SA(t.rfresh, G); SA(t.rnode, G); SA(t.active, G); SA(t.gresult, G);
+    uint64_t* zko = nullptr;
+    if (go) { SA(t.rko, G); SA(t.rpass, G); SA(t.rposh, (size_t)G * t.hmax); SA(t.rnposh, G); SA(zko, A + 1); }
     SA(t.path, (size_t)G * AZ_DMAX); SA(t.plen, G); SA(t.lstatus, G); SA(t.lvalue, G); SA(t.lhash, G); SA(t.ttstore, G);
     SA(t.ttref, G); SA(t.tthslot, G); SA(t.need_eval, G); SA(t.eval_slot, G); SA(t.eval_games, G); SA(t.n_eval, 1);
     SA(t.planes, (size_t)G * A * 16);
@@ -888,12 +906,26 @@ int az_search_create(az_engine* e, az_net* net, const az_search_cfg* c, az_searc
     if (c->eval_kind == AZ_EVAL_RANDOM) SA(t.mt, (size_t)G * 625);
     SA(t.err, 1);
     SA(s->d_src_of, NG);
-    if (c->eval_kind == AZ_EVAL_NET) { SA(s->d_batch, (size_t)G * A * 16); SA(s->d_logits, (size_t)G * A); SA(s->d_value, G); }
-    SA(s->d_noise, (size_t)G * A); SA(s->d_mask, G); SA(s->d_actions, G); SA(s->d_values, G); SA(s->d_probs, (size_t)G * A);
-    SA(s->d_cact, (size_t)G * A); SA(s->d_nch, G); SA(s->d_term, G); SA(s->d_res, G); SA(s->d_games, G); SA(s->d_seed_ids, G); SA(s->d_temps, G);
+    if (c->eval_kind == AZ_EVAL_NET) { SA(s->d_batch, (size_t)G * A * 16); SA(s->d_logits, (size_t)G * NA); SA(s->d_value, G); }
+    SA(s->d_noise, (size_t)G * NA); SA(s->d_mask, G); SA(s->d_actions, G); SA(s->d_values, G); SA(s->d_probs, (size_t)G * NA);
+    SA(s->d_cact, (size_t)G * NA); SA(s->d_nch, G); SA(s->d_term, G); SA(s->d_res, G); SA(s->d_games, G); SA(s->d_seed_ids, G); SA(s->d_temps, G);
 #undef SA
     if (r) { az_search_destroy(s); return r; }
-    t.zpiece = zp; t.zplayer = zpl; t.fresh_order = fo;
+    t.zpiece = zp; t.zplayer = zpl; t.fresh_order = fo; t.zko = zko;
+    if (go) {
+        // GoState Zobrist features (go_state.cpp:48-51; ZobristHash::addFeature, zobrist_hash.cpp:58-70):
+        // mt19937_64 seeded with std::hash<std::string> of the feature name
+        std::mt19937_64 rk(std::hash<std::string>{}("ko_point"));
+        std::vector<uint64_t> ko(A + 1);
+        for (auto& k : ko) k = rk();
+        HIPCHK(hipMemcpy(zko, ko.data(), (A + 1) * 8, hipMemcpyHostToDevice));
+        std::mt19937_64 rr(std::hash<std::string>{}("rules"));
+        uint64_t rules[2] = {rr(), rr()};
+        std::mt19937_64 rm(std::hash<std::string>{}("komi"));
+        uint64_t komi[16];
+        for (auto& k : komi) k = rm();
+        t.zconst = rules[1] ^ komi[((int)(7.5f * 2)) & 0xF];   // Chinese rules, komi 7.5
+    }
     t.net_logits = s->d_logits; t.net_value = s->d_value;
     // Zobrist keys: ZobristHash(bs, 2, 2, seed) (src/core/zobrist_hash.cpp:9-36)
     {
@@ -914,7 +946,7 @@ int az_search_create(az_engine* e, az_net* net, const az_search_cfg* c, az_searc
     HIPCHK(hipMemset(t.active, 0, G * 4));
     s->stones.assign(G, 0); s->active.assign(G, 0); s->fresh.assign(G, 1); s->ply.assign(G, 0); s->expanded.assign(G, 0);
     s->rng.resize(G);
-    s->h_noise.assign((size_t)G * A, 0.0f);
+    s->h_noise.assign((size_t)G * NA, 0.0f);
     s->h_mask.assign(G, 0);
     *out = s;
     return 0;
@@ -936,6 +968,8 @@ void az_search_destroy(az_search* s) {
                           (const void*)t.tt_hash, (const void*)t.tt_visits, (const void*)t.tt_value, (const void*)t.tt_ref,
                           (const void*)t.ring_buf, (const void*)t.ring_cur, (const void*)t.cnt, (const void*)t.zpiece,
                           (const void*)t.zplayer, (const void*)t.fresh_order, (const void*)t.mt, (const void*)t.err,
+                          (const void*)t.rko, (const void*)t.rpass, (const void*)t.rposh, (const void*)t.rnposh,
+                          (const void*)t.zko,
                           (const void*)t.log_pol, (const void*)t.log_val, (const void*)t.log_planes, (const void*)t.log_n,
                           (const void*)s->d_src_of, (const void*)s->d_batch, (const void*)s->d_logits,
                           (const void*)s->d_value, (const void*)s->d_noise, (const void*)s->d_mask, (const void*)s->d_actions,
@@ -987,7 +1021,8 @@ int az_search_apply(az_search* s, const int* actions, int* terminal, int* result
     HIPCHK(hipSetDevice(s->e->device));
     const int G = s->c.n_games, A = s->t.A;
     for (int g = 0; g < G; ++g)
-        if (actions[g] >= A) return fail(AZ_ERR_ARG, "action %d out of range for game %d", actions[g], g);
+        if (actions[g] >= A || (s->t.game == GAME_GO && actions[g] < AZ_ACTION_NONE))
+            return fail(AZ_ERR_ARG, "action %d out of range for game %d", actions[g], g);
     HIPCHK(hipMemcpyAsync(s->d_actions, actions, G * 4, hipMemcpyHostToDevice, s->e->stream));
     return search_apply_dev(s, terminal, result);
 }
@@ -997,7 +1032,7 @@ int az_search_root_children(az_search* s, int game, int* actions, int* N, int* V
     std::lock_guard<std::mutex> lk(s->mu);
     HIPCHK(hipSetDevice(s->e->device));
     hipStream_t st = s->e->stream;
-    const int A = s->t.A;
+    const int A = s->t.NA;
     int *da, *dN, *dVL, *dn, *dri; float *dW, *dP, *drw;
     DALLOC(da, A); DALLOC(dN, A); DALLOC(dVL, A); DALLOC(dn, 1); DALLOC(dri, 2); DALLOC(dW, A); DALLOC(dP, A); DALLOC(drw, 1);
     s->t.nd = s->arena[s->cur];
@@ -1046,7 +1081,8 @@ int az_search_enable_eval_log(az_search* s, int game, int capacity) {
     TreeDev& t = s->t;
     if (t.log_pol) { hipFree(t.log_pol); hipFree(t.log_val); hipFree(t.log_planes); hipFree(t.log_n); }
     t.log_pol = nullptr; t.log_val = nullptr; t.log_planes = nullptr; t.log_n = nullptr;
-    DALLOC(t.log_pol, (size_t)capacity * t.A); DALLOC(t.log_val, capacity); DALLOC(t.log_planes, (size_t)capacity * 11 * t.A);
+    const int npl = t.game == GAME_GO ? 8 : 11;
+    DALLOC(t.log_pol, (size_t)capacity * t.NA); DALLOC(t.log_val, capacity); DALLOC(t.log_planes, (size_t)capacity * npl * t.A);
     DALLOC(t.log_n, 1);
     HIPCHK(hipMemset(t.log_n, 0, 4));
     t.log_game = game; t.log_cap = capacity;
@@ -1061,9 +1097,10 @@ int az_search_read_eval_log(az_search* s, float* policy, float* value, float* pl
     if (!t.log_pol) { *count = 0; return 0; }
     int n = 0;
     HIPCHK(hipMemcpy(&n, t.log_n, 4, hipMemcpyDeviceToHost));
-    if (policy) HIPCHK(hipMemcpy(policy, t.log_pol, (size_t)n * t.A * 4, hipMemcpyDeviceToHost));
+    if (policy) HIPCHK(hipMemcpy(policy, t.log_pol, (size_t)n * t.NA * 4, hipMemcpyDeviceToHost));
     if (value) HIPCHK(hipMemcpy(value, t.log_val, (size_t)n * 4, hipMemcpyDeviceToHost));
-    if (planes) HIPCHK(hipMemcpy(planes, t.log_planes, (size_t)n * 11 * t.A * 4, hipMemcpyDeviceToHost));
+    if (planes) HIPCHK(hipMemcpy(planes, t.log_planes, (size_t)n * (t.game == GAME_GO ? 8 : 11) * t.A * 4,
+                                 hipMemcpyDeviceToHost));
     *count = n;
     return 0;
 }
@@ -1087,8 +1124,9 @@ int az_selfplay_step(az_search* s, const az_selfplay_cfg* cfg, int64_t* moves_do
     if (int r = search_apply_dev(s, term.data(), res.data())) return r;
     int64_t moves = 0;
     std::vector<uint8_t> noise_mask(G, 0);
+    const int none = s->t.game == GAME_GO ? AZ_ACTION_NONE : -1;
     for (int g = 0; g < G; ++g) {
-        if (!was_active[g] || actions[g] < 0) continue;
+        if (!was_active[g] || actions[g] == none) continue;
         ++moves;
         if (ply0[g] % 2 == 0) noise_mask[g] = 1;
     }
@@ -1119,7 +1157,8 @@ int az_selfplay_run(az_search* s, const az_selfplay_cfg* cfg, int total_games, i
     std::lock_guard<std::mutex> lk(s->mu);
     HIPCHK(hipSetDevice(s->e->device));
     hipStream_t st = s->e->stream;
-    const int G = s->c.n_games, A = s->t.A;
+    const int G = s->c.n_games, A = s->t.NA;     // child-order records: up to NA children
+    const int none = s->t.game == GAME_GO ? AZ_ACTION_NONE : -1;
     struct Rec {
         std::vector<az_move_rec> moves;
         std::vector<std::vector<float>> pol;
@@ -1163,7 +1202,7 @@ int az_selfplay_run(az_search* s, const az_selfplay_cfg* cfg, int total_games, i
         const int64_t ms = std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::steady_clock::now() - t0).count();
         std::vector<int> was_active = s->active, ply0 = s->ply;
         for (int g = 0; g < G; ++g) {
-            if (!was_active[g] || actions[g] < 0) continue;
+            if (!was_active[g] || actions[g] == none) continue;
             Rec& R = rec[g];
             R.pol.emplace_back(probs.begin() + (size_t)g * A, probs.begin() + (size_t)g * A + nch[g]);
             R.cact.emplace_back(cact.begin() + (size_t)g * A, cact.begin() + (size_t)g * A + nch[g]);

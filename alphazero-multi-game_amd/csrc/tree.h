@@ -7,7 +7,8 @@
 #pragma once
 #include <stdint.h>
 
-#define AZ_MAXA 361          // largest action space handled on device (19x19)
+#define AZ_MAXA 361          // largest board handled on device (19x19)
+#define AZ_MAXNA 362         // largest action space (Go 19x19: 361 points + pass)
 #define AZ_DMAX 96           // longest selection path (root + 95 plies); overflow => AZ_ERR_CAPACITY
 #define AZ_NCNT 8            // per-game counters
 
@@ -16,7 +17,8 @@ enum { MODE_SIM = 0, MODE_ROOT_NOISE = 1, MODE_ROOT_SEARCH = 2 };
 enum { FL_EXPANDED = 1, FL_TERMINAL = 2 };   // result (GameResult) in bits 2..3
 enum { CNT_EVALS = 0, CNT_LOOKUPS = 1, CNT_HITS = 2, CNT_SIMS = 3, CNT_NODES = 4, CNT_EVALS_TOTAL = 5,
        CNT_BYTES_SEL = 6, CNT_BYTES_EXP = 7 };   // [5..7] survive new games; 6/7: algorithmic HBM bytes of K1 / K3
-enum { ERR_NODES = 1, ERR_PATH = 2, ERR_RING = 4, ERR_BATCH = 8 };
+enum { ERR_NODES = 1, ERR_PATH = 2, ERR_RING = 4, ERR_BATCH = 8, ERR_HIST = 16 };
+enum { GAME_GOMOKU = 0, GAME_GO = 1 };
 
 struct Nodes {          // one arena: [G][ncap]
     int* N; float* W; int* VL; float* P; int* first; int16_t* act; int16_t* cnt; uint8_t* flag;
@@ -24,6 +26,8 @@ struct Nodes {          // one arena: [G][ncap]
 
 struct TreeDev {
     int G, bs, A, ncap;
+    int game;                    // GAME_GOMOKU / GAME_GO
+    int NA;                      // action space = policy length = max children (A, Go: A + 1 with pass = -1)
     int vl; float cpuct, fpu;
     int eval_kind;
     uint64_t tt_mask; int tt_slots;
@@ -34,6 +38,11 @@ struct TreeDev {
     int* rhist;                  // [G][6]   last moves, [0] most recent, -1 none
     int* rplayer; int* rstones; int* rply; uint64_t* rhash; int* rfresh; int* rnode;
     int* active;                 // [G] game searching (not finished)
+    // Go root state (GoState): ko point, consecutive passes, position_history_ (hashes of the
+    // positions after every stone move, go_state.cpp:250-252); rhash holds the stones-only hash
+    int* rko; int* rpass; uint64_t* rposh; int* rnposh; int hmax;
+    const uint64_t* zko;         // [A + 1] "ko_point" feature keys
+    uint64_t zconst;             // "rules"[1] ^ "komi"[int(7.5*2) & 15] (Chinese rules, komi 7.5)
     int* gresult;                // [G] GameResult of the root state
     int* path; int* plen;        // [G][AZ_DMAX], [G]
     int* lstatus; float* lvalue; uint64_t* lhash; int* ttstore; uint64_t* ttref; int* tthslot;

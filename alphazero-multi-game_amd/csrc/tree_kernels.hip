@@ -216,6 +216,260 @@ __device__ void write_planes(const TreeDev& t, int g, int lane, const uint8_t* b
     }
 }
 
+// ---------------------------------------------------------------------------
+// Go (GoState as GoState(bs, 7.5, true, true): go_state.cpp / go_rules.cpp).  Rules code runs
+// on lane 0 over the game's LDS board (a few hundred LDS operations per move; the network
+// forward of the same step is four orders of magnitude longer); per-point work is lane-parallel.
+struct GoLds {
+    int16_t list[AZ_MAXA];       // BFS list / stack
+    int16_t mark[AZ_MAXA];       // visit stamps
+    int16_t gid[AZ_MAXA];        // group id of every stone (-1 empty)
+    int16_t glib[AZ_MAXA];       // distinct liberties of group id
+    uint64_t gxor[AZ_MAXA];      // XOR of the group's piece keys
+    uint64_t phist[AZ_DMAX];     // position hashes pushed along the selection path
+    int nph, stamp;
+};
+
+__device__ __forceinline__ int go_adj(int pos, int bs, int A, int* nb) {   // getAdjacentPositions (:800-816)
+    const int x = pos % bs;
+    int n = 0;
+    if (pos >= bs) nb[n++] = pos - bs;
+    if (x + 1 < bs) nb[n++] = pos + 1;
+    if (pos + bs < A) nb[n++] = pos + bs;
+    if (x > 0) nb[n++] = pos - 1;
+    return n;
+}
+
+__device__ void go_clear_marks(GoLds& L, int A, int lane) {
+    for (int a = lane; a < A; a += 64) L.mark[a] = -1;
+    if (lane == 0) L.stamp = 0;
+    __syncthreads();
+}
+
+// makeMove (go_state.cpp:192-257) on lane 0: place, remove libertyless opponent groups (only
+// groups adjacent to the new stone can have none), ko point, stones hash.  Returns 1 when the
+// move pushes a position (stone moves), 0 for a pass.
+__device__ int go_play_seq(const TreeDev& t, uint8_t* b, GoLds& L, int a, int p, int& ko, int& passes, uint64_t& bh) {
+    const int bs = t.bs, A = t.A;
+    if (a < 0) { ++passes; ko = -1; return 0; }
+    passes = 0;
+    b[a] = (uint8_t)p;
+    bh ^= t.zpiece[(size_t)(p - 1) * A + a];
+    const int opp = 3 - p;
+    int ngroups = 0, nstones = 0, last = -1;
+    int nb[4];
+    const int k = go_adj(a, bs, A, nb);
+    const int base = L.stamp;          // stamps of this call are > base
+    for (int j = 0; j < k; ++j) {
+        const int s0 = nb[j];
+        if (b[s0] != opp || L.mark[s0] > base) continue;   // empty / own / group already examined
+        const int st = ++L.stamp;
+        int n = 0;
+        L.list[n++] = (int16_t)s0;
+        L.mark[s0] = (int16_t)st;
+        bool lib = false;
+        for (int i = 0; i < n; ++i) {
+            int nb2[4];
+            const int k2 = go_adj(L.list[i], bs, A, nb2);
+            for (int q = 0; q < k2; ++q) {
+                const int c = nb2[q];
+                if (b[c] == 0) lib = true;
+                else if (b[c] == opp && L.mark[c] != st) { L.mark[c] = (int16_t)st; L.list[n++] = (int16_t)c; }
+            }
+        }
+        if (!lib) {
+            for (int i = 0; i < n; ++i) {
+                const int c = L.list[i];
+                b[c] = 0;
+                bh ^= t.zpiece[(size_t)(opp - 1) * A + c];
+            }
+            ++ngroups;
+            nstones += n;
+            last = L.list[0];
+        }
+    }
+    ko = (ngroups == 1 && nstones == 1) ? last : -1;
+    return 1;
+}
+
+// updateHash (go_state.cpp:846-877)
+__device__ __forceinline__ uint64_t go_hash(const TreeDev& t, uint64_t bh, int player, int ko) {
+    uint64_t h = bh ^ t.zplayer[player - 1];
+    if (ko >= 0) h ^= t.zko[ko];
+    return h ^ t.zconst;
+}
+
+// Every group of the board: id, distinct liberties, piece-key XOR (lane 0, then visible to all).
+__device__ void go_groups(const TreeDev& t, const uint8_t* b, GoLds& L, int lane) {
+    const int bs = t.bs, A = t.A;
+    for (int a = lane; a < A; a += 64) L.gid[a] = -1;
+    __syncthreads();
+    if (lane == 0) {
+        int ng = 0;
+        for (int p0 = 0; p0 < A; ++p0) {
+            const int c = b[p0];
+            if (c == 0 || L.gid[p0] >= 0) continue;
+            const int st = ++L.stamp;
+            int n = 0, libs = 0;
+            uint64_t x = 0;
+            L.list[n++] = (int16_t)p0;
+            L.gid[p0] = (int16_t)ng;
+            for (int i = 0; i < n; ++i) {
+                const int s0 = L.list[i];
+                x ^= t.zpiece[(size_t)(c - 1) * A + s0];
+                int nb[4];
+                const int k = go_adj(s0, bs, A, nb);
+                for (int q = 0; q < k; ++q) {
+                    const int e = nb[q];
+                    if (b[e] == 0) { if (L.mark[e] != st) { L.mark[e] = (int16_t)st; ++libs; } }
+                    else if (b[e] == c && L.gid[e] < 0) { L.gid[e] = (int16_t)ng; L.list[n++] = (int16_t)e; }
+                }
+            }
+            L.glib[ng] = (int16_t)libs;
+            L.gxor[ng] = x;
+            ++ng;
+        }
+    }
+    __syncthreads();
+}
+
+// GoRules::getTerritoryOwnership + calculateScores, Chinese rules (go_rules.cpp:211-361) ->
+// GameResult of a finished game (go_state.cpp:295-312).  Lane 0.
+__device__ int go_result_seq(const TreeDev& t, const uint8_t* b, GoLds& L) {
+    const int bs = t.bs, A = t.A;
+    float bsc = 0.0f, wsc = 0.0f;
+    const int st = ++L.stamp;
+    for (int p0 = 0; p0 < A; ++p0) {
+        if (b[p0] == 1) { bsc += 1.0f; continue; }
+        if (b[p0] == 2) { wsc += 1.0f; continue; }
+    }
+    for (int p0 = 0; p0 < A; ++p0) {
+        if (b[p0] != 0 || L.mark[p0] == st) continue;
+        int n = 0;
+        bool tb = false, tw = false;
+        L.list[n++] = (int16_t)p0;
+        L.mark[p0] = (int16_t)st;
+        for (int i = 0; i < n; ++i) {
+            int nb[4];
+            const int k = go_adj(L.list[i], bs, A, nb);
+            for (int q = 0; q < k; ++q) {
+                const int e = nb[q];
+                if (b[e] == 0) { if (L.mark[e] != st) { L.mark[e] = (int16_t)st; L.list[n++] = (int16_t)e; } }
+                else if (b[e] == 1) tb = true;
+                else tw = true;
+            }
+        }
+        if (tb && !tw) bsc += (float)n;
+        else if (tw && !tb) wsc += (float)n;
+    }
+    wsc += 7.5f;
+    if (bsc > wsc) return R_WIN1;
+    if (wsc > bsc) return R_WIN2;
+    return R_DRAW;
+}
+
+// Leaf state of a Go game = root state + path moves (lane 0), with the position hashes the path
+// pushes (for positional superko at expansion).
+__device__ void go_build_leaf(const TreeDev& t, int g, int lane, const GamePtrs& nd, const int* spath, int depth,
+                              uint8_t* board, GoLds& L, int* hist6, int& player, int& ko, int& passes, uint64_t& bh,
+                              uint64_t& hash) {
+    const int A = t.A;
+    const uint8_t* rb = t.rboard + (size_t)g * A;
+    for (int a = lane; a < A; a += 64) board[a] = rb[a];
+    go_clear_marks(L, A, lane);
+    if (lane == 0) {
+        int p = t.rplayer[g], k = t.rko[g], ps = t.rpass[g];
+        uint64_t h = t.rhash[g];
+        int nph = 0;
+        for (int i = 1; i <= depth; ++i) {
+            const int a = nd.act[spath[i]];
+            if (go_play_seq(t, board, L, a, p, k, ps, h)) L.phist[nph++] = go_hash(t, h, p, k);
+            p = 3 - p;
+        }
+        L.nph = nph;
+        L.list[0] = (int16_t)p; L.list[1] = (int16_t)k; L.list[2] = (int16_t)ps;
+        L.gxor[0] = h;
+    }
+    __syncthreads();
+    player = L.list[0]; ko = L.list[1]; passes = L.list[2]; bh = L.gxor[0];
+    __syncthreads();
+    hash = go_hash(t, bh, player, ko);
+    for (int i = 0; i < 6; ++i) {
+        if (i < depth) hist6[i] = nd.act[spath[depth - i]];
+        else hist6[i] = t.rhist[g * 6 + (i - depth)];
+    }
+}
+
+// getEnhancedTensorRepresentation (go_state.cpp:338-420) in NHWC16: black, white, black to move,
+// black / white group liberties min(1, libs / 10), ko point, border distances x / y.
+__device__ void go_write_planes(const TreeDev& t, int g, int lane, const uint8_t* b, const GoLds& L, int player, int ko) {
+    const int A = t.A, bs = t.bs;
+    float4* out = reinterpret_cast<float4*>(t.planes + (size_t)g * A * 16);
+    const float half = (float)(bs / 2);
+    for (int a = lane; a < A; a += 64) {
+        float c[16];
+        for (int k = 0; k < 16; ++k) c[k] = 0.0f;
+        const int v = b[a];
+        if (v == 1) c[0] = 1.0f;
+        else if (v == 2) c[1] = 1.0f;
+        c[2] = player == 1 ? 1.0f : 0.0f;
+        if (v) c[v == 1 ? 3 : 4] = fminf(1.0f, (float)L.glib[L.gid[a]] / 10.0f);
+        if (a == ko) c[5] = 1.0f;
+        const int x = a % bs, y = a / bs;
+        c[6] = (float)min(x, bs - 1 - x) / half;
+        c[7] = (float)min(y, bs - 1 - y) / half;
+        for (int k = 0; k < 4; ++k) out[(size_t)a * 4 + k] = make_float4(c[4 * k], c[4 * k + 1], c[4 * k + 2], c[4 * k + 3]);
+    }
+}
+
+// getLegalMoves (go_state.cpp:116-160): pass, then every empty non-ko point that is not suicide
+// (GoRules::isSuicidalMove) and whose resulting position -- same side to move, the old ko point --
+// is not in position_history_ (root history + the path's pushes).  Needs go_groups().
+__device__ int go_legal(const TreeDev& t, int g, int lane, const uint8_t* b, const GoLds& L, int player, int ko,
+                        uint64_t bh, int* legal) {
+    const int A = t.A, bs = t.bs;
+    const int opp = 3 - player;
+    const uint64_t* rh = t.rposh + (size_t)g * t.hmax;
+    const int nr = t.rnposh[g];
+    const uint64_t tail = t.zplayer[player - 1] ^ (ko >= 0 ? t.zko[ko] : 0ULL) ^ t.zconst;
+    if (lane == 0) legal[0] = -1;
+    int n = 1;
+    for (int c0 = 0; c0 < A; c0 += 64) {
+        const int a = c0 + lane;
+        bool ok = a < A && b[a] == 0 && a != ko;
+        if (ok) {
+            int nb[4];
+            const int k = go_adj(a, bs, A, nb);
+            bool alive = false;
+            int capg[4], nc = 0;
+            uint64_t h = bh ^ t.zpiece[(size_t)(player - 1) * A + a];
+            for (int q = 0; q < k; ++q) {
+                const int e = nb[q];
+                const int v = b[e];
+                if (v == 0) { alive = true; continue; }
+                const int gi = L.gid[e];
+                if (v == player) { if (L.glib[gi] >= 2) alive = true; continue; }
+                if (L.glib[gi] == 1) {                // its only liberty is a: captured
+                    bool dup = false;
+                    for (int r = 0; r < nc; ++r) dup |= capg[r] == gi;
+                    if (!dup) { capg[nc++] = gi; h ^= L.gxor[gi]; }
+                }
+            }
+            ok = alive || nc > 0;
+            if (ok) {
+                h ^= tail;
+                for (int r = 0; r < nr && ok; ++r) ok = rh[r] != h;
+                for (int r = 0; r < L.nph && ok; ++r) ok = L.phist[r] != h;
+            }
+        }
+        const unsigned long long m = __ballot(ok);
+        if (ok) legal[n + __popcll(m & ((1ULL << lane) - 1ULL))] = a;
+        n += __popcll(m);
+    }
+    __syncthreads();
+    return n;
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------
@@ -225,6 +479,8 @@ __global__ __launch_bounds__(64) void k_select(TreeDev t, int mode) {
     const int lane = threadIdx.x;
     __shared__ uint8_t board[AZ_MAXA];
     __shared__ int spath[AZ_DMAX];
+    __shared__ GoLds gl;
+    const bool go = t.game == GAME_GO;
     if (g >= t.G) return;
     if (!t.active[g]) {
         if (lane == 0) { t.lstatus[g] = ST_NONE; t.need_eval[g] = 0; }
@@ -295,9 +551,12 @@ __global__ __launch_bounds__(64) void k_select(TreeDev t, int mode) {
     __syncthreads();
 
     int hist6[6];
-    int player, stones;
+    int player, stones = 0;
     uint64_t hash;
-    build_leaf(t, g, lane, nd, spath, depth, board, hist6, player, stones, hash);
+    int gko = -1, gpass = 0;
+    uint64_t gbh = 0;
+    if (go) go_build_leaf(t, g, lane, nd, spath, depth, board, gl, hist6, player, gko, gpass, gbh, hash);
+    else build_leaf(t, g, lane, nd, spath, depth, board, hist6, player, stones, hash);
     const int leaf = node;
     int store = 0;
     uint64_t ref = 0;
@@ -310,12 +569,19 @@ __global__ __launch_bounds__(64) void k_select(TreeDev t, int mode) {
             status = ST_TERMINAL;
             value = convert_value((f >> 2) & 3, player);
         } else {
-            if (depth > 0) {
+            if (depth == 0) {
+                result = t.gresult[g];
+            } else if (go) {
+                // GoState::isTerminal: two consecutive passes; area score (go_state.cpp:291-312)
+                if (gpass >= 2) {
+                    int r = 0;
+                    if (lane == 0) r = go_result_seq(t, board, gl);
+                    result = __shfl(r, 0);
+                }
+            } else {
                 const int a = nd.act[leaf];
                 if (five_at(board, t.bs, a, 3 - player)) result = (3 - player) == 1 ? R_WIN1 : R_WIN2;
                 else if (stones >= t.A) result = R_DRAW;
-            } else {
-                result = t.gresult[g];
             }
             if (result != R_ONGOING) {
                 status = ST_TERMINAL;
@@ -325,8 +591,9 @@ __global__ __launch_bounds__(64) void k_select(TreeDev t, int mode) {
                 status = ST_EXPANDED;   // depth cap only (reference: node->getValue())
             }
         }
-    } else if (stones >= t.A) {
-        // expandNode: no legal moves -> terminal (parallel_mcts.cpp:646-654)
+    } else if (!go && stones >= t.A) {
+        // expandNode: no legal moves -> terminal (parallel_mcts.cpp:646-654); a Go state always
+        // has the pass
         if (lane == 0) {
             nd.flag[leaf] = (uint8_t)(nd.flag[leaf] | FL_TERMINAL | FL_EXPANDED | (R_DRAW << 2));
             t.lstatus[g] = ST_NONE; t.need_eval[g] = 0;
@@ -353,7 +620,12 @@ __global__ __launch_bounds__(64) void k_select(TreeDev t, int mode) {
             status = ST_EVAL;
             store = (vis == 0 || vis < 5) ? 1 : 0;     // empty slot, or shouldReplace (visits < 5)
             if (lane == 0) cnt[CNT_LOOKUPS] += (mode == MODE_ROOT_SEARCH ? 1 : 2);
-            write_planes(t, g, lane, board, hist6, player);
+            if (go) {
+                go_groups(t, board, gl, lane);
+                go_write_planes(t, g, lane, board, gl, player, gko);
+            } else {
+                write_planes(t, g, lane, board, hist6, player);
+            }
         }
     }
     if (lane == 0) {
@@ -411,10 +683,12 @@ __global__ __launch_bounds__(64) void k_expand_backup(TreeDev t, int mode) {
     const int lane = threadIdx.x;
     __shared__ uint8_t board[AZ_MAXA];
     __shared__ int spath[AZ_DMAX];
-    __shared__ float pol[AZ_MAXA];
-    __shared__ int legal[AZ_MAXA];
-    __shared__ float lp[AZ_MAXA];
+    __shared__ float pol[AZ_MAXNA];
+    __shared__ int legal[AZ_MAXNA];
+    __shared__ float lp[AZ_MAXNA];
     __shared__ float s_scalar[2];
+    __shared__ GoLds gl;
+    const bool go = t.game == GAME_GO;
     if (g >= t.G) return;
     const int status = t.lstatus[g];
     if (status == ST_NONE) return;
@@ -427,8 +701,12 @@ __global__ __launch_bounds__(64) void k_expand_backup(TreeDev t, int mode) {
     for (int i = lane; i < plen; i += 64) spath[i] = t.path[(size_t)g * AZ_DMAX + i];
     __syncthreads();
     const int leaf = spath[depth];
-    int hist6[6]; int player, stones; uint64_t hash;
-    build_leaf(t, g, lane, nd, spath, depth, board, hist6, player, stones, hash);
+    const int NA = t.NA;
+    int hist6[6]; int player, stones = 0; uint64_t hash;
+    int gko = -1, gpass = 0;
+    uint64_t gbh = 0;
+    if (go) go_build_leaf(t, g, lane, nd, spath, depth, board, gl, hist6, player, gko, gpass, gbh, hash);
+    else build_leaf(t, g, lane, nd, spath, depth, board, hist6, player, stones, hash);
     float value = t.lvalue[g];
     // algorithmic bytes: path (4 + 2 B per level), root board, then below: policy / TT / ring,
     // new child records (25 B), VL-removal + backup read-modify-write (24 B per path node)
@@ -437,8 +715,11 @@ __global__ __launch_bounds__(64) void k_expand_backup(TreeDev t, int mode) {
     if (status == ST_EVAL || status == ST_TTHIT) {
         // legal moves in child order (gomoku_state.cpp:531-578)
         int n = 0;
-        const bool fresh = (depth == 0) && t.rfresh[g];
-        if (fresh) {
+        const bool fresh = !go && (depth == 0) && t.rfresh[g];
+        if (go) {
+            go_groups(t, board, gl, lane);
+            n = go_legal(t, g, lane, board, gl, player, gko, gbh, legal);
+        } else if (fresh) {
             for (int i = lane; i < A; i += 64) legal[i] = t.fresh_order[i];
             n = A - t.rstones[g];   // fresh root is the empty board
         } else {
@@ -452,36 +733,46 @@ __global__ __launch_bounds__(64) void k_expand_backup(TreeDev t, int mode) {
             }
         }
         __syncthreads();
-        if (status == ST_EVAL) {
+        if (status == ST_EVAL || go) {
+          if (status == ST_TTHIT) {
+            // Go transposition hit: a position's legal set also depends on its history (superko),
+            // so the ring keeps the cached policy itself (NA floats) and expandNodeWithPolicy's
+            // gather is redone over the current legal set, as the reference does with entry.policy
+            const uint64_t cur = t.ring_cur[g];
+            if (cur - t.ttref[g] > (uint64_t)t.ring) { if (lane == 0) atomicOr(t.err, ERR_RING); return; }
+            const float* rb = t.ring_buf + (size_t)g * t.ring;
+            for (int a = lane; a < NA; a += 64) pol[a] = rb[(t.ttref[g] + a) % (uint64_t)t.ring];
+            __syncthreads();
+          } else {
             if (lane == 0) { cnt[CNT_EVALS] += 1; cnt[CNT_EVALS_TOTAL] += 1; }
             if (t.eval_kind == 0) {
                 const int slot = t.eval_slot[g];
-                const float* lg = t.net_logits + (size_t)slot * A;
+                const float* lg = t.net_logits + (size_t)slot * NA;
                 float mx = -FLT_MAX;
-                for (int a = lane; a < A; a += 64) { float v = lg[a]; pol[a] = v; mx = fmaxf(mx, v); }
+                for (int a = lane; a < NA; a += 64) { float v = lg[a]; pol[a] = v; mx = fmaxf(mx, v); }
                 mx = wave_max(mx);
                 __syncthreads();
-                for (int a = lane; a < A; a += 64) pol[a] = expf(pol[a] - mx);
+                for (int a = lane; a < NA; a += 64) pol[a] = expf(pol[a] - mx);
                 __syncthreads();
                 if (lane == 0) {
                     float sum = 0.0f;
-                    for (int a = 0; a < A; ++a) sum += pol[a];
+                    for (int a = 0; a < NA; ++a) sum += pol[a];
                     s_scalar[0] = sum;
                 }
                 __syncthreads();
                 const float sum = s_scalar[0];
-                if (sum > 0.0f) for (int a = lane; a < A; a += 64) pol[a] = pol[a] / sum;
+                if (sum > 0.0f) for (int a = lane; a < NA; a += 64) pol[a] = pol[a] / sum;
                 value = t.net_value[slot];
             } else if (t.eval_kind == 3) {
                 // no network: 1/|legal| on the legal actions, value 0 (parallel_mcts.cpp:903-916)
                 const float u = n > 0 ? 1.0f / (float)n : 0.0f;
-                for (int a = lane; a < A; a += 64) pol[a] = 0.0f;
+                for (int a = lane; a < NA; a += 64) pol[a] = 0.0f;
                 __syncthreads();
-                for (int i = lane; i < n; i += 64) pol[legal[i]] = u;
+                for (int i = lane; i < n; i += 64) if (legal[i] >= 0) pol[legal[i]] = u;
                 value = 0.0f;
             } else if (t.eval_kind == 1) {
                 const uint64_t key = hash_eval_key(hash, hist6);
-                for (int a = lane; a < A; a += 64) pol[a] = hash_eval_p(key, a);
+                for (int a = lane; a < NA; a += 64) pol[a] = hash_eval_p(key, a);
                 value = hash_eval_v(key);
             } else {
                 uint32_t* st = t.mt + (size_t)g * 625;
@@ -502,17 +793,19 @@ __global__ __launch_bounds__(64) void k_expand_backup(TreeDev t, int mode) {
             if (g == t.log_game && t.log_pol) {
                 const int k = *t.log_n;
                 if (k < t.log_cap) {
-                    for (int a = lane; a < A; a += 64) t.log_pol[(size_t)k * A + a] = pol[a];
+                    for (int a = lane; a < NA; a += 64) t.log_pol[(size_t)k * NA + a] = pol[a];
                     if (t.log_planes) {
+                        const int npl = go ? 8 : 11;
                         const float* src = t.planes + (size_t)g * A * 16;
                         for (int a = lane; a < A; a += 64)
-                            for (int c = 0; c < 11; ++c) t.log_planes[((size_t)k * 11 + c) * A + a] = src[(size_t)a * 16 + c];
+                            for (int c = 0; c < npl; ++c) t.log_planes[((size_t)k * npl + c) * A + a] = src[(size_t)a * 16 + c];
                     }
                     if (lane == 0) { t.log_val[k] = value; *t.log_n = k + 1; }
                 }
             }
+          }
             // expandNodeWithPolicy: gather, sequential sum, renormalise (parallel_mcts.cpp:702-724)
-            for (int i = lane; i < n; i += 64) lp[i] = pol[legal[i]];
+            for (int i = lane; i < n; i += 64) lp[i] = legal[i] >= 0 ? pol[legal[i]] : 0.0f;   // pass: no prior
             __syncthreads();
             if (lane == 0) {
                 float sum = 0.0f;
@@ -536,11 +829,13 @@ __global__ __launch_bounds__(64) void k_expand_backup(TreeDev t, int mode) {
         if (status == ST_EVAL && t.ttstore[g]) {
             const uint64_t cur = t.ring_cur[g];
             float* rb = t.ring_buf + (size_t)g * t.ring;
-            for (int i = lane; i < n; i += 64) rb[(cur + i) % (uint64_t)t.ring] = lp[i];
+            const int len = go ? NA : n;            // Go keeps the policy, Gomoku the children priors
+            const float* src = go ? pol : lp;
+            for (int i = lane; i < len; i += 64) rb[(cur + i) % (uint64_t)t.ring] = src[i];
             if (lane == 0) {
                 const size_t tb = (size_t)g * t.tt_slots + t.tthslot[g];
                 t.tt_hash[tb] = hash; t.tt_visits[tb] = 1; t.tt_value[tb] = value; t.tt_ref[tb] = cur;
-                t.ring_cur[g] = cur + (uint64_t)n;
+                t.ring_cur[g] = cur + (uint64_t)len;
             }
         }
         // create children (include/alphazero/mcts/mcts_node.h: N=W=VL=0, prior, action)
@@ -561,7 +856,7 @@ __global__ __launch_bounds__(64) void k_expand_backup(TreeDev t, int mode) {
             nd.first[leaf] = first; nd.cnt[leaf] = (int16_t)n; nd.flag[leaf] = (uint8_t)(nd.flag[leaf] | FL_EXPANDED);
             cnt[CNT_NODES] = first + n;
         }
-        kb += 25LL * n + 7 + 4LL * n + (status == ST_EVAL ? 4LL * A + 4 + 24 : 0);
+        kb += 25LL * n + 7 + 4LL * n + (status == ST_EVAL ? 4LL * NA + 4 + 24 : 0);
     } else if (status == ST_EXPANDED) {
         value = nd.N[leaf] == 0 ? 0.0f : nd.W[leaf] / (float)nd.N[leaf];
     }
@@ -592,11 +887,12 @@ __global__ __launch_bounds__(64) void k_select_action(TreeDev t, int training, f
     const int g = blockIdx.x;
     if (temps && g < t.G) temperature = temps[g];         // per-game schedule (self-play driver)
     const int lane = threadIdx.x;
-    __shared__ float c[AZ_MAXA];
+    __shared__ float c[AZ_MAXNA];
     if (g >= t.G) return;
-    const int A = t.A;
+    const int A = t.A, NA = t.NA;
+    const bool go = t.game == GAME_GO;
     if (!t.active[g]) {
-        if (lane == 0) { actions[g] = -1; values[g] = 0.0f; nchild[g] = 0; }
+        if (lane == 0) { actions[g] = go ? -2 : -1; values[g] = 0.0f; nchild[g] = 0; }
         return;
     }
     GamePtrs nd = game_nodes(t.nd, (size_t)g * t.ncap);
@@ -606,9 +902,10 @@ __global__ __launch_bounds__(64) void k_select_action(TreeDev t, int training, f
     if ((f & FL_TERMINAL) || nc == 0) {
         if (lane == 0) {
             // first legal move of the root state (parallel_mcts.cpp:994-1004)
-            int a = -1;
+            int a = -1;                                         // Go: the pass leads getLegalMoves
             const uint8_t* rb = t.rboard + (size_t)g * A;
-            if (t.rfresh[g]) a = t.fresh_order[0];
+            if (go) a = -1;
+            else if (t.rfresh[g]) a = t.fresh_order[0];
             else for (int x = A - 1; x >= 0; --x) if (rb[x] == 0) { a = x; break; }
             actions[g] = a; values[g] = 0.0f; nchild[g] = 0;
         }
@@ -621,13 +918,13 @@ __global__ __launch_bounds__(64) void k_select_action(TreeDev t, int training, f
         if (ex == 1.0f) v = Nf;                                // pow(x, 1) == x exactly
         else v = (float)pow((double)Nf, (double)ex);
         c[i] = v;
-        child_actions[(size_t)g * A + i] = nd.act[fc + i];
+        child_actions[(size_t)g * NA + i] = nd.act[fc + i];
     }
     __syncthreads();
     if (lane == 0) {
         float total = 0.0f;
         for (int i = 0; i < nc; ++i) total += c[i];
-        float* pr = probs + (size_t)g * A;
+        float* pr = probs + (size_t)g * NA;
         if (total > 0.0f) for (int i = 0; i < nc; ++i) pr[i] = c[i] / total;
         else { const float u = 1.0f / (float)nc; for (int i = 0; i < nc; ++i) pr[i] = u; }
         int bi = 0;
@@ -645,15 +942,34 @@ __global__ __launch_bounds__(64) void k_select_action(TreeDev t, int training, f
     }
 }
 
+// updateWithMove's subtree reuse (parallel_mcts.cpp:1065-1108): the child that played `a`
+// becomes the root, else a fresh root node.  Lane 0.
+__device__ void reuse_child(const TreeDev& t, int g, const GamePtrs& nd, int a) {
+    const int root = t.rnode[g];
+    const int fc = nd.first[root], nc = nd.cnt[root];
+    int child = -1;
+    for (int i = 0; i < nc; ++i) if (nd.act[fc + i] == a) { child = fc + i; break; }
+    if (child < 0) {
+        child = t.atop[g];
+        if (child + 1 > t.ncap) { atomicOr(t.err, ERR_NODES); child = 0; }
+        else t.atop[g] = child + 1;
+        nd.N[child] = 0; nd.W[child] = 0.0f; nd.VL[child] = 0; nd.P[child] = 0.0f;
+        nd.first[child] = -1; nd.act[child] = -1; nd.cnt[child] = 0; nd.flag[child] = 0;
+    }
+    t.rnode[g] = child;
+}
+
 // K5: makeMove + updateWithMove; terminal test of the new root (game loop condition).
 __global__ __launch_bounds__(64) void k_apply(TreeDev t, const int* actions, int* terminal, int* result) {
     const int g = blockIdx.x;
     const int lane = threadIdx.x;
     __shared__ uint8_t board[AZ_MAXA];
+    __shared__ GoLds gl;
     if (g >= t.G) return;
     const int a = actions[g];
     const int A = t.A;
-    if (!t.active[g] || a < 0 || a >= A) {
+    const bool go = t.game == GAME_GO;
+    if (!t.active[g] || a < (go ? -1 : 0) || a >= A) {          // Go: -1 is the pass
         if (lane == 0) { terminal[g] = t.active[g] ? 0 : 1; result[g] = t.gresult[g]; }
         return;
     }
@@ -662,6 +978,35 @@ __global__ __launch_bounds__(64) void k_apply(TreeDev t, const int* actions, int
     const int p = t.rplayer[g];
     for (int i = lane; i < A; i += 64) board[i] = rb[i];
     __syncthreads();
+    if (go) {
+        // GoState::makeMove (go_state.cpp:192-257)
+        go_clear_marks(gl, A, lane);
+        if (lane == 0) {
+            int pp = p, k = t.rko[g], ps = t.rpass[g];
+            uint64_t bh = t.rhash[g];
+            if (go_play_seq(t, board, gl, a, pp, k, ps, bh)) {
+                const int n = t.rnposh[g];
+                if (n >= t.hmax) atomicOr(t.err, ERR_HIST);
+                else { t.rposh[(size_t)g * t.hmax + n] = go_hash(t, bh, pp, k); t.rnposh[g] = n + 1; }
+            }
+            t.rhash[g] = bh; t.rko[g] = k; t.rpass[g] = ps; t.rplayer[g] = 3 - p;
+            int* h = t.rhist + g * 6;
+            for (int i = 5; i > 0; --i) h[i] = h[i - 1];
+            h[0] = a;
+            t.rstones[g] += a >= 0 ? 1 : 0;
+            t.rply[g] += 1;
+            t.rfresh[g] = 0;
+            const int res = ps >= 2 ? go_result_seq(t, board, gl) : R_ONGOING;
+            t.gresult[g] = res;
+            if (res != R_ONGOING) t.active[g] = 0;
+            terminal[g] = res != R_ONGOING;
+            result[g] = res;
+            reuse_child(t, g, nd, a);
+        }
+        __syncthreads();
+        for (int i = lane; i < A; i += 64) rb[i] = board[i];
+        return;
+    }
     if (lane == 0) {
         board[a] = (uint8_t)p;
         rb[a] = (uint8_t)p;
@@ -682,19 +1027,7 @@ __global__ __launch_bounds__(64) void k_apply(TreeDev t, const int* actions, int
         if (res != R_ONGOING) t.active[g] = 0;
         terminal[g] = res != R_ONGOING;
         result[g] = res;
-        // subtree reuse
-        const int root = t.rnode[g];
-        const int fc = nd.first[root], nc = nd.cnt[root];
-        int child = -1;
-        for (int i = 0; i < nc; ++i) if (nd.act[fc + i] == a) { child = fc + i; break; }
-        if (child < 0) {
-            child = t.atop[g];
-            if (child + 1 > t.ncap) { atomicOr(t.err, ERR_NODES); child = 0; }
-            else t.atop[g] = child + 1;
-            nd.N[child] = 0; nd.W[child] = 0.0f; nd.VL[child] = 0; nd.P[child] = 0.0f;
-            nd.first[child] = -1; nd.act[child] = -1; nd.cnt[child] = 0; nd.flag[child] = 0;
-        }
-        t.rnode[g] = child;
+        reuse_child(t, g, nd, a);
     }
 }
 
@@ -754,7 +1087,7 @@ __global__ __launch_bounds__(64) void k_noise(TreeDev t, const float* noise, con
     GamePtrs nd = game_nodes(t.nd, (size_t)g * t.ncap);
     const int root = t.rnode[g];
     const int fc = nd.first[root], nc = nd.cnt[root];
-    const float* nz = noise + (size_t)g * t.A;
+    const float* nz = noise + (size_t)g * t.NA;
     for (int i = lane; i < nc; i += 64) {
         const float old = nd.P[fc + i];
         nd.P[fc + i] = (1.0f - eps) * old + eps * nz[i];
@@ -775,7 +1108,9 @@ __global__ __launch_bounds__(64) void k_new_games(TreeDev t, const int* games, c
     if (lane < CNT_EVALS_TOTAL) cnt[lane] = 0;
     if (lane < 6) t.rhist[g * 6 + lane] = -1;
     if (lane == 0) {
-        t.rplayer[g] = 1; t.rstones[g] = 0; t.rply[g] = 0; t.rhash[g] = t.zplayer[0]; t.rfresh[g] = 1;
+        t.rplayer[g] = 1; t.rstones[g] = 0; t.rply[g] = 0; t.rfresh[g] = 1;
+        t.rhash[g] = t.game == GAME_GO ? 0ULL : t.zplayer[0];   // Go: stones-only hash of the empty board
+        if (t.game == GAME_GO) { t.rko[g] = -1; t.rpass[g] = 0; t.rnposh[g] = 0; }
         t.rnode[g] = 0; t.atop[g] = 1; t.active[g] = 1; t.gresult[g] = R_ONGOING; t.ring_cur[g] = 0;
         nd.N[0] = 0; nd.W[0] = 0.0f; nd.VL[0] = 0; nd.P[0] = 0.0f; nd.first[0] = -1; nd.act[0] = -1;
         nd.cnt[0] = 0; nd.flag[0] = 0;
@@ -807,4 +1142,13 @@ __global__ void k_root_children(TreeDev t, int g, int* act, int* N, int* VL, flo
         act[i] = nd.act[fc + i]; N[i] = nd.N[fc + i]; VL[i] = nd.VL[fc + i]; W[i] = nd.W[fc + i]; P[i] = nd.P[fc + i];
     }
     if (threadIdx.x == 0) { *n = nc; rootinfo[0] = nd.N[root]; rootinfo[1] = nd.VL[root]; *rootW = nd.W[root]; }
+}
+
+// Root child counts (host-side Dirichlet draws need |children| per game).
+__global__ void k_root_nchild(TreeDev t, int* out) {
+    const int g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= t.G) return;
+    GamePtrs nd = game_nodes(t.nd, (size_t)g * t.ncap);
+    const int root = t.rnode[g];
+    out[g] = (nd.flag[root] & FL_EXPANDED) ? (int)nd.cnt[root] : 0;
 }

@@ -121,7 +121,15 @@ typedef struct az_search_cfg {
     int tt_log2;          /* TranspositionTable slots = 2^tt_log2 per game (reference: 20) */
     int node_capacity;    /* per-game node pool (0: auto = sims*A + 4*A) */
     int prior_ring;       /* per-game prior ring floats for TT hits (0: auto) */
+    int game;             /* AZ_GAME_GOMOKU (0) or AZ_GAME_GO (1): GoState(bs, komi 7.5, Chinese rules,
+                             superko), bs 9/13/19, action space bs*bs + 1, pass = action -1.  For Go,
+                             az_search_select reports finished games as AZ_ACTION_NONE and
+                             az_search_apply skips them (Gomoku: -1, as before). */
 } az_search_cfg;
+
+#define AZ_GAME_GOMOKU 0
+#define AZ_GAME_GO 1
+#define AZ_ACTION_NONE (-2)   /* Go: no move (finished game); -1 is the pass */
 
 int az_search_create(az_engine* e, az_net* net, const az_search_cfg* cfg, az_search** out);
 void az_search_destroy(az_search* s);
@@ -135,8 +143,9 @@ int az_search_add_noise_masked(az_search* s, float alpha, float eps, const uint8
 /* ParallelMCTS::search() for every active (non-terminal) game. */
 int az_search_run(az_search* s);
 /* getActionProbabilities(T) + selectAction(isTraining, T) + getRootValue() for every
- * game.  probs: [G][A] in CHILD order (n_children[g] valid entries), children_actions
- * [G][A]; actions[g] = -1 for finished games. */
+ * game.  probs: [G][NA] in CHILD order (n_children[g] valid entries), children_actions
+ * [G][NA] (NA = action space: bs*bs, Go bs*bs + 1); actions[g] = -1 (Go: AZ_ACTION_NONE)
+ * for finished games. */
 int az_search_select(az_search* s, int training, float temperature, int* actions, float* root_values,
                      float* probs, int* children_actions, int* n_children);
 /* state.makeMove(a) + updateWithMove(a) for every game with actions[g] >= 0;

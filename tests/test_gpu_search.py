@@ -62,7 +62,7 @@ def play_and_compare(m, refs, n_games, max_moves=None):
             assert bits([val[g]])[0] == r["value"], (g, ply, "value")
             c = m.counters(g)
             assert (c["tt_lookups"], c["tt_hits"], c["evals"]) == (r["tt_lookups"], r["tt_hits"], r["evals"]), (g, ply)
-        act = np.array([act[g] if live[g] else -1 for g in range(n_games)], np.int32)
+        act = np.array([act[g] if live[g] else m.none for g in range(n_games)], np.int32)
         term, res = m.updateWithMove(act)
         for g in range(n_games):
             if live[g] and (term[g] or ply + 1 >= len(refs[g]["moves"])):
