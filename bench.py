@@ -11,6 +11,9 @@ backup).  Games shard across ranks with no data-path collective (weak scaling:
 
 Synthetic data: games start from the empty board; weights are random-init of the
 named architecture (counter-based generator, identical on every rank).
+
+--game go: the C4 workload (BASELINE.json configs[3]) on one GPU per rank: Go 19x19 (GoState:
+captures, ko, superko, area scoring on device), 8 input planes, 362-way policy, 1024 games.
 """
 import argparse
 import json
@@ -28,6 +31,7 @@ import numpy as np  # noqa: E402
 METRIC = "self-play positions/sec (+ NN evals/sec) at 800 sims/move, 1/2/4/8 GPU"
 PEAK_TFLOPS = {"bf16x3": 2500.0, "bf16": 2500.0, "fp16": 2500.0, "f32": 157.3}   # dense MFMA peaks, MI355X_MICROARCH.md
 PREC = {"f32": 0, "bf16x3": 1, "bf16": 2, "fp16": 3}
+KERNEL = {"fp16": "conv3x3_v6<2>", "bf16": "conv3x3_v6<1>", "bf16x3": "conv3x3_v4<0>", "f32": "gemm_f32"}
 
 
 def parse():
@@ -35,9 +39,10 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--games", type=int, default=2048, help="games per GPU")
+    ap.add_argument("--game", default="gomoku", choices=["gomoku", "go"])
+    ap.add_argument("--games", type=int, default=None, help="games per GPU (C3: 2048, C4: 1024)")
     ap.add_argument("--sims", type=int, default=800)
-    ap.add_argument("--board", type=int, default=15)
+    ap.add_argument("--board", type=int, default=None, help="board size (Gomoku 15, Go 19)")
     ap.add_argument("--channels", type=int, default=256)
     ap.add_argument("--blocks", type=int, default=20)
     ap.add_argument("--precision", default="fp16", choices=list(PREC),
@@ -45,11 +50,14 @@ def parse():
                          "~2^-19 residual stream; C3 logits within 5.9e-5 of fp32), bf16x3 = fp32-faithful")
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU oracle on rank 0 at N=1")
     ap.add_argument("--cpu-moves", type=int, default=1)
+    ap.add_argument("--cpu-sims", type=int, default=None,
+                    help="simulations of the CPU sample move (default: --sims for Gomoku, 100 for Go 19x19); a "
+                         "shorter sample is scaled to --sims by its evaluations/s")
     ap.add_argument("--seed", type=int, default=1234)
     return ap.parse_args()
 
 
-def cpu_baseline(desc, blob, board, sims, moves):
+def cpu_baseline(desc, blob, board, sims, moves, game="gomoku", sample_sims=None):
     """The CPU restatement (oracle/, Mode S, one game) with the fp32 PyTorch-CPU network
     evaluating one state per call, as the reference's ParallelMCTS::evaluateState does."""
     import torch
@@ -63,20 +71,30 @@ def cpu_baseline(desc, blob, board, sims, moves):
         lo, v = model(planes[None])
         return lo[0], float(v[0])
 
-    ev(0, np.zeros((11, board, board), np.float32))   # warm-up
+    ev(0, np.zeros((desc.in_planes, board, board), np.float32))   # warm-up
     calls[0] = 0
+    ss = sample_sims or sims
     t0 = time.perf_counter()
-    O.play(bs=board, sims=sims, max_moves=moves, eval_kind=O.EVAL_NET, evaluator=ev)
+    O.play(bs=board, sims=ss, max_moves=moves, eval_kind=O.EVAL_NET, evaluator=ev,
+           game=O.GAME_GO if game == "go" else O.GAME_GOMOKU)
     dt = time.perf_counter() - t0
-    return {"value": moves / dt, "unit": "positions/s", "cores": torch.get_num_threads(), "kind": "port",
-            "evals_per_s": calls[0] / dt,
-            "sample": f"1 game x {moves} move(s) x {sims} sims, Gomoku {board}x{board}, {desc.blocks}b x "
+    eps = calls[0] / dt
+    value = moves / dt if ss == sims else eps / (sims + 1)      # one evaluation per simulation + the root
+    return {"value": value, "unit": "positions/s", "cores": torch.get_num_threads(), "kind": "port",
+            "evals_per_s": eps,
+            "sample": ("" if ss == sims else f"scaled to {sims} sims/move from ") +
+                      f"1 game x {moves} move(s) x {ss} sims, {game.capitalize()} {board}x{board}, {desc.blocks}b x "
                       f"{desc.channels}f fp32 net on PyTorch-CPU (B=1 per evaluation), oracle/ Mode S search; "
                       f"{calls[0]} evaluations in {dt:.1f} s"}
 
 
 def main():
     a = parse()
+    go = a.game == "go"
+    if a.board is None:
+        a.board = 19 if go else 15
+    if a.games is None:
+        a.games = 1024 if go else 2048
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -90,8 +108,12 @@ def main():
     import az_amd
     import net_oracle
     eng = az_amd.Engine(local)
-    desc = az_amd.gomoku_net_desc(board_size=a.board, channels=a.channels, blocks=a.blocks,
-                                  precision=PREC[a.precision], max_batch=a.games)
+    if go:
+        desc = az_amd.NetDesc(a.board, 8, a.channels, a.blocks, a.board * a.board + 1, 32, 8, 256, 1, 0,
+                              PREC[a.precision], a.games)
+    else:
+        desc = az_amd.gomoku_net_desc(board_size=a.board, channels=a.channels, blocks=a.blocks,
+                                      precision=PREC[a.precision], max_batch=a.games)
     net = az_amd.HipNeuralNetwork(eng, desc)
     from az_amd import dist as azdist
     blob = None
@@ -104,7 +126,8 @@ def main():
     sh = azdist.shard(rank, a.games)       # global game ids / seeds of this rank
     m = az_amd.ParallelMCTS(eng, n_games=a.games, board_size=a.board, num_simulations=a.sims,
                             evaluator=az_amd.AZ_EVAL_NET, net=net, noise_seed=sh["noise_seed"],
-                            noise_seed_stride=sh["noise_seed_stride"])
+                            noise_seed_stride=sh["noise_seed_stride"],
+                            game=az_amd.AZ_GAME_GO if go else az_amd.AZ_GAME_GOMOKU)
     m.newGames()
     m.addDirichletNoise(0.03, 0.25)
     for _ in range(a.warmup):
@@ -151,12 +174,14 @@ def main():
             "vs_baseline": None,
             "dtype": a.precision,
             "data": "synthetic: self-play from empty boards, counter-based random-init weights of the named net",
-            "config": {"workload": f"C3 Gomoku {a.board}x{a.board}, {a.blocks}b x {a.channels}f ResNet, "
-                                   f"{a.sims} sims/move", "games_per_gpu": a.games, "global_games": a.games * world,
+            "config": {"workload": f"{'C4 Go' if go else 'C3 Gomoku'} {a.board}x{a.board}, {a.blocks}b x "
+                                   f"{a.channels}f ResNet, {a.sims} sims/move", "game": a.game,
+                       "games_per_gpu": a.games, "global_games": a.games * world,
                        "sims_per_move": a.sims, "board": a.board, "blocks": a.blocks, "channels": a.channels,
                        "parallelism": f"game-shard x{world}"},
             "nn_evals_per_s": evals / elapsed,
-            "roofline": {"kernel": f"conv3x3_{a.precision} (trunk)", "bound": "mfma", "achieved": achieved,
+            "roofline": {"kernel": f"{KERNEL[a.precision]} ({a.precision} trunk, {a.board}x{a.board})", "bound": "mfma",
+                         "achieved": achieved,
                          "peak": peak, "unit": "TFLOP/s", "frac": achieved / peak, "traffic": None,
                          "launches": launches, "avg_launch_ms": per_launch_ms,
                          "flops_per_launch": per_launch_flops},
@@ -178,7 +203,8 @@ def main():
         if a.cpu_baseline and world == 1:
             if blob is None:
                 blob = net_oracle.init_blob(desc, a.seed)
-            out["cpu_baseline"] = cpu_baseline(desc, blob, a.board, a.sims, a.cpu_moves)
+            out["cpu_baseline"] = cpu_baseline(desc, blob, a.board, a.sims, a.cpu_moves, a.game,
+                                               a.cpu_sims or (100 if go else a.sims))
         else:
             out["cpu_baseline"] = None
         print(json.dumps(out))
