@@ -60,7 +60,7 @@ class IGameState {
     GameType type_;
 };
 
-// Gomoku only (Go / Chess rules are SURVEY.md row f2): throws std::invalid_argument otherwise.
+// Gomoku (15x15 default) and Go (19x19, komi 7.5, Chinese rules); Chess throws std::invalid_argument.
 std::unique_ptr<IGameState> createGameState(GameType type, int boardSize = 0, bool variantRules = false);
 
 }  // namespace core

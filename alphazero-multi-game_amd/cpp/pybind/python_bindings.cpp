@@ -7,6 +7,7 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include "alphazero/games/go/go_state.h"
 #include "alphazero/games/gomoku/gomoku_state.h"
 #include "alphazero/mcts/parallel_mcts.h"
 #include "alphazero/nn/hip_neural_network.h"
@@ -67,6 +68,16 @@ PYBIND11_MODULE(_alphazero_cpp, m) {
              py::arg("use_omok") = false, py::arg("seed") = 0, py::arg("use_pro_long_opening") = false)
         .def("is_occupied", &gomoku::GomokuState::is_occupied)
         .def("get_board", &gomoku::GomokuState::get_board);
+
+    // not in the reference module (its GoState is C++-only); bound for the device Go path
+    py::class_<go::GoState, core::IGameState>(m, "GoState")
+        .def(py::init<int, float, bool, bool>(), py::arg("board_size") = 19, py::arg("komi") = 7.5f,
+             py::arg("chinese_rules") = true, py::arg("enforce_superko") = true)
+        .def("getStone", py::overload_cast<int>(&go::GoState::getStone, py::const_))
+        .def("getCapturedStones", &go::GoState::getCapturedStones)
+        .def("getKoPoint", &go::GoState::getKoPoint)
+        .def("getKomi", &go::GoState::getKomi)
+        .def("calculateScore", &go::GoState::calculateScore);
 
     m.def("createGameState", &core::createGameState, py::arg("type"), py::arg("boardSize") = 0,
           py::arg("variantRules") = false);

@@ -1,6 +1,7 @@
 // Host Gomoku position for the API surface (createGameState, ParallelMCTS roots, predict).
 // The search itself never calls this: the device keeps its own boards (tree_kernels.hip).
 #include "alphazero/games/gomoku/gomoku_state.h"
+#include "alphazero/games/go/go_state.h"
 
 #include <algorithm>
 #include <random>
@@ -209,7 +210,10 @@ std::vector<std::vector<int>> GomokuState::get_board() const {
 
 namespace core {
 std::unique_ptr<IGameState> createGameState(GameType type, int boardSize, bool variantRules) {
-    if (type != GameType::GOMOKU) throw std::invalid_argument("only Gomoku is backed by the engine (Go/Chess: row f2)");
+    // igamestate.cpp:17-49 / game_factory.cpp:88-115: Gomoku 15x15 standard rules, Go 19x19 komi 7.5
+    // Chinese rules; Chess has no rules on this engine (its network shape runs)
+    if (type == GameType::GO) return std::make_unique<go::GoState>(boardSize > 0 ? boardSize : 19, 7.5f, true, true);
+    if (type != GameType::GOMOKU) throw std::invalid_argument("createGameState: Chess rules are not implemented");
     return std::make_unique<gomoku::GomokuState>(boardSize > 0 ? boardSize : 15, variantRules, false);
 }
 }  // namespace core

@@ -10,6 +10,7 @@
 #include <mutex>
 #include <sstream>
 
+#include "alphazero/games/go/go_state.h"
 #include "alphazero/games/gomoku/gomoku_state.h"
 #include "alphazero/nn/hip_neural_network.h"
 #include "alphazero/nn/random_policy_network.h"
@@ -108,6 +109,7 @@ void HipNeuralNetwork::save(const std::string& path) const {
 
 static void statePlanes(const core::IGameState& st, float* out) {
     if (auto* g = dynamic_cast<const gomoku::GomokuState*>(&st)) { g->enhancedPlanes(out); return; }
+    if (auto* g = dynamic_cast<const go::GoState*>(&st)) { g->enhancedPlanes(out); return; }
     const core::Planes t = st.getEnhancedTensorRepresentation();
     size_t k = 0;
     for (const auto& p : t)
@@ -166,7 +168,9 @@ std::string HipNeuralNetwork::getModelInfo() const {
 }
 
 void HipNeuralNetwork::benchmark(int iters, int batch) {
-    gomoku::GomokuState s(shape_.boardSize);
+    gomoku::GomokuState sg(shape_.boardSize >= 5 ? shape_.boardSize : 15);
+    go::GoState sgo(shape_.boardSize);
+    const core::IGameState& s = shape_.inPlanes == 8 ? (const core::IGameState&)sgo : (const core::IGameState&)sg;
     std::vector<std::reference_wrapper<const core::IGameState>> states(batch, std::cref(s));
     std::vector<std::vector<float>> p;
     std::vector<float> v;
@@ -191,7 +195,8 @@ std::pair<std::vector<float>, float> RandomPolicyNetwork::predict(const core::IG
     std::vector<float> p(A, 0.001f);
     std::uniform_real_distribution<float> u(0.0f, 1.0f);
     float sum = 0.0f;
-    for (int a : state.getLegalMoves()) { p[a] = u(rng_); sum += p[a]; }
+    for (int a : state.getLegalMoves())
+        if (a >= 0 && a < A) { p[a] = u(rng_); sum += p[a]; }     // Go's pass (-1) has no entry
     if (sum > 0.0f)
         for (float& x : p) x /= sum;
     std::uniform_real_distribution<float> vd(-0.1f, 0.1f);
@@ -217,7 +222,7 @@ std::future<std::pair<std::vector<float>, float>> RandomPolicyNetwork::predictAs
 
 // --------------------------------------------------------------------------
 std::unique_ptr<NeuralNetwork> NeuralNetwork::create(const std::string& path, core::GameType type, int bs, bool useGpu) {
-    if (type != core::GameType::GOMOKU) throw std::invalid_argument("only Gomoku networks are supported");
+    if (type == core::GameType::CHESS) throw std::invalid_argument("Chess networks are created from .azw files only");
     if (path.empty() || path == "random") return std::make_unique<RandomPolicyNetwork>(type, bs, 0);
     if (!useGpu) throw std::invalid_argument("the engine has no CPU network path (useGpu=false)");
     auto net = HipNeuralNetwork::load(path);

@@ -6,6 +6,7 @@
 #include <iostream>
 #include <sstream>
 
+#include "alphazero/games/go/go_state.h"
 #include "alphazero/nn/hip_neural_network.h"
 #include "alphazero/nn/random_policy_network.h"
 
@@ -60,10 +61,17 @@ ParallelMCTS::~ParallelMCTS() {
 }
 
 void ParallelMCTS::rebuild() {
-    if (root_->getGameType() != core::GameType::GOMOKU) throw std::invalid_argument("ParallelMCTS: Gomoku only");
+    const bool go = root_->getGameType() == core::GameType::GO;
+    if (!go && root_->getGameType() != core::GameType::GOMOKU) throw std::invalid_argument("ParallelMCTS: Gomoku or Go");
+    if (go) {
+        auto* g = dynamic_cast<const go::GoState*>(root_.get());
+        if (!g || g->getKomi() != 7.5f || !g->isChineseRules() || !g->isEnforcingSuperko())
+            throw std::invalid_argument("ParallelMCTS: the device Go rules are komi 7.5, Chinese rules, superko");
+    }
     if (s_) { az_search_destroy(s_); s_ = nullptr; }
     const DeviceEvaluator ev = deviceEvaluator(nn_);
     az_search_cfg c{};
+    c.game = go ? AZ_GAME_GO : AZ_GAME_GOMOKU;
     c.n_games = 1;
     c.board_size = root_->getBoardSize();
     c.num_simulations = config_.numSimulations;

@@ -72,19 +72,21 @@ void progress(void* user, int gid, int move, int total_games, int64_t /*total_mo
 }  // namespace
 
 std::vector<GameRecord> SelfPlayManager::generateGames(core::GameType type, int boardSize, bool variant) {
-    if (type != core::GameType::GOMOKU) throw std::invalid_argument("generateGames: Gomoku only (Go/Chess: row f2)");
+    const bool go = type == core::GameType::GO;
+    if (!go && type != core::GameType::GOMOKU) throw std::invalid_argument("generateGames: Gomoku or Go (no Chess rules)");
     if (variant) throw std::invalid_argument("generateGames: variant rules are not supported");
     running_ = true;
     abort_ = 0;
     completed_ = 0;
     totalMoves_ = 0;
-    const int bs = boardSize > 0 ? boardSize : 15;
+    const int bs = boardSize > 0 ? boardSize : go ? 19 : 15;
     if (save_) std::filesystem::create_directories(outDir_);
     std::vector<GameRecord> records(numGames_, GameRecord(type, bs, variant));
     std::vector<char> done(numGames_, 0);
     try {
         const mcts::DeviceEvaluator ev = mcts::deviceEvaluator(nn_);
         az_search_cfg c{};
+        c.game = go ? AZ_GAME_GO : AZ_GAME_GOMOKU;
         c.n_games = slots_ > 0 ? slots_ : std::min(std::max(numGames_, 1), 2048);
         c.board_size = bs;
         c.num_simulations = numSimulations_;

@@ -861,8 +861,6 @@ int az_search_create(az_engine* e, az_net* net, const az_search_cfg* c, az_searc
         return fail(AZ_ERR_ARG, "unsupported search configuration");
     if (go && bs != 9 && bs != 13 && bs != 19)
         return fail(AZ_ERR_ARG, "Go board %d: GoState supports 9, 13 and 19 (go_state.cpp:24-26)", bs);
-    if (go && c->eval_kind == AZ_EVAL_RANDOM)
-        return fail(AZ_ERR_ARG, "AZ_EVAL_RANDOM (RandomPolicyNetwork) is Gomoku-only");
     if (c->eval_kind == AZ_EVAL_NET) {
         if (!net) return fail(AZ_ERR_ARG, "AZ_EVAL_NET needs a network");
         if (net->d.board_size != bs || net->d.action_size != NA || net->d.in_planes != (go ? 8 : 11))

@@ -775,18 +775,22 @@ __global__ __launch_bounds__(64) void k_expand_backup(TreeDev t, int mode) {
                 for (int a = lane; a < NA; a += 64) pol[a] = hash_eval_p(key, a);
                 value = hash_eval_v(key);
             } else {
+                // RandomPolicyNetwork (random_policy_network.cpp:93-130): draws for legal a >= 0
                 uint32_t* st = t.mt + (size_t)g * 625;
-                for (int a = lane; a < A; a += 64) pol[a] = 0.001f;
+                for (int a = lane; a < NA; a += 64) pol[a] = 0.001f;
                 __syncthreads();
                 if (lane == 0) {
                     float sum = 0.0f;
-                    for (int i = 0; i < n; ++i) { float u = mt_uniform(st, 0.0f, 1.0f); pol[legal[i]] = u; sum += u; }
+                    for (int i = 0; i < n; ++i) {
+                        if (legal[i] < 0) continue;
+                        float u = mt_uniform(st, 0.0f, 1.0f); pol[legal[i]] = u; sum += u;
+                    }
                     s_scalar[0] = sum;
                     s_scalar[1] = mt_uniform(st, -0.1f, 0.1f);
                 }
                 __syncthreads();
                 const float sum = s_scalar[0];
-                if (sum > 0.0f) for (int a = lane; a < A; a += 64) pol[a] = pol[a] / sum;
+                if (sum > 0.0f) for (int a = lane; a < NA; a += 64) pol[a] = pol[a] / sum;
                 value = s_scalar[1];
             }
             __syncthreads();

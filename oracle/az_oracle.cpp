@@ -392,18 +392,20 @@ struct HashEval : Evaluator<S> {
 };
 
 // RandomPolicyNetwork (src/nn/random_policy_network.cpp:9-24,93-138), one instance per game.
+template <class State>
 struct RandomEval : Evaluator<State> {
     std::vector<std::mt19937> rng;
     RandomEval(int games, unsigned seed) { for (int g = 0; g < games; ++g) rng.emplace_back(seed + g); }
     void eval(int game, const State& s, std::vector<float>& p, float& v) override {
-        ++calls;
+        ++this->calls;
         std::uniform_real_distribution<float> dist(0.0f, 1.0f);
-        p.assign(s.A, 0.001f);
+        const int NA = s.NA();
+        p.assign(NA, 0.001f);
         float sum = 0.0f;
         auto legal = s.legal();
-        for (int m : legal) { p[m] = dist(rng[game]); sum += p[m]; }
-        if (sum > 0.0f) for (int i = 0; i < s.A; ++i) p[i] /= sum;
-        else if (!legal.empty()) { float u = 1.0f / (float)legal.size(); for (int m : legal) p[m] = u; }
+        for (int m : legal) if (m >= 0 && m < NA) { p[m] = dist(rng[game]); sum += p[m]; }
+        if (sum > 0.0f) for (int i = 0; i < NA; ++i) p[i] /= sum;
+        else if (!legal.empty()) { float u = 1.0f / (float)legal.size(); for (int m : legal) if (m >= 0) p[m] = u; }
         std::uniform_real_distribution<float> vd(-0.1f, 0.1f);
         v = vd(rng[game]);
     }
@@ -821,13 +823,13 @@ char* az_oracle_play(const az_oracle_cfg* c, int seed_stride, az_eval_cb cb, voi
     if (c->game == 1) {
         GoZobrist z(cfg.bs * cfg.bs, cfg.zobrist_seed);
         HashEval<GoState> he; CallbackEval<GoState> ne(cb, user, c->eval_kind == 2); UniformEval<GoState> ue;
-        Evaluator<GoState>* ev = c->eval_kind == 0 ? (Evaluator<GoState>*)&he
+        RandomEval<GoState> re(c->n_games, c->eval_seed);
+        Evaluator<GoState>* ev = c->eval_kind == 0 ? (Evaluator<GoState>*)&he : c->eval_kind == 1 ? (Evaluator<GoState>*)&re
                                : c->eval_kind == 4 ? (Evaluator<GoState>*)&ue : (Evaluator<GoState>*)&ne;
-        if (c->eval_kind == 1) return nullptr;     // RandomPolicyNetwork is Gomoku-only here
         play_games<GoState, GoZobrist>(c, cfg, z, ev, seed_stride, o);
     } else {
         Zobrist z(cfg.bs * cfg.bs, cfg.zobrist_seed);
-        HashEval<State> he; RandomEval re(c->n_games, c->eval_seed);
+        HashEval<State> he; RandomEval<State> re(c->n_games, c->eval_seed);
         CallbackEval<State> ne(cb, user, c->eval_kind == 2);
         UniformEval<State> ue;
         Evaluator<State>* ev = c->eval_kind == 0 ? (Evaluator<State>*)&he : c->eval_kind == 1 ? (Evaluator<State>*)&re

@@ -120,3 +120,31 @@ def test_host_hip_network_predict_batch_matches_torch():
     p1, v1 = net.predict(states[3])
     assert np.allclose(p1, pol[3]) and abs(v1 - val[3]) < 1e-6
     assert net.isGpuAvailable() and net.getBatchSize() == 8 and "MI355X" in net.getDeviceInfo()
+
+
+@pytest.mark.gpu
+def test_host_go_parallel_mcts_and_selfplay_match_oracle():
+    """Go through the C++ host API: ParallelMCTS(GoState, RandomPolicyNetwork) and
+    SelfPlayManager.generateGames(GO) reproduce the oracle's GoState games bit for bit."""
+    import az_oracle as O
+    bs, sims, mm = 9, 120, 24
+    ref = O.play(bs=bs, sims=sims, max_moves=mm, eval_kind=O.EVAL_RANDOM, eval_seed=5, game=O.GAME_GO)[0]
+    net = az.RandomPolicyNetwork(az.GameType.GO, bs, 5)
+    m = az.ParallelMCTS(az.GoState(bs), net, None, 1, sims, 1.5, 0.0, 3)
+    got = host_play(m, ref["moves"])
+    for ply, (g, r) in enumerate(zip(got, ref["moves"])):
+        assert g == (r["action"], r["probs"], r["value"]), ply
+    total = 4
+    refs = O.play(seed_stride=1, bs=bs, sims=64, max_moves=mm, eval_kind=O.EVAL_RANDOM, eval_seed=5, n_games=total,
+                  game=O.GAME_GO)
+    mgr = az.SelfPlayManager(az.RandomPolicyNetwork(az.GameType.GO, bs, 5), total, 64, 4)
+    mgr.setConcurrentGames(2)
+    mgr.setMaxMoves(mm)
+    mgr.setSeeds(42, 1)
+    recs = mgr.generateGames(az.GameType.GO, bs, False)
+    assert len(recs) == total
+    for g, (rec, r) in enumerate(zip(recs, refs)):
+        mv = rec.getMoves()
+        assert [(x.action, bits(x.policy), bits([x.value])[0]) for x in mv] == \
+               [(y["action"], y["probs"], y["value"]) for y in r["moves"]], g
+        assert int(rec.getResult()) == (r["result"] if r["terminal"] else 0)

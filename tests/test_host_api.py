@@ -136,3 +136,52 @@ def test_no_gpu_fails_loudly():
         az.HipNeuralNetwork(boardSize=9, channels=32, blocks=1)
     with pytest.raises(RuntimeError):
         az.ParallelMCTS(az.GomokuState(9), None)
+
+
+def test_host_go_state_matches_reference_positions():
+    """Host GoState (cpp/src/go_state.cpp) against the reference GoState goldens
+    (tests/golden/ref_go_positions.json.gz): board after captures, ko point, hash, legal order
+    (suicide / ko / superko), result, area score and the 8 feature planes."""
+    import gzip
+    import os
+    gold = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "ref_go_positions.json.gz")
+    with gzip.open(gold, "rt") as f:
+        pos = json.load(f)
+    for bs, d in pos.items():
+        bs = int(bs)
+        for k, p in enumerate(d["positions"]):
+            s = az.GoState(bs)
+            for a in p["moves"]:
+                s.makeMove(a)
+            assert [s.getStone(a) for a in range(bs * bs)] == p["board"], (bs, k)
+            assert s.getKoPoint() == p["ko"] and str(s.getHash()) == p["hash"], (bs, k)
+            assert s.getLegalMoves() == p["legal"], (bs, k)
+            assert int(s.getGameResult()) == p["result"] and s.isTerminal() == bool(p["terminal"]), (bs, k)
+            assert [s.getCapturedStones(1), s.getCapturedStones(2)] == p["captured"], (bs, k)
+            sc = np.asarray(s.calculateScore(), np.float32).view(np.uint32).tolist()
+            assert sc == p["score"], (bs, k)
+            planes = np.asarray(s.getEnhancedTensorRepresentation(), np.float32).reshape(-1)
+            ref = np.zeros_like(planes)
+            for i, b in p["planes"]:
+                ref[i] = np.array([b], np.uint32).view(np.float32)[0]
+            assert np.array_equal(planes.view(np.uint32), ref.view(np.uint32)), (bs, k)
+            # undo back to the empty board
+            for _ in p["moves"]:
+                assert s.undoMove()
+            assert s.getHash() == az.GoState(bs).getHash() and not s.undoMove()
+
+
+def test_host_go_rules_and_factory():
+    s = az.createGameState(az.GameType.GO, 9)
+    assert isinstance(s, az.GoState) and s.getActionSpaceSize() == 82 and s.getLegalMoves()[0] == -1
+    assert az.createGameState(az.GameType.GO).getBoardSize() == 19
+    assert az.GoState(7).getBoardSize() == 19            # the reference constructor's fallback
+    # a few stones, then pass / pass ends the game (area scoring, komi 7.5)
+    s = az.GoState(9)
+    for a in [1, 2, 9, 12, 19, 20, 11, 10]:
+        s.makeMove(a)
+    s.makeMove(-1)
+    s.makeMove(-1)
+    assert s.isTerminal() and s.getGameResult() in (az.GameResult.WIN_PLAYER1, az.GameResult.WIN_PLAYER2)
+    with pytest.raises(Exception):
+        az.createGameState(az.GameType.CHESS)
