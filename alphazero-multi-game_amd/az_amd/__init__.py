@@ -10,6 +10,8 @@ Reference surfaces mirrored (paths relative to the reference root):
                     getActionProbabilities(), getRootValue(), updateWithMove(), addDirichletNoise()
   SelfPlayManager   alphazero::selfplay::SelfPlayManager (src/selfplay/self_play_manager.cpp:47-240):
                     generateGames() with the playSingleGame move loop and temperature schedule.
+  Dataset           alphazero::selfplay::Dataset (src/selfplay/dataset.cpp): extractExamples with the
+                    8-fold augmentation on device, getBatch, shuffle, getRandomSubset, save/load.
 """
 import ctypes
 from dataclasses import dataclass, field
@@ -20,6 +22,7 @@ from ._lib import (AZ_EVAL_HASH, AZ_EVAL_NET, AZ_EVAL_RANDOM, AZ_EVAL_UNIFORM, A
                    GAME_SINK, PROGRESS_FN, NetDesc, SearchCfg, SelfPlayCfg, check, lib)
 
 __all__ = ["Engine", "HipNeuralNetwork", "ParallelMCTS", "SelfPlayManager", "GameRecord", "MoveData", "AzError",
+           "Dataset", "TrainingExample", "GAME_GOMOKU", "GAME_GO",
            "AZ_PREC_F32", "AZ_PREC_BF16X3", "AZ_PREC_BF16", "AZ_PREC_FP16", "AZ_EVAL_NET", "AZ_EVAL_HASH", "AZ_EVAL_RANDOM", "AZ_EVAL_UNIFORM",
            "gomoku_net_desc"]
 
@@ -377,3 +380,175 @@ class SelfPlayManager:
                 m.addDirichletNoise(self.dirichletAlpha, self.dirichletEpsilon)
             move += 1
         return records
+
+
+# ---------------------------------------------------------------------------- Dataset (row f3)
+GAME_GOMOKU, GAME_GO = 0, 1
+_i64 = ctypes.POINTER(ctypes.c_int64)
+
+
+def _json_number(x):
+    """nlohmann::json's text for a float widened to double: shortest round-trip digits, NaN as null."""
+    v = float(x)
+    if v != v or v in (float("inf"), float("-inf")):
+        return "null"
+    return repr(v)
+
+
+@dataclass
+class TrainingExample:
+    """selfplay::TrainingExample (include/alphazero/selfplay/dataset.h:21-28): state [planes][bs][bs],
+    policy (the record's child-order visit distribution), value."""
+    state: np.ndarray
+    policy: np.ndarray
+    value: float
+
+    def toJson(self):
+        # TrainingExample::toJson (src/selfplay/dataset.cpp:16-33): j.dump(), keys sorted
+        st = "[" + ",".join("[" + ",".join("[" + ",".join(_json_number(v) for v in row) + "]" for row in pl) + "]"
+                            for pl in np.asarray(self.state)) + "]"
+        pol = "[" + ",".join(_json_number(v) for v in np.asarray(self.policy)) + "]"
+        return '{"policy":' + pol + ',"state":' + st + ',"value":' + _json_number(self.value) + "}"
+
+    @staticmethod
+    def fromJson(s):
+        import json
+        j = json.loads(s) if isinstance(s, str) else s
+        nan = float("nan")
+        state = np.array([[[nan if v is None else v for v in row] for row in pl] for pl in j["state"]], np.float32)
+        policy = np.array([nan if v is None else v for v in j["policy"]], np.float32)
+        return TrainingExample(state, policy, float(nan if j["value"] is None else j["value"]))
+
+
+class Dataset:
+    """selfplay::Dataset (include/alphazero/selfplay/dataset.h:33-118, src/selfplay/dataset.cpp) over a
+    device-resident example store (az_dataset_*): extractExamples replays every record on the GPU and
+    writes each position's examples (original + 7 symmetries) straight into their shuffled slots;
+    getBatch / getRandomSubset / shuffle are device gathers.  rng_ is the handle's std::mt19937,
+    seeded from std::random_device as the reference does unless `seed` is given."""
+
+    def __init__(self, engine, game_type=GAME_GOMOKU, board_size=15, seed=None):
+        h = ctypes.c_void_p()
+        check(lib().az_dataset_create(engine.h, int(game_type), int(board_size), ctypes.byref(h)))
+        self.h = h
+        self.engine = engine
+        self.game_type, self.bs = int(game_type), int(board_size)
+        if seed is not None:
+            check(lib().az_dataset_seed(self.h, int(seed) & 0xFFFFFFFF))
+        n, c, b, st = ctypes.c_int64(), ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        check(lib().az_dataset_info(self.h, ctypes.byref(n), ctypes.byref(c), ctypes.byref(b), ctypes.byref(st)))
+        self.planes, self.policy_stride = c.value, st.value
+        self.gameRecords = []
+
+    def addGameRecord(self, record, useEnhancedFeatures=True):
+        if record.board_size != self.bs:
+            raise ValueError(f"record board {record.board_size} != dataset board {self.bs}")
+        self.gameRecords.append(record)
+
+    def _order(self, n):
+        out = np.empty(n, np.int64)
+        check(lib().az_dataset_shuffle_order(self.h, int(n), out.ctypes.data_as(_i64)))
+        return out
+
+    def extractExamples(self, includeAugmentations=True, shuffle=True):
+        """Dataset::extractExamples (dataset.cpp:60-114); shuffle=False keeps the pre-shuffle order
+        (record order, per position the original then augmentExample's 7)."""
+        recs = self.gameRecords
+        n_moves = np.array([len(r.moves) for r in recs], np.int32)
+        actions = np.array([m.action for r in recs for m in r.moves], np.int32)
+        nch = np.array([len(m.policy) for r in recs for m in r.moves], np.int32)
+        pols = [np.asarray(m.policy, np.float32) for r in recs for m in r.moves]
+        pol = np.concatenate(pols) if pols else np.zeros(0, np.float32)
+        res = np.array([r.result for r in recs], np.int32)
+        E = int(n_moves.sum()) * (8 if includeAugmentations else 1)
+        order = self._order(E) if shuffle else None
+        ne = ctypes.c_int64()
+        check(lib().az_dataset_extract(self.h, len(recs), _ip(n_moves), _ip(actions), _ip(nch), _fp(pol), _ip(res),
+                                       int(bool(includeAugmentations)),
+                                       order.ctypes.data_as(_i64) if order is not None else None, ctypes.byref(ne)))
+        return ne.value
+
+    def size(self):
+        n = ctypes.c_int64()
+        check(lib().az_dataset_info(self.h, ctypes.byref(n), None, None, None))
+        return n.value
+
+    def gather(self, idx):
+        """Examples idx as arrays: states [n][planes][bs][bs], policy [n][stride], policy_len [n], value [n]."""
+        idx = np.ascontiguousarray(idx, np.int64)
+        n = len(idx)
+        st = np.empty((n, self.planes, self.bs, self.bs), np.float32)
+        po = np.empty((n, self.policy_stride), np.float32)
+        pl = np.empty(n, np.int32)
+        va = np.empty(n, np.float32)
+        if n:
+            check(lib().az_dataset_gather(self.h, idx.ctypes.data_as(_i64), n, _fp(st), _fp(po), _ip(pl), _fp(va)))
+        return st, po, pl, va
+
+    def getBatch(self, batchSize):
+        """Dataset::getBatch (dataset.cpp:120-145): std::shuffle of all indices, the first batchSize."""
+        n = self.size()
+        b = min(int(batchSize), n)
+        st, po, pl, va = self.gather(self._order(n)[:b])
+        return st, [po[i, :pl[i]].copy() for i in range(b)], va
+
+    def shuffle(self):
+        n = self.size()
+        if n:
+            check(lib().az_dataset_permute(self.h, self._order(n).ctypes.data_as(_i64)))
+
+    def getRandomSubset(self, count):
+        n = self.size()
+        st, po, pl, va = self.gather(self._order(n)[:min(int(count), n)])
+        return [TrainingExample(st[i], po[i, :pl[i]].copy(), float(va[i])) for i in range(len(va))]
+
+    def examples(self):
+        st, po, pl, va = self.gather(np.arange(self.size()))
+        return [TrainingExample(st[i], po[i, :pl[i]].copy(), float(va[i])) for i in range(len(va))]
+
+    def saveToFile(self, filename):
+        """Dataset::saveToFile (dataset.cpp:151-186): {"examples":[...]} as j.dump()."""
+        try:
+            with open(filename, "w") as f:
+                f.write('{"examples":[' + ",".join(e.toJson() for e in self.examples()) + "]}")
+            return True
+        except Exception:
+            return False
+
+    def loadFromFile(self, filename):
+        """Dataset::loadFromFile (dataset.cpp:188-227); examples go to the device store."""
+        import json
+        try:
+            with open(filename) as f:
+                j = json.load(f)
+            exs = [TrainingExample.fromJson(e) for e in j["examples"]]
+        except Exception:
+            return False
+        n = len(exs)
+        st = np.zeros((n, self.planes, self.bs, self.bs), np.float32)
+        po = np.zeros((n, self.policy_stride), np.float32)
+        pl = np.zeros(n, np.int32)
+        va = np.zeros(n, np.float32)
+        for i, e in enumerate(exs):
+            st[i] = e.state
+            pl[i] = len(e.policy)
+            po[i, :pl[i]] = e.policy
+            va[i] = e.value
+        check(lib().az_dataset_upload(self.h, n, _fp(st), _fp(po), _ip(pl), _fp(va)))
+        return True
+
+    def profile_read(self):
+        ms, by = ctypes.c_double(), ctypes.c_double()
+        check(lib().az_dataset_profile_read(self.h, ctypes.byref(ms), ctypes.byref(by)))
+        return ms.value, by.value
+
+    def close(self):
+        if self.h:
+            lib().az_dataset_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -73,6 +73,17 @@ EXPORTS = {
     "az_search_read_eval_log": (c_int, [vp, P(c_float), P(c_float), P(c_float), P(c_int)]),
     "az_selfplay_step": (c_int, [vp, P(SelfPlayCfg), P(c_int64), P(c_int64)]),
     "az_selfplay_run": (c_int, [vp, P(SelfPlayCfg), c_int, c_int, GAME_SINK, PROGRESS_FN, vp, P(c_int)]),
+    "az_dataset_create": (c_int, [vp, c_int, c_int, P(vp)]),
+    "az_dataset_destroy": (None, [vp]),
+    "az_dataset_extract": (c_int, [vp, c_int, P(c_int), P(c_int), P(c_int), P(c_float), P(c_int), c_int, P(c_int64),
+                                   P(c_int64)]),
+    "az_dataset_info": (c_int, [vp, P(c_int64), P(c_int), P(c_int), P(c_int)]),
+    "az_dataset_seed": (c_int, [vp, c_uint32]),
+    "az_dataset_shuffle_order": (c_int, [vp, c_int64, P(c_int64)]),
+    "az_dataset_upload": (c_int, [vp, c_int64, P(c_float), P(c_float), P(c_int), P(c_float)]),
+    "az_dataset_permute": (c_int, [vp, P(c_int64)]),
+    "az_dataset_gather": (c_int, [vp, P(c_int64), c_int, P(c_float), P(c_float), P(c_int), P(c_float)]),
+    "az_dataset_profile_read": (c_int, [vp, P(ctypes.c_double), P(ctypes.c_double)]),
 }
 
 _lib = None

@@ -1,7 +1,7 @@
 // _alphazero_cpp: the reference's Python module surface (src/pybind/python_bindings.cpp:26-458)
 // over the MI355X host API.  The GIL is released around search / generateGames / predict /
 // predictBatch / benchmark and re-acquired for the progress callback, as in the reference.
-// Not bound: the LibTorch module classes (DDWRandWire, SEBlock, ...) and Dataset (out of scope).
+// Not bound: the LibTorch module classes (DDWRandWire, SEBlock, ...).
 #include <pybind11/functional.h>
 #include <pybind11/numpy.h>
 #include <pybind11/pybind11.h>
@@ -12,6 +12,7 @@
 #include "alphazero/mcts/parallel_mcts.h"
 #include "alphazero/nn/hip_neural_network.h"
 #include "alphazero/nn/random_policy_network.h"
+#include "alphazero/selfplay/dataset.h"
 #include "alphazero/selfplay/game_record.h"
 #include "alphazero/selfplay/self_play_manager.h"
 
@@ -264,6 +265,34 @@ PYBIND11_MODULE(_alphazero_cpp, m) {
         .def_static("fromJson", &selfplay::GameRecord::fromJson)
         .def_static("loadFromFile", &selfplay::GameRecord::loadFromFile);
     m.def("jsonNumber", &selfplay::jsonNumber);
+
+    // python_bindings.cpp:339-358
+    py::class_<selfplay::TrainingExample>(m, "TrainingExample")
+        .def(py::init<>())
+        .def_readwrite("state", &selfplay::TrainingExample::state)
+        .def_readwrite("policy", &selfplay::TrainingExample::policy)
+        .def_readwrite("value", &selfplay::TrainingExample::value)
+        .def("toJson", &selfplay::TrainingExample::toJson)
+        .def_static("fromJson", &selfplay::TrainingExample::fromJson);
+
+    py::class_<selfplay::Dataset>(m, "Dataset")
+        .def(py::init<>())
+        .def(py::init<int>(), py::arg("device"))
+        .def("addGameRecord", &selfplay::Dataset::addGameRecord, py::arg("record"),
+             py::arg("useEnhancedFeatures") = true)
+        .def("extractExamples", [](selfplay::Dataset& self, bool aug) {
+            py::gil_scoped_release release;
+            self.extractExamples(aug);
+        }, py::arg("includeAugmentations") = true)
+        .def("size", &selfplay::Dataset::size)
+        .def("getBatch", &selfplay::Dataset::getBatch)
+        .def("shuffle", &selfplay::Dataset::shuffle)
+        .def("saveToFile", &selfplay::Dataset::saveToFile)
+        .def("loadFromFile", &selfplay::Dataset::loadFromFile)
+        .def("getRandomSubset", &selfplay::Dataset::getRandomSubset)
+        .def("setSeed", &selfplay::Dataset::setSeed)
+        .def("getExamples", &selfplay::Dataset::getExamples)
+        .def("lastExtractMs", &selfplay::Dataset::lastExtractMs);
 
     py::class_<selfplay::SelfPlayManager>(m, "SelfPlayManager")
         .def(py::init<nn::NeuralNetwork*, int, int, int>(), py::arg("neuralNetwork"), py::arg("numGames") = 100,

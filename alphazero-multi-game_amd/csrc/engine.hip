@@ -19,6 +19,7 @@
 #include <vector>
 
 #include "../../include/az_engine.h"
+#include "engine_internal.h"
 #include "net.h"
 #include "tree.h"
 
@@ -54,10 +55,10 @@ void az_launch_split_bf16(const float* in, uint16_t* hi, uint16_t* lo, size_t n,
                           int C, hipStream_t st);
 
 namespace {
-
 thread_local std::string g_err;
+}  // namespace
 
-int fail(int code, const char* fmt, ...) {
+int az_fail(int code, const char* fmt, ...) {
     char buf[512];
     va_list ap;
     va_start(ap, fmt);
@@ -67,20 +68,8 @@ int fail(int code, const char* fmt, ...) {
     return code;
 }
 
-#define HIPCHK(x)                                                                            \
-    do {                                                                                     \
-        hipError_t e_ = (x);                                                                 \
-        if (e_ != hipSuccess) return fail(AZ_ERR_HIP, "%s: %s (%s:%d)", #x, hipGetErrorString(e_), __FILE__, __LINE__); \
-    } while (0)
+namespace {
 
-template <class T>
-int dalloc(T** p, size_t n) {
-    if (n == 0) n = 1;
-    hipError_t e = hipMalloc((void**)p, n * sizeof(T));
-    if (e != hipSuccess) return fail(AZ_ERR_OOM, "hipMalloc(%zu bytes): %s", n * sizeof(T), hipGetErrorString(e));
-    return 0;
-}
-#define DALLOC(p, n) do { int r_ = dalloc(&(p), (n)); if (r_) return r_; } while (0)
 
 uint64_t splitmix64(uint64_t x) {
     x += 0x9E3779B97F4A7C15ULL;
@@ -91,13 +80,6 @@ uint64_t splitmix64(uint64_t x) {
 
 }  // namespace
 
-// ===========================================================================
-struct az_engine {
-    int device = 0;
-    hipStream_t stream = nullptr;
-    hipDeviceProp_t prop{};
-    std::mutex mu;
-};
 
 struct Layer {            // one implicit-GEMM layer, BN folded
     float* W = nullptr;   // [N][K] fp32
@@ -256,7 +238,7 @@ int net_load(az_net* n, const float* blob) {
         b.assign(bb, bb + 1);
         if (int r = upload_layer(n->vfc2, W, b, 1, d.fc_hidden, 1, d.fc_hidden, false)) return r;
     }
-    if (pc.off != n->nparams) return fail(AZ_ERR_ARG, "parameter blob size mismatch (%zu vs %zu)", pc.off, n->nparams);
+    if (pc.off != n->nparams) return az_fail(AZ_ERR_ARG, "parameter blob size mismatch (%zu vs %zu)", pc.off, n->nparams);
     n->loaded = true;
     return 0;
 }
@@ -303,7 +285,7 @@ int net_forward(az_net* n, const float* x0, int B, const int* nb, float* logits,
         a.a_tail = n->act_elems * 2;          // th's zeroed tail sits behind its full capacity
         a.zero = n->zero;
         a.stamp = -1;
-        if (az_conv_g8_launch(a, mode, st)) return fail(AZ_ERR_ARG, "g8 input conv: unsupported shape");
+        if (az_conv_g8_launch(a, mode, st)) return az_fail(AZ_ERR_ARG, "g8 input conv: unsupported shape");
     } else if (g8) {
         // few input planes on a board v6 cannot take at 16 channels: f32 input conv, then to g8
         az_launch_gemm_f32(gemm_args(n->in, x0, n->cin_pad, n->h0, F, nullptr, rows, H, W, nb, HW), ACT_RELU, false, st);
@@ -350,7 +332,7 @@ int net_forward(az_net* n, const float* x0, int B, const int* nb, float* logits,
                 a.a_tail = n->act_elems * 2;
                 a.zero = n->zero;
                 a.stamp = 2 * i;
-                if (az_conv_g8_launch(a, mode, st)) return fail(AZ_ERR_ARG, "g8 trunk conv: unsupported shape");
+                if (az_conv_g8_launch(a, mode, st)) return az_fail(AZ_ERR_ARG, "g8 trunk conv: unsupported shape");
                 ConvBf16Args b2 = a;
                 b2.stamp = 2 * i + 1;
                 b2.Ahi = n->th;
@@ -358,7 +340,7 @@ int net_forward(az_net* n, const float* x0, int B, const int* nb, float* logits,
                 b2.Chi = n->hh[cur ^ 1]; b2.Cq = hq[cur ^ 1];
                 b2.bias = L2.b;
                 if (d.residual) { b2.Rhi = n->hh[cur]; b2.Rq = hq[cur]; }
-                if (az_conv_g8_launch(b2, mode, st)) return fail(AZ_ERR_ARG, "g8 trunk conv: unsupported shape");
+                if (az_conv_g8_launch(b2, mode, st)) return az_fail(AZ_ERR_ARG, "g8 trunk conv: unsupported shape");
                 cur ^= 1;
             }
             if (ev1) HIPCHK(hipEventRecord(ev1, st));
@@ -461,7 +443,7 @@ int check_err(az_search* s) {
     int err = 0;
     HIPCHK(hipMemcpyAsync(&err, s->t.err, 4, hipMemcpyDeviceToHost, s->e->stream));
     HIPCHK(hipStreamSynchronize(s->e->stream));
-    if (err) return fail(AZ_ERR_CAPACITY, "device capacity exceeded (flags 0x%x: 1 node pool, 2 path, 4 prior ring)", err);
+    if (err) return az_fail(AZ_ERR_CAPACITY, "device capacity exceeded (flags 0x%x: 1 node pool, 2 path, 4 prior ring)", err);
     return 0;
 }
 
@@ -555,7 +537,7 @@ int search_new_games(az_search* s, const int* games, int n, const int* seed_ids 
     if (n <= 0) return 0;
     hipStream_t st = s->e->stream;
     for (int i = 0; i < n; ++i)
-        if (games[i] < 0 || games[i] >= s->c.n_games) return fail(AZ_ERR_ARG, "game index %d out of range", games[i]);
+        if (games[i] < 0 || games[i] >= s->c.n_games) return az_fail(AZ_ERR_ARG, "game index %d out of range", games[i]);
     HIPCHK(hipMemcpyAsync(s->d_games, games, n * 4, hipMemcpyHostToDevice, st));
     if (seed_ids) HIPCHK(hipMemcpyAsync(s->d_seed_ids, seed_ids, n * 4, hipMemcpyHostToDevice, st));
     s->t.nd = s->arena[s->cur];
@@ -626,17 +608,17 @@ extern "C" {
 const char* az_last_error(void) { return g_err.c_str(); }
 
 int az_engine_create(int device, az_engine** out) {
-    if (!out) return fail(AZ_ERR_ARG, "null out");
+    if (!out) return az_fail(AZ_ERR_ARG, "null out");
     int n = 0;
     hipError_t e = hipGetDeviceCount(&n);
-    if (e != hipSuccess || n <= 0) return fail(AZ_ERR_HIP, "no HIP device available (hipGetDeviceCount: %s)", hipGetErrorString(e));
-    if (device < 0 || device >= n) return fail(AZ_ERR_ARG, "device %d out of range (%d devices)", device, n);
+    if (e != hipSuccess || n <= 0) return az_fail(AZ_ERR_HIP, "no HIP device available (hipGetDeviceCount: %s)", hipGetErrorString(e));
+    if (device < 0 || device >= n) return az_fail(AZ_ERR_ARG, "device %d out of range (%d devices)", device, n);
     auto* en = new az_engine();
     en->device = device;
     hipError_t r = hipSetDevice(device);
     if (r == hipSuccess) r = hipGetDeviceProperties(&en->prop, device);
     if (r == hipSuccess) r = hipStreamCreateWithFlags(&en->stream, hipStreamNonBlocking);
-    if (r != hipSuccess) { delete en; return fail(AZ_ERR_HIP, "device init: %s", hipGetErrorString(r)); }
+    if (r != hipSuccess) { delete en; return az_fail(AZ_ERR_HIP, "device init: %s", hipGetErrorString(r)); }
     *out = en;
     return 0;
 }
@@ -649,29 +631,29 @@ void az_engine_destroy(az_engine* e) {
 }
 
 int az_engine_device_name(az_engine* e, char* buf, int len) {
-    if (!e || !buf || len <= 0) return fail(AZ_ERR_ARG, "bad args");
+    if (!e || !buf || len <= 0) return az_fail(AZ_ERR_ARG, "bad args");
     snprintf(buf, len, "%s (%s)", e->prop.name, e->prop.gcnArchName);
     return 0;
 }
 
 // ------------------------------------------------------------------ net
 static int check_precision(const az_net_desc& d, int precision) {
-    if (precision < 0 || precision > 3) return fail(AZ_ERR_ARG, "bad precision %d", precision);
-    if (precision != AZ_PREC_F32 && d.channels % 32) return fail(AZ_ERR_ARG, "bf16/fp16 trunk needs channels %% 32 == 0");
+    if (precision < 0 || precision > 3) return az_fail(AZ_ERR_ARG, "bad precision %d", precision);
+    if (precision != AZ_PREC_F32 && d.channels % 32) return az_fail(AZ_ERR_ARG, "bf16/fp16 trunk needs channels %% 32 == 0");
     if (precision == AZ_PREC_FP16 && !az_conv_v4_supported(d.board_size, d.board_size, d.channels, d.channels) &&
         !az_conv_g8_supported(d.board_size, d.board_size, d.channels, d.channels))
-        return fail(AZ_ERR_ARG, "AZ_PREC_FP16 trunk needs 15x15 boards and channels %% 64 == 0, or an 8/9/13/15/19 board "
+        return az_fail(AZ_ERR_ARG, "AZ_PREC_FP16 trunk needs 15x15 boards and channels %% 64 == 0, or an 8/9/13/15/19 board "
                                 "and channels %% 128 == 0");
     return 0;
 }
 
 int az_net_create(az_engine* e, const az_net_desc* d, az_net** out) {
-    if (!e || !d || !out) return fail(AZ_ERR_ARG, "null argument");
+    if (!e || !d || !out) return az_fail(AZ_ERR_ARG, "null argument");
     if (d->board_size < 2 || d->board_size * d->board_size > AZ_MAXA || d->in_planes < 1 || d->in_planes > 128 ||
         d->channels < 4 || d->channels % 4 || d->blocks < 0 || d->action_size < 1 || d->action_size > 8192 ||
         d->head_channels < 1 || d->head_channels % 4 || d->pool < 1 || d->fc_hidden < 1 || d->fc_hidden % 4 ||
         d->max_batch < 1)
-        return fail(AZ_ERR_ARG, "unsupported network description");
+        return az_fail(AZ_ERR_ARG, "unsupported network description");
     if (int r = check_precision(*d, d->precision)) return r;
     std::lock_guard<std::mutex> lk(e->mu);
     HIPCHK(hipSetDevice(e->device));
@@ -693,7 +675,7 @@ int az_net_create(az_engine* e, const az_net_desc* d, az_net** out) {
     // DMA of halo padding rows there
     auto H_ = [&](uint16_t** p, size_t cnt) {
         if (!r) r = dalloc(p, cnt + AZ_ACT_TAIL);
-        if (!r && hipMemset(*p + cnt, 0, AZ_ACT_TAIL * 2) != hipSuccess) r = fail(AZ_ERR_HIP, "hipMemset");
+        if (!r && hipMemset(*p + cnt, 0, AZ_ACT_TAIL * 2) != hipSuccess) r = az_fail(AZ_ERR_HIP, "hipMemset");
     };
     A_(&n->x0, rows * n->cin_pad);
     A_(&n->h0, rows * F); A_(&n->h1, rows * F); A_(&n->t, rows * F);
@@ -709,7 +691,7 @@ int az_net_create(az_engine* e, const az_net_desc* d, az_net** out) {
     A_(&n->in_nchw, B * d->in_planes * n->HW);
     if (!r) r = dalloc(&n->d_nb, 1);
     if (!r) r = dalloc(&n->zero, 128);
-    if (!r && hipMemset(n->zero, 0, 256) != hipSuccess) r = fail(AZ_ERR_HIP, "memset");
+    if (!r && hipMemset(n->zero, 0, 256) != hipSuccess) r = az_fail(AZ_ERR_HIP, "memset");
     if (const char* v = getenv("AZ_CONV_VARIANT")) az_conv_set_variant(atoi(v));
     if (const char* v = getenv("AZ_V4_SCHED")) az_conv_set_v4_sched(atoi(v));
     if (const char* v = getenv("AZ_CONV_FLAGS")) az_diag_set_conv_flags(atoi(v));
@@ -734,14 +716,14 @@ void az_net_destroy(az_net* n) {
 }
 
 int az_net_num_params(az_net* n, size_t* count) {
-    if (!n || !count) return fail(AZ_ERR_ARG, "null argument");
+    if (!n || !count) return az_fail(AZ_ERR_ARG, "null argument");
     *count = n->nparams;
     return 0;
 }
 
 int az_net_load_weights(az_net* n, const float* blob, size_t count) {
-    if (!n || !blob) return fail(AZ_ERR_ARG, "null argument");
-    if (count != n->nparams) return fail(AZ_ERR_ARG, "expected %zu parameters, got %zu", n->nparams, count);
+    if (!n || !blob) return az_fail(AZ_ERR_ARG, "null argument");
+    if (count != n->nparams) return az_fail(AZ_ERR_ARG, "expected %zu parameters, got %zu", n->nparams, count);
     std::lock_guard<std::mutex> lk(n->mu);
     HIPCHK(hipSetDevice(n->e->device));
     return net_load(n, blob);
@@ -749,7 +731,7 @@ int az_net_load_weights(az_net* n, const float* blob, size_t count) {
 
 // Counter-based init; tests/nn_weights.py restates it in numpy (same fp32 ops).
 int az_net_init_random(az_net* n, uint64_t seed) {
-    if (!n) return fail(AZ_ERR_ARG, "null net");
+    if (!n) return az_fail(AZ_ERR_ARG, "null net");
     const az_net_desc& d = n->d;
     std::vector<float> blob(n->nparams);
     size_t off = 0;
@@ -786,20 +768,20 @@ int az_net_init_random(az_net* n, uint64_t seed) {
     conv(HC, F, 1);
     fill((size_t)d.fc_hidden * HC * PP, 0, HC * PP); fill(d.fc_hidden, 1, HC * PP);
     fill(d.fc_hidden, 0, d.fc_hidden); fill(1, 1, d.fc_hidden);
-    if (off != n->nparams) return fail(AZ_ERR_STATE, "init size mismatch");
+    if (off != n->nparams) return az_fail(AZ_ERR_STATE, "init size mismatch");
     return az_net_load_weights(n, blob.data(), blob.size());
 }
 
 int az_net_set_precision(az_net* n, int precision) {
-    if (!n) return fail(AZ_ERR_ARG, "null net");
+    if (!n) return az_fail(AZ_ERR_ARG, "null net");
     if (int r = check_precision(n->d, precision)) return r;
     n->d.precision = precision;
     return 0;
 }
 
 static int net_host_forward(az_net* n, const float* planes, int B, float* logits, float* value, bool soft) {
-    if (!n || !planes || B < 1 || B > n->d.max_batch) return fail(AZ_ERR_ARG, "bad batch (1..%d)", n ? n->d.max_batch : 0);
-    if (!n->loaded) return fail(AZ_ERR_STATE, "weights not loaded");
+    if (!n || !planes || B < 1 || B > n->d.max_batch) return az_fail(AZ_ERR_ARG, "bad batch (1..%d)", n ? n->d.max_batch : 0);
+    if (!n->loaded) return az_fail(AZ_ERR_STATE, "weights not loaded");
     std::lock_guard<std::mutex> lk(n->mu);
     HIPCHK(hipSetDevice(n->e->device));
     hipStream_t st = n->e->stream;
@@ -818,7 +800,7 @@ static int net_host_forward(az_net* n, const float* planes, int B, float* logits
 }
 
 int az_net_profile(az_net* n, int enable) {
-    if (!n) return fail(AZ_ERR_ARG, "null net");
+    if (!n) return az_fail(AZ_ERR_ARG, "null net");
     std::lock_guard<std::mutex> lk(n->mu);
     n->prof = enable != 0;
     n->evused = 0; n->prof_launches = 0; n->prof_forwards = 0;
@@ -826,7 +808,7 @@ int az_net_profile(az_net* n, int enable) {
 }
 
 int az_net_profile_read(az_net* n, double* trunk_ms, int64_t* trunk_launches, int64_t* forwards) {
-    if (!n) return fail(AZ_ERR_ARG, "null net");
+    if (!n) return az_fail(AZ_ERR_ARG, "null net");
     std::lock_guard<std::mutex> lk(n->mu);
     HIPCHK(hipSetDevice(n->e->device));
     HIPCHK(hipStreamSynchronize(n->e->stream));
@@ -852,21 +834,21 @@ int az_net_predict_batch(az_net* n, const float* planes, int B, float* policy, f
 
 // ------------------------------------------------------------------ search
 int az_search_create(az_engine* e, az_net* net, const az_search_cfg* c, az_search** out) {
-    if (!e || !c || !out) return fail(AZ_ERR_ARG, "null argument");
+    if (!e || !c || !out) return az_fail(AZ_ERR_ARG, "null argument");
     const int bs = c->board_size, A = bs * bs, G = c->n_games;
     const bool go = c->game == AZ_GAME_GO;
     const int NA = go ? A + 1 : A;
     if (bs < 3 || A > AZ_MAXA || G < 1 || c->num_simulations < 0 || c->virtual_loss < 0 || c->tt_log2 < 4 ||
         c->tt_log2 > 24 || c->eval_kind < 0 || c->eval_kind > 3 || (c->game != AZ_GAME_GOMOKU && !go))
-        return fail(AZ_ERR_ARG, "unsupported search configuration");
+        return az_fail(AZ_ERR_ARG, "unsupported search configuration");
     if (go && bs != 9 && bs != 13 && bs != 19)
-        return fail(AZ_ERR_ARG, "Go board %d: GoState supports 9, 13 and 19 (go_state.cpp:24-26)", bs);
+        return az_fail(AZ_ERR_ARG, "Go board %d: GoState supports 9, 13 and 19 (go_state.cpp:24-26)", bs);
     if (c->eval_kind == AZ_EVAL_NET) {
-        if (!net) return fail(AZ_ERR_ARG, "AZ_EVAL_NET needs a network");
+        if (!net) return az_fail(AZ_ERR_ARG, "AZ_EVAL_NET needs a network");
         if (net->d.board_size != bs || net->d.action_size != NA || net->d.in_planes != (go ? 8 : 11))
-            return fail(AZ_ERR_ARG, "network shape does not match the board");
-        if (net->d.max_batch < G) return fail(AZ_ERR_ARG, "network max_batch %d < n_games %d", net->d.max_batch, G);
-        if (!net->loaded) return fail(AZ_ERR_STATE, "network weights not loaded");
+            return az_fail(AZ_ERR_ARG, "network shape does not match the board");
+        if (net->d.max_batch < G) return az_fail(AZ_ERR_ARG, "network max_batch %d < n_games %d", net->d.max_batch, G);
+        if (!net->loaded) return az_fail(AZ_ERR_STATE, "network weights not loaded");
     }
     std::lock_guard<std::mutex> lk(e->mu);
     HIPCHK(hipSetDevice(e->device));
@@ -898,7 +880,7 @@ int az_search_create(az_engine* e, az_net* net, const az_search_cfg* c, az_searc
     SA(t.tt_hash, (size_t)G * t.tt_slots); SA(t.tt_visits, (size_t)G * t.tt_slots); SA(t.tt_value, (size_t)G * t.tt_slots);
     SA(t.tt_ref, (size_t)G * t.tt_slots);
     SA(t.ring_buf, (size_t)G * ring); SA(t.ring_cur, G); SA(t.cnt, (size_t)G * AZ_NCNT);
-    if (!r) r = hipMemset(t.cnt, 0, (size_t)G * AZ_NCNT * 8) == hipSuccess ? 0 : fail(AZ_ERR_HIP, "memset");
+    if (!r) r = hipMemset(t.cnt, 0, (size_t)G * AZ_NCNT * 8) == hipSuccess ? 0 : az_fail(AZ_ERR_HIP, "memset");
     uint64_t* zp = nullptr; uint64_t* zpl = nullptr; int* fo = nullptr;
     SA(zp, 2 * A); SA(zpl, 2); SA(fo, A);
     if (c->eval_kind == AZ_EVAL_RANDOM) SA(t.mt, (size_t)G * 625);
@@ -978,28 +960,28 @@ void az_search_destroy(az_search* s) {
 }
 
 int az_search_new_games(az_search* s, const int* games, int n) {
-    if (!s || (!games && n)) return fail(AZ_ERR_ARG, "null argument");
+    if (!s || (!games && n)) return az_fail(AZ_ERR_ARG, "null argument");
     std::lock_guard<std::mutex> lk(s->mu);
     HIPCHK(hipSetDevice(s->e->device));
     return search_new_games(s, games, n);
 }
 
 int az_search_add_noise(az_search* s, float alpha, float eps) {
-    if (!s) return fail(AZ_ERR_ARG, "null search");
+    if (!s) return az_fail(AZ_ERR_ARG, "null search");
     std::lock_guard<std::mutex> lk(s->mu);
     HIPCHK(hipSetDevice(s->e->device));
     return search_noise(s, alpha, eps, nullptr);
 }
 
 int az_search_add_noise_masked(az_search* s, float alpha, float eps, const uint8_t* mask) {
-    if (!s || !mask) return fail(AZ_ERR_ARG, "null argument");
+    if (!s || !mask) return az_fail(AZ_ERR_ARG, "null argument");
     std::lock_guard<std::mutex> lk(s->mu);
     HIPCHK(hipSetDevice(s->e->device));
     return search_noise(s, alpha, eps, mask);
 }
 
 int az_search_run(az_search* s) {
-    if (!s) return fail(AZ_ERR_ARG, "null search");
+    if (!s) return az_fail(AZ_ERR_ARG, "null search");
     std::lock_guard<std::mutex> lk(s->mu);
     HIPCHK(hipSetDevice(s->e->device));
     return search_run(s);
@@ -1007,26 +989,26 @@ int az_search_run(az_search* s) {
 
 int az_search_select(az_search* s, int training, float temperature, int* actions, float* root_values, float* probs,
                      int* children_actions, int* n_children) {
-    if (!s) return fail(AZ_ERR_ARG, "null search");
+    if (!s) return az_fail(AZ_ERR_ARG, "null search");
     std::lock_guard<std::mutex> lk(s->mu);
     HIPCHK(hipSetDevice(s->e->device));
     return search_select(s, training, nullptr, temperature, actions, root_values, probs, children_actions, n_children);
 }
 
 int az_search_apply(az_search* s, const int* actions, int* terminal, int* result) {
-    if (!s || !actions) return fail(AZ_ERR_ARG, "null argument");
+    if (!s || !actions) return az_fail(AZ_ERR_ARG, "null argument");
     std::lock_guard<std::mutex> lk(s->mu);
     HIPCHK(hipSetDevice(s->e->device));
     const int G = s->c.n_games, A = s->t.A;
     for (int g = 0; g < G; ++g)
         if (actions[g] >= A || (s->t.game == GAME_GO && actions[g] < AZ_ACTION_NONE))
-            return fail(AZ_ERR_ARG, "action %d out of range for game %d", actions[g], g);
+            return az_fail(AZ_ERR_ARG, "action %d out of range for game %d", actions[g], g);
     HIPCHK(hipMemcpyAsync(s->d_actions, actions, G * 4, hipMemcpyHostToDevice, s->e->stream));
     return search_apply_dev(s, terminal, result);
 }
 
 int az_search_root_children(az_search* s, int game, int* actions, int* N, int* VL, float* W, float* P, int* n_children) {
-    if (!s || game < 0 || game >= s->c.n_games || !n_children) return fail(AZ_ERR_ARG, "bad argument");
+    if (!s || game < 0 || game >= s->c.n_games || !n_children) return az_fail(AZ_ERR_ARG, "bad argument");
     std::lock_guard<std::mutex> lk(s->mu);
     HIPCHK(hipSetDevice(s->e->device));
     hipStream_t st = s->e->stream;
@@ -1049,7 +1031,7 @@ int az_search_root_children(az_search* s, int game, int* actions, int* N, int* V
 }
 
 int az_search_root_node(az_search* s, int game, int* N, int* VL, float* W) {
-    if (!s || game < 0 || game >= s->c.n_games) return fail(AZ_ERR_ARG, "bad argument");
+    if (!s || game < 0 || game >= s->c.n_games) return az_fail(AZ_ERR_ARG, "bad argument");
     std::lock_guard<std::mutex> lk(s->mu);
     HIPCHK(hipSetDevice(s->e->device));
     int root = 0;
@@ -1063,7 +1045,7 @@ int az_search_root_node(az_search* s, int game, int* N, int* VL, float* W) {
 }
 
 int az_search_counters(az_search* s, int game, int64_t* out5) {
-    if (!s || game < 0 || game >= s->c.n_games || !out5) return fail(AZ_ERR_ARG, "bad argument");
+    if (!s || game < 0 || game >= s->c.n_games || !out5) return az_fail(AZ_ERR_ARG, "bad argument");
     std::lock_guard<std::mutex> lk(s->mu);
     HIPCHK(hipSetDevice(s->e->device));
     long long c[AZ_NCNT];
@@ -1073,7 +1055,7 @@ int az_search_counters(az_search* s, int game, int64_t* out5) {
 }
 
 int az_search_enable_eval_log(az_search* s, int game, int capacity) {
-    if (!s || game < 0 || game >= s->c.n_games || capacity < 1) return fail(AZ_ERR_ARG, "bad argument");
+    if (!s || game < 0 || game >= s->c.n_games || capacity < 1) return az_fail(AZ_ERR_ARG, "bad argument");
     std::lock_guard<std::mutex> lk(s->mu);
     HIPCHK(hipSetDevice(s->e->device));
     TreeDev& t = s->t;
@@ -1088,7 +1070,7 @@ int az_search_enable_eval_log(az_search* s, int game, int capacity) {
 }
 
 int az_search_read_eval_log(az_search* s, float* policy, float* value, float* planes, int* count) {
-    if (!s || !count) return fail(AZ_ERR_ARG, "bad argument");
+    if (!s || !count) return az_fail(AZ_ERR_ARG, "bad argument");
     std::lock_guard<std::mutex> lk(s->mu);
     HIPCHK(hipSetDevice(s->e->device));
     TreeDev& t = s->t;
@@ -1105,7 +1087,7 @@ int az_search_read_eval_log(az_search* s, float* policy, float* value, float* pl
 
 // One playSingleGame move for every active game (self_play_manager.cpp:187-216).
 int az_selfplay_step(az_search* s, const az_selfplay_cfg* cfg, int64_t* moves_done, int64_t* evals_done) {
-    if (!s || !cfg) return fail(AZ_ERR_ARG, "null argument");
+    if (!s || !cfg) return az_fail(AZ_ERR_ARG, "null argument");
     std::lock_guard<std::mutex> lk(s->mu);
     HIPCHK(hipSetDevice(s->e->device));
     const int G = s->c.n_games;
@@ -1151,7 +1133,7 @@ int az_selfplay_step(az_search* s, const az_selfplay_cfg* cfg, int64_t* moves_do
 
 int az_selfplay_run(az_search* s, const az_selfplay_cfg* cfg, int total_games, int max_moves, az_game_sink sink,
                     az_progress_fn progress, void* user, const volatile int* abort_flag) {
-    if (!s || !cfg || total_games < 0) return fail(AZ_ERR_ARG, "bad argument");
+    if (!s || !cfg || total_games < 0) return az_fail(AZ_ERR_ARG, "bad argument");
     std::lock_guard<std::mutex> lk(s->mu);
     HIPCHK(hipSetDevice(s->e->device));
     hipStream_t st = s->e->stream;
@@ -1241,7 +1223,7 @@ int az_selfplay_run(az_search* s, const az_selfplay_cfg* cfg, int total_games, i
 }
 
 int az_search_profile(az_search* s, int enable) {
-    if (!s) return fail(AZ_ERR_ARG, "null search");
+    if (!s) return az_fail(AZ_ERR_ARG, "null search");
     std::lock_guard<std::mutex> lk(s->mu);
     HIPCHK(hipSetDevice(s->e->device));
     HIPCHK(hipStreamSynchronize(s->e->stream));
@@ -1255,7 +1237,7 @@ int az_search_profile(az_search* s, int enable) {
 
 int az_search_profile_read(az_search* s, double* select_ms, double* expand_ms, int64_t* sim_steps,
                            int64_t* select_bytes, int64_t* expand_bytes) {
-    if (!s) return fail(AZ_ERR_ARG, "null search");
+    if (!s) return az_fail(AZ_ERR_ARG, "null search");
     std::lock_guard<std::mutex> lk(s->mu);
     HIPCHK(hipSetDevice(s->e->device));
     HIPCHK(hipStreamSynchronize(s->e->stream));

@@ -60,3 +60,22 @@ struct TreeDev {
     const float* net_value;      // [B]
     int log_game, log_cap; float* log_pol; float* log_val; float* log_planes; int* log_n;
 };
+
+// Training-example extraction (Dataset::extractExamples + augmentExample).
+// Records are flattened: game g owns moves [move_off[g], move_off[g+1]); move m owns policy
+// floats [pol_off[m], pol_off[m] + n_children[m]).  Pre-shuffle example e = m * K + s (s = 0
+// original, 1..7 the reference's augmentation order); dst[e] is its slot (null: e).
+struct DatasetDev {
+    int game, bs, A, NA, C, K, n_games;
+    const int* move_off;         // [n_games + 1]
+    const int* actions;          // [M]
+    const long long* pol_off;    // [M]
+    const int* n_children;       // [M]
+    const float* policies;       // [sum n_children]
+    const int* results;          // [n_games] GameResult
+    const long long* dst;        // [M * K] or null
+    float* states;               // [E][C][A]   (state[plane][row][col], NCHW)
+    float* policy;               // [E][NA]     child-order targets, zero past plen
+    int* plen;                   // [E]
+    float* value;                // [E]
+};

@@ -1156,3 +1156,161 @@ __global__ void k_root_nchild(TreeDev t, int* out) {
     const int root = t.rnode[g];
     out[g] = (nd.flag[root] & FL_EXPANDED) ? (int)nd.cnt[root] : 0;
 }
+
+// ---------------------------------------------------------------------------
+// K-D: training examples (Dataset::extractExamples, src/selfplay/dataset.cpp:60-114, with
+// augmentExample :245-436).  One wave per game replays the record (GomokuState / GoState
+// makeMove on the LDS board), builds the position's planes in LDS (getEnhancedTensorRepresentation)
+// and writes the K = 8 (or 1) examples of every position straight to their shuffled slots:
+// no intermediate copy, HBM-bound on the example writes.
+//
+// Symmetry s maps a state pixel (row, col) to a destination; the kernel runs it backwards
+// (src[s][dest]) so the writes are contiguous.  The reference's order: 0 original, 1 rot90
+// (i,j)->(j,bs-1-i), 2 rot180, 3 rot270 (i,j)->(bs-1-j,i), 4 flipH (i,j)->(i,bs-1-j),
+// 5..7 flipH applied to rot90 / rot180 / rot270 (:372-433).
+namespace {
+__device__ __forceinline__ int sym_src(int s, int a, int bs) {
+    const int r = a / bs, c = a % bs, m = bs - 1;
+    switch (s) {
+        case 1: return (m - c) * bs + r;
+        case 2: return (m - r) * bs + (m - c);
+        case 3: return c * bs + (m - r);
+        case 4: return r * bs + (m - c);
+        case 5: return c * bs + r;
+        case 6: return (m - r) * bs + c;
+        case 7: return (m - c) * bs + (m - r);
+        default: return a;
+    }
+}
+}  // namespace
+
+__global__ __launch_bounds__(64) void k_dataset_extract(DatasetDev d, TreeDev t) {
+    const int g = blockIdx.x;
+    const int lane = threadIdx.x;
+    if (g >= d.n_games) return;
+    const int bs = d.bs, A = d.A, C = d.C, K = d.K, NA = d.NA;
+    __shared__ uint8_t board[AZ_MAXA];
+    __shared__ float pl[11 * AZ_MAXA];          // planes of the current position, [C][A]
+    __shared__ float pin[AZ_MAXNA];             // the move's child-order policy
+    __shared__ int16_t src[8][AZ_MAXA];         // sym_src tables
+    __shared__ GoLds L;
+    __shared__ int hist6[6];
+    for (int a = lane; a < A; a += 64) {
+        board[a] = 0;
+        for (int s = 0; s < K; ++s) src[s][a] = (int16_t)sym_src(s, a, bs);
+    }
+    if (lane < 6) hist6[lane] = -1;
+    int player = 1, ko = -1, passes = 0;
+    uint64_t bh = 0;
+    // GameResult -> value of player 1 (:83-89); flipped for player 2 as -gameValue (-0.0f for draws)
+    const int res = d.results[g];
+    const float gv = res == R_WIN1 ? 1.0f : res == R_WIN2 ? -1.0f : 0.0f;
+    const int m0 = d.move_off[g], m1 = d.move_off[g + 1];
+    __syncthreads();
+    for (int m = m0; m < m1; ++m) {
+        // ---- planes of the position before move m
+        if (d.game == GAME_GO) {
+            go_clear_marks(L, A, lane);
+            go_groups(t, board, L, lane);
+            const float half = (float)(bs / 2);
+            for (int a = lane; a < A; a += 64) {
+                const int v = board[a];
+                const int x = a % bs, y = a / bs;
+                pl[a] = v == 1 ? 1.0f : 0.0f;
+                pl[A + a] = v == 2 ? 1.0f : 0.0f;
+                pl[2 * A + a] = player == 1 ? 1.0f : 0.0f;
+                const float lib = v ? fminf(1.0f, (float)L.glib[L.gid[a]] / 10.0f) : 0.0f;
+                pl[3 * A + a] = v == 1 ? lib : 0.0f;
+                pl[4 * A + a] = v == 2 ? lib : 0.0f;
+                pl[5 * A + a] = a == ko ? 1.0f : 0.0f;
+                pl[6 * A + a] = (float)min(x, bs - 1 - x) / half;
+                pl[7 * A + a] = (float)min(y, bs - 1 - y) / half;
+            }
+        } else {
+            int hp[6];
+            for (int i = 0; i < 6; ++i) hp[i] = (((player == 1) == ((i % 2) == 0)) ? 3 : 6) + i / 2;
+            for (int a = lane; a < A; a += 64) {
+                float c[11];
+                for (int k = 0; k < 11; ++k) c[k] = 0.0f;
+                const int v = board[a];
+                if (v == player) c[0] = 1.0f;
+                else if (v == 3 - player) c[1] = 1.0f;
+                if (player == 1) c[2] = 1.0f;
+                for (int i = 0; i < 6; ++i)
+                    if (hist6[i] == a) c[hp[i]] = 1.0f;
+                c[9] = (float)(a / bs) / (float)(bs - 1);
+                c[10] = (float)(a % bs) / (float)(bs - 1);
+                for (int k = 0; k < 11; ++k) pl[k * A + a] = c[k];
+            }
+        }
+        const int n = d.n_children[m];
+        const float* pg = d.policies + d.pol_off[m];
+        for (int k = lane; k < n; k += 64) pin[k] = pg[k];
+        __syncthreads();
+        const float val = player == 2 ? -gv : gv;
+        for (int s = 0; s < K; ++s) {
+            const long long e = (long long)m * K + s;
+            const long long slot = d.dst ? d.dst[e] : e;
+            float* o = d.states + slot * (long long)(C * A);
+            for (int c = 0; c < C; ++c)
+                for (int a = lane; a < A; a += 64) o[c * A + a] = pl[c * A + src[s][a]];
+            // policy: the reference permutes the child-order vector by board index, guarded by
+            // oldIdx/newIdx < size; entries it does not overwrite keep the copied value
+            float* op = d.policy + slot * (long long)NA;
+            for (int k = lane; k < NA; k += 64) {
+                float v = 0.0f;
+                if (k < n) {
+                    if (s == 0) {
+                        v = pin[k];
+                    } else if (s <= 4) {
+                        const int j = k < A ? src[s][k] : n;
+                        v = (k < A && j < n) ? pin[j] : pin[k];
+                    } else {
+                        const int f = k < A ? src[4][k] : n;       // flip source, then the rotation
+                        const int q = (k < A && f < n) ? f : k;
+                        const int r = q < A ? src[s - 4][q] : n;
+                        v = (q < A && r < n) ? pin[r] : pin[q];
+                    }
+                }
+                op[k] = v;
+            }
+            if (lane == 0) { d.plen[slot] = n; d.value[slot] = val; }
+        }
+        __syncthreads();
+        // ---- makeMove
+        const int a = d.actions[m];
+        if (d.game == GAME_GO) {
+            go_clear_marks(L, A, lane);
+            if (lane == 0) go_play_seq(t, board, L, a, player, ko, passes, bh);
+        } else if (lane == 0) {
+            board[a] = (uint8_t)player;
+            for (int i = 5; i > 0; --i) hist6[i] = hist6[i - 1];
+            hist6[0] = a;
+        }
+        player = 3 - player;
+        __syncthreads();
+        ko = __shfl(ko, 0);
+    }
+}
+
+// Example gather (getBatch / getRandomSubset / shuffle): destination row i <- source row idx[i];
+// one block per row, 16-byte copies when the row length allows.
+__global__ __launch_bounds__(256) void k_dataset_gather(const float* states, const float* policy, const int* plen,
+                                                        const float* value, int row, int NA, const long long* idx,
+                                                        int n, float* ostates, float* opolicy, int* oplen,
+                                                        float* ovalue) {
+    const int i = blockIdx.x;
+    if (i >= n) return;
+    const long long j = idx[i];
+    const float* s = states + j * row;
+    float* o = ostates + (long long)i * row;
+    if ((row & 3) == 0) {
+        const float4* s4 = reinterpret_cast<const float4*>(s);
+        float4* o4 = reinterpret_cast<float4*>(o);
+        for (int k = threadIdx.x; k < row / 4; k += 256) o4[k] = s4[k];
+    } else {
+        for (int k = threadIdx.x; k < row; k += 256) o[k] = s[k];
+    }
+    for (int k = threadIdx.x; k < NA; k += 256) opolicy[(long long)i * NA + k] = policy[j * NA + k];
+    if (threadIdx.x == 0) { oplen[i] = plen[j]; ovalue[i] = value[j]; }
+}

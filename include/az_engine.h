@@ -212,6 +212,45 @@ typedef void (*az_progress_fn)(void* user, int game_id, int move_num, int total_
 int az_selfplay_run(az_search* s, const az_selfplay_cfg* cfg, int total_games, int max_moves, az_game_sink sink,
                     az_progress_fn progress, void* user, const volatile int* abort_flag);
 
+/* --------------------------------------------------------------- dataset */
+/* alphazero::selfplay::Dataset (include/alphazero/selfplay/dataset.h:33-118,
+ * src/selfplay/dataset.cpp): device-resident training examples.  Example layout in HBM:
+ * states fp32 [E][planes][bs][bs] (TrainingExample::state[plane][row][col]), policy fp32
+ * [E][policy_stride] in the record's CHILD order (MoveData::policy, zero past its length),
+ * policy length int32 [E], value fp32 [E]. */
+typedef struct az_dataset az_dataset;
+int az_dataset_create(az_engine* e, int game_type, int board_size, az_dataset** out);   /* AZ_GAME_* */
+void az_dataset_destroy(az_dataset* d);
+/* Dataset::extractExamples (dataset.cpp:60-114) over n_games records, replacing the examples:
+ * game g has n_moves[g] moves; actions[] and n_children[] are concatenated over all moves,
+ * policies[] concatenates every move's child-order policy; results[g] is the GameResult.
+ * augment != 0: each position yields the original and the 7 augmentExample symmetries
+ * (dataset.cpp:245-436) in the reference's order.  order (optional, E entries): slot i receives
+ * pre-shuffle example order[i] -- the permutation Dataset::shuffle's std::shuffle applies
+ * (dataset.cpp:112-113,147-149); null keeps the pre-shuffle order. */
+int az_dataset_extract(az_dataset* d, int n_games, const int* n_moves, const int* actions, const int* n_children,
+                       const float* policies, const int* results, int augment, const int64_t* order,
+                       int64_t* n_examples);
+int az_dataset_info(az_dataset* d, int64_t* n_examples, int* planes, int* board_size, int* policy_stride);
+/* The handle's std::mt19937 (Dataset::rng_, dataset.h:115; the reference seeds it from
+ * std::random_device, dataset.cpp:57 -- az_dataset_create does the same, az_dataset_seed fixes it). */
+int az_dataset_seed(az_dataset* d, uint32_t seed);
+/* std::shuffle of 0..n-1 on the handle's engine (libstdc++, as dataset.cpp:113,131,148,235 call it):
+ * the order argument of az_dataset_extract / az_dataset_permute, or getBatch's index list. */
+int az_dataset_shuffle_order(az_dataset* d, int64_t n, int64_t* order);
+/* Replace the examples with n host examples (Dataset::loadFromFile, dataset.cpp:188-227). */
+int az_dataset_upload(az_dataset* d, int64_t n, const float* states, const float* policy, const int* policy_len,
+                      const float* value);
+/* Dataset::shuffle (dataset.cpp:147-149) on device: slot i receives the current example order[i]. */
+int az_dataset_permute(az_dataset* d, const int64_t* order);
+/* Dataset::getBatch / getRandomSubset (dataset.cpp:120-145,229-243): examples idx[0..n) gathered on
+ * the device, then copied to the host buffers (states [n][planes][bs][bs], policy [n][stride]). */
+int az_dataset_gather(az_dataset* d, const int64_t* idx, int n, float* states, float* policy, int* policy_len,
+                      float* value);
+/* Measurement: time (HIP events on the engine stream) and algorithmic HBM bytes of the last
+ * extraction kernel. */
+int az_dataset_profile_read(az_dataset* d, double* extract_ms, double* bytes);
+
 #ifdef __cplusplus
 }
 #endif

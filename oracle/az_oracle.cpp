@@ -891,3 +891,133 @@ int az_oracle_gamma(unsigned seed, float alpha, int calls, int n, float* out) {
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------------------
+// Dataset::extractExamples (src/selfplay/dataset.cpp:60-114) + augmentExample (:245-436), written
+// the way the reference writes them (nested vectors, one copy-and-permute loop per transform,
+// the policy permuted by board index under the oldIdx/newIdx < size guard), BEFORE the final
+// shuffle (:112-113).  Examples are emitted per move: original, then the 7 augmentations.
+// Chess is not restated (no rules here); variant rules are not supported.
+namespace {
+using Planes = std::vector<std::vector<std::vector<float>>>;
+struct Example { Planes state; std::vector<float> policy; float value; };
+
+template <class S>
+Planes nested_planes(const S& s) {
+    std::vector<float> flat((size_t)S::NPLANES * s.A);
+    s.planes(flat.data());
+    Planes st(S::NPLANES, std::vector<std::vector<float>>(s.bs, std::vector<float>(s.bs)));
+    for (int p = 0; p < S::NPLANES; ++p)
+        for (int i = 0; i < s.bs; ++i)
+            for (int j = 0; j < s.bs; ++j) st[p][i][j] = flat[(size_t)p * s.A + i * s.bs + j];
+    return st;
+}
+
+enum Tf { ROT90, ROT180, ROT270, FLIPH };
+// one transform of augmentExample: state loop + policy loop (e.g. rot90 :262-287)
+Example transform(const Example& in, Tf tf) {
+    Example out = in;
+    const size_t P = in.state.size(), bs = in.state[0].size();
+    auto dest = [&](size_t i, size_t j, size_t& r, size_t& c) {
+        switch (tf) {
+            case ROT90: r = j; c = bs - 1 - i; break;
+            case ROT180: r = bs - 1 - i; c = bs - 1 - j; break;
+            case ROT270: r = bs - 1 - j; c = i; break;
+            default: r = i; c = bs - 1 - j; break;
+        }
+    };
+    for (size_t p = 0; p < P; ++p)
+        for (size_t i = 0; i < bs; ++i)
+            for (size_t j = 0; j < bs; ++j) { size_t r, c; dest(i, j, r, c); out.state[p][r][c] = in.state[p][i][j]; }
+    out.policy.resize(in.policy.size());
+    for (size_t i = 0; i < bs; ++i)
+        for (size_t j = 0; j < bs; ++j) {
+            size_t r, c;
+            dest(i, j, r, c);
+            const size_t oldIdx = i * bs + j, newIdx = r * bs + c;
+            if (oldIdx < in.policy.size() && newIdx < out.policy.size()) out.policy[newIdx] = in.policy[oldIdx];
+        }
+    return out;
+}
+
+template <class S, class Z>
+void extract_game(int bs, unsigned zseed, int n, const int* actions, const int* nch, const float* pol, int result,
+                  bool augment, std::vector<Example>& ex) {
+    Z z(bs * bs, zseed);
+    S state(bs, &z);
+    for (int i = 0; i < n; ++i) {
+        if (i > 0) state.play(actions[i - 1]);
+        Example e;
+        e.state = nested_planes(state);
+        e.policy.assign(pol, pol + nch[i]);
+        pol += nch[i];
+        float gameValue = 0.0f;
+        if (result == WIN_P1) gameValue = 1.0f;
+        else if (result == WIN_P2) gameValue = -1.0f;
+        if (state.player == 2) gameValue = -gameValue;
+        e.value = gameValue;
+        ex.push_back(e);
+        if (augment) {
+            Example r90 = transform(e, ROT90), r180 = transform(e, ROT180), r270 = transform(e, ROT270);
+            ex.push_back(r90);
+            ex.push_back(r180);
+            ex.push_back(r270);
+            ex.push_back(transform(e, FLIPH));
+            ex.push_back(transform(r90, FLIPH));
+            ex.push_back(transform(r180, FLIPH));
+            ex.push_back(transform(r270, FLIPH));
+        }
+    }
+}
+}  // namespace
+
+extern "C" {
+// game_type 0 Gomoku / 1 Go.  Outputs (pre-shuffle order): states [E][planes][bs][bs],
+// policy [E][pstride] (zero past the length), plen [E], value [E].  Returns E or -1.
+long long az_oracle_dataset(int game_type, int bs, int n_games, const int* n_moves, const int* actions,
+                            const int* n_children, const float* policies, const int* results, int augment,
+                            float* states_out, float* policy_out, int pstride, int* plen_out, float* value_out) {
+    std::vector<Example> ex;
+    for (int g = 0; g < n_games; ++g) {
+        if (game_type == 1)
+            extract_game<GoState, GoZobrist>(bs, 12345u, n_moves[g], actions, n_children, policies, results[g],
+                                             augment != 0, ex);
+        else if (game_type == 0)
+            extract_game<State, Zobrist>(bs, 12345u, n_moves[g], actions, n_children, policies, results[g],
+                                         augment != 0, ex);
+        else
+            return -1;
+        for (int i = 0; i < n_moves[g]; ++i) policies += n_children[i];
+        actions += n_moves[g];
+        n_children += n_moves[g];
+    }
+    const int A = bs * bs;
+    for (size_t e = 0; e < ex.size(); ++e) {
+        const Example& x = ex[e];
+        const size_t P = x.state.size();
+        if (states_out)
+            for (size_t p = 0; p < P; ++p)
+                for (int i = 0; i < bs; ++i)
+                    for (int j = 0; j < bs; ++j) states_out[(e * P + p) * A + i * bs + j] = x.state[p][i][j];
+        if (policy_out) {
+            for (int k = 0; k < pstride; ++k) policy_out[e * pstride + k] = k < (int)x.policy.size() ? x.policy[k] : 0.0f;
+            plen_out[e] = (int)x.policy.size();
+        }
+        if (value_out) value_out[e] = x.value;
+    }
+    return (long long)ex.size();
+}
+
+// Dataset::shuffle's std::shuffle over n indices with std::mt19937(seed), `calls` times in a row
+// on the same engine (dataset.cpp:147-149): out[c][i] = source index of slot i after call c.
+int az_oracle_shuffle(unsigned seed, long long n, int calls, long long* out) {
+    std::mt19937 rng(seed);
+    for (int c = 0; c < calls; ++c) {
+        std::vector<long long> idx((size_t)n);
+        for (long long i = 0; i < n; ++i) idx[(size_t)i] = i;
+        std::shuffle(idx.begin(), idx.end(), rng);
+        std::copy(idx.begin(), idx.end(), out + (size_t)c * n);
+    }
+    return 0;
+}
+}  // extern "C"

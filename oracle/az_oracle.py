@@ -64,6 +64,12 @@ def lib():
         L.az_oracle_fresh_order.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
         L.az_oracle_gamma.argtypes = [ctypes.c_uint, ctypes.c_float, ctypes.c_int, ctypes.c_int,
                                       ctypes.POINTER(ctypes.c_float)]
+        fp, ip = ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_int)
+        L.az_oracle_dataset.restype = ctypes.c_longlong
+        L.az_oracle_dataset.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ip, ip, ip, fp, ip, ctypes.c_int,
+                                        fp, fp, ctypes.c_int, ip, fp]
+        L.az_oracle_shuffle.argtypes = [ctypes.c_uint, ctypes.c_longlong, ctypes.c_int,
+                                        ctypes.POINTER(ctypes.c_longlong)]
         _lib = L
     return _lib
 
@@ -151,3 +157,34 @@ def gamma_draws(seed, alpha, calls, n):
     out = np.zeros(calls * n, dtype=np.float32)
     lib().az_oracle_gamma(seed, alpha, calls, n, out.ctypes.data_as(ctypes.POINTER(ctypes.c_float)))
     return out.reshape(calls, n)
+
+
+def dataset(game_type, bs, records, augment=True):
+    """Dataset::extractExamples before its shuffle.  records: [(actions, [policy per move], result)].
+    Returns states [E][planes][bs][bs], policy [E][stride] (zero past the length), plen [E], value [E]."""
+    fp, ip = ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_int)
+    A = bs * bs
+    planes, stride = (8, A + 1) if game_type == 1 else (11, A)
+    n_moves = np.array([len(r[0]) for r in records], np.int32)
+    actions = np.array([a for r in records for a in r[0]], np.int32)
+    nch = np.array([len(p) for r in records for p in r[1]], np.int32)
+    pol = np.array([x for r in records for p in r[1] for x in p], np.float32)
+    res = np.array([r[2] for r in records], np.int32)
+    E = int(n_moves.sum()) * (8 if augment else 1)
+    st = np.zeros((max(E, 1), planes, bs, bs), np.float32)
+    po = np.zeros((max(E, 1), stride), np.float32)
+    pl = np.zeros(max(E, 1), np.int32)
+    va = np.zeros(max(E, 1), np.float32)
+    e = lib().az_oracle_dataset(game_type, bs, len(records), n_moves.ctypes.data_as(ip), actions.ctypes.data_as(ip),
+                                nch.ctypes.data_as(ip), pol.ctypes.data_as(fp), res.ctypes.data_as(ip), int(augment),
+                                st.ctypes.data_as(fp), po.ctypes.data_as(fp), stride, pl.ctypes.data_as(ip),
+                                va.ctypes.data_as(fp))
+    assert e == E, (e, E)
+    return st[:E], po[:E], pl[:E], va[:E]
+
+
+def shuffle_orders(seed, n, calls=1):
+    """std::shuffle of 0..n-1 on std::mt19937(seed), `calls` successive shuffles (Dataset::shuffle)."""
+    out = np.zeros((calls, max(n, 1)), np.int64)
+    lib().az_oracle_shuffle(seed, n, calls, out.ctypes.data_as(ctypes.POINTER(ctypes.c_longlong)))
+    return out[:, :n]

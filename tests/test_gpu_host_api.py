@@ -148,3 +148,51 @@ def test_host_go_parallel_mcts_and_selfplay_match_oracle():
         assert [(x.action, bits(x.policy), bits([x.value])[0]) for x in mv] == \
                [(y["action"], y["probs"], y["value"]) for y in r["moves"]], g
         assert int(rec.getResult()) == (r["result"] if r["terminal"] else 0)
+
+
+@pytest.mark.gpu
+def test_host_dataset_from_selfplay_matches_oracle(tmp_path):
+    """Dataset (dataset.cpp) through the host API: generateGames records -> extractExamples
+    (device replay + 8-fold augmentation, written into std::shuffle's slots) == the oracle's
+    examples permuted by the same libstdc++ shuffle; getBatch / getRandomSubset / shuffle draw
+    from the same rng_; save/load round trip."""
+    import az_oracle as O
+    total, bs, sims = 4, 7, 48
+    net = az.RandomPolicyNetwork(az.GameType.GOMOKU, bs, 5)
+    mgr = az.SelfPlayManager(net, total, sims, 4)
+    mgr.setMaxMoves(24)
+    recs = mgr.generateGames(az.GameType.GOMOKU, bs, False)
+    ds = az.Dataset()
+    ds.setSeed(77)
+    for r in recs:
+        ds.addGameRecord(r)
+    ds.extractExamples(True)
+    E = ds.size()
+    ref = O.dataset(0, bs, [([m.action for m in r.getMoves()], [m.policy for m in r.getMoves()],
+                             int(r.getResult())) for r in recs])
+    assert E == len(ref[0]) == 8 * sum(len(r.getMoves()) for r in recs)
+    orders = O.shuffle_orders(77, E, 4)
+    slot = [x[orders[0]] for x in ref]
+    ex = ds.getExamples()
+    for i in (0, 1, E // 2, E - 1):
+        assert bits(np.asarray(ex[i].state).reshape(-1)) == bits(slot[0][i].reshape(-1))
+        assert bits(ex[i].policy) == bits(slot[1][i, :slot[2][i]])
+        assert bits([ex[i].value]) == bits([slot[3][i]])
+    st, pol, val = ds.getBatch(16)
+    idx = orders[1][:16]
+    assert bits(np.asarray(st).reshape(-1)) == bits(slot[0][idx].reshape(-1))
+    assert bits(val) == bits(slot[3][idx])
+    sub = ds.getRandomSubset(3)
+    assert [bits([e.value])[0] for e in sub] == bits(slot[3][orders[2][:3]])
+    ds.shuffle()
+    ex2 = ds.getExamples()
+    perm = slot[3][orders[3]]
+    assert bits([e.value for e in ex2]) == bits(perm)
+    f = str(tmp_path / "d.json")
+    assert ds.saveToFile(f)
+    ds2 = az.Dataset()
+    assert ds2.loadFromFile(f)
+    assert ds2.size() == E
+    ex3 = ds2.getExamples()
+    assert all(bits(np.asarray(a.state).reshape(-1)) == bits(np.asarray(b.state).reshape(-1)) for a, b in zip(ex2[:8], ex3[:8]))
+    assert bits([e.value for e in ex3]) == bits(perm)

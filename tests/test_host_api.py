@@ -185,3 +185,34 @@ def test_host_go_rules_and_factory():
     assert s.isTerminal() and s.getGameResult() in (az.GameResult.WIN_PLAYER1, az.GameResult.WIN_PLAYER2)
     with pytest.raises(Exception):
         az.createGameState(az.GameType.CHESS)
+
+
+def test_training_example_json_matches_python_mirror_and_nlohmann_layout():
+    """TrainingExample::toJson (dataset.cpp:16-33): j.dump() -- compact, keys sorted, NaN as null."""
+    import az_amd
+    e = az.TrainingExample()
+    e.state = [[[0.0, 1.0], [0.5, 0.1]], [[1.0, 0.0], [0.0, 0.25]]]
+    e.policy = [0.1, float("nan"), 1e-05]
+    e.value = -0.0
+    txt = e.toJson()
+    assert txt == ('{"policy":[0.10000000149011612,null,9.999999747378752e-06],'
+                   '"state":[[[0.0,1.0],[0.5,0.10000000149011612]],[[1.0,0.0],[0.0,0.25]]],"value":-0.0}')
+    py = az_amd.TrainingExample(np.array(e.state, np.float32), np.array(e.policy, np.float32), e.value)
+    assert py.toJson() == txt
+    back = az.TrainingExample.fromJson(txt)
+    assert back.state == e.state and back.policy[0] == e.policy[0] and math.isnan(back.policy[1])
+    assert math.copysign(1.0, back.value) == -1.0
+
+
+def test_dataset_without_gpu_fails_loudly():
+    ds = az.Dataset()
+    assert ds.size() == 0
+    r = az.GameRecord(az.GameType.GOMOKU, 9)
+    r.addMove(40, [1.0], 0.0, 0)
+    ds.addGameRecord(r)
+    with pytest.raises(RuntimeError, match="HIP|device"):
+        ds.extractExamples(True)
+    chess = az.Dataset()
+    chess.addGameRecord(az.GameRecord(az.GameType.CHESS, 8))
+    with pytest.raises(Exception, match="Chess"):
+        chess.extractExamples(True)
