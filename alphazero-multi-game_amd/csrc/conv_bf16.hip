@@ -1247,17 +1247,26 @@ __device__ __forceinline__ void static_for(Fn&& f) {
 
 // Board geometry of conv3x3_v6 for an HB x HB board: outputs on an HB x (HB+2) grid (two dead
 // columns) so tap (dy, dx) of 16 consecutive outputs is 16 consecutive rows of the zero-padded
-// (HB+2)^2 halo; a board's grid is padded to 128 / 256 / 512 rows and a 512-row block tile holds
-// BOARDS boards (15: 2 boards, 88% live rows; 19: 1 board, 71%; 8 / 9: 4 boards; 13: 2 boards).
+// (HB+2)^2 halo.
+//  * 15x15 (FLAT = false): a board's grid is padded to 256 rows and a 512-row block tile holds two
+//    boards (88% live rows).
+//  * other boards (FLAT = true): boards are laid end to end, S = (HB+1)(HB+2) grid rows each -- the
+//    bottom zero row of the halo of board b is the top zero row of board b+1, so output row Q of
+//    the flattened sequence reads halo row Q + dy*WG + dx for every board at once -- and a tile is
+//    any 512 consecutive rows, which may span boards (live rows 19x19: 86% instead of 71% with one
+//    board per tile; 13x13 80% / 66%; 9x9 74% / 63%; 8x8 71% / 50%).
 template <int HB>
 struct G8Geom {
+    static constexpr bool FLAT = HB != 15;
     static constexpr int WG = HB + 2;                       // grid / halo row width
     static constexpr int HALO = WG * WG;                    // halo rows per board
-    static constexpr int HROWS = (HALO + 63) / 64 * 64;     // padded to whole 1 KiB DMA pieces
+    static constexpr int S = (HB + 1) * WG;                 // FLAT: grid rows per board
+    static constexpr int TROWS = 512 + 2 * WG + 2;          // FLAT: halo rows one 512-row tile reads
+    static constexpr int HROWS = ((FLAT ? TROWS : HALO) + 63) / 64 * 64;   // whole 1 KiB DMA pieces
     static constexpr int HP = HROWS / 64;                   // pieces per (board, 8-channel group)
     static constexpr int OUTR = HB * WG;                    // grid rows per board
-    static constexpr int OUTP = OUTR <= 128 ? 128 : OUTR <= 256 ? 256 : 512;
-    static constexpr int BOARDS = 512 / OUTP;
+    static constexpr int OUTP = FLAT ? 512 : OUTR <= 128 ? 128 : OUTR <= 256 ? 256 : 512;
+    static constexpr int BOARDS = 512 / OUTP;               // FLAT: one flattened tile
     static constexpr int HW = HB * HB;
     static_assert(OUTR <= 512, "board too large for a 512-row tile");
 };
@@ -1295,8 +1304,8 @@ __global__ __launch_bounds__(512, 1) void conv3x3_v6(ConvBf16Args p) {
     const int nb = slot % nsplit, pair = (slot / nsplit) * 8 + xcd;
     const int n0 = nb * BNT;
     const int nboards = p.m_limit ? *p.m_limit : p.M / (p.H * p.W);
-    const int b0 = pair * BOARDS;
-    if (b0 >= nboards) return;
+    const int b0 = pair * BOARDS;                        // FLAT: pair is the tile index
+    if (GM::FLAT ? pair * 512 >= nboards * GM::S : b0 >= nboards) return;
     float* sbias = reinterpret_cast<float*>(lds + LDS_BIAS);
     if (tid < BNT) sbias[tid] = p.bias[n0 + tid];
     const int C = p.C, GI = C / 8, GO = p.N / 8;
@@ -1336,9 +1345,20 @@ __global__ __launch_bounds__(512, 1) void conv3x3_v6(ConvBf16Args p) {
         const int q = wave + 8 * j;
         const int rb = q % GM::HP, g = (q / GM::HP) % KG, bd = q / (GM::HP * KG);
         const int hr = rb * 64 + lane;
-        const int Y = hr / WG, X = hr - Y * WG;
-        const int b = b0 + bd;
-        const bool ok = hr < GM::HALO && Y >= 1 && Y <= HB && X >= 1 && X <= HB && b < nboards;
+        int Y, X, b;
+        bool in;
+        if constexpr (GM::FLAT) {                          // flattened halo row -> (board, Y, X)
+            const int h = pair * 512 + hr;
+            b = h / GM::S;
+            const int rr = h - b * GM::S;
+            Y = rr / WG; X = rr - Y * WG;
+            in = hr < GM::TROWS;
+        } else {
+            Y = hr / WG; X = hr - Y * WG;
+            b = b0 + bd;
+            in = hr < GM::HALO;
+        }
+        const bool ok = in && Y >= 1 && Y <= HB && X >= 1 && X <= HB && b < nboards;
         a_vo[j] = ok ? (uint32_t)((((size_t)b * GI + g) * HW + (Y - 1) * HB + (X - 1)) * 16) : PAD;
         a_off[j] = bd * A_PLANE + g * (GM::HROWS * 16) + rb * 1024;
     }
@@ -1478,15 +1498,38 @@ __global__ __launch_bounds__(512, 1) void conv3x3_v6(ConvBf16Args p) {
     V4_STAMP(1);
 
     // epilogue (as v5): two 64-column passes over the block's boards, staged [BOARDS][OUTP][68] fp32
-    constexpr int ITEMS = BOARDS * (SC / 8) * HW;
+    constexpr int ITEMS = GM::FLAT ? 512 * (SC / 8) : BOARDS * (SC / 8) * HW;
     constexpr int ITER = (ITEMS + 511) / 512;
     float* ep = reinterpret_cast<float*>(lds);
     struct Res { uint4 h; uint2 q; };
+    // item v -> (board, pixel, 8-channel group gl, staged row); live: a real output of this tile
+    struct Item { int b, pix, gl, srow; bool live; };
+    auto item = [&](int v) {
+        Item it;
+        if constexpr (GM::FLAT) {                          // v = gl * 512 + tile row (rows contiguous)
+            const int row = v & 511;
+            it.gl = v >> 9;
+            const int h = pair * 512 + row;
+            it.b = h / GM::S;
+            const int rr = h - it.b * GM::S, y = rr / WG, x = rr - y * WG;
+            it.pix = y * HB + x;
+            it.srow = row;
+            it.live = y < HB && x < HB && it.b < nboards;
+        } else {
+            it.pix = v % HW;
+            const int t = v / HW, bd = t / 8;
+            it.gl = t % 8;
+            it.b = b0 + bd;
+            it.srow = bd * OUTP + (it.pix / HB) * WG + it.pix % HB;
+            it.live = v < ITEMS && it.b < nboards;
+        }
+        return it;
+    };
     auto fetch = [&](int pp, int v) {
         Res rr{};
-        const int pix = v % HW, t = v / HW, gl = t % 8, bd = t / 8;
-        const int b = b0 + bd;
-        if (v < ITEMS && b < nboards) {
+        const Item it = item(v);
+        const int pix = it.pix, gl = it.gl, b = it.b;
+        if (it.live) {
             const int n = n0 + (gl / 4) * 64 + pp * 32 + (gl % 4) * 8;
             const size_t e = (((size_t)b * GO + n / 8) * HW + pix) * 8;
             rr.h = *reinterpret_cast<const uint4*>(p.Rhi + e);
@@ -1519,11 +1562,11 @@ __global__ __launch_bounds__(512, 1) void conv3x3_v6(ConvBf16Args p) {
 #pragma unroll
         for (int k = 0; k < ITER; ++k) {
             const int v = tid + 512 * k;
-            const int pix = v % HW, t = v / HW, gl = t % 8, bd = t / 8;
-            const int b = b0 + bd;
-            if (v < ITEMS && b < nboards) {
+            const Item it = item(v);
+            const int pix = it.pix, gl = it.gl, b = it.b;
+            if (it.live) {
                 const int nl = (gl / 4) * 64 + pp * 32 + (gl % 4) * 8, n = n0 + nl;
-                const float* src = ep + (bd * OUTP + (pix / HB) * WG + pix % HB) * SLD + gl * 8;
+                const float* src = ep + it.srow * SLD + gl * 8;
                 const float4 x0 = *reinterpret_cast<const float4*>(src);
                 const float4 x1 = *reinterpret_cast<const float4*>(src + 4);
                 const float4 c0v = *reinterpret_cast<const float4*>(sbias + nl);
@@ -1652,7 +1695,8 @@ extern "C" int az_diag_set_conv_flags(int flags) { g_conv_flags = flags; return 
 template <int HB>
 static void v6_launch(const ConvBf16Args& a, int mode, hipStream_t st) {
     typedef G8Geom<HB> GM;
-    const int groups = (a.M / GM::HW + GM::BOARDS - 1) / GM::BOARDS;
+    const int boards = a.M / GM::HW;
+    const int groups = GM::FLAT ? (boards * GM::S + 511) / 512 : (boards + GM::BOARDS - 1) / GM::BOARDS;
     const int grid = (groups + 7) / 8 * 8 * (a.N / 128);   // XCD-aware group/half mapping: whole groups of 8
     if (mode == 2) hipLaunchKernelGGL((conv3x3_v6<2, HB>), dim3(grid), dim3(512), 0, st, a);
     else hipLaunchKernelGGL((conv3x3_v6<1, HB>), dim3(grid), dim3(512), 0, st, a);

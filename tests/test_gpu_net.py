@@ -144,8 +144,8 @@ def test_gpu_c3_net_error_over_many_positions(engine, prec):
 
 
 G8_CASES = [  # (board, in_planes, action_size, channels, blocks, B): the g8 conv3x3_v6 board geometries
-    (19, 8, 362, 128, 2, 5),      # Go shape (C4: 8 planes, 361 + pass); 1 board per 512-row tile
-    (8, 111, 4672, 128, 2, 9),    # Chess shape (C5: 111 planes, 4672 moves); 4 boards per tile, v6 input conv
+    (19, 8, 362, 128, 2, 5),      # Go shape (C4: 8 planes, 361 + pass); flattened tiles span boards
+    (8, 111, 4672, 128, 2, 9),    # Chess shape (C5: 111 planes, 4672 moves); flattened tiles, v6 input conv
     (9, 11, 81, 128, 2, 6),       # Gomoku 9x9 (C1 board)
     (13, 11, 169, 256, 1, 3),     # Go 13x13
     (15, 20, 225, 128, 1, 4),     # 15x15 with > 16 planes: the input conv runs on v6 (32-channel chunks)
