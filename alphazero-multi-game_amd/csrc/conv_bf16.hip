@@ -1255,12 +1255,19 @@ __device__ __forceinline__ void static_for(Fn&& f) {
 //    the flattened sequence reads halo row Q + dy*WG + dx for every board at once -- and a tile is
 //    any 512 consecutive rows, which may span boards (live rows 19x19: 86% instead of 71% with one
 //    board per tile; 13x13 80% / 66%; 9x9 74% / 63%; 8x8 71% / 50%).
-template <int HB>
+//  * DENSE (any board): no padding rows or columns at all -- output row Q of a tile is pixel
+//    tile*512 + Q of the batch, it reads input pixel Q + (dy-1)*HB + (dx-1), i.e. halo row
+//    Q + dy*HB + dx of a halo that starts HB+1 pixels before the tile, and the taps that cross a
+//    board edge are zeroed in the A fragments (per-lane masks: x = 0 / HB-1 for dx = 0 / 2,
+//    y = 0 / HB-1 for dy = 0 / 2).  Every MFMA row is a live output (100% at every board size,
+//    the last tile aside) for 8 v_cndmask per fragment and tap.
+template <int HB, bool DENSE_ = false>
 struct G8Geom {
-    static constexpr bool FLAT = HB != 15;
-    static constexpr int WG = HB + 2;                       // grid / halo row width
-    static constexpr int HALO = WG * WG;                    // halo rows per board
-    static constexpr int S = (HB + 1) * WG;                 // FLAT: grid rows per board
+    static constexpr bool DENSE = DENSE_;
+    static constexpr bool FLAT = DENSE || HB != 15;
+    static constexpr int WG = DENSE ? HB : HB + 2;          // grid / halo row width
+    static constexpr int HALO = (HB + 2) * (HB + 2);        // halo rows per board (one board per tile)
+    static constexpr int S = DENSE ? HB * HB : (HB + 1) * WG;   // FLAT: grid rows per board
     static constexpr int TROWS = 512 + 2 * WG + 2;          // FLAT: halo rows one 512-row tile reads
     static constexpr int HROWS = ((FLAT ? TROWS : HALO) + 63) / 64 * 64;   // whole 1 KiB DMA pieces
     static constexpr int HP = HROWS / 64;                   // pieces per (board, 8-channel group)
@@ -1271,11 +1278,11 @@ struct G8Geom {
     static_assert(OUTR <= 512, "board too large for a 512-row tile");
 };
 
-template <int MODE, int HB = 15>
+template <int MODE, int HB = 15, bool DENSE = false, int DV = 0>   // DV: timing-only variants (AZ_V6_DIAG)
 __global__ __launch_bounds__(512, 1) void conv3x3_v6(ConvBf16Args p) {
     static_assert(MODE == 1 || MODE == 2, "v6: single-plane modes");
     typedef Half16<MODE> H16;
-    typedef G8Geom<HB> GM;
+    typedef G8Geom<HB, DENSE> GM;
     constexpr int BNT = 128, BOARDS = GM::BOARDS, KG = 4, WG = GM::WG, HW = GM::HW, OUTP = GM::OUTP;
     constexpr int A_PLANE = KG * GM::HROWS * 16;         // one board, 32 channels: [4 groups][halo rows][16 B]
     constexpr int A_BUF = BOARDS * A_PLANE;              // 40 KB at 15x15
@@ -1306,6 +1313,12 @@ __global__ __launch_bounds__(512, 1) void conv3x3_v6(ConvBf16Args p) {
     const int nboards = p.m_limit ? *p.m_limit : p.M / (p.H * p.W);
     const int b0 = pair * BOARDS;                        // FLAT: pair is the tile index
     if (GM::FLAT ? pair * 512 >= nboards * GM::S : b0 >= nboards) return;
+    V4_STAMP(3);
+#ifdef AZ_V4_STAMPS
+    if (threadIdx.x == 0 && blockIdx.x < V4_MAXBLK && p.stamp >= 0 && p.stamp < V4_SLOTS)
+        g_v4_stamps[((size_t)p.stamp * V4_MAXBLK + blockIdx.x) * 8 + 7] =
+            (unsigned long long)__builtin_amdgcn_s_getreg(0xF804) | ((unsigned long long)__builtin_amdgcn_s_getreg(0xF814) << 32);
+#endif
     float* sbias = reinterpret_cast<float*>(lds + LDS_BIAS);
     if (tid < BNT) sbias[tid] = p.bias[n0 + tid];
     const int C = p.C, GI = C / 8, GO = p.N / 8;
@@ -1347,7 +1360,13 @@ __global__ __launch_bounds__(512, 1) void conv3x3_v6(ConvBf16Args p) {
         const int hr = rb * 64 + lane;
         int Y, X, b;
         bool in;
-        if constexpr (GM::FLAT) {                          // flattened halo row -> (board, Y, X)
+        if constexpr (GM::DENSE) {                         // halo row -> pixel pair*512 - HB - 1 + hr
+            const int gpx = pair * 512 - (HB + 1) + hr;
+            b = gpx >= 0 ? gpx / HW : -1;
+            const int pix = gpx - b * HW;
+            Y = pix / HB + 1; X = pix - (Y - 1) * HB + 1;
+            in = hr < GM::TROWS && gpx >= 0;
+        } else if constexpr (GM::FLAT) {                   // flattened halo row -> (board, Y, X)
             const int h = pair * 512 + hr;
             b = h / GM::S;
             const int rr = h - b * GM::S;
@@ -1405,6 +1424,17 @@ __global__ __launch_bounds__(512, 1) void conv3x3_v6(ConvBf16Args p) {
     const int l16 = lane & 15, lg = lane >> 4;
     const uint32_t a_lane = lds_addr(abuf) + bd_w * A_PLANE + lg * (GM::HROWS * 16) + (q0 + l16) * 16;
     const uint32_t b_lane = lds_addr(bbuf) + lg * (BNT * 16) + (wn * 64 + l16) * 16;
+    // DENSE: board-edge bits of the output row behind each of the lane's 8 A fragments,
+    // 4 bits per fragment f: x = 0, x = HB-1, y = 0, y = HB-1
+    uint32_t mbits = 0;
+    if constexpr (GM::DENSE) {
+#pragma unroll
+        for (int f = 0; f < 8; ++f) {
+            const int gq = pair * 512 + q0 + f * 16 + l16;
+            const int pix = gq % HW, y = pix / HB, x = pix - y * HB;
+            mbits |= ((x == 0 ? 1u : 0u) | (x == HB - 1 ? 2u : 0u) | (y == 0 ? 4u : 0u) | (y == HB - 1 ? 8u : 0u)) << (4 * f);
+        }
+    }
     for (int s = 0; s < NS; ++s) {
         const int c = s / 3, r = s - 3 * c;
         // retire B(s) (and A(c) at r == 0): pieces issued after B(s) may stay in flight
@@ -1416,7 +1446,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_v6(ConvBf16Args p) {
         else allow = issued(s - 1) + (s >= 2 && ((s - 2) % 3) == 0 && (s - 2) / 3 + 1 < NCH ? PA : 0);
         wait_vm(allow);
         __builtin_amdgcn_sched_barrier(0);
-        __builtin_amdgcn_s_barrier();
+        if constexpr (!(DV & 2)) __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_sched_barrier(0);
         const uint32_t ab = a_lane + (c & 1) * A_BUF;
         const uint32_t bb = b_lane + (s % 3) * B_STAGE;
@@ -1432,6 +1462,16 @@ __global__ __launch_bounds__(512, 1) void conv3x3_v6(ConvBf16Args p) {
         };
         frag alo[4], ahi[4], bc[4], bn[4];
         const uint32_t abr = ab + r * (WG * 16);       // tap row r: halo rows shifted by WG r
+        // DENSE: zero the A rows whose tap (r, t) crosses a board edge
+        const uint32_t rtest = r == 0 ? 4u : r == 2 ? 8u : 0u;
+        auto maskA = [&](frag (&a)[4], int half, int t) {
+            if constexpr (GM::DENSE) {
+                const uint32_t test = rtest | (t == 0 ? 1u : t == 2 ? 2u : 0u);
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    if (mbits & (test << (4 * (half * 4 + i)))) a[i] = frag{};
+            }
+        };
         // fragment reads with compile-time LDS offsets (one base VGPR per operand)
         auto loadA = [&](frag (&a)[4], auto tc, auto hc) {
             constexpr int t = decltype(tc)::value, half = decltype(hc)::value;
@@ -1461,7 +1501,9 @@ __global__ __launch_bounds__(512, 1) void conv3x3_v6(ConvBf16Args p) {
                 }
 #pragma unroll
                 for (int j = 0; j < FN; ++j) {
-                    if constexpr (MODE == 2)
+                    if constexpr (DV & 1)
+                        asm volatile("" : "+v"(acc[half * 4 + i][j]) : "v"(a[i]), "v"(b[j]));
+                    else if constexpr (MODE == 2)
                         acc[half * 4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[i], b[j], acc[half * 4 + i][j], 0, 0, 0);
                     else
                         acc[half * 4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[half * 4 + i][j], 0, 0, 0);
@@ -1474,23 +1516,29 @@ __global__ __launch_bounds__(512, 1) void conv3x3_v6(ConvBf16Args p) {
         // tap 0
         loadB(bn, I1{});
         AZ_LGKM_WAIT(4, alo); AZ_LGKM_WAIT(4, bc);
+        maskA(alo, 0, 0);
         mma(alo, bc, 0, 0);
         loadA(alo, I1{}, I0{});
         AZ_LGKM_WAIT(8, ahi);
+        maskA(ahi, 1, 0);
         mma(ahi, bc, 1, 0);
         loadA(ahi, I1{}, I1{});
         // tap 1 (bn holds B(1))
         loadB(bc, I2{});
         AZ_LGKM_WAIT(8, alo); AZ_LGKM_WAIT(8, bn);
+        maskA(alo, 0, 1);
         mma(alo, bn, 0, 1);
         loadA(alo, I2{}, I0{});
         AZ_LGKM_WAIT(8, ahi);
+        maskA(ahi, 1, 1);
         mma(ahi, bn, 1, 1);
         loadA(ahi, I2{}, I1{});
         // tap 2 (bc holds B(2))
         AZ_LGKM_WAIT(4, alo); AZ_LGKM_WAIT(4, bc);
+        maskA(alo, 0, 2);
         mma(alo, bc, 0, 2);
         AZ_LGKM_WAIT(0, ahi);
+        maskA(ahi, 1, 2);
         mma(ahi, bc, 1, 2);
     }
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
@@ -1506,7 +1554,15 @@ __global__ __launch_bounds__(512, 1) void conv3x3_v6(ConvBf16Args p) {
     struct Item { int b, pix, gl, srow; bool live; };
     auto item = [&](int v) {
         Item it;
-        if constexpr (GM::FLAT) {                          // v = gl * 512 + tile row (rows contiguous)
+        if constexpr (GM::DENSE) {                         // v = gl * 512 + tile row = pixel pair*512 + row
+            const int row = v & 511;
+            it.gl = v >> 9;
+            const int h = pair * 512 + row;
+            it.b = h / HW;
+            it.pix = h - it.b * HW;
+            it.srow = row;
+            it.live = it.b < nboards;
+        } else if constexpr (GM::FLAT) {                   // v = gl * 512 + tile row (rows contiguous)
             const int row = v & 511;
             it.gl = v >> 9;
             const int h = pair * 512 + row;
@@ -1525,11 +1581,16 @@ __global__ __launch_bounds__(512, 1) void conv3x3_v6(ConvBf16Args p) {
         }
         return it;
     };
+#ifdef AZ_V6_DIAG
+    const bool d_noload = (p.flags >> 20) & 1, d_nostore = (p.flags >> 21) & 1;   // timing-only epilogue variants
+#else
+    constexpr bool d_noload = false, d_nostore = false;
+#endif
     auto fetch = [&](int pp, int v) {
         Res rr{};
         const Item it = item(v);
         const int pix = it.pix, gl = it.gl, b = it.b;
-        if (it.live) {
+        if (it.live && !d_noload) {
             const int n = n0 + (gl / 4) * 64 + pp * 32 + (gl % 4) * 8;
             const size_t e = (((size_t)b * GO + n / 8) * HW + pix) * 8;
             rr.h = *reinterpret_cast<const uint4*>(p.Rhi + e);
@@ -1584,11 +1645,17 @@ __global__ __launch_bounds__(512, 1) void conv3x3_v6(ConvBf16Args p) {
                 uint16_t oh[8];
                 int8_t oq[8];
 #pragma unroll
-                for (int e = 0; e < 8; ++e) {
+                for (int e = 0; e < 8; ++e)
                     if (p.relu) o[e] = o[e] > 0.0f ? o[e] : 0.0f;
-                    H16::split(o[e], oh[e], oq[e]);
+                if (p.Cq) {                                // residual-stream output: 16-bit + int8 remainder
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) H16::split(o[e], oh[e], oq[e]);
+                } else {
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) oh[e] = H16::from_f(o[e]);
                 }
                 const size_t e = (((size_t)b * GO + n / 8) * HW + pix) * 8;
+                if (d_nostore && o[0] != 1234.5f) continue;
                 *reinterpret_cast<uint4*>(p.Chi + e) = *reinterpret_cast<const uint4*>(oh);
                 if (p.Cq) *reinterpret_cast<uint2*>(p.Cq + e) = *reinterpret_cast<const uint2*>(oq);
                 if (p.Cf) {
@@ -1692,14 +1759,34 @@ static int g_conv_flags = 4;   // bit 2: v6 (16x16x32) at 15x15 (other boards al
 // fragment prefetch and a mid-row barrier variant measured 1.5-2% slower)
 extern "C" int az_diag_set_conv_flags(int flags) { g_conv_flags = flags; return 0; }
 
-template <int HB>
-static void v6_launch(const ConvBf16Args& a, int mode, hipStream_t st) {
-    typedef G8Geom<HB> GM;
+template <int HB, bool DENSE>
+static void v6_launch_g(const ConvBf16Args& a, int mode, hipStream_t st) {
+    typedef G8Geom<HB, DENSE> GM;
     const int boards = a.M / GM::HW;
     const int groups = GM::FLAT ? (boards * GM::S + 511) / 512 : (boards + GM::BOARDS - 1) / GM::BOARDS;
     const int grid = (groups + 7) / 8 * 8 * (a.N / 128);   // XCD-aware group/half mapping: whole groups of 8
-    if (mode == 2) hipLaunchKernelGGL((conv3x3_v6<2, HB>), dim3(grid), dim3(512), 0, st, a);
-    else hipLaunchKernelGGL((conv3x3_v6<1, HB>), dim3(grid), dim3(512), 0, st, a);
+#ifdef AZ_V6_DIAG
+    if (HB == 15 && !DENSE && mode == 2 && (a.flags >> 24) & 3) {
+        switch ((a.flags >> 24) & 3) {
+            case 1: hipLaunchKernelGGL((conv3x3_v6<2, 15, false, 1>), dim3(grid), dim3(512), 0, st, a); return;
+            case 2: hipLaunchKernelGGL((conv3x3_v6<2, 15, false, 2>), dim3(grid), dim3(512), 0, st, a); return;
+            default: hipLaunchKernelGGL((conv3x3_v6<2, 15, false, 3>), dim3(grid), dim3(512), 0, st, a); return;
+        }
+    }
+#endif
+    if (mode == 2) hipLaunchKernelGGL((conv3x3_v6<2, HB, DENSE>), dim3(grid), dim3(512), 0, st, a);
+    else hipLaunchKernelGGL((conv3x3_v6<1, HB, DENSE>), dim3(grid), dim3(512), 0, st, a);
+}
+// DENSE is the default for every board but 15x15, where two padded boards fill a 512-row tile
+// at 88% and B = 2048 comes to exactly 8 rounds of 256 blocks (dense: 1800 blocks, still 8
+// rounds, plus the masking).  Measured at B = 2048 (tools/net_bench.py --flags 0x4,0xc): dense
+// 19x19 -3.1%, 13x13 -4.0%, 9x9 -14%, 8x8 (C5) -20% trunk time; 15x15 +8.7%.
+// Flag 8 forces DENSE, flag 0x4000000 the padded geometry (A/B measurement).
+template <int HB>
+static void v6_launch(const ConvBf16Args& a, int mode, hipStream_t st) {
+    const bool dense = (a.flags & 8) || (HB != 15 && !(a.flags & 0x4000000));
+    if (dense) v6_launch_g<HB, true>(a, mode, st);
+    else v6_launch_g<HB, false>(a, mode, st);
 }
 
 int az_conv_g8_launch(const ConvBf16Args& a_in, int mode, hipStream_t st) {

@@ -11,3 +11,7 @@ timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.
 tail -1 $O/smoke.log
 timeout -k 10 600 python bench.py > $O/bench.json 2> $O/bench.err || { echo BENCH_FAIL; tail -20 $O/bench.err; exit 1; }
 cat $O/bench.json
+if [ "${WITH_GO:-0}" = 1 ]; then
+  timeout -k 10 600 python bench.py --game go --steps 1 --warmup 1 > $O/bench_go.json 2> $O/bench_go.err || { echo GO_BENCH_FAIL; tail -20 $O/bench_go.err; exit 1; }
+  cat $O/bench_go.json
+fi
