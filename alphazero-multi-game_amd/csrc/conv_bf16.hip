@@ -1278,6 +1278,8 @@ struct G8Geom {
     static_assert(OUTR <= 512, "board too large for a 512-row tile");
 };
 
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
 template <int MODE, int HB = 15, bool DENSE = false, int DV = 0>   // DV: timing-only variants (AZ_V6_DIAG)
 __global__ __launch_bounds__(512, 1) void conv3x3_v6(ConvBf16Args p) {
     static_assert(MODE == 1 || MODE == 2, "v6: single-plane modes");
@@ -1593,8 +1595,13 @@ __global__ __launch_bounds__(512, 1) void conv3x3_v6(ConvBf16Args p) {
         if (it.live && !d_noload) {
             const int n = n0 + (gl / 4) * 64 + pp * 32 + (gl % 4) * 8;
             const size_t e = (((size_t)b * GO + n / 8) * HW + pix) * 8;
-            rr.h = *reinterpret_cast<const uint4*>(p.Rhi + e);
-            rr.q = *reinterpret_cast<const uint2*>(p.Rq + e);
+            // streaming (nt) loads: the residual is read once (-2% trunk time at C3)
+            const __amdgpu_buffer_rsrc_t rh = __builtin_amdgcn_make_buffer_rsrc((void*)p.Rhi, (short)0, 0x7fffffff, 0x00020000);
+            const __amdgpu_buffer_rsrc_t rqq = __builtin_amdgcn_make_buffer_rsrc((void*)p.Rq, (short)0, 0x7fffffff, 0x00020000);
+            const u32x4_t h = __builtin_amdgcn_raw_buffer_load_b128(rh, (int)(e * 2), 0, 2);
+            const u32x2_t q = __builtin_amdgcn_raw_buffer_load_b64(rqq, (int)e, 0, 2);
+            __builtin_memcpy(&rr.h, &h, 16);
+            __builtin_memcpy(&rr.q, &q, 8);
         }
         return rr;
     };
@@ -1656,8 +1663,14 @@ __global__ __launch_bounds__(512, 1) void conv3x3_v6(ConvBf16Args p) {
                 }
                 const size_t e = (((size_t)b * GO + n / 8) * HW + pix) * 8;
                 if (d_nostore && o[0] != 1234.5f) continue;
-                *reinterpret_cast<uint4*>(p.Chi + e) = *reinterpret_cast<const uint4*>(oh);
-                if (p.Cq) *reinterpret_cast<uint2*>(p.Cq + e) = *reinterpret_cast<const uint2*>(oq);
+                {                                          // streaming (nt) output stores (-1%)
+                    u32x4_t h; __builtin_memcpy(&h, oh, 16);
+                    asm volatile("global_store_dwordx4 %0, %1, off nt" ::"v"(p.Chi + e), "v"(h) : "memory");
+                    if (p.Cq) {
+                        u32x2_t q; __builtin_memcpy(&q, oq, 8);
+                        asm volatile("global_store_dwordx2 %0, %1, off nt" ::"v"(p.Cq + e), "v"(q) : "memory");
+                    }
+                }
                 if (p.Cf) {
                     float* cf = p.Cf + ((size_t)b * HW + pix) * p.N + n;
                     *reinterpret_cast<float4*>(cf) = make_float4(o[0], o[1], o[2], o[3]);
@@ -1708,32 +1721,51 @@ void az_launch_to_g8(const float* in, uint16_t* hi, int8_t* q, int C, int HW, co
 // adaptive_avg_pool2d(x, (P, P)) of an H x H g8 trunk output (16-bit + int8 remainder) -> fp32 NHWC
 // [B][P*P][C]; one thread per (board, 8-channel group, output cell), same summation order as
 // k_adaptive_pool (rows, then columns; sum / kh / kw)
+// Adaptive average pool of the g8 trunk output (16-bit + int8 remainder) to P x P, fp32
+// [B][P*P][C] for the head 1x1 convs.  One block per (board, 32-channel slice): the slice's
+// H*W x 32 values are read once, coalesced per 8-channel group, joined to fp32 in LDS (row stride
+// 36 floats: conflict-free 16-byte writes; H*W*144 B of dynamic LDS), then every output sums its
+// window from LDS in the same order as before (y-major, then x; / kh / kw).
 template <int MODE>
-__global__ void k_pool_g8(const uint16_t* hi, const int8_t* q, float* out, int C, int H, int P, const int* m_limit, int maxB) {
-    const int G = C / 8, PP = P * P;
+__global__ __launch_bounds__(256) void k_pool_g8(const uint16_t* hi, const int8_t* q, float* out, int C, int H, int P,
+                                                 const int* m_limit, int maxB) {
+    constexpr int SL = 36;                              // LDS row stride (floats) for 32 channels
+    extern __shared__ __attribute__((aligned(16))) float f[];
+    const int G = C / 8, HW = H * H, PP = P * P, NS = G / 4;
     const int B = m_limit ? min(*m_limit, maxB) : maxB;
-    const size_t total = (size_t)B * G * PP;
-    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
-        const int o = (int)(i % PP);
-        const size_t bg = i / PP;
-        const int g = (int)(bg % G);
-        const size_t b = bg / G;
-        const int oy = o / P, ox = o % P;
+    const int b = blockIdx.x / NS, sl = blockIdx.x - b * NS;
+    if (b >= B) return;
+    for (int idx = threadIdx.x; idx < 4 * HW; idx += 256) {
+        const int gl = idx / HW, pix = idx - gl * HW;
+        const size_t e = ((size_t)(b * G + sl * 4 + gl) * HW + pix) * 8;
+        uint16_t h[8];
+        int8_t r[8];
+        *reinterpret_cast<uint4*>(h) = *reinterpret_cast<const uint4*>(hi + e);
+        *reinterpret_cast<uint2*>(r) = *reinterpret_cast<const uint2*>(q + e);
+        float v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = Half16<MODE>::join(h[k], r[k]);
+        float* d = f + pix * SL + gl * 8;
+        *reinterpret_cast<float4*>(d) = make_float4(v[0], v[1], v[2], v[3]);
+        *reinterpret_cast<float4*>(d + 4) = make_float4(v[4], v[5], v[6], v[7]);
+    }
+    __syncthreads();
+    const int c8 = (threadIdx.x & 3) * 8;
+    for (int o = threadIdx.x >> 2; o < PP; o += 64) {
+        const int oy = o / P, ox = o - oy * P;
         const int y0 = (oy * H) / P, y1 = ((oy + 1) * H + P - 1) / P;
         const int x0 = (ox * H) / P, x1 = ((ox + 1) * H + P - 1) / P;
         float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         for (int y = y0; y < y1; ++y)
             for (int x = x0; x < x1; ++x) {
-                const size_t e = ((b * G + g) * H * H + y * H + x) * 8;
-                uint16_t h[8];
-                int8_t r[8];
-                *reinterpret_cast<uint4*>(h) = *reinterpret_cast<const uint4*>(hi + e);
-                *reinterpret_cast<uint2*>(r) = *reinterpret_cast<const uint2*>(q + e);
-#pragma unroll
-                for (int k = 0; k < 8; ++k) s[k] += Half16<MODE>::join(h[k], r[k]);
+                const float* src = f + (y * H + x) * SL + c8;
+                const float4 t0 = *reinterpret_cast<const float4*>(src);
+                const float4 t1 = *reinterpret_cast<const float4*>(src + 4);
+                s[0] += t0.x; s[1] += t0.y; s[2] += t0.z; s[3] += t0.w;
+                s[4] += t1.x; s[5] += t1.y; s[6] += t1.z; s[7] += t1.w;
             }
         const float kh = (float)(y1 - y0), kw = (float)(x1 - x0);
-        float* dst = out + (b * PP + o) * C + g * 8;
+        float* dst = out + ((size_t)b * PP + o) * C + sl * 32 + c8;
         *reinterpret_cast<float4*>(dst) = make_float4(s[0] / kh / kw, s[1] / kh / kw, s[2] / kh / kw, s[3] / kh / kw);
         *reinterpret_cast<float4*>(dst + 4) = make_float4(s[4] / kh / kw, s[5] / kh / kw, s[6] / kh / kw, s[7] / kh / kw);
     }
@@ -1741,8 +1773,10 @@ __global__ void k_pool_g8(const uint16_t* hi, const int8_t* q, float* out, int C
 
 void az_launch_pool_g8(const uint16_t* hi, const int8_t* q, float* out, int B, int C, int H, int P, const int* m_limit,
                        int mode, hipStream_t st) {
-    if (mode == 2) hipLaunchKernelGGL(k_pool_g8<2>, dim3(4096), dim3(256), 0, st, hi, q, out, C, H, P, m_limit, B);
-    else hipLaunchKernelGGL(k_pool_g8<1>, dim3(4096), dim3(256), 0, st, hi, q, out, C, H, P, m_limit, B);
+    const int grid = B * (C / 32);
+    const size_t lds = (size_t)H * H * 36 * sizeof(float);
+    if (mode == 2) hipLaunchKernelGGL(k_pool_g8<2>, dim3(grid), dim3(256), lds, st, hi, q, out, C, H, P, m_limit, B);
+    else hipLaunchKernelGGL(k_pool_g8<1>, dim3(grid), dim3(256), lds, st, hi, q, out, C, H, P, m_limit, B);
 }
 
 // true when the g8 trunk (conv3x3_v5 at 15x15 / conv3x3_v6) handles this shape: square boards with a
