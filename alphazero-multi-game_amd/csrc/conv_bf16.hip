@@ -920,21 +920,22 @@ struct Half16 {                                         // MODE 2: fp16, MODE 1:
         u += 0x7fffu + ((u >> 16) & 1u);
         return (uint16_t)(u >> 16);
     }
-    // x -> (h, q): h = round(x), q = round((x - h) / u * 254) with u = 2^(frexp_exp(h) - MANT), the
-    // spacing of 16-bit values at h's binade (MANT = 11 fp16, 8 bf16); |q| <= 127 (clamped at
-    // subnormal h, where |x - h| < 2^-24 anyway).  A handful of VALU ops per element.
+    // x -> (h, q): h = round(x) in 16 bits, q = the next 8 bits of x below h's precision, taken from
+    // the fp32 bit patterns: d = bits(x) - bits(float(h)) counts fp32 ulps (x and h share the sign,
+    // and the patterns are monotone across binades), q = round(d / 2^SH) clamped to +-127, and
+    // x = bits(float(h)) + q * 2^SH reads back to 2^-20 relative (fp16: SH = 5, |d| <= 2^12;
+    // bf16: SH = 8, |d| <= 2^15).  Where h is zero or subnormal the clamp bounds the absolute
+    // error by the 16-bit subnormal spacing.  Integer adds and shifts: 3 VALU ops to join.
     static constexpr int MANT = MODE == 2 ? 11 : 8;
+    static constexpr int SH = 16 - MANT;
     __device__ static void split(float x, uint16_t& h, int8_t& q) {
         h = from_f(x);
-        const float hf = to_f(h);
-        const int e = __builtin_amdgcn_frexp_expf(hf);
-        const float s = __builtin_rintf(__builtin_amdgcn_ldexpf((x - hf) * 254.0f, MANT - e));
-        q = (int8_t)(int)__builtin_amdgcn_fmed3f(s, -127.0f, 127.0f);
+        const int d = (int)(__float_as_uint(x) - __float_as_uint(to_f(h)));
+        const int r = (d + (1 << (SH - 1))) >> SH;
+        q = (int8_t)min(127, max(-127, r));
     }
     __device__ static float join(uint16_t h, int8_t q) {
-        const float hf = to_f(h);
-        const int e = __builtin_amdgcn_frexp_expf(hf);
-        return hf + __builtin_amdgcn_ldexpf((float)q * (1.0f / 254.0f), e - MANT);
+        return __uint_as_float(__float_as_uint(to_f(h)) + ((uint32_t)(int)q << SH));
     }
 };
 
