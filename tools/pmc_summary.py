@@ -49,6 +49,7 @@ def main():
     ap.add_argument("--board", type=int, default=15)
     ap.add_argument("--channels", type=int, default=256)
     ap.add_argument("--blocks", type=int, default=20)
+    ap.add_argument("--game", default="gomoku15", help="tools/net_bench.py --game of the profiled run")
     a = ap.parse_args()
     c = {}
     n = 0
@@ -62,7 +63,8 @@ def main():
     B, C, HW = a.boards, a.channels, a.board * a.board
     act = B * HW * C * 2
     out = {"kernel": name or a.kernel,
-           "workload": f"tools/net_bench.py --precision {a.precision}: C3 net forward, B={B} boards per launch "
+           "workload": f"tools/net_bench.py --game {a.game} --precision {a.precision} --batch {B}: "
+                       f"{'C3' if a.game == 'gomoku15' else a.game} net forward, B={B} boards per launch "
                        f"({2 * a.blocks} trunk launches per forward)",
            "command": "tools/pmc_conv.sh (rocprofv3 --kernel-trace --stats pass, then separate --pmc passes: "
                       "SQ/GRBM, FETCH_SIZE, WRITE_SIZE)",
