@@ -1441,12 +1441,16 @@ __global__ __launch_bounds__(512, 1) void conv3x3_v6(ConvBf16Args p) {
     for (int s = 0; s < NS; ++s) {
         const int c = s / 3, r = s - 3 * c;
         // retire B(s) (and A(c) at r == 0): pieces issued after B(s) may stay in flight
+        // halo pieces this wave really issues per chunk: issueA skips wave + 8j >= A_INS, so where
+        // A_INS is not a multiple of 8 (FLAT / DENSE tiles: 36) waves differ by one, and the vmcnt
+        // budget must count exactly or a wave could pass its wait with a weight piece in flight
+        const int pa_w = A_INS / 8 + (wave < A_INS % 8 ? 1 : 0);
         auto issued = [&](int u) {          // pieces this wave issued during tap row u
-            return (u + 2 < NS ? PB : 0) + ((u % 3) == 0 && u / 3 + 1 < NCH ? PA : 0);
+            return (u + 2 < NS ? PB : 0) + ((u % 3) == 0 && u / 3 + 1 < NCH ? pa_w : 0);
         };
         int allow;
         if (s == 0) allow = NS > 1 ? PB : 0;
-        else allow = issued(s - 1) + (s >= 2 && ((s - 2) % 3) == 0 && (s - 2) / 3 + 1 < NCH ? PA : 0);
+        else allow = issued(s - 1) + (s >= 2 && ((s - 2) % 3) == 0 && (s - 2) / 3 + 1 < NCH ? pa_w : 0);
         wait_vm(allow);
         __builtin_amdgcn_sched_barrier(0);
         if constexpr (!(DV & 2)) __builtin_amdgcn_s_barrier();
