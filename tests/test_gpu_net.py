@@ -158,6 +158,29 @@ def _rand_planes(B, ci, bs, seed, p=0.2):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("bs,ci", [(8, 32), (9, 11), (13, 8), (15, 11), (19, 8)])
+def test_gpu_g8_batch_position_independent(engine, bs, ci):
+    """g8 trunk (DENSE tiles on 8/9/13/19, where a 512-row tile spans boards and the batch's last
+    tile is partial; the padded two-board tile on 15x15): a board's output is bitwise the same
+    whatever its position in the batch, its tile-mates and the batch size."""
+    import az_amd
+    import net_oracle
+    B = 23
+    desc = az_amd.NetDesc(bs, ci, 128, 2, bs * bs, 32, 8, 256, 1, 0, az_amd.AZ_PREC_FP16, B)
+    net = az_amd.HipNeuralNetwork(engine, desc)
+    net.load_weights(net_oracle.init_blob(desc, seed=9))
+    x = _rand_planes(B, ci, bs, seed=100 + bs)
+    lo, v = net.forward(x)
+    perm = np.random.default_rng(bs).permutation(B)
+    lo2, v2 = net.forward(x[perm])
+    assert np.array_equal(lo2, lo[perm]) and np.array_equal(v2, v[perm])
+    for a, b in ((0, 1), (5, 12), (22, 23)):
+        lo3, v3 = net.forward(x[a:b])
+        assert np.array_equal(lo3, lo[a:b]) and np.array_equal(v3, v[a:b]), (a, b)
+    net.close()
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("prec", ["fp16", "bf16"])
 @pytest.mark.parametrize("case", G8_CASES, ids=[str(c) for c in G8_CASES])
 def test_gpu_g8_boards_match_fp32_reference(engine, case, prec):
