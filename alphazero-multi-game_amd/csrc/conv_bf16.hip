@@ -1657,8 +1657,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_v6(ConvBf16Args p) {
                 uint16_t oh[8];
                 int8_t oq[8];
 #pragma unroll
-                for (int e = 0; e < 8; ++e)
-                    if (p.relu) o[e] = o[e] > 0.0f ? o[e] : 0.0f;
+                for (int e = 0; e < 8; ++e) o[e] = __builtin_amdgcn_fmed3f(o[e], 0.0f, 3.0e38f);   // ReLU: every g8 conv has one
                 if (p.Cq) {                                // residual-stream output: 16-bit + int8 remainder
 #pragma unroll
                     for (int e = 0; e < 8; ++e) H16::split(o[e], oh[e], oq[e]);
@@ -1840,7 +1839,7 @@ int az_conv_g8_launch(const ConvBf16Args& a_in, int mode, hipStream_t st) {
     const bool v6_ok = a.C % 32 == 0 && a.a_tail + AZ_ACT_TAIL * 2 < ((size_t)1 << 31) &&
                        (size_t)(a.C / 32) * 4 * HW * 16 + 16 <= AZ_ACT_TAIL * 2;
     if (a.H != 15 || ((g_conv_flags & 4) && a.C % 32 == 0)) {
-        if (!v6_ok) return -1;
+        if (!v6_ok || !a.relu) return -1;                // conv3x3_v6 always applies the ReLU
         switch (a.H) {
             case 8: v6_launch<8>(a, mode, st); return 0;
             case 9: v6_launch<9>(a, mode, st); return 0;
