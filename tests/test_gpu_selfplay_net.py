@@ -67,3 +67,69 @@ def test_gpu_net_selfplay_matches_oracle_replay(prec, logged):
     assert np.abs(pol - net_oracle.softmax_policy(rl)).max() <= 1e-4
     m.close()
     net.close()
+
+
+@pytest.mark.gpu
+def test_gpu_c3_full_size_replay():
+    """The C3 workload at full size (BASELINE.json configs[2]: 2048 games, 15x15, 800 sims, the
+    20 x 256 net, fp16 trunk): the first two moves of every game, one game (id 1337, in the middle
+    of the batch) logged and replayed through the CPU restatement bit for bit; the logged network
+    outputs of a sample of its positions within 1e-4 of the fp32 reference network; size-independent
+    properties of every game's root (visit sum, probability sum, value range)."""
+    import az_amd
+    import az_oracle as O
+    import net_oracle
+    bs, sims, G, moves, logged = 15, 800, 2048, 2, 1337
+    eng = az_amd.Engine(0)
+    desc = az_amd.gomoku_net_desc(board_size=bs, channels=256, blocks=20, precision=az_amd.AZ_PREC_FP16, max_batch=G)
+    net = az_amd.HipNeuralNetwork(eng, desc)
+    blob = net_oracle.init_blob(desc, seed=1234)
+    net.load_weights(blob)
+    m = az_amd.ParallelMCTS(eng, n_games=G, board_size=bs, num_simulations=sims, evaluator=az_amd.AZ_EVAL_NET,
+                            net=net, noise_seed=42, noise_seed_stride=1)
+    cap = (sims + 2) * (moves + 1)
+    m.enableEvalLog(logged, cap)
+    m.newGames()
+    m.addDirichletNoise(0.03, 0.25)
+    dev = []
+    for ply in range(moves):
+        m.search()
+        act, val, probs, cact, nch = m.select(True, 1.0)
+        # every game: one child per empty cell, probabilities sum to 1, values within [-1, 1]
+        assert (nch == bs * bs - ply).all()
+        sums = np.array([probs[g, :nch[g]].astype(np.float64).sum() for g in range(G)])
+        assert np.abs(sums - 1.0).max() < 1e-5
+        assert (np.abs(val) <= 1.0 + 1e-6).all()
+        a, N, VL, W, P = m.rootChildren(logged)
+        assert int(np.sum(N)) >= sims - 1
+        dev.append(dict(action=int(act[logged]), value=float(val[logged]), N=N.tolist(), VL=VL.tolist(),
+                        W=W.view(np.uint32).tolist(), P=P.view(np.uint32).tolist(),
+                        probs=probs[logged, :nch[logged]].view(np.uint32).tolist()))
+        m.updateWithMove(act)
+        if ply % 2 == 0:
+            m.addDirichletNoise(0.03, 0.25)
+    pol, valv, planes = m.readEvalLog(cap)
+    assert len(pol) >= moves * sims - 10
+    k = [0]
+
+    def replay(game, x):
+        i = k[0]
+        k[0] += 1
+        assert np.array_equal(x, planes[i]), f"feature planes differ at evaluation {i}"
+        return pol[i], float(valv[i])
+
+    ref = O.play(bs=bs, sims=sims, max_moves=moves, eval_kind=O.EVAL_REPLAY, evaluator=replay,
+                 noise_seed=42 + logged)[0]
+    assert k[0] == len(pol)
+    for ply, (d, r) in enumerate(zip(dev, ref["moves"])):
+        kids = r["children"]
+        assert d["N"] == [c[1] for c in kids] and d["VL"] == [c[2] for c in kids], ply
+        assert d["W"] == [c[3] for c in kids] and d["P"] == [c[4] for c in kids], ply
+        assert d["probs"] == r["probs"] and d["action"] == r["action"], ply
+        assert np.float32(d["value"]).view(np.uint32) == r["value"], ply
+    idx = np.random.default_rng(0).choice(len(pol), 48, replace=False)
+    rl, rv = net_oracle.forward(desc, blob, planes[idx])
+    assert np.abs(valv[idx] - rv).max() <= 1e-4
+    assert np.abs(pol[idx] - net_oracle.softmax_policy(rl)).max() <= 1e-4
+    m.close()
+    net.close()
