@@ -133,3 +133,61 @@ def test_gpu_go_net_selfplay_matches_oracle_replay(engine, prec):
     sm = net_oracle.softmax_policy(rl)
     assert np.abs(sm - pol[:64]).max() <= 1e-4 and np.abs(rv - valv[:64]).max() <= 1e-4
     net.close()
+
+
+@pytest.mark.gpu
+def test_gpu_c4_full_size_replay(engine):
+    """C4 at full per-GPU size (BASELINE.json configs[3]: Go 19x19, 1024 games, 800 sims, the 20 x 256
+    net with 8 planes / 362 actions, fp16 trunk on DENSE tiles): the first two moves of every game,
+    game 777 replayed bit for bit through the CPU restatement, sampled network outputs within 1e-4
+    of the fp32 reference network, and every root's probabilities summing to 1."""
+    import az_amd
+    import az_oracle as O
+    import net_oracle
+    bs, sims, G, moves, logged = 19, 800, 1024, 2, 777
+    desc = az_amd.NetDesc(bs, 8, 256, 20, bs * bs + 1, 32, 8, 256, 1, 0, az_amd.AZ_PREC_FP16, G)
+    net = az_amd.HipNeuralNetwork(engine, desc)
+    blob = net_oracle.init_blob(desc, seed=1234)
+    net.load_weights(blob)
+    m = az_amd.ParallelMCTS(engine, n_games=G, board_size=bs, num_simulations=sims, evaluator=az_amd.AZ_EVAL_NET,
+                            net=net, noise_seed=42, noise_seed_stride=1, game=az_amd.AZ_GAME_GO)
+    cap = (sims + 2) * (moves + 1)
+    m.enableEvalLog(logged, cap)
+    m.newGames()
+    m.addDirichletNoise(0.03, 0.25)
+    dev = []
+    try:
+        for ply in range(moves):
+            m.search()
+            act, val, probs, cact, nch = m.select(True, 1.0)
+            sums = np.array([probs[g, :nch[g]].astype(np.float64).sum() for g in range(G)])
+            assert np.abs(sums - 1.0).max() < 1e-5
+            a, N, VL, W, P = m.rootChildren(logged)
+            dev.append(dict(action=int(act[logged]), N=N.tolist(), VL=VL.tolist(), W=W.view(np.uint32).tolist(),
+                            P=P.view(np.uint32).tolist(), probs=probs[logged, :nch[logged]].view(np.uint32).tolist()))
+            m.updateWithMove(act)
+            if ply % 2 == 0:
+                m.addDirichletNoise(0.03, 0.25)
+        pol, valv, planes = m.readEvalLog(cap)
+    finally:
+        m.close()
+    k = [0]
+
+    def replay(game, x):
+        i = k[0]
+        k[0] += 1
+        assert np.array_equal(x, planes[i]), f"feature planes differ at evaluation {i}"
+        return pol[i], float(valv[i])
+
+    ref = O.play(bs=bs, sims=sims, max_moves=moves, eval_kind=O.EVAL_REPLAY, evaluator=replay,
+                 noise_seed=42 + logged, game=O.GAME_GO)[0]
+    assert k[0] == len(pol)
+    for ply, (d, r) in enumerate(zip(dev, ref["moves"])):
+        kids = r["children"]
+        assert d["N"] == [c[1] for c in kids] and d["VL"] == [c[2] for c in kids], ply
+        assert d["W"] == [c[3] for c in kids] and d["P"] == [c[4] for c in kids], ply
+        assert d["probs"] == r["probs"] and d["action"] == r["action"], ply
+    idx = np.random.default_rng(1).choice(len(pol), 32, replace=False)
+    rl, rv = net_oracle.forward(desc, blob, planes[idx])
+    assert np.abs(net_oracle.softmax_policy(rl) - pol[idx]).max() <= 1e-4 and np.abs(rv - valv[idx]).max() <= 1e-4
+    net.close()
