@@ -1322,8 +1322,6 @@ __global__ __launch_bounds__(512, 1) void conv3x3_v6(ConvBf16Args p) {
         g_v4_stamps[((size_t)p.stamp * V4_MAXBLK + blockIdx.x) * 8 + 7] =
             (unsigned long long)__builtin_amdgcn_s_getreg(0xF804) | ((unsigned long long)__builtin_amdgcn_s_getreg(0xF814) << 32);
 #endif
-    float* sbias = reinterpret_cast<float*>(lds + LDS_BIAS);
-    if (tid < BNT) sbias[tid] = p.bias[n0 + tid];
     const int C = p.C, GI = C / 8, GO = p.N / 8;
     const int NCH = C / 32, NS = NCH * 3;
 
@@ -1412,7 +1410,12 @@ __global__ __launch_bounds__(512, 1) void conv3x3_v6(ConvBf16Args p) {
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
-        for (int j = 0; j < FN; ++j) acc[i][j] = f32x4v{0.0f, 0.0f, 0.0f, 0.0f};
+        for (int j = 0; j < FN; ++j) {
+            // the bias seeds the accumulators (the lane's column is wn*64 + j*16 + l16), so the
+            // epilogue adds nothing for it
+            const float bj = p.bias[n0 + wn * 64 + j * 16 + (lane & 15)];
+            acc[i][j] = f32x4v{bj, bj, bj, bj};
+        }
 
     // prologue: halo of chunk 0, weights of tap rows 0 and 1
 #pragma unroll
@@ -1642,10 +1645,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_v6(ConvBf16Args p) {
                 const float* src = ep + it.srow * SLD + gl * 8;
                 const float4 x0 = *reinterpret_cast<const float4*>(src);
                 const float4 x1 = *reinterpret_cast<const float4*>(src + 4);
-                const float4 c0v = *reinterpret_cast<const float4*>(sbias + nl);
-                const float4 c1v = *reinterpret_cast<const float4*>(sbias + nl + 4);
-                float o[8] = {x0.x + c0v.x, x0.y + c0v.y, x0.z + c0v.z, x0.w + c0v.w,
-                              x1.x + c1v.x, x1.y + c1v.y, x1.z + c1v.z, x1.w + c1v.w};
+                float o[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
                 if (p.Rhi) {
                     uint16_t hh[8];
                     int8_t qq[8];
