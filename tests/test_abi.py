@@ -46,3 +46,33 @@ def test_no_device_fails_loudly():
     with pytest.raises(az_amd.AzError, match="HIP"):
         az_amd.Engine(0)
     assert lib().az_last_error()
+
+
+def test_header_is_plain_c_and_links(tmp_path):
+    """A C99 translation unit (what a cgo / JNI / N-API binding compiles) includes the header with
+    -Wall -Werror, links against libaz_hip.so and runs: without a device az_engine_create returns
+    an error code and az_last_error names it; with one it creates and destroys an engine."""
+    import shutil
+    import subprocess
+    import az_amd._lib as L
+    cc = shutil.which("gcc")
+    if cc is None:
+        pytest.skip("no C compiler")
+    src = tmp_path / "t.c"
+    src.write_text('''#include "az_engine.h"
+#include <stdio.h>
+int main(void) {
+    az_engine* e = 0;
+    int r = az_engine_create(0, &e);
+    if (r != 0) { printf("err %d %s\\n", r, az_last_error()); return 0; }
+    az_engine_destroy(e);
+    printf("ok\\n");
+    return 0;
+}
+''')
+    exe = tmp_path / "t"
+    libdir = os.path.dirname(L.LIB_PATH)
+    subprocess.run([cc, "-std=c99", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"), str(src), "-L", libdir,
+                    "-laz_hip", "-Wl,-rpath," + libdir, "-o", str(exe)], check=True)
+    out = subprocess.run([str(exe)], check=True, capture_output=True, text=True, timeout=120).stdout
+    assert out.startswith("ok") or ("err" in out and "HIP" in out), out
