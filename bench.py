@@ -47,7 +47,7 @@ def parse():
     ap.add_argument("--blocks", type=int, default=20)
     ap.add_argument("--precision", default="fp16", choices=list(PREC),
                     help="trunk precision: fp16 = the reference useFp16 option (fp16 MFMA operands, fp32 accumulate, "
-                         "~2^-19 residual stream; C3 logits within 5.9e-5 of fp32), bf16x3 = fp32-faithful")
+                         "~2^-20 residual stream; C3 logits within ~6e-5 of fp32), bf16x3 = fp32-faithful")
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU oracle on rank 0 at N=1")
     ap.add_argument("--cpu-moves", type=int, default=1)
     ap.add_argument("--cpu-sims", type=int, default=None,
