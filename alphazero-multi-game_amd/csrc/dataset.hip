@@ -218,7 +218,7 @@ int az_dataset_extract(az_dataset* d, int n_games, const int* n_moves, const int
     t.bs = d->bs; t.A = d->A; t.NA = d->NA; t.game = d->game; t.zpiece = d->zzero;
     hipError_t he = hipEventRecord(d->ev0, d->e->stream);
     if (he == hipSuccess) {
-        hipLaunchKernelGGL(k_dataset_extract, dim3(n_games), dim3(64), 0, d->e->stream, dv, t);
+        hipLaunchKernelGGL(k_dataset_extract, dim3(n_games), dim3(AZ_DS_THREADS), 0, d->e->stream, dv, t);
         he = hipGetLastError();
     }
     if (he == hipSuccess) he = hipEventRecord(d->ev1, d->e->stream);

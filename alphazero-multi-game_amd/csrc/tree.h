@@ -65,6 +65,7 @@ struct TreeDev {
 // Records are flattened: game g owns moves [move_off[g], move_off[g+1]); move m owns policy
 // floats [pol_off[m], pol_off[m] + n_children[m]).  Pre-shuffle example e = m * K + s (s = 0
 // original, 1..7 the reference's augmentation order); dst[e] is its slot (null: e).
+constexpr int AZ_DS_THREADS = 256;   // k_dataset_extract: one 4-wave block per game record (8 waves: no faster, Go slower)
 struct DatasetDev {
     int game, bs, A, NA, C, K, n_games;
     const int* move_off;         // [n_games + 1]

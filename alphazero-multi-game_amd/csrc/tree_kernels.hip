@@ -1184,9 +1184,9 @@ __device__ __forceinline__ int sym_src(int s, int a, int bs) {
 }
 }  // namespace
 
-__global__ __launch_bounds__(64) void k_dataset_extract(DatasetDev d, TreeDev t) {
+__global__ __launch_bounds__(AZ_DS_THREADS) void k_dataset_extract(DatasetDev d, TreeDev t) {
     const int g = blockIdx.x;
-    const int lane = threadIdx.x;
+    const int lane = threadIdx.x;                 // AZ_DS_THREADS threads (4 waves) per game
     if (g >= d.n_games) return;
     const int bs = d.bs, A = d.A, C = d.C, K = d.K, NA = d.NA;
     __shared__ uint8_t board[AZ_MAXA];
@@ -1195,7 +1195,8 @@ __global__ __launch_bounds__(64) void k_dataset_extract(DatasetDev d, TreeDev t)
     __shared__ int16_t src[8][AZ_MAXA];         // sym_src tables
     __shared__ GoLds L;
     __shared__ int hist6[6];
-    for (int a = lane; a < A; a += 64) {
+    __shared__ int s_ko;
+    for (int a = lane; a < A; a += AZ_DS_THREADS) {
         board[a] = 0;
         for (int s = 0; s < K; ++s) src[s][a] = (int16_t)sym_src(s, a, bs);
     }
@@ -1213,7 +1214,7 @@ __global__ __launch_bounds__(64) void k_dataset_extract(DatasetDev d, TreeDev t)
             go_clear_marks(L, A, lane);
             go_groups(t, board, L, lane);
             const float half = (float)(bs / 2);
-            for (int a = lane; a < A; a += 64) {
+            for (int a = lane; a < A; a += AZ_DS_THREADS) {
                 const int v = board[a];
                 const int x = a % bs, y = a / bs;
                 pl[a] = v == 1 ? 1.0f : 0.0f;
@@ -1229,7 +1230,7 @@ __global__ __launch_bounds__(64) void k_dataset_extract(DatasetDev d, TreeDev t)
         } else {
             int hp[6];
             for (int i = 0; i < 6; ++i) hp[i] = (((player == 1) == ((i % 2) == 0)) ? 3 : 6) + i / 2;
-            for (int a = lane; a < A; a += 64) {
+            for (int a = lane; a < A; a += AZ_DS_THREADS) {
                 float c[11];
                 for (int k = 0; k < 11; ++k) c[k] = 0.0f;
                 const int v = board[a];
@@ -1245,19 +1246,21 @@ __global__ __launch_bounds__(64) void k_dataset_extract(DatasetDev d, TreeDev t)
         }
         const int n = d.n_children[m];
         const float* pg = d.policies + d.pol_off[m];
-        for (int k = lane; k < n; k += 64) pin[k] = pg[k];
+        for (int k = lane; k < n; k += AZ_DS_THREADS) pin[k] = pg[k];
         __syncthreads();
         const float val = player == 2 ? -gv : gv;
         for (int s = 0; s < K; ++s) {
             const long long e = (long long)m * K + s;
             const long long slot = d.dst ? d.dst[e] : e;
             float* o = d.states + slot * (long long)(C * A);
-            for (int c = 0; c < C; ++c)
-                for (int a = lane; a < A; a += 64) o[c * A + a] = pl[c * A + src[s][a]];
+            for (int ca = lane; ca < C * A; ca += AZ_DS_THREADS) {
+                const int c = ca / A, a = ca - c * A;
+                o[ca] = pl[c * A + src[s][a]];
+            }
             // policy: the reference permutes the child-order vector by board index, guarded by
             // oldIdx/newIdx < size; entries it does not overwrite keep the copied value
             float* op = d.policy + slot * (long long)NA;
-            for (int k = lane; k < NA; k += 64) {
+            for (int k = lane; k < NA; k += AZ_DS_THREADS) {
                 float v = 0.0f;
                 if (k < n) {
                     if (s == 0) {
@@ -1288,8 +1291,9 @@ __global__ __launch_bounds__(64) void k_dataset_extract(DatasetDev d, TreeDev t)
             hist6[0] = a;
         }
         player = 3 - player;
+        if (lane == 0) s_ko = ko;
         __syncthreads();
-        ko = __shfl(ko, 0);
+        ko = s_ko;
     }
 }
 
