@@ -196,7 +196,8 @@ def main():
         out["tree_kernels"]["note"] = ("rank-0 HIP events around each kernel of every simulation step; algorithmic "
                                        "bytes counted by the kernels (child records scanned, path VL/backup "
                                        "read-modify-writes, new nodes, leaf planes); latency-bound (one wave per game, "
-                                       "dependent tree levels), peak 8 TB/s")
+                                       "dependent tree levels), peak 8 TB/s; rocprofv3 PMC traffic of the same kernels: "
+                                       "profiles/r01e_tree_pmc.json (tools/tree_pmc.sh)")
         tr = pmc_traffic(a, per_launch_flops / (conv_flops_per_eval / (2 * a.blocks)) if launches else 0)
         if tr:
             out["roofline"].update(tr)
