@@ -231,3 +231,26 @@ def test_gpu_c4_c5_nets_fp16_within_tolerance(engine, shape):
     print(f"{shape} fp16: max|dlogit|={el:.3e} max|dvalue|={ev:.3e} (|logit|max {np.abs(rl).max():.3f})")
     assert el <= TOL and ev <= TOL
     net.close()
+
+
+@pytest.mark.gpu
+def test_gpu_c5_net_full_batch(engine):
+    """C5 at its full per-GPU batch (BASELINE.json configs[4]: 8x8x111 planes -> 4672-way policy, 20 x
+    256 net, B = 1024 -- the chess rules are not runnable in the reference): a
+    sample of the 1024 outputs within 1e-4 of the fp32 network, and a board's outputs bitwise the
+    same in a sub-batch (DENSE tiles of 8 boards, full last round)."""
+    import az_amd
+    import net_oracle
+    B = 1024
+    desc = az_amd.NetDesc(8, 111, 256, 20, 4672, 32, 8, 256, 1, 0, az_amd.AZ_PREC_FP16, B)
+    net = az_amd.HipNeuralNetwork(engine, desc)
+    blob = net_oracle.init_blob(desc, seed=1234)
+    net.load_weights(blob)
+    x = _rand_planes(B, 111, 8, seed=11, p=0.05)
+    lo, v = net.forward(x)
+    idx = np.random.default_rng(5).choice(B, 24, replace=False)
+    rl, rv = net_oracle.forward(desc, blob, x[idx])
+    assert np.abs(lo[idx] - rl).max() <= TOL and np.abs(v[idx] - rv).max() <= TOL
+    lo2, v2 = net.forward(x[517:530])
+    assert np.array_equal(lo2, lo[517:530]) and np.array_equal(v2, v[517:530])
+    net.close()
