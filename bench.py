@@ -49,7 +49,7 @@ def parse():
                     help="trunk precision: fp16 = the reference useFp16 option (fp16 MFMA operands, fp32 accumulate, "
                          "~2^-20 residual stream; C3 logits within ~6e-5 of fp32), bf16x3 = fp32-faithful")
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU oracle on rank 0 at N=1")
-    ap.add_argument("--cpu-moves", type=int, default=1)
+    ap.add_argument("--cpu-moves", type=int, default=2)   # ~13 s of CPU work at C3
     ap.add_argument("--cpu-sims", type=int, default=None,
                     help="simulations of the CPU sample move (default: --sims for Gomoku, 100 for Go 19x19); a "
                          "shorter sample is scaled to --sims by its evaluations/s")
