@@ -19,7 +19,7 @@ from dataclasses import dataclass, field
 import numpy as np
 
 from ._lib import (AZ_EVAL_HASH, AZ_EVAL_NET, AZ_EVAL_RANDOM, AZ_EVAL_UNIFORM, AZ_PREC_BF16, AZ_PREC_BF16X3, AZ_PREC_F32, AZ_PREC_FP16, AzError,
-                   GAME_SINK, PROGRESS_FN, NetDesc, SearchCfg, SelfPlayCfg, check, lib)
+                   GAME_SINK, PROGRESS_FN, MoveRec as _lib_MoveRec, NetDesc, SearchCfg, SelfPlayCfg, check, lib)
 
 __all__ = ["Engine", "HipNeuralNetwork", "ParallelMCTS", "SelfPlayManager", "GameRecord", "MoveData", "AzError",
            "Dataset", "TrainingExample", "GAME_GOMOKU", "GAME_GO",
@@ -90,6 +90,12 @@ class HipNeuralNetwork:
 
     def init_random(self, seed):
         check(lib().az_net_init_random(self.h, seed))
+
+    def get_weights(self):
+        """The loaded weights as the canonical fp32 blob (az_net_get_weights)."""
+        blob = np.empty(self.num_params, np.float32)
+        check(lib().az_net_get_weights(self.h, _fp(blob), blob.size))
+        return blob
 
     def set_precision(self, precision):
         check(lib().az_net_set_precision(self.h, precision))
@@ -268,6 +274,20 @@ class ParallelMCTS:
         evals = ctypes.c_int64(0)
         check(lib().az_selfplay_step(self.h, ctypes.byref(cfg), ctypes.byref(moves), ctypes.byref(evals)))
         return moves.value, evals.value
+
+    def stepMoves(self):
+        """MoveData of the last selfplayStep: [(slot, MoveData)] for every game that moved."""
+        mv = ctypes.POINTER(_lib_MoveRec)()
+        sl = ctypes.POINTER(ctypes.c_int)()
+        n = ctypes.c_int()
+        check(lib().az_selfplay_step_moves(self.h, ctypes.byref(mv), ctypes.byref(sl), ctypes.byref(n)))
+        out = []
+        for i in range(n.value):
+            r = mv[i]
+            k = r.n_children
+            out.append((int(sl[i]), MoveData(int(r.action), [float(r.policy[j]) for j in range(k)], float(r.value),
+                                             int(r.thinking_time_ms), [int(r.child_actions[j]) for j in range(k)])))
+        return out
 
     def close(self):
         if self.h:

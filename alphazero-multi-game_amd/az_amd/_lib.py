@@ -51,6 +51,7 @@ EXPORTS = {
     "az_net_num_params": (c_int, [vp, P(c_size_t)]),
     "az_net_load_weights": (c_int, [vp, P(c_float), c_size_t]),
     "az_net_init_random": (c_int, [vp, c_uint64]),
+    "az_net_get_weights": (c_int, [vp, P(c_float), c_size_t]),
     "az_net_set_precision": (c_int, [vp, c_int]),
     "az_net_forward": (c_int, [vp, P(c_float), c_int, P(c_float), P(c_float)]),
     "az_net_predict_batch": (c_int, [vp, P(c_float), c_int, P(c_float), P(c_float)]),
@@ -72,6 +73,7 @@ EXPORTS = {
     "az_search_enable_eval_log": (c_int, [vp, c_int, c_int]),
     "az_search_read_eval_log": (c_int, [vp, P(c_float), P(c_float), P(c_float), P(c_int)]),
     "az_selfplay_step": (c_int, [vp, P(SelfPlayCfg), P(c_int64), P(c_int64)]),
+    "az_selfplay_step_moves": (c_int, [vp, P(P(MoveRec)), P(P(c_int)), P(c_int)]),
     "az_selfplay_run": (c_int, [vp, P(SelfPlayCfg), c_int, c_int, GAME_SINK, PROGRESS_FN, vp, P(c_int)]),
     "az_dataset_create": (c_int, [vp, c_int, c_int, P(vp)]),
     "az_dataset_destroy": (None, [vp]),

@@ -21,6 +21,17 @@ def shard(rank, games_per_rank, noise_seed=NOISE_SEED, eval_seed=0):
             "eval_seed": eval_seed + g0}
 
 
+def shard_range(rank, world, total_games, noise_seed=NOISE_SEED, eval_seed=0):
+    """Contiguous split of `total_games` global game ids over `world` ranks (the first
+    total % world ranks take one more), with shard()'s seeds: BASELINE.json C3's "2048 games,
+    sharded 1/2/4/8" is shard_range(rank, N, 2048)."""
+    base, extra = divmod(int(total_games), int(world))
+    g0 = rank * base + min(rank, extra)
+    n = base + (1 if rank < extra else 0)
+    return {"first_game": g0, "games": n, "noise_seed": noise_seed + g0, "noise_seed_stride": 1,
+            "eval_seed": eval_seed + g0}
+
+
 def broadcast_weights(dist, blob, n_params, device="cpu"):
     """Rank 0's fp32 blob (numpy, or None elsewhere) to every rank; returns the numpy blob."""
     import torch

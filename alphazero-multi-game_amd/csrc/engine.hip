@@ -108,6 +108,7 @@ struct az_net {
     int* d_nb = nullptr;
     uint16_t* zero = nullptr;   // 256 zero bytes: glds source for the board edge
     bool loaded = false;
+    std::vector<float> host_blob;   // canonical blob of the loaded weights (az_net_get_weights)
     // profiling: HIP events bracketing the 3x3 trunk of every forward (on the launch stream)
     bool prof = false;
     std::vector<hipEvent_t> evpool;
@@ -434,6 +435,10 @@ struct az_search {
     std::vector<long long> prof_cnt0;
     std::vector<std::mt19937> rng;
     std::vector<float> h_noise; std::vector<uint8_t> h_mask;
+    // az_selfplay_step's MoveData records of the last step (az_selfplay_step_moves)
+    std::vector<float> sp_probs, sp_values;
+    std::vector<int> sp_cact, sp_nch, sp_slots;
+    std::vector<az_move_rec> sp_moves;
     std::mutex mu;
 };
 
@@ -726,7 +731,18 @@ int az_net_load_weights(az_net* n, const float* blob, size_t count) {
     if (count != n->nparams) return az_fail(AZ_ERR_ARG, "expected %zu parameters, got %zu", n->nparams, count);
     std::lock_guard<std::mutex> lk(n->mu);
     HIPCHK(hipSetDevice(n->e->device));
-    return net_load(n, blob);
+    if (int r = net_load(n, blob)) return r;
+    n->host_blob.assign(blob, blob + count);
+    return 0;
+}
+
+int az_net_get_weights(az_net* n, float* blob, size_t count) {
+    if (!n || !blob) return az_fail(AZ_ERR_ARG, "null argument");
+    std::lock_guard<std::mutex> lk(n->mu);
+    if (!n->loaded) return az_fail(AZ_ERR_STATE, "weights not loaded");
+    if (count != n->nparams) return az_fail(AZ_ERR_ARG, "expected %zu parameters, got %zu", n->nparams, count);
+    std::copy(n->host_blob.begin(), n->host_blob.end(), blob);
+    return 0;
 }
 
 // Counter-based init; tests/nn_weights.py restates it in numpy (same fp32 ops).
@@ -1093,22 +1109,35 @@ int az_selfplay_step(az_search* s, const az_selfplay_cfg* cfg, int64_t* moves_do
     const int G = s->c.n_games;
     std::vector<long long> c0((size_t)G * AZ_NCNT), c1((size_t)G * AZ_NCNT);
     if (evals_done) HIPCHK(hipMemcpy(c0.data(), s->t.cnt, c0.size() * 8, hipMemcpyDeviceToHost));
+    const auto t0 = std::chrono::steady_clock::now();
     if (int r = search_run(s)) return r;
     std::vector<float> temps(G);
     std::vector<int> was_active = s->active;
     std::vector<int> ply0 = s->ply;
     for (int g = 0; g < G; ++g) temps[g] = s->ply[g] >= cfg->temp_drop_move ? cfg->t_final : cfg->t_init;
     std::vector<int> actions(G);
-    if (int r = search_select(s, 1, temps.data(), 0.0f, actions.data(), nullptr, nullptr, nullptr, nullptr)) return r;
+    // the same D2H and MoveData assembly as az_selfplay_run (getActionProbabilities + getRootValue
+    // per game, self_play_manager.cpp:187-203); read back with az_selfplay_step_moves
+    const int NA = s->t.NA;
+    s->sp_probs.resize((size_t)G * NA); s->sp_cact.resize((size_t)G * NA);
+    s->sp_values.resize(G); s->sp_nch.resize(G);
+    if (int r = search_select(s, 1, temps.data(), 0.0f, actions.data(), s->sp_values.data(), s->sp_probs.data(),
+                              s->sp_cact.data(), s->sp_nch.data()))
+        return r;
+    const int64_t ms = std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::steady_clock::now() - t0).count();
     std::vector<int> term(G), res(G);
     if (int r = search_apply_dev(s, term.data(), res.data())) return r;
     int64_t moves = 0;
     std::vector<uint8_t> noise_mask(G, 0);
     const int none = s->t.game == GAME_GO ? AZ_ACTION_NONE : -1;
+    s->sp_moves.clear(); s->sp_slots.clear();
     for (int g = 0; g < G; ++g) {
         if (!was_active[g] || actions[g] == none) continue;
         ++moves;
         if (ply0[g] % 2 == 0) noise_mask[g] = 1;
+        s->sp_moves.push_back(az_move_rec{actions[g], s->sp_values[g], s->sp_nch[g], s->sp_probs.data() + (size_t)g * NA,
+                                          s->sp_cact.data() + (size_t)g * NA, ms});
+        s->sp_slots.push_back(g);
     }
     if (int r = search_noise(s, s->c.dirichlet_alpha, s->c.dirichlet_eps, noise_mask.data())) return r;
     if (cfg->restart_finished) {
@@ -1128,6 +1157,15 @@ int az_selfplay_step(az_search* s, const az_selfplay_cfg* cfg, int64_t* moves_do
         for (int g = 0; g < G; ++g) ev += c1[(size_t)g * AZ_NCNT + CNT_EVALS_TOTAL] - c0[(size_t)g * AZ_NCNT + CNT_EVALS_TOTAL];
         *evals_done += ev;
     }
+    return 0;
+}
+
+int az_selfplay_step_moves(az_search* s, const az_move_rec** moves, const int** slots, int* n) {
+    if (!s || !moves || !n) return az_fail(AZ_ERR_ARG, "null argument");
+    std::lock_guard<std::mutex> lk(s->mu);
+    *moves = s->sp_moves.data();
+    if (slots) *slots = s->sp_slots.data();
+    *n = (int)s->sp_moves.size();
     return 0;
 }
 

@@ -1,216 +1,262 @@
 #!/usr/bin/env python3
 """bench.py -- self-play positions/s (+ NN evals/s) at 800 sims/move on MI355X.
 
-Workload (BASELINE.json configs[2], "C3"): Gomoku 15x15, 20-block x 256-filter residual
-policy/value net, 2048 concurrent games per GPU, 800 simulations per move, the
-reference's playSingleGame loop (Dirichlet noise, temperature schedule, subtree
-reuse, per-game transposition table).  One step = one committed move of every game
-(800 batched simulations: PUCT select -> leaf batch through the ConvNet -> expand /
-backup).  Games shard across ranks with no data-path collective (weak scaling:
-2048 games per GPU); RCCL only broadcasts the weights and reduces counters.
+Workload (BASELINE.json configs[2], "C3", the default): Gomoku 15x15, 20-block x 256-filter
+residual policy/value net, 2048 concurrent games sharded over the N GPUs (2048/N per GPU,
+contiguous global game ids), 800 simulations per move, the reference's playSingleGame loop
+(Dirichlet noise, temperature schedule, subtree reuse, per-game transposition table).  One step
+= one committed move of every game (800 batched simulations: PUCT select -> leaf batch through
+the ConvNet -> expand / backup), with the MoveData records of every move assembled on the host.
+Games shard across ranks with no data-path collective; RCCL only broadcasts rank 0's weights
+and reduces the counters.  `--scaling weak` keeps 2048 games per GPU instead.
 
-Synthetic data: games start from the empty board; weights are random-init of the
-named architecture (counter-based generator, identical on every rank).
+  --config c2   BASELINE.json configs[1]: 15x15, 6b x 64f, 256 games, 400 sims, 1 GPU
+  --config c4   BASELINE.json configs[3]: Go 19x19 (GoState on device), 8 planes, 362 actions,
+                1024 games sharded over the GPUs
 
---game go: the C4 workload (BASELINE.json configs[3]) on one GPU per rank: Go 19x19 (GoState:
-captures, ko, superko, area scoring on device), 8 input planes, 362-way policy, 1024 games.
+Launch: `python bench.py --gpus N` starts N ranks itself (torch.distributed.run, one process
+per GPU, 127.0.0.1 rendezvous) unless WORLD_SIZE is already set by a launcher; it fails loudly
+when fewer than N GPUs are visible or WORLD_SIZE != N.
+
+Synthetic data: games start from the empty board; weights are the counter-based random init of
+the named architecture (az_net_init_random on rank 0, broadcast to the other ranks).
+
+cpu_baseline (rank 0, N=1): the CPU restatement of the reference search (oracle/, Mode S) with the
+fp32 PyTorch-CPU network, one game per worker process, one thread each, on the host's CPU share
+(self_play_manager.cpp:69-89), timed over a fixed window.
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
-for _p in (os.path.join(ROOT, "alphazero-multi-game_amd"), os.path.join(ROOT, "oracle")):
-    if _p not in sys.path:
-        sys.path.insert(0, _p)
+PKG = os.path.join(ROOT, "alphazero-multi-game_amd")
+if PKG not in sys.path:
+    sys.path.insert(0, PKG)
 
 import numpy as np  # noqa: E402
 
 METRIC = "self-play positions/sec (+ NN evals/sec) at 800 sims/move, 1/2/4/8 GPU"
 PEAK_TFLOPS = {"bf16x3": 2500.0, "bf16": 2500.0, "fp16": 2500.0, "f32": 157.3}   # dense MFMA peaks, MI355X_MICROARCH.md
 PREC = {"f32": 0, "bf16x3": 1, "bf16": 2, "fp16": 3}
-KERNEL = {"fp16": "conv3x3_v6<2>", "bf16": "conv3x3_v6<1>", "bf16x3": "conv3x3_v4<0>", "f32": "gemm_f32"}
+# BASELINE.json configs: game, board, blocks, channels, sims/move, global games
+CONFIGS = {
+    "c2": dict(game="gomoku", board=15, blocks=6, channels=64, sims=400, games=256,
+               name="C2 Gomoku 15x15, 6b x 64f ResNet"),
+    "c3": dict(game="gomoku", board=15, blocks=20, channels=256, sims=800, games=2048,
+               name="C3 Gomoku 15x15, 20b x 256f ResNet"),
+    "c4": dict(game="go", board=19, blocks=20, channels=256, sims=800, games=1024,
+               name="C4 Go 19x19, 20b x 256f ResNet"),
+}
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--game", default="gomoku", choices=["gomoku", "go"])
-    ap.add_argument("--games", type=int, default=None, help="games per GPU (C3: 2048, C4: 1024)")
-    ap.add_argument("--sims", type=int, default=800)
-    ap.add_argument("--board", type=int, default=None, help="board size (Gomoku 15, Go 19)")
-    ap.add_argument("--channels", type=int, default=256)
-    ap.add_argument("--blocks", type=int, default=20)
+    ap.add_argument("--config", default=None, choices=list(CONFIGS), help="BASELINE.json workload (default c3)")
+    ap.add_argument("--game", default=None, choices=["gomoku", "go"], help="go = --config c4")
+    ap.add_argument("--global-games", type=int, default=None, help="games over all GPUs (C2 256, C3 2048, C4 1024)")
+    ap.add_argument("--games", type=int, default=None, help="games per GPU (implies --scaling weak)")
+    ap.add_argument("--scaling", default="strong", choices=["strong", "weak"],
+                    help="strong: the global games are sharded over the GPUs (BASELINE 'sharded 1/2/4/8'); "
+                         "weak: every GPU plays --global-games games")
+    ap.add_argument("--sims", type=int, default=None)
+    ap.add_argument("--board", type=int, default=None)
+    ap.add_argument("--channels", type=int, default=None)
+    ap.add_argument("--blocks", type=int, default=None)
     ap.add_argument("--precision", default="fp16", choices=list(PREC),
                     help="trunk precision: fp16 = the reference useFp16 option (fp16 MFMA operands, fp32 accumulate, "
-                         "~2^-20 residual stream; C3 logits within ~6e-5 of fp32), bf16x3 = fp32-faithful")
-    ap.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU oracle on rank 0 at N=1")
-    ap.add_argument("--cpu-moves", type=int, default=2)   # ~13 s of CPU work at C3
-    ap.add_argument("--cpu-sims", type=int, default=None,
-                    help="simulations of the CPU sample move (default: --sims for Gomoku, 100 for Go 19x19); a "
-                         "shorter sample is scaled to --sims by its evaluations/s")
+                         "2^-20 residual stream), bf16x3 = fp32-faithful (three bf16 MFMAs per product)")
+    ap.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU restatement on rank 0 at N=1")
+    ap.add_argument("--cpu-window", type=float, default=20.0, help="seconds of the CPU baseline's timed window")
+    ap.add_argument("--cpu-workers", type=int, default=0, help="CPU baseline processes (0: the host's CPU share, <=16)")
     ap.add_argument("--seed", type=int, default=1234)
-    return ap.parse_args()
+    a = ap.parse_args(argv)
+    cfg = a.config or ("c4" if a.game == "go" else "c3")
+    c = CONFIGS[cfg]
+    a.config = cfg
+    a.game = c["game"]
+    for k in ("board", "blocks", "channels", "sims"):
+        if getattr(a, k) is None:
+            setattr(a, k, c[k])
+    if a.games is not None:
+        a.scaling = "weak"
+        a.global_games = a.games
+    if a.global_games is None:
+        a.global_games = c["games"]
+    a.workload_name = c["name"]
+    return a
 
 
-def cpu_baseline(desc, blob, board, sims, moves, game="gomoku", sample_sims=None):
-    """The CPU restatement (oracle/, Mode S, one game) with the fp32 PyTorch-CPU network
-    evaluating one state per call, as the reference's ParallelMCTS::evaluateState does."""
+# ------------------------------------------------------------------------------- launching
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_ranks(a, argv):
+    """--gpus N without a launcher: start N ranks with torch.distributed.run as a child process
+    (nothing here has touched the GPU; torch.cuda.device_count() does not initialise it)."""
     import torch
-    import az_oracle as O
-    import net_oracle
-    model = net_oracle.Model(desc, blob)
-    calls = [0]
-
-    def ev(game, planes):
-        calls[0] += 1
-        lo, v = model(planes[None])
-        return lo[0], float(v[0])
-
-    ev(0, np.zeros((desc.in_planes, board, board), np.float32))   # warm-up
-    calls[0] = 0
-    ss = sample_sims or sims
-    t0 = time.perf_counter()
-    O.play(bs=board, sims=ss, max_moves=moves, eval_kind=O.EVAL_NET, evaluator=ev,
-           game=O.GAME_GO if game == "go" else O.GAME_GOMOKU)
-    dt = time.perf_counter() - t0
-    eps = calls[0] / dt
-    value = moves / dt if ss == sims else eps / (sims + 1)      # one evaluation per simulation + the root
-    return {"value": value, "unit": "positions/s", "cores": torch.get_num_threads(), "kind": "port",
-            "evals_per_s": eps,
-            "sample": ("" if ss == sims else f"scaled to {sims} sims/move from ") +
-                      f"1 game x {moves} move(s) x {ss} sims, {game.capitalize()} {board}x{board}, {desc.blocks}b x "
-                      f"{desc.channels}f fp32 net on PyTorch-CPU (B=1 per evaluation), oracle/ Mode S search; "
-                      f"{calls[0]} evaluations in {dt:.1f} s"}
+    n = torch.cuda.device_count()
+    if n < a.gpus:
+        print(f"bench.py: --gpus {a.gpus} requested but only {n} GPU(s) are visible", file=sys.stderr)
+        return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + list(argv)
+    return subprocess.call(cmd)
 
 
-def main():
-    a = parse()
-    go = a.game == "go"
-    if a.board is None:
-        a.board = 19 if go else 15
-    if a.games is None:
-        a.games = 1024 if go else 2048
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        import torch
-        import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", init_method="env://")
+# ------------------------------------------------------------------------------- GPU workload
+class GpuWorkload:
+    """The device self-play handle of one rank: HipNeuralNetwork + ParallelMCTS over `games` slots."""
 
-    import az_amd
-    import net_oracle
-    eng = az_amd.Engine(local)
-    if go:
-        desc = az_amd.NetDesc(a.board, 8, a.channels, a.blocks, a.board * a.board + 1, 32, 8, 256, 1, 0,
-                              PREC[a.precision], a.games)
-    else:
-        desc = az_amd.gomoku_net_desc(board_size=a.board, channels=a.channels, blocks=a.blocks,
-                                      precision=PREC[a.precision], max_batch=a.games)
-    net = az_amd.HipNeuralNetwork(eng, desc)
+    def __init__(self, a, local, shard):
+        import az_amd
+        self.eng = az_amd.Engine(local)
+        go = a.game == "go"
+        if go:
+            desc = az_amd.NetDesc(a.board, 8, a.channels, a.blocks, a.board * a.board + 1, 32, 8, 256, 1, 0,
+                                  PREC[a.precision], shard["games"])
+        else:
+            desc = az_amd.gomoku_net_desc(board_size=a.board, channels=a.channels, blocks=a.blocks,
+                                          precision=PREC[a.precision], max_batch=shard["games"])
+        self.desc = desc
+        self.net = az_amd.HipNeuralNetwork(self.eng, desc)
+        self.mcts_args = dict(n_games=shard["games"], board_size=a.board, num_simulations=a.sims,
+                              evaluator=az_amd.AZ_EVAL_NET, noise_seed=shard["noise_seed"],
+                              noise_seed_stride=shard["noise_seed_stride"],
+                              game=az_amd.AZ_GAME_GO if go else az_amd.AZ_GAME_GOMOKU)
+        self.mcts = None
+
+    def start(self):
+        import az_amd
+        self.mcts = az_amd.ParallelMCTS(self.eng, net=self.net, **self.mcts_args)
+        self.mcts.newGames()
+        self.mcts.addDirichletNoise(0.03, 0.25)
+
+    def step(self):
+        mv, ev = self.mcts.selfplayStep()
+        self.mcts.stepMoves()          # the MoveData records of this move (as generateGames keeps them)
+        return mv, ev
+
+    def sync(self):
+        pass                           # selfplayStep returns after a stream synchronize
+
+
+def conv_kernel_name(a):
+    if a.precision == "f32":
+        return "gemm_f32"
+    if a.channels % 128 == 0:
+        return f"conv3x3_v6<{2 if a.precision == 'fp16' else 1}, {a.board}>" if a.precision != "bf16x3" else \
+            "conv3x3_v4<0,128>"
+    return f"conv3x3_v4<{ {'fp16': 2, 'bf16': 1, 'bf16x3': 0}[a.precision] },64>"
+
+
+def run_rank(a, rank, world, dist, make_workload, coll_device):
+    """One rank of the bench: shard, weights (rank 0 init + broadcast), warmup, timed steps between
+    barriers, MAX elapsed / SUM counters over ranks.  Returns the JSON dict on rank 0, else None."""
     from az_amd import dist as azdist
-    blob = None
-    if dist is None:
+    sh = azdist.shard_range(rank, world, a.global_games if a.scaling == "strong" else a.global_games * world)
+    if sh["games"] < 1:
+        raise SystemExit(f"bench.py: rank {rank} got no games ({a.global_games} over {world} ranks)")
+    wl = make_workload(a, int(os.environ.get("LOCAL_RANK", "0")), sh)
+    net = wl.net
+    if rank == 0:
         net.init_random(a.seed)
-    else:
-        blob = net_oracle.init_blob(desc, a.seed) if rank == 0 else None
-        blob = azdist.broadcast_weights(dist, blob, net.num_params, f"cuda:{local}")   # RCCL over xGMI, once
-        net.load_weights(blob)
-    sh = azdist.shard(rank, a.games)       # global game ids / seeds of this rank
-    m = az_amd.ParallelMCTS(eng, n_games=a.games, board_size=a.board, num_simulations=a.sims,
-                            evaluator=az_amd.AZ_EVAL_NET, net=net, noise_seed=sh["noise_seed"],
-                            noise_seed_stride=sh["noise_seed_stride"],
-                            game=az_amd.AZ_GAME_GO if go else az_amd.AZ_GAME_GOMOKU)
-    m.newGames()
-    m.addDirichletNoise(0.03, 0.25)
+    if world > 1:
+        blob = net.get_weights() if rank == 0 else None
+        blob = azdist.broadcast_weights(dist, blob, net.num_params, coll_device)   # RCCL over xGMI, once
+        if rank != 0:
+            net.load_weights(blob)
+    wl.start()
     for _ in range(a.warmup):
-        m.selfplayStep()
+        wl.step()
 
     def barrier():
+        wl.sync()
         if dist is not None:
             dist.barrier()
     barrier()
     net.profile(True)
-    m.profile(True)
+    wl.mcts.profile(True)
     t0 = time.perf_counter()
     moves = evals = 0
     for _ in range(a.steps):
-        mv, ev = m.selfplayStep()
+        mv, ev = wl.step()
         moves += mv
         evals += ev
-    elapsed = time.perf_counter() - t0     # selfplayStep returns after a stream sync
+    wl.sync()
+    elapsed = time.perf_counter() - t0
     barrier()
-    trunk_ms, launches, forwards = net.profile_read()
-    tree = m.profile_read()
-
+    trunk_ms, launches, _ = net.profile_read()
+    tree = wl.mcts.profile_read()
+    my_evals = evals
+    tot_moves, tot_evals = moves, evals
     if dist is not None:
-        elapsed, (moves, evals) = azdist.reduce_counters(dist, elapsed, [moves, evals], f"cuda:{local}")
+        elapsed, (tot_moves, tot_evals) = azdist.reduce_counters(dist, elapsed, [moves, evals], coll_device)
+    if rank != 0:
+        return None
 
-    if rank == 0:
-        HW = a.board * a.board
-        conv_flops_per_eval = 2 * a.blocks * 2.0 * 9 * a.channels * a.channels * HW
-        local_evals = evals // max(1, world)
-        per_launch_flops = local_evals * conv_flops_per_eval / max(1, launches)
-        per_launch_ms = trunk_ms / max(1, launches)
-        achieved = per_launch_flops / (per_launch_ms * 1e-3) / 1e12 if launches else 0.0
-        peak = PEAK_TFLOPS[a.precision]
-        out = {
-            "metric": METRIC,
-            "value": moves / elapsed,
-            "unit": "positions/s",
-            "n_gpus": world,
-            "steps": a.steps,
-            "warmup": a.warmup,
-            "ms_per_step": 1e3 * elapsed / a.steps,
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": a.precision,
-            "data": "synthetic: self-play from empty boards, counter-based random-init weights of the named net",
-            "config": {"workload": f"{'C4 Go' if go else 'C3 Gomoku'} {a.board}x{a.board}, {a.blocks}b x "
-                                   f"{a.channels}f ResNet, {a.sims} sims/move", "game": a.game,
-                       "games_per_gpu": a.games, "global_games": a.games * world,
-                       "sims_per_move": a.sims, "board": a.board, "blocks": a.blocks, "channels": a.channels,
-                       "parallelism": f"game-shard x{world}"},
-            "nn_evals_per_s": evals / elapsed,
-            "roofline": {"kernel": f"{KERNEL[a.precision]} ({a.precision} trunk, {a.board}x{a.board})", "bound": "mfma",
-                         "achieved": achieved,
-                         "peak": peak, "unit": "TFLOP/s", "frac": achieved / peak, "traffic": None,
-                         "launches": launches, "avg_launch_ms": per_launch_ms,
-                         "flops_per_launch": per_launch_flops},
-        }
-        steps = max(1, tree["sim_steps"])
-        out["tree_kernels"] = {
-            name: {"avg_launch_us": 1e3 * tree[f"{k}_ms"] / steps,
-                   "bytes_per_launch": tree[f"{k}_bytes"] / steps,
-                   "GB_per_s": tree[f"{k}_bytes"] / max(1e-12, 1e-3 * tree[f"{k}_ms"]) / 1e9,
-                   "frac_of_hbm_peak": tree[f"{k}_bytes"] / max(1e-12, 1e-3 * tree[f"{k}_ms"]) / 8.0e12}
-            for name, k in (("k_select", "select"), ("k_expand_backup", "expand"))}
-        out["tree_kernels"]["note"] = ("rank-0 HIP events around each kernel of every simulation step; algorithmic "
-                                       "bytes counted by the kernels (child records scanned, path VL/backup "
-                                       "read-modify-writes, new nodes, leaf planes); latency-bound (one wave per game, "
-                                       "dependent tree levels), peak 8 TB/s; rocprofv3 PMC traffic of the same kernels: "
-                                       "profiles/r01e_tree_pmc.json (tools/tree_pmc.sh)")
-        tr = pmc_traffic(a, per_launch_flops / (conv_flops_per_eval / (2 * a.blocks)) if launches else 0)
-        if tr:
-            out["roofline"].update(tr)
-        if a.cpu_baseline and world == 1:
-            if blob is None:
-                blob = net_oracle.init_blob(desc, a.seed)
-            out["cpu_baseline"] = cpu_baseline(desc, blob, a.board, a.sims, a.cpu_moves, a.game,
-                                               a.cpu_sims or (100 if go else a.sims))
-        else:
-            out["cpu_baseline"] = None
-        print(json.dumps(out))
-    if dist is not None:
-        dist.destroy_process_group()
+    HW = a.board * a.board
+    conv_flops_per_eval = 2 * a.blocks * 2.0 * 9 * a.channels * a.channels * HW
+    boards_per_launch = my_evals * 2 * a.blocks / max(1, launches)        # rank 0's own launches and boards
+    per_launch_flops = boards_per_launch * conv_flops_per_eval / (2 * a.blocks)
+    per_launch_ms = trunk_ms / max(1, launches)
+    achieved = per_launch_flops / (per_launch_ms * 1e-3) / 1e12 if launches else 0.0
+    peak = PEAK_TFLOPS[a.precision]
+    strong = a.scaling == "strong"
+    out = {
+        "metric": METRIC,
+        "value": tot_moves / elapsed,
+        "unit": "positions/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": 1e3 * elapsed / a.steps,
+        "higher_is_better": True,
+        "scaling": "strong" if strong else "weak",
+        "vs_baseline": None,
+        "dtype": a.precision,
+        "data": "synthetic: self-play from empty boards, counter-based random-init weights of the named net",
+        "config": {"workload": f"{a.workload_name}, {a.global_games if strong else a.global_games * world} games"
+                               f"{' sharded' if strong else ''} over {world} GPU(s), {a.sims} sims/move",
+                   "baseline_config": a.config, "game": a.game, "global_games": a.global_games if strong else
+                   a.global_games * world, "games_per_gpu": sh["games"], "sims_per_move": a.sims, "board": a.board,
+                   "blocks": a.blocks, "channels": a.channels, "parallelism": f"game-shard x{world}"},
+        "nn_evals_per_s": tot_evals / elapsed,
+        "evals_per_move": tot_evals / max(1, tot_moves),
+        "roofline": {"kernel": f"{conv_kernel_name(a)} ({a.precision} trunk, {a.board}x{a.board}, "
+                               f"{a.channels} ch)", "bound": "mfma",
+                     "achieved": achieved, "peak": peak, "unit": "TFLOP/s", "frac": achieved / peak, "traffic": None,
+                     "launches": launches, "avg_launch_ms": per_launch_ms, "boards_per_launch": boards_per_launch,
+                     "flops_per_launch": per_launch_flops},
+    }
+    steps = max(1, tree["sim_steps"])
+    out["tree_kernels"] = {
+        name: {"avg_launch_us": 1e3 * tree[f"{k}_ms"] / steps,
+               "bytes_per_launch": tree[f"{k}_bytes"] / steps,
+               "GB_per_s": tree[f"{k}_bytes"] / max(1e-12, 1e-3 * tree[f"{k}_ms"]) / 1e9,
+               "frac_of_hbm_peak": tree[f"{k}_bytes"] / max(1e-12, 1e-3 * tree[f"{k}_ms"]) / 8.0e12}
+        for name, k in (("k_select", "select"), ("k_expand_backup", "expand"))}
+    out["tree_kernels"]["note"] = ("rank-0 HIP events around each kernel of every simulation step; algorithmic "
+                                   "bytes counted by the kernels (child records scanned, path VL/backup "
+                                   "read-modify-writes, new nodes, leaf planes); latency-bound (one wave per game, "
+                                   "dependent tree levels), peak 8 TB/s; rocprofv3 PMC traffic of the same kernels: "
+                                   "profiles/r01e_tree_pmc.json (tools/tree_pmc.sh)")
+    tr = pmc_traffic(a, boards_per_launch if launches else 0)
+    if tr:
+        out["roofline"].update(tr)
+    return out
 
 
 def pmc_traffic(a, boards_per_launch):
@@ -236,5 +282,128 @@ def pmc_traffic(a, boards_per_launch):
             "traffic_source": os.path.relpath(f, ROOT) + f" (PMC at B={d['boards_per_launch']}, scaled x{scale:.4f})"}
 
 
+# ------------------------------------------------------------------------------- CPU baseline
+def cpu_share():
+    """Host cores this process may use: the affinity mask, capped at 16 (a GPU box's CPU share per GPU;
+    nproc there reports the whole machine)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit() and int(env) > 0:
+        n = min(n, int(env))
+    return max(1, min(16, n))
+
+
+def _cpu_worker(i, desc_fields, blob_path, game, board, sims, window, barrier, q):
+    """One game on one core: oracle Mode S search, fp32 PyTorch-CPU net at B=1 per evaluation (as
+    ParallelMCTS::evaluateState calls NeuralNetwork::predict), evaluations counted in the window."""
+    import torch
+    torch.set_num_threads(1)
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import types
+    import az_oracle as O
+    import net_oracle
+    desc = types.SimpleNamespace(**desc_fields)
+    model = net_oracle.Model(desc, np.load(blob_path, mmap_mode="r"))
+    model(np.zeros((1, desc.in_planes, board, board), np.float32))          # warm-up evaluation
+    st = {"n": 0, "deadline": None}
+
+    def ev(_g, planes):
+        if time.perf_counter() >= st["deadline"]:
+            raise O.StopPlay()
+        lo, v = model(planes[None])
+        st["n"] += 1
+        return lo[0], float(v[0])
+
+    barrier.wait(timeout=600)
+    t0 = time.perf_counter()
+    st["deadline"] = t0 + window
+    k = 0
+    while time.perf_counter() < st["deadline"]:
+        O.play(bs=board, sims=sims, eval_kind=O.EVAL_NET, evaluator=ev, noise_seed=42 + i + 1000 * k,
+               game=O.GAME_GO if game == "go" else O.GAME_GOMOKU)
+        k += 1
+    q.put((i, st["n"], time.perf_counter() - t0))
+
+
+def cpu_baseline(a, workers, window):
+    """Raw CPU sample: {evals_per_s, cores, window, workers}; positions/s is derived after the GPU run
+    from its measured evaluations per move.  Runs before anything touches the GPU."""
+    import multiprocessing as mp
+    import tempfile
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import net_oracle
+    go = a.game == "go"
+    fields = dict(board_size=a.board, in_planes=8 if go else 11, channels=a.channels, blocks=a.blocks,
+                  action_size=a.board * a.board + (1 if go else 0), head_channels=32, pool=8, fc_hidden=256,
+                  residual=1, conv_bias=0)
+    blob = net_oracle.init_blob(__import__("types").SimpleNamespace(**fields), a.seed)   # == az_net_init_random
+    fd, path = tempfile.mkstemp(suffix=".npy")
+    os.close(fd)
+    try:
+        np.save(path, blob)
+        ctx = mp.get_context("spawn")
+        barrier = ctx.Barrier(workers + 1)
+        q = ctx.Queue()
+        procs = [ctx.Process(target=_cpu_worker, args=(i, fields, path, a.game, a.board, a.sims, window, barrier, q))
+                 for i in range(workers)]
+        for p in procs:
+            p.start()
+        barrier.wait(timeout=600)
+        res = [q.get(timeout=window + 600) for _ in procs]
+        for p in procs:
+            p.join(timeout=60)
+    finally:
+        os.unlink(path)
+    evals = sum(r[1] for r in res)
+    span = max(r[2] for r in res)
+    return {"evals": evals, "evals_per_s": evals / span, "cores": workers, "window_s": span}
+
+
+def cpu_baseline_line(a, raw, evals_per_move):
+    go = a.game == "go"
+    return {"value": raw["evals_per_s"] / evals_per_move, "unit": "positions/s", "cores": raw["cores"],
+            "kind": "port", "evals_per_s": raw["evals_per_s"],
+            "sample": f"{raw['cores']} worker processes x 1 thread, one {'Go' if go else 'Gomoku'} {a.board}x{a.board} "
+                      f"game each from the empty board (oracle/ Mode S search, {a.sims} sims/move, fp32 "
+                      f"{a.blocks}b x {a.channels}f net on PyTorch-CPU, B=1 per evaluation), {raw['evals']} "
+                      f"evaluations in a {raw['window_s']:.1f} s window; positions/s = evaluations/s / "
+                      f"{evals_per_move:.1f} evaluations per move (measured on the GPU run of the same workload)"}
+
+
+# ------------------------------------------------------------------------------- main
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    a = parse(argv)
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        return launch_ranks(a, argv)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != a.gpus:
+        print(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        return 2
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    raw_cpu = None
+    if a.cpu_baseline and world == 1:
+        raw_cpu = cpu_baseline(a, a.cpu_workers or cpu_share(), a.cpu_window)
+    dist = None
+    dev = "cpu"
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        if torch.cuda.device_count() <= local:
+            print(f"bench.py: LOCAL_RANK {local} but {torch.cuda.device_count()} GPU(s) visible", file=sys.stderr)
+            return 2
+        torch.cuda.set_device(local)
+        dev = f"cuda:{local}"
+        dist.init_process_group("nccl", init_method="env://")
+    out = run_rank(a, rank, world, dist, GpuWorkload, dev)
+    if out is not None:
+        out["cpu_baseline"] = cpu_baseline_line(a, raw_cpu, out["evals_per_move"]) if raw_cpu else None
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+    return 0
+
+
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -85,6 +85,9 @@ int az_net_num_params(az_net* n, size_t* count);
 int az_net_load_weights(az_net* n, const float* blob, size_t count);
 /* Counter-based deterministic init (SplitMix64), identical to tests' generator. */
 int az_net_init_random(az_net* n, uint64_t seed);
+/* The loaded weights as the canonical blob (count = az_net_num_params): what rank 0 broadcasts
+ * to the other ranks; AZ_ERR_STATE before any load/init. */
+int az_net_get_weights(az_net* n, float* blob, size_t count);
 int az_net_set_precision(az_net* n, int precision);
 /* planes: host fp32 NCHW [B][in_planes][H][W].  logits [B][A] raw, value [B] (tanh). */
 int az_net_forward(az_net* n, const float* planes, int B, float* logits, float* value);
@@ -194,6 +197,10 @@ typedef struct az_move_rec {
     const int* child_actions;
     int64_t thinking_time_ms;
 } az_move_rec;
+
+/* The MoveData records az_selfplay_step assembled for its last step (one per game that moved;
+ * slots[i] is the device slot of moves[i]); valid until the next call on the handle. */
+int az_selfplay_step_moves(az_search* s, const az_move_rec** moves, const int** slots, int* n);
 
 /* Receives every finished game once, on the calling thread between device steps; the arrays
  * are valid only during the call.  result: core::GameResult (0 ONGOING, 1 DRAW, 2 WIN_PLAYER1,

@@ -432,6 +432,9 @@ struct UniformEval : Evaluator<S> {
 // applied here.  Replay evaluator: the callback returns final (post-softmax) policy.
 typedef int (*az_eval_cb)(void* user, int game, const float* planes, int n_planes, int A,
                           float* policy_out, float* value_out);
+// A callback returning 2 stops the play (bench.py's fixed CPU-baseline window); az_oracle_play
+// then returns "null".
+struct StopPlay {};
 template <class S>
 struct CallbackEval : Evaluator<S> {
     az_eval_cb cb; void* user; bool softmax;
@@ -442,7 +445,9 @@ struct CallbackEval : Evaluator<S> {
         buf.resize(S::NPLANES * s.A);
         s.planes(buf.data());
         p.assign(s.NA(), 0.0f);
-        if (cb(user, game, buf.data(), S::NPLANES, s.NA(), p.data(), &v) != 0) { std::fprintf(stderr, "eval cb failed\n"); std::abort(); }
+        const int rc = cb(user, game, buf.data(), S::NPLANES, s.NA(), p.data(), &v);
+        if (rc == 2) throw StopPlay{};
+        if (rc != 0) { std::fprintf(stderr, "eval cb failed\n"); std::abort(); }
         if (softmax) {
             float mx = *std::max_element(p.begin(), p.end());
             float sum = 0.0f;
@@ -826,7 +831,7 @@ char* az_oracle_play(const az_oracle_cfg* c, int seed_stride, az_eval_cb cb, voi
         RandomEval<GoState> re(c->n_games, c->eval_seed);
         Evaluator<GoState>* ev = c->eval_kind == 0 ? (Evaluator<GoState>*)&he : c->eval_kind == 1 ? (Evaluator<GoState>*)&re
                                : c->eval_kind == 4 ? (Evaluator<GoState>*)&ue : (Evaluator<GoState>*)&ne;
-        play_games<GoState, GoZobrist>(c, cfg, z, ev, seed_stride, o);
+        try { play_games<GoState, GoZobrist>(c, cfg, z, ev, seed_stride, o); } catch (const StopPlay&) { return dup("null"); }
     } else {
         Zobrist z(cfg.bs * cfg.bs, cfg.zobrist_seed);
         HashEval<State> he; RandomEval<State> re(c->n_games, c->eval_seed);
@@ -834,7 +839,7 @@ char* az_oracle_play(const az_oracle_cfg* c, int seed_stride, az_eval_cb cb, voi
         UniformEval<State> ue;
         Evaluator<State>* ev = c->eval_kind == 0 ? (Evaluator<State>*)&he : c->eval_kind == 1 ? (Evaluator<State>*)&re
                              : c->eval_kind == 4 ? (Evaluator<State>*)&ue : (Evaluator<State>*)&ne;
-        play_games<State, Zobrist>(c, cfg, z, ev, seed_stride, o);
+        try { play_games<State, Zobrist>(c, cfg, z, ev, seed_stride, o); } catch (const StopPlay&) { return dup("null"); }
     }
     o << "]";
     return dup(o.str());

@@ -81,6 +81,10 @@ def make_cfg(bs=9, sims=100, max_moves=1 << 30, eval_kind=EVAL_HASH, eval_seed=7
                      cpuct, fpu, alpha, eps, t_init, t_final, noise_seed, zobrist_seed, eval_seed, n_games, game)
 
 
+class StopPlay(Exception):
+    """Raised by an evaluator to end play() early; play() then returns None."""
+
+
 def play(seed_stride=0, evaluator=None, **kw):
     """Play games with the restated Mode S loop; returns a list of per-game dicts
     with the same structure as oracle/_ref/ref_harness `game` output.
@@ -100,6 +104,8 @@ def play(seed_stride=0, evaluator=None, **kw):
             ctypes.memmove(pol, p.ctypes.data, 4 * A)
             val[0] = float(v)
             return 0
+        except StopPlay:
+            return 2
         except Exception as e:  # surfaced as an abort in the oracle
             print("oracle evaluator failed:", repr(e))
             return 1

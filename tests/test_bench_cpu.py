@@ -1,0 +1,163 @@
+"""bench.py's own rank logic on CPU (no GPU): argument handling and the loud failures of the
+launcher, the strong-scaling shard of BASELINE C3 (2048 games sharded over the ranks), rank 0's
+weights broadcast into every other rank's load_weights, MAX-elapsed / SUM-counter reduction and
+the JSON line -- driven over gloo at world size 2 with a stand-in for the device workload (the
+stand-in replaces only the GPU handle; run_rank is bench.py's code).  Also the CPU-baseline leg
+(worker processes, fixed window) on a tiny net."""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+class _Net:
+    num_params = 777
+
+    def __init__(self):
+        self.blob = None
+        self.loaded = None
+        self.prof = False
+
+    def init_random(self, seed):
+        self.blob = (np.arange(self.num_params, dtype=np.float32) + seed) * 0.25
+
+    def get_weights(self):
+        return self.blob.copy()
+
+    def load_weights(self, blob):
+        self.loaded = np.asarray(blob, np.float32).copy()
+        self.blob = self.loaded
+
+    def profile(self, on):
+        self.prof = on
+
+    def profile_read(self):
+        return 4.0, 40 * 2, 2      # 4 ms over 80 trunk launches
+
+
+class _Mcts:
+    def profile(self, on):
+        pass
+
+    def profile_read(self):
+        return {"select_ms": 1.0, "expand_ms": 0.5, "sim_steps": 10, "select_bytes": 10 ** 6, "expand_bytes": 10 ** 5}
+
+
+class _Workload:
+    def __init__(self, a, local, shard):
+        self.shard = shard
+        self.net = _Net()
+        self.mcts = _Mcts()
+        self.steps = 0
+
+    def start(self):
+        pass
+
+    def step(self):
+        self.steps += 1
+        g = self.shard["games"]
+        return g, g * 800
+
+    def sync(self):
+        pass
+
+
+def _rank(rank, world, port, q):
+    import torch.distributed as dist
+    import bench
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), LOCAL_RANK=str(rank))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        a = bench.parse(["--gpus", str(world), "--steps", "3", "--warmup", "1"])
+        wls = []
+
+        def make(a_, local, shard):
+            wls.append(_Workload(a_, local, shard))
+            return wls[-1]
+        out = bench.run_rank(a, rank, world, dist, make, "cpu")
+        w = wls[0]
+        q.put((rank, out, w.shard, None if w.net.loaded is None else float(w.net.loaded.sum()), w.steps))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bench_rank_logic_gloo_world2():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted((q.get(timeout=180) for _ in procs), key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    (_, out0, sh0, ld0, st0), (_, out1, sh1, ld1, st1) = res
+    # C3 default: 2048 games sharded 1024 + 1024, contiguous ids, per-game seeds
+    assert (sh0["first_game"], sh0["games"], sh1["first_game"], sh1["games"]) == (0, 1024, 1024, 1024)
+    assert sh1["noise_seed"] == 42 + 1024 and sh1["noise_seed_stride"] == 1
+    # rank 0 initialised; rank 1 loaded rank 0's blob through the broadcast
+    want = float(((np.arange(777, dtype=np.float32) + 1234) * 0.25).sum())
+    assert ld0 is None and ld1 == want
+    assert st0 == st1 == 4                          # warmup + 3 timed steps
+    assert out1 is None
+    assert out0["n_gpus"] == 2 and out0["scaling"] == "strong"
+    assert out0["config"]["global_games"] == 2048 and out0["config"]["games_per_gpu"] == 1024
+    assert out0["steps"] == 3 and out0["warmup"] == 1
+    # value = all ranks' moves / slowest rank's elapsed
+    moves = 2 * 3 * 1024
+    assert abs(out0["value"] - moves / (out0["ms_per_step"] * 3 / 1e3)) < 1e-6 * out0["value"]
+    assert abs(out0["nn_evals_per_s"] / out0["value"] - 800) < 1e-6
+    # roofline from rank 0's own launches: 3 steps x 1024 boards x 40 convs / 80 launches
+    assert out0["roofline"]["boards_per_launch"] == 3 * 1024 * 800 * 40 / 80
+    assert out0["roofline"]["bound"] == "mfma" and 0 < out0["roofline"]["frac"]
+
+
+def test_bench_weak_scaling_and_configs():
+    import bench
+    a = bench.parse(["--scaling", "weak"])
+    assert a.scaling == "weak" and a.global_games == 2048
+    a = bench.parse(["--config", "c2"])
+    assert (a.board, a.blocks, a.channels, a.sims, a.global_games) == (15, 6, 64, 400, 256)
+    a = bench.parse(["--game", "go"])
+    assert (a.config, a.board, a.global_games, a.game) == ("c4", 19, 1024, "go")
+    a = bench.parse(["--games", "512"])
+    assert a.scaling == "weak" and a.global_games == 512
+    from az_amd import dist as azdist
+    parts = [azdist.shard_range(r, 3, 10) for r in range(3)]
+    assert [p["games"] for p in parts] == [4, 3, 3] and [p["first_game"] for p in parts] == [0, 4, 7]
+
+
+def test_bench_gpus_without_enough_devices_fails_loudly(monkeypatch, capsys):
+    import bench
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    assert bench.main(["--gpus", "2"]) == 2          # this container has no GPU
+    assert "only 0 GPU" in capsys.readouterr().err
+    monkeypatch.setenv("WORLD_SIZE", "1")
+    assert bench.main(["--gpus", "2"]) == 2
+    assert "WORLD_SIZE=1" in capsys.readouterr().err
+
+
+@pytest.mark.timeout(300)
+def test_cpu_baseline_workers_window():
+    import bench
+    a = bench.parse(["--board", "9", "--blocks", "1", "--channels", "16", "--sims", "20"])
+    raw = bench.cpu_baseline(a, workers=2, window=2.0)
+    assert raw["cores"] == 2 and raw["evals"] > 10 and 1.9 < raw["window_s"] < 10
+    line = bench.cpu_baseline_line(a, raw, 20.0)
+    assert line["kind"] == "port" and line["cores"] == 2
+    assert abs(line["value"] - raw["evals_per_s"] / 20.0) < 1e-9
