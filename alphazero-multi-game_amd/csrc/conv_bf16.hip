@@ -1791,7 +1791,7 @@ bool az_conv_g8_supported(int H, int W, int C, int N) {
     return H == 15 ? C % 16 == 0 : C % 32 == 0;
 }
 
-static int g_conv_flags = 4;   // bit 2: v6 (16x16x32) at 15x15 (other boards always use v6)
+static int g_conv_flags = 4 | 0x200;   // bit 2: v6 (16x16x32) at 15x15; 0x200: v7 on 15x15 boards only
 // Variant bits for A/B measurement inside one process (tools/net_bench.py --flags); none defined now
 // (a residual L2 prefetch during the main loop measured 0.6% slower and was removed; a cross-row
 // fragment prefetch and a mid-row barrier variant measured 1.5-2% slower)
@@ -1827,10 +1827,23 @@ static void v6_launch(const ConvBf16Args& a, int mode, hipStream_t st) {
     else v6_launch_g<HB, false>(a, mode, st);
 }
 
+bool az_conv_v7_supported(const ConvBf16Args& a);
+int az_conv_v7_launch(const ConvBf16Args& a, int mode, int geo15, hipStream_t st);
+
 int az_conv_g8_launch(const ConvBf16Args& a_in, int mode, hipStream_t st) {
     ConvBf16Args a = a_in;
     a.flags = g_conv_flags;
     if (a.H != a.W || !az_conv_g8_supported(a.H, a.W, a.C, a.N)) return -1;
+    if (a.a_tail == 0) a.a_tail = (size_t)a.M * a.C * 2;
+    // conv3x3_v7 (conv_v7.hip, two 256-thread blocks per CU, epilogue from registers) takes every
+    // layer it supports (trunk convs: C % 64 == 0) unless flag 0x100 selects v6 (A/B measurement);
+    // flag 0x200: v7 only on 15x15 boards; 15x15 tile geometry: SLIM (default), flag 8 DENSE, 0x400 PAD.
+    // Below 1024 boards a launch is one or two rounds of blocks and v6 is faster (B = 256: 61 vs 65 us);
+    // flag 0x800 forces v7 at any batch.
+    const int boards_g8 = a.M / (a.H * a.W);
+    if (!(g_conv_flags & 0x100) && (a.H == 15 || !(g_conv_flags & 0x200)) && (boards_g8 >= 1024 || (g_conv_flags & 0x800)) &&
+        az_conv_v7_supported(a))
+        return az_conv_v7_launch(a, mode, (g_conv_flags & 8) ? 2 : (g_conv_flags & 0x400) ? 0 : 1, st);
     const size_t HW = (size_t)a.H * a.W;
     if (a.a_tail == 0) a.a_tail = (size_t)a.M * a.C * 2;
     if (a.a_tail < (size_t)a.M * a.C * 2) return -1;

@@ -1,0 +1,436 @@
+// conv_v7.hip -- 3x3 trunk convolution of the g8 residual stream (fp16 / bf16 MFMA, gfx950).
+//
+//   out[b][n][pix] = relu( sum_{tap,c} A[b][c][pix + tap] * W[n][tap][c] + bias[n] (+ res) )
+//
+// Same data formats as conv3x3_v6 (conv_bf16.hip): activations in the g8 layout
+// [board][C/8][pixel][8] 16-bit with an int8 remainder plane of the residual stream, weights
+// chunk-blocked [C/16][9][2][N][8], zero padding read from the zeroed tail behind every
+// activation buffer (AZ_ACT_TAIL).  What changes is the shape of the work:
+//
+//  * a 256-thread block (4 waves) owns a 256-row output tile x 128 channels and needs 72 KB of
+//    LDS (halo of one 32-channel chunk double-buffered, 2 x 20 KB; a 4-slot ring of per-tap
+//    weight tiles, 4 x 8 KB), so TWO blocks share a CU.  The scheduler interleaves them: while one
+//    block sits in a barrier or in its epilogue, the other block's waves keep the SIMD's matrix
+//    pipe busy (v6 runs one 512-thread block per CU and its epilogue leaves the pipes idle);
+//  * the MFMA operands are swapped (weights as the 16-row operand, activations as the 16-column
+//    one), so a lane's accumulator holds 4 consecutive output CHANNELS of one pixel: the epilogue
+//    joins the residual, applies the ReLU, splits the result into 16 bits + int8 remainder and
+//    stores straight from registers -- no LDS staging, no block barrier, each wave on its own;
+//  * one barrier per tap.  Weight tiles land 4 taps ahead; each barrier certifies the NEXT tap's
+//    tile, so every fragment of tap s+1 is read during tap s's MFMAs (no read latency after a
+//    barrier).  The halo of chunk c+1 is fetched during taps 0..4 of chunk c.
+//
+// Tile geometry (as v6): 15x15 boards use the padded grid (outputs on a 15x17 grid, one board per
+// 256-row tile, 225 of 256 rows live) or DENSE tiles; every other board uses DENSE tiles (256
+// consecutive pixels of the batch; taps that leave the board are zeroed in the fragments).
+// The result is bit-identical to conv3x3_v6 (same products, same accumulation order).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <type_traits>
+
+#include "net.h"
+
+namespace {
+
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) void lds_void_t;
+
+template <int MODE>
+struct H16 {                                           // MODE 2: fp16, MODE 1: bf16 (as Half16, conv_bf16.hip)
+    __device__ static float to_f(uint16_t h) {
+        if (MODE == 2) { _Float16 x; __builtin_memcpy(&x, &h, 2); return (float)x; }
+        return __uint_as_float((uint32_t)h << 16);
+    }
+    __device__ static uint16_t from_f(float f) {
+        if (MODE == 2) { _Float16 x = (_Float16)f; uint16_t h; __builtin_memcpy(&h, &x, 2); return h; }
+        uint32_t u = __float_as_uint(f);
+        u += 0x7fffu + ((u >> 16) & 1u);
+        return (uint16_t)(u >> 16);
+    }
+    static constexpr int SH = 16 - (MODE == 2 ? 11 : 8);
+    __device__ static void split(float x, uint16_t& h, int8_t& q) {
+        h = from_f(x);
+        const int d = (int)(__float_as_uint(x) - __float_as_uint(to_f(h)));
+        const int r = (d + (1 << (SH - 1))) >> SH;
+        q = (int8_t)min(127, max(-127, r));
+    }
+    __device__ static float join(uint16_t h, int8_t q) {
+        return __uint_as_float(__float_as_uint(to_f(h)) + ((uint32_t)(int)q << SH));
+    }
+};
+
+__device__ __forceinline__ uint32_t lds_addr(const void* p) { return (uint32_t)(uintptr_t)p; }
+
+template <int OFF, typename F>
+__device__ __forceinline__ void ds_rd(F& d, uint32_t addr) {
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(d) : "v"(addr), "i"(OFF) : "memory");
+}
+// s_waitcnt lgkmcnt(N) with the fragments it certifies as in-out operands, so every MFMA that
+// reads them is ordered after the wait (the ds_reads are inline asm the compiler does not track)
+template <int N, typename F>
+__device__ __forceinline__ void lgkm(F (&x)[4]) {
+    asm volatile("s_waitcnt lgkmcnt(%4)" : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]) : "i"(N) : "memory");
+}
+
+__device__ __forceinline__ void wait_vm(int n) {      // s_waitcnt vmcnt(n), n wave-uniform
+    switch (n) {
+        case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+        case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+        case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+        case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+        case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+        case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+        case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+        case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
+        default: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    }
+}
+
+template <int I, int N, typename Fn>
+__device__ __forceinline__ void static_for(Fn&& f) {
+    if constexpr (I < N) {
+        f(std::integral_constant<int, I>{});
+        static_for<I + 1, N>(f);
+    }
+}
+
+// Tile geometries (one board per tile unless DENSE):
+//  GEO_PAD   outputs on an HB x (HB+2) grid: tap (dy, dx) of output row q is halo row q + dy*WG + dx
+//            of the zero-padded (HB+2)^2 halo (two dead columns per grid row; 15x15: 225 of 256 rows live)
+//  GEO_SLIM  outputs on an HB x (HB+1) grid over a halo of HB+2 rows of HB+1 columns whose column 0
+//            is zero: the one zero column is the right neighbour of x = HB-1 (the next grid row's
+//            column 0) and the left neighbour of x = 0, so no tap needs masking; one dead column per
+//            grid row (15x15: 240 rows = 15 fragments of 16; the 16th fragment of the tile reads the
+//            halo's all-zero rows >= 256 instead, so its MFMAs run on zero operands, which cost the
+//            power-limited chip little -- a branch around them would route every accumulator
+//            through phi copies and spill)
+//  GEO_DENSE 256 consecutive pixels of the batch, taps that leave the board zeroed in the fragments
+enum { GEO_PAD = 0, GEO_SLIM = 1, GEO_DENSE = 2 };
+template <int HB, int GEO>
+struct Geom7 {
+    static constexpr bool DENSE = GEO == GEO_DENSE, SLIM = GEO == GEO_SLIM;
+    static constexpr int WG = DENSE ? HB : SLIM ? HB + 1 : HB + 2;   // grid / halo row width
+    static constexpr int HW = HB * HB;
+    static constexpr int GRID = DENSE ? 256 : HB * WG;               // output grid rows of a tile
+    static constexpr int NFRAG = (GRID + 15) / 16;                   // 16-row fragments with live rows
+    static constexpr int TROWS = DENSE ? 256 + 2 * HB + 2 : SLIM ? NFRAG * 16 + 2 * WG + 2 : (HB + 2) * (HB + 2);
+    static constexpr int HROWS = 320;                         // 5 DMA pieces of 64 rows per 8-channel group
+    static_assert(TROWS <= HROWS, "halo does not fit 320 rows");
+    static_assert(GRID <= 256 && NFRAG > 8, "grid does not fit a 256-row tile");
+};
+
+}  // namespace
+
+// MODE 2: fp16 operands, MODE 1: bf16.  Requires C % 64 == 0 (an even number of 32-channel
+// chunks), N % 128 == 0, a ReLU (every g8 conv has one), no fp32 output.
+template <int MODE, int HB, int GEO>
+__global__ __launch_bounds__(256, 2) void conv3x3_v7(ConvBf16Args p) {
+    typedef H16<MODE> H;
+    typedef Geom7<HB, GEO> GM;
+    constexpr bool DENSE = GM::DENSE, SLIM = GM::SLIM;
+    typedef typename std::conditional<MODE == 2, f16x8, bf16x8>::type frag;
+    constexpr int BNT = 128, WG = GM::WG, HW = GM::HW, HROWS = GM::HROWS;
+    constexpr int A_BUF = 4 * HROWS * 16;                 // one chunk: [4 groups][320 rows][16 B] = 20 KB
+    constexpr int B_TAP = 4 * BNT * 16;                   // one tap: [4 groups][128 ch][16 B] = 8 KB
+    constexpr int LDS = 2 * A_BUF + 4 * B_TAP;            // 72 KB
+    __shared__ __attribute__((aligned(16))) uint8_t lds[LDS];
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave >> 1, wn = wave & 1;             // 128 pixels x 64 channels per wave
+    const int nsplit = p.N / BNT;
+    const int xcd = blockIdx.x % 8, slot = blockIdx.x / 8;
+    const int nb = slot % nsplit, tile = (slot / nsplit) * 8 + xcd;   // a tile's channel halves share an XCD
+    const int n0 = nb * BNT;
+    const int nboards = p.m_limit ? *p.m_limit : p.M / HW;
+    if (DENSE ? tile * 256 >= nboards * HW : tile >= nboards) return;
+    const int C = p.C, GI = C / 8, GO = p.N / 8;
+    const int NCH = C / 32, NS = 9 * NCH;
+
+    const uint32_t a_bytes = (uint32_t)p.a_tail, b_bytes = (uint32_t)((size_t)9 * C * p.N * 2);
+    const __amdgpu_buffer_rsrc_t rsA =
+        __builtin_amdgcn_make_buffer_rsrc((void*)p.Ahi, (short)0, (int)(a_bytes + AZ_ACT_TAIL * 2), 0x00020000);
+    const __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc((void*)p.Bblk, (short)0, (int)b_bytes, 0x00020000);
+    const uint32_t PAD = a_bytes;                         // zeroed tail: padding rows
+
+    // halo piece j of this wave: q = wave + 4j -> (8-channel group g, 64-row block rb); the lane's
+    // source offset is recomputed at every issue (a handful of VALU; keeping five offsets live
+    // across the main loop would spill)
+    auto a_src = [&](int j, int ln) -> uint32_t {
+        const int q = wave + 4 * j, rb = q % 5, g = q / 5;
+        const int hr = rb * 64 + ln;
+        int Y, X, b;
+        bool in;
+        if constexpr (DENSE) {                            // halo row -> pixel tile*256 - HB - 1 + hr
+            const int gpx = tile * 256 - (HB + 1) + hr;
+            b = gpx >= 0 ? gpx / HW : -1;
+            const int pix = gpx - b * HW;
+            Y = pix / HB + 1; X = pix - (Y - 1) * HB + 1;
+            in = hr < GM::TROWS && gpx >= 0;
+        } else {
+            Y = hr / WG; X = hr - Y * WG;
+            b = tile;
+            in = hr < GM::TROWS;
+        }
+        const bool ok = in && Y >= 1 && Y <= HB && X >= 1 && X <= HB && b < nboards;   // SLIM: X = 0 is the zero column
+        return ok ? (uint32_t)((((size_t)b * GI + g) * HW + (Y - 1) * HB + (X - 1)) * 16) : PAD;
+    };
+    // weight pieces: q = wave + 4j (j = 0, 1) -> (group g = q / 2, 64-channel block rb = q % 2)
+    int b_src[2], b_dst[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const int q = wave + 4 * j, rb = q & 1, g = q >> 1;
+        b_src[j] = (((g >> 1) * 18 + (g & 1)) * p.N + n0 + rb * 64) * 16;
+        b_dst[j] = g * (BNT * 16) + rb * 1024;
+    }
+    const uint32_t lane16 = lane * 16;
+    uint8_t* abuf = lds;
+    uint8_t* bbuf = lds + 2 * A_BUF;
+    // voffset = the lane's part (VGPR), soffset = the wave-uniform part (SGPR): keeps the per-tap
+    // offsets out of vector registers
+    auto issueA = [&](int j, int c, int buf) {            // piece j of chunk c's halo into A buffer `buf`
+        const int q = wave + 4 * j, rb = q % 5, g = q / 5;
+        int ln = lane;
+        asm volatile("" : "+v"(ln));                      // recompute here, do not hoist
+        const uint32_t vo = a_src(j, ln);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (lds_void_t*)(abuf + buf * A_BUF + g * (HROWS * 16) + rb * 1024),
+                                                 16, (int)vo, __builtin_amdgcn_readfirstlane(c * (4 * HW * 16)), 0, 0);
+    };
+    auto issueB = [&](int s, int slot) {                  // the wave's two pieces of tap s's weights
+        const int c = s / 9, t = s - 9 * c;
+        const int so = __builtin_amdgcn_readfirstlane((36 * c + 2 * t) * p.N * 16);
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, (lds_void_t*)(bbuf + slot * B_TAP + b_dst[j]), 16,
+                                                     (int)lane16, so + b_src[j], 0, 0);
+    };
+
+    f32x4v acc[8][4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {                         // the bias seeds the accumulators
+        const float4 bv = *reinterpret_cast<const float4*>(p.bias + n0 + wn * 64 + j * 16 + 4 * (lane >> 4));
+#pragma unroll
+        for (int i = 0; i < 8; ++i) acc[i][j] = f32x4v{bv.x, bv.y, bv.z, bv.w};
+    }
+
+    // fragment addresses: activations (MFMA column operand) at halo row wm*128 + 16i + l16 + tap
+    // shift, group l >> 4; weights (row operand) at channel wn*64 + 16j + l16, group l >> 4
+    const int l16 = lane & 15, lg = lane >> 4;
+    const uint32_t a_lane = lds_addr(abuf) + lg * (HROWS * 16) + (wm * 128 + l16) * 16;
+    const uint32_t b_lane = lds_addr(bbuf) + lg * (BNT * 16) + (wn * 64 + l16) * 16;
+    uint32_t mbits = 0;                                   // DENSE: board-edge bits of the lane's 8 pixels
+    if constexpr (DENSE) {
+#pragma unroll
+        for (int f = 0; f < 8; ++f) {
+            const int gq = tile * 256 + wm * 128 + f * 16 + l16;
+            const int pix = gq % HW, y = pix / HB, x = pix - y * HB;
+            mbits |= ((x == 0 ? 1u : 0u) | (x == HB - 1 ? 2u : 0u) | (y == 0 ? 4u : 0u) | (y == HB - 1 ? 8u : 0u)) << (4 * f);
+        }
+    }
+
+    // prologue: halo of chunk 0, weights of taps 0..3
+#pragma unroll
+    for (int j = 0; j < 5; ++j) issueA(j, 0, 0);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) issueB(s, s);
+    wait_vm(6);                                           // A(0), B(0) landed; B(1..3) may fly
+    __builtin_amdgcn_s_barrier();
+
+    frag alo[4], ahi[4], bw[2][4];
+    auto maskA = [&](frag (&a)[4], int half, int dy, int dx) {
+        if constexpr (DENSE) {
+            const uint32_t test = (dy == 0 ? 4u : dy == 2 ? 8u : 0u) | (dx == 0 ? 1u : dx == 2 ? 2u : 0u);
+            if (test) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    if (mbits & (test << (4 * (half * 4 + i)))) a[i] = frag{};
+            }
+        }
+    };
+    // fragments of tap t (compile time) of the chunk in A buffer `ab`, weights in slot `bs`
+    // SLIM: the 16th fragment (rows 240..255, no live outputs) of the second row half reads 16 rows
+    // further on, where every halo row of every tap is zero (rows >= 256: halo row Y >= 16)
+    const uint32_t z16 = (SLIM && wm == 1) ? 16 * 16 : 0;
+    auto loadA = [&](frag (&a)[4], uint32_t ab, auto tc, auto hc) {
+        constexpr int t = decltype(tc)::value, half = decltype(hc)::value;
+        constexpr int sh = (t / 3) * WG + (t % 3);
+        static_for<0, 4>([&](auto ic) {
+            constexpr int i = decltype(ic)::value;
+            if constexpr (SLIM && half == 1 && i == 3) ds_rd<((half * 4 + i) * 16 + sh) * 16>(a[i], ab + z16);
+            else ds_rd<((half * 4 + i) * 16 + sh) * 16>(a[i], ab);
+        });
+    };
+    auto loadB = [&](frag (&b)[4], uint32_t bs) {
+        static_for<0, 4>([&](auto jc) {
+            constexpr int j = decltype(jc)::value;
+            ds_rd<j * 256>(b[j], bs);
+        });
+    };
+    auto mma = [&](const frag (&a)[4], const frag (&b)[4], int half) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                if constexpr (MODE == 2)
+                    acc[half * 4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(b[j], a[i], acc[half * 4 + i][j], 0, 0, 0);
+                else
+                    acc[half * 4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a[i], acc[half * 4 + i][j], 0, 0, 0);
+            }
+        }
+    };
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
+    // tap 0 of chunk 0
+    loadB(bw[0], b_lane);
+    loadA(alo, a_lane, I0{}, I0{});
+    loadA(ahi, a_lane, I0{}, I1{});
+
+    // Two chunks per iteration: 18 taps, the weight registers alternate by tap parity.  Every tap
+    // issues the same DMA pieces (a halo piece at taps 0..4, two weight pieces), past the end as
+    // harmless reloads into free buffers, so the vmcnt budget is a compile-time constant: the
+    // weights of tap s+1 were issued in tap s-3 (the prologue for s < 3), followed by the pieces of
+    // taps s-2 and s-1.  Fragments are read one tap ahead, past the end from free buffers.
+    for (int c2 = 0; c2 < NCH; c2 += 2) {
+        static_for<0, 18>([&](auto tc18) {
+            constexpr int T = decltype(tc18)::value;      // tap of the chunk pair
+            constexpr int t = T % 9, cur = T & 1, nxt = cur ^ 1;
+            constexpr int allow = (t >= 2 && t - 2 < 5 ? 1 : 0) + (t >= 1 && t - 1 < 5 ? 1 : 0) + 4;
+            const int c = c2 + T / 9;
+            const int s = 9 * c + t;
+            if constexpr (DENSE) asm volatile("" : "+v"(mbits));   // keep the edge masks inside the loop (no SGPR hoisting)
+            // the 8 youngest LDS reads are this tap's activation fragments: the weights of tap s
+            // (read one tap ago) are in registers -- required before the barrier frees their slot
+            lgkm<8>(bw[cur]);
+            wait_vm(allow);                               // weights of tap s+1 (and at t == 8 the next halo) landed
+            __builtin_amdgcn_s_barrier();
+            __builtin_amdgcn_sched_barrier(0);
+            // DMA for later taps: a halo piece of chunk c+1 at taps 0..4 (the last chunk reloads
+            // itself into the free buffer), then the weights of tap s+4 (clamped to the last tap)
+            if constexpr (t < 5) issueA(t, c + 1 < NCH ? c + 1 : c, (c + 1) & 1);
+            issueB(s + 4 < NS ? s + 4 : NS - 1, (s + 4) & 3);
+            // weights of tap s+1 (certified by the barrier above)
+            loadB(bw[nxt], b_lane + ((s + 1) & 3) * B_TAP);
+            __builtin_amdgcn_sched_barrier(0);
+            lgkm<8>(alo);                                 // activations of tap s, low half
+            maskA(alo, 0, t / 3, t % 3);
+            mma(alo, bw[cur], 0);
+            __builtin_amdgcn_sched_barrier(0);
+            const uint32_t an = a_lane + ((t == 8 ? c + 1 : c) & 1) * A_BUF;
+            constexpr int tn = (t + 1) % 9;
+            loadA(alo, an, std::integral_constant<int, tn>{}, I0{});
+            lgkm<8>(ahi);                                 // activations of tap s, high half
+            maskA(ahi, 1, t / 3, t % 3);
+            __builtin_amdgcn_sched_barrier(0);
+            mma(ahi, bw[cur], 1);
+            __builtin_amdgcn_sched_barrier(0);
+            loadA(ahi, an, std::integral_constant<int, tn>{}, I1{});
+            __builtin_amdgcn_sched_barrier(0);
+        });
+    }
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+
+    // epilogue, straight from the accumulators: lane holds channels 4*(l >> 4) + e of pixel l16
+    // of every 16 x 16 tile; residual join, ReLU, 16-bit + int8 split, streaming stores
+    const __amdgpu_buffer_rsrc_t rh = __builtin_amdgcn_make_buffer_rsrc((void*)p.Rhi, (short)0, 0x7fffffff, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rq = __builtin_amdgcn_make_buffer_rsrc((void*)p.Rq, (short)0, 0x7fffffff, 0x00020000);
+    const int chl = n0 + wn * 64 + 4 * lg;                // first channel of the lane in tile j = 0
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const int q = wm * 128 + i * 16 + l16;            // output grid row of the tile
+        int b, pix;
+        bool live;
+        if constexpr (DENSE) {
+            const int gq = tile * 256 + q;
+            b = gq / HW;
+            pix = gq - b * HW;
+            live = b < nboards;
+        } else {
+            const int y = q / WG, x = q - y * WG;
+            b = tile;
+            pix = y * HB + x;
+            live = y < HB && x < HB;
+        }
+        if (!live) continue;
+        u32x2_t hv[4];
+        uint32_t qv[4];
+        if (p.Rhi) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int ch = chl + j * 16;
+                const size_t e = (((size_t)b * GO + (ch >> 3)) * HW + pix) * 8 + (ch & 7);
+                hv[j] = __builtin_amdgcn_raw_buffer_load_b64(rh, (int)(e * 2), 0, 2);
+                qv[j] = __builtin_amdgcn_raw_buffer_load_b32(rq, (int)e, 0, 2);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int ch = chl + j * 16;
+            const size_t e = (((size_t)b * GO + (ch >> 3)) * HW + pix) * 8 + (ch & 7);
+            float o[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+            if (p.Rhi) {
+                uint16_t hh[4];
+                int8_t qq[4];
+                __builtin_memcpy(hh, &hv[j], 8);
+                __builtin_memcpy(qq, &qv[j], 4);
+#pragma unroll
+                for (int k = 0; k < 4; ++k) o[k] += H::join(hh[k], qq[k]);
+            }
+            uint16_t oh[4];
+            int8_t oq[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                o[k] = __builtin_amdgcn_fmed3f(o[k], 0.0f, 3.0e38f);   // ReLU
+                if (p.Cq) H::split(o[k], oh[k], oq[k]);
+                else oh[k] = H::from_f(o[k]);
+            }
+            u32x2_t hs;
+            __builtin_memcpy(&hs, oh, 8);
+            asm volatile("global_store_dwordx2 %0, %1, off nt" ::"v"(p.Chi + e), "v"(hs) : "memory");
+            if (p.Cq) {
+                uint32_t qs;
+                __builtin_memcpy(&qs, oq, 4);
+                asm volatile("global_store_dword %0, %1, off nt" ::"v"(p.Cq + e), "v"(qs) : "memory");
+            }
+        }
+    }
+}
+
+// Host side ----------------------------------------------------------------------------------
+template <int HB, int GEO>
+static void v7_launch_g(const ConvBf16Args& a, int mode, hipStream_t st) {
+    const int boards = a.M / (HB * HB);
+    const int tiles = GEO == GEO_DENSE ? (boards * HB * HB + 255) / 256 : boards;
+    const int grid = (tiles + 7) / 8 * 8 * (a.N / 128);   // XCD-aware tile/half mapping: whole groups of 8
+    if (mode == 2) hipLaunchKernelGGL((conv3x3_v7<2, HB, GEO>), dim3(grid), dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((conv3x3_v7<1, HB, GEO>), dim3(grid), dim3(256), 0, st, a);
+}
+
+// true when conv3x3_v7 takes this layer
+bool az_conv_v7_supported(const ConvBf16Args& a) {
+    if (a.H != a.W || a.C % 64 || a.N % 128 || !a.relu || a.Cf || a.Clo) return false;
+    const int HB = a.H;
+    if (HB != 8 && HB != 9 && HB != 13 && HB != 15 && HB != 19) return false;
+    const size_t HW = (size_t)HB * HB;
+    // the padding offset walks C/32 chunk steps into the zeroed tail; 32-bit buffer ranges
+    return a.a_tail + AZ_ACT_TAIL * 2 < ((size_t)1 << 31) && (size_t)(a.C / 32) * 4 * HW * 16 + 16 <= AZ_ACT_TAIL * 2 &&
+           (size_t)9 * a.C * a.N * 2 < ((size_t)1 << 31);
+}
+
+// geo15: the 15x15 tile geometry (GEO_PAD / GEO_SLIM / GEO_DENSE); other boards are DENSE
+int az_conv_v7_launch(const ConvBf16Args& a, int mode, int geo15, hipStream_t st) {
+    if (!az_conv_v7_supported(a)) return -1;
+    switch (a.H) {
+        case 8: v7_launch_g<8, GEO_DENSE>(a, mode, st); return 0;
+        case 9: v7_launch_g<9, GEO_DENSE>(a, mode, st); return 0;
+        case 13: v7_launch_g<13, GEO_DENSE>(a, mode, st); return 0;
+        case 19: v7_launch_g<19, GEO_DENSE>(a, mode, st); return 0;
+        default:
+            if (geo15 == GEO_DENSE) v7_launch_g<15, GEO_DENSE>(a, mode, st);
+            else if (geo15 == GEO_PAD) v7_launch_g<15, GEO_PAD>(a, mode, st);
+            else v7_launch_g<15, GEO_SLIM>(a, mode, st);
+            return 0;
+    }
+}

@@ -1,0 +1,56 @@
+"""conv3x3_v7 (csrc/conv_v7.hip: two 256-thread blocks per CU, swapped MFMA operands, epilogue from
+registers; the default for batches of >= 1024 boards on 15x15) against conv3x3_v6 (csrc/conv_bf16.hip): same products in the same accumulation order,
+so every output of the whole network must be BITWISE equal -- on the SLIM and padded 15x15 tiles, on DENSE
+tiles of every board, for ragged batches and in both 16-bit modes.  Both kernels are also pinned to
+the fp32 reference by tests/test_gpu_net.py (v7 is the default kernel there)."""
+import numpy as np
+import pytest
+
+
+@pytest.fixture(scope="module")
+def engine():
+    import az_amd
+    return az_amd.Engine(0)
+
+
+def _flags(f):
+    from az_amd import _lib
+    _lib.lib().az_diag_set_conv_flags(int(f))
+
+
+CASES = [  # board, in_planes, actions, channels, blocks, B, flags selecting v7 (v6 = flags | 0x100)
+    (15, 11, 225, 256, 2, 37, 0xa04),     # SLIM 15x16 tile (the default), ragged batch
+    (15, 11, 225, 256, 1, 1, 0xa04),      # a single board
+    (15, 11, 225, 128, 2, 64, 0xa04),     # 128 channels (one channel half)
+    (15, 11, 225, 256, 2, 37, 0xe04),     # padded 15x17 tile
+    (15, 11, 225, 256, 2, 37, 0xa0c),     # DENSE 15x15 tiles
+    (19, 8, 362, 256, 2, 13, 0x804),      # DENSE 19x19 (Go)
+    (9, 11, 81, 128, 2, 29, 0x804),       # DENSE 9x9
+    (13, 8, 170, 256, 1, 7, 0x804),       # DENSE 13x13
+    (8, 111, 4672, 256, 2, 33, 0x804),    # DENSE 8x8 chess: the 128-channel input conv runs on v7 too
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["fp16", "bf16"])
+@pytest.mark.parametrize("case", CASES, ids=[str(c) for c in CASES])
+def test_gpu_v7_bitwise_equals_v6(engine, case, mode):
+    import az_amd
+    import net_oracle
+    bs, ci, A, ch, blocks, B, fl = case
+    prec = az_amd.AZ_PREC_FP16 if mode == "fp16" else az_amd.AZ_PREC_BF16
+    desc = az_amd.NetDesc(bs, ci, ch, blocks, A, 32, 8, 256, 1, 0, prec, B)
+    net = az_amd.HipNeuralNetwork(engine, desc)
+    net.load_weights(net_oracle.init_blob(desc, seed=31))
+    rng = np.random.default_rng(bs * 7 + B)
+    x = (rng.random((B, ci, bs, bs)) < (0.05 if ci > 16 else 0.25)).astype(np.float32)
+    try:
+        _flags(fl | 0x100)
+        l6, v6 = net.forward(x)
+        _flags(fl)
+        l7, v7 = net.forward(x)
+    finally:
+        _flags(0x204)                     # the library default
+    print(f"{case} {mode}: max|v7 - v6| logits {np.abs(l7 - l6).max():.3e} value {np.abs(v7 - v6).max():.3e}")
+    assert np.array_equal(l7, l6) and np.array_equal(v7, v6)
+    net.close()
