@@ -18,12 +18,12 @@ from dataclasses import dataclass, field
 
 import numpy as np
 
-from ._lib import (AZ_EVAL_HASH, AZ_EVAL_NET, AZ_EVAL_RANDOM, AZ_EVAL_UNIFORM, AZ_PREC_BF16, AZ_PREC_BF16X3, AZ_PREC_F32, AZ_PREC_FP16, AzError,
+from ._lib import (AZ_EVAL_CALLBACK, AZ_EVAL_HASH, AZ_EVAL_NET, AZ_EVAL_RANDOM, AZ_EVAL_UNIFORM, EVAL_FN, AZ_PREC_BF16, AZ_PREC_BF16X3, AZ_PREC_F32, AZ_PREC_FP16, AzError,
                    GAME_SINK, PROGRESS_FN, MoveRec as _lib_MoveRec, NetDesc, SearchCfg, SelfPlayCfg, check, lib)
 
 __all__ = ["Engine", "HipNeuralNetwork", "ParallelMCTS", "SelfPlayManager", "GameRecord", "MoveData", "AzError",
            "Dataset", "TrainingExample", "GAME_GOMOKU", "GAME_GO",
-           "AZ_PREC_F32", "AZ_PREC_BF16X3", "AZ_PREC_BF16", "AZ_PREC_FP16", "AZ_EVAL_NET", "AZ_EVAL_HASH", "AZ_EVAL_RANDOM", "AZ_EVAL_UNIFORM",
+           "AZ_PREC_F32", "AZ_PREC_BF16X3", "AZ_PREC_BF16", "AZ_PREC_FP16", "AZ_EVAL_NET", "AZ_EVAL_HASH", "AZ_EVAL_RANDOM", "AZ_EVAL_UNIFORM", "AZ_EVAL_CALLBACK",
            "gomoku_net_desc"]
 
 _f = ctypes.POINTER(ctypes.c_float)
@@ -157,9 +157,11 @@ class ParallelMCTS:
     def __init__(self, engine, n_games=1, board_size=15, num_simulations=800, c_puct=1.5, fpu_reduction=0.0,
                  virtual_loss=3, evaluator=AZ_EVAL_HASH, net=None, eval_seed=7, zobrist_seed=12345, noise_seed=42,
                  noise_seed_stride=0, use_dirichlet_each_search=False, dirichlet_alpha=0.03, dirichlet_eps=0.25,
-                 tt_log2=20, node_capacity=0, prior_ring=0, game=0):
+                 tt_log2=20, node_capacity=0, prior_ring=0, game=0, callback=None):
         """game: AZ_GAME_GOMOKU (0) or AZ_GAME_GO (1) -- GoState(bs 9/13/19, komi 7.5, Chinese rules,
-        superko); Go actions are -1 (pass) .. bs*bs-1 and finished games report AZ_ACTION_NONE."""
+        superko); Go actions are -1 (pass) .. bs*bs-1 and finished games report AZ_ACTION_NONE.
+        evaluator=AZ_EVAL_CALLBACK: callback(games [n], moves: list of root-to-leaf move lists,
+        planes [n][C][bs][bs]) -> (policy [n][NA] as NeuralNetwork::predict returns it, value [n])."""
         self.G = n_games
         self.bs = board_size
         self.game = game
@@ -173,6 +175,30 @@ class ParallelMCTS:
         check(lib().az_search_create(engine.h, net.h if net is not None else None, ctypes.byref(cfg), ctypes.byref(h)))
         self.h = h
         self.engine, self.net = engine, net
+        self._cb = None
+        if evaluator == AZ_EVAL_CALLBACK:
+            if callback is None:
+                raise ValueError("AZ_EVAL_CALLBACK needs a callback")
+            NA = self.A
+
+            def _eval(_user, n, games, plen, moves, max_path, planes, n_planes, pol, val):
+                try:
+                    g = np.ctypeslib.as_array(games, shape=(n,)).copy()
+                    ln = np.ctypeslib.as_array(plen, shape=(n,))
+                    mv = np.ctypeslib.as_array(moves, shape=(n, max_path))
+                    x = np.ctypeslib.as_array(planes, shape=(n, n_planes, board_size, board_size)).copy()
+                    p, v = callback(g, [mv[i, :ln[i]].tolist() for i in range(n)], x)
+                    p = np.ascontiguousarray(p, np.float32).reshape(n, NA)
+                    v = np.ascontiguousarray(v, np.float32).reshape(n)
+                    ctypes.memmove(pol, p.ctypes.data, p.nbytes)
+                    ctypes.memmove(val, v.ctypes.data, v.nbytes)
+                    return 0
+                except Exception as e:  # surfaced as AZ_ERR_STATE
+                    print("az_amd evaluator failed:", repr(e))
+                    return 1
+
+            self._cb = EVAL_FN(_eval)
+            check(lib().az_search_set_evaluator(self.h, self._cb, None))
 
     def newGames(self, games=None):
         games = np.arange(self.G, dtype=np.int32) if games is None else np.asarray(games, np.int32)
@@ -188,6 +214,30 @@ class ParallelMCTS:
 
     def search(self):
         check(lib().az_search_run(self.h))
+
+    def runSingleSimulation(self, n=1):
+        """ParallelMCTS::runSingleSimulation (parallel_mcts.cpp:276-380), n times, every game."""
+        check(lib().az_search_simulate(self.h, int(n)))
+
+    def runBatchedSearch(self):
+        """ParallelMCTS::runBatchedSearch (parallel_mcts.cpp:1531-1590): numSimulations single simulations."""
+        check(lib().az_search_simulate(self.h, self.cfg.num_simulations))
+
+    def releaseMemory(self, visitThreshold=10):
+        """ParallelMCTS::releaseMemory (parallel_mcts.cpp:1481-1496): nodes pruned per game."""
+        out = np.zeros(self.G, np.int64)
+        check(lib().az_search_release(self.h, int(visitThreshold), out.ctypes.data_as(ctypes.POINTER(ctypes.c_int64))))
+        return out
+
+    def selectActionFor(self, game, isTraining=False, temperature=1.0, legal=(), useBatchInference=True):
+        """ParallelMCTS::selectAction of one game (parallel_mcts.cpp:987-1047); with useBatchInference
+        off it draws on the game's rng_ (libstdc++ discrete / uniform_int distributions).  legal: the
+        root state's getLegalMoves(), used when the root has no children."""
+        lg = np.ascontiguousarray(legal, np.int32)
+        a = ctypes.c_int()
+        check(lib().az_search_select_action(self.h, int(game), int(bool(isTraining)), float(temperature),
+                                            int(bool(useBatchInference)), _ip(lg), int(lg.size), ctypes.byref(a)))
+        return a.value
 
     def select(self, is_training=True, temperature=1.0):
         """(actions [G], root values [G], probs [G][A] child order, child actions [G][A], n_children [G])."""

@@ -13,7 +13,7 @@ P = ctypes.POINTER
 vp = ctypes.c_void_p
 
 AZ_PREC_F32, AZ_PREC_BF16X3, AZ_PREC_BF16, AZ_PREC_FP16 = 0, 1, 2, 3
-AZ_EVAL_NET, AZ_EVAL_HASH, AZ_EVAL_RANDOM, AZ_EVAL_UNIFORM = 0, 1, 2, 3
+AZ_EVAL_NET, AZ_EVAL_HASH, AZ_EVAL_RANDOM, AZ_EVAL_UNIFORM, AZ_EVAL_CALLBACK = 0, 1, 2, 3, 4
 
 
 class NetDesc(ctypes.Structure):
@@ -38,6 +38,8 @@ class MoveRec(ctypes.Structure):
                 ("child_actions", P(c_int)), ("thinking_time_ms", c_int64)]
 
 
+EVAL_FN = ctypes.CFUNCTYPE(c_int, vp, c_int, P(c_int), P(c_int), P(c_int), c_int, P(c_float), c_int, P(c_float),
+                           P(c_float))
 GAME_SINK = ctypes.CFUNCTYPE(None, vp, c_int, c_int, c_int, P(MoveRec), c_int)
 PROGRESS_FN = ctypes.CFUNCTYPE(None, vp, c_int, c_int, c_int, c_int64)
 
@@ -63,9 +65,16 @@ EXPORTS = {
     "az_search_add_noise": (c_int, [vp, c_float, c_float]),
     "az_search_add_noise_masked": (c_int, [vp, c_float, c_float, P(ctypes.c_uint8)]),
     "az_search_run": (c_int, [vp]),
+    "az_search_simulate": (c_int, [vp, c_int]),
+    "az_search_release": (c_int, [vp, c_int, P(c_int64)]),
+    "az_search_select_action": (c_int, [vp, c_int, c_int, c_float, c_int, P(c_int), c_int, P(c_int)]),
     "az_search_select": (c_int, [vp, c_int, c_float, P(c_int), P(c_float), P(c_float), P(c_int), P(c_int)]),
     "az_search_apply": (c_int, [vp, P(c_int), P(c_int), P(c_int)]),
     "az_search_root_children": (c_int, [vp, c_int, P(c_int), P(c_int), P(c_int), P(c_float), P(c_float), P(c_int)]),
+    "az_search_root_flags": (c_int, [vp, c_int, P(c_int)]),
+    "az_search_seed": (c_int, [vp, c_int, c_uint32]),
+    "az_search_set_evaluator": (c_int, [vp, EVAL_FN, vp]),
+    "az_search_set_params": (c_int, [vp, P(SearchCfg)]),
     "az_search_root_node": (c_int, [vp, c_int, P(c_int), P(c_int), P(c_float)]),
     "az_search_counters": (c_int, [vp, c_int, P(c_int64)]),
     "az_search_profile": (c_int, [vp, c_int]),

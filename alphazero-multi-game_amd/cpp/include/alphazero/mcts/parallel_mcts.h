@@ -1,10 +1,10 @@
 // alphazero/mcts/parallel_mcts.h -- ParallelMCTS of the host API on the MI355X engine.
 // One tree (one az_search game slot) per object; search() runs the Mode S simulations of
 // parallel_mcts.cpp:276-380 on the device, bit-exact with the reference
-// for the hash / random / uniform evaluators.  Selection is always the deterministic
-// (batch-inference) rule SelfPlayManager forces (selectAction: argmax of the visit
-// distribution, first max); numThreads / batch settings are accepted and ignored (the device
-// runs one simulation per game per step, Mode S).
+// for the hash / random / uniform evaluators.  selectAction follows MCTSConfig::useBatchInference
+// as the reference does: the deterministic rules (forced by setDeterministicMode and by
+// SelfPlayManager) or libstdc++ draws on rng_ (parallel_mcts.cpp:987-1047).  numThreads / batch
+// settings are accepted and ignored (the device runs one simulation per game per step, Mode S).
 #pragma once
 #include <atomic>
 #include <functional>
@@ -14,6 +14,7 @@
 #include <vector>
 
 #include "alphazero/core/igamestate.h"
+#include "alphazero/mcts/mcts_node.h"
 #include "alphazero/mcts/transposition_table.h"
 #include "alphazero/nn/neural_network.h"
 #include "az_engine.h"
@@ -61,8 +62,9 @@ struct MCTSStats {
 };
 
 // The device evaluator a NeuralNetwork* maps to: HipNeuralNetwork -> AZ_EVAL_NET,
-// RandomPolicyNetwork(seed) -> AZ_EVAL_RANDOM, nullptr -> AZ_EVAL_UNIFORM; any other class is
-// refused (std::invalid_argument) -- there is no host-evaluated path.
+// RandomPolicyNetwork(seed) -> AZ_EVAL_RANDOM, nullptr -> AZ_EVAL_UNIFORM, any other subclass ->
+// AZ_EVAL_CALLBACK (the device search hands each simulation step's leaves to the subclass's
+// predict / predictBatch on the calling thread).
 struct DeviceEvaluator {
     int kind;
     unsigned seed;
@@ -83,6 +85,8 @@ class ParallelMCTS {
     ParallelMCTS& operator=(const ParallelMCTS&) = delete;
 
     void search();
+    void runSingleSimulation();                      // parallel_mcts.cpp:276-380
+    void runBatchedSearch();                         // :1531-1590 (numSimulations single simulations)
     int selectAction(bool isTraining = false, float temperature = 1.0f);
     std::vector<float> getActionProbabilities(float temperature = 1.0f) const;   // child order
     std::vector<int> getChildActions() const;                                    // matching actions
@@ -109,12 +113,19 @@ class ParallelMCTS {
     std::string getSearchInfo() const;
     void printSearchPath(int action) const;
     size_t getMemoryUsage() const;
+    size_t releaseMemory(int visitThreshold = 10);   // :1481-1496 (MCTSNode::pruneTree)
+    // Extension: a host snapshot of the root and its children (the reference keeps rootNode_ private)
+    MCTSNode getRootNode() const;
     std::vector<std::tuple<int, int, float, float>> analyzePosition(int topN = 10) const;   // (action, N, Q, P)
     const MCTSStats& getStats() const { return stats_; }
     az_search* handle() const { return s_; }
 
  private:
     void rebuild();           // (re)create the device search for the current config / root
+    void applyConfig();       // new parameters in place (tree kept), or rebuild
+    static int hostEvaluate(void* user, int n, const int* games, const int* pathLen, const int* moves, int maxPath,
+                            const float* planes, int nPlanes, float* policy, float* value);
+    az_search_cfg deviceConfig() const;
     MCTSConfig config_;
     nn::NeuralNetwork* nn_;
     TranspositionTable* tt_;

@@ -25,6 +25,56 @@ static std::vector<std::reference_wrapper<const core::IGameState>> stateRefs(con
     return v;
 }
 
+// Python subclasses of NeuralNetwork (a user evaluator written in Python): ParallelMCTS reaches them
+// through the AZ_EVAL_CALLBACK host evaluator.  predict / predictBatch take the GIL; predictBatch
+// may be overridden as predictBatch(states) -> (policies, values).
+class PyNeuralNetwork : public nn::NeuralNetwork {
+ public:
+    using nn::NeuralNetwork::NeuralNetwork;
+    std::pair<std::vector<float>, float> predict(const core::IGameState& s) override {
+        py::gil_scoped_acquire gil;
+        py::function f = py::get_override(static_cast<const nn::NeuralNetwork*>(this), "predict");
+        if (!f) throw std::runtime_error("NeuralNetwork subclass without predict");
+        py::object r = f(py::cast(s, py::return_value_policy::reference));
+        auto t = r.cast<py::tuple>();
+        return {t[0].cast<std::vector<float>>(), t[1].cast<float>()};
+    }
+    void predictBatch(const std::vector<std::reference_wrapper<const core::IGameState>>& states,
+                      std::vector<std::vector<float>>& policies, std::vector<float>& values) override {
+        py::gil_scoped_acquire gil;
+        py::function f = py::get_override(static_cast<const nn::NeuralNetwork*>(this), "predictBatch");
+        policies.clear();
+        values.clear();
+        if (!f) {
+            for (auto& r : states) {
+                auto pv = predict(r.get());
+                policies.push_back(pv.first);
+                values.push_back(pv.second);
+            }
+            return;
+        }
+        py::list l;
+        for (auto& r : states) l.append(py::cast(r.get(), py::return_value_policy::reference));
+        auto t = f(l).cast<py::tuple>();
+        policies = t[0].cast<std::vector<std::vector<float>>>();
+        values = t[1].cast<std::vector<float>>();
+    }
+    std::future<std::pair<std::vector<float>, float>> predictAsync(const core::IGameState& s) override {
+        std::promise<std::pair<std::vector<float>, float>> p;
+        p.set_value(predict(s));
+        return p.get_future();
+    }
+    bool isGpuAvailable() const override { return false; }
+    std::string getDeviceInfo() const override { return "python"; }
+    float getInferenceTimeMs() const override { return 0.0f; }
+    int getBatchSize() const override { return 1; }
+    std::string getModelInfo() const override { return "Python NeuralNetwork subclass"; }
+    size_t getModelSizeBytes() const override { return 0; }
+    void benchmark(int, int) override {}
+    void enableDebugMode(bool) override {}
+    void printModelSummary() const override {}
+};
+
 PYBIND11_MODULE(_alphazero_cpp, m) {
     m.doc() = "AlphaZero multi-game engine, MI355X (HIP) backend";
 
@@ -83,7 +133,8 @@ PYBIND11_MODULE(_alphazero_cpp, m) {
     m.def("createGameState", &core::createGameState, py::arg("type"), py::arg("boardSize") = 0,
           py::arg("variantRules") = false);
 
-    py::class_<nn::NeuralNetwork>(m, "NeuralNetwork")
+    py::class_<nn::NeuralNetwork, PyNeuralNetwork>(m, "NeuralNetwork")
+        .def(py::init<>())
         .def("predict", [](nn::NeuralNetwork& self, const core::IGameState& s) {
             py::gil_scoped_release release;
             return self.predict(s);
@@ -200,6 +251,27 @@ PYBIND11_MODULE(_alphazero_cpp, m) {
         .def("clear", &mcts::TranspositionTable::clear)
         .def("resize", &mcts::TranspositionTable::resize);
 
+    // python_bindings.cpp:245-253 of the reference; here a host snapshot (ParallelMCTS.getRootNode)
+    py::class_<mcts::MCTSNode, std::shared_ptr<mcts::MCTSNode>>(m, "MCTSNode")
+        .def("getUcbScore", &mcts::MCTSNode::getUcbScore, py::arg("cPuct"), py::arg("currentPlayer"),
+             py::arg("fpuReduction") = 0.0f, py::arg("parentVisits") = 0)
+        .def("getTerminalValue", &mcts::MCTSNode::getTerminalValue)
+        .def("getValue", &mcts::MCTSNode::getValue)
+        .def("getBestAction", &mcts::MCTSNode::getBestAction)
+        .def("getBestActions", &mcts::MCTSNode::getBestActions)
+        .def("getVisitCountDistribution", &mcts::MCTSNode::getVisitCountDistribution, py::arg("temperature") = 1.0f)
+        .def("toString", &mcts::MCTSNode::toString, py::arg("maxDepth") = 1)
+        .def("hasChildren", &mcts::MCTSNode::hasChildren)
+        .def_readonly("visitCount", &mcts::MCTSNode::visitCount)
+        .def_readonly("valueSum", &mcts::MCTSNode::valueSum)
+        .def_readonly("virtualLoss", &mcts::MCTSNode::virtualLoss)
+        .def_readonly("prior", &mcts::MCTSNode::prior)
+        .def_readonly("action", &mcts::MCTSNode::action)
+        .def_readonly("isExpanded", &mcts::MCTSNode::isExpanded)
+        .def_readonly("isTerminal", &mcts::MCTSNode::isTerminal)
+        .def_readonly("actions", &mcts::MCTSNode::actions)
+        .def_readonly("children", &mcts::MCTSNode::children);
+
     py::class_<mcts::ParallelMCTS>(m, "ParallelMCTS")
         .def(py::init<const core::IGameState&, nn::NeuralNetwork*, mcts::TranspositionTable*, int, int, float, float, int>(),
              py::arg("rootState"), py::arg("nn") = nullptr, py::arg("tt") = nullptr, py::arg("numThreads") = 1,
@@ -212,6 +284,16 @@ PYBIND11_MODULE(_alphazero_cpp, m) {
             py::gil_scoped_release release;
             self.search();
         })
+        .def("runSingleSimulation", [](mcts::ParallelMCTS& self) {
+            py::gil_scoped_release release;
+            self.runSingleSimulation();
+        })
+        .def("runBatchedSearch", [](mcts::ParallelMCTS& self) {
+            py::gil_scoped_release release;
+            self.runBatchedSearch();
+        })
+        .def("releaseMemory", &mcts::ParallelMCTS::releaseMemory, py::arg("visitThreshold") = 10)
+        .def("getRootNode", &mcts::ParallelMCTS::getRootNode)
         .def("selectAction", &mcts::ParallelMCTS::selectAction, py::arg("isTraining") = false, py::arg("temperature") = 1.0f)
         .def("getActionProbabilities", &mcts::ParallelMCTS::getActionProbabilities, py::arg("temperature") = 1.0f)
         .def("getChildActions", &mcts::ParallelMCTS::getChildActions)

@@ -4,6 +4,7 @@
 #include <algorithm>
 #include <cmath>
 #include <iostream>
+#include <random>
 #include <sstream>
 
 #include "alphazero/games/go/go_state.h"
@@ -35,8 +36,54 @@ DeviceEvaluator deviceEvaluator(nn::NeuralNetwork* nn) {
     if (!nn) return {AZ_EVAL_UNIFORM, 0u, nullptr, nn::engineForDevice(-1)};
     if (auto* h = dynamic_cast<nn::HipNeuralNetwork*>(nn)) return {AZ_EVAL_NET, 0u, h->handle(), h->engine()};
     if (auto* r = dynamic_cast<nn::RandomPolicyNetwork*>(nn)) return {AZ_EVAL_RANDOM, r->seed(), nullptr, nn::engineForDevice(-1)};
-    throw std::invalid_argument("ParallelMCTS: evaluator class has no device implementation "
-                                "(use HipNeuralNetwork, RandomPolicyNetwork or nullptr)");
+    // any other NeuralNetwork subclass: the device search hands its leaves to the host
+    // (AZ_EVAL_CALLBACK, ParallelMCTS::hostEvaluate)
+    return {AZ_EVAL_CALLBACK, 0u, nullptr, nn::engineForDevice(-1)};
+}
+
+// AZ_EVAL_CALLBACK trampoline: every leaf is the root state plus the moves from the root; one leaf
+// goes to nn_->predict as evaluateState calls it (parallel_mcts.cpp:886-901), several to
+// predictBatch.  A throwing evaluator gets the reference's fallback: uniform policy, value 0.
+int ParallelMCTS::hostEvaluate(void* user, int n, const int* games, const int* pathLen, const int* moves, int maxPath,
+                               const float* planes, int nPlanes, float* policy, float* value) {
+    auto* self = static_cast<ParallelMCTS*>(user);
+    const int A = self->root_->getActionSpaceSize();
+    std::vector<std::unique_ptr<core::IGameState>> leaves;
+    leaves.reserve(n);
+    for (int i = 0; i < n; ++i) {
+        auto st = self->root_->clone();
+        for (int k = 0; k < pathLen[i]; ++k) st->makeMove(moves[(size_t)i * maxPath + k]);
+        leaves.push_back(std::move(st));
+    }
+    auto fallback = [&](int i) {
+        for (int a = 0; a < A; ++a) policy[(size_t)i * A + a] = 1.0f / (float)A;
+        value[i] = 0.0f;
+    };
+    auto put = [&](int i, const std::vector<float>& p, float v) {
+        for (int a = 0; a < A; ++a) policy[(size_t)i * A + a] = a < (int)p.size() ? p[a] : 0.0f;
+        value[i] = v;
+    };
+    if (n == 1) {
+        try {
+            auto pv = self->nn_->predict(*leaves[0]);
+            put(0, pv.first, pv.second);
+        } catch (const std::exception&) { fallback(0); }
+        return 0;
+    }
+    std::vector<std::reference_wrapper<const core::IGameState>> refs;
+    for (auto& l : leaves) refs.emplace_back(*l);
+    std::vector<std::vector<float>> ps;
+    std::vector<float> vs;
+    try {
+        self->nn_->predictBatch(refs, ps, vs);
+        for (int i = 0; i < n; ++i) {
+            if (i < (int)ps.size() && i < (int)vs.size()) put(i, ps[i], vs[i]);
+            else fallback(i);
+        }
+    } catch (const std::exception&) {
+        for (int i = 0; i < n; ++i) fallback(i);
+    }
+    return 0;
 }
 
 ParallelMCTS::ParallelMCTS(const core::IGameState& root, nn::NeuralNetwork* nn, TranspositionTable* tt, int numThreads,
@@ -60,15 +107,8 @@ ParallelMCTS::~ParallelMCTS() {
     if (s_) az_search_destroy(s_);
 }
 
-void ParallelMCTS::rebuild() {
+az_search_cfg ParallelMCTS::deviceConfig() const {
     const bool go = root_->getGameType() == core::GameType::GO;
-    if (!go && root_->getGameType() != core::GameType::GOMOKU) throw std::invalid_argument("ParallelMCTS: Gomoku or Go");
-    if (go) {
-        auto* g = dynamic_cast<const go::GoState*>(root_.get());
-        if (!g || g->getKomi() != 7.5f || !g->isChineseRules() || !g->isEnforcingSuperko())
-            throw std::invalid_argument("ParallelMCTS: the device Go rules are komi 7.5, Chinese rules, superko");
-    }
-    if (s_) { az_search_destroy(s_); s_ = nullptr; }
     const DeviceEvaluator ev = deviceEvaluator(nn_);
     az_search_cfg c{};
     c.game = go ? AZ_GAME_GO : AZ_GAME_GOMOKU;
@@ -90,7 +130,31 @@ void ParallelMCTS::rebuild() {
     int k = 0;
     while (((size_t)1 << k) < ttsize && k < 24) ++k;
     c.tt_log2 = k;
+    return c;
+}
+
+// The reference's setters change config_ and keep the tree (parallel_mcts.h:172-182); the device
+// handle takes the new parameters in place when it can, and is rebuilt (history replayed) when the
+// evaluator, the table size or a larger node pool is needed.
+void ParallelMCTS::applyConfig() {
+    const az_search_cfg c = deviceConfig();
+    if (s_ && az_search_set_params(s_, &c) == 0) return;
+    rebuild();
+}
+
+void ParallelMCTS::rebuild() {
+    const bool go = root_->getGameType() == core::GameType::GO;
+    if (!go && root_->getGameType() != core::GameType::GOMOKU) throw std::invalid_argument("ParallelMCTS: Gomoku or Go");
+    if (go) {
+        auto* g = dynamic_cast<const go::GoState*>(root_.get());
+        if (!g || g->getKomi() != 7.5f || !g->isChineseRules() || !g->isEnforcingSuperko())
+            throw std::invalid_argument("ParallelMCTS: the device Go rules are komi 7.5, Chinese rules, superko");
+    }
+    if (s_) { az_search_destroy(s_); s_ = nullptr; }
+    const DeviceEvaluator ev = deviceEvaluator(nn_);
+    const az_search_cfg c = deviceConfig();
     check(az_search_create(ev.engine, ev.net, &c, &s_), "az_search_create");
+    if (c.eval_kind == AZ_EVAL_CALLBACK) check(az_search_set_evaluator(s_, &ParallelMCTS::hostEvaluate, this), "az_search_set_evaluator");
     const int g0 = 0;
     check(az_search_new_games(s_, &g0, 1), "az_search_new_games");
     // a non-initial root: replay its history (each move a fresh root, as updateWithMove without a search)
@@ -116,15 +180,56 @@ void ParallelMCTS::search() {
     if (progress_) progress_(config_.numSimulations, config_.numSimulations);
 }
 
+void ParallelMCTS::runSingleSimulation() {
+    check(az_search_simulate(s_, 1), "az_search_simulate");
+    searched_ = true;
+}
+
+void ParallelMCTS::runBatchedSearch() {
+    if (config_.numSimulations <= 0) return;
+    check(az_search_simulate(s_, config_.numSimulations), "az_search_simulate");
+    searched_ = true;
+}
+
+size_t ParallelMCTS::releaseMemory(int visitThreshold) {
+    int64_t pruned = 0;
+    check(az_search_release(s_, visitThreshold, &pruned), "az_search_release");
+    return (size_t)pruned;
+}
+
 int ParallelMCTS::selectAction(bool isTraining, float temperature) {
-    int act = -1, nch = 0;
-    float val = 0.0f;
-    const int A = root_->getActionSpaceSize();
-    std::vector<float> probs(A);
-    std::vector<int> cact(A);
-    check(az_search_select(s_, isTraining ? 1 : 0, temperature, &act, &val, probs.data(), cact.data(), &nch),
-          "az_search_select");
+    int flags = 0;
+    check(az_search_root_flags(s_, 0, &flags), "az_search_root_flags");
+    if (!(flags & AZ_NODE_EXPANDED)) search();        // parallel_mcts.cpp:988-991
+    const std::vector<int> legal = root_->getLegalMoves();
+    int act = -1;
+    check(az_search_select_action(s_, 0, isTraining ? 1 : 0, temperature, config_.useBatchInference ? 1 : 0,
+                                  legal.data(), (int)legal.size(), &act),
+          "az_search_select_action");
     return act;
+}
+
+MCTSNode ParallelMCTS::getRootNode() const {
+    MCTSNode r;
+    int flags = 0;
+    check(az_search_root_flags(s_, 0, &flags), "az_search_root_flags");
+    check(az_search_root_node(s_, 0, &r.visitCount, &r.virtualLoss, &r.valueSum), "az_search_root_node");
+    r.isExpanded = (flags & AZ_NODE_EXPANDED) != 0;
+    r.isTerminal = (flags & AZ_NODE_TERMINAL) != 0;
+    r.gameResult = r.isTerminal ? (core::GameResult)((flags >> 2) & 3) : root_->getGameResult();
+    r.prior = 0.0f;
+    const int A = root_->getActionSpaceSize();
+    std::vector<int> act(A), N(A), VL(A);
+    std::vector<float> W(A), P(A);
+    int n = 0;
+    check(az_search_root_children(s_, 0, act.data(), N.data(), VL.data(), W.data(), P.data(), &n), "az_search_root_children");
+    for (int i = 0; i < n; ++i) {
+        auto c = std::make_shared<MCTSNode>();
+        c->visitCount = N[i]; c->virtualLoss = VL[i]; c->valueSum = W[i]; c->prior = P[i]; c->action = act[i];
+        r.actions.push_back(act[i]);
+        r.children.push_back(c);
+    }
+    return r;
 }
 
 std::vector<float> ParallelMCTS::getActionProbabilities(float temperature) const {
@@ -171,16 +276,19 @@ void ParallelMCTS::addDirichletNoise(float alpha, float epsilon) {
     check(az_search_add_noise(s_, alpha, epsilon), "az_search_add_noise");
 }
 
-void ParallelMCTS::setNumSimulations(int n) { config_.numSimulations = n; rebuild(); }
-void ParallelMCTS::setCPuct(float c) { config_.cPuct = c; rebuild(); }
-void ParallelMCTS::setFpuReduction(float f) { config_.fpuReduction = f; rebuild(); }
-void ParallelMCTS::setVirtualLoss(int v) { config_.virtualLoss = v; rebuild(); }
+void ParallelMCTS::setNumSimulations(int n) { config_.numSimulations = n; applyConfig(); }
+void ParallelMCTS::setCPuct(float c) { config_.cPuct = c; applyConfig(); }
+void ParallelMCTS::setFpuReduction(float f) { config_.fpuReduction = f; applyConfig(); }
+void ParallelMCTS::setVirtualLoss(int v) { config_.virtualLoss = v; applyConfig(); }
 void ParallelMCTS::setNeuralNetwork(nn::NeuralNetwork* nn) { nn_ = nn; rebuild(); }
 void ParallelMCTS::setTranspositionTable(TranspositionTable* tt) { tt_ = tt; rebuild(); }
-void ParallelMCTS::setConfig(const MCTSConfig& config) { config_ = config; rebuild(); }
+void ParallelMCTS::setConfig(const MCTSConfig& config) { config_ = config; applyConfig(); }
+// parallel_mcts.cpp:1263-1274: useBatchInference = enable; rng_ seeded 42, or from std::random_device
 void ParallelMCTS::setDeterministicMode(bool enable) {
     config_.deterministic = enable;
-    config_.useBatchInference = config_.useBatchInference || enable;   // the device rule is already deterministic
+    config_.useBatchInference = enable;
+    std::random_device rd;
+    check(az_search_seed(s_, 0, enable ? 42u : rd()), "az_search_seed");
 }
 
 std::vector<std::tuple<int, int, float, float>> ParallelMCTS::analyzePosition(int topN) const {

@@ -31,6 +31,8 @@ __global__ void k_select_action(TreeDev t, int training, float temperature, cons
                                 int* child_actions, int* nchild);
 __global__ void k_apply(TreeDev t, const int* actions, int* terminal, int* result);
 __global__ void k_compact(TreeDev t, Nodes dst, int* src_of);
+__global__ void k_leaf_moves(TreeDev t, int* moves, int* len);
+__global__ void k_prune(TreeDev t, Nodes dst, int* src_of, int thr, long long* pruned);
 __global__ void k_noise(TreeDev t, const float* noise, const uint8_t* mask, float eps);
 __global__ void k_new_games(TreeDev t, const int* games, const int* seed_ids, int n, uint32_t eval_seed);
 __global__ void k_tt_clear(TreeDev t, const int* games, int n);
@@ -420,6 +422,11 @@ struct az_search {
     int cur = 0;
     int* d_src_of = nullptr;
     float* d_batch = nullptr;       // gathered NHWC16 planes [G][A][16]
+    // AZ_EVAL_CALLBACK: host evaluator, leaf moves / lengths and host staging
+    az_eval_fn eval_fn = nullptr; void* eval_user = nullptr;
+    int* d_lmoves = nullptr; int* d_llen = nullptr;
+    std::vector<float> h_planes, h_nchw, h_pol, h_val;
+    std::vector<int> h_games, h_lmoves, h_llen;
     float* d_logits = nullptr; float* d_value = nullptr;
     float* d_noise = nullptr; uint8_t* d_mask = nullptr;
     int* d_actions = nullptr; float* d_values = nullptr; float* d_probs = nullptr; int* d_cact = nullptr; int* d_nch = nullptr;
@@ -463,6 +470,39 @@ static hipEvent_t prof_event(az_search* s) {
     return s->evpool[s->evused++];
 }
 
+// AZ_EVAL_CALLBACK: the leaves that need an evaluation go to the host evaluator as (game, moves
+// from the root, NCHW feature planes); its policies / values come back for k_expand_backup.
+int host_evaluate(az_search* s) {
+    hipStream_t st = s->e->stream;
+    const int G = s->c.n_games, A = s->t.A, NA = s->t.NA, C = s->t.game == GAME_GO ? 8 : 11;
+    hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, st, s->t);
+    int n = 0;
+    HIPCHK(hipMemcpyAsync(&n, s->t.n_eval, 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    if (n == 0) return 0;
+    if (!s->eval_fn) return az_fail(AZ_ERR_STATE, "AZ_EVAL_CALLBACK search without az_search_set_evaluator");
+    az_launch_gather_planes(s->t.planes, s->d_batch, s->t.eval_games, s->t.n_eval, A * 16, G, st);
+    hipLaunchKernelGGL(k_leaf_moves, dim3(G), dim3(64), 0, st, s->t, s->d_lmoves, s->d_llen);
+    s->h_planes.resize((size_t)n * A * 16); s->h_games.resize(n); s->h_lmoves.resize((size_t)n * AZ_DMAX); s->h_llen.resize(n);
+    HIPCHK(hipMemcpyAsync(s->h_planes.data(), s->d_batch, (size_t)n * A * 16 * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(s->h_games.data(), s->t.eval_games, (size_t)n * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(s->h_lmoves.data(), s->d_lmoves, (size_t)n * AZ_DMAX * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(s->h_llen.data(), s->d_llen, (size_t)n * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    s->h_nchw.resize((size_t)n * C * A);
+    for (int i = 0; i < n; ++i)
+        for (int c = 0; c < C; ++c)
+            for (int a = 0; a < A; ++a) s->h_nchw[((size_t)i * C + c) * A + a] = s->h_planes[((size_t)i * A + a) * 16 + c];
+    s->h_pol.assign((size_t)n * NA, 0.0f);
+    s->h_val.assign(n, 0.0f);
+    if (s->eval_fn(s->eval_user, n, s->h_games.data(), s->h_llen.data(), s->h_lmoves.data(), AZ_DMAX, s->h_nchw.data(), C,
+                   s->h_pol.data(), s->h_val.data()) != 0)
+        return az_fail(AZ_ERR_STATE, "host evaluator failed");
+    HIPCHK(hipMemcpyAsync(s->d_logits, s->h_pol.data(), (size_t)n * NA * 4, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(s->d_value, s->h_val.data(), (size_t)n * 4, hipMemcpyHostToDevice, st));
+    return 0;
+}
+
 int search_step(az_search* s, int mode) {
     hipStream_t st = s->e->stream;
     const int G = s->c.n_games;
@@ -471,6 +511,9 @@ int search_step(az_search* s, int mode) {
     if (prof) HIPCHK(hipEventRecord(prof_event(s), st));
     hipLaunchKernelGGL(k_select, dim3(G), dim3(64), 0, st, s->t, mode);
     if (prof) HIPCHK(hipEventRecord(prof_event(s), st));
+    if (s->c.eval_kind == AZ_EVAL_CALLBACK) {
+        if (int r = host_evaluate(s)) return r;
+    }
     if (s->c.eval_kind == AZ_EVAL_NET) {
         hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, st, s->t);
         az_launch_gather_planes(s->t.planes, s->d_batch, s->t.eval_games, s->t.n_eval, s->t.A * 16, G, st);
@@ -855,7 +898,7 @@ int az_search_create(az_engine* e, az_net* net, const az_search_cfg* c, az_searc
     const bool go = c->game == AZ_GAME_GO;
     const int NA = go ? A + 1 : A;
     if (bs < 3 || A > AZ_MAXA || G < 1 || c->num_simulations < 0 || c->virtual_loss < 0 || c->tt_log2 < 4 ||
-        c->tt_log2 > 24 || c->eval_kind < 0 || c->eval_kind > 3 || (c->game != AZ_GAME_GOMOKU && !go))
+        c->tt_log2 > 24 || c->eval_kind < 0 || c->eval_kind > 4 || (c->game != AZ_GAME_GOMOKU && !go))
         return az_fail(AZ_ERR_ARG, "unsupported search configuration");
     if (go && bs != 9 && bs != 13 && bs != 19)
         return az_fail(AZ_ERR_ARG, "Go board %d: GoState supports 9, 13 and 19 (go_state.cpp:24-26)", bs);
@@ -902,7 +945,10 @@ int az_search_create(az_engine* e, az_net* net, const az_search_cfg* c, az_searc
     if (c->eval_kind == AZ_EVAL_RANDOM) SA(t.mt, (size_t)G * 625);
     SA(t.err, 1);
     SA(s->d_src_of, NG);
-    if (c->eval_kind == AZ_EVAL_NET) { SA(s->d_batch, (size_t)G * A * 16); SA(s->d_logits, (size_t)G * NA); SA(s->d_value, G); }
+    if (c->eval_kind == AZ_EVAL_NET || c->eval_kind == AZ_EVAL_CALLBACK) {
+        SA(s->d_batch, (size_t)G * A * 16); SA(s->d_logits, (size_t)G * NA); SA(s->d_value, G);
+    }
+    if (c->eval_kind == AZ_EVAL_CALLBACK) { SA(s->d_lmoves, (size_t)G * AZ_DMAX); SA(s->d_llen, G); }
     SA(s->d_noise, (size_t)G * NA); SA(s->d_mask, G); SA(s->d_actions, G); SA(s->d_values, G); SA(s->d_probs, (size_t)G * NA);
     SA(s->d_cact, (size_t)G * NA); SA(s->d_nch, G); SA(s->d_term, G); SA(s->d_res, G); SA(s->d_games, G); SA(s->d_seed_ids, G); SA(s->d_temps, G);
 #undef SA
@@ -965,7 +1011,7 @@ void az_search_destroy(az_search* s) {
                           (const void*)t.ring_buf, (const void*)t.ring_cur, (const void*)t.cnt, (const void*)t.zpiece,
                           (const void*)t.zplayer, (const void*)t.fresh_order, (const void*)t.mt, (const void*)t.err,
                           (const void*)t.rko, (const void*)t.rpass, (const void*)t.rposh, (const void*)t.rnposh,
-                          (const void*)t.zko,
+                          (const void*)t.zko, (const void*)s->d_lmoves, (const void*)s->d_llen,
                           (const void*)t.log_pol, (const void*)t.log_val, (const void*)t.log_planes, (const void*)t.log_n,
                           (const void*)s->d_src_of, (const void*)s->d_batch, (const void*)s->d_logits,
                           (const void*)s->d_value, (const void*)s->d_noise, (const void*)s->d_mask, (const void*)s->d_actions,
@@ -1011,6 +1057,98 @@ int az_search_select(az_search* s, int training, float temperature, int* actions
     return search_select(s, training, nullptr, temperature, actions, root_values, probs, children_actions, n_children);
 }
 
+int az_search_simulate(az_search* s, int n) {
+    if (!s || n < 0) return az_fail(AZ_ERR_ARG, "bad argument");
+    std::lock_guard<std::mutex> lk(s->mu);
+    HIPCHK(hipSetDevice(s->e->device));
+    for (int i = 0; i < n; ++i)
+        if (int r = search_step(s, MODE_SIM)) return r;
+    return check_err(s);
+}
+
+int az_search_release(az_search* s, int threshold, int64_t* pruned) {
+    if (!s) return az_fail(AZ_ERR_ARG, "null search");
+    std::lock_guard<std::mutex> lk(s->mu);
+    HIPCHK(hipSetDevice(s->e->device));
+    hipStream_t st = s->e->stream;
+    const int G = s->c.n_games;
+    long long* d_pr = nullptr;
+    DALLOC(d_pr, G);
+    s->t.nd = s->arena[s->cur];
+    hipLaunchKernelGGL(k_prune, dim3(G), dim3(64), 0, st, s->t, s->arena[s->cur ^ 1], s->d_src_of, threshold, d_pr);
+    s->cur ^= 1;
+    s->t.nd = s->arena[s->cur];
+    std::vector<long long> pr(G);
+    hipError_t e1 = hipGetLastError();
+    hipError_t e2 = hipMemcpyAsync(pr.data(), d_pr, (size_t)G * 8, hipMemcpyDeviceToHost, st);
+    hipError_t e3 = hipStreamSynchronize(st);
+    hipFree(d_pr);
+    if (e1 != hipSuccess || e2 != hipSuccess || e3 != hipSuccess)
+        return az_fail(AZ_ERR_HIP, "az_search_release: %s", hipGetErrorString(e1 != hipSuccess ? e1 : e2 != hipSuccess ? e2 : e3));
+    if (pruned) for (int g = 0; g < G; ++g) pruned[g] = pr[g];
+    return check_err(s);
+}
+
+int az_search_select_action(az_search* s, int game, int training, float temperature, int batch_inference,
+                            const int* legal, int n_legal, int* action) {
+    if (!s || !action || game < 0 || game >= s->c.n_games || n_legal < 0 || (n_legal > 0 && !legal))
+        return az_fail(AZ_ERR_ARG, "bad argument");
+    std::lock_guard<std::mutex> lk(s->mu);
+    HIPCHK(hipSetDevice(s->e->device));
+    const int G = s->c.n_games, NA = s->t.NA;
+    std::vector<int> acts(G), cact((size_t)G * NA), nch(G);
+    std::vector<float> vals(G), probs((size_t)G * NA);
+    const bool stoch = training && temperature > 0.0f;
+    if (int r = search_select(s, training ? 1 : 0, nullptr, temperature, acts.data(), vals.data(), probs.data(), cact.data(),
+                              nch.data()))
+        return r;
+    std::mt19937& rng = s->rng[game];
+    const int nc = nch[game];
+    if (nc == 0) {                                   // no children: a legal move (parallel_mcts.cpp:994-1010)
+        if (n_legal == 0) { *action = -1; return 0; }
+        if (batch_inference) { *action = legal[0]; return 0; }
+        std::uniform_int_distribution<size_t> dist(0, (size_t)n_legal - 1);
+        *action = legal[dist(rng)];
+        return 0;
+    }
+    const int* ca = cact.data() + (size_t)game * NA;
+    if (batch_inference) { *action = acts[game]; return 0; }   // k_select_action: the deterministic rules
+    if (stoch) {                                     // sample the visit distribution (:1013-1027)
+        const float* pd = probs.data() + (size_t)game * NA;
+        std::discrete_distribution<int> dist(pd, pd + nc);
+        *action = ca[dist(rng)];
+        return 0;
+    }
+    // evaluation or T = 0: the most visited children, one at random when tied (:1028-1046)
+    std::vector<int> N(NA), act(NA), VL(NA);
+    std::vector<float> W(NA), P(NA);
+    int n = 0;
+    s->t.nd = s->arena[s->cur];
+    int* d_tmp = nullptr;
+    DALLOC(d_tmp, 4 * (size_t)NA + 8);
+    float* d_f = nullptr;
+    if (int r = dalloc(&d_f, 2 * (size_t)NA + 4)) { hipFree(d_tmp); return r; }
+    hipStream_t st = s->e->stream;
+    hipLaunchKernelGGL(k_root_children, dim3(1), dim3(64), 0, st, s->t, game, d_tmp, d_tmp + NA, d_tmp + 2 * NA, d_f,
+                       d_f + NA, d_tmp + 3 * NA, d_tmp + 3 * NA + 1, d_f + 2 * NA);
+    hipError_t e1 = hipMemcpyAsync(act.data(), d_tmp, NA * 4, hipMemcpyDeviceToHost, st);
+    hipError_t e2 = hipMemcpyAsync(N.data(), d_tmp + NA, NA * 4, hipMemcpyDeviceToHost, st);
+    hipError_t e3 = hipMemcpyAsync(&n, d_tmp + 3 * NA, 4, hipMemcpyDeviceToHost, st);
+    hipError_t e4 = hipStreamSynchronize(st);
+    hipFree(d_tmp); hipFree(d_f);
+    if (e1 != hipSuccess || e2 != hipSuccess || e3 != hipSuccess || e4 != hipSuccess)
+        return az_fail(AZ_ERR_HIP, "az_search_sample_action: root children readback failed");
+    int mx = 0;
+    for (int i = 0; i < n; ++i) mx = std::max(mx, N[i]);
+    std::vector<int> best;
+    for (int i = 0; i < n; ++i) if (N[i] == mx) best.push_back(act[i]);
+    if (best.empty()) { *action = -1; return 0; }
+    if (best.size() == 1) { *action = best[0]; return 0; }
+    std::uniform_int_distribution<size_t> dist(0, best.size() - 1);
+    *action = best[dist(rng)];
+    return 0;
+}
+
 int az_search_apply(az_search* s, const int* actions, int* terminal, int* result) {
     if (!s || !actions) return az_fail(AZ_ERR_ARG, "null argument");
     std::lock_guard<std::mutex> lk(s->mu);
@@ -1043,6 +1181,57 @@ int az_search_root_children(az_search* s, int game, int* actions, int* N, int* V
     if (P) HIPCHK(hipMemcpy(P, dP, n * 4, hipMemcpyDeviceToHost));
     *n_children = n;
     for (void* p : {(void*)da, (void*)dN, (void*)dVL, (void*)dn, (void*)dri, (void*)dW, (void*)dP, (void*)drw}) hipFree(p);
+    return 0;
+}
+
+int az_search_set_evaluator(az_search* s, az_eval_fn fn, void* user) {
+    if (!s) return az_fail(AZ_ERR_ARG, "null search");
+    if (s->c.eval_kind != AZ_EVAL_CALLBACK) return az_fail(AZ_ERR_STATE, "the handle was not created with AZ_EVAL_CALLBACK");
+    std::lock_guard<std::mutex> lk(s->mu);
+    s->eval_fn = fn; s->eval_user = user;
+    return 0;
+}
+
+int az_search_set_params(az_search* s, const az_search_cfg* c) {
+    if (!s || !c) return az_fail(AZ_ERR_ARG, "null argument");
+    std::lock_guard<std::mutex> lk(s->mu);
+    const az_search_cfg& o = s->c;
+    if (c->n_games != o.n_games || c->board_size != o.board_size || c->eval_kind != o.eval_kind ||
+        c->eval_seed != o.eval_seed || c->zobrist_seed != o.zobrist_seed || c->tt_log2 != o.tt_log2 ||
+        c->game != o.game || (c->node_capacity > 0 && c->node_capacity != o.node_capacity) ||
+        (c->prior_ring > 0 && c->prior_ring != o.prior_ring) || c->num_simulations < 0 || c->virtual_loss < 0)
+        return az_fail(AZ_ERR_ARG, "az_search_set_params: shape / evaluator / table changes need a new handle");
+    // the node pool and prior ring were sized for the creation's simulations per search
+    const int NA = s->t.NA;
+    if (3 * std::max(64, c->num_simulations) * NA + 8 * NA + 64 > o.node_capacity ||
+        12 * std::max(64, c->num_simulations) * NA > o.prior_ring)
+        return az_fail(AZ_ERR_CAPACITY, "az_search_set_params: %d simulations exceed the node pool sized at creation",
+                       c->num_simulations);
+    s->c.num_simulations = c->num_simulations;
+    s->c.c_puct = c->c_puct; s->c.fpu_reduction = c->fpu_reduction; s->c.virtual_loss = c->virtual_loss;
+    s->c.use_dirichlet_each_search = c->use_dirichlet_each_search;
+    s->c.dirichlet_alpha = c->dirichlet_alpha; s->c.dirichlet_eps = c->dirichlet_eps;
+    s->c.noise_seed = c->noise_seed; s->c.noise_seed_stride = c->noise_seed_stride;
+    s->t.cpuct = c->c_puct; s->t.fpu = c->fpu_reduction; s->t.vl = c->virtual_loss;
+    return 0;
+}
+
+int az_search_seed(az_search* s, int game, uint32_t seed) {
+    if (!s || game < 0 || game >= s->c.n_games) return az_fail(AZ_ERR_ARG, "bad argument");
+    std::lock_guard<std::mutex> lk(s->mu);
+    s->rng[game].seed(seed);
+    return 0;
+}
+
+int az_search_root_flags(az_search* s, int game, int* flags) {
+    if (!s || !flags || game < 0 || game >= s->c.n_games) return az_fail(AZ_ERR_ARG, "bad argument");
+    std::lock_guard<std::mutex> lk(s->mu);
+    HIPCHK(hipSetDevice(s->e->device));
+    int root = 0;
+    uint8_t f = 0;
+    HIPCHK(hipMemcpy(&root, s->t.rnode + game, 4, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(&f, s->arena[s->cur].flag + (size_t)game * s->t.ncap + root, 1, hipMemcpyDeviceToHost));
+    *flags = f;
     return 0;
 }
 

@@ -12,7 +12,9 @@
 #define AZ_DMAX 96           // longest selection path (root + 95 plies); overflow => AZ_ERR_CAPACITY
 #define AZ_NCNT 8            // per-game counters
 
-enum { ST_NONE = 0, ST_TERMINAL = 1, ST_TTHIT = 2, ST_EVAL = 3, ST_EXPANDED = 4 };
+// ST_EXPANDED: the leaf is already expanded (a childless node after releaseMemory, or the depth
+// cap): TT lookup, value = getValue() on a miss; ST_EXPVAL: the same with a TT hit (value cached)
+enum { ST_NONE = 0, ST_TERMINAL = 1, ST_TTHIT = 2, ST_EVAL = 3, ST_EXPANDED = 4, ST_EXPVAL = 5 };
 enum { MODE_SIM = 0, MODE_ROOT_NOISE = 1, MODE_ROOT_SEARCH = 2 };
 enum { FL_EXPANDED = 1, FL_TERMINAL = 2 };   // result (GameResult) in bits 2..3
 enum { CNT_EVALS = 0, CNT_LOOKUPS = 1, CNT_HITS = 2, CNT_SIMS = 3, CNT_NODES = 4, CNT_EVALS_TOTAL = 5,

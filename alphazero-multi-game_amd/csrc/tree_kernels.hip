@@ -588,7 +588,20 @@ __global__ __launch_bounds__(64) void k_select(TreeDev t, int mode) {
                 value = convert_value(result, player);
                 if (lane == 0) nd.flag[leaf] = (uint8_t)(f | FL_TERMINAL | (result << 2));
             } else if (f & FL_EXPANDED) {
-                status = ST_EXPANDED;   // depth cap only (reference: node->getValue())
+                // an expanded leaf: a childless node (releaseMemory pruned its children) or the depth
+                // cap.  runSingleSimulation still looks it up in the TT (parallel_mcts.cpp:319-335) and
+                // takes the cached value on a hit (no re-expansion), node->getValue() otherwise (:340-344)
+                const size_t tb = (size_t)g * t.tt_slots;
+                const int hs = (int)(hash & t.tt_mask);
+                const int vis = t.tt_visits[tb + hs];
+                if (vis > 0 && t.tt_hash[tb + hs] == hash) {
+                    status = ST_EXPVAL;
+                    value = t.tt_value[tb + hs];
+                    if (lane == 0) { t.tt_visits[tb + hs] = vis + 1; cnt[CNT_LOOKUPS] += 1; cnt[CNT_HITS] += 1; }
+                } else {
+                    status = ST_EXPANDED;
+                    if (lane == 0) cnt[CNT_LOOKUPS] += 1;
+                }
             }
         }
     } else if (!go && stones >= t.A) {
@@ -636,7 +649,7 @@ __global__ __launch_bounds__(64) void k_select(TreeDev t, int mode) {
         t.ttref[g] = ref;
         t.tthslot[g] = hslot;
         t.plen[g] = depth + 1;
-        t.need_eval[g] = (status == ST_EVAL && t.eval_kind == 0) ? 1 : 0;
+        t.need_eval[g] = (status == ST_EVAL && (t.eval_kind == 0 || t.eval_kind == 4)) ? 1 : 0;
     }
     for (int i = lane; i <= depth; i += 64) t.path[(size_t)g * AZ_DMAX + i] = spath[i];
     if (lane == 0 && mode == MODE_SIM) {
@@ -648,6 +661,17 @@ __global__ __launch_bounds__(64) void k_select(TreeDev t, int mode) {
         if (status == ST_EVAL) b += 64LL * t.A;
         cnt[CNT_BYTES_SEL] += b;
     }
+}
+
+// Host evaluator: the moves from the root to every leaf of the evaluation batch (slot order).
+__global__ void k_leaf_moves(TreeDev t, int* moves, int* len) {
+    const int i = blockIdx.x;
+    if (i >= *t.n_eval) return;
+    const int g = t.eval_games[i];
+    const int depth = t.plen[g] - 1;
+    const GamePtrs nd = game_nodes(t.nd, (size_t)g * t.ncap);
+    for (int j = threadIdx.x; j < depth; j += blockDim.x) moves[(size_t)i * AZ_DMAX + j] = nd.act[t.path[(size_t)g * AZ_DMAX + j + 1]];
+    if (threadIdx.x == 0) len[i] = depth;
 }
 
 // K2: deterministic compaction of the leaves that need the network (one block).
@@ -763,6 +787,12 @@ __global__ __launch_bounds__(64) void k_expand_backup(TreeDev t, int mode) {
                 const float sum = s_scalar[0];
                 if (sum > 0.0f) for (int a = lane; a < NA; a += 64) pol[a] = pol[a] / sum;
                 value = t.net_value[slot];
+            } else if (t.eval_kind == 4) {
+                // host evaluator (az_search_set_evaluator): the policy as NeuralNetwork::predict
+                // returns it, used as is by expandNodeWithPolicy (parallel_mcts.cpp:886-901)
+                const int slot = t.eval_slot[g];
+                for (int a = lane; a < NA; a += 64) pol[a] = t.net_logits[(size_t)slot * NA + a];
+                value = t.net_value[slot];
             } else if (t.eval_kind == 3) {
                 // no network: 1/|legal| on the legal actions, value 0 (parallel_mcts.cpp:903-916)
                 const float u = n > 0 ? 1.0f / (float)n : 0.0f;
@@ -863,7 +893,7 @@ __global__ __launch_bounds__(64) void k_expand_backup(TreeDev t, int mode) {
         kb += 25LL * n + 7 + 4LL * n + (status == ST_EVAL ? 4LL * NA + 4 + 24 : 0);
     } else if (status == ST_EXPANDED) {
         value = nd.N[leaf] == 0 ? 0.0f : nd.W[leaf] / (float)nd.N[leaf];
-    }
+    }   // ST_EXPVAL: the TT value k_select cached in lvalue
 
     if (mode == MODE_SIM && lane == 0) {
         // backpropagate(node, value, searchPath) (parallel_mcts.cpp:782-833)
@@ -1081,6 +1111,72 @@ __global__ __launch_bounds__(64) void k_compact(TreeDev t, Nodes dst, int* src_o
         top += tot;
     }
     if (lane == 0) { t.rnode[g] = 0; t.atop[g] = top; }
+}
+
+// releaseMemory(visitThreshold) (parallel_mcts.cpp:1481-1496; MCTSNode::pruneTree mcts_node.cpp:451-477):
+// BFS copy of the tree into the other arena keeping, below every node, only the children with
+// visitCount >= threshold (in child order; the root itself stays).  A node whose children all go
+// stays expanded with none.  pruned[g] = nodes before - nodes after (getTreeSize of every removed
+// subtree: the arena holds exactly the tree).
+__global__ __launch_bounds__(64) void k_prune(TreeDev t, Nodes dst, int* src_of, int thr, long long* pruned) {
+    const int g = blockIdx.x;
+    const int lane = threadIdx.x;
+    if (g >= t.G) return;
+    const size_t base = (size_t)g * t.ncap;
+    GamePtrs s = game_nodes(t.nd, base);
+    GamePtrs d = game_nodes(dst, base);
+    int* so = src_of + base;
+    const int root = t.rnode[g];
+    const int before = t.atop[g];
+    if (lane == 0) {
+        d.N[0] = s.N[root]; d.W[0] = s.W[root]; d.VL[0] = s.VL[root]; d.P[0] = s.P[root];
+        d.act[0] = s.act[root]; d.cnt[0] = s.cnt[root]; d.flag[0] = s.flag[root]; d.first[0] = -1;
+        so[0] = root;
+    }
+    __syncthreads();
+    int j = 0, top = 1;
+    while (j < top) {
+        const int k = j + lane;
+        const bool valid = k < top;
+        const int sn = valid ? so[k] : 0;
+        const int fsrc = valid ? s.first[sn] : 0;
+        const int ncs = valid ? (int)s.cnt[sn] : 0;
+        int nc = 0;                                  // children this node keeps
+        for (int i = 0; i < ncs; ++i) nc += s.N[fsrc + i] >= thr ? 1 : 0;
+        const int incl = wave_incl_scan(nc, lane);
+        const int tot = __shfl(incl, 63);
+        const int nf = top + incl - nc;
+        if (valid) { d.first[k] = nc ? nf : -1; d.cnt[k] = (int16_t)nc; }
+        const int m = min(64, top - j);
+        for (int e = 0; e < m; ++e) {
+            const int ce = __shfl(ncs, e);
+            if (__shfl(nc, e) == 0) continue;
+            const int fs = __shfl(fsrc, e);
+            int fd = __shfl(nf, e);
+            if (fd + __shfl(nc, e) > t.ncap) { if (lane == 0) atomicOr(t.err, ERR_NODES); return; }
+            for (int i0 = 0; i0 < ce; i0 += 64) {
+                const int i = i0 + lane;
+                const int a = fs + i;
+                const bool keep = i < ce && s.N[a] >= thr;
+                const unsigned long long bm = __ballot(keep);
+                if (keep) {
+                    const int b = fd + __popcll(bm & ((1ULL << lane) - 1ULL));
+                    d.N[b] = s.N[a]; d.W[b] = s.W[a]; d.VL[b] = s.VL[a]; d.P[b] = s.P[a];
+                    d.act[b] = s.act[a]; d.cnt[b] = s.cnt[a]; d.flag[b] = s.flag[a]; d.first[b] = -1;
+                    so[b] = a;
+                }
+                fd += __popcll(bm);
+            }
+        }
+        __syncthreads();
+        j += m;
+        top += tot;
+    }
+    if (lane == 0) {
+        t.rnode[g] = 0; t.atop[g] = top;
+        t.cnt[(size_t)g * AZ_NCNT + CNT_NODES] = top;
+        pruned[g] = before - top;
+    }
 }
 
 // K7: Dirichlet mix on the root children (noise already normalised on the host).

@@ -104,7 +104,9 @@ enum az_eval_kind {
     AZ_EVAL_NET = 0,    /* the ConvNet above (az_search_create's `net`) */
     AZ_EVAL_HASH = 1,   /* HashEvaluator (oracle/ref_harness.cpp hash_eval), tests */
     AZ_EVAL_RANDOM = 2, /* RandomPolicyNetwork(seed + game) semantics (random_policy_network.cpp) */
-    AZ_EVAL_UNIFORM = 3 /* no network: ParallelMCTS::evaluateState fallback (parallel_mcts.cpp:903-916) */
+    AZ_EVAL_UNIFORM = 3,/* no network: ParallelMCTS::evaluateState fallback (parallel_mcts.cpp:903-916) */
+    AZ_EVAL_CALLBACK = 4/* a host evaluator (az_search_set_evaluator): any NeuralNetwork subclass's
+                           predict / predictBatch (parallel_mcts.cpp:886-901), once per simulation step */
 };
 typedef struct az_search_cfg {
     int n_games;          /* G: independent games (trees) on this device */
@@ -135,6 +137,15 @@ typedef struct az_search_cfg {
 #define AZ_ACTION_NONE (-2)   /* Go: no move (finished game); -1 is the pass */
 
 int az_search_create(az_engine* e, az_net* net, const az_search_cfg* cfg, az_search** out);
+/* AZ_EVAL_CALLBACK: every simulation step hands the n leaves that need an evaluation to the host,
+ * in one call on the calling thread: games[i] (the game slot), path_len[i] moves from the root to
+ * leaf i in moves[i * max_path ...], and the leaf's feature planes [n][n_planes][bs][bs]
+ * (getEnhancedTensorRepresentation).  The evaluator fills policy [n][NA] -- as
+ * NeuralNetwork::predict returns it (post-softmax; used as is by expandNodeWithPolicy) -- and
+ * value [n], and returns 0 (nonzero aborts the search with AZ_ERR_STATE). */
+typedef int (*az_eval_fn)(void* user, int n, const int* games, const int* path_len, const int* moves, int max_path,
+                          const float* planes, int n_planes, float* policy, float* value);
+int az_search_set_evaluator(az_search* s, az_eval_fn fn, void* user);
 void az_search_destroy(az_search* s);
 /* Start fresh games (empty board, new tree and TT) for the listed game slots. */
 int az_search_new_games(az_search* s, const int* games, int n);
@@ -145,6 +156,24 @@ int az_search_add_noise(az_search* s, float alpha, float eps);
 int az_search_add_noise_masked(az_search* s, float alpha, float eps, const uint8_t* mask);
 /* ParallelMCTS::search() for every active (non-terminal) game. */
 int az_search_run(az_search* s);
+/* ParallelMCTS::runSingleSimulation() n times for every active game (parallel_mcts.cpp:276-380):
+ * no root-expansion step and no noise, unlike az_search_run; an unexpanded root is the first
+ * leaf.  runBatchedSearch (:1531-1590, numThreads 1) is n = numSimulations. */
+int az_search_simulate(az_search* s, int n);
+/* ParallelMCTS::releaseMemory(visitThreshold) (parallel_mcts.cpp:1481-1496, MCTSNode::pruneTree
+ * mcts_node.cpp:451-477) for every game: children with visitCount < threshold are removed with
+ * their subtrees, recursively from the root (child order kept; a node that loses every child
+ * stays expanded).  pruned[g] (optional, G entries) = nodes removed (getTreeSize of each). */
+int az_search_release(az_search* s, int threshold, int64_t* pruned);
+/* ParallelMCTS::selectAction(isTraining, T) of one game (parallel_mcts.cpp:987-1047).
+ * batch_inference != 0 (MCTSConfig::useBatchInference, forced by setDeterministicMode and
+ * SelfPlayManager): the deterministic rules of az_search_select.  Otherwise draws on the game's
+ * rng_ (the std::mt19937 of its Dirichlet draws) with libstdc++: discrete_distribution over
+ * getActionProbabilities(T) when training with T > 0, else uniform_int_distribution over the
+ * most-visited children when they tie.  `legal` (the root state's getLegalMoves()) is used when
+ * the root has no children (after releaseMemory): legal[0], or a uniform draw; -1 if empty. */
+int az_search_select_action(az_search* s, int game, int training, float temperature, int batch_inference,
+                            const int* legal, int n_legal, int* action);
 /* getActionProbabilities(T) + selectAction(isTraining, T) + getRootValue() for every
  * game.  probs: [G][NA] in CHILD order (n_children[g] valid entries), children_actions
  * [G][NA] (NA = action space: bs*bs, Go bs*bs + 1); actions[g] = -1 (Go: AZ_ACTION_NONE)
@@ -159,6 +188,20 @@ int az_search_root_children(az_search* s, int game, int* actions, int* N, int* V
                             int* n_children);
 /* Root node's own N, VL, W. */
 int az_search_root_node(az_search* s, int game, int* N, int* VL, float* W);
+/* Update the search parameters of a live handle without touching its trees (the reference's
+ * setters / setConfig keep the tree, parallel_mcts.h:172-182, parallel_mcts.cpp:1225-1261):
+ * num_simulations (up to the node pool sized at creation, else AZ_ERR_CAPACITY), c_puct,
+ * fpu_reduction, virtual_loss, the Dirichlet fields and the noise seeds of later new games.
+ * Shape, evaluator and table changes need a new handle (AZ_ERR_ARG). */
+int az_search_set_params(az_search* s, const az_search_cfg* cfg);
+/* Reseed game's rng_ (ParallelMCTS::setDeterministicMode, parallel_mcts.cpp:1263-1274: 42, or
+ * std::random_device): the std::mt19937 of the Dirichlet draws and of az_search_select_action. */
+int az_search_seed(az_search* s, int game, uint32_t seed);
+/* Root node flags of one game: 1 expanded (MCTSNode::isExpanded), 2 terminal, bits 2..3 the
+ * GameResult of a terminal root. */
+#define AZ_NODE_EXPANDED 1
+#define AZ_NODE_TERMINAL 2
+int az_search_root_flags(az_search* s, int game, int* flags);
 /* Counters per game: [0] evals, [1] tt_lookups, [2] tt_hits, [3] simulations, [4] nodes used. */
 int az_search_counters(az_search* s, int game, int64_t* out5);
 /* Tree-kernel profiling: enable resets; read returns the summed GPU time of K1 (selection +

@@ -14,6 +14,8 @@
 //             hash (:620-656), terminal/result (:477-529), legal-move order.
 //   gamma     libstdc++ gamma_distribution<float> draws on mt19937(42), as used
 //             by ParallelMCTS::addDirichletNoise (parallel_mcts.cpp:1136-1142).
+//   api       ParallelMCTS API operations beyond the self-play loop (runSingleSimulation,
+//             runBatchedSearch, releaseMemory, stochastic selectAction; see run_api)
 //   go_positions / go_game  the same for GoState(bs, komi 7.5, Chinese rules, superko)
 //             (src/games/go/go_state.cpp, go_rules.cpp; patch P6 seeds its Zobrist keys).
 //
@@ -302,6 +304,64 @@ static int run_gamma(float alpha, int n, int calls) {
     return 0;
 }
 
+// ParallelMCTS public API beyond the playSingleGame loop (include/alphazero/mcts/parallel_mcts.h:
+// 155-159,162-163,198): a script of operations on one tree, with the root statistics after each.
+//   n  runSingleSimulation()            b  runBatchedSearch()         s  search()
+//   r<k> releaseMemory(k) (returns the pruned node count)
+//   d  stochastic selection: setConfig with useBatchInference = false (the rng keeps the state
+//      setDeterministicMode(true) seeded, 42), so selectAction samples on rng_
+//   a<T> selectAction(true, T)          e<T> selectAction(false, T)
+//   m  play the last selected action (state.makeMove + updateWithMove)   x  addDirichletNoise
+static int run_api(int bs, int sims, const std::string& script, const std::string& evalKind, unsigned evalSeed) {
+    gomoku::GomokuState state(bs, false, false, 1, false);
+    mcts::TranspositionTable tt(1048576);
+    mcts::MCTSConfig cfg;
+    cfg.numThreads = 1;
+    cfg.numSimulations = sims;
+    cfg.useBatchInference = false;
+    cfg.useBatchedMCTS = false;
+    std::unique_ptr<nn::NeuralNetwork> net;
+    if (evalKind == "hash") net.reset(new HashEvaluator());
+    else net.reset(new CountingRandom(bs, evalSeed));
+    mcts::ParallelMCTS m(state, cfg, net.get(), &tt);
+    m.setDeterministicMode(true);
+    std::ostream& o = std::cout;
+    o << "{\"mode\":\"api\",\"bs\":" << bs << ",\"sims\":" << sims << ",\"eval\":\"" << evalKind << "\",\"eval_seed\":"
+      << evalSeed << ",\"script\":\"" << script << "\",\"ops\":[";
+    int last = -1;
+    size_t i = 0;
+    bool firstOp = true;
+    while (i < script.size()) {
+        const char op = script[i++];
+        std::string arg;
+        while (i < script.size() && script[i] != ',') arg += script[i++];
+        if (i < script.size()) ++i;
+        long long ret = 0;
+        if (op == 'n') m.runSingleSimulation();
+        else if (op == 'b') m.runBatchedSearch();
+        else if (op == 's') m.search();
+        else if (op == 'r') ret = (long long)m.releaseMemory(std::atoi(arg.c_str()));
+        else if (op == 'd') { mcts::MCTSConfig c = m.config_; c.useBatchInference = false; m.setConfig(c); }
+        else if (op == 'a') ret = last = m.selectAction(true, (float)std::atof(arg.c_str()));
+        else if (op == 'e') ret = last = m.selectAction(false, (float)std::atof(arg.c_str()));
+        else if (op == 'm') { state.makeMove(last); m.updateWithMove(last); ret = last; }
+        else if (op == 'x') m.addDirichletNoise(0.03f, 0.25f);
+        else { std::fprintf(stderr, "bad op %c\n", op); return 2; }
+        auto* root = m.rootNode_.get();
+        if (!firstOp) o << ",";
+        firstOp = false;
+        o << "{\"op\":\"" << op << arg << "\",\"ret\":" << ret << ",\"root\":[" << root->visitCount.load() << ","
+          << root->virtualLoss.load() << "," << fbits(root->valueSum.load()) << "],\"children\":";
+        dump_node_children(o, root);
+        o << "}";
+    }
+    o << "]}\n";
+    o.flush();
+    // ~ParallelMCTS deletes a borrowed TT unless useBatchInference: this one is on the stack
+    m.config_.useBatchInference = true;
+    return 0;
+}
+
 int main(int argc, char** argv) {
     if (argc < 2) { std::fprintf(stderr, "usage: ref_harness game|positions|gamma|go_positions|go_game ...\n"); return 2; }
     std::string mode = argv[1];
@@ -313,6 +373,7 @@ int main(int argc, char** argv) {
     if (mode == "positions") return run_positions(I(2, 9), I(3, 16), (unsigned)I(4, 1));
     if (mode == "gamma") return run_gamma(F(2, 0.03f), I(3, 81), I(4, 4));
     if (mode == "go_positions") return run_go_positions(I(2, 9), I(3, 16), (unsigned)I(4, 1));
+    if (mode == "api") return run_api(I(2, 9), I(3, 50), argc > 4 ? argv[4] : "s", argc > 5 ? argv[5] : "hash", (unsigned)I(6, 7));
     if (mode == "go_game")
         return run_game(I(2, 9), I(3, 100), I(4, 1000), argc > 5 ? argv[5] : "hash", (unsigned)I(6, 7), I(7, 0),
                         F(8, 1.5f), F(9, 0.0f), true);

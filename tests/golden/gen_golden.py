@@ -40,6 +40,15 @@ GO_GAME_CASES = [
     (19, 500, 2, "hash", 7, 0, 1.5, 0.0),       # C4 board
 ]
 
+# ParallelMCTS API scripts (ref_harness api): (bs, sims, script, evaluator, eval_seed)
+API_CASES = [
+    (9, 30, "n,n,n,s,r3,s,d,a1,m,x,s,a1,m,s,e0,m,n,b,r2,s,a0.5,m,s,a0,m", "hash", 7),
+    (7, 60, "x,s,d,a1,m,x,s,a1,m,r5,s,a1,m,s,e0,m,s,a0,m,s,a1,m,s,e1,m", "random", 11),
+    (9, 40, "b,a1,m,b,e0,m,r1,s,a0,m,n,n,s,d,a0,m,s,e1,m,r4,s,a1,m", "hash", 5),
+    (15, 100, "x,s,r2,s,d,a1,m,x,s,a1,m,s,a0,m", "hash", 3),
+    (5, 80, "s,r40,s,a1,m,s,r1000,s,a0,m,d,s,a1,m,s,r2,e0,m", "hash", 9),
+]
+
 
 def run(*args):
     r = subprocess.run([HARNESS] + [str(a) for a in args], capture_output=True, text=True, timeout=900)
@@ -51,6 +60,16 @@ def run(*args):
 def main():
     if not os.path.exists(HARNESS):
         sys.exit("build oracle/_ref/ref_harness first (oracle/build_ref.sh)")
+    api = []
+    for c in API_CASES:
+        d = run("api", *c)
+        d["case"] = list(c)
+        api.append(d)
+        print("api", c[:2], c[3], "ops", len(d["ops"]))
+    with gzip.open(os.path.join(OUT, "ref_api.json.gz"), "wt") as f:
+        json.dump(api, f, separators=(",", ":"))
+    if sys.argv[1:] == ["--only", "api"]:
+        return
     go = []
     for c in GO_GAME_CASES:
         d = run("go_game", *c)

@@ -17,7 +17,9 @@ def bits(a):
 
 
 def host_play(m, moves, n=None):
-    """SelfPlayManager::playSingleGame's loop (self_play_manager.cpp:184-215) on a ParallelMCTS."""
+    """SelfPlayManager::playSingleGame's loop (self_play_manager.cpp:184-215) on a ParallelMCTS, in
+    the deterministic mode the reference harness sets (useBatchInference, rng_ seeded 42)."""
+    m.setDeterministicMode(True)
     m.addDirichletNoise(0.03, 0.25)
     out = []
     for ply in range(len(moves) if n is None else n):
@@ -196,3 +198,51 @@ def test_host_dataset_from_selfplay_matches_oracle(tmp_path):
     ex3 = ds2.getExamples()
     assert all(bits(np.asarray(a.state).reshape(-1)) == bits(np.asarray(b.state).reshape(-1)) for a, b in zip(ex2[:8], ex3[:8]))
     assert bits([e.value for e in ex3]) == bits(perm)
+
+
+@pytest.mark.gpu
+def test_host_api_script_matches_reference():
+    """The host ParallelMCTS runs the reference's API script (tests/golden/ref_api.json.gz case 1,
+    RandomPolicyNetwork): noise, search, releaseMemory, stochastic selectAction after
+    setConfig(useBatchInference = false) (tree and rng_ kept); root statistics through
+    getRootNode() (the MCTSNode snapshot) bit for bit after every operation."""
+    case = json.load(gzip.open(os.path.join(GOLD, "ref_api.json.gz"), "rt"))[1]
+    bs, sims, script, ev, seed = case["case"]
+    assert ev == "random"
+    cfg = az.MCTSConfig()
+    cfg.numSimulations = sims
+    st = az.GomokuState(bs)
+    net = az.RandomPolicyNetwork(az.GameType.GOMOKU, bs, seed)
+    m = az.ParallelMCTS(st, cfg, net, az.TranspositionTable(1 << 20))
+    m.setDeterministicMode(True)
+    last = -1
+    for k, op in enumerate(case["ops"]):
+        c, arg = op["op"][0], op["op"][1:]
+        ret = 0
+        if c == "n":
+            m.runSingleSimulation()
+        elif c == "b":
+            m.runBatchedSearch()
+        elif c == "s":
+            m.search()
+        elif c == "r":
+            ret = m.releaseMemory(int(arg))
+        elif c == "d":                                      # setConfig keeps the tree and rng_
+            cfg2 = az.MCTSConfig()
+            cfg2.numSimulations = sims
+            cfg2.useBatchInference = False
+            m.setConfig(cfg2)
+        elif c in "ae":
+            ret = last = m.selectAction(c == "a", float(arg))
+        elif c == "m":
+            m.updateWithMove(last)
+            ret = last
+        elif c == "x":
+            m.addDirichletNoise(0.03, 0.25)
+        assert ret == op["ret"], (k, op["op"])
+        r = m.getRootNode()
+        assert [r.visitCount, r.virtualLoss, bits([r.valueSum])[0]] == op["root"], (k, op["op"])
+        got = [[a, ch.visitCount, ch.virtualLoss, bits([ch.valueSum])[0], bits([ch.prior])[0]]
+               for a, ch in zip(r.actions, r.children)]
+        assert got == op["children"], (k, op["op"])
+    assert "Node: V=" in m.getRootNode().toString(1)
