@@ -160,7 +160,7 @@ class ParallelMCTS:
                  tt_log2=20, node_capacity=0, prior_ring=0, game=0, callback=None):
         """game: AZ_GAME_GOMOKU (0) or AZ_GAME_GO (1) -- GoState(bs 9/13/19, komi 7.5, Chinese rules,
         superko); Go actions are -1 (pass) .. bs*bs-1 and finished games report AZ_ACTION_NONE.
-        evaluator=AZ_EVAL_CALLBACK: callback(games [n], moves: list of root-to-leaf move lists,
+        evaluator=AZ_EVAL_CALLBACK: callback(games [n], moves: per leaf the moves from the empty board,
         planes [n][C][bs][bs]) -> (policy [n][NA] as NeuralNetwork::predict returns it, value [n])."""
         self.G = n_games
         self.bs = board_size

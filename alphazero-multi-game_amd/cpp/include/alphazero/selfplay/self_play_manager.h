@@ -18,7 +18,9 @@ namespace selfplay {
 class SelfPlayManager {
  public:
     // numThreads is kept for the signature; concurrency is the device slot count
-    // (setConcurrentGames, default min(numGames, 2048)).
+    // (setConcurrentGames, default min(numGames, 2048)).  setBatchConfig(batchSize, ...) caps the
+    // network batch of a simulation step -- one leaf per game slot -- at batchSize slots (the
+    // BatchQueue's batch size, self_play_manager.cpp:133-136, 162-173).
     SelfPlayManager(nn::NeuralNetwork* neuralNetwork, int numGames = 100, int numSimulations = 800,
                     int numThreads = 4);
     ~SelfPlayManager();
@@ -28,7 +30,9 @@ class SelfPlayManager {
                               float initialTemperature = 1.0f, int temperatureDropMove = 30,
                               float finalTemperature = 0.0f);
     void setProgressCallback(std::function<void(int, int, int, int)> callback) { progress_ = std::move(callback); }
-    void setBatchConfig(int batchSize, int batchTimeoutMs) { batchSize_ = batchSize; batchTimeoutMs_ = batchTimeoutMs; }
+    void setBatchConfig(int batchSize, int batchTimeoutMs) {
+        batchSize_ = batchSize; batchTimeoutMs_ = batchTimeoutMs; batchSet_ = true;
+    }
     void setSaveGames(bool saveGames, const std::string& outputDir = "games");
     void setAbort(bool abort) { abort_ = abort ? 1 : 0; }
     bool isRunning() const { return running_; }
@@ -56,6 +60,7 @@ class SelfPlayManager {
     std::atomic<bool> running_{false};
     std::atomic<int> completed_{0}, totalMoves_{0};
     int slots_ = 0, maxMoves_ = 0;
+    bool batchSet_ = false;
     unsigned noiseSeed_ = 42;
     int noiseStride_ = 1;
 };

@@ -48,11 +48,12 @@ int ParallelMCTS::hostEvaluate(void* user, int n, const int* games, const int* p
                                const float* planes, int nPlanes, float* policy, float* value) {
     auto* self = static_cast<ParallelMCTS*>(user);
     const int A = self->root_->getActionSpaceSize();
+    const int h = (int)self->root_->getMoveHistory().size();   // moves[] start from the empty board
     std::vector<std::unique_ptr<core::IGameState>> leaves;
     leaves.reserve(n);
     for (int i = 0; i < n; ++i) {
         auto st = self->root_->clone();
-        for (int k = 0; k < pathLen[i]; ++k) st->makeMove(moves[(size_t)i * maxPath + k]);
+        for (int k = h; k < pathLen[i]; ++k) st->makeMove(moves[(size_t)i * maxPath + k]);
         leaves.push_back(std::move(st));
     }
     auto fallback = [&](int i) {

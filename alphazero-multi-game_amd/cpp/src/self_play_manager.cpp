@@ -64,6 +64,40 @@ void sink(void* user, int gid, int bs, int n, const az_move_rec* moves, int resu
     c->completed->fetch_add(1);
 }
 
+// AZ_EVAL_CALLBACK (a NeuralNetwork subclass without a device implementation): every leaf is the
+// initial state of the game type plus the moves the engine reports; predictBatch evaluates them all
+// (a throwing evaluator gets the reference's uniform / 0 fallback, parallel_mcts.cpp:903-916)
+struct EvalCtx {
+    nn::NeuralNetwork* nn;
+    core::GameType type;
+    int bs;
+};
+
+int host_eval(void* user, int n, const int* /*games*/, const int* len, const int* moves, int maxPath,
+              const float* /*planes*/, int /*nPlanes*/, float* policy, float* value) {
+    auto* c = static_cast<EvalCtx*>(user);
+    std::vector<std::unique_ptr<core::IGameState>> leaves;
+    for (int i = 0; i < n; ++i) {
+        auto st = core::createGameState(c->type, c->bs, false);
+        for (int k = 0; k < len[i]; ++k) st->makeMove(moves[(size_t)i * maxPath + k]);
+        leaves.push_back(std::move(st));
+    }
+    const int A = leaves.empty() ? 0 : leaves[0]->getActionSpaceSize();
+    std::vector<std::reference_wrapper<const core::IGameState>> refs;
+    for (auto& l : leaves) refs.emplace_back(*l);
+    std::vector<std::vector<float>> ps;
+    std::vector<float> vs;
+    bool ok = true;
+    try { c->nn->predictBatch(refs, ps, vs); } catch (const std::exception&) { ok = false; }
+    for (int i = 0; i < n; ++i) {
+        const bool have = ok && i < (int)ps.size() && i < (int)vs.size();
+        for (int a = 0; a < A; ++a)
+            policy[(size_t)i * A + a] = have ? (a < (int)ps[i].size() ? ps[i][a] : 0.0f) : 1.0f / (float)A;
+        value[i] = have ? vs[i] : 0.0f;
+    }
+    return 0;
+}
+
 void progress(void* user, int gid, int move, int total_games, int64_t /*total_moves*/) {
     auto* c = static_cast<RunCtx*>(user);
     const int tm = c->totalMoves->fetch_add(1);
@@ -88,6 +122,7 @@ std::vector<GameRecord> SelfPlayManager::generateGames(core::GameType type, int 
         az_search_cfg c{};
         c.game = go ? AZ_GAME_GO : AZ_GAME_GOMOKU;
         c.n_games = slots_ > 0 ? slots_ : std::min(std::max(numGames_, 1), 2048);
+        if (batchSet_ && batchSize_ > 0) c.n_games = std::min(c.n_games, batchSize_);   // network batch per step
         c.board_size = bs;
         c.num_simulations = numSimulations_;
         c.c_puct = mcts_.cPuct > 0.0f ? mcts_.cPuct : 1.5f;       // :177-178
@@ -104,6 +139,11 @@ std::vector<GameRecord> SelfPlayManager::generateGames(core::GameType type, int 
         c.tt_log2 = 20;                                            // TranspositionTable tt(1048576), :159
         az_search* s = nullptr;
         if (az_search_create(ev.engine, ev.net, &c, &s)) throw std::runtime_error(az_last_error());
+        EvalCtx ectx{nn_, type, bs};
+        if (ev.kind == AZ_EVAL_CALLBACK && az_search_set_evaluator(s, host_eval, &ectx)) {
+            az_search_destroy(s);
+            throw std::runtime_error(az_last_error());
+        }
         az_selfplay_cfg sc{tempDrop_, tInit_, tFinal_, 0};
         RunCtx ctx{this, &records, type, variant, save_, outDir_, &progress_, &completed_, &totalMoves_, &done};
         const int rc = az_selfplay_run(s, &sc, numGames_, maxMoves_, sink, progress, &ctx, &abort_);

@@ -426,7 +426,8 @@ struct az_search {
     az_eval_fn eval_fn = nullptr; void* eval_user = nullptr;
     int* d_lmoves = nullptr; int* d_llen = nullptr;
     std::vector<float> h_planes, h_nchw, h_pol, h_val;
-    std::vector<int> h_games, h_lmoves, h_llen;
+    std::vector<int> h_games, h_lmoves, h_llen, h_full;
+    std::vector<std::vector<int>> hist;    // per slot: the moves committed since the game started
     float* d_logits = nullptr; float* d_value = nullptr;
     float* d_noise = nullptr; uint8_t* d_mask = nullptr;
     int* d_actions = nullptr; float* d_values = nullptr; float* d_probs = nullptr; int* d_cact = nullptr; int* d_nch = nullptr;
@@ -495,7 +496,20 @@ int host_evaluate(az_search* s) {
             for (int a = 0; a < A; ++a) s->h_nchw[((size_t)i * C + c) * A + a] = s->h_planes[((size_t)i * A + a) * 16 + c];
     s->h_pol.assign((size_t)n * NA, 0.0f);
     s->h_val.assign(n, 0.0f);
-    if (s->eval_fn(s->eval_user, n, s->h_games.data(), s->h_llen.data(), s->h_lmoves.data(), AZ_DMAX, s->h_nchw.data(), C,
+    // moves from the game's initial state: the slot's committed moves, then the path
+    size_t mx = 1;
+    for (int i = 0; i < n; ++i) mx = std::max(mx, s->hist[s->h_games[i]].size() + (size_t)s->h_llen[i]);
+    s->h_full.assign((size_t)n * mx, 0);
+    std::vector<int> len(n);
+    for (int i = 0; i < n; ++i) {
+        const std::vector<int>& h = s->hist[s->h_games[i]];
+        int* dst = s->h_full.data() + (size_t)i * mx;
+        std::copy(h.begin(), h.end(), dst);
+        std::copy(s->h_lmoves.begin() + (size_t)i * AZ_DMAX, s->h_lmoves.begin() + (size_t)i * AZ_DMAX + s->h_llen[i],
+                  dst + h.size());
+        len[i] = (int)h.size() + s->h_llen[i];
+    }
+    if (s->eval_fn(s->eval_user, n, s->h_games.data(), len.data(), s->h_full.data(), (int)mx, s->h_nchw.data(), C,
                    s->h_pol.data(), s->h_val.data()) != 0)
         return az_fail(AZ_ERR_STATE, "host evaluator failed");
     HIPCHK(hipMemcpyAsync(s->d_logits, s->h_pol.data(), (size_t)n * NA * 4, hipMemcpyHostToDevice, st));
@@ -597,6 +611,7 @@ int search_new_games(az_search* s, const int* games, int n, const int* seed_ids 
     for (int i = 0; i < n; ++i) {
         const int g = games[i];
         s->stones[g] = 0; s->active[g] = 1; s->fresh[g] = 1; s->ply[g] = 0;
+        s->hist[g].clear();
         const int id = seed_ids ? seed_ids[i] : g;
         s->rng[g].seed(s->c.noise_seed + (uint32_t)(s->c.noise_seed_stride * id));
     }
@@ -639,6 +654,7 @@ int search_apply_dev(az_search* s, int* terminal, int* result) {
     HIPCHK(hipStreamSynchronize(st));
     for (int g = 0; g < G; ++g) {
         if (s->active[g] && acts[g] >= (s->t.game == GAME_GO ? -1 : 0)) {
+            s->hist[g].push_back(acts[g]);
             s->stones[g] += 1; s->ply[g] += 1; s->fresh[g] = 0;
             if (term[g]) s->active[g] = 0;
         }
@@ -988,6 +1004,7 @@ int az_search_create(az_engine* e, az_net* net, const az_search_cfg* c, az_searc
     HIPCHK(hipMemset(t.active, 0, G * 4));
     s->stones.assign(G, 0); s->active.assign(G, 0); s->fresh.assign(G, 1); s->ply.assign(G, 0); s->expanded.assign(G, 0);
     s->rng.resize(G);
+    s->hist.assign(G, {});
     s->h_noise.assign((size_t)G * NA, 0.0f);
     s->h_mask.assign(G, 0);
     *out = s;

@@ -138,8 +138,9 @@ typedef struct az_search_cfg {
 
 int az_search_create(az_engine* e, az_net* net, const az_search_cfg* cfg, az_search** out);
 /* AZ_EVAL_CALLBACK: every simulation step hands the n leaves that need an evaluation to the host,
- * in one call on the calling thread: games[i] (the game slot), path_len[i] moves from the root to
- * leaf i in moves[i * max_path ...], and the leaf's feature planes [n][n_planes][bs][bs]
+ * in one call on the calling thread: games[i] (the game slot), the path_len[i] moves that lead
+ * from the game's initial (empty) state to leaf i -- the moves committed so far, then the search
+ * path -- in moves[i * max_path ...], and the leaf's feature planes [n][n_planes][bs][bs]
  * (getEnhancedTensorRepresentation).  The evaluator fills policy [n][NA] -- as
  * NeuralNetwork::predict returns it (post-softmax; used as is by expandNodeWithPolicy) -- and
  * value [n], and returns 0 (nonzero aborts the search with AZ_ERR_STATE). */

@@ -5,7 +5,9 @@ subclass takes, parallel_mcts.cpp:886-901):
       roots, children, visit distributions, actions and values;
   (2) the C++ host ParallelMCTS with a Python subclass of NeuralNetwork -- the reference test
       evaluator HashEvaluator written in Python over state.getHash() / getMoveHistory() -- against
-      the REFERENCE's own API golden (tests/golden/ref_api.json.gz case 0) and its 9x9 golden game."""
+      the REFERENCE's own API golden (tests/golden/ref_api.json.gz case 0) and its 9x9 golden game;
+  (3) SelfPlayManager with that Python network and setBatchConfig capping the batch, against the
+      CPU restatement."""
 import gzip
 import json
 import os
@@ -146,3 +148,42 @@ def test_gpu_host_python_network_matches_reference():
         m.updateWithMove(act)
         if ply % 2 == 0:
             m.addDirichletNoise(0.03, 0.25)
+
+
+@pytest.mark.gpu
+def test_gpu_selfplay_manager_python_network_matches_oracle():
+    """SelfPlayManager.generateGames with a Python NeuralNetwork subclass (the leaves of every
+    simulation step go to its predictBatch as states rebuilt from the moves the engine reports),
+    setBatchConfig(2, 5) capping the network batch at two game slots for five games: every record
+    equals the CPU restatement with the same evaluator."""
+    az = pytest.importorskip("_alphazero_cpp")
+    import az_oracle as O
+
+    class HashEvaluator(az.NeuralNetwork):
+        def __init__(self):
+            super().__init__()
+            self.batches = []
+
+        def predict(self, state):
+            return _hash_eval(state.getHash(), list(state.getMoveHistory()), state.getActionSpaceSize())
+
+        def predictBatch(self, states):
+            self.batches.append(len(states))
+            out = [self.predict(s) for s in states]
+            return [list(map(float, o[0])) for o in out], [o[1] for o in out]
+
+    total, bs, sims, max_moves = 5, 7, 48, 12
+    refs = O.play(seed_stride=1, bs=bs, sims=sims, max_moves=max_moves, eval_kind=O.EVAL_HASH, n_games=total)
+    net = HashEvaluator()
+    mgr = az.SelfPlayManager(net, total, sims, 4)
+    mgr.setBatchConfig(2, 5)
+    mgr.setMaxMoves(max_moves)
+    mgr.setSeeds(42, 1)
+    recs = mgr.generateGames(az.GameType.GOMOKU, bs, False)
+    assert len(recs) == total
+    for g, (rec, ref) in enumerate(zip(recs, refs)):
+        mv = rec.getMoves()
+        assert len(mv) == len(ref["moves"]), g
+        for ply, (m, r) in enumerate(zip(mv, ref["moves"])):
+            assert (m.action, bits(m.policy), bits([m.value])[0]) == (r["action"], r["probs"], r["value"]), (g, ply)
+    assert max(net.batches) == 2
