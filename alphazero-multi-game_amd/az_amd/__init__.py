@@ -136,6 +136,12 @@ class HipNeuralNetwork:
         check(lib().az_net_profile_read(self.h, ctypes.byref(ms), ctypes.byref(la), ctypes.byref(fw)))
         return ms.value, la.value, fw.value
 
+    def trunk_kernel(self):
+        """Name of the HIP kernel the 3x3 trunk convs dispatch at this net's max_batch."""
+        buf = ctypes.create_string_buffer(128)
+        check(lib().az_net_trunk_kernel(self.h, buf, 128))
+        return buf.value.decode()
+
     def getBatchSize(self):
         return self.desc.max_batch
 

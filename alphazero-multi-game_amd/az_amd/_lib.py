@@ -59,6 +59,7 @@ EXPORTS = {
     "az_net_predict_batch": (c_int, [vp, P(c_float), c_int, P(c_float), P(c_float)]),
     "az_net_profile": (c_int, [vp, c_int]),
     "az_net_profile_read": (c_int, [vp, P(ctypes.c_double), P(c_int64), P(c_int64)]),
+    "az_net_trunk_kernel": (c_int, [vp, ctypes.c_char_p, c_int]),
     "az_search_create": (c_int, [vp, vp, P(SearchCfg), P(vp)]),
     "az_search_destroy": (None, [vp]),
     "az_search_new_games": (c_int, [vp, P(c_int), c_int]),

@@ -202,7 +202,8 @@ void az_launch_split_bf16(const float* in, uint16_t* hi, uint16_t* lo, size_t n,
 }
 
 // ===========================================================================
-// v2: block tile BM pixels x BN channels, 8 waves (WM x WN), BK = 32.  Operand tiles
+// v3 (below; its v2 predecessor without fragment double buffering was removed in round 2):
+// block tile BM pixels x BN channels, 8 waves (WM x WN), BK = 32.  Operand tiles
 // move HBM/L2 -> LDS by global_load_lds_dwordx4 (LDS-DMA, per-lane source address
 // = the im2col gather, zero page for the board edge) into a STAGES-deep ring; each
 // wave issues its share of the 16-row pieces and retires them with a counted
@@ -212,188 +213,6 @@ void az_launch_split_bf16(const float* in, uint16_t* hi, uint16_t* lo, size_t n,
 // epilogue stages the fp32 tile through LDS and stores 16-byte vectors.
 typedef __attribute__((address_space(3))) void lds_void_t;
 typedef __attribute__((address_space(1))) const void g_void_t;
-
-template <bool SPLIT, int BM, int BN, int WM, int WN, int STAGES>
-__global__ __launch_bounds__(WM * WN * 64, 1) void conv3x3_v2(ConvBf16Args p) {
-    constexpr int NT = WM * WN * 64, NW = WM * WN;
-    constexpr int ROWB = 64;                          // 32 bf16 per row
-    constexpr int NPL = SPLIT ? 2 : 1;                // hi (+ lo) planes
-    constexpr int A_BYTES = BM * ROWB, B_BYTES = BN * ROWB;
-    constexpr int STAGE = NPL * (A_BYTES + B_BYTES);
-    constexpr int EPI_LD = BN + 4;                    // fp32 row stride of the epilogue tile
-    constexpr int EPI = BM * EPI_LD * 4;
-    constexpr int LDS = STAGES * STAGE > EPI ? STAGES * STAGE : EPI;
-    constexpr int A_INS = BM / 16, B_INS = BN / 16;   // 1 KiB pieces per plane
-    constexpr int INS = NPL * (A_INS + B_INS);
-    constexpr int PW = INS / NW;                      // pieces per wave per k-step
-    static_assert(INS % NW == 0, "pieces must split evenly over waves");
-    constexpr int TM = BM / WM, TN = BN / WN;         // wave tile
-    constexpr int FM = TM / 16, FN = TN / 16;         // 16x16 MFMA tiles per wave
-    __shared__ __attribute__((aligned(16))) uint8_t lds[LDS];
-
-    const int tid = threadIdx.x;
-    const int lane = tid & 63, wave = tid >> 6;
-    const int wm = wave / WN, wn = wave % WN;
-    const int nbm = (p.M + BM - 1) / BM;
-    const int bm = blockIdx.x % nbm, bn = blockIdx.x / nbm;
-    const int m0 = bm * BM, n0 = bn * BN;
-    const int Mact = p.m_limit ? min(p.M, *p.m_limit * p.rows_per_sample) : p.M;
-    if (m0 >= Mact) return;
-    const int C = p.C, H = p.H, W = p.W, HW = H * W, K = 9 * C;
-    const int cpt = C / 32, nk = 9 * cpt;
-
-    // Per-lane source description of this wave's PW pieces (same rows every k-step).
-    const uint16_t* src_base[PW];     // A: sample base; B: weight row base
-    int src_y[PW], src_x[PW];         // A: pixel coords (-1000: row out of range)
-    bool isA[PW];
-    int lds_off[PW];                  // wave-uniform LDS offset of the piece inside a stage
-    int chunk[PW];                    // logical 16-byte chunk this lane fetches
-#pragma unroll
-    for (int j = 0; j < PW; ++j) {
-        const int q = wave + NW * j;
-        const int row_in_piece = lane >> 2, phys = lane & 3;
-        if (q < NPL * A_INS) {
-            const int plane = q / A_INS, rb = q % A_INS;
-            const int row = rb * 16 + row_in_piece;
-            const int m = m0 + row;
-            isA[j] = true;
-            lds_off[j] = plane * A_BYTES + rb * 1024;
-            chunk[j] = phys ^ swz(row);
-            const uint16_t* base = plane ? p.Alo : p.Ahi;
-            if (m < Mact) {
-                const int b = m / HW, r = m - b * HW;
-                src_base[j] = base + (size_t)b * HW * C;
-                src_y[j] = r / W; src_x[j] = r - (r / W) * W;
-            } else {
-                src_base[j] = base; src_y[j] = -1000; src_x[j] = -1000;
-            }
-        } else {
-            const int qq = q - NPL * A_INS;
-            const int plane = qq / B_INS, rb = qq % B_INS;
-            const int row = rb * 16 + row_in_piece;
-            const int n = n0 + row;
-            isA[j] = false;
-            lds_off[j] = NPL * A_BYTES + plane * B_BYTES + rb * 1024;
-            chunk[j] = phys ^ swz(row);
-            const uint16_t* base = plane ? p.Blo : p.Bhi;
-            src_base[j] = n < p.N ? base + (size_t)n * K : nullptr;
-            src_y[j] = 0; src_x[j] = 0;
-        }
-    }
-    auto issue = [&](int kt) {
-        const int tap = kt / cpt;
-        const int c0 = (kt - tap * cpt) * 32;
-        const int dy = tap / 3 - 1, dx = tap % 3 - 1;
-        uint8_t* stage = lds + (kt % STAGES) * STAGE;
-#pragma unroll
-        for (int j = 0; j < PW; ++j) {
-            const uint16_t* src;
-            if (isA[j]) {
-                const int y = src_y[j] + dy, x = src_x[j] + dx;
-                src = (y >= 0 && y < H && x >= 0 && x < W) ? src_base[j] + ((size_t)(y * W + x) * C + c0 + chunk[j] * 8)
-                                                           : p.zero + chunk[j] * 8;
-            } else {
-                src = src_base[j] ? src_base[j] + (size_t)kt * 32 + chunk[j] * 8 : p.zero + chunk[j] * 8;
-            }
-            __builtin_amdgcn_global_load_lds((g_void_t*)src, (lds_void_t*)(stage + lds_off[j]), 16, 0, 0);
-        }
-    };
-
-    floatx4 acc[FM][FN];
-#pragma unroll
-    for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int j = 0; j < FN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
-
-#pragma unroll
-    for (int s = 0; s < STAGES - 1; ++s)
-        if (s < nk) issue(s);
-    const int fr = lane & 15, fh = lane >> 4;
-    for (int kt = 0; kt < nk; ++kt) {
-        // retire this wave's pieces of k-step kt, leaving later k-steps in flight
-        if (kt + STAGES - 2 < nk) {
-            if constexpr (STAGES == 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PW) : "memory");
-            else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PW * (STAGES - 2)) : "memory");
-        } else {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        __builtin_amdgcn_s_barrier();
-        __builtin_amdgcn_sched_barrier(0);
-        if (kt + STAGES - 1 < nk) issue(kt + STAGES - 1);
-        const uint8_t* st = lds + (kt % STAGES) * STAGE;
-        bf16x8 ah[FM], al[FM], bh[FN], bl[FN];
-#pragma unroll
-        for (int i = 0; i < FM; ++i) {
-            const int row = wm * TM + i * 16 + fr;
-            const int off = row * ROWB + 16 * (fh ^ swz(row));
-            ah[i] = *reinterpret_cast<const bf16x8*>(st + off);
-            if (SPLIT) al[i] = *reinterpret_cast<const bf16x8*>(st + A_BYTES + off);
-        }
-#pragma unroll
-        for (int j = 0; j < FN; ++j) {
-            const int row = wn * TN + j * 16 + fr;
-            const int off = row * ROWB + 16 * (fh ^ swz(row));
-            bh[j] = *reinterpret_cast<const bf16x8*>(st + NPL * A_BYTES + off);
-            if (SPLIT) bl[j] = *reinterpret_cast<const bf16x8*>(st + NPL * A_BYTES + B_BYTES + off);
-        }
-#pragma unroll
-        for (int i = 0; i < FM; ++i)
-#pragma unroll
-            for (int j = 0; j < FN; ++j) {
-                if (SPLIT) {
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
-                }
-                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
-            }
-    }
-    // epilogue: fp32 tile through LDS (ring is free once every wave passed its last read)
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    __syncthreads();
-    float* ep = reinterpret_cast<float*>(lds);
-#pragma unroll
-    for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int j = 0; j < FN; ++j)
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-                ep[(wm * TM + i * 16 + 4 * fh + r) * EPI_LD + wn * TN + j * 16 + fr] = acc[i][j][r];
-    __syncthreads();
-    constexpr int VPR = BN / 8;                        // 8-channel vectors per row
-    for (int v = tid; v < BM * VPR; v += NT) {
-        const int row = v / VPR, cv = (v % VPR) * 8;
-        const int m = m0 + row, n = n0 + cv;
-        if (m >= Mact || n >= p.N) continue;
-        const float4 x0 = *reinterpret_cast<const float4*>(ep + row * EPI_LD + cv);
-        const float4 x1 = *reinterpret_cast<const float4*>(ep + row * EPI_LD + cv + 4);
-        float o[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
-        const size_t g = (size_t)m * p.N + n;
-        const float4 b0 = *reinterpret_cast<const float4*>(p.bias + n);
-        const float4 b1 = *reinterpret_cast<const float4*>(p.bias + n + 4);
-        const float bb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
-        uint16_t rh[8], rl[8];
-        if (p.Rhi) {
-            *reinterpret_cast<uint4*>(rh) = *reinterpret_cast<const uint4*>(p.Rhi + g);
-            if (SPLIT) *reinterpret_cast<uint4*>(rl) = *reinterpret_cast<const uint4*>(p.Rlo + g);
-        }
-        uint16_t oh[8], ol[8];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-            float val = o[e] + bb[e];
-            if (p.Rhi) val += bf2f(rh[e]) + (SPLIT ? bf2f(rl[e]) : 0.0f);
-            if (p.relu) val = val > 0.0f ? val : 0.0f;
-            o[e] = val;
-            oh[e] = f2bf(val);
-            if (SPLIT) ol[e] = f2bf(val - bf2f(oh[e]));
-        }
-        *reinterpret_cast<uint4*>(p.Chi + g) = *reinterpret_cast<const uint4*>(oh);
-        if (SPLIT) *reinterpret_cast<uint4*>(p.Clo + g) = *reinterpret_cast<const uint4*>(ol);
-        if (p.Cf) {
-            *reinterpret_cast<float4*>(p.Cf + g) = make_float4(o[0], o[1], o[2], o[3]);
-            *reinterpret_cast<float4*>(p.Cf + g + 4) = make_float4(o[4], o[5], o[6], o[7]);
-        }
-    }
-}
 
 // ===========================================================================
 // v3: v2's glds ring + fragment double buffering.  The wait/barrier that publishes
@@ -1830,51 +1649,75 @@ static void v6_launch(const ConvBf16Args& a, int mode, hipStream_t st) {
 bool az_conv_v7_supported(const ConvBf16Args& a);
 int az_conv_v7_launch(const ConvBf16Args& a, int mode, int geo15, hipStream_t st);
 
-int az_conv_g8_launch(const ConvBf16Args& a_in, int mode, hipStream_t st) {
-    ConvBf16Args a = a_in;
-    a.flags = g_conv_flags;
-    if (a.H != a.W || !az_conv_g8_supported(a.H, a.W, a.C, a.N)) return -1;
-    if (a.a_tail == 0) a.a_tail = (size_t)a.M * a.C * 2;
+// Which kernel az_conv_g8_launch takes for a layer (a.flags already set): 0 none (unsupported),
+// 1 conv3x3_v7 (*geo = its 15x15 tile geometry), 2 conv3x3_v6 (*geo = 1 when DENSE), 3 conv3x3_v5.
+static int g8_choice(const ConvBf16Args& a, int* geo) {
+    if (a.H != a.W || !az_conv_g8_supported(a.H, a.W, a.C, a.N)) return 0;
     // conv3x3_v7 (conv_v7.hip, two 256-thread blocks per CU, epilogue from registers) takes every
     // layer it supports (trunk convs: C % 64 == 0) unless flag 0x100 selects v6 (A/B measurement);
     // flag 0x200: v7 only on 15x15 boards; 15x15 tile geometry: SLIM (default), flag 8 DENSE, 0x400 PAD.
     // Below 1024 boards a launch is one or two rounds of blocks and v6 is faster (B = 256: 61 vs 65 us);
     // flag 0x800 forces v7 at any batch.
     const int boards_g8 = a.M / (a.H * a.W);
-    if (!(g_conv_flags & 0x100) && (a.H == 15 || !(g_conv_flags & 0x200)) && (boards_g8 >= 1024 || (g_conv_flags & 0x800)) &&
-        az_conv_v7_supported(a))
-        return az_conv_v7_launch(a, mode, (g_conv_flags & 8) ? 2 : (g_conv_flags & 0x400) ? 0 : 1, st);
+    if (!(a.flags & 0x100) && (a.H == 15 || !(a.flags & 0x200)) && (boards_g8 >= 1024 || (a.flags & 0x800)) &&
+        az_conv_v7_supported(a)) {
+        *geo = (a.flags & 8) ? 2 : (a.flags & 0x400) ? 0 : 1;
+        return 1;
+    }
     const size_t HW = (size_t)a.H * a.W;
-    if (a.a_tail == 0) a.a_tail = (size_t)a.M * a.C * 2;
-    if (a.a_tail < (size_t)a.M * a.C * 2) return -1;
+    if (a.a_tail < (size_t)a.M * a.C * 2) return 0;
     // v6: the padding offset walks (C/32) chunk steps of 4*HW*16 B into the zeroed tail, and the
     // buffer descriptor's 32-bit range must cover the activations plus that tail
     const bool v6_ok = a.C % 32 == 0 && a.a_tail + AZ_ACT_TAIL * 2 < ((size_t)1 << 31) &&
                        (size_t)(a.C / 32) * 4 * HW * 16 + 16 <= AZ_ACT_TAIL * 2;
-    if (a.H != 15 || ((g_conv_flags & 4) && a.C % 32 == 0)) {
-        if (!v6_ok || !a.relu) return -1;                // conv3x3_v6 always applies the ReLU
-        switch (a.H) {
-            case 8: v6_launch<8>(a, mode, st); return 0;
-            case 9: v6_launch<9>(a, mode, st); return 0;
-            case 13: v6_launch<13>(a, mode, st); return 0;
-            case 19: v6_launch<19>(a, mode, st); return 0;
-            default: v6_launch<15>(a, mode, st); return 0;
-        }
+    if (a.H != 15 || ((a.flags & 4) && a.C % 32 == 0)) {
+        if (!v6_ok || !a.relu) return 0;                 // conv3x3_v6 always applies the ReLU
+        *geo = (a.flags & 8) || (a.H != 15 && !(a.flags & 0x4000000));
+        return 2;
+    }
+    return 3;
+}
+
+int az_conv_g8_launch(const ConvBf16Args& a_in, int mode, hipStream_t st) {
+    ConvBf16Args a = a_in;
+    a.flags = g_conv_flags;
+    if (a.a_tail == 0) a.a_tail = (size_t)a.M * a.C * 2;
+    int geo = 0;
+    switch (g8_choice(a, &geo)) {
+        case 1: return az_conv_v7_launch(a, mode, geo, st);
+        case 2:
+            switch (a.H) {
+                case 8: v6_launch<8>(a, mode, st); return 0;
+                case 9: v6_launch<9>(a, mode, st); return 0;
+                case 13: v6_launch<13>(a, mode, st); return 0;
+                case 19: v6_launch<19>(a, mode, st); return 0;
+                default: v6_launch<15>(a, mode, st); return 0;
+            }
+        case 3: break;
+        default: return -1;
     }
     const int boards = a.M / 225;
     const int pairs = (boards + 1) / 2;
     const int nsplit = a.N / 128;
     const int grid = (pairs + 7) / 8 * 8 * nsplit;     // XCD-aware pair/half mapping needs whole groups of 8
-    const bool dw4 = (g_conv_flags & 1) != 0;
-    if (mode == 2) {
-        if (g_conv_flags & 2) hipLaunchKernelGGL((conv3x3_v5<2, 8, 2>), dim3(grid), dim3(512), 0, st, a);
-        else if (dw4) hipLaunchKernelGGL((conv3x3_v5<2, 4>), dim3(grid), dim3(512), 0, st, a);
-        else hipLaunchKernelGGL((conv3x3_v5<2, 8>), dim3(grid), dim3(512), 0, st, a);
-    } else {
-        if (dw4) hipLaunchKernelGGL((conv3x3_v5<1, 4>), dim3(grid), dim3(512), 0, st, a);
-        else hipLaunchKernelGGL((conv3x3_v5<1, 8>), dim3(grid), dim3(512), 0, st, a);
-    }
+    if (mode == 2) hipLaunchKernelGGL((conv3x3_v5<2, 8>), dim3(grid), dim3(512), 0, st, a);
+    else hipLaunchKernelGGL((conv3x3_v5<1, 8>), dim3(grid), dim3(512), 0, st, a);
     return 0;
+}
+
+// The name of the kernel az_conv_g8_launch takes for this layer (bench.py's roofline label)
+int az_conv_g8_name(const ConvBf16Args& a_in, int mode, char* out, int len) {
+    ConvBf16Args a = a_in;
+    a.flags = g_conv_flags;
+    if (a.a_tail == 0) a.a_tail = (size_t)a.M * a.C * 2;
+    int geo = 0;
+    static const char* g7[3] = {"PAD", "SLIM", "DENSE"};
+    switch (g8_choice(a, &geo)) {
+        case 1: snprintf(out, len, "conv3x3_v7<%d, %d, %s>", mode, a.H, g7[a.H == 15 ? geo : 2]); return 0;
+        case 2: snprintf(out, len, "conv3x3_v6<%d, %d%s>", mode, a.H, geo ? ", DENSE" : ""); return 0;
+        case 3: snprintf(out, len, "conv3x3_v5<%d, 8>", mode); return 0;
+        default: return -1;
+    }
 }
 
 // fp32 -> fp16 activations (first trunk input, AZ_PREC_FP16)
@@ -1892,62 +1735,56 @@ void az_launch_to_f16(const float* in, uint16_t* out, size_t n, const int* m_lim
 // true when conv3x3_v4 handles this shape
 bool az_conv_v4_supported(int H, int W, int C, int N) { return H == 15 && W == 15 && C % 16 == 0 && N % 64 == 0; }
 
-static int g_v4_sched = 1;
-void az_conv_set_v4_sched(int v) { g_v4_sched = v; }
-
-template <int BNT, int SCHED>
+template <int BNT>
 static void v4_launch(const ConvBf16Args& a, int mode, int grid, hipStream_t st) {
     // bf16x3 keeps the single-buffered schedule: the double buffer spills at 256 VGPRs
     if (mode == 0) hipLaunchKernelGGL((conv3x3_v4<0, BNT, 0>), dim3(grid), dim3(512), 0, st, a);
-    else if (mode == 1) hipLaunchKernelGGL((conv3x3_v4<1, BNT, SCHED>), dim3(grid), dim3(512), 0, st, a);
-    else hipLaunchKernelGGL((conv3x3_v4<2, BNT, SCHED>), dim3(grid), dim3(512), 0, st, a);
+    else if (mode == 1) hipLaunchKernelGGL((conv3x3_v4<1, BNT, 1>), dim3(grid), dim3(512), 0, st, a);
+    else hipLaunchKernelGGL((conv3x3_v4<2, BNT, 1>), dim3(grid), dim3(512), 0, st, a);
 }
 
 void az_conv_v4_launch(const ConvBf16Args& a, int mode, hipStream_t st) {
     const int boards = a.M / 225;
     const int bnt = a.N % 128 == 0 ? 128 : 64;
     const int grid = (boards + 1) / 2 * (a.N / bnt);
-    if (bnt == 128) {
-        if (g_v4_sched) v4_launch<128, 1>(a, mode, grid, st);
-        else v4_launch<128, 0>(a, mode, grid, st);
-    } else {
-        if (g_v4_sched) v4_launch<64, 1>(a, mode, grid, st);
-        else v4_launch<64, 0>(a, mode, grid, st);
+    if (bnt == 128) v4_launch<128>(a, mode, grid, st);
+    else v4_launch<64>(a, mode, grid, st);
+}
+
+// bf16 / bf16x3 trunk conv outside the g8 path: v4 on 15x15 boards, else v3 (N % 256 == 0 or
+// N == 64, C % 32 == 0), else v1 (128 x 128 register-staged tiles, any shape)
+static int bf16_choice(const ConvBf16Args& a) {
+    if (a.rows_per_sample == 225 && az_conv_v4_supported(a.H, a.W, a.C, a.N)) return 4;
+    if (a.C % 32 == 0 && (a.N % 256 == 0 || a.N == 64)) return 3;
+    return 1;
+}
+
+void az_conv_bf16_launch_v(const ConvBf16Args& a, bool split, hipStream_t st) {
+    switch (bf16_choice(a)) {
+        case 4: az_conv_v4_launch(a, split ? 0 : 1, st); return;
+        case 3:
+            if (a.N % 256 == 0) {
+                const int nbm = (a.M + 127) / 128, nbn = a.N / 256;
+                if (split) hipLaunchKernelGGL((conv3x3_v3<true, 128, 256, 2, 4>), dim3(nbm * nbn), dim3(512), 0, st, a);
+                else hipLaunchKernelGGL((conv3x3_v3<false, 128, 256, 2, 4>), dim3(nbm * nbn), dim3(512), 0, st, a);
+            } else {
+                const int nbm = (a.M + 255) / 256;
+                if (split) hipLaunchKernelGGL((conv3x3_v3<true, 256, 64, 4, 1>), dim3(nbm), dim3(256), 0, st, a);
+                else hipLaunchKernelGGL((conv3x3_v3<false, 256, 64, 4, 1>), dim3(nbm), dim3(256), 0, st, a);
+            }
+            return;
+        default: az_conv_bf16_launch(a, split, st); return;
     }
 }
 
-// variant selector: 0 = v1 (128x128, register staged), 1 = v2 (glds ring), 2 = v3
-static int g_conv_variant = 3;
-void az_conv_set_variant(int v) { g_conv_variant = v; }
-
-void az_conv_bf16_launch_v(const ConvBf16Args& a, bool split, hipStream_t st) {
-    if (g_conv_variant == 3 && a.rows_per_sample == 225 && az_conv_v4_supported(a.H, a.W, a.C, a.N)) {
-        az_conv_v4_launch(a, split ? 0 : 1, st);
-        return;
-    }
-    if (g_conv_variant >= 2 && a.N % 256 == 0 && a.C % 32 == 0) {
-        const int nbm = (a.M + 127) / 128, nbn = a.N / 256;
-        if (split) hipLaunchKernelGGL((conv3x3_v3<true, 128, 256, 2, 4>), dim3(nbm * nbn), dim3(512), 0, st, a);
-        else hipLaunchKernelGGL((conv3x3_v3<false, 128, 256, 2, 4>), dim3(nbm * nbn), dim3(512), 0, st, a);
-        return;
-    }
-    if (g_conv_variant >= 2 && a.N == 64 && a.C % 32 == 0) {
-        const int nbm = (a.M + 255) / 256;
-        if (split) hipLaunchKernelGGL((conv3x3_v3<true, 256, 64, 4, 1>), dim3(nbm), dim3(256), 0, st, a);
-        else hipLaunchKernelGGL((conv3x3_v3<false, 256, 64, 4, 1>), dim3(nbm), dim3(256), 0, st, a);
-        return;
-    }
-    if (g_conv_variant >= 1 && a.N % 256 == 0 && a.C % 32 == 0) {
-        const int nbm = (a.M + 127) / 128, nbn = a.N / 256;
-        if (split) hipLaunchKernelGGL((conv3x3_v2<true, 128, 256, 2, 4, 3>), dim3(nbm * nbn), dim3(512), 0, st, a);
-        else hipLaunchKernelGGL((conv3x3_v2<false, 128, 256, 2, 4, 4>), dim3(nbm * nbn), dim3(512), 0, st, a);
-        return;
-    }
-    if (g_conv_variant >= 1 && a.N == 64 && a.C % 32 == 0) {
-        const int nbm = (a.M + 255) / 256;
-        if (split) hipLaunchKernelGGL((conv3x3_v2<true, 256, 64, 4, 1, 3>), dim3(nbm), dim3(256), 0, st, a);
-        else hipLaunchKernelGGL((conv3x3_v2<false, 256, 64, 4, 1, 4>), dim3(nbm), dim3(256), 0, st, a);
-        return;
-    }
-    az_conv_bf16_launch(a, split, st);
+// The name of the kernel az_conv_bf16_launch_v (mode 0 bf16x3 / 1 bf16) or, for fp16 (mode 2),
+// az_conv_v4_launch takes for this layer
+int az_conv_bf16_name(const ConvBf16Args& a, int mode, char* out, int len) {
+    const int c = mode == 2 ? 4 : bf16_choice(a);
+    const bool split = mode == 0;
+    if (c == 4) snprintf(out, len, "conv3x3_v4<%d, %d>", mode, a.N % 128 == 0 ? 128 : 64);
+    else if (c == 3) snprintf(out, len, a.N % 256 == 0 ? "conv3x3_v3<%s, 128, 256>" : "conv3x3_v3<%s, 256, 64>",
+                              split ? "split" : "bf16");
+    else snprintf(out, len, "conv3x3_bf16<%s>", split ? "split" : "bf16");
+    return 0;
 }

@@ -40,10 +40,10 @@ __global__ void k_root_nchild(TreeDev t, int* out);
 __global__ void k_root_children(TreeDev t, int g, int* act, int* N, int* VL, float* W, float* P, int* n, int* rootinfo,
                                 float* rootW);
 void az_conv_bf16_launch_v(const ConvBf16Args& a, bool split, hipStream_t st);
-void az_conv_set_variant(int v);
 bool az_conv_v4_supported(int H, int W, int C, int N);
 void az_conv_v4_launch(const ConvBf16Args& a, int mode, hipStream_t st);
-void az_conv_set_v4_sched(int v);
+int az_conv_bf16_name(const ConvBf16Args& a, int mode, char* out, int len);
+int az_conv_g8_name(const ConvBf16Args& a, int mode, char* out, int len);
 extern "C" int az_diag_set_conv_flags(int flags);
 bool az_conv_g8_supported(int H, int W, int C, int N);
 int az_conv_g8_launch(const ConvBf16Args& a, int mode, hipStream_t st);
@@ -756,8 +756,6 @@ int az_net_create(az_engine* e, const az_net_desc* d, az_net** out) {
     if (!r) r = dalloc(&n->d_nb, 1);
     if (!r) r = dalloc(&n->zero, 128);
     if (!r && hipMemset(n->zero, 0, 256) != hipSuccess) r = az_fail(AZ_ERR_HIP, "memset");
-    if (const char* v = getenv("AZ_CONV_VARIANT")) az_conv_set_variant(atoi(v));
-    if (const char* v = getenv("AZ_V4_SCHED")) az_conv_set_v4_sched(atoi(v));
     if (const char* v = getenv("AZ_CONV_FLAGS")) az_diag_set_conv_flags(atoi(v));
     if (r) { az_net_destroy(n); return r; }
     *out = n;
@@ -872,6 +870,23 @@ static int net_host_forward(az_net* n, const float* planes, int B, float* logits
     if (value) HIPCHK(hipMemcpyAsync(value, n->value, (size_t)B * 4, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
     return 0;
+}
+
+int az_net_trunk_kernel(az_net* n, char* name, int len) {
+    if (!n || !name || len < 1) return az_fail(AZ_ERR_ARG, "null net / name");
+    const az_net_desc& d = n->d;
+    const int prec = d.precision, F = d.channels, H = d.board_size;
+    const bool bf = (prec == AZ_PREC_BF16X3 || prec == AZ_PREC_BF16 || prec == AZ_PREC_FP16) && F % 32 == 0;
+    const bool f16 = prec == AZ_PREC_FP16;
+    if (!bf || d.blocks < 1) { snprintf(name, len, "gemm_f32"); return 0; }
+    // the trunk's second conv of a block, as net_forward builds it at the net's capacity
+    ConvBf16Args a{};
+    a.M = d.max_batch * n->HW; a.N = F; a.C = F; a.H = H; a.W = H; a.rows_per_sample = n->HW; a.relu = 1;
+    a.a_tail = n->act_elems * 2;
+    const bool g8 = prec != AZ_PREC_BF16X3 && az_conv_g8_supported(H, H, F, F);
+    const int r = g8 ? az_conv_g8_name(a, f16 ? 2 : 1, name, len)
+                     : az_conv_bf16_name(a, f16 ? 2 : prec == AZ_PREC_BF16X3 ? 0 : 1, name, len);
+    return r ? az_fail(AZ_ERR_ARG, "no trunk kernel for this net") : 0;
 }
 
 int az_net_profile(az_net* n, int enable) {

@@ -153,15 +153,6 @@ class GpuWorkload:
         pass                           # selfplayStep returns after a stream synchronize
 
 
-def conv_kernel_name(a):
-    if a.precision == "f32":
-        return "gemm_f32"
-    if a.channels % 128 == 0:
-        return f"conv3x3_v6<{2 if a.precision == 'fp16' else 1}, {a.board}>" if a.precision != "bf16x3" else \
-            "conv3x3_v4<0,128>"
-    return f"conv3x3_v4<{ {'fp16': 2, 'bf16': 1, 'bf16x3': 0}[a.precision] },64>"
-
-
 def run_rank(a, rank, world, dist, make_workload, coll_device):
     """One rank of the bench: shard, weights (rank 0 init + broadcast), warmup, timed steps between
     barriers, MAX elapsed / SUM counters over ranks.  Returns the JSON dict on rank 0, else None."""
@@ -207,6 +198,7 @@ def run_rank(a, rank, world, dist, make_workload, coll_device):
     if rank != 0:
         return None
 
+    kernel = net.trunk_kernel()      # the kernel the library dispatches for this net (engine's own choice)
     HW = a.board * a.board
     conv_flops_per_eval = 2 * a.blocks * 2.0 * 9 * a.channels * a.channels * HW
     boards_per_launch = my_evals * 2 * a.blocks / max(1, launches)        # rank 0's own launches and boards
@@ -235,8 +227,8 @@ def run_rank(a, rank, world, dist, make_workload, coll_device):
                    "blocks": a.blocks, "channels": a.channels, "parallelism": f"game-shard x{world}"},
         "nn_evals_per_s": tot_evals / elapsed,
         "evals_per_move": tot_evals / max(1, tot_moves),
-        "roofline": {"kernel": f"{conv_kernel_name(a)} ({a.precision} trunk, {a.board}x{a.board}, "
-                               f"{a.channels} ch)", "bound": "mfma",
+        "roofline": {"kernel": f"{kernel} ({a.precision} trunk, {a.board}x{a.board}, {a.channels} ch)",
+                     "bound": "mfma",
                      "achieved": achieved, "peak": peak, "unit": "TFLOP/s", "frac": achieved / peak, "traffic": None,
                      "launches": launches, "avg_launch_ms": per_launch_ms, "boards_per_launch": boards_per_launch,
                      "flops_per_launch": per_launch_flops},
@@ -253,17 +245,17 @@ def run_rank(a, rank, world, dist, make_workload, coll_device):
                                    "read-modify-writes, new nodes, leaf planes); latency-bound (one wave per game, "
                                    "dependent tree levels), peak 8 TB/s; rocprofv3 PMC traffic of the same kernels: "
                                    "profiles/r01e_tree_pmc.json (tools/tree_pmc.sh)")
-    tr = pmc_traffic(a, boards_per_launch if launches else 0)
+    tr = pmc_traffic(a, kernel, boards_per_launch if launches else 0)
     if tr:
         out["roofline"].update(tr)
     return out
 
 
-def pmc_traffic(a, boards_per_launch):
+def pmc_traffic(a, kernel, boards_per_launch):
     """HBM bytes per trunk launch from the committed rocprofv3 PMC summary of the same kernel
     (profiles/*_trunk_pmc.json: FETCH_SIZE x2 per the gfx950 correction + WRITE_SIZE, measured at
     B boards per launch), scaled to this run's average boards per launch.  None if no summary
-    matches the precision / net."""
+    matches the kernel (template name) and the precision / net."""
     import glob
     best = None
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_trunk_pmc.json"))):
@@ -272,7 +264,7 @@ def pmc_traffic(a, boards_per_launch):
         except (OSError, ValueError):
             continue
         if (d.get("precision"), d.get("board"), d.get("channels"), d.get("blocks")) == \
-                (a.precision, a.board, a.channels, a.blocks):
+                (a.precision, a.board, a.channels, a.blocks) and _same_kernel(d.get("kernel", ""), kernel):
             best = (f, d)
     if best is None or boards_per_launch <= 0:
         return None
@@ -280,6 +272,15 @@ def pmc_traffic(a, boards_per_launch):
     scale = boards_per_launch / d["boards_per_launch"]
     return {"traffic": d["hbm_bytes_per_launch"] * scale, "traffic_unit": "bytes/launch",
             "traffic_source": os.path.relpath(f, ROOT) + f" (PMC at B={d['boards_per_launch']}, scaled x{scale:.4f})"}
+
+
+def _same_kernel(profiled, name):
+    """rocprof's demangled name ("void conv3x3_v7<2, 15, 1>(ConvBf16Args)") vs the library's label
+    ("conv3x3_v7<2, 15, SLIM>"): same template and first two template arguments."""
+    import re
+    m1 = re.search(r"(conv3x3_v\d+)<(\d+), ?(\d+)", profiled)
+    m2 = re.search(r"(conv3x3_v\d+)<(\d+), ?(\d+)", name)
+    return bool(m1 and m2 and m1.groups() == m2.groups())
 
 
 # ------------------------------------------------------------------------------- CPU baseline

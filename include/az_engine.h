@@ -95,6 +95,9 @@ int az_net_forward(az_net* n, const float* planes, int B, float* logits, float* 
  * simulation-batch forward on the engine stream.  read returns the summed trunk time. */
 int az_net_profile(az_net* n, int enable);
 int az_net_profile_read(az_net* n, double* trunk_ms, int64_t* trunk_launches, int64_t* forwards);
+/* The name of the HIP kernel the 3x3 trunk convs of this net dispatch at its max_batch
+ * (measurement label, e.g. "conv3x3_v7<2, 15, SLIM>"; "gemm_f32" for the f32 path). */
+int az_net_trunk_kernel(az_net* n, char* name, int len);
 /* predictBatch semantics: policy = softmax over A (max-subtracted, sequential fp32 sum,
  * torch_neural_network.cpp:296-316), value [B]. */
 int az_net_predict_batch(az_net* n, const float* planes, int B, float* policy, float* value);

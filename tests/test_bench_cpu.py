@@ -48,6 +48,9 @@ class _Net:
     def profile_read(self):
         return 4.0, 40 * 2, 2      # 4 ms over 80 trunk launches
 
+    def trunk_kernel(self):
+        return "conv3x3_v7<2, 15, SLIM>"
+
 
 class _Mcts:
     def profile(self, on):

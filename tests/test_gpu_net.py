@@ -254,3 +254,23 @@ def test_gpu_c5_net_full_batch(engine):
     lo2, v2 = net.forward(x[517:530])
     assert np.array_equal(lo2, lo[517:530]) and np.array_equal(v2, v[517:530])
     net.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", [
+    # (board, in_planes, channels, blocks, actions, precision, max_batch) -> trunk kernel prefix
+    ((15, 11, 256, 20, 225, "fp16", 2048), "conv3x3_v7<2, 15, SLIM>"),   # C3 at N = 1, 2
+    ((15, 11, 256, 20, 225, "fp16", 256), "conv3x3_v6<2, 15>"),          # C3 shard at N = 8
+    ((15, 11, 64, 6, 225, "fp16", 256), "conv3x3_v4<2, 64>"),            # C2
+    ((15, 11, 256, 20, 225, "bf16x3", 64), "conv3x3_v4<0, 128>"),
+    ((19, 8, 256, 20, 362, "fp16", 1024), "conv3x3_v6<2, 19, DENSE>"),   # C4
+    ((15, 11, 32, 2, 225, "f32", 4), "gemm_f32"),
+])
+def test_gpu_trunk_kernel_name(engine, case):
+    """az_net_trunk_kernel names the kernel the trunk actually dispatches (bench.py's roofline label)."""
+    import az_amd
+    (bs, ci, ch, blocks, A, prec, B), want = case
+    p = {"f32": az_amd.AZ_PREC_F32, "bf16x3": az_amd.AZ_PREC_BF16X3, "fp16": az_amd.AZ_PREC_FP16}[prec]
+    net = az_amd.HipNeuralNetwork(engine, az_amd.NetDesc(bs, ci, ch, blocks, A, 32, 8, 256, 1, 0, p, B))
+    assert net.trunk_kernel() == want
+    net.close()
