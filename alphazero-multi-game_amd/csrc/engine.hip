@@ -109,6 +109,9 @@ struct az_net {
     float* in_nchw = nullptr;
     int* d_nb = nullptr;
     uint16_t* zero = nullptr;   // 256 zero bytes: glds source for the board edge
+    // k_smallnet (64-filter fp16 nets): [2*blocks+1][9][64][64] fp16 trunk weights incl. the input conv, biases
+    uint16_t* sm_W = nullptr;
+    float* sm_b = nullptr;
     bool loaded = false;
     std::vector<float> host_blob;   // canonical blob of the loaded weights (az_net_get_weights)
     // profiling: HIP events bracketing the 3x3 trunk of every forward (on the launch stream)
@@ -208,12 +211,35 @@ int net_load(az_net* n, const float* blob) {
     const int F = d.channels, HC = d.head_channels, PP = d.pool * d.pool;
     std::vector<float> W, b;
     const bool split = F % 32 == 0;
+    // k_smallnet weights: every 3x3 layer as [tap][n][c] fp16 over 64 channels (input conv zero-padded)
+    const bool sm = d.precision == AZ_PREC_FP16 && az_smallnet_supported(d.board_size, F, n->cin_pad, d.pool, HC) &&
+                    d.blocks <= az_smallnet_max_blocks();
+    std::vector<uint16_t> smw;
+    std::vector<float> smb;
+    auto sm_add = [&](const std::vector<float>& Wl, const std::vector<float>& bl, int cl) {
+        const size_t o = smw.size();
+        smw.resize(o + (size_t)9 * F * F, 0);
+        for (int t = 0; t < 9; ++t)
+            for (int nn = 0; nn < F; ++nn)
+                for (int c = 0; c < cl; ++c) {
+                    _Float16 h = (_Float16)Wl[((size_t)nn * 9 + t) * cl + c];
+                    std::memcpy(&smw[o + ((size_t)t * F + nn) * F + c], &h, 2);
+                }
+        smb.insert(smb.end(), bl.begin(), bl.end());
+    };
     fold_conv(pc, F, d.in_planes, 3, n->cin_pad, d.conv_bias, W, b);
     if (int r = upload_layer(n->in, W, b, F, 9 * n->cin_pad, 9, n->cin_pad, F % 32 == 0)) return r;  // 16-bit copies: g8 input conv
+    if (sm) sm_add(W, b, n->cin_pad);
     n->blk.resize(2 * d.blocks);
     for (int i = 0; i < 2 * d.blocks; ++i) {
         fold_conv(pc, F, F, 3, F, d.conv_bias, W, b);
         if (int r = upload_layer(n->blk[i], W, b, F, 9 * F, 9, F, split)) return r;
+        if (sm) sm_add(W, b, F);
+    }
+    if (sm) {
+        if (!n->sm_W) { DALLOC(n->sm_W, smw.size()); DALLOC(n->sm_b, smb.size()); }
+        HIPCHK(hipMemcpy(n->sm_W, smw.data(), smw.size() * 2, hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(n->sm_b, smb.data(), smb.size() * 4, hipMemcpyHostToDevice));
     }
     // policy head: 1x1 conv + BN, FC over the flattened (c, y, x) pooled map
     fold_conv(pc, HC, F, 1, F, d.conv_bias, W, b);
@@ -255,13 +281,17 @@ GemmArgs gemm_args(const Layer& L, const float* A, int lda, float* C, int ldc, c
     return p;
 }
 
-// K slices for an FC layer of B rows: enough blocks to cover the chip, slices of >= 256 K
+// K slices for an FC layer of B rows: enough blocks to cover the chip (a 128 x 128 f32 tile is
+// bound by the CU's f32 MFMA rate), slices of >= 64 K
+constexpr int FC_MAX_SPLITS = 64;
 static int fc_splits(int B, int K) {
     const int tiles = (B + 127) / 128 * 2;
     int s = 1;
-    while (s < 16 && tiles * s < 512 && K / (2 * s) >= 256) s *= 2;
+    while (s < FC_MAX_SPLITS && tiles * s < 512 && K / (2 * s) >= 64) s *= 2;
     return s;
 }
+
+int net_heads_fc(az_net* n, int B, const int* nb, float* logits, float* value, hipStream_t st);
 
 // Forward of B samples (B = capacity; *nb = active samples, device side) from the
 // NHWC16 input x0 -> logits [B][A], value [B].
@@ -276,6 +306,32 @@ int net_forward(az_net* n, const float* x0, int B, const int* nb, float* logits,
     const bool g8 = bf && prec != AZ_PREC_BF16X3 && az_conv_g8_supported(H, W, F, F);
     const int mode = f16 ? 2 : 1;
     int8_t* hq[2] = {reinterpret_cast<int8_t*>(n->hl[0]), reinterpret_cast<int8_t*>(n->hl[1])};
+    if (n->sm_W && prec == AZ_PREC_FP16 && d.blocks > 0) {
+        // one launch: input conv, trunk, pool and the two head 1x1 convs (smallnet.hip)
+        hipEvent_t e0 = nullptr, e1 = nullptr;
+        if (n->prof) {
+            while (n->evpool.size() < n->evused + 2) {
+                hipEvent_t ev;
+                HIPCHK(hipEventCreate(&ev));
+                n->evpool.push_back(ev);
+            }
+            e0 = n->evpool[n->evused]; e1 = n->evpool[n->evused + 1];
+            n->evused += 2;
+            n->prof_launches += 2 * d.blocks;    // counted in trunk-conv equivalents (bench.py's per-conv rate)
+            n->prof_forwards += 1;
+            HIPCHK(hipEventRecord(e0, st));
+        }
+        SmallNetArgs sa{};
+        sa.x0 = x0; sa.m_limit = nb; sa.W = n->sm_W; sa.bias = n->sm_b;
+        sa.Wpc = n->pconv.W; sa.bpc = n->pconv.b; sa.Wvc = n->vconv.W; sa.bvc = n->vconv.b;
+        sa.pp = n->pp; sa.vp = n->vp;
+        sa.H = H; sa.blocks = d.blocks; sa.residual = d.residual; sa.HC = d.head_channels; sa.P = P;
+        static const int stamps = getenv("AZ_SM_STAMPS") ? atoi(getenv("AZ_SM_STAMPS")) : 0;   // diagnostic phase stamps
+        sa.stamps = stamps;
+        if (az_smallnet_launch(sa, B, st)) return az_fail(AZ_ERR_ARG, "smallnet: unsupported shape");
+        if (e1) HIPCHK(hipEventRecord(e1, st));
+        return net_heads_fc(n, B, nb, logits, value, st);
+    }
     if (g8 && n->in.Wbk_h != nullptr && az_conv_g8_supported(H, W, n->cin_pad, F)) {
         // input planes -> g8 16-bit (0/1 planes are exact), then the input conv on the g8 kernel
         az_launch_to_g8(x0, n->th, nullptr, n->cin_pad, HW, nb, B, mode, st);
@@ -397,15 +453,26 @@ int net_forward(az_net* n, const float* x0, int B, const int* nb, float* logits,
     if (!g8) az_launch_pool(h, n->pool, B, H, W, F, P, nb, st);
     az_launch_gemm_f32(gemm_args(n->pconv, n->pool, F, n->pp, d.head_channels, nullptr, B * PP, 1, 1, nb, PP), ACT_RELU, false, st);
     az_launch_gemm_f32(gemm_args(n->vconv, n->pool, F, n->vp, d.head_channels, nullptr, B * PP, 1, 1, nb, PP), ACT_RELU, false, st);
+    return net_heads_fc(n, B, nb, logits, value, st);
+}
+
+// The FC layers of both heads from the head feature maps pp / vp ([B][P*P][HC]).
+int net_heads_fc(az_net* n, int B, const int* nb, float* logits, float* value, hipStream_t st) {
+    const az_net_desc& d = n->d;
+    const int PP = n->P2;
     const int HK = d.head_channels * PP;
-    // FC layers: few rows, long K -> split-K over the workspace (deterministic reduction)
+    // FC layers: few rows, long K -> split-K partials (deterministic reductions).  The policy FC
+    // reduces into the logits; the value head's FC1 partials are reduced, ReLU'd and dotted with FC2
+    // by one kernel per board (k_value_head: FC1 + FC2 + tanh)
     GemmArgs pf = gemm_args(n->pfc, n->pp, HK, logits, d.action_size, nullptr, B, 1, 1, nb, 1);
     GemmArgs v1 = gemm_args(n->vfc1, n->vp, HK, n->v1, d.fc_hidden, nullptr, B, 1, 1, nb, 1);
     const int splits = fc_splits(B, HK);
-    if (splits > 1) { pf.part = v1.part = n->ws; pf.splits = v1.splits = splits; }
-    az_launch_gemm_f32(pf, ACT_NONE, false, st);
-    az_launch_gemm_f32(v1, ACT_RELU, false, st);
-    az_launch_gemm_f32(gemm_args(n->vfc2, n->v1, d.fc_hidden, value, 1, nullptr, B, 1, 1, nb, 1), ACT_TANH, false, st);
+    pf.part = n->ws; pf.splits = splits;
+    v1.part = n->ws + (size_t)B * d.action_size * splits; v1.splits = splits;
+    if (splits > 1) az_launch_gemm_f32(pf, ACT_NONE, false, st);
+    else { pf.part = nullptr; az_launch_gemm_f32(pf, ACT_NONE, false, st); }
+    az_launch_gemm_f32_partials(v1, st);
+    az_launch_value_head(v1.part, splits, n->vfc1.b, n->vfc2.W, n->vfc2.b, n->v1, value, B, d.fc_hidden, nb, st);
     HIPCHK(hipGetLastError());
     return 0;
 }
@@ -750,7 +817,7 @@ int az_net_create(az_engine* e, const az_net_desc* d, az_net** out) {
     A_(&n->pool, B * n->P2 * F);
     A_(&n->pp, B * n->P2 * d->head_channels); A_(&n->vp, B * n->P2 * d->head_channels);
     A_(&n->v1, B * d->fc_hidden);
-    A_(&n->ws, (size_t)B * std::max(d->action_size, d->fc_hidden) * 16);
+    A_(&n->ws, (size_t)B * (d->action_size + d->fc_hidden) * FC_MAX_SPLITS);
     A_(&n->logits, B * d->action_size); A_(&n->value, B); A_(&n->soft, B * d->action_size);
     A_(&n->in_nchw, B * d->in_planes * n->HW);
     if (!r) r = dalloc(&n->d_nb, 1);
@@ -772,7 +839,7 @@ void az_net_destroy(az_net* n) {
     for (void* p : {(void*)n->x0, (void*)n->h0, (void*)n->h1, (void*)n->t, (void*)n->pool, (void*)n->pp, (void*)n->vp,
                     (void*)n->v1, (void*)n->ws, (void*)n->logits, (void*)n->value, (void*)n->soft, (void*)n->in_nchw, (void*)n->d_nb,
                     (void*)n->hh[0], (void*)n->hh[1], (void*)n->hl[0], (void*)n->hl[1], (void*)n->th, (void*)n->tl,
-                    (void*)n->zero})
+                    (void*)n->zero, (void*)n->sm_W, (void*)n->sm_b})
         F(p);
     delete n;
 }
@@ -879,6 +946,10 @@ int az_net_trunk_kernel(az_net* n, char* name, int len) {
     const bool bf = (prec == AZ_PREC_BF16X3 || prec == AZ_PREC_BF16 || prec == AZ_PREC_FP16) && F % 32 == 0;
     const bool f16 = prec == AZ_PREC_FP16;
     if (!bf || d.blocks < 1) { snprintf(name, len, "gemm_f32"); return 0; }
+    if (f16 && az_smallnet_supported(H, F, n->cin_pad, d.pool, d.head_channels) && d.blocks <= az_smallnet_max_blocks()) {
+        snprintf(name, len, "k_smallnet<%d>", H);
+        return 0;
+    }
     // the trunk's second conv of a block, as net_forward builds it at the net's capacity
     ConvBf16Args a{};
     a.M = d.max_batch * n->HW; a.N = F; a.C = F; a.H = H; a.W = H; a.rows_per_sample = n->HW; a.relu = 1;

@@ -44,7 +44,26 @@ struct ConvBf16Args {
     int flags;                                  // kernel variant bits (az_diag_set_conv_flags; A/B tests)
 };
 
+// k_smallnet (smallnet.hip): the whole trunk + pool + head 1x1 convs of a 64-filter net, one board per block
+struct SmallNetArgs {
+    const float* x0;                // leaf planes [B][H*W][16] fp32 (NHWC16)
+    const int* m_limit;             // device: active boards
+    const uint16_t* W;              // [2*blocks+1][9][64 n][64 c] fp16, BN folded; layer 0 = input conv (c >= planes zero)
+    const float* bias;              // [2*blocks+1][64]
+    const float* Wpc; const float* bpc;   // policy 1x1 conv [HC][64], [HC] (BN folded)
+    const float* Wvc; const float* bvc;   // value 1x1 conv
+    float* pp; float* vp;           // head feature maps [B][P*P][HC] fp32
+    int H, blocks, residual, HC, P;
+    int stamps;                     // diagnostic: block 0 writes phase stamps (az_diag_smallnet_stamps)
+};
+bool az_smallnet_supported(int H, int C, int cin_pad, int pool, int head_channels);
+int az_smallnet_max_blocks();
+int az_smallnet_launch(const SmallNetArgs& a, int B, hipStream_t st);
+
 void az_launch_gemm_f32(const GemmArgs& p, int act, bool res, hipStream_t st);
+void az_launch_gemm_f32_partials(const GemmArgs& p, hipStream_t st);
+void az_launch_value_head(const float* part, int splits, const float* b1, const float* w2, const float* b2, float* hid,
+                          float* value, int B, int H, const int* m_limit, hipStream_t st);
 void az_launch_pool(const float* in, float* out, int B, int H, int W, int C, int P, const int* m_limit, hipStream_t st);
 void az_launch_pack_input(const float* in, float* out, int B, int Cin, int HW, int Cp, hipStream_t st);
 void az_launch_gather_planes(const float* src, float* dst, const int* eval_games, const int* n_eval, int per, int maxB,

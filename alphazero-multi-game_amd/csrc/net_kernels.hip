@@ -284,6 +284,45 @@ static void launch_f32(const GemmArgs& p, hipStream_t st) {
     hipLaunchKernelGGL((gemm_f32<BN, ACT, RES>), dim3(nbm * nbn), dim3(256), 0, st, q);
 }
 
+// split-K partial sums only (p.part, p.splits): the caller reduces them
+void az_launch_gemm_f32_partials(const GemmArgs& p, hipStream_t st) {
+    const int nbm = (p.M + 127) / 128;
+    if (p.N <= 64) hipLaunchKernelGGL((gemm_f32<64, ACT_NONE, false>), dim3(nbm * ((p.N + 63) / 64), p.splits), dim3(256), 0, st, p);
+    else hipLaunchKernelGGL((gemm_f32<128, ACT_NONE, false>), dim3(nbm * ((p.N + 127) / 128), p.splits), dim3(256), 0, st, p);
+}
+
+// Value head after FC1's split-K partials, one block per board: h = relu(sum_s part[s][b] + b1)
+// (slices summed in order), value = tanh(sum_n h[n] * w2[n] + b2) with a fixed-order block
+// reduction.  H <= 1024 hidden units.
+__global__ __launch_bounds__(256) void k_value_head(const float* part, int splits, const float* b1, const float* w2,
+                                                    const float* b2, float* hid, float* value, int B, int H,
+                                                    const int* m_limit) {
+    const int b = blockIdx.x;
+    if (m_limit && b >= *m_limit) return;
+    __shared__ float red[256];
+    float acc = 0.0f;
+    for (int n = threadIdx.x; n < H; n += 256) {
+        float v = 0.0f;
+        for (int s = 0; s < splits; ++s) v += part[((size_t)s * B + b) * H + n];
+        v += b1[n];
+        v = v > 0.0f ? v : 0.0f;
+        hid[(size_t)b * H + n] = v;
+        acc = __builtin_fmaf(v, w2[n], acc);
+    }
+    red[threadIdx.x] = acc;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) value[b] = tanhf(red[0] + b2[0]);
+}
+
+void az_launch_value_head(const float* part, int splits, const float* b1, const float* w2, const float* b2, float* hid,
+                          float* value, int B, int H, const int* m_limit, hipStream_t st) {
+    hipLaunchKernelGGL(k_value_head, dim3(B), dim3(256), 0, st, part, splits, b1, w2, b2, hid, value, B, H, m_limit);
+}
+
 void az_launch_gemm_f32(const GemmArgs& p, int act, bool res, hipStream_t st) {
     const bool small = p.N <= 64;
     if (small) {

@@ -1,0 +1,352 @@
+// smallnet.hip -- the whole ConvNet trunk of a small net in ONE launch, one board per block
+// (fp16 MFMA operands, fp32 accumulation, fp32 residual stream).
+//
+// For 64-filter nets (BASELINE.json C2: 15x15, 6 blocks x 64 filters, 256 games) a trunk conv is
+// 4.2 GFLOP at 256 boards: one launch per layer is latency-bound (a 2-board v4 tile gives 128
+// blocks for 256 CUs) and the activations make an HBM round trip per layer.  A board's
+// activations are small (225 px x 64 ch: 57.6 KB fp32, 28.8 KB fp16), so one 256-thread block
+// keeps them in LDS through every layer:
+//
+//   input planes -> input conv -> 2*blocks residual convs -> adaptive pool -> policy / value 1x1 convs
+//
+// and writes only the two head feature maps (pp / vp, [board][P*P][HC] fp32, the layout the FC
+// layers read).  Weights stream per tap from L2 (every block reads the same 74 KB per layer) into a
+// ring of LDS tiles with global_load_lds; one barrier per tap.
+//
+// The fp32 residual stream stays in REGISTERS: a lane owns the same (pixel, 4 channels) outputs in
+// every layer, so the second conv of a block adds its own values (64 VGPRs per lane).
+// LDS (15x15): two zero-padded halo images X and Y fp16 [IR][64] (2 x 37.4 KB), a ring of 8 weight
+// tiles [64 n][64 c] fp16 (8 x 8 KB, loaded 6 taps ahead so the L2 latency is hidden), the biases.
+// Every tap ends with a barrier that certifies the weight tile two taps ahead, so the fragments of
+// the next (tap, chunk) step are read while the current step's 16 MFMAs run.
+// Rows of 64 fp16 channels
+// are 8 chunks of 16 B stored at chunk ^ (row & 7): conflict-free ds_read_b128 for every tap shift.
+// Outputs live on the HB x (HB+2) grid (two dead columns per row): tap (dy, dx) of output grid row q
+// is halo row q + dy*(HB+2) + dx, so an operand fragment is 16 consecutive halo rows.
+//
+// MFMA v_mfma_f32_16x16x32_f16 with the weights as the 16-row operand and the activations as the
+// 16-column one: a lane's accumulator holds 4 consecutive output channels of one pixel, so the
+// epilogue (bias already in the accumulator, residual join, ReLU) writes xs and the next image from
+// registers.  Layer roles: 0 = input conv (reads Y = planes, writes xs + X), odd = first conv of a
+// residual block (reads X, writes Y), even >= 2 = second conv (reads Y, adds xs, writes xs + X).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <type_traits>
+
+#include "net.h"
+
+namespace {
+
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void lds_void_t;
+
+constexpr int SF = 64;           // filters (channels) of the fused trunk
+
+template <int HB>
+struct SmGeom {
+    static constexpr int WG = HB + 2;                    // grid / halo row width
+    static constexpr int HW = HB * HB;
+    static constexpr int GRID = HB * WG;                 // output grid rows
+    static constexpr int NFRAG = (GRID + 15) / 16;       // 16-row pixel fragments
+    static constexpr int FPW = (NFRAG + 3) / 4;          // fragments per wave (4 waves)
+    static constexpr int IR = NFRAG * 16 + 2 * WG + 2;   // halo rows the last fragment's taps read
+    static constexpr int IMG = IR * SF * 2;              // bytes of one halo image
+    static constexpr int XS = HW * SF * 4;               // fp32 stream at the end (over the two images)
+    static constexpr int WT = SF * SF * 2;               // bytes of one tap's weight tile
+    static constexpr int NSLOT = 8, DIST = 6;            // weight ring: tiles DIST taps ahead
+    static constexpr int MAXL = 32;                      // layers (biases staged in LDS)
+    static constexpr int LDS = 2 * IMG + NSLOT * WT + MAXL * SF * 4;
+    static_assert(LDS <= 160 * 1024, "board does not fit the CU's LDS");
+    static_assert(XS <= 2 * IMG, "fp32 stream does not fit over the images");
+};
+
+__device__ __forceinline__ uint32_t img_off(int row, int chunk) {   // byte offset of (row, 16-B chunk)
+    return (uint32_t)(row * 128 + ((chunk ^ (row & 7)) << 4));
+}
+__device__ __forceinline__ uint32_t xs_off(int p, int chunk4) {     // fp32 stream: 16 chunks of 4 channels
+    return (uint32_t)(p * 256 + ((chunk4 ^ (p & 15)) << 4));
+}
+
+template <int I, int N, typename Fn>
+__device__ __forceinline__ void static_for(Fn&& f) {
+    if constexpr (I < N) {
+        f(std::integral_constant<int, I>{});
+        static_for<I + 1, N>(f);
+    }
+}
+
+// diagnostic phase stamps of block 0 (s_memrealtime, 100 MHz): SmallNetArgs.stamps != 0
+__device__ unsigned long long g_sm_stamps[128];      // [0, 64): s_memrealtime, [64, 128): s_memtime (shader clock)
+__device__ __forceinline__ void sm_stamp(const SmallNetArgs& p, int i) {
+    if (p.stamps && blockIdx.x == 0 && threadIdx.x == 0 && i < 64) {
+        g_sm_stamps[i] = __builtin_amdgcn_s_memrealtime();
+        g_sm_stamps[64 + i] = __builtin_amdgcn_s_memtime();
+    }
+}
+
+}  // namespace
+
+extern "C" int az_diag_smallnet_stamps(unsigned long long* out, int n) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sm_stamps), sizeof(unsigned long long) * (n < 128 ? n : 128)) == hipSuccess ? 0 : -1;
+}
+
+// DV: timing-only variants (build with -DAZ_SM_DIAG, AZ_SM_STAMPS=<DV+1>): 1 = no per-tap barriers
+// (waits only), 2 = no MFMAs, 3 = neither, 4 = no fragment reads after a layer's first steps
+// (MFMAs on stale registers), 8 = no weight DMA in the layers.  Their outputs are wrong.
+template <int HB, int DV = 0>
+__global__ __launch_bounds__(256, 1) void k_smallnet(SmallNetArgs p) {
+    typedef SmGeom<HB> GM;
+    constexpr int WG = GM::WG, HW = GM::HW, NFRAG = GM::NFRAG, FPW = GM::FPW, NSLOT = GM::NSLOT, DIST = GM::DIST;
+    __shared__ __attribute__((aligned(16))) uint8_t lds[GM::LDS];
+    uint8_t* imgX = lds;
+    uint8_t* imgY = lds + GM::IMG;
+    uint8_t* wbuf = lds + 2 * GM::IMG;
+    float* bsm = reinterpret_cast<float*>(wbuf + NSLOT * GM::WT);   // [L][64] biases
+
+    const int b = blockIdx.x;
+    if (p.m_limit && b >= *p.m_limit) return;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int L = 2 * p.blocks + 1;
+    const int S = 9 * L;                                 // weight tiles streamed: (layer, tap)
+    sm_stamp(p, 0);
+
+    // weight tile s -> ring slot s % NSLOT: 512 pieces of 16 B, two per thread; LDS position (row n,
+    // physical chunk pc) holds logical chunk pc ^ (n & 7) (the swizzle applied at the source).
+    // Past the last tile the last tile is reloaded into the free slot, so every tap issues the
+    // same two loads and the vmcnt budget is a constant.
+    auto issue_w = [&](int s) {
+        uint8_t* dst = wbuf + (s % NSLOT) * GM::WT;
+        const int sl = s < S ? s : S - 1;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int P = j * 256 + tid, n = P >> 3, pc = P & 7, k = pc ^ (n & 7);
+            const uint16_t* src = p.W + ((size_t)sl * SF + n) * SF + 8 * k;
+            __builtin_amdgcn_global_load_lds((const void*)src, (lds_void_t*)(dst + (j * 256 + wave * 64) * 16), 16, 0, 0);
+        }
+    };
+    for (int s = 0; s < DIST; ++s) issue_w(s);
+
+    // zero both halo images (borders and dead columns stay zero), the input planes into Y, biases
+    for (int i = tid; i < 2 * GM::IMG / 16; i += 256) *reinterpret_cast<uint4*>(imgX + i * 16) = uint4{0, 0, 0, 0};
+    for (int i = tid; i < L * SF; i += 256) bsm[i] = p.bias[i];
+    __syncthreads();
+    // the head 1x1 conv weights, transposed to [c][o], fetched now (written to LDS after the trunk)
+    constexpr int HWT = SF * SF / 256;                   // weights per thread (2 * HC == SF outputs)
+    float wpre[HWT];
+#pragma unroll
+    for (int k = 0; k < HWT; ++k) {
+        const int i = tid + 256 * k, o = i / SF, c = i - o * SF;
+        wpre[k] = o < p.HC ? p.Wpc[o * SF + c] : p.Wvc[(o - p.HC) * SF + c];
+    }
+    const float* x0 = p.x0 + (size_t)b * HW * 16;
+    for (int i = tid; i < HW * 2; i += 256) {              // (pixel, 8-channel half) of the 16 input channels
+        const int px = i >> 1, h = i & 1;
+        const float4 u = *reinterpret_cast<const float4*>(x0 + px * 16 + 8 * h);
+        const float4 v = *reinterpret_cast<const float4*>(x0 + px * 16 + 8 * h + 4);
+        f16x8 o = {(_Float16)u.x, (_Float16)u.y, (_Float16)u.z, (_Float16)u.w,
+                   (_Float16)v.x, (_Float16)v.y, (_Float16)v.z, (_Float16)v.w};
+        const int y = px / HB, x = px - y * HB;
+        *reinterpret_cast<f16x8*>(imgY + img_off((y + 1) * WG + x + 1, h)) = o;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    sm_stamp(p, 1);
+
+    const int l16 = lane & 15, lg = lane >> 4;
+    f32x4v acc[FPW][4];
+    f32x4v xr[FPW][4];                                   // the lane's residual-stream values (fp32), kept in registers
+    f16x8 fa[2][4], fb[2][FPW];                          // operand fragments, double-buffered across steps
+
+    // one (tap, 32-channel chunk) step: fragments into buffer `r` / MFMAs from buffer `r`
+    auto load = [&](int r, const uint8_t* src, int s, auto tc, auto kc) {
+        constexpr int t = decltype(tc)::value, kk = decltype(kc)::value;
+        constexpr int sh = (t / 3) * WG + (t % 3);
+        const uint8_t* wt = wbuf + (s % NSLOT) * GM::WT;
+        static_for<0, 4>([&](auto jc) {
+            constexpr int j = decltype(jc)::value;
+            fa[r][j] = *reinterpret_cast<const f16x8*>(wt + img_off(16 * j + l16, 4 * kk + lg));
+        });
+        static_for<0, FPW>([&](auto ic) {
+            constexpr int i = decltype(ic)::value;
+            const int f = wave + 4 * i;
+            if (NFRAG % 4 == 0 || f < NFRAG)
+                fb[r][i] = *reinterpret_cast<const f16x8*>(src + img_off(16 * f + l16 + sh, 4 * kk + lg));
+        });
+    };
+    auto mma = [&](int r) {
+        static_for<0, FPW>([&](auto ic) {
+            constexpr int i = decltype(ic)::value;
+            if (NFRAG % 4 == 0 || wave + 4 * i < NFRAG)
+                static_for<0, 4>([&](auto jc) {
+                    constexpr int j = decltype(jc)::value;
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[r][j], fb[r][i], acc[i][j], 0, 0, 0);
+                });
+        });
+    };
+    // epilogue: lane holds channels 16j + 4lg + e of output grid row q
+    auto epilogue = [&](int layer, uint8_t* dst) {
+        const bool odd = layer & 1;
+        static_for<0, FPW>([&](auto ic) {
+            constexpr int i = decltype(ic)::value;
+            const int f = wave + 4 * i;
+            const int q = 16 * f + l16, y = q / WG, x = q - y * WG;
+            const bool live = f < NFRAG && y < HB && x < HB;
+            const int row = (y + 1) * WG + x + 1;
+            static_for<0, 4>([&](auto jc) {
+                constexpr int j = decltype(jc)::value;
+                const int c0 = 16 * j + 4 * lg;
+                f32x4v v = acc[i][j];
+                if (layer > 0 && !odd && p.residual) v += xr[i][j];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.0f);
+                if (!odd) xr[i][j] = v;
+                typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+                const f16x4 h = {(_Float16)v[0], (_Float16)v[1], (_Float16)v[2], (_Float16)v[3]};
+                if (live) *reinterpret_cast<f16x4*>(dst + img_off(row, c0 >> 3) + (c0 & 7) * 2) = h;
+            });
+        });
+    };
+    // One layer: 9 taps x NCH chunks.  The weight tile of tap s+1 is certified (landed + barrier)
+    // before tap s starts, so the last step of a tap prefetches the next tap's fragments.
+    auto run_layer = [&](int layer, auto nchc) {
+        constexpr int NCH = decltype(nchc)::value;
+        const bool odd = layer & 1;
+        const uint8_t* src = odd ? imgX : imgY;
+        uint8_t* dst = odd ? imgY : imgX;
+        static_for<0, 4>([&](auto jc) {
+            constexpr int j = decltype(jc)::value;
+            const f32x4v bv = *reinterpret_cast<const f32x4v*>(bsm + layer * SF + 16 * j + 4 * lg);
+            static_for<0, FPW>([&](auto ic) { acc[decltype(ic)::value][j] = bv; });
+        });
+        const int s0 = layer * 9;
+        load(0, src, s0, std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{});
+        static_for<0, 9 * NCH>([&](auto qc) {
+            constexpr int q = decltype(qc)::value, t = q / NCH, kk = q % NCH, r = q & 1;
+            if constexpr (kk == 0 && !(DV & 8)) issue_w(s0 + t + DIST);   // its slot was last read at tap s - 2
+            if constexpr (q + 1 < 9 * NCH && !((DV & 4) && q > 1))
+                load(r ^ 1, src, s0 + (q + 1) / NCH, std::integral_constant<int, (q + 1) / NCH>{},
+                     std::integral_constant<int, (q + 1) % NCH>{});
+            // pin the order: the next step's reads are in flight while this step's MFMAs issue (the
+            // scheduler would otherwise pull each read next to its first use behind an lgkmcnt(0))
+            __builtin_amdgcn_sched_barrier(0);
+            if constexpr (!(DV & 2)) mma(r);
+            __builtin_amdgcn_sched_barrier(0);
+            if constexpr (kk == NCH - 1) {
+                // tile s+2 landed (s+3..s+DIST stay in flight: no __syncthreads, whose vmcnt(0) would
+                // drain them); the epilogue's image writes are complete before the barrier
+                if constexpr (t == 8) {
+                    epilogue(layer, dst);
+                    asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+                } else if constexpr (DV & 1) {
+                    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+                } else {
+                    asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
+                }
+            }
+        });
+    };
+    run_layer(0, std::integral_constant<int, 1>{});
+    sm_stamp(p, 2);
+    for (int layer = 1; layer < L; ++layer) {
+        run_layer(layer, std::integral_constant<int, 2>{});
+        sm_stamp(p, 2 + layer);
+    }
+    __syncthreads();                                     // every wave's reload DMAs into the ring landed
+
+    // the fp32 stream to LDS (over the two images), adaptive average pool to P x P cells (torch
+    // adaptive_avg_pool2d bins), then the policy / value 1x1 convs (BN folded, k-ordered fp32 FMA
+    // chain + bias, ReLU); the 1x1 weights are staged transposed ([c][o]) in the ring
+    uint8_t* xs = lds;
+    static_for<0, FPW>([&](auto ic) {
+        constexpr int i = decltype(ic)::value;
+        const int f = wave + 4 * i;
+        const int q = 16 * f + l16, y = q / WG, x = q - y * WG;
+        if (f < NFRAG && y < HB && x < HB)
+            static_for<0, 4>([&](auto jc) {
+                constexpr int j = decltype(jc)::value;
+                *reinterpret_cast<f32x4v*>(xs + xs_off(y * HB + x, (16 * j + 4 * lg) >> 2)) = xr[i][j];
+            });
+    });
+    const int P = p.P, PP = P * P, HC = p.HC;
+    constexpr int HO = SF;                               // 2 * HC head outputs
+    float* pooled = reinterpret_cast<float*>(wbuf);      // [64 c][64 cells] (cells >= PP zero)
+    float* wt = pooled + SF * 64;                        // [64 c][HO o] (policy outputs, then value)
+#pragma unroll
+    for (int k = 0; k < HWT; ++k) {
+        const int i = tid + 256 * k, o = i / SF, c = i - o * SF;
+        wt[c * HO + o] = wpre[k];
+    }
+    for (int i = tid; i < SF * 64; i += 256) pooled[i] = 0.0f;
+    __syncthreads();
+    sm_stamp(p, 40);
+    for (int i = tid; i < PP * (SF / 4); i += 256) {
+        const int cell = i / (SF / 4), c4 = i - cell * (SF / 4), oy = cell / P, ox = cell - oy * P;
+        const int y0 = (oy * HB) / P, y1 = ((oy + 1) * HB + P - 1) / P;
+        const int xa = (ox * HB) / P, xb = ((ox + 1) * HB + P - 1) / P;
+        f32x4v sum = {0.0f, 0.0f, 0.0f, 0.0f};
+        for (int y = y0; y < y1; ++y)
+            for (int x = xa; x < xb; ++x) sum += *reinterpret_cast<const f32x4v*>(xs + xs_off(y * HB + x, c4));
+        const float cnt = (float)((y1 - y0) * (xb - xa));
+#pragma unroll
+        for (int e = 0; e < 4; ++e) pooled[(4 * c4 + e) * 64 + cell] = sum[e] / cnt;
+    }
+    __syncthreads();
+    sm_stamp(p, 41);
+    // head 1x1 convs on the f32 MFMA (v_mfma_f32_16x16x4_f32: an exact k-ordered fmaf chain, as
+    // gemm_f32): D[o][cell] = sum_c W[o][c] pooled[cell][c]; wave w owns cells 16w..16w+15
+    {
+        const int cell = 16 * wave + l16;
+        f32x4v hacc[4] = {};
+        for (int kb = 0; kb < SF / 4; ++kb) {
+            const int c = 4 * kb + lg;
+            const float bv = pooled[c * 64 + cell];
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                hacc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(wt[c * HO + 16 * j + l16], bv, hacc[j], 0, 0, 0);
+        }
+        if (cell < PP) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int o = 16 * j + 4 * lg;              // 4 consecutive outputs, all policy or all value
+                const bool pol = o < HC;
+                const int oc = pol ? o : o - HC;
+                const float* bias = (pol ? p.bpc : p.bvc) + oc;
+                f32x4v v;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const float t = hacc[j][e] + bias[e];
+                    v[e] = t > 0.0f ? t : 0.0f;
+                }
+                *reinterpret_cast<f32x4v*>((pol ? p.pp : p.vp) + ((size_t)b * PP + cell) * HC + oc) = v;
+            }
+        }
+    }
+    sm_stamp(p, 42);
+}
+
+bool az_smallnet_supported(int H, int C, int cin_pad, int pool, int head_channels) {
+    return H == 15 && C == SF && cin_pad == 16 && pool >= 1 && pool <= 8 && 2 * head_channels == SF && head_channels % 4 == 0;
+}
+// layers (2 * blocks + 1) whose biases fit the kernel's LDS
+int az_smallnet_max_blocks() { return (SmGeom<15>::MAXL - 1) / 2; }
+
+int az_smallnet_launch(const SmallNetArgs& a, int B, hipStream_t st) {
+    if (!az_smallnet_supported(a.H, SF, 16, a.P, a.HC)) return -1;
+#ifdef AZ_SM_DIAG
+    switch (a.stamps) {
+        case 2: hipLaunchKernelGGL((k_smallnet<15, 1>), dim3(B), dim3(256), 0, st, a); return 0;
+        case 3: hipLaunchKernelGGL((k_smallnet<15, 2>), dim3(B), dim3(256), 0, st, a); return 0;
+        case 4: hipLaunchKernelGGL((k_smallnet<15, 3>), dim3(B), dim3(256), 0, st, a); return 0;
+        case 5: hipLaunchKernelGGL((k_smallnet<15, 4>), dim3(B), dim3(256), 0, st, a); return 0;
+        case 6: hipLaunchKernelGGL((k_smallnet<15, 5>), dim3(B), dim3(256), 0, st, a); return 0;
+        case 7: hipLaunchKernelGGL((k_smallnet<15, 12>), dim3(B), dim3(256), 0, st, a); return 0;
+        case 8: hipLaunchKernelGGL((k_smallnet<15, 8>), dim3(B), dim3(256), 0, st, a); return 0;
+        default: break;
+    }
+#endif
+    hipLaunchKernelGGL(k_smallnet<15>, dim3(B), dim3(256), 0, st, a);
+    return 0;
+}

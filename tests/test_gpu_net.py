@@ -86,7 +86,7 @@ def test_gpu_net_bf16_sanity(engine):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("prec", [0, 1])
+@pytest.mark.parametrize("prec", [0, 1, 3])
 def test_gpu_net_batch_position_independent(engine, prec):
     """A sample's output does not depend on its position or batch-mates (bitwise)."""
     import az_amd
@@ -261,7 +261,8 @@ def test_gpu_c5_net_full_batch(engine):
     # (board, in_planes, channels, blocks, actions, precision, max_batch) -> trunk kernel prefix
     ((15, 11, 256, 20, 225, "fp16", 2048), "conv3x3_v7<2, 15, SLIM>"),   # C3 at N = 1, 2
     ((15, 11, 256, 20, 225, "fp16", 256), "conv3x3_v6<2, 15>"),          # C3 shard at N = 8
-    ((15, 11, 64, 6, 225, "fp16", 256), "conv3x3_v4<2, 64>"),            # C2
+    ((15, 11, 64, 6, 225, "fp16", 256), "k_smallnet<15>"),               # C2: the fused 64-filter forward
+    ((15, 11, 64, 6, 225, "bf16x3", 256), "conv3x3_v4<0, 64>"),
     ((15, 11, 256, 20, 225, "bf16x3", 64), "conv3x3_v4<0, 128>"),
     ((19, 8, 256, 20, 362, "fp16", 1024), "conv3x3_v6<2, 19, DENSE>"),   # C4
     ((15, 11, 32, 2, 225, "f32", 4), "gemm_f32"),

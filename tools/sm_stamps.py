@@ -1,0 +1,32 @@
+#!/usr/bin/env python3
+"""Phase stamps of k_smallnet's block 0 (AZ_SM_STAMPS=1): prologue, each layer, pool, head convs (us)."""
+import ctypes
+import os
+import sys
+
+import numpy as np
+
+os.environ.setdefault("AZ_SM_STAMPS", "1")
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "alphazero-multi-game_amd"))
+import az_amd  # noqa: E402
+from az_amd import _lib  # noqa: E402
+
+B, blocks = int(sys.argv[1]) if len(sys.argv) > 1 else 256, 6
+eng = az_amd.Engine(0)
+net = az_amd.HipNeuralNetwork(eng, az_amd.NetDesc(15, 11, 64, blocks, 225, 32, 8, 256, 1, 0, az_amd.AZ_PREC_FP16, B))
+net.init_random(1)
+x = (np.random.default_rng(0).random((B, 11, 15, 15)) < 0.2).astype(np.float32)
+for _ in range(5):
+    net.forward(x)
+buf = (ctypes.c_ulonglong * 128)()
+_lib.lib().az_diag_smallnet_stamps(buf, 128)
+st = list(buf)
+t0 = st[0]
+names = {1: "prologue"} | {2 + i: f"layer {i}" for i in range(2 * blocks + 1)} | {40: "stream->LDS, wt", 41: "pool", 42: "head convs"}
+prev, prevk = t0, 0
+for i in sorted(names):
+    dt = (st[i] - prev) / 100.0
+    cyc = st[64 + i] - st[64 + prevk]
+    print(f"{names[i]:16s} {dt:8.2f} us {cyc:8d} cyc {cyc / max(dt, 1e-9) / 1e3:5.2f} GHz  (t = {(st[i] - t0) / 100.0:8.2f})")
+    prev, prevk = st[i], i
