@@ -461,12 +461,24 @@ int net_heads_fc(az_net* n, int B, const int* nb, float* logits, float* value, h
     const az_net_desc& d = n->d;
     const int PP = n->P2;
     const int HK = d.head_channels * PP;
-    // FC layers: few rows, long K -> split-K partials (deterministic reductions).  The policy FC
-    // reduces into the logits; the value head's FC1 partials are reduced, ReLU'd and dotted with FC2
-    // by one kernel per board (k_value_head: FC1 + FC2 + tanh)
+    // Both FC heads: k_fc_heads (split-K partials of both FCs in one GEMM) + k_fc_finish (per board)
+    if (HK % 32 == 0 && HK % 4 == 0) {
+        FcHeadArgs fa{};
+        fa.pp = n->pp; fa.vp = n->vp;
+        fa.Wp = n->pfc.W; fa.bp = n->pfc.b; fa.Wv1 = n->vfc1.W; fa.bv1 = n->vfc1.b; fa.wv2 = n->vfc2.W; fa.bv2 = n->vfc2.b;
+        fa.logits = logits; fa.hid = n->v1; fa.value = value;
+        fa.part = n->ws; fa.m_limit = nb;
+        fa.B = B; fa.K = HK; fa.A = d.action_size; fa.H = d.fc_hidden;
+        fa.S = az_fc_heads_splits(d.max_batch, HK, d.action_size, d.fc_hidden);   // from the capacity: batch-size independent
+        az_launch_fc_heads(fa, st);
+        HIPCHK(hipGetLastError());
+        return 0;
+    }
+    // generic shapes: split-K partials (deterministic reductions); the value head's FC1 partials
+    // are reduced, ReLU'd and dotted with FC2 by one kernel per board
     GemmArgs pf = gemm_args(n->pfc, n->pp, HK, logits, d.action_size, nullptr, B, 1, 1, nb, 1);
     GemmArgs v1 = gemm_args(n->vfc1, n->vp, HK, n->v1, d.fc_hidden, nullptr, B, 1, 1, nb, 1);
-    const int splits = fc_splits(B, HK);
+    const int splits = fc_splits(d.max_batch, HK);
     pf.part = n->ws; pf.splits = splits;
     v1.part = n->ws + (size_t)B * d.action_size * splits; v1.splits = splits;
     if (splits > 1) az_launch_gemm_f32(pf, ACT_NONE, false, st);
@@ -817,7 +829,10 @@ int az_net_create(az_engine* e, const az_net_desc* d, az_net** out) {
     A_(&n->pool, B * n->P2 * F);
     A_(&n->pp, B * n->P2 * d->head_channels); A_(&n->vp, B * n->P2 * d->head_channels);
     A_(&n->v1, B * d->fc_hidden);
-    A_(&n->ws, (size_t)B * (d->action_size + d->fc_hidden) * FC_MAX_SPLITS);
+    {   // split-K workspace: gemm_f32 partials, or k_fc_heads' [<= 16 slices][B padded to 64][64-column tiles]
+        const size_t nc = (size_t)((d->action_size + 63) / 64 + (d->fc_hidden + 63) / 64) * 64;
+        A_(&n->ws, std::max((size_t)B * (d->action_size + d->fc_hidden) * FC_MAX_SPLITS, 16 * ((size_t)B + 63) / 64 * 64 * nc));
+    }
     A_(&n->logits, B * d->action_size); A_(&n->value, B); A_(&n->soft, B * d->action_size);
     A_(&n->in_nchw, B * d->in_planes * n->HW);
     if (!r) r = dalloc(&n->d_nb, 1);

@@ -62,6 +62,20 @@ int az_smallnet_launch(const SmallNetArgs& a, int B, hipStream_t st);
 
 void az_launch_gemm_f32(const GemmArgs& p, int act, bool res, hipStream_t st);
 void az_launch_gemm_f32_partials(const GemmArgs& p, hipStream_t st);
+
+// k_fc_heads + k_fc_finish: policy FC + value FC1/FC2 (split-K partials, then one block per board)
+struct FcHeadArgs {
+    const float* pp; const float* vp;           // head feature maps [B][K] (K = HC * P * P)
+    const float* Wp; const float* bp;           // policy FC [A][K], [A]
+    const float* Wv1; const float* bv1;         // value FC1 [H][K], [H]
+    const float* wv2; const float* bv2;         // value FC2 [H], [1]
+    float* logits; float* hid; float* value;    // [B][A], [B][H], [B]
+    float* part;                                // split-K workspace [S][B64][NT * 64]
+    const int* m_limit;
+    int B, K, A, H, S;
+};
+int az_fc_heads_splits(int B, int K, int A, int H);
+void az_launch_fc_heads(const FcHeadArgs& a, hipStream_t st);
 void az_launch_value_head(const float* part, int splits, const float* b1, const float* w2, const float* b2, float* hid,
                           float* value, int B, int H, const int* m_limit, hipStream_t st);
 void az_launch_pool(const float* in, float* out, int B, int H, int W, int C, int P, const int* m_limit, hipStream_t st);

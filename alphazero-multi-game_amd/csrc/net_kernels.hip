@@ -284,6 +284,120 @@ static void launch_f32(const GemmArgs& p, hipStream_t st) {
     hipLaunchKernelGGL((gemm_f32<BN, ACT, RES>), dim3(nbm * nbn), dim3(256), 0, st, q);
 }
 
+// ---------------------------------------------------------------------------
+// Both FC heads in two launches: k_fc_heads computes the split-K partials of the policy FC
+// (K -> A logits) and the value FC1 (K -> H hidden) as one GEMM over 64-column tiles of
+// [policy | value] (f32 MFMA v_mfma_f32_16x16x4_f32: every partial a k-ordered fmaf chain, as
+// gemm_f32); k_fc_finish (one block per board) sums the slices in order and finishes both heads
+// (bias, ReLU, value FC2, tanh).  Deterministic and batch-position independent.
+typedef float f32x4n __attribute__((ext_vector_type(4)));
+
+__global__ __launch_bounds__(256) void k_fc_heads(FcHeadArgs p) {
+    constexpr int BK = 32;
+    __shared__ float As[BK][64 + 1];                   // [k][board]
+    __shared__ float Bs[BK][64 + 1];                   // [k][output]
+    const int NTP = (p.A + 63) / 64, NTV = (p.H + 63) / 64, NT = NTP + NTV;
+    const int mt = blockIdx.x / NT, nt = blockIdx.x - mt * NT, sl = blockIdx.y, S = gridDim.y;
+    const int mlim = p.m_limit ? min(p.B, *p.m_limit) : p.B;
+    const int m0 = mt * 64;
+    if (m0 >= mlim) return;                            // the whole row of tiles is idle (no counter touched)
+    const bool pol = nt < NTP;
+    const int n0 = pol ? nt * 64 : (nt - NTP) * 64;    // first output of the tile within its head
+    const int NO = pol ? p.A : p.H;
+    const float* X = pol ? p.pp : p.vp;                // [B][K]
+    const float* Wt = pol ? p.Wp : p.Wv1;              // [NO][K]
+    const int KS = p.K / S, k0 = sl * KS;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l16 = lane & 15, lg = lane >> 4;
+    // staging: thread -> (row r = tid / 4 (+ 64 * second half), float4 column c4 = tid % 4 (+4)) of a 64 x 32 chunk
+    f32x4n ra[2], rb[2];
+    auto fetch = [&](int kc) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int r = tid >> 2, c4 = (tid & 3) + 4 * h, k = kc + 4 * c4;
+            const int m = m0 + r, n = n0 + r;
+            ra[h] = m < mlim ? *reinterpret_cast<const f32x4n*>(X + (size_t)m * p.K + k) : f32x4n{0.f, 0.f, 0.f, 0.f};
+            rb[h] = n < NO ? *reinterpret_cast<const f32x4n*>(Wt + (size_t)n * p.K + k) : f32x4n{0.f, 0.f, 0.f, 0.f};
+        }
+    };
+    auto stash = [&]() {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int r = tid >> 2, c4 = (tid & 3) + 4 * h;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) { As[4 * c4 + e][r] = ra[h][e]; Bs[4 * c4 + e][r] = rb[h][e]; }
+        }
+    };
+    f32x4n acc[4] = {};
+    fetch(k0);
+    for (int kc = k0; kc < k0 + KS; kc += BK) {
+        __syncthreads();
+        stash();
+        __syncthreads();
+        if (kc + BK < k0 + KS) fetch(kc + BK);
+#pragma unroll
+        for (int kk = 0; kk < BK / 4; ++kk) {
+            const float a = As[4 * kk + lg][16 * wave + l16];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, Bs[4 * kk + lg][16 * j + l16], acc[j], 0, 0, 0);
+        }
+    }
+    // partial tile: D[board 16 wave + 4 lg + e][output 16 j + l16]
+    const int NC = NT * 64, BP = (p.B + 63) / 64 * 64;
+    float* part = p.part + (size_t)sl * BP * NC;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) part[(size_t)(m0 + 16 * wave + 4 * lg + e) * NC + nt * 64 + 16 * j + l16] = acc[j][e];
+}
+
+// Finish both heads, one block per board: K slices summed in slice order (loads unrolled), biases,
+// the value hidden layer (ReLU) and value = tanh(hid . w2 + b2) with a fixed-order block reduction.
+__global__ __launch_bounds__(256) void k_fc_finish(FcHeadArgs p) {
+    const int b = blockIdx.x;
+    if (p.m_limit && b >= *p.m_limit) return;
+    const int NTP = (p.A + 63) / 64, NTV = (p.H + 63) / 64, NC = (NTP + NTV) * 64, BP = (p.B + 63) / 64 * 64, S = p.S;
+    const float* row = p.part + (size_t)b * NC;
+    const size_t sstride = (size_t)BP * NC;
+    auto sum = [&](int col) {
+        float v[16];
+#pragma unroll
+        for (int s = 0; s < 16; ++s) v[s] = s < S ? row[s * sstride + col] : 0.0f;
+        float t = 0.0f;
+#pragma unroll
+        for (int s = 0; s < 16; ++s) if (s < S) t += v[s];
+        return t;
+    };
+    for (int n = threadIdx.x; n < p.A; n += 256) p.logits[(size_t)b * p.A + n] = sum(n) + p.bp[n];
+    float d = 0.0f;
+    for (int h = threadIdx.x; h < p.H; h += 256) {
+        float v = sum(NTP * 64 + h) + p.bv1[h];
+        v = v > 0.0f ? v : 0.0f;
+        p.hid[(size_t)b * p.H + h] = v;
+        d = __builtin_fmaf(v, p.wv2[h], d);
+    }
+    __shared__ float red[256];
+    red[threadIdx.x] = d;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) p.value[b] = tanhf(red[0] + p.bv2[0]);
+}
+
+int az_fc_heads_splits(int B, int K, int A, int H) {
+    const int tiles = (B + 63) / 64 * ((A + 63) / 64 + (H + 63) / 64);
+    int s = 1;
+    while (s < 16 && tiles * s * 2 <= 1024 && K % (2 * s * 32) == 0 && K / (2 * s) >= 128) s *= 2;
+    return s;
+}
+
+void az_launch_fc_heads(const FcHeadArgs& a, hipStream_t st) {
+    const int NT = (a.A + 63) / 64 + (a.H + 63) / 64, MT = (a.B + 63) / 64;
+    hipLaunchKernelGGL(k_fc_heads, dim3(MT * NT, a.S), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(k_fc_finish, dim3(a.B), dim3(256), 0, st, a);
+}
+
 // split-K partial sums only (p.part, p.splits): the caller reduces them
 void az_launch_gemm_f32_partials(const GemmArgs& p, hipStream_t st) {
     const int nbm = (p.M + 127) / 128;
