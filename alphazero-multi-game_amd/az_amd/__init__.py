@@ -341,8 +341,9 @@ class ParallelMCTS:
         for i in range(n.value):
             r = mv[i]
             k = r.n_children
-            out.append((int(sl[i]), MoveData(int(r.action), [float(r.policy[j]) for j in range(k)], float(r.value),
-                                             int(r.thinking_time_ms), [int(r.child_actions[j]) for j in range(k)])))
+            # pointer slices copy the k entries in one C-level call (per-element indexing is ~8 ms/move at C2)
+            out.append((int(sl[i]), MoveData(int(r.action), r.policy[:k], float(r.value),
+                                             int(r.thinking_time_ms), r.child_actions[:k])))
         return out
 
     def close(self):

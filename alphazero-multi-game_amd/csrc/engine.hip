@@ -15,6 +15,7 @@
 #include <chrono>
 #include <random>
 #include <string>
+#include <thread>
 #include <unordered_set>
 #include <vector>
 
@@ -24,7 +25,7 @@
 #include "tree.h"
 
 // kernels (tree_kernels.hip)
-__global__ void k_select(TreeDev t, int mode);
+void az_launch_select(const TreeDev& t, int mode, hipStream_t st);
 __global__ void k_scan(TreeDev t);
 __global__ void k_expand_backup(TreeDev t, int mode);
 __global__ void k_select_action(TreeDev t, int training, float temperature, const float* temps, int* actions, float* values, float* probs,
@@ -119,8 +120,17 @@ struct az_net {
     std::vector<hipEvent_t> evpool;
     size_t evused = 0;
     long long prof_launches = 0, prof_forwards = 0;
+    long long prof_tick = 0, prof_sampled = 0;    // events on every prof_every()-th forward only
     std::mutex mu;
 };
+
+// Profiling events are recorded on one simulation step / forward in AZ_PROF_EVERY (default 16):
+// each hipEventRecord leaves a ~6 us gap on the queue, which at C2 (a ~140 us simulation step)
+// would otherwise inflate the timed loop by a fifth.  Reads scale the sampled times to all steps.
+static int prof_every() {
+    static const int p = getenv("AZ_PROF_EVERY") ? std::max(1, atoi(getenv("AZ_PROF_EVERY"))) : 16;
+    return p;
+}
 
 // ---------------------------------------------------------------- network
 namespace {
@@ -310,6 +320,11 @@ int net_forward(az_net* n, const float* x0, int B, const int* nb, float* logits,
         // one launch: input conv, trunk, pool and the two head 1x1 convs (smallnet.hip)
         hipEvent_t e0 = nullptr, e1 = nullptr;
         if (n->prof) {
+            n->prof_launches += 2 * d.blocks;    // counted in trunk-conv equivalents (bench.py's per-conv rate)
+            n->prof_forwards += 1;
+        }
+        if (n->prof && n->prof_tick++ % prof_every() == 0) {
+            n->prof_sampled += 1;
             while (n->evpool.size() < n->evused + 2) {
                 hipEvent_t ev;
                 HIPCHK(hipEventCreate(&ev));
@@ -317,8 +332,6 @@ int net_forward(az_net* n, const float* x0, int B, const int* nb, float* logits,
             }
             e0 = n->evpool[n->evused]; e1 = n->evpool[n->evused + 1];
             n->evused += 2;
-            n->prof_launches += 2 * d.blocks;    // counted in trunk-conv equivalents (bench.py's per-conv rate)
-            n->prof_forwards += 1;
             HIPCHK(hipEventRecord(e0, st));
         }
         SmallNetArgs sa{};
@@ -356,6 +369,11 @@ int net_forward(az_net* n, const float* x0, int B, const int* nb, float* logits,
     float* other = n->h1;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     if (n->prof && d.blocks > 0) {
+        n->prof_launches += 2 * d.blocks;
+        n->prof_forwards += 1;
+    }
+    if (n->prof && d.blocks > 0 && n->prof_tick++ % prof_every() == 0) {
+        n->prof_sampled += 1;
         while (n->evpool.size() < n->evused + 2) {
             hipEvent_t ev;
             HIPCHK(hipEventCreate(&ev));
@@ -364,8 +382,6 @@ int net_forward(az_net* n, const float* x0, int B, const int* nb, float* logits,
         ev0 = n->evpool[n->evused]; ev1 = n->evpool[n->evused + 1];
         n->evused += 2;
         HIPCHK(hipEventRecord(ev0, st));
-        n->prof_launches += 2 * d.blocks;
-        n->prof_forwards += 1;
     }
     if (!bf) {
         for (int i = 0; i < d.blocks; ++i) {
@@ -518,7 +534,7 @@ struct az_search {
     bool prof = false;
     std::vector<hipEvent_t> evpool;
     size_t evused = 0;
-    int64_t prof_steps = 0;
+    int64_t prof_steps = 0, prof_sampled = 0;
     std::vector<long long> prof_cnt0;
     std::vector<std::mt19937> rng;
     std::vector<float> h_noise; std::vector<uint8_t> h_mask;
@@ -600,9 +616,9 @@ int search_step(az_search* s, int mode) {
     hipStream_t st = s->e->stream;
     const int G = s->c.n_games;
     s->t.nd = s->arena[s->cur];
-    const bool prof = s->prof && mode == MODE_SIM;
+    const bool prof = s->prof && mode == MODE_SIM && s->prof_steps++ % prof_every() == 0;
     if (prof) HIPCHK(hipEventRecord(prof_event(s), st));
-    hipLaunchKernelGGL(k_select, dim3(G), dim3(64), 0, st, s->t, mode);
+    az_launch_select(s->t, mode, st);
     if (prof) HIPCHK(hipEventRecord(prof_event(s), st));
     if (s->c.eval_kind == AZ_EVAL_CALLBACK) {
         if (int r = host_evaluate(s)) return r;
@@ -618,9 +634,20 @@ int search_step(az_search* s, int mode) {
     }
     if (prof) HIPCHK(hipEventRecord(prof_event(s), st));
     hipLaunchKernelGGL(k_expand_backup, dim3(G), dim3(64), 0, st, s->t, mode);
-    if (prof) { HIPCHK(hipEventRecord(prof_event(s), st)); s->prof_steps += 1; }
+    if (prof) { HIPCHK(hipEventRecord(prof_event(s), st)); s->prof_sampled += 1; }
     HIPCHK(hipGetLastError());
     return 0;
+}
+
+// Host worker threads for per-game host work: the CPU share (OMP_NUM_THREADS where set, as on the
+// GPU boxes, where hardware_concurrency reports the whole machine), at most 16.
+int host_threads() {
+    static const int n = [] {
+        int h = (int)std::thread::hardware_concurrency();
+        if (const char* e = getenv("OMP_NUM_THREADS")) if (atoi(e) > 0) h = std::min(h, atoi(e));
+        return std::max(1, std::min(16, h));
+    }();
+    return n;
 }
 
 int search_noise(az_search* s, float alpha, float eps, const uint8_t* mask) {
@@ -636,21 +663,34 @@ int search_noise(az_search* s, float alpha, float eps, const uint8_t* mask) {
     }
     // addDirichletNoise draws (parallel_mcts.cpp:1136-1156): libstdc++ gamma on the host,
     // one fresh gamma_distribution per call on the game's mt19937.
-    bool any = false;
-    for (int g = 0; g < G; ++g) {
-        s->h_mask[g] = 0;
-        if (!s->active[g] || (mask && !mask[g])) continue;
-        const int nc = !nroot.empty() ? nroot[g] : s->fresh[g] ? A : A - s->stones[g];
-        if (nc <= 0) continue;
-        float* nz = s->h_noise.data() + (size_t)g * NA;
-        std::gamma_distribution<float> gamma(alpha, 1.0f);
-        float sum = 0.0f;
-        for (int i = 0; i < nc; ++i) { nz[i] = std::max(1e-10f, gamma(s->rng[g])); sum += nz[i]; }
-        if (sum <= 0.0f) { sum = 1.0f; for (int i = 0; i < nc; ++i) nz[i] = 1.0f / (float)nc; }
-        for (int i = 0; i < nc; ++i) nz[i] /= sum;
-        s->h_mask[g] = 1;
-        any = true;
+    // Every game draws from its own mt19937, so the games split over host threads without changing
+    // a single draw (a C2 move's 128 x 225 draws take ~6 ms on one core).
+    auto draw = [&](int g0, int g1) {
+        for (int g = g0; g < g1; ++g) {
+            s->h_mask[g] = 0;
+            if (!s->active[g] || (mask && !mask[g])) continue;
+            const int nc = !nroot.empty() ? nroot[g] : s->fresh[g] ? A : A - s->stones[g];
+            if (nc <= 0) continue;
+            float* nz = s->h_noise.data() + (size_t)g * NA;
+            std::gamma_distribution<float> gamma(alpha, 1.0f);
+            float sum = 0.0f;
+            for (int i = 0; i < nc; ++i) { nz[i] = std::max(1e-10f, gamma(s->rng[g])); sum += nz[i]; }
+            if (sum <= 0.0f) { sum = 1.0f; for (int i = 0; i < nc; ++i) nz[i] = 1.0f / (float)nc; }
+            for (int i = 0; i < nc; ++i) nz[i] /= sum;
+            s->h_mask[g] = 1;
+        }
+    };
+    const int nt = std::max(1, std::min({host_threads(), G / 32}));
+    if (nt == 1) {
+        draw(0, G);
+    } else {
+        std::vector<std::thread> th;
+        for (int t = 1; t < nt; ++t) th.emplace_back(draw, (int)((long)G * t / nt), (int)((long)G * (t + 1) / nt));
+        draw(0, (int)((long)G / nt));
+        for (auto& x : th) x.join();
     }
+    bool any = false;
+    for (int g = 0; g < G && !any; ++g) any = s->h_mask[g] != 0;
     if (!any) return 0;
     hipStream_t st = s->e->stream;
     HIPCHK(hipMemcpyAsync(s->d_noise, s->h_noise.data(), (size_t)G * NA * 4, hipMemcpyHostToDevice, st));
@@ -979,7 +1019,7 @@ int az_net_profile(az_net* n, int enable) {
     if (!n) return az_fail(AZ_ERR_ARG, "null net");
     std::lock_guard<std::mutex> lk(n->mu);
     n->prof = enable != 0;
-    n->evused = 0; n->prof_launches = 0; n->prof_forwards = 0;
+    n->evused = 0; n->prof_launches = 0; n->prof_forwards = 0; n->prof_tick = 0; n->prof_sampled = 0;
     return 0;
 }
 
@@ -994,7 +1034,8 @@ int az_net_profile_read(az_net* n, double* trunk_ms, int64_t* trunk_launches, in
         HIPCHK(hipEventElapsedTime(&t, n->evpool[i], n->evpool[i + 1]));
         ms += t;
     }
-    if (trunk_ms) *trunk_ms = ms;
+    // the sampled forwards' trunk time scaled to every profiled forward
+    if (trunk_ms) *trunk_ms = n->prof_sampled ? ms * (double)n->prof_forwards / (double)n->prof_sampled : 0.0;
     if (trunk_launches) *trunk_launches = n->prof_launches;
     if (forwards) *forwards = n->prof_forwards;
     return 0;
@@ -1050,7 +1091,7 @@ int az_search_create(az_engine* e, az_net* net, const az_search_cfg* c, az_searc
     SA(t.rhash, G); SA(t.rfresh, G); SA(t.rnode, G); SA(t.active, G); SA(t.gresult, G);
     uint64_t* zko = nullptr;
     if (go) { SA(t.rko, G); SA(t.rpass, G); SA(t.rposh, (size_t)G * t.hmax); SA(t.rnposh, G); SA(zko, A + 1); }
-    SA(t.path, (size_t)G * AZ_DMAX); SA(t.plen, G); SA(t.lstatus, G); SA(t.lvalue, G); SA(t.lhash, G); SA(t.ttstore, G);
+    SA(t.path, (size_t)G * AZ_DMAX); SA(t.pact, (size_t)G * AZ_DMAX); SA(t.plen, G); SA(t.lstatus, G); SA(t.lvalue, G); SA(t.lhash, G); SA(t.ttstore, G);
     SA(t.ttref, G); SA(t.tthslot, G); SA(t.need_eval, G); SA(t.eval_slot, G); SA(t.eval_games, G); SA(t.n_eval, 1);
     SA(t.planes, (size_t)G * A * 16);
     SA(t.tt_hash, (size_t)G * t.tt_slots); SA(t.tt_visits, (size_t)G * t.tt_slots); SA(t.tt_value, (size_t)G * t.tt_slots);
@@ -1121,7 +1162,7 @@ void az_search_destroy(az_search* s) {
     TreeDev& t = s->t;
     for (const void* p : {(const void*)t.atop, (const void*)t.rboard, (const void*)t.rhist, (const void*)t.rplayer,
                           (const void*)t.rstones, (const void*)t.rply, (const void*)t.rhash, (const void*)t.rfresh,
-                          (const void*)t.rnode, (const void*)t.active, (const void*)t.gresult, (const void*)t.path,
+                          (const void*)t.rnode, (const void*)t.active, (const void*)t.gresult, (const void*)t.path, (const void*)t.pact,
                           (const void*)t.plen, (const void*)t.lstatus, (const void*)t.lvalue, (const void*)t.lhash,
                           (const void*)t.ttstore, (const void*)t.ttref, (const void*)t.tthslot, (const void*)t.need_eval,
                           (const void*)t.eval_slot, (const void*)t.eval_games, (const void*)t.n_eval, (const void*)t.planes,
@@ -1574,7 +1615,7 @@ int az_search_profile(az_search* s, int enable) {
     HIPCHK(hipStreamSynchronize(s->e->stream));
     s->prof = enable != 0;
     s->evused = 0;
-    s->prof_steps = 0;
+    s->prof_steps = 0; s->prof_sampled = 0;
     s->prof_cnt0.assign((size_t)s->c.n_games * AZ_NCNT, 0);
     HIPCHK(hipMemcpy(s->prof_cnt0.data(), s->t.cnt, s->prof_cnt0.size() * 8, hipMemcpyDeviceToHost));
     return 0;
@@ -1603,8 +1644,10 @@ int az_search_profile_read(az_search* s, double* select_ms, double* expand_ms, i
         bs += c[o + CNT_BYTES_SEL] - (c0 ? c0[CNT_BYTES_SEL] : 0);
         be += c[o + CNT_BYTES_EXP] - (c0 ? c0[CNT_BYTES_EXP] : 0);
     }
-    if (select_ms) *select_ms = sel;
-    if (expand_ms) *expand_ms = exp;
+    // sampled steps' kernel times scaled to every simulation step
+    const double k = s->prof_sampled ? (double)s->prof_steps / (double)s->prof_sampled : 0.0;
+    if (select_ms) *select_ms = sel * k;
+    if (expand_ms) *expand_ms = exp * k;
     if (sim_steps) *sim_steps = s->prof_steps;
     if (select_bytes) *select_bytes = bs;
     if (expand_bytes) *expand_bytes = be;

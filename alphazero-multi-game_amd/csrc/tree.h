@@ -47,6 +47,7 @@ struct TreeDev {
     uint64_t zconst;             // "rules"[1] ^ "komi"[int(7.5*2) & 15] (Chinese rules, komi 7.5)
     int* gresult;                // [G] GameResult of the root state
     int* path; int* plen;        // [G][AZ_DMAX], [G]
+    int* pact;                   // [G][AZ_DMAX] action of every path node (pact[0] unused)
     int* lstatus; float* lvalue; uint64_t* lhash; int* ttstore; uint64_t* ttref; int* tthslot;
     int* need_eval; int* eval_slot; int* eval_games; int* n_eval;
     float* planes;               // [G][A][16] NHWC, channels 11..15 zero (NET)

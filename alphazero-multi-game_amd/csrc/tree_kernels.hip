@@ -155,33 +155,36 @@ __device__ __forceinline__ GamePtrs game_nodes(const Nodes& nd, size_t base) {
 }
 
 // Leaf state = root state + path moves.  Fills the LDS board, returns side to move,
-// stone count, Zobrist hash and the last six moves (most recent first).
-__device__ void build_leaf(const TreeDev& t, int g, int lane, const GamePtrs& nd, const int* spath, int depth,
+// stone count, Zobrist hash and the last six moves (most recent first).  sact[i] is the action
+// of path node i (1..depth).  Path cells are distinct, so the moves go down lane-parallel; the
+// hash is the XOR of the root hash and the moves' piece keys (XOR order does not matter).
+__device__ __forceinline__ uint64_t wave_xor64(uint64_t v) {
+    for (int o = 32; o > 0; o >>= 1) v ^= __shfl_xor(v, o);
+    return v;
+}
+
+__device__ void build_leaf(const TreeDev& t, int g, int lane, const int* sact, int depth,
                            uint8_t* board, int* hist6, int& player, int& stones, uint64_t& hash) {
     const int A = t.A;
+    const int p0 = t.rplayer[g];
+    static_assert(AZ_DMAX <= 128, "two path cells per lane");
+    const int i0 = 1 + lane, i1 = 65 + lane;          // path nodes of this lane (odd i: p0 moved)
+    const int m0 = i0 <= depth ? sact[i0] : -1, m1 = i1 <= depth ? sact[i1] : -1;
+    uint64_t x = 0;                                   // piece keys first: their loads overlap the root board's
+    if (m0 >= 0) x ^= t.zpiece[(size_t)((i0 & 1) ? p0 - 1 : 2 - p0) * A + m0];
+    if (m1 >= 0) x ^= t.zpiece[(size_t)((i1 & 1) ? p0 - 1 : 2 - p0) * A + m1];
     const uint8_t* rb = t.rboard + (size_t)g * A;
     for (int a = lane; a < A; a += 64) board[a] = rb[a];
     __syncthreads();
-    int p = t.rplayer[g];
-    uint64_t h = t.rhash[g];
-    const int p0 = p;
-    if (lane == 0) {
-        for (int i = 1; i <= depth; ++i) {
-            int a = nd.act[spath[i]];
-            board[a] = (uint8_t)p;
-            h ^= t.zpiece[(size_t)(p - 1) * A + a];
-            p = 3 - p;
-        }
-    }
+    if (m0 >= 0) board[m0] = (uint8_t)((i0 & 1) ? p0 : 3 - p0);
+    if (m1 >= 0) board[m1] = (uint8_t)((i1 & 1) ? p0 : 3 - p0);
     __syncthreads();
-    p = __shfl(p, 0);
-    h = __shfl(h, 0);
-    h ^= t.zplayer[p0 - 1] ^ t.zplayer[p - 1];
+    const int p = (depth & 1) ? 3 - p0 : p0;
     player = p;
     stones = t.rstones[g] + depth;
-    hash = h;
+    hash = t.rhash[g] ^ wave_xor64(x) ^ t.zplayer[p0 - 1] ^ t.zplayer[p - 1];
     for (int i = 0; i < 6; ++i) {
-        if (i < depth) hist6[i] = nd.act[spath[depth - i]];
+        if (i < depth) hist6[i] = sact[depth - i];
         else hist6[i] = t.rhist[g * 6 + (i - depth)];
     }
 }
@@ -370,7 +373,7 @@ __device__ int go_result_seq(const TreeDev& t, const uint8_t* b, GoLds& L) {
 
 // Leaf state of a Go game = root state + path moves (lane 0), with the position hashes the path
 // pushes (for positional superko at expansion).
-__device__ void go_build_leaf(const TreeDev& t, int g, int lane, const GamePtrs& nd, const int* spath, int depth,
+__device__ void go_build_leaf(const TreeDev& t, int g, int lane, const int* sact, int depth,
                               uint8_t* board, GoLds& L, int* hist6, int& player, int& ko, int& passes, uint64_t& bh,
                               uint64_t& hash) {
     const int A = t.A;
@@ -382,7 +385,7 @@ __device__ void go_build_leaf(const TreeDev& t, int g, int lane, const GamePtrs&
         uint64_t h = t.rhash[g];
         int nph = 0;
         for (int i = 1; i <= depth; ++i) {
-            const int a = nd.act[spath[i]];
+            const int a = sact[i];
             if (go_play_seq(t, board, L, a, p, k, ps, h)) L.phist[nph++] = go_hash(t, h, p, k);
             p = 3 - p;
         }
@@ -395,7 +398,7 @@ __device__ void go_build_leaf(const TreeDev& t, int g, int lane, const GamePtrs&
     __syncthreads();
     hash = go_hash(t, bh, player, ko);
     for (int i = 0; i < 6; ++i) {
-        if (i < depth) hist6[i] = nd.act[spath[depth - i]];
+        if (i < depth) hist6[i] = sact[depth - i];
         else hist6[i] = t.rhist[g * 6 + (i - depth)];
     }
 }
@@ -474,11 +477,17 @@ __device__ int go_legal(const TreeDev& t, int g, int lane, const uint8_t* b, con
 
 // ---------------------------------------------------------------------------
 // K1: selection + virtual loss + leaf classification (+ planes for the network).
+// K1.  IT = child records per lane per level (IT * 64 >= the action space).  Every level of the
+// descent is ONE dependent round trip to memory: each lane loads all IT of its child records in
+// full (N, W, VL, P and the child's own header first / cnt / flag / act) before the PUCT scores,
+// and the winner's record is broadcast from its lane, so the next level needs no header load.
+template <int IT>
 __global__ __launch_bounds__(64) void k_select(TreeDev t, int mode) {
     const int g = blockIdx.x;
     const int lane = threadIdx.x;
     __shared__ uint8_t board[AZ_MAXA];
     __shared__ int spath[AZ_DMAX];
+    __shared__ int sact[AZ_DMAX];
     __shared__ GoLds gl;
     const bool go = t.game == GAME_GO;
     if (g >= t.G) return;
@@ -494,12 +503,12 @@ __global__ __launch_bounds__(64) void k_select(TreeDev t, int mode) {
     int node = root;
     int status = ST_NONE;
     float value = 0.0f;
-    long long scanned = 0;       // child records read by the PUCT scans (16 B each: N, W, VL, P)
+    long long scanned = 0;       // child records read by the PUCT scans (25 B each)
+    uint8_t nflag = nd.flag[root];   // flag of the current node (the leaf's after the descent)
 
     if (mode != MODE_SIM) {
         // Root expansion: expandNode (noise) / search() root branch.
-        uint8_t f = nd.flag[root];
-        if ((f & (FL_EXPANDED | FL_TERMINAL)) || t.gresult[g] != R_ONGOING) {
+        if ((nflag & (FL_EXPANDED | FL_TERMINAL)) || t.gresult[g] != R_ONGOING) {
             if (lane == 0) { t.lstatus[g] = ST_NONE; t.need_eval[g] = 0; }
             return;
         }
@@ -508,24 +517,38 @@ __global__ __launch_bounds__(64) void k_select(TreeDev t, int mode) {
         // selectLeafWithPath: VL on the root, then PUCT descent.
         int rN = nd.N[root], rVL = nd.VL[root];
         float rW = nd.W[root];
+        int fc = nd.first[root], nc = nd.cnt[root];
         rN += t.vl; rVL += t.vl; rW = rW - (float)t.vl;           // addVirtualLoss (root, first)
         if (lane == 0) spath[0] = root;
+        int pN = rN, pVL = rVL;
+        float pW = rW;
         while (true) {
-            uint8_t f = nd.flag[node];
-            if (!(f & FL_EXPANDED) || (f & FL_TERMINAL) || depth >= 1000) break;
-            int pN, pVL; float pW;
-            if (node == root) { pN = rN; pVL = rVL; pW = rW; }
-            else { pN = nd.N[node]; pVL = nd.VL[node]; pW = nd.W[node]; }
-            const int fc = nd.first[node], nc = nd.cnt[node];
+            if (!(nflag & FL_EXPANDED) || (nflag & FL_TERMINAL) || depth >= 1000 || nc <= 0) break;
             scanned += nc;
             const float sq = sqrtf((float)pN);
-            float best = -FLT_MAX;
-            int bi = INT_MAX;
-            for (int i = lane; i < nc; i += 64) {
-                const int c = fc + i;
-                float s = puct_score(nd.N[c], nd.W[c], nd.VL[c], nd.P[c], depth, pN, pVL, pW, t.cpuct, t.fpu, sq);
-                if (s > best) { best = s; bi = i; }
+            int cN[IT], cVL[IT], cF[IT], cC[IT], cA[IT], cFl[IT];
+            float cW[IT], cP[IT];
+#pragma unroll
+            for (int k = 0; k < IT; ++k) {                 // all loads of the level before any use
+                const int c = fc + min(lane + 64 * k, nc - 1);
+                cN[k] = nd.N[c]; cW[k] = nd.W[c]; cVL[k] = nd.VL[c]; cP[k] = nd.P[c];
+                cF[k] = nd.first[c]; cC[k] = nd.cnt[c]; cA[k] = nd.act[c]; cFl[k] = nd.flag[c];
             }
+            float best = -FLT_MAX;
+            int bi = INT_MAX, bk = 0;
+#pragma unroll
+            for (int k = 0; k < IT; ++k) {
+                const int i = lane + 64 * k;
+                if (i < nc) {
+                    float s = puct_score(cN[k], cW[k], cVL[k], cP[k], depth, pN, pVL, pW, t.cpuct, t.fpu, sq);
+                    if (s > best) { best = s; bi = i; bk = k; }
+                }
+            }
+            int bN = cN[0], bVL = cVL[0], bF = cF[0], bC = cC[0], bA = cA[0], bFl = cFl[0];
+            float bW = cW[0];
+#pragma unroll
+            for (int k = 1; k < IT; ++k)
+                if (bk == k) { bN = cN[k]; bVL = cVL[k]; bF = cF[k]; bC = cC[k]; bA = cA[k]; bFl = cFl[k]; bW = cW[k]; }
             for (int o = 32; o > 0; o >>= 1) {
                 float ob = __shfl_xor(best, o);
                 int oi = __shfl_xor(bi, o);
@@ -533,9 +556,14 @@ __global__ __launch_bounds__(64) void k_select(TreeDev t, int mode) {
             }
             if (bi == INT_MAX) break;
             if (depth + 1 >= AZ_DMAX) { if (lane == 0) atomicOr(t.err, ERR_PATH); break; }
+            const int src = bi & 63;
+            pN = __shfl(bN, src); pVL = __shfl(bVL, src); pW = __shfl(bW, src);
+            nflag = (uint8_t)__shfl(bFl, src);
+            const int act = __shfl(bA, src);
             node = fc + bi;
+            fc = __shfl(bF, src); nc = __shfl(bC, src);
             ++depth;
-            if (lane == 0) spath[depth] = node;
+            if (lane == 0) { spath[depth] = node; sact[depth] = act; }
         }
         // addVirtualLoss on every path node, root a second time (parallel_mcts.cpp:293-295)
         if (lane == 0) {
@@ -555,15 +583,15 @@ __global__ __launch_bounds__(64) void k_select(TreeDev t, int mode) {
     uint64_t hash;
     int gko = -1, gpass = 0;
     uint64_t gbh = 0;
-    if (go) go_build_leaf(t, g, lane, nd, spath, depth, board, gl, hist6, player, gko, gpass, gbh, hash);
-    else build_leaf(t, g, lane, nd, spath, depth, board, hist6, player, stones, hash);
+    if (go) go_build_leaf(t, g, lane, sact, depth, board, gl, hist6, player, gko, gpass, gbh, hash);
+    else build_leaf(t, g, lane, sact, depth, board, hist6, player, stones, hash);
     const int leaf = node;
     int store = 0;
     uint64_t ref = 0;
     int hslot = 0;
 
     if (mode == MODE_SIM) {
-        uint8_t f = nd.flag[leaf];
+        const uint8_t f = nflag;
         int result = R_ONGOING;
         if (f & FL_TERMINAL) {
             status = ST_TERMINAL;
@@ -579,7 +607,7 @@ __global__ __launch_bounds__(64) void k_select(TreeDev t, int mode) {
                     result = __shfl(r, 0);
                 }
             } else {
-                const int a = nd.act[leaf];
+                const int a = sact[depth];
                 if (five_at(board, t.bs, a, 3 - player)) result = (3 - player) == 1 ? R_WIN1 : R_WIN2;
                 else if (stones >= t.A) result = R_DRAW;
             }
@@ -608,7 +636,7 @@ __global__ __launch_bounds__(64) void k_select(TreeDev t, int mode) {
         // expandNode: no legal moves -> terminal (parallel_mcts.cpp:646-654); a Go state always
         // has the pass
         if (lane == 0) {
-            nd.flag[leaf] = (uint8_t)(nd.flag[leaf] | FL_TERMINAL | FL_EXPANDED | (R_DRAW << 2));
+            nd.flag[leaf] = (uint8_t)(nflag | FL_TERMINAL | FL_EXPANDED | (R_DRAW << 2));
             t.lstatus[g] = ST_NONE; t.need_eval[g] = 0;
         }
         return;
@@ -651,16 +679,26 @@ __global__ __launch_bounds__(64) void k_select(TreeDev t, int mode) {
         t.plen[g] = depth + 1;
         t.need_eval[g] = (status == ST_EVAL && (t.eval_kind == 0 || t.eval_kind == 4)) ? 1 : 0;
     }
-    for (int i = lane; i <= depth; i += 64) t.path[(size_t)g * AZ_DMAX + i] = spath[i];
+    for (int i = lane; i <= depth; i += 64) {
+        t.path[(size_t)g * AZ_DMAX + i] = spath[i];
+        t.pact[(size_t)g * AZ_DMAX + i] = i ? sact[i] : -1;
+    }
     if (lane == 0 && mode == MODE_SIM) {
-        // algorithmic bytes: child scans, node headers (first/cnt/flag/act 9 B) and VL read-modify-
-        // write (12 B + 12 B) along the path, root board, TT probe (12 B, +20 on a hit), planes
-        // (64 B per cell, fp32 NHWC16) when the leaf goes to the network, path record
-        long long b = scanned * 16 + (long long)(depth + 1) * (9 + 24 + 4) + t.A + 12;
+        // algorithmic bytes: child scans (whole 25 B records: N, W, VL, P + the child's header),
+        // root header (21 B), VL read-modify-write (12 B + 12 B) and piece key (8 B) per path
+        // node, root board, TT probe (12 B, +20 on a hit), planes (64 B per cell, fp32 NHWC16)
+        // when the leaf goes to the network, path record (8 B per node)
+        long long b = scanned * 25 + 21 + (long long)(depth + 1) * (24 + 8 + 8) + t.A + 12;
         if (status == ST_TTHIT) b += 20;
         if (status == ST_EVAL) b += 64LL * t.A;
         cnt[CNT_BYTES_SEL] += b;
     }
+}
+
+void az_launch_select(const TreeDev& t, int mode, hipStream_t st) {
+    if (t.NA <= 128) hipLaunchKernelGGL(k_select<2>, dim3(t.G), dim3(64), 0, st, t, mode);
+    else if (t.NA <= 256) hipLaunchKernelGGL(k_select<4>, dim3(t.G), dim3(64), 0, st, t, mode);
+    else hipLaunchKernelGGL(k_select<(AZ_MAXNA + 63) / 64>, dim3(t.G), dim3(64), 0, st, t, mode);
 }
 
 // Host evaluator: the moves from the root to every leaf of the evaluation batch (slot order).
@@ -669,8 +707,7 @@ __global__ void k_leaf_moves(TreeDev t, int* moves, int* len) {
     if (i >= *t.n_eval) return;
     const int g = t.eval_games[i];
     const int depth = t.plen[g] - 1;
-    const GamePtrs nd = game_nodes(t.nd, (size_t)g * t.ncap);
-    for (int j = threadIdx.x; j < depth; j += blockDim.x) moves[(size_t)i * AZ_DMAX + j] = nd.act[t.path[(size_t)g * AZ_DMAX + j + 1]];
+    for (int j = threadIdx.x; j < depth; j += blockDim.x) moves[(size_t)i * AZ_DMAX + j] = t.pact[(size_t)g * AZ_DMAX + j + 1];
     if (threadIdx.x == 0) len[i] = depth;
 }
 
@@ -707,6 +744,7 @@ __global__ __launch_bounds__(64) void k_expand_backup(TreeDev t, int mode) {
     const int lane = threadIdx.x;
     __shared__ uint8_t board[AZ_MAXA];
     __shared__ int spath[AZ_DMAX];
+    __shared__ int sact[AZ_DMAX];
     __shared__ float pol[AZ_MAXNA];
     __shared__ int legal[AZ_MAXNA];
     __shared__ float lp[AZ_MAXNA];
@@ -722,19 +760,22 @@ __global__ __launch_bounds__(64) void k_expand_backup(TreeDev t, int mode) {
     const int A = t.A;
     const int plen = t.plen[g];
     const int depth = plen - 1;
-    for (int i = lane; i < plen; i += 64) spath[i] = t.path[(size_t)g * AZ_DMAX + i];
+    for (int i = lane; i < plen; i += 64) {
+        spath[i] = t.path[(size_t)g * AZ_DMAX + i];
+        sact[i] = t.pact[(size_t)g * AZ_DMAX + i];
+    }
     __syncthreads();
     const int leaf = spath[depth];
     const int NA = t.NA;
     int hist6[6]; int player, stones = 0; uint64_t hash;
     int gko = -1, gpass = 0;
     uint64_t gbh = 0;
-    if (go) go_build_leaf(t, g, lane, nd, spath, depth, board, gl, hist6, player, gko, gpass, gbh, hash);
-    else build_leaf(t, g, lane, nd, spath, depth, board, hist6, player, stones, hash);
+    if (go) go_build_leaf(t, g, lane, sact, depth, board, gl, hist6, player, gko, gpass, gbh, hash);
+    else build_leaf(t, g, lane, sact, depth, board, hist6, player, stones, hash);
     float value = t.lvalue[g];
-    // algorithmic bytes: path (4 + 2 B per level), root board, then below: policy / TT / ring,
+    // algorithmic bytes: path (4 + 4 B per level), root board, then below: policy / TT / ring,
     // new child records (25 B), VL-removal + backup read-modify-write (24 B per path node)
-    long long kb = (long long)plen * 6 + A;
+    long long kb = (long long)plen * 8 + A;
 
     if (status == ST_EVAL || status == ST_TTHIT) {
         // legal moves in child order (gomoku_state.cpp:531-578)
@@ -895,20 +936,22 @@ __global__ __launch_bounds__(64) void k_expand_backup(TreeDev t, int mode) {
         value = nd.N[leaf] == 0 ? 0.0f : nd.W[leaf] / (float)nd.N[leaf];
     }   // ST_EXPVAL: the TT value k_select cached in lvalue
 
-    if (mode == MODE_SIM && lane == 0) {
-        // backpropagate(node, value, searchPath) (parallel_mcts.cpp:782-833)
-        float v = value;
-        for (int i = depth; i >= 0; --i) {
+    if (mode == MODE_SIM) {
+        // backpropagate(node, value, searchPath) (parallel_mcts.cpp:782-833): the reference walks the
+        // path leaf -> root negating v at every step, so node i gets (-1)^(depth-i) * value.  Path
+        // nodes are distinct and each gets its own unchanged sequence of fp32 operations, so the
+        // update runs one lane per node (bit-identical to the sequential walk).
+        for (int i = lane; i <= depth; i += 64) {
             const int nn = spath[i];
+            const float v = ((depth - i) & 1) ? -value : value;
             int N = nd.N[nn], VL = nd.VL[nn];
             float W = nd.W[nn];
             N -= t.vl; VL -= t.vl; W = W + (float)t.vl;   // removeVirtualLoss
             N += 1;
             W = W + v;
-            v = -v;
             nd.N[nn] = N; nd.VL[nn] = VL; nd.W[nn] = W;
         }
-        cnt[CNT_SIMS] += 1;
+        if (lane == 0) cnt[CNT_SIMS] += 1;
         kb += 24LL * plen;
     }
     if (lane == 0 && mode == MODE_SIM) cnt[CNT_BYTES_EXP] += kb;
