@@ -17,6 +17,7 @@
 #include <stdint.h>
 #include <type_traits>
 #include "net.h"
+#include "leaf_planes.h"
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float floatx4 __attribute__((ext_vector_type(4)));
@@ -1539,6 +1540,36 @@ void az_launch_to_g8(const float* in, uint16_t* hi, int8_t* q, int C, int HW, co
                      hipStream_t st) {
     if (mode == 2) hipLaunchKernelGGL(k_to_g8<2>, dim3(2048), dim3(256), 0, st, in, hi, q, C, HW, m_limit, maxB);
     else hipLaunchKernelGGL(k_to_g8<1>, dim3(2048), dim3(256), 0, st, in, hi, q, C, HW, m_limit, maxB);
+}
+
+// The search's leaf records -> the g8 16-bit input of the input conv (16 channels = two groups of 8):
+// board b's planes are built from record gidx[b] (leaf_planes.h) and rounded as k_to_g8 rounds them.
+template <int MODE>
+__global__ void k_rec_to_g8(const uint8_t* rec, const int* gidx, uint16_t* hi, int go, int bs, const int* m_limit,
+                            int maxB) {
+    const int HW = bs * bs;
+    const int B = m_limit ? min(*m_limit, maxB) : maxB;
+    const size_t total = (size_t)B * HW;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+        const int pix = (int)(i % HW);
+        const size_t b = i / HW;
+        float c[16];
+        az_leaf_planes(rec + (size_t)gidx[b] * AZ_REC_BYTES, go, bs, pix, c);
+#pragma unroll
+        for (int g = 0; g < 2; ++g) {
+            uint16_t h[8];
+            int8_t r[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) Half16<MODE>::split(c[8 * g + e], h[e], r[e]);
+            *reinterpret_cast<uint4*>(hi + ((b * 2 + g) * HW + pix) * 8) = *reinterpret_cast<const uint4*>(h);
+        }
+    }
+}
+
+void az_launch_rec_to_g8(const uint8_t* rec, const int* gidx, uint16_t* hi, int go, int bs, const int* m_limit, int maxB,
+                         int mode, hipStream_t st) {
+    if (mode == 2) hipLaunchKernelGGL(k_rec_to_g8<2>, dim3(1024), dim3(256), 0, st, rec, gidx, hi, go, bs, m_limit, maxB);
+    else hipLaunchKernelGGL(k_rec_to_g8<1>, dim3(1024), dim3(256), 0, st, rec, gidx, hi, go, bs, m_limit, maxB);
 }
 
 // adaptive_avg_pool2d(x, (P, P)) of an H x H g8 trunk output (16-bit + int8 remainder) -> fp32 NHWC

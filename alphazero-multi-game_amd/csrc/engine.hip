@@ -23,6 +23,7 @@
 #include "engine_internal.h"
 #include "net.h"
 #include "tree.h"
+#include "leaf_planes.h"
 
 // kernels (tree_kernels.hip)
 void az_launch_select(const TreeDev& t, int mode, hipStream_t st);
@@ -50,6 +51,10 @@ bool az_conv_g8_supported(int H, int W, int C, int N);
 int az_conv_g8_launch(const ConvBf16Args& a, int mode, hipStream_t st);
 void az_launch_to_g8(const float* in, uint16_t* hi, int8_t* q, int C, int HW, const int* m_limit, int maxB, int mode,
                      hipStream_t st);
+void az_launch_rec_to_g8(const uint8_t* rec, const int* gidx, uint16_t* hi, int go, int bs, const int* m_limit, int maxB,
+                         int mode, hipStream_t st);
+void az_launch_rec_planes(const uint8_t* rec, float* dst, const int* eval_games, const int* n_eval, int go, int bs, int maxB,
+                          hipStream_t st);
 void az_launch_pool_g8(const uint16_t* hi, const int8_t* q, float* out, int B, int C, int H, int P, const int* m_limit,
                        int mode, hipStream_t st);
 void az_launch_to_f16(const float* in, uint16_t* out, size_t n, const int* m_limit, int rows_per_sample, int C,
@@ -303,9 +308,30 @@ static int fc_splits(int B, int K) {
 
 int net_heads_fc(az_net* n, int B, const int* nb, float* logits, float* value, hipStream_t st);
 
+// How the forward reads its input planes: NET_IN_SMALL (k_smallnet), NET_IN_G8 (k_to_g8 + the
+// g8 input conv) -- both can build board b's planes from the search's leaf record gidx[b]
+// (leaf_planes.h), so the search hands its leaves over without a plane batch -- or NET_IN_GEMM
+// (f32 input conv on x0).
+enum { NET_IN_GEMM = 0, NET_IN_SMALL = 1, NET_IN_G8 = 2 };
+int net_input_path(const az_net* n) {
+    const az_net_desc& d = n->d;
+    const int H = d.board_size, F = d.channels, prec = d.precision;
+    if (n->sm_W && prec == AZ_PREC_FP16 && d.blocks > 0) return NET_IN_SMALL;
+    const bool bf = (prec == AZ_PREC_BF16 || prec == AZ_PREC_FP16) && F % 32 == 0;
+    if (bf && az_conv_g8_supported(H, H, F, F) && n->in.Wbk_h != nullptr && az_conv_g8_supported(H, H, n->cin_pad, F))
+        return NET_IN_G8;
+    return NET_IN_GEMM;
+}
+
+struct LeafRecs {                 // the search's leaf records: sample b = record gidx[b]
+    const uint8_t* rec; const int* gidx; int go;
+};
+
 // Forward of B samples (B = capacity; *nb = active samples, device side) from the
-// NHWC16 input x0 -> logits [B][A], value [B].
-int net_forward(az_net* n, const float* x0, int B, const int* nb, float* logits, float* value, hipStream_t st) {
+// NHWC16 input x0 -> logits [B][A], value [B].  lr (optional; only where
+// net_input_path != NET_IN_GEMM): the planes come from leaf records instead of x0.
+int net_forward(az_net* n, const float* x0, int B, const int* nb, float* logits, float* value, hipStream_t st,
+                const LeafRecs* lr = nullptr) {
     const az_net_desc& d = n->d;
     const int H = d.board_size, W = d.board_size, HW = n->HW, F = d.channels, P = d.pool, PP = n->P2;
     const int rows = B * HW;
@@ -316,7 +342,9 @@ int net_forward(az_net* n, const float* x0, int B, const int* nb, float* logits,
     const bool g8 = bf && prec != AZ_PREC_BF16X3 && az_conv_g8_supported(H, W, F, F);
     const int mode = f16 ? 2 : 1;
     int8_t* hq[2] = {reinterpret_cast<int8_t*>(n->hl[0]), reinterpret_cast<int8_t*>(n->hl[1])};
-    if (n->sm_W && prec == AZ_PREC_FP16 && d.blocks > 0) {
+    const int inpath = net_input_path(n);
+    if (lr && inpath == NET_IN_GEMM) return az_fail(AZ_ERR_ARG, "net_forward: this net cannot read leaf records");
+    if (inpath == NET_IN_SMALL) {
         // one launch: input conv, trunk, pool and the two head 1x1 convs (smallnet.hip)
         hipEvent_t e0 = nullptr, e1 = nullptr;
         if (n->prof) {
@@ -335,7 +363,11 @@ int net_forward(az_net* n, const float* x0, int B, const int* nb, float* logits,
             HIPCHK(hipEventRecord(e0, st));
         }
         SmallNetArgs sa{};
-        sa.x0 = x0; sa.m_limit = nb; sa.W = n->sm_W; sa.bias = n->sm_b;
+        sa.x0 = x0; sa.m_limit = nb;
+        if (lr) {
+            if (lr->go) return az_fail(AZ_ERR_ARG, "smallnet: Gomoku leaf records only");
+            sa.x0 = nullptr; sa.rec = lr->rec; sa.gidx = lr->gidx;
+        } sa.W = n->sm_W; sa.bias = n->sm_b;
         sa.Wpc = n->pconv.W; sa.bpc = n->pconv.b; sa.Wvc = n->vconv.W; sa.bvc = n->vconv.b;
         sa.pp = n->pp; sa.vp = n->vp;
         sa.H = H; sa.blocks = d.blocks; sa.residual = d.residual; sa.HC = d.head_channels; sa.P = P;
@@ -345,9 +377,14 @@ int net_forward(az_net* n, const float* x0, int B, const int* nb, float* logits,
         if (e1) HIPCHK(hipEventRecord(e1, st));
         return net_heads_fc(n, B, nb, logits, value, st);
     }
-    if (g8 && n->in.Wbk_h != nullptr && az_conv_g8_supported(H, W, n->cin_pad, F)) {
+    if (inpath == NET_IN_G8) {
         // input planes -> g8 16-bit (0/1 planes are exact), then the input conv on the g8 kernel
-        az_launch_to_g8(x0, n->th, nullptr, n->cin_pad, HW, nb, B, mode, st);
+        if (lr) {
+            if (n->cin_pad != 16) return az_fail(AZ_ERR_ARG, "leaf records carry 16 planes");
+            az_launch_rec_to_g8(lr->rec, lr->gidx, n->th, lr->go, H, nb, B, mode, st);
+        } else {
+            az_launch_to_g8(x0, n->th, nullptr, n->cin_pad, HW, nb, B, mode, st);
+        }
         ConvBf16Args a{};
         a.Ahi = n->th;
         a.Bblk = f16 ? n->in.Wbk_h : n->in.Wbk_bf;
@@ -577,7 +614,7 @@ int host_evaluate(az_search* s) {
     HIPCHK(hipStreamSynchronize(st));
     if (n == 0) return 0;
     if (!s->eval_fn) return az_fail(AZ_ERR_STATE, "AZ_EVAL_CALLBACK search without az_search_set_evaluator");
-    az_launch_gather_planes(s->t.planes, s->d_batch, s->t.eval_games, s->t.n_eval, A * 16, G, st);
+    az_launch_rec_planes(s->t.leafrec, s->d_batch, s->t.eval_games, s->t.n_eval, s->t.game == GAME_GO, s->t.bs, G, st);
     hipLaunchKernelGGL(k_leaf_moves, dim3(G), dim3(64), 0, st, s->t, s->d_lmoves, s->d_llen);
     s->h_planes.resize((size_t)n * A * 16); s->h_games.resize(n); s->h_lmoves.resize((size_t)n * AZ_DMAX); s->h_llen.resize(n);
     HIPCHK(hipMemcpyAsync(s->h_planes.data(), s->d_batch, (size_t)n * A * 16 * 4, hipMemcpyDeviceToHost, st));
@@ -625,10 +662,15 @@ int search_step(az_search* s, int mode) {
     }
     if (s->c.eval_kind == AZ_EVAL_NET) {
         hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, st, s->t);
-        az_launch_gather_planes(s->t.planes, s->d_batch, s->t.eval_games, s->t.n_eval, s->t.A * 16, G, st);
+        // the net's input stage builds the leaves' planes from their records (record eval_games[b])
+        // where it can; otherwise a dense fp32 plane batch is built first
+        const bool in_place = net_input_path(s->net) != NET_IN_GEMM;
+        const LeafRecs lr{s->t.leafrec, s->t.eval_games, s->t.game == GAME_GO};
+        if (!in_place) az_launch_rec_planes(s->t.leafrec, s->d_batch, s->t.eval_games, s->t.n_eval, lr.go, s->t.bs, G, st);
         const bool prof = s->net->prof;
         if (mode != MODE_SIM) s->net->prof = false;   // time only the simulation batches
-        int r = net_forward(s->net, s->d_batch, G, s->t.n_eval, s->d_logits, s->d_value, st);
+        int r = in_place ? net_forward(s->net, nullptr, G, s->t.n_eval, s->d_logits, s->d_value, st, &lr)
+                         : net_forward(s->net, s->d_batch, G, s->t.n_eval, s->d_logits, s->d_value, st);
         s->net->prof = prof;
         if (r) return r;
     }
@@ -1079,6 +1121,7 @@ int az_search_create(az_engine* e, az_net* net, const az_search_cfg* c, az_searc
     t.hmax = go ? 2048 : 0; t.vl = c->virtual_loss; t.cpuct = c->c_puct; t.fpu = c->fpu_reduction;
     t.eval_kind = c->eval_kind; t.tt_slots = 1 << c->tt_log2; t.tt_mask = (uint64_t)t.tt_slots - 1; t.ring = ring;
     t.log_game = -1; t.log_cap = 0;
+    t.stamp_game = getenv("AZ_TREE_STAMPS") ? atoi(getenv("AZ_TREE_STAMPS")) : -1;   // diagnostic phase stamps
     const size_t NG = (size_t)G * ncap;
     int r = 0;
 #define SA(p, n) do { if (!r) r = dalloc(&(p), (size_t)(n)); } while (0)
@@ -1093,7 +1136,7 @@ int az_search_create(az_engine* e, az_net* net, const az_search_cfg* c, az_searc
     if (go) { SA(t.rko, G); SA(t.rpass, G); SA(t.rposh, (size_t)G * t.hmax); SA(t.rnposh, G); SA(zko, A + 1); }
     SA(t.path, (size_t)G * AZ_DMAX); SA(t.pact, (size_t)G * AZ_DMAX); SA(t.plen, G); SA(t.lstatus, G); SA(t.lvalue, G); SA(t.lhash, G); SA(t.ttstore, G);
     SA(t.ttref, G); SA(t.tthslot, G); SA(t.need_eval, G); SA(t.eval_slot, G); SA(t.eval_games, G); SA(t.n_eval, 1);
-    SA(t.planes, (size_t)G * A * 16);
+    SA(t.leafrec, (size_t)G * AZ_REC_BYTES);
     SA(t.tt_hash, (size_t)G * t.tt_slots); SA(t.tt_visits, (size_t)G * t.tt_slots); SA(t.tt_value, (size_t)G * t.tt_slots);
     SA(t.tt_ref, (size_t)G * t.tt_slots);
     SA(t.ring_buf, (size_t)G * ring); SA(t.ring_cur, G); SA(t.cnt, (size_t)G * AZ_NCNT);
@@ -1165,7 +1208,7 @@ void az_search_destroy(az_search* s) {
                           (const void*)t.rnode, (const void*)t.active, (const void*)t.gresult, (const void*)t.path, (const void*)t.pact,
                           (const void*)t.plen, (const void*)t.lstatus, (const void*)t.lvalue, (const void*)t.lhash,
                           (const void*)t.ttstore, (const void*)t.ttref, (const void*)t.tthslot, (const void*)t.need_eval,
-                          (const void*)t.eval_slot, (const void*)t.eval_games, (const void*)t.n_eval, (const void*)t.planes,
+                          (const void*)t.eval_slot, (const void*)t.eval_games, (const void*)t.n_eval, (const void*)t.leafrec,
                           (const void*)t.tt_hash, (const void*)t.tt_visits, (const void*)t.tt_value, (const void*)t.tt_ref,
                           (const void*)t.ring_buf, (const void*)t.ring_cur, (const void*)t.cnt, (const void*)t.zpiece,
                           (const void*)t.zplayer, (const void*)t.fresh_order, (const void*)t.mt, (const void*)t.err,

@@ -46,7 +46,9 @@ struct ConvBf16Args {
 
 // k_smallnet (smallnet.hip): the whole trunk + pool + head 1x1 convs of a 64-filter net, one board per block
 struct SmallNetArgs {
-    const float* x0;                // leaf planes [B][H*W][16] fp32 (NHWC16)
+    const float* x0;                // leaf planes [B][H*W][16] fp32 (NHWC16), or null with rec
+    const uint8_t* rec;             // or: leaf records (leaf_planes.h, Gomoku), board b = record gidx[b]
+    const int* gidx;                // with rec: the batch's games
     const int* m_limit;             // device: active boards
     const uint16_t* W;              // [2*blocks+1][9][64 n][64 c] fp16, BN folded; layer 0 = input conv (c >= planes zero)
     const float* bias;              // [2*blocks+1][64]
@@ -80,6 +82,4 @@ void az_launch_value_head(const float* part, int splits, const float* b1, const 
                           float* value, int B, int H, const int* m_limit, hipStream_t st);
 void az_launch_pool(const float* in, float* out, int B, int H, int W, int C, int P, const int* m_limit, hipStream_t st);
 void az_launch_pack_input(const float* in, float* out, int B, int Cin, int HW, int Cp, hipStream_t st);
-void az_launch_gather_planes(const float* src, float* dst, const int* eval_games, const int* n_eval, int per, int maxB,
-                             hipStream_t st);
 void az_launch_softmax_rows(const float* logits, float* out, int B, int A, hipStream_t st);

@@ -12,6 +12,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include "net.h"
+#include "leaf_planes.h"
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
@@ -223,15 +224,25 @@ __global__ void k_pack_input(const float* in, float* out, int B, int Cin, int HW
     out[i] = c < Cin ? in[((size_t)b * Cin + c) * HW + px] : 0.0f;
 }
 
-// Gather the staged per-game planes of the leaves that need the network into a
-// dense batch: dst[s] = src[eval_games[s]].
-__global__ void k_gather_planes(const float* src, float* dst, const int* eval_games, const int* n_eval, int per) {
+// The planes of the leaves that need the network as a dense fp32 NHWC16 batch built from their
+// leaf records (leaf_planes.h): dst[s] = planes(rec[eval_games[s]]) (f32 input path, host evaluator).
+__global__ void k_rec_planes(const uint8_t* rec, float* dst, const int* eval_games, const int* n_eval, int go, int bs) {
     const int s = blockIdx.y;
     if (s >= *n_eval) return;
-    const int g = eval_games[s];
-    const float4* a = reinterpret_cast<const float4*>(src + (size_t)g * per);
-    float4* b = reinterpret_cast<float4*>(dst + (size_t)s * per);
-    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < per / 4; i += gridDim.x * blockDim.x) b[i] = a[i];
+    const uint8_t* r = rec + (size_t)eval_games[s] * AZ_REC_BYTES;
+    const int A = bs * bs;
+    float4* out = reinterpret_cast<float4*>(dst + (size_t)s * A * 16);
+    for (int a = blockIdx.x * blockDim.x + threadIdx.x; a < A; a += gridDim.x * blockDim.x) {
+        float c[16];
+        az_leaf_planes(r, go, bs, a, c);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) out[(size_t)a * 4 + k] = make_float4(c[4 * k], c[4 * k + 1], c[4 * k + 2], c[4 * k + 3]);
+    }
+}
+
+void az_launch_rec_planes(const uint8_t* rec, float* dst, const int* eval_games, const int* n_eval, int go, int bs, int maxB,
+                          hipStream_t st) {
+    hipLaunchKernelGGL(k_rec_planes, dim3(2, maxB), dim3(256), 0, st, rec, dst, eval_games, n_eval, go, bs);
 }
 
 // softmax over A per row (predictBatch semantics; host-facing az_net_predict_batch)
@@ -459,11 +470,6 @@ void az_launch_pool(const float* in, float* out, int B, int H, int W, int C, int
 void az_launch_pack_input(const float* in, float* out, int B, int Cin, int HW, int Cp, hipStream_t st) {
     const size_t total = (size_t)B * HW * Cp;
     hipLaunchKernelGGL(k_pack_input, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, in, out, B, Cin, HW, Cp);
-}
-
-void az_launch_gather_planes(const float* src, float* dst, const int* eval_games, const int* n_eval, int per, int maxB,
-                             hipStream_t st) {
-    hipLaunchKernelGGL(k_gather_planes, dim3(4, maxB), dim3(256), 0, st, src, dst, eval_games, n_eval, per);
 }
 
 void az_launch_softmax_rows(const float* logits, float* out, int B, int A, hipStream_t st) {

@@ -35,6 +35,7 @@
 #include <type_traits>
 
 #include "net.h"
+#include "leaf_planes.h"
 
 namespace {
 
@@ -141,15 +142,31 @@ __global__ __launch_bounds__(256, 1) void k_smallnet(SmallNetArgs p) {
         const int i = tid + 256 * k, o = i / SF, c = i - o * SF;
         wpre[k] = o < p.HC ? p.Wpc[o * SF + c] : p.Wvc[(o - p.HC) * SF + c];
     }
-    const float* x0 = p.x0 + (size_t)b * HW * 16;
-    for (int i = tid; i < HW * 2; i += 256) {              // (pixel, 8-channel half) of the 16 input channels
-        const int px = i >> 1, h = i & 1;
-        const float4 u = *reinterpret_cast<const float4*>(x0 + px * 16 + 8 * h);
-        const float4 v = *reinterpret_cast<const float4*>(x0 + px * 16 + 8 * h + 4);
-        f16x8 o = {(_Float16)u.x, (_Float16)u.y, (_Float16)u.z, (_Float16)u.w,
-                   (_Float16)v.x, (_Float16)v.y, (_Float16)v.z, (_Float16)v.w};
-        const int y = px / HB, x = px - y * HB;
-        *reinterpret_cast<f16x8*>(imgY + img_off((y + 1) * WG + x + 1, h)) = o;
+    if (p.rec) {
+        // the search's leaf record: the 16 planes of every cell built here (leaf_planes.h)
+        const uint8_t* rec = p.rec + (size_t)p.gidx[b] * AZ_REC_BYTES;
+        for (int px = tid; px < HW; px += 256) {
+            float c[16];
+            az_leaf_planes(rec, 0, HB, px, c);
+            const int y = px / HB, x = px - y * HB;
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                f16x8 o = {(_Float16)c[8 * h], (_Float16)c[8 * h + 1], (_Float16)c[8 * h + 2], (_Float16)c[8 * h + 3],
+                           (_Float16)c[8 * h + 4], (_Float16)c[8 * h + 5], (_Float16)c[8 * h + 6], (_Float16)c[8 * h + 7]};
+                *reinterpret_cast<f16x8*>(imgY + img_off((y + 1) * WG + x + 1, h)) = o;
+            }
+        }
+    } else {
+        const float* x0 = p.x0 + (size_t)b * HW * 16;
+        for (int i = tid; i < HW * 2; i += 256) {          // (pixel, 8-channel half) of the 16 input channels
+            const int px = i >> 1, h = i & 1;
+            const float4 u = *reinterpret_cast<const float4*>(x0 + px * 16 + 8 * h);
+            const float4 v = *reinterpret_cast<const float4*>(x0 + px * 16 + 8 * h + 4);
+            f16x8 o = {(_Float16)u.x, (_Float16)u.y, (_Float16)u.z, (_Float16)u.w,
+                       (_Float16)v.x, (_Float16)v.y, (_Float16)v.z, (_Float16)v.w};
+            const int y = px / HB, x = px - y * HB;
+            *reinterpret_cast<f16x8*>(imgY + img_off((y + 1) * WG + x + 1, h)) = o;
+        }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();

@@ -50,7 +50,7 @@ struct TreeDev {
     int* pact;                   // [G][AZ_DMAX] action of every path node (pact[0] unused)
     int* lstatus; float* lvalue; uint64_t* lhash; int* ttstore; uint64_t* ttref; int* tthslot;
     int* need_eval; int* eval_slot; int* eval_games; int* n_eval;
-    float* planes;               // [G][A][16] NHWC, channels 11..15 zero (NET)
+    uint8_t* leafrec;            // [G][AZ_REC_BYTES] leaf records (leaf_planes.h): the planes' inputs (NET)
     uint64_t* tt_hash; int* tt_visits; float* tt_value; uint64_t* tt_ref;   // [G][slots]
     float* ring_buf; uint64_t* ring_cur;                                     // [G][ring], [G]
     long long* cnt;              // [G][AZ_NCNT]
@@ -62,6 +62,7 @@ struct TreeDev {
     const float* net_logits;     // [B][A] (NET) raw policy logits, by eval slot
     const float* net_value;      // [B]
     int log_game, log_cap; float* log_pol; float* log_val; float* log_planes; int* log_n;
+    int stamp_game;              // diagnostic: this game's k_select / k_expand_backup write phase stamps (-1 off)
 };
 
 // Training-example extraction (Dataset::extractExamples + augmentExample).

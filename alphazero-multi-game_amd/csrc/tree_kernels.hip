@@ -22,6 +22,7 @@
 #include <float.h>
 #include <limits.h>
 #include "tree.h"
+#include "leaf_planes.h"
 
 namespace {
 
@@ -30,11 +31,6 @@ __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
     x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ULL;
     x = (x ^ (x >> 27)) * 0x94D049BB133111EBULL;
     return x ^ (x >> 31);
-}
-
-__device__ __forceinline__ int wave_sum(int v) {
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-    return v;
 }
 
 __device__ __forceinline__ float wave_max(float v) {
@@ -49,6 +45,16 @@ __device__ __forceinline__ int wave_incl_scan(int v, int lane) {
         if (lane >= o) v += t;
     }
     return v;
+}
+
+// Diagnostic phase stamps (TreeDev.stamp_game >= 0, env AZ_TREE_STAMPS=<game>): [kernel][i] =
+// s_memrealtime (100 MHz) in [0, 32), s_memtime (shader clock) in [32, 64); tools/tree_stamps.py.
+__device__ unsigned long long g_tree_stamps[2][64];
+__device__ __forceinline__ void tstamp(const TreeDev& t, int g, int k, int i) {
+    if (g == t.stamp_game && threadIdx.x == 0) {
+        g_tree_stamps[k][i] = __builtin_amdgcn_s_memrealtime();
+        g_tree_stamps[k][32 + i] = __builtin_amdgcn_s_memtime();
+    }
 }
 
 // GameResult (include/alphazero/core/igamestate.h:26-31)
@@ -76,6 +82,26 @@ __device__ int five_at(const uint8_t* board, int bs, int a, int p) {
         if (p == 1 ? len == 5 : len >= 5) return 1;
     }
     return 0;
+}
+
+// five_at over the wave: lanes 0..7 walk the 8 rays (4 directions x 2 sides) at once, each capped
+// at 5 cells (1 + min(L,5) + min(R,5) is 5 exactly when the run is 5, and >= 5 exactly when it is).
+// Every lane of the wave must call it (wave-uniform arguments).
+__device__ int five_at_wave(const uint8_t* board, int bs, int a, int p, int lane) {
+    const int x0 = a / bs, y0 = a % bs;
+    int run = 0;
+    if (lane < 8) {
+        const int d = lane >> 1, sg = (lane & 1) ? 1 : -1;
+        const int dx = d == 0 ? 0 : 1, dy = d == 0 ? 1 : d == 1 ? 0 : d == 2 ? 1 : -1;   // {0,1},{1,0},{1,1},{1,-1}
+        int x = x0 + sg * dx, y = y0 + sg * dy;
+        while (run < 5 && x >= 0 && x < bs && y >= 0 && y < bs && board[x * bs + y] == p) {
+            ++run; x += sg * dx; y += sg * dy;
+        }
+    }
+    const int other = __shfl_xor(run, 1);
+    const int len = board[a] == p ? 1 + run + other : -1;
+    const bool win = lane < 8 && (lane & 1) == 0 && (p == 1 ? len == 5 : len >= 5);
+    return __ballot(win) != 0ULL;
 }
 
 // getPuctScore (mcts_node.cpp:61-119).  parentDepth: depth of the node being selected
@@ -154,68 +180,20 @@ __device__ __forceinline__ GamePtrs game_nodes(const Nodes& nd, size_t base) {
     return p;
 }
 
-// Leaf state = root state + path moves.  Fills the LDS board, returns side to move,
-// stone count, Zobrist hash and the last six moves (most recent first).  sact[i] is the action
-// of path node i (1..depth).  Path cells are distinct, so the moves go down lane-parallel; the
-// hash is the XOR of the root hash and the moves' piece keys (XOR order does not matter).
-__device__ __forceinline__ uint64_t wave_xor64(uint64_t v) {
-    for (int o = 32; o > 0; o >>= 1) v ^= __shfl_xor(v, o);
-    return v;
-}
+// Leaf state = root state + path moves: k_select and k_expand_backup build the Gomoku leaf board
+// inline from the root board (loaded up front) and the path actions (sact[i], i = 1..depth):
+// path cells are distinct, so the moves go down lane-parallel, and the Zobrist hash is the root
+// hash XOR the moves' piece keys XOR the side-to-move keys (gomoku_state.cpp:620-656).
 
-__device__ void build_leaf(const TreeDev& t, int g, int lane, const int* sact, int depth,
-                           uint8_t* board, int* hist6, int& player, int& stones, uint64_t& hash) {
-    const int A = t.A;
-    const int p0 = t.rplayer[g];
-    static_assert(AZ_DMAX <= 128, "two path cells per lane");
-    const int i0 = 1 + lane, i1 = 65 + lane;          // path nodes of this lane (odd i: p0 moved)
-    const int m0 = i0 <= depth ? sact[i0] : -1, m1 = i1 <= depth ? sact[i1] : -1;
-    uint64_t x = 0;                                   // piece keys first: their loads overlap the root board's
-    if (m0 >= 0) x ^= t.zpiece[(size_t)((i0 & 1) ? p0 - 1 : 2 - p0) * A + m0];
-    if (m1 >= 0) x ^= t.zpiece[(size_t)((i1 & 1) ? p0 - 1 : 2 - p0) * A + m1];
-    const uint8_t* rb = t.rboard + (size_t)g * A;
-    for (int a = lane; a < A; a += 64) board[a] = rb[a];
-    __syncthreads();
-    if (m0 >= 0) board[m0] = (uint8_t)((i0 & 1) ? p0 : 3 - p0);
-    if (m1 >= 0) board[m1] = (uint8_t)((i1 & 1) ? p0 : 3 - p0);
-    __syncthreads();
-    const int p = (depth & 1) ? 3 - p0 : p0;
-    player = p;
-    stones = t.rstones[g] + depth;
-    hash = t.rhash[g] ^ wave_xor64(x) ^ t.zplayer[p0 - 1] ^ t.zplayer[p - 1];
-    for (int i = 0; i < 6; ++i) {
-        if (i < depth) hist6[i] = sact[depth - i];
-        else hist6[i] = t.rhist[g * 6 + (i - depth)];
-    }
-}
-
-// getEnhancedTensorRepresentation (gomoku_state.cpp:207-258) in NHWC with 16 channels.
-__device__ void write_planes(const TreeDev& t, int g, int lane, const uint8_t* board, const int* hist6, int player) {
-    const int A = t.A, bs = t.bs;
-    // history plane per slot: the reference's get_previous_moves parity rule (:852-869)
-    // puts h0,h2,h4 into the "BLACK" planes 3..5 when BLACK is to move, else 6..8.
-    int hp[6];
-    for (int i = 0; i < 6; ++i) {
-        bool evenSlot = (i % 2) == 0;
-        int base = (player == 1) == evenSlot ? 3 : 6;
-        hp[i] = base + i / 2;
-    }
-    float4* out = reinterpret_cast<float4*>(t.planes + (size_t)g * A * 16);
-    const float inv = 1.0f / 1.0f;
-    (void)inv;
-    for (int a = lane; a < A; a += 64) {
-        float c[16];
-        for (int k = 0; k < 16; ++k) c[k] = 0.0f;
-        int v = board[a];
-        if (v == player) c[0] = 1.0f;
-        else if (v == 3 - player) c[1] = 1.0f;
-        if (player == 1) c[2] = 1.0f;
-        for (int i = 0; i < 6; ++i)
-            if (hist6[i] == a) c[hp[i]] = 1.0f;
-        int x = a / bs, y = a % bs;
-        c[9] = (float)x / (float)(bs - 1);
-        c[10] = (float)y / (float)(bs - 1);
-        for (int k = 0; k < 4; ++k) out[(size_t)a * 4 + k] = make_float4(c[4 * k], c[4 * k + 1], c[4 * k + 2], c[4 * k + 3]);
+// The leaf record of a Gomoku leaf (leaf_planes.h): board, side to move, last six moves.
+__device__ void write_leafrec(const TreeDev& t, int g, int lane, const uint8_t* board, const int* hist6, int player) {
+    uint8_t* rec = t.leafrec + (size_t)g * AZ_REC_BYTES;
+    for (int a = lane; a < t.A; a += 64) rec[a] = board[a];
+    int* meta = reinterpret_cast<int*>(rec + AZ_REC_META);
+    if (lane == 0) {
+        meta[0] = player; meta[1] = -1;
+#pragma unroll
+        for (int i = 0; i < 6; ++i) meta[2 + i] = hist6[i];
     }
 }
 
@@ -403,26 +381,18 @@ __device__ void go_build_leaf(const TreeDev& t, int g, int lane, const int* sact
     }
 }
 
-// getEnhancedTensorRepresentation (go_state.cpp:338-420) in NHWC16: black, white, black to move,
-// black / white group liberties min(1, libs / 10), ko point, border distances x / y.
-__device__ void go_write_planes(const TreeDev& t, int g, int lane, const uint8_t* b, const GoLds& L, int player, int ko) {
-    const int A = t.A, bs = t.bs;
-    float4* out = reinterpret_cast<float4*>(t.planes + (size_t)g * A * 16);
-    const float half = (float)(bs / 2);
-    for (int a = lane; a < A; a += 64) {
-        float c[16];
-        for (int k = 0; k < 16; ++k) c[k] = 0.0f;
-        const int v = b[a];
-        if (v == 1) c[0] = 1.0f;
-        else if (v == 2) c[1] = 1.0f;
-        c[2] = player == 1 ? 1.0f : 0.0f;
-        if (v) c[v == 1 ? 3 : 4] = fminf(1.0f, (float)L.glib[L.gid[a]] / 10.0f);
-        if (a == ko) c[5] = 1.0f;
-        const int x = a % bs, y = a / bs;
-        c[6] = (float)min(x, bs - 1 - x) / half;
-        c[7] = (float)min(y, bs - 1 - y) / half;
-        for (int k = 0; k < 4; ++k) out[(size_t)a * 4 + k] = make_float4(c[4 * k], c[4 * k + 1], c[4 * k + 2], c[4 * k + 3]);
+// The leaf record of a Go leaf (leaf_planes.h; planes of go_state.cpp:338-420): board, side to
+// move, ko point and min(10, group liberties) per stone (go_groups() must have run).
+__device__ void go_write_leafrec(const TreeDev& t, int g, int lane, const uint8_t* b, const GoLds& L, int player, int ko) {
+    uint8_t* rec = t.leafrec + (size_t)g * AZ_REC_BYTES;
+    for (int a = lane; a < t.A; a += 64) {
+        rec[a] = b[a];
+        rec[AZ_REC_LIBS + a] = b[a] ? (uint8_t)min(10, (int)L.glib[L.gid[a]]) : 0;
     }
+    int* meta = reinterpret_cast<int*>(rec + AZ_REC_META);
+    if (lane == 0) meta[0] = player;
+    if (lane == 1) meta[1] = ko;
+    if (lane < 6) meta[2 + lane] = -1;
 }
 
 // getLegalMoves (go_state.cpp:116-160): pass, then every empty non-ko point that is not suicide
@@ -491,14 +461,27 @@ __global__ __launch_bounds__(64) void k_select(TreeDev t, int mode) {
     __shared__ GoLds gl;
     const bool go = t.game == GAME_GO;
     if (g >= t.G) return;
-    if (!t.active[g]) {
+    // per-game inputs that do not depend on the tree, loaded before anything waits
+    constexpr int BK = (AZ_MAXA + 63) / 64;
+    const int A = t.A;
+    const int active = t.active[g];
+    const int root = t.rnode[g];
+    uint8_t rb[BK];
+#pragma unroll
+    for (int k = 0; k < BK; ++k) rb[k] = lane + 64 * k < A ? t.rboard[(size_t)g * A + lane + 64 * k] : 0;
+    const int p0 = t.rplayer[g], rstones = t.rstones[g], gres = t.gresult[g];
+    const uint64_t rhash = t.rhash[g], zpl0 = t.zplayer[0], zpl1 = t.zplayer[1];
+    const int rhist = lane < 6 ? t.rhist[g * 6 + lane] : -1;
+    long long* cnt = t.cnt + (size_t)g * AZ_NCNT;
+    const long long c_look = cnt[CNT_LOOKUPS], c_hits = cnt[CNT_HITS], c_bytes = cnt[CNT_BYTES_SEL];
+    tstamp(t, g, 0, 0);
+    if (!active) {
         if (lane == 0) { t.lstatus[g] = ST_NONE; t.need_eval[g] = 0; }
         return;
     }
     const size_t base = (size_t)g * t.ncap;
     GamePtrs nd = game_nodes(t.nd, base);
-    long long* cnt = t.cnt + (size_t)g * AZ_NCNT;
-    const int root = t.rnode[g];
+    uint64_t zx = 0;             // XOR of the path moves' piece keys (Gomoku), loaded level by level
     int depth = 0;
     int node = root;
     int status = ST_NONE;
@@ -508,7 +491,7 @@ __global__ __launch_bounds__(64) void k_select(TreeDev t, int mode) {
 
     if (mode != MODE_SIM) {
         // Root expansion: expandNode (noise) / search() root branch.
-        if ((nflag & (FL_EXPANDED | FL_TERMINAL)) || t.gresult[g] != R_ONGOING) {
+        if ((nflag & (FL_EXPANDED | FL_TERMINAL)) || gres != R_ONGOING) {
             if (lane == 0) { t.lstatus[g] = ST_NONE; t.need_eval[g] = 0; }
             return;
         }
@@ -520,6 +503,7 @@ __global__ __launch_bounds__(64) void k_select(TreeDev t, int mode) {
         int fc = nd.first[root], nc = nd.cnt[root];
         rN += t.vl; rVL += t.vl; rW = rW - (float)t.vl;           // addVirtualLoss (root, first)
         if (lane == 0) spath[0] = root;
+        tstamp(t, g, 0, 1);
         int pN = rN, pVL = rVL;
         float pW = rW;
         while (true) {
@@ -564,7 +548,10 @@ __global__ __launch_bounds__(64) void k_select(TreeDev t, int mode) {
             fc = __shfl(bF, src); nc = __shfl(bC, src);
             ++depth;
             if (lane == 0) { spath[depth] = node; sact[depth] = act; }
+            // its piece key lands while the next level's records load (no extra round trip)
+            if (!go) zx ^= t.zpiece[(size_t)((depth & 1) ? p0 - 1 : 2 - p0) * A + act];
         }
+        tstamp(t, g, 0, 2);
         // addVirtualLoss on every path node, root a second time (parallel_mcts.cpp:293-295)
         if (lane == 0) {
             rN += t.vl; rVL += t.vl; rW = rW - (float)t.vl;
@@ -583,12 +570,27 @@ __global__ __launch_bounds__(64) void k_select(TreeDev t, int mode) {
     uint64_t hash;
     int gko = -1, gpass = 0;
     uint64_t gbh = 0;
-    if (go) go_build_leaf(t, g, lane, sact, depth, board, gl, hist6, player, gko, gpass, gbh, hash);
-    else build_leaf(t, g, lane, sact, depth, board, hist6, player, stones, hash);
+    if (go) {
+        go_build_leaf(t, g, lane, sact, depth, board, gl, hist6, player, gko, gpass, gbh, hash);
+    } else {
+        // leaf board = root board + path moves (distinct cells, lane-parallel); hash = root hash ^
+        // the path's piece keys ^ the side-to-move keys (build_leaf, on registers already loaded)
+#pragma unroll
+        for (int k = 0; k < BK; ++k) if (lane + 64 * k < A) board[lane + 64 * k] = rb[k];
+        __syncthreads();
+        for (int i = 1 + lane; i <= depth; i += 64) board[sact[i]] = (uint8_t)((i & 1) ? p0 : 3 - p0);
+        player = (depth & 1) ? 3 - p0 : p0;
+        stones = rstones + depth;
+        hash = rhash ^ zx ^ (p0 == 1 ? zpl0 : zpl1) ^ (player == 1 ? zpl0 : zpl1);
+        for (int i = 0; i < 6; ++i) hist6[i] = i < depth ? sact[depth - i] : __shfl(rhist, i - depth);
+        __syncthreads();
+    }
+    tstamp(t, g, 0, 3);
     const int leaf = node;
     int store = 0;
     uint64_t ref = 0;
     int hslot = 0;
+    long long d_look = 0, d_hits = 0;   // counter increments (written once at the end)
 
     if (mode == MODE_SIM) {
         const uint8_t f = nflag;
@@ -598,7 +600,7 @@ __global__ __launch_bounds__(64) void k_select(TreeDev t, int mode) {
             value = convert_value((f >> 2) & 3, player);
         } else {
             if (depth == 0) {
-                result = t.gresult[g];
+                result = gres;
             } else if (go) {
                 // GoState::isTerminal: two consecutive passes; area score (go_state.cpp:291-312)
                 if (gpass >= 2) {
@@ -608,7 +610,7 @@ __global__ __launch_bounds__(64) void k_select(TreeDev t, int mode) {
                 }
             } else {
                 const int a = sact[depth];
-                if (five_at(board, t.bs, a, 3 - player)) result = (3 - player) == 1 ? R_WIN1 : R_WIN2;
+                if (five_at_wave(board, t.bs, a, 3 - player, lane)) result = (3 - player) == 1 ? R_WIN1 : R_WIN2;
                 else if (stones >= t.A) result = R_DRAW;
             }
             if (result != R_ONGOING) {
@@ -622,13 +624,16 @@ __global__ __launch_bounds__(64) void k_select(TreeDev t, int mode) {
                 const size_t tb = (size_t)g * t.tt_slots;
                 const int hs = (int)(hash & t.tt_mask);
                 const int vis = t.tt_visits[tb + hs];
-                if (vis > 0 && t.tt_hash[tb + hs] == hash) {
+                const uint64_t th = t.tt_hash[tb + hs];
+                const float tv = t.tt_value[tb + hs];
+                if (vis > 0 && th == hash) {
                     status = ST_EXPVAL;
-                    value = t.tt_value[tb + hs];
-                    if (lane == 0) { t.tt_visits[tb + hs] = vis + 1; cnt[CNT_LOOKUPS] += 1; cnt[CNT_HITS] += 1; }
+                    value = tv;
+                    if (lane == 0) t.tt_visits[tb + hs] = vis + 1;
+                    d_look += 1; d_hits += 1;
                 } else {
                     status = ST_EXPANDED;
-                    if (lane == 0) cnt[CNT_LOOKUPS] += 1;
+                    d_look += 1;
                 }
             }
         }
@@ -636,36 +641,38 @@ __global__ __launch_bounds__(64) void k_select(TreeDev t, int mode) {
         // expandNode: no legal moves -> terminal (parallel_mcts.cpp:646-654); a Go state always
         // has the pass
         if (lane == 0) {
-            nd.flag[leaf] = (uint8_t)(nflag | FL_TERMINAL | FL_EXPANDED | (R_DRAW << 2));
+            nd.flag[leaf] = (uint8_t)(nflag | FL_TERMINAL | FL_EXPANDED | (R_DRAW << 2));   // no lookups: counters unchanged
             t.lstatus[g] = ST_NONE; t.need_eval[g] = 0;
         }
         return;
     }
 
+    tstamp(t, g, 0, 4);
     if (status == ST_NONE) {
         // Transposition table (direct-mapped emulation, transposition_table.cpp:44-191)
         const size_t tb = (size_t)g * t.tt_slots;
         hslot = (int)(hash & t.tt_mask);
-        const int vis = t.tt_visits[tb + hslot];
-        const bool hit = vis > 0 && t.tt_hash[tb + hslot] == hash;
+        const int vis = t.tt_visits[tb + hslot];     // the whole entry in one round trip
+        const uint64_t th = t.tt_hash[tb + hslot];
+        const float tv = t.tt_value[tb + hslot];
+        const uint64_t tr = t.tt_ref[tb + hslot];
+        const bool hit = vis > 0 && th == hash;
         if (hit) {
             status = ST_TTHIT;
-            value = t.tt_value[tb + hslot];
-            ref = t.tt_ref[tb + hslot];
-            if (lane == 0) {
-                t.tt_visits[tb + hslot] = vis + (mode == MODE_ROOT_SEARCH ? 2 : 1);
-                cnt[CNT_LOOKUPS] += 1;
-                cnt[CNT_HITS] += 1;
-            }
+            value = tv;
+            ref = tr;
+            if (lane == 0) t.tt_visits[tb + hslot] = vis + (mode == MODE_ROOT_SEARCH ? 2 : 1);
+            d_look += 1; d_hits += 1;
         } else {
             status = ST_EVAL;
             store = (vis == 0 || vis < 5) ? 1 : 0;     // empty slot, or shouldReplace (visits < 5)
-            if (lane == 0) cnt[CNT_LOOKUPS] += (mode == MODE_ROOT_SEARCH ? 1 : 2);
+            d_look += (mode == MODE_ROOT_SEARCH ? 1 : 2);
+            tstamp(t, g, 0, 5);
             if (go) {
                 go_groups(t, board, gl, lane);
-                go_write_planes(t, g, lane, board, gl, player, gko);
+                go_write_leafrec(t, g, lane, board, gl, player, gko);
             } else {
-                write_planes(t, g, lane, board, hist6, player);
+                write_leafrec(t, g, lane, board, hist6, player);
             }
         }
     }
@@ -683,16 +690,23 @@ __global__ __launch_bounds__(64) void k_select(TreeDev t, int mode) {
         t.path[(size_t)g * AZ_DMAX + i] = spath[i];
         t.pact[(size_t)g * AZ_DMAX + i] = i ? sact[i] : -1;
     }
+    tstamp(t, g, 0, 6);
+    if (lane == 0) { cnt[CNT_LOOKUPS] = c_look + d_look; cnt[CNT_HITS] = c_hits + d_hits; }
     if (lane == 0 && mode == MODE_SIM) {
         // algorithmic bytes: child scans (whole 25 B records: N, W, VL, P + the child's header),
         // root header (21 B), VL read-modify-write (12 B + 12 B) and piece key (8 B) per path
-        // node, root board, TT probe (12 B, +20 on a hit), planes (64 B per cell, fp32 NHWC16)
-        // when the leaf goes to the network, path record (8 B per node)
+        // node, root board, TT probe (12 B, +20 on a hit), the leaf record (A board bytes + 32 B,
+        // Go: + A liberty bytes) when the leaf goes to the network, path record (8 B per node)
         long long b = scanned * 25 + 21 + (long long)(depth + 1) * (24 + 8 + 8) + t.A + 12;
         if (status == ST_TTHIT) b += 20;
-        if (status == ST_EVAL) b += 64LL * t.A;
-        cnt[CNT_BYTES_SEL] += b;
+        if (status == ST_EVAL) b += (go ? 2LL : 1LL) * t.A + 32;
+        cnt[CNT_BYTES_SEL] = c_bytes + b;
     }
+    tstamp(t, g, 0, 7);
+}
+
+extern "C" int az_diag_tree_stamps(unsigned long long* out, int n) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_tree_stamps), sizeof(unsigned long long) * (n < 128 ? n : 128)) == hipSuccess ? 0 : -1;
 }
 
 void az_launch_select(const TreeDev& t, int mode, hipStream_t st) {
@@ -739,6 +753,11 @@ __global__ __launch_bounds__(1024) void k_scan(TreeDev t) {
 }
 
 // K3: evaluator output -> TT store -> expansion -> backup.
+// Latency layout: every per-game input (status, path, cached leaf value / hash / batch slot, root
+// board, TT / ring / pool cursors, counters) is loaded before anything waits -- one round trip --
+// then the leaf's network outputs and the path nodes' statistics -- the second and last one.
+// The Gomoku leaf board is the root board plus the path moves (no Zobrist work: k_select stored
+// the leaf hash); Go replays its captures on lane 0 (go_build_leaf).
 __global__ __launch_bounds__(64) void k_expand_backup(TreeDev t, int mode) {
     const int g = blockIdx.x;
     const int lane = threadIdx.x;
@@ -750,29 +769,76 @@ __global__ __launch_bounds__(64) void k_expand_backup(TreeDev t, int mode) {
     __shared__ float lp[AZ_MAXNA];
     __shared__ float s_scalar[2];
     __shared__ GoLds gl;
+    static_assert(AZ_DMAX <= 128, "two path entries per lane");
+    constexpr int BK = (AZ_MAXA + 63) / 64, PK = (AZ_MAXNA + 63) / 64;
     const bool go = t.game == GAME_GO;
     if (g >= t.G) return;
+    const int A = t.A, NA = t.NA;
+    // ---- round trip 1
+    const size_t pb = (size_t)g * AZ_DMAX;
     const int status = t.lstatus[g];
+    const int plen = t.plen[g];
+    const float lvalue = t.lvalue[g];
+    const uint64_t lhash = t.lhash[g];
+    const int slot = t.eval_slot[g];
+    const int pth0 = t.path[pb + lane], pac0 = t.pact[pb + lane];
+    const int pth1 = lane < AZ_DMAX - 64 ? t.path[pb + 64 + lane] : 0;
+    const int pac1 = lane < AZ_DMAX - 64 ? t.pact[pb + 64 + lane] : -1;
+    uint8_t rb[BK];
+#pragma unroll
+    for (int k = 0; k < BK; ++k) rb[k] = lane + 64 * k < A ? t.rboard[(size_t)g * A + lane + 64 * k] : 0;
+    const int p0 = t.rplayer[g], rstones = t.rstones[g], rfresh = t.rfresh[g];
+    const int atop = t.atop[g], ttstore = t.ttstore[g], tthslot = t.tthslot[g];
+    const uint64_t ring_cur = t.ring_cur[g], ttref = t.ttref[g];
+    long long* cnt = t.cnt + (size_t)g * AZ_NCNT;
+    const long long c_ev = cnt[CNT_EVALS], c_evt = cnt[CNT_EVALS_TOTAL], c_sims = cnt[CNT_SIMS], c_bytes = cnt[CNT_BYTES_EXP];
+    tstamp(t, g, 1, 0);
     if (status == ST_NONE) return;
+    tstamp(t, g, 1, 1);
     const size_t base = (size_t)g * t.ncap;
     GamePtrs nd = game_nodes(t.nd, base);
-    long long* cnt = t.cnt + (size_t)g * AZ_NCNT;
-    const int A = t.A;
-    const int plen = t.plen[g];
     const int depth = plen - 1;
-    for (int i = lane; i < plen; i += 64) {
-        spath[i] = t.path[(size_t)g * AZ_DMAX + i];
-        sact[i] = t.pact[(size_t)g * AZ_DMAX + i];
+    // ---- round trip 2: the leaf's network outputs and the path statistics of the backup
+    const bool net_in = status == ST_EVAL && (t.eval_kind == 0 || t.eval_kind == 4);
+    float lg[PK];
+    float netv = 0.0f;
+    if (net_in) {
+        const float* src = t.net_logits + (size_t)slot * NA;
+#pragma unroll
+        for (int k = 0; k < PK; ++k) lg[k] = lane + 64 * k < NA ? src[lane + 64 * k] : 0.0f;
+        netv = t.net_value[slot];
     }
-    __syncthreads();
-    const int leaf = spath[depth];
-    const int NA = t.NA;
-    int hist6[6]; int player, stones = 0; uint64_t hash;
+    const bool sim = mode == MODE_SIM;
+    int bN0 = 0, bVL0 = 0, bN1 = 0, bVL1 = 0;
+    float bW0 = 0.0f, bW1 = 0.0f;
+    if (sim && lane <= depth) { bN0 = nd.N[pth0]; bVL0 = nd.VL[pth0]; bW0 = nd.W[pth0]; }
+    if (sim && lane + 64 <= depth) { bN1 = nd.N[pth1]; bVL1 = nd.VL[pth1]; bW1 = nd.W[pth1]; }
+
+    spath[lane] = pth0; sact[lane] = pac0;
+    if (lane < AZ_DMAX - 64) { spath[64 + lane] = pth1; sact[64 + lane] = pac1; }
+    int hist6[6]; int player; uint64_t hash = lhash;
     int gko = -1, gpass = 0;
     uint64_t gbh = 0;
-    if (go) go_build_leaf(t, g, lane, sact, depth, board, gl, hist6, player, gko, gpass, gbh, hash);
-    else build_leaf(t, g, lane, sact, depth, board, hist6, player, stones, hash);
-    float value = t.lvalue[g];
+    if (go) {
+        __syncthreads();
+        int stones;
+        go_build_leaf(t, g, lane, sact, depth, board, gl, hist6, player, gko, gpass, gbh, hash);
+        (void)stones;
+    } else {
+#pragma unroll
+        for (int k = 0; k < BK; ++k) if (lane + 64 * k < A) board[lane + 64 * k] = rb[k];
+        __syncthreads();
+        if (lane >= 1 && lane <= depth) board[pac0] = (uint8_t)((lane & 1) ? p0 : 3 - p0);
+        if (lane + 64 <= depth) board[pac1] = (uint8_t)(((lane + 64) & 1) ? p0 : 3 - p0);
+        player = (depth & 1) ? 3 - p0 : p0;
+        if (t.eval_kind == 1)
+            for (int i = 0; i < 6; ++i) hist6[i] = i < depth ? sact[depth - i] : t.rhist[g * 6 + (i - depth)];
+        __syncthreads();
+    }
+    tstamp(t, g, 1, 2);
+    const int leaf = spath[depth];
+    float value = lvalue;
+    long long ev_add = 0;
     // algorithmic bytes: path (4 + 4 B per level), root board, then below: policy / TT / ring,
     // new child records (25 B), VL-removal + backup read-modify-write (24 B per path node)
     long long kb = (long long)plen * 8 + A;
@@ -780,13 +846,13 @@ __global__ __launch_bounds__(64) void k_expand_backup(TreeDev t, int mode) {
     if (status == ST_EVAL || status == ST_TTHIT) {
         // legal moves in child order (gomoku_state.cpp:531-578)
         int n = 0;
-        const bool fresh = !go && (depth == 0) && t.rfresh[g];
+        const bool fresh = !go && (depth == 0) && rfresh;
         if (go) {
             go_groups(t, board, gl, lane);
             n = go_legal(t, g, lane, board, gl, player, gko, gbh, legal);
         } else if (fresh) {
             for (int i = lane; i < A; i += 64) legal[i] = t.fresh_order[i];
-            n = A - t.rstones[g];   // fresh root is the empty board
+            n = A - rstones;   // fresh root is the empty board
         } else {
             for (int c0 = 0; c0 < A; c0 += 64) {
                 const int a = A - 1 - (c0 + lane);
@@ -798,26 +864,25 @@ __global__ __launch_bounds__(64) void k_expand_backup(TreeDev t, int mode) {
             }
         }
         __syncthreads();
+        tstamp(t, g, 1, 3);
         if (status == ST_EVAL || go) {
           if (status == ST_TTHIT) {
             // Go transposition hit: a position's legal set also depends on its history (superko),
             // so the ring keeps the cached policy itself (NA floats) and expandNodeWithPolicy's
             // gather is redone over the current legal set, as the reference does with entry.policy
-            const uint64_t cur = t.ring_cur[g];
-            if (cur - t.ttref[g] > (uint64_t)t.ring) { if (lane == 0) atomicOr(t.err, ERR_RING); return; }
-            const float* rb = t.ring_buf + (size_t)g * t.ring;
-            for (int a = lane; a < NA; a += 64) pol[a] = rb[(t.ttref[g] + a) % (uint64_t)t.ring];
+            if (ring_cur - ttref > (uint64_t)t.ring) { if (lane == 0) atomicOr(t.err, ERR_RING); return; }
+            const float* rbuf = t.ring_buf + (size_t)g * t.ring;
+            for (int a = lane; a < NA; a += 64) pol[a] = rbuf[(ttref + a) % (uint64_t)t.ring];
             __syncthreads();
           } else {
-            if (lane == 0) { cnt[CNT_EVALS] += 1; cnt[CNT_EVALS_TOTAL] += 1; }
+            ev_add = 1;
             if (t.eval_kind == 0) {
-                const int slot = t.eval_slot[g];
-                const float* lg = t.net_logits + (size_t)slot * NA;
                 float mx = -FLT_MAX;
-                for (int a = lane; a < NA; a += 64) { float v = lg[a]; pol[a] = v; mx = fmaxf(mx, v); }
+#pragma unroll
+                for (int k = 0; k < PK; ++k) if (lane + 64 * k < NA) { pol[lane + 64 * k] = lg[k]; mx = fmaxf(mx, lg[k]); }
                 mx = wave_max(mx);
-                __syncthreads();
-                for (int a = lane; a < NA; a += 64) pol[a] = expf(pol[a] - mx);
+#pragma unroll
+                for (int k = 0; k < PK; ++k) if (lane + 64 * k < NA) pol[lane + 64 * k] = expf(lg[k] - mx);
                 __syncthreads();
                 if (lane == 0) {
                     float sum = 0.0f;
@@ -827,13 +892,14 @@ __global__ __launch_bounds__(64) void k_expand_backup(TreeDev t, int mode) {
                 __syncthreads();
                 const float sum = s_scalar[0];
                 if (sum > 0.0f) for (int a = lane; a < NA; a += 64) pol[a] = pol[a] / sum;
-                value = t.net_value[slot];
+                value = netv;
+                tstamp(t, g, 1, 4);
             } else if (t.eval_kind == 4) {
                 // host evaluator (az_search_set_evaluator): the policy as NeuralNetwork::predict
                 // returns it, used as is by expandNodeWithPolicy (parallel_mcts.cpp:886-901)
-                const int slot = t.eval_slot[g];
-                for (int a = lane; a < NA; a += 64) pol[a] = t.net_logits[(size_t)slot * NA + a];
-                value = t.net_value[slot];
+#pragma unroll
+                for (int k = 0; k < PK; ++k) if (lane + 64 * k < NA) pol[lane + 64 * k] = lg[k];
+                value = netv;
             } else if (t.eval_kind == 3) {
                 // no network: 1/|legal| on the legal actions, value 0 (parallel_mcts.cpp:903-916)
                 const float u = n > 0 ? 1.0f / (float)n : 0.0f;
@@ -871,9 +937,14 @@ __global__ __launch_bounds__(64) void k_expand_backup(TreeDev t, int mode) {
                     for (int a = lane; a < NA; a += 64) t.log_pol[(size_t)k * NA + a] = pol[a];
                     if (t.log_planes) {
                         const int npl = go ? 8 : 11;
-                        const float* src = t.planes + (size_t)g * A * 16;
-                        for (int a = lane; a < A; a += 64)
-                            for (int c = 0; c < npl; ++c) t.log_planes[((size_t)k * npl + c) * A + a] = src[(size_t)a * 16 + c];
+                        const uint8_t* rec = t.leafrec + (size_t)g * AZ_REC_BYTES;
+                        for (int a = lane; a < A; a += 64) {
+                            float c[16];
+                            az_leaf_planes(rec, go, t.bs, a, c);
+#pragma unroll
+                            for (int ch = 0; ch < 11; ++ch)
+                                if (ch < npl) t.log_planes[((size_t)k * npl + ch) * A + a] = c[ch];
+                        }
                     }
                     if (lane == 0) { t.log_val[k] = value; *t.log_n = k + 1; }
                 }
@@ -891,70 +962,75 @@ __global__ __launch_bounds__(64) void k_expand_backup(TreeDev t, int mode) {
             const float ps = s_scalar[0];
             if (ps > 0.0f) for (int i = lane; i < n; i += 64) lp[i] = lp[i] / ps;
             else { const float u = 1.0f / (float)n; for (int i = lane; i < n; i += 64) lp[i] = u; }
+            tstamp(t, g, 1, 5);
         } else {
             // transposition hit: the stored priors are exactly the renormalised gather of
             // the cached policy over the same legal set (same position => same order).
-            const uint64_t cur = t.ring_cur[g];
-            if (cur - t.ttref[g] > (uint64_t)t.ring) { if (lane == 0) atomicOr(t.err, ERR_RING); return; }
-            const float* rb = t.ring_buf + (size_t)g * t.ring;
-            for (int i = lane; i < n; i += 64) lp[i] = rb[(t.ttref[g] + i) % (uint64_t)t.ring];
+            if (ring_cur - ttref > (uint64_t)t.ring) { if (lane == 0) atomicOr(t.err, ERR_RING); return; }
+            const float* rbuf = t.ring_buf + (size_t)g * t.ring;
+            for (int i = lane; i < n; i += 64) lp[i] = rbuf[(ttref + i) % (uint64_t)t.ring];
         }
         __syncthreads();
         // TT store (new entry) + prior ring
-        if (status == ST_EVAL && t.ttstore[g]) {
-            const uint64_t cur = t.ring_cur[g];
-            float* rb = t.ring_buf + (size_t)g * t.ring;
+        if (status == ST_EVAL && ttstore) {
+            float* rbuf = t.ring_buf + (size_t)g * t.ring;
             const int len = go ? NA : n;            // Go keeps the policy, Gomoku the children priors
             const float* src = go ? pol : lp;
-            for (int i = lane; i < len; i += 64) rb[(cur + i) % (uint64_t)t.ring] = src[i];
+            for (int i = lane; i < len; i += 64) rbuf[(ring_cur + i) % (uint64_t)t.ring] = src[i];
             if (lane == 0) {
-                const size_t tb = (size_t)g * t.tt_slots + t.tthslot[g];
-                t.tt_hash[tb] = hash; t.tt_visits[tb] = 1; t.tt_value[tb] = value; t.tt_ref[tb] = cur;
-                t.ring_cur[g] = cur + (uint64_t)len;
+                const size_t tb = (size_t)g * t.tt_slots + tthslot;
+                t.tt_hash[tb] = hash; t.tt_visits[tb] = 1; t.tt_value[tb] = value; t.tt_ref[tb] = ring_cur;
+                t.ring_cur[g] = ring_cur + (uint64_t)len;
             }
         }
         // create children (include/alphazero/mcts/mcts_node.h: N=W=VL=0, prior, action)
-        int first = 0;
-        if (lane == 0) {
-            first = t.atop[g];
-            if (first + n > t.ncap) { atomicOr(t.err, ERR_NODES); first = -1; }
-            else t.atop[g] = first + n;
-        }
-        first = __shfl(first, 0);
-        if (first < 0) return;
+        if (atop + n > t.ncap) { if (lane == 0) atomicOr(t.err, ERR_NODES); return; }
+        const int first = atop;
         for (int i = lane; i < n; i += 64) {
             const int c = first + i;
             nd.N[c] = 0; nd.W[c] = 0.0f; nd.VL[c] = 0; nd.P[c] = lp[i];
             nd.first[c] = -1; nd.act[c] = (int16_t)legal[i]; nd.cnt[c] = 0; nd.flag[c] = 0;
         }
         if (lane == 0) {
+            t.atop[g] = first + n;
             nd.first[leaf] = first; nd.cnt[leaf] = (int16_t)n; nd.flag[leaf] = (uint8_t)(nd.flag[leaf] | FL_EXPANDED);
             cnt[CNT_NODES] = first + n;
         }
         kb += 25LL * n + 7 + 4LL * n + (status == ST_EVAL ? 4LL * NA + 4 + 24 : 0);
+        tstamp(t, g, 1, 6);
     } else if (status == ST_EXPANDED) {
         value = nd.N[leaf] == 0 ? 0.0f : nd.W[leaf] / (float)nd.N[leaf];
     }   // ST_EXPVAL: the TT value k_select cached in lvalue
 
-    if (mode == MODE_SIM) {
+    if (sim) {
         // backpropagate(node, value, searchPath) (parallel_mcts.cpp:782-833): the reference walks the
         // path leaf -> root negating v at every step, so node i gets (-1)^(depth-i) * value.  Path
         // nodes are distinct and each gets its own unchanged sequence of fp32 operations, so the
-        // update runs one lane per node (bit-identical to the sequential walk).
-        for (int i = lane; i <= depth; i += 64) {
-            const int nn = spath[i];
-            const float v = ((depth - i) & 1) ? -value : value;
-            int N = nd.N[nn], VL = nd.VL[nn];
-            float W = nd.W[nn];
-            N -= t.vl; VL -= t.vl; W = W + (float)t.vl;   // removeVirtualLoss
+        // update runs one lane per node (bit-identical to the sequential walk) on the statistics
+        // loaded in round trip 2 (nothing in this kernel writes a path node's N / VL / W before).
+        if (lane <= depth) {
+            const float v = ((depth - lane) & 1) ? -value : value;
+            int N = bN0 - t.vl, VL = bVL0 - t.vl;
+            float W = bW0 + (float)t.vl;                   // removeVirtualLoss
             N += 1;
             W = W + v;
-            nd.N[nn] = N; nd.VL[nn] = VL; nd.W[nn] = W;
+            nd.N[pth0] = N; nd.VL[pth0] = VL; nd.W[pth0] = W;
         }
-        if (lane == 0) cnt[CNT_SIMS] += 1;
+        if (lane + 64 <= depth) {
+            const float v = ((depth - lane - 64) & 1) ? -value : value;
+            int N = bN1 - t.vl, VL = bVL1 - t.vl;
+            float W = bW1 + (float)t.vl;
+            N += 1;
+            W = W + v;
+            nd.N[pth1] = N; nd.VL[pth1] = VL; nd.W[pth1] = W;
+        }
         kb += 24LL * plen;
     }
-    if (lane == 0 && mode == MODE_SIM) cnt[CNT_BYTES_EXP] += kb;
+    if (lane == 0) {
+        if (ev_add) { cnt[CNT_EVALS] = c_ev + 1; cnt[CNT_EVALS_TOTAL] = c_evt + 1; }
+        if (sim) { cnt[CNT_SIMS] = c_sims + 1; cnt[CNT_BYTES_EXP] = c_bytes + kb; }
+    }
+    tstamp(t, g, 1, 7);
 }
 
 // K4: visit distribution, action choice and root value per game.
