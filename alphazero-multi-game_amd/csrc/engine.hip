@@ -323,8 +323,8 @@ int net_input_path(const az_net* n) {
     return NET_IN_GEMM;
 }
 
-struct LeafRecs {                 // the search's leaf records: sample b = record gidx[b]
-    const uint8_t* rec; const int* gidx; int go;
+struct LeafRecs {                 // the search's leaf records: sample b = record gidx[b] (n records)
+    const uint8_t* rec; const int* gidx; int go; int n;
 };
 
 // Forward of B samples (B = capacity; *nb = active samples, device side) from the
@@ -366,7 +366,7 @@ int net_forward(az_net* n, const float* x0, int B, const int* nb, float* logits,
         sa.x0 = x0; sa.m_limit = nb;
         if (lr) {
             if (lr->go) return az_fail(AZ_ERR_ARG, "smallnet: Gomoku leaf records only");
-            sa.x0 = nullptr; sa.rec = lr->rec; sa.gidx = lr->gidx;
+            sa.x0 = nullptr; sa.rec = lr->rec; sa.gidx = lr->gidx; sa.rec_n = lr->n;
         } sa.W = n->sm_W; sa.bias = n->sm_b;
         sa.Wpc = n->pconv.W; sa.bpc = n->pconv.b; sa.Wvc = n->vconv.W; sa.bvc = n->vconv.b;
         sa.pp = n->pp; sa.vp = n->vp;
@@ -665,7 +665,7 @@ int search_step(az_search* s, int mode) {
         // the net's input stage builds the leaves' planes from their records (record eval_games[b])
         // where it can; otherwise a dense fp32 plane batch is built first
         const bool in_place = net_input_path(s->net) != NET_IN_GEMM;
-        const LeafRecs lr{s->t.leafrec, s->t.eval_games, s->t.game == GAME_GO};
+        const LeafRecs lr{s->t.leafrec, s->t.eval_games, s->t.game == GAME_GO, G};
         if (!in_place) az_launch_rec_planes(s->t.leafrec, s->d_batch, s->t.eval_games, s->t.n_eval, lr.go, s->t.bs, G, st);
         const bool prof = s->net->prof;
         if (mode != MODE_SIM) s->net->prof = false;   // time only the simulation batches

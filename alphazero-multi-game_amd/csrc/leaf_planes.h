@@ -16,12 +16,11 @@ constexpr int AZ_REC_LIBS = 384;     // Go: min(10, liberties of the cell's grou
 constexpr int AZ_REC_META = 768;     // int32: [0] side to move, [1] ko point (Go, -1 none), [2..7] last six moves
 constexpr int AZ_REC_BYTES = 800;    // per game (a multiple of 16)
 
-// The 16 NHWC channels of cell a (channels 11..15 Gomoku / 8..15 Go are zero).
-__device__ __forceinline__ void az_leaf_planes(const uint8_t* rec, int go, int bs, int a, float c[16]) {
+// The 16 NHWC channels of cell a (channels 11..15 Gomoku / 8..15 Go are zero) from the record's
+// values: v = board[a], lib = liberties byte of a (Go), meta = the record's 8 meta ints.
+__device__ __forceinline__ void az_leaf_planes_v(int v, int lib8, const int* meta, int go, int bs, int a, float c[16]) {
 #pragma clang fp contract(off)
-    const int* meta = reinterpret_cast<const int*>(rec + AZ_REC_META);
     const int player = meta[0];
-    const int v = rec[a];
 #pragma unroll
     for (int k = 0; k < 16; ++k) c[k] = 0.0f;
     if (go) {
@@ -29,7 +28,7 @@ __device__ __forceinline__ void az_leaf_planes(const uint8_t* rec, int go, int b
         else if (v == 2) c[1] = 1.0f;
         c[2] = player == 1 ? 1.0f : 0.0f;
         if (v) {
-            const float lib = fminf(1.0f, (float)rec[AZ_REC_LIBS + a] / 10.0f);
+            const float lib = fminf(1.0f, (float)lib8 / 10.0f);
             if (v == 1) c[3] = lib;
             else c[4] = lib;
         }
@@ -58,4 +57,8 @@ __device__ __forceinline__ void az_leaf_planes(const uint8_t* rec, int go, int b
         c[9] = (float)x / (float)(bs - 1);
         c[10] = (float)y / (float)(bs - 1);
     }
+}
+
+__device__ __forceinline__ void az_leaf_planes(const uint8_t* rec, int go, int bs, int a, float c[16]) {
+    az_leaf_planes_v(rec[a], go ? rec[AZ_REC_LIBS + a] : 0, reinterpret_cast<const int*>(rec + AZ_REC_META), go, bs, a, c);
 }

@@ -49,6 +49,7 @@ struct SmallNetArgs {
     const float* x0;                // leaf planes [B][H*W][16] fp32 (NHWC16), or null with rec
     const uint8_t* rec;             // or: leaf records (leaf_planes.h, Gomoku), board b = record gidx[b]
     const int* gidx;                // with rec: the batch's games
+    int rec_n;                      // with rec: records (games); gidx entries are clamped to it
     const int* m_limit;             // device: active boards
     const uint16_t* W;              // [2*blocks+1][9][64 n][64 c] fp16, BN folded; layer 0 = input conv (c >= planes zero)
     const float* bias;              // [2*blocks+1][64]

@@ -107,8 +107,22 @@ __global__ __launch_bounds__(256, 1) void k_smallnet(SmallNetArgs p) {
     float* bsm = reinterpret_cast<float*>(wbuf + NSLOT * GM::WT);   // [L][64] biases
 
     const int b = blockIdx.x;
-    if (p.m_limit && b >= *p.m_limit) return;
     const int tid = threadIdx.x, lane = tid & 63;
+    // the leaf record's bytes of this thread's pixel and its meta ints, fetched first: the batch
+    // index loads beside m_limit (clamped: entries past the active boards are stale), the record
+    // right after it
+    int rv = 0;
+    int meta[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (p.rec) {
+        const int gi = min(max(p.gidx[b], 0), p.rec_n - 1);
+        const uint8_t* rec = p.rec + (size_t)gi * AZ_REC_BYTES;
+        rv = tid < HW ? rec[tid] : 0;
+        const int4 m0 = *reinterpret_cast<const int4*>(rec + AZ_REC_META);
+        const int4 m1 = *reinterpret_cast<const int4*>(rec + AZ_REC_META + 16);
+        meta[0] = m0.x; meta[1] = m0.y; meta[2] = m0.z; meta[3] = m0.w;
+        meta[4] = m1.x; meta[5] = m1.y; meta[6] = m1.z; meta[7] = m1.w;
+    }
+    if (p.m_limit && b >= *p.m_limit) return;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int L = 2 * p.blocks + 1;
     const int S = 9 * L;                                 // weight tiles streamed: (layer, tap)
@@ -143,11 +157,12 @@ __global__ __launch_bounds__(256, 1) void k_smallnet(SmallNetArgs p) {
         wpre[k] = o < p.HC ? p.Wpc[o * SF + c] : p.Wvc[(o - p.HC) * SF + c];
     }
     if (p.rec) {
-        // the search's leaf record: the 16 planes of every cell built here (leaf_planes.h)
-        const uint8_t* rec = p.rec + (size_t)p.gidx[b] * AZ_REC_BYTES;
-        for (int px = tid; px < HW; px += 256) {
+        // the search's leaf record: the 16 planes of this thread's cell built here (leaf_planes.h)
+        static_assert(HW <= 256, "one cell per thread");
+        if (tid < HW) {
+            const int px = tid;
             float c[16];
-            az_leaf_planes(rec, 0, HB, px, c);
+            az_leaf_planes_v(rv, 0, meta, 0, HB, px, c);
             const int y = px / HB, x = px - y * HB;
 #pragma unroll
             for (int h = 0; h < 2; ++h) {

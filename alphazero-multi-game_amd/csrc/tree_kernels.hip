@@ -33,6 +33,23 @@ __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
     return x ^ (x >> 31);
 }
 
+// sum_{i < n} x[i] in index order from 0.0f (the reference's sequential float loops) by lane 0,
+// 16 values per step read as four ds_read_b128 ahead of their adds; x is 16-B aligned and padded
+// with +0.0f to a multiple of 16 entries (adding +0.0f to a non-negative sum changes no bit).
+// Returns the sum on lane 0 only.
+__device__ __forceinline__ float seq_sum_lds(const float* x, int n) {
+    float s = 0.0f;
+    const float4* q = reinterpret_cast<const float4*>(x);
+    for (int j = 0; j < (n + 15) / 16; ++j) {
+        const float4 a = q[4 * j], b = q[4 * j + 1], c = q[4 * j + 2], d = q[4 * j + 3];
+        s += a.x; s += a.y; s += a.z; s += a.w;
+        s += b.x; s += b.y; s += b.z; s += b.w;
+        s += c.x; s += c.y; s += c.z; s += c.w;
+        s += d.x; s += d.y; s += d.z; s += d.w;
+    }
+    return s;
+}
+
 __device__ __forceinline__ float wave_max(float v) {
     for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
     return v;
@@ -764,9 +781,10 @@ __global__ __launch_bounds__(64) void k_expand_backup(TreeDev t, int mode) {
     __shared__ uint8_t board[AZ_MAXA];
     __shared__ int spath[AZ_DMAX];
     __shared__ int sact[AZ_DMAX];
-    __shared__ float pol[AZ_MAXNA];
+    constexpr int NPAD = ((AZ_MAXNA + 63) / 64) * 64;   // pol / lp padded with +0.0f for seq_sum_lds
+    __shared__ __attribute__((aligned(16))) float pol[NPAD];
     __shared__ int legal[AZ_MAXNA];
-    __shared__ float lp[AZ_MAXNA];
+    __shared__ __attribute__((aligned(16))) float lp[NPAD];
     __shared__ float s_scalar[2];
     __shared__ GoLds gl;
     static_assert(AZ_DMAX <= 128, "two path entries per lane");
@@ -881,17 +899,19 @@ __global__ __launch_bounds__(64) void k_expand_backup(TreeDev t, int mode) {
 #pragma unroll
                 for (int k = 0; k < PK; ++k) if (lane + 64 * k < NA) { pol[lane + 64 * k] = lg[k]; mx = fmaxf(mx, lg[k]); }
                 mx = wave_max(mx);
+                float e[PK];
 #pragma unroll
-                for (int k = 0; k < PK; ++k) if (lane + 64 * k < NA) pol[lane + 64 * k] = expf(lg[k] - mx);
-                __syncthreads();
-                if (lane == 0) {
-                    float sum = 0.0f;
-                    for (int a = 0; a < NA; ++a) sum += pol[a];
-                    s_scalar[0] = sum;
+                for (int k = 0; k < PK; ++k) {
+                    e[k] = lane + 64 * k < NA ? expf(lg[k] - mx) : 0.0f;
+                    pol[lane + 64 * k] = e[k];                 // +0.0f past NA
                 }
                 __syncthreads();
+                if (lane == 0) s_scalar[0] = seq_sum_lds(pol, NA);
+                __syncthreads();
                 const float sum = s_scalar[0];
-                if (sum > 0.0f) for (int a = lane; a < NA; a += 64) pol[a] = pol[a] / sum;
+#pragma unroll
+                for (int k = 0; k < PK; ++k)
+                    if (lane + 64 * k < NA && sum > 0.0f) pol[lane + 64 * k] = e[k] / sum;
                 value = netv;
                 tstamp(t, g, 1, 4);
             } else if (t.eval_kind == 4) {
@@ -951,17 +971,22 @@ __global__ __launch_bounds__(64) void k_expand_backup(TreeDev t, int mode) {
             }
           }
             // expandNodeWithPolicy: gather, sequential sum, renormalise (parallel_mcts.cpp:702-724)
-            for (int i = lane; i < n; i += 64) lp[i] = legal[i] >= 0 ? pol[legal[i]] : 0.0f;   // pass: no prior
-            __syncthreads();
-            if (lane == 0) {
-                float sum = 0.0f;
-                for (int i = 0; i < n; ++i) sum += lp[i];
-                s_scalar[0] = sum;
+            float gv[PK];
+#pragma unroll
+            for (int k = 0; k < PK; ++k) {
+                const int i = lane + 64 * k;
+                gv[k] = i < n && legal[i] >= 0 ? pol[legal[i]] : 0.0f;   // pass: no prior
             }
+#pragma unroll
+            for (int k = 0; k < PK; ++k) lp[lane + 64 * k] = gv[k];   // +0.0f past n
+            __syncthreads();
+            if (lane == 0) s_scalar[0] = seq_sum_lds(lp, n);
             __syncthreads();
             const float ps = s_scalar[0];
-            if (ps > 0.0f) for (int i = lane; i < n; i += 64) lp[i] = lp[i] / ps;
-            else { const float u = 1.0f / (float)n; for (int i = lane; i < n; i += 64) lp[i] = u; }
+            const float u = 1.0f / (float)n;
+#pragma unroll
+            for (int k = 0; k < PK; ++k)
+                if (lane + 64 * k < n) lp[lane + 64 * k] = ps > 0.0f ? gv[k] / ps : u;
             tstamp(t, g, 1, 5);
         } else {
             // transposition hit: the stored priors are exactly the renormalised gather of
