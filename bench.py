@@ -244,7 +244,7 @@ def run_rank(a, rank, world, dist, make_workload, coll_device):
                                    "bytes counted by the kernels (child records scanned, path VL/backup "
                                    "read-modify-writes, new nodes, leaf planes); latency-bound (one wave per game, "
                                    "dependent tree levels), peak 8 TB/s; rocprofv3 PMC traffic of the same kernels: "
-                                   "profiles/r01e_tree_pmc.json (tools/tree_pmc.sh)")
+                                   "profiles/r02h_tree_pmc.json (tools/tree_pmc.sh: C3 games at 400 sims; 800-sim moves hang rocprofv3 --pmc)")
     tr = pmc_traffic(a, kernel, boards_per_launch if launches else 0)
     if tr:
         out["roofline"].update(tr)
