@@ -31,6 +31,7 @@
 // residual block (reads X, writes Y), even >= 2 = second conv (reads Y, adds xs, writes xs + X).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include <type_traits>
 
@@ -45,13 +46,14 @@ typedef __attribute__((address_space(3))) void lds_void_t;
 
 constexpr int SF = 64;           // filters (channels) of the fused trunk
 
-template <int HB>
+template <int HB, int NW = 4>
 struct SmGeom {
     static constexpr int WG = HB + 2;                    // grid / halo row width
     static constexpr int HW = HB * HB;
     static constexpr int GRID = HB * WG;                 // output grid rows
     static constexpr int NFRAG = (GRID + 15) / 16;       // 16-row pixel fragments
-    static constexpr int FPW = (NFRAG + 3) / 4;          // fragments per wave (4 waves)
+    static constexpr int FPW = (NFRAG + 3) / 4;          // fragments per pixel-wave (4 pixel groups)
+    static constexpr int JN = 4 * 4 / NW;                // 16-channel output blocks per wave (NW = 4: all 4, 8: 2)
     static constexpr int IR = NFRAG * 16 + 2 * WG + 2;   // halo rows the last fragment's taps read
     static constexpr int IMG = IR * SF * 2;              // bytes of one halo image
     static constexpr int XS = HW * SF * 4;               // fp32 stream at the end (over the two images)
@@ -96,10 +98,18 @@ extern "C" int az_diag_smallnet_stamps(unsigned long long* out, int n) {
 // DV: timing-only variants (build with -DAZ_SM_DIAG, AZ_SM_STAMPS=<DV+1>): 1 = no per-tap barriers
 // (waits only), 2 = no MFMAs, 3 = neither, 4 = no fragment reads after a layer's first steps
 // (MFMAs on stale registers), 8 = no weight DMA in the layers.  Their outputs are wrong.
-template <int HB, int DV = 0>
-__global__ __launch_bounds__(256, 1) void k_smallnet(SmallNetArgs p) {
-    typedef SmGeom<HB> GM;
+// NW = 4: one wave per SIMD, each wave all 64 output channels of its 4 pixel fragments.  NW = 8
+// (default; AZ_SM_WAVES=4 selects the other): two waves per SIMD, wave w owns the pixel fragments
+// of group w & 3 and output channels 32 (w >> 2) .. +31.  Measured (phase stamps, 256 boards): the
+// layers take the same 11.3k cycles either way -- every layer ends in a block-wide epilogue and
+// barrier that no MFMA can overlap, one board per CU -- while the prologue, pool and head convs
+// are 2.4 us shorter with 8 waves.
+template <int HB, int DV = 0, int NW = 4>
+__global__ __launch_bounds__(64 * NW, 1) void k_smallnet(SmallNetArgs p) {
+    typedef SmGeom<HB, NW> GM;
+    constexpr int NT = 64 * NW;                          // threads
     constexpr int WG = GM::WG, HW = GM::HW, NFRAG = GM::NFRAG, FPW = GM::FPW, NSLOT = GM::NSLOT, DIST = GM::DIST;
+    constexpr int JN = GM::JN;
     __shared__ __attribute__((aligned(16))) uint8_t lds[GM::LDS];
     uint8_t* imgX = lds;
     uint8_t* imgY = lds + GM::IMG;
@@ -124,6 +134,8 @@ __global__ __launch_bounds__(256, 1) void k_smallnet(SmallNetArgs p) {
     }
     if (p.m_limit && b >= *p.m_limit) return;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wp = wave & 3;                             // pixel group: fragments wp + 4 i
+    const int j0 = (wave >> 2) * JN;                     // first 16-channel output block of this wave
     const int L = 2 * p.blocks + 1;
     const int S = 9 * L;                                 // weight tiles streamed: (layer, tap)
     sm_stamp(p, 0);
@@ -132,30 +144,34 @@ __global__ __launch_bounds__(256, 1) void k_smallnet(SmallNetArgs p) {
     // physical chunk pc) holds logical chunk pc ^ (n & 7) (the swizzle applied at the source).
     // Past the last tile the last tile is reloaded into the free slot, so every tap issues the
     // same two loads and the vmcnt budget is a constant.
+    constexpr int WPT = 512 / NT;                        // weight pieces per thread per tile
     auto issue_w = [&](int s) {
         uint8_t* dst = wbuf + (s % NSLOT) * GM::WT;
         const int sl = s < S ? s : S - 1;
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            const int P = j * 256 + tid, n = P >> 3, pc = P & 7, k = pc ^ (n & 7);
+        for (int j = 0; j < WPT; ++j) {
+            const int P = j * NT + tid, n = P >> 3, pc = P & 7, k = pc ^ (n & 7);
             const uint16_t* src = p.W + ((size_t)sl * SF + n) * SF + 8 * k;
-            __builtin_amdgcn_global_load_lds((const void*)src, (lds_void_t*)(dst + (j * 256 + wave * 64) * 16), 16, 0, 0);
+            __builtin_amdgcn_global_load_lds((const void*)src, (lds_void_t*)(dst + (j * NT + wave * 64) * 16), 16, 0, 0);
         }
     };
     for (int s = 0; s < DIST; ++s) issue_w(s);
 
     // zero both halo images (borders and dead columns stay zero), the input planes into Y, biases
-    for (int i = tid; i < 2 * GM::IMG / 16; i += 256) *reinterpret_cast<uint4*>(imgX + i * 16) = uint4{0, 0, 0, 0};
-    for (int i = tid; i < L * SF; i += 256) bsm[i] = p.bias[i];
+    for (int i = tid; i < 2 * GM::IMG / 16; i += NT) *reinterpret_cast<uint4*>(imgX + i * 16) = uint4{0, 0, 0, 0};
+    for (int i = tid; i < L * SF; i += NT) bsm[i] = p.bias[i];
     __syncthreads();
     // the head 1x1 conv weights, transposed to [c][o], fetched now (written to LDS after the trunk)
-    constexpr int HWT = SF * SF / 256;                   // weights per thread (2 * HC == SF outputs)
+    constexpr int HWT = SF * SF / NT;                    // weights per thread (2 * HC == SF outputs)
     float wpre[HWT];
+    auto head_w = [&]() {
 #pragma unroll
-    for (int k = 0; k < HWT; ++k) {
-        const int i = tid + 256 * k, o = i / SF, c = i - o * SF;
-        wpre[k] = o < p.HC ? p.Wpc[o * SF + c] : p.Wvc[(o - p.HC) * SF + c];
-    }
+        for (int k = 0; k < HWT; ++k) {
+            const int i = tid + NT * k, o = i / SF, c = i - o * SF;
+            wpre[k] = o < p.HC ? p.Wpc[o * SF + c] : p.Wvc[(o - p.HC) * SF + c];
+        }
+    };
+    if constexpr (NW == 4) head_w();                     // NW = 8: after the trunk (registers)
     if (p.rec) {
         // the search's leaf record: the 16 planes of this thread's cell built here (leaf_planes.h)
         static_assert(HW <= 256, "one cell per thread");
@@ -173,7 +189,7 @@ __global__ __launch_bounds__(256, 1) void k_smallnet(SmallNetArgs p) {
         }
     } else {
         const float* x0 = p.x0 + (size_t)b * HW * 16;
-        for (int i = tid; i < HW * 2; i += 256) {          // (pixel, 8-channel half) of the 16 input channels
+        for (int i = tid; i < HW * 2; i += NT) {           // (pixel, 8-channel half) of the 16 input channels
             const int px = i >> 1, h = i & 1;
             const float4 u = *reinterpret_cast<const float4*>(x0 + px * 16 + 8 * h);
             const float4 v = *reinterpret_cast<const float4*>(x0 + px * 16 + 8 * h + 4);
@@ -188,22 +204,28 @@ __global__ __launch_bounds__(256, 1) void k_smallnet(SmallNetArgs p) {
     sm_stamp(p, 1);
 
     const int l16 = lane & 15, lg = lane >> 4;
-    f32x4v acc[FPW][4];
-    f32x4v xr[FPW][4];                                   // the lane's residual-stream values (fp32), kept in registers
-    f16x8 fa[2][4], fb[2][FPW];                          // operand fragments, double-buffered across steps
+    f32x4v acc[FPW][JN];
+    f32x4v xr[FPW][JN];                                  // the lane's residual-stream values (fp32), kept in registers
+    f16x8 fa[2][JN], fb[2][FPW];                         // operand fragments, double-buffered across steps
 
     // one (tap, 32-channel chunk) step: fragments into buffer `r` / MFMAs from buffer `r`
     auto load = [&](int r, const uint8_t* src, int s, auto tc, auto kc) {
         constexpr int t = decltype(tc)::value, kk = decltype(kc)::value;
         constexpr int sh = (t / 3) * WG + (t % 3);
         const uint8_t* wt = wbuf + (s % NSLOT) * GM::WT;
-        static_for<0, 4>([&](auto jc) {
+        // NW = 8: recompute the lane's fragment addresses at every step (an opaque copy of the lane
+        // id): hoisted out of the layer loop, the 18 steps' addresses alone would spill the
+        // 256-register budget of two waves per SIMD
+        int ln = lane;
+        if constexpr (NW == 8) asm volatile("" : "+v"(ln));
+        const int l16 = ln & 15, lg = ln >> 4;
+        static_for<0, JN>([&](auto jc) {
             constexpr int j = decltype(jc)::value;
-            fa[r][j] = *reinterpret_cast<const f16x8*>(wt + img_off(16 * j + l16, 4 * kk + lg));
+            fa[r][j] = *reinterpret_cast<const f16x8*>(wt + img_off(16 * (j0 + j) + l16, 4 * kk + lg));
         });
         static_for<0, FPW>([&](auto ic) {
             constexpr int i = decltype(ic)::value;
-            const int f = wave + 4 * i;
+            const int f = wp + 4 * i;
             if (NFRAG % 4 == 0 || f < NFRAG)
                 fb[r][i] = *reinterpret_cast<const f16x8*>(src + img_off(16 * f + l16 + sh, 4 * kk + lg));
         });
@@ -211,8 +233,8 @@ __global__ __launch_bounds__(256, 1) void k_smallnet(SmallNetArgs p) {
     auto mma = [&](int r) {
         static_for<0, FPW>([&](auto ic) {
             constexpr int i = decltype(ic)::value;
-            if (NFRAG % 4 == 0 || wave + 4 * i < NFRAG)
-                static_for<0, 4>([&](auto jc) {
+            if (NFRAG % 4 == 0 || wp + 4 * i < NFRAG)
+                static_for<0, JN>([&](auto jc) {
                     constexpr int j = decltype(jc)::value;
                     acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[r][j], fb[r][i], acc[i][j], 0, 0, 0);
                 });
@@ -223,13 +245,13 @@ __global__ __launch_bounds__(256, 1) void k_smallnet(SmallNetArgs p) {
         const bool odd = layer & 1;
         static_for<0, FPW>([&](auto ic) {
             constexpr int i = decltype(ic)::value;
-            const int f = wave + 4 * i;
+            const int f = wp + 4 * i;
             const int q = 16 * f + l16, y = q / WG, x = q - y * WG;
             const bool live = f < NFRAG && y < HB && x < HB;
             const int row = (y + 1) * WG + x + 1;
-            static_for<0, 4>([&](auto jc) {
+            static_for<0, JN>([&](auto jc) {
                 constexpr int j = decltype(jc)::value;
-                const int c0 = 16 * j + 4 * lg;
+                const int c0 = 16 * (j0 + j) + 4 * lg;
                 f32x4v v = acc[i][j];
                 if (layer > 0 && !odd && p.residual) v += xr[i][j];
 #pragma unroll
@@ -248,9 +270,9 @@ __global__ __launch_bounds__(256, 1) void k_smallnet(SmallNetArgs p) {
         const bool odd = layer & 1;
         const uint8_t* src = odd ? imgX : imgY;
         uint8_t* dst = odd ? imgY : imgX;
-        static_for<0, 4>([&](auto jc) {
+        static_for<0, JN>([&](auto jc) {
             constexpr int j = decltype(jc)::value;
-            const f32x4v bv = *reinterpret_cast<const f32x4v*>(bsm + layer * SF + 16 * j + 4 * lg);
+            const f32x4v bv = *reinterpret_cast<const f32x4v*>(bsm + layer * SF + 16 * (j0 + j) + 4 * lg);
             static_for<0, FPW>([&](auto ic) { acc[decltype(ic)::value][j] = bv; });
         });
         const int s0 = layer * 9;
@@ -269,13 +291,14 @@ __global__ __launch_bounds__(256, 1) void k_smallnet(SmallNetArgs p) {
             if constexpr (kk == NCH - 1) {
                 // tile s+2 landed (s+3..s+DIST stay in flight: no __syncthreads, whose vmcnt(0) would
                 // drain them); the epilogue's image writes are complete before the barrier
+                // (DIST - 2) tiles of WPT loads each stay in flight
                 if constexpr (t == 8) {
                     epilogue(layer, dst);
-                    asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+                    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"i"((DIST - 2) * WPT) : "memory");
                 } else if constexpr (DV & 1) {
-                    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+                    asm volatile("s_waitcnt vmcnt(%0)" ::"i"((DIST - 2) * WPT) : "memory");
                 } else {
-                    asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
+                    asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"i"((DIST - 2) * WPT) : "memory");
                 }
             }
         });
@@ -291,15 +314,16 @@ __global__ __launch_bounds__(256, 1) void k_smallnet(SmallNetArgs p) {
     // the fp32 stream to LDS (over the two images), adaptive average pool to P x P cells (torch
     // adaptive_avg_pool2d bins), then the policy / value 1x1 convs (BN folded, k-ordered fp32 FMA
     // chain + bias, ReLU); the 1x1 weights are staged transposed ([c][o]) in the ring
+    if constexpr (NW == 8) head_w();
     uint8_t* xs = lds;
     static_for<0, FPW>([&](auto ic) {
         constexpr int i = decltype(ic)::value;
-        const int f = wave + 4 * i;
+        const int f = wp + 4 * i;
         const int q = 16 * f + l16, y = q / WG, x = q - y * WG;
         if (f < NFRAG && y < HB && x < HB)
-            static_for<0, 4>([&](auto jc) {
+            static_for<0, JN>([&](auto jc) {
                 constexpr int j = decltype(jc)::value;
-                *reinterpret_cast<f32x4v*>(xs + xs_off(y * HB + x, (16 * j + 4 * lg) >> 2)) = xr[i][j];
+                *reinterpret_cast<f32x4v*>(xs + xs_off(y * HB + x, (16 * (j0 + j) + 4 * lg) >> 2)) = xr[i][j];
             });
     });
     const int P = p.P, PP = P * P, HC = p.HC;
@@ -308,13 +332,13 @@ __global__ __launch_bounds__(256, 1) void k_smallnet(SmallNetArgs p) {
     float* wt = pooled + SF * 64;                        // [64 c][HO o] (policy outputs, then value)
 #pragma unroll
     for (int k = 0; k < HWT; ++k) {
-        const int i = tid + 256 * k, o = i / SF, c = i - o * SF;
+        const int i = tid + NT * k, o = i / SF, c = i - o * SF;
         wt[c * HO + o] = wpre[k];
     }
-    for (int i = tid; i < SF * 64; i += 256) pooled[i] = 0.0f;
+    for (int i = tid; i < SF * 64; i += NT) pooled[i] = 0.0f;
     __syncthreads();
     sm_stamp(p, 40);
-    for (int i = tid; i < PP * (SF / 4); i += 256) {
+    for (int i = tid; i < PP * (SF / 4); i += NT) {
         const int cell = i / (SF / 4), c4 = i - cell * (SF / 4), oy = cell / P, ox = cell - oy * P;
         const int y0 = (oy * HB) / P, y1 = ((oy + 1) * HB + P - 1) / P;
         const int xa = (ox * HB) / P, xb = ((ox + 1) * HB + P - 1) / P;
@@ -330,19 +354,19 @@ __global__ __launch_bounds__(256, 1) void k_smallnet(SmallNetArgs p) {
     // head 1x1 convs on the f32 MFMA (v_mfma_f32_16x16x4_f32: an exact k-ordered fmaf chain, as
     // gemm_f32): D[o][cell] = sum_c W[o][c] pooled[cell][c]; wave w owns cells 16w..16w+15
     {
-        const int cell = 16 * wave + l16;
-        f32x4v hacc[4] = {};
+        const int cell = 16 * wp + l16;                  // wave w: cells 16 (w & 3) .., outputs 16 (j0 + j) ..
+        f32x4v hacc[JN] = {};
         for (int kb = 0; kb < SF / 4; ++kb) {
             const int c = 4 * kb + lg;
             const float bv = pooled[c * 64 + cell];
 #pragma unroll
-            for (int j = 0; j < 4; ++j)
-                hacc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(wt[c * HO + 16 * j + l16], bv, hacc[j], 0, 0, 0);
+            for (int j = 0; j < JN; ++j)
+                hacc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(wt[c * HO + 16 * (j0 + j) + l16], bv, hacc[j], 0, 0, 0);
         }
         if (cell < PP) {
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int o = 16 * j + 4 * lg;              // 4 consecutive outputs, all policy or all value
+            for (int j = 0; j < JN; ++j) {
+                const int o = 16 * (j0 + j) + 4 * lg;       // 4 consecutive outputs, all policy or all value
                 const bool pol = o < HC;
                 const int oc = pol ? o : o - HC;
                 const float* bias = (pol ? p.bpc : p.bvc) + oc;
@@ -379,6 +403,8 @@ int az_smallnet_launch(const SmallNetArgs& a, int B, hipStream_t st) {
         default: break;
     }
 #endif
-    hipLaunchKernelGGL(k_smallnet<15>, dim3(B), dim3(256), 0, st, a);
+    static const int nw = getenv("AZ_SM_WAVES") ? atoi(getenv("AZ_SM_WAVES")) : 8;
+    if (nw == 4) hipLaunchKernelGGL((k_smallnet<15, 0, 4>), dim3(B), dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((k_smallnet<15, 0, 8>), dim3(B), dim3(512), 0, st, a);
     return 0;
 }
