@@ -89,6 +89,17 @@ __device__ __forceinline__ void sm_stamp(const SmallNetArgs& p, int i) {
     }
 }
 
+// s_waitcnt lgkmcnt(N), then every fragment of a and b tied to that point (empty asm rewriting
+// them), so no MFMA that reads them is scheduled above the wait
+template <int N, int JA, int JB, typename F>
+__device__ __forceinline__ void certify_frags(F (&a)[JA], F (&b)[JB]) {
+    asm volatile("s_waitcnt lgkmcnt(%0)" ::"i"(N) : "memory");
+#pragma unroll
+    for (int j = 0; j < JA; ++j) asm volatile("" : "+v"(a[j]));
+#pragma unroll
+    for (int i = 0; i < JB; ++i) asm volatile("" : "+v"(b[i]));
+}
+
 }  // namespace
 
 extern "C" int az_diag_smallnet_stamps(unsigned long long* out, int n) {
@@ -206,9 +217,15 @@ __global__ __launch_bounds__(64 * NW, 1) void k_smallnet(SmallNetArgs p) {
     const int l16 = lane & 15, lg = lane >> 4;
     f32x4v acc[FPW][JN];
     f32x4v xr[FPW][JN];                                  // the lane's residual-stream values (fp32), kept in registers
-    f16x8 fa[2][JN], fb[2][FPW];                         // operand fragments, double-buffered across steps
+    f16x8 fa[3][JN], fb[3][FPW];                         // operand fragments, three buffers: reads run 2 steps ahead
 
     // one (tap, 32-channel chunk) step: fragments into buffer `r` / MFMAs from buffer `r`
+    // fragment reads as inline-asm ds_read_b128 with explicit lgkmcnt waits: the compiler's own
+    // waits drained to lgkmcnt(0) before every other step's MFMAs, i.e. the next step's reads had to
+    // land before this step's MFMAs could issue (no prefetch distance for half the steps)
+    auto rd = [&](f16x8& d, const uint8_t* ptr) {
+        asm volatile("ds_read_b128 %0, %1" : "=v"(d) : "v"((uint32_t)(uintptr_t)ptr) : "memory");
+    };
     auto load = [&](int r, const uint8_t* src, int s, auto tc, auto kc) {
         constexpr int t = decltype(tc)::value, kk = decltype(kc)::value;
         constexpr int sh = (t / 3) * WG + (t % 3);
@@ -221,15 +238,22 @@ __global__ __launch_bounds__(64 * NW, 1) void k_smallnet(SmallNetArgs p) {
         const int l16 = ln & 15, lg = ln >> 4;
         static_for<0, JN>([&](auto jc) {
             constexpr int j = decltype(jc)::value;
-            fa[r][j] = *reinterpret_cast<const f16x8*>(wt + img_off(16 * (j0 + j) + l16, 4 * kk + lg));
+            rd(fa[r][j], wt + img_off(16 * (j0 + j) + l16, 4 * kk + lg));
         });
         static_for<0, FPW>([&](auto ic) {
             constexpr int i = decltype(ic)::value;
             const int f = wp + 4 * i;
             if (NFRAG % 4 == 0 || f < NFRAG)
-                fb[r][i] = *reinterpret_cast<const f16x8*>(src + img_off(16 * f + l16 + sh, 4 * kk + lg));
+                rd(fb[r][i], src + img_off(16 * f + l16 + sh, 4 * kk + lg));
         });
     };
+    // wait until at most N fragment reads are outstanding (the next step's), then tie buffer r's
+    // fragments to that point so no MFMA reading them is scheduled above the wait
+    auto certify = [&](auto rc, auto nc) {
+        constexpr int R = decltype(rc)::value, N = decltype(nc)::value;
+        certify_frags<N>(fa[R], fb[R]);
+    };
+    static_assert(NFRAG % 4 == 0, "every pixel-wave loads FPW fragments (the certify counts)");
     auto mma = [&](int r) {
         static_for<0, FPW>([&](auto ic) {
             constexpr int i = decltype(ic)::value;
@@ -276,15 +300,23 @@ __global__ __launch_bounds__(64 * NW, 1) void k_smallnet(SmallNetArgs p) {
             static_for<0, FPW>([&](auto ic) { acc[decltype(ic)::value][j] = bv; });
         });
         const int s0 = layer * 9;
+        // step x's fragments are read at step x - 2 (buffer x % 3); the two steps of a layer's first
+        // tap before the loop.  A step's reads are certified once at most the younger batches are
+        // outstanding.  Tile (tap) t+1 is certified before tap t starts, so reads one tap ahead are legal.
+        constexpr int NSTEP = 9 * NCH;
+        auto LD = [](int x) constexpr { return x < NSTEP && !((DV & 4) && x > 2); };
         load(0, src, s0, std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{});
-        static_for<0, 9 * NCH>([&](auto qc) {
-            constexpr int q = decltype(qc)::value, t = q / NCH, kk = q % NCH, r = q & 1;
-            if constexpr (kk == 0 && !(DV & 8)) issue_w(s0 + t + DIST);   // its slot was last read at tap s - 2
-            if constexpr (q + 1 < 9 * NCH && !((DV & 4) && q > 1))
-                load(r ^ 1, src, s0 + (q + 1) / NCH, std::integral_constant<int, (q + 1) / NCH>{},
-                     std::integral_constant<int, (q + 1) % NCH>{});
-            // pin the order: the next step's reads are in flight while this step's MFMAs issue (the
-            // scheduler would otherwise pull each read next to its first use behind an lgkmcnt(0))
+        if constexpr (LD(1))
+            load(1, src, s0 + 1 / NCH, std::integral_constant<int, 1 / NCH>{}, std::integral_constant<int, 1 % NCH>{});
+        static_for<0, NSTEP>([&](auto qc) {
+            constexpr int q = decltype(qc)::value, t = q / NCH, kk = q % NCH, r = q % 3;
+            if constexpr (kk == 0 && !(DV & 8)) issue_w(s0 + t + DIST);   // its slot was last read at tap s - 3
+            if constexpr (LD(q + 2))
+                load((q + 2) % 3, src, s0 + (q + 2) / NCH, std::integral_constant<int, (q + 2) / NCH>{},
+                     std::integral_constant<int, (q + 2) % NCH>{});
+            constexpr int younger = ((LD(q + 1) ? 1 : 0) + (LD(q + 2) ? 1 : 0)) * (JN + FPW);
+            certify(std::integral_constant<int, r>{}, std::integral_constant<int, (younger > 15 ? 15 : younger)>{});   // lgkmcnt <= 15
+            // pin the order: the next steps' reads are in flight while this step's MFMAs issue
             __builtin_amdgcn_sched_barrier(0);
             if constexpr (!(DV & 2)) mma(r);
             __builtin_amdgcn_sched_barrier(0);
@@ -293,11 +325,14 @@ __global__ __launch_bounds__(64 * NW, 1) void k_smallnet(SmallNetArgs p) {
                 // drain them); the epilogue's image writes are complete before the barrier
                 // (DIST - 2) tiles of WPT loads each stay in flight
                 if constexpr (t == 8) {
+                    if (layer == 5) sm_stamp(p, 52);             // diagnostic: MFMAs of the layer issued
                     epilogue(layer, dst);
+                    if (layer == 5) sm_stamp(p, 53);             // epilogue issued
                     asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"i"((DIST - 2) * WPT) : "memory");
                 } else if constexpr (DV & 1) {
                     asm volatile("s_waitcnt vmcnt(%0)" ::"i"((DIST - 2) * WPT) : "memory");
                 } else {
+                    if (layer == 5) sm_stamp(p, 43 + t);         // tap t's MFMAs issued (before the wait)
                     asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"i"((DIST - 2) * WPT) : "memory");
                 }
             }
