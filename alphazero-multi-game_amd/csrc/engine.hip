@@ -554,6 +554,7 @@ struct az_search {
     int cur = 0;
     int* d_src_of = nullptr;
     float* d_batch = nullptr;       // gathered NHWC16 planes [G][A][16]
+    int* d_id = nullptr;            // AZ_EVAL_NET: [G + 1] = 0, 1, ..., G-1, G (identity batch map + its count)
     // AZ_EVAL_CALLBACK: host evaluator, leaf moves / lengths and host staging
     az_eval_fn eval_fn = nullptr; void* eval_user = nullptr;
     int* d_lmoves = nullptr; int* d_llen = nullptr;
@@ -660,22 +661,34 @@ int search_step(az_search* s, int mode) {
     if (s->c.eval_kind == AZ_EVAL_CALLBACK) {
         if (int r = host_evaluate(s)) return r;
     }
+    TreeDev tt = s->t;
     if (s->c.eval_kind == AZ_EVAL_NET) {
-        hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, st, s->t);
+        // The batch: in a simulation step with every game active, every game has a leaf and nearly
+        // all of them need the network (C3: 800 evaluations per 800-sim move), so the batch is the
+        // identity (slot = game; the few terminal / TT-hit leaves are computed and ignored: the
+        // net's outputs are batch-position independent) and k_scan's compaction is skipped.
+        // Otherwise (root steps, finished slots) k_scan compacts the leaves that need it.
+        bool identity = mode == MODE_SIM && s->d_id != nullptr;
+        for (int g = 0; identity && g < G; ++g) identity = s->active[g] != 0;
+        if (identity) {
+            tt.eval_slot = s->d_id; tt.eval_games = s->d_id; tt.n_eval = s->d_id + G;
+        } else {
+            hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, st, s->t);
+        }
         // the net's input stage builds the leaves' planes from their records (record eval_games[b])
         // where it can; otherwise a dense fp32 plane batch is built first
         const bool in_place = net_input_path(s->net) != NET_IN_GEMM;
-        const LeafRecs lr{s->t.leafrec, s->t.eval_games, s->t.game == GAME_GO, G};
-        if (!in_place) az_launch_rec_planes(s->t.leafrec, s->d_batch, s->t.eval_games, s->t.n_eval, lr.go, s->t.bs, G, st);
+        const LeafRecs lr{tt.leafrec, tt.eval_games, tt.game == GAME_GO, G};
+        if (!in_place) az_launch_rec_planes(tt.leafrec, s->d_batch, tt.eval_games, tt.n_eval, lr.go, tt.bs, G, st);
         const bool prof = s->net->prof;
         if (mode != MODE_SIM) s->net->prof = false;   // time only the simulation batches
-        int r = in_place ? net_forward(s->net, nullptr, G, s->t.n_eval, s->d_logits, s->d_value, st, &lr)
-                         : net_forward(s->net, s->d_batch, G, s->t.n_eval, s->d_logits, s->d_value, st);
+        int r = in_place ? net_forward(s->net, nullptr, G, tt.n_eval, s->d_logits, s->d_value, st, &lr)
+                         : net_forward(s->net, s->d_batch, G, tt.n_eval, s->d_logits, s->d_value, st);
         s->net->prof = prof;
         if (r) return r;
     }
     if (prof) HIPCHK(hipEventRecord(prof_event(s), st));
-    hipLaunchKernelGGL(k_expand_backup, dim3(G), dim3(64), 0, st, s->t, mode);
+    hipLaunchKernelGGL(k_expand_backup, dim3(G), dim3(64), 0, st, tt, mode);
     if (prof) { HIPCHK(hipEventRecord(prof_event(s), st)); s->prof_sampled += 1; }
     HIPCHK(hipGetLastError());
     return 0;
@@ -1149,12 +1162,18 @@ int az_search_create(az_engine* e, az_net* net, const az_search_cfg* c, az_searc
     if (c->eval_kind == AZ_EVAL_NET || c->eval_kind == AZ_EVAL_CALLBACK) {
         SA(s->d_batch, (size_t)G * A * 16); SA(s->d_logits, (size_t)G * NA); SA(s->d_value, G);
     }
+    if (c->eval_kind == AZ_EVAL_NET) SA(s->d_id, G + 1);
     if (c->eval_kind == AZ_EVAL_CALLBACK) { SA(s->d_lmoves, (size_t)G * AZ_DMAX); SA(s->d_llen, G); }
     SA(s->d_noise, (size_t)G * NA); SA(s->d_mask, G); SA(s->d_actions, G); SA(s->d_values, G); SA(s->d_probs, (size_t)G * NA);
     SA(s->d_cact, (size_t)G * NA); SA(s->d_nch, G); SA(s->d_term, G); SA(s->d_res, G); SA(s->d_games, G); SA(s->d_seed_ids, G); SA(s->d_temps, G);
 #undef SA
     if (r) { az_search_destroy(s); return r; }
     t.zpiece = zp; t.zplayer = zpl; t.fresh_order = fo; t.zko = zko;
+    if (s->d_id) {
+        std::vector<int> id(G + 1);
+        for (int i = 0; i <= G; ++i) id[i] = i;
+        HIPCHK(hipMemcpy(s->d_id, id.data(), (G + 1) * 4, hipMemcpyHostToDevice));
+    }
     if (go) {
         // GoState Zobrist features (go_state.cpp:48-51; ZobristHash::addFeature, zobrist_hash.cpp:58-70):
         // mt19937_64 seeded with std::hash<std::string> of the feature name
@@ -1215,7 +1234,7 @@ void az_search_destroy(az_search* s) {
                           (const void*)t.rko, (const void*)t.rpass, (const void*)t.rposh, (const void*)t.rnposh,
                           (const void*)t.zko, (const void*)s->d_lmoves, (const void*)s->d_llen,
                           (const void*)t.log_pol, (const void*)t.log_val, (const void*)t.log_planes, (const void*)t.log_n,
-                          (const void*)s->d_src_of, (const void*)s->d_batch, (const void*)s->d_logits,
+                          (const void*)s->d_src_of, (const void*)s->d_batch, (const void*)s->d_id, (const void*)s->d_logits,
                           (const void*)s->d_value, (const void*)s->d_noise, (const void*)s->d_mask, (const void*)s->d_actions,
                           (const void*)s->d_values, (const void*)s->d_probs, (const void*)s->d_cact, (const void*)s->d_nch,
                           (const void*)s->d_term, (const void*)s->d_res, (const void*)s->d_games, (const void*)s->d_seed_ids, (const void*)s->d_temps})
