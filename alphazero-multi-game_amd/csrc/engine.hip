@@ -27,6 +27,7 @@
 
 // kernels (tree_kernels.hip)
 void az_launch_select(const TreeDev& t, int mode, hipStream_t st);
+void az_launch_expand_select(const TreeDev& te, const TreeDev& ts, hipStream_t st);
 __global__ void k_scan(TreeDev t);
 __global__ void k_expand_backup(TreeDev t, int mode);
 __global__ void k_select_action(TreeDev t, int training, float temperature, const float* temps, int* actions, float* values, float* probs,
@@ -650,13 +651,15 @@ int host_evaluate(az_search* s) {
     return 0;
 }
 
-int search_step(az_search* s, int mode) {
+// pre: this step's selection was already issued (fused into the previous step's expansion);
+// fuse_next: issue this step's expansion fused with the next simulation step's selection.
+int search_step(az_search* s, int mode, bool pre = false, bool fuse_next = false) {
     hipStream_t st = s->e->stream;
     const int G = s->c.n_games;
     s->t.nd = s->arena[s->cur];
     const bool prof = s->prof && mode == MODE_SIM && s->prof_steps++ % prof_every() == 0;
     if (prof) HIPCHK(hipEventRecord(prof_event(s), st));
-    az_launch_select(s->t, mode, st);
+    if (!pre) az_launch_select(s->t, mode, st);
     if (prof) HIPCHK(hipEventRecord(prof_event(s), st));
     if (s->c.eval_kind == AZ_EVAL_CALLBACK) {
         if (int r = host_evaluate(s)) return r;
@@ -688,9 +691,26 @@ int search_step(az_search* s, int mode) {
         if (r) return r;
     }
     if (prof) HIPCHK(hipEventRecord(prof_event(s), st));
-    hipLaunchKernelGGL(k_expand_backup, dim3(G), dim3(64), 0, st, tt, mode);
+    if (fuse_next) az_launch_expand_select(tt, s->t, st);
+    else hipLaunchKernelGGL(k_expand_backup, dim3(G), dim3(64), 0, st, tt, mode);
     if (prof) { HIPCHK(hipEventRecord(prof_event(s), st)); s->prof_sampled += 1; }
     HIPCHK(hipGetLastError());
+    return 0;
+}
+
+// n simulation steps.  Step i's expansion and step i+1's selection share one launch
+// (k_expand_select) except around the profiled steps (their kernels are timed separately) and
+// with the host evaluator (which runs between the two).
+int search_sims(az_search* s, int n) {
+    const bool can_fuse = s->c.eval_kind != AZ_EVAL_CALLBACK;
+    bool pre = false;
+    for (int i = 0; i < n; ++i) {
+        const bool sampled = s->prof && s->prof_steps % prof_every() == 0;
+        const bool next_sampled = s->prof && (s->prof_steps + 1) % prof_every() == 0;
+        const bool fuse = can_fuse && i + 1 < n && !sampled && !next_sampled;
+        if (int r = search_step(s, MODE_SIM, pre, fuse)) return r;
+        pre = fuse;
+    }
     return 0;
 }
 
@@ -761,8 +781,7 @@ int search_run(az_search* s) {
     if (int r = search_step(s, MODE_ROOT_SEARCH)) return r;
     if (s->c.use_dirichlet_each_search)
         if (int r = search_noise(s, s->c.dirichlet_alpha, s->c.dirichlet_eps, nullptr)) return r;
-    for (int i = 0; i < s->c.num_simulations; ++i)
-        if (int r = search_step(s, MODE_SIM)) return r;
+    if (int r = search_sims(s, s->c.num_simulations)) return r;
     return check_err(s);
 }
 
@@ -1282,8 +1301,7 @@ int az_search_simulate(az_search* s, int n) {
     if (!s || n < 0) return az_fail(AZ_ERR_ARG, "bad argument");
     std::lock_guard<std::mutex> lk(s->mu);
     HIPCHK(hipSetDevice(s->e->device));
-    for (int i = 0; i < n; ++i)
-        if (int r = search_step(s, MODE_SIM)) return r;
+    if (int r = search_sims(s, n)) return r;
     return check_err(s);
 }
 

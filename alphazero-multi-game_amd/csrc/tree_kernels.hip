@@ -469,7 +469,7 @@ __device__ int go_legal(const TreeDev& t, int g, int lane, const uint8_t* b, con
 // full (N, W, VL, P and the child's own header first / cnt / flag / act) before the PUCT scores,
 // and the winner's record is broadcast from its lane, so the next level needs no header load.
 template <int IT>
-__global__ __launch_bounds__(64) void k_select(TreeDev t, int mode) {
+__device__ __forceinline__ void select_game(const TreeDev& t, int mode) {
     const int g = blockIdx.x;
     const int lane = threadIdx.x;
     __shared__ uint8_t board[AZ_MAXA];
@@ -722,6 +722,9 @@ __global__ __launch_bounds__(64) void k_select(TreeDev t, int mode) {
     tstamp(t, g, 0, 7);
 }
 
+template <int IT>
+__global__ __launch_bounds__(64) void k_select(TreeDev t, int mode) { select_game<IT>(t, mode); }
+
 extern "C" int az_diag_tree_stamps(unsigned long long* out, int n) {
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_tree_stamps), sizeof(unsigned long long) * (n < 128 ? n : 128)) == hipSuccess ? 0 : -1;
 }
@@ -775,7 +778,7 @@ __global__ __launch_bounds__(1024) void k_scan(TreeDev t) {
 // then the leaf's network outputs and the path nodes' statistics -- the second and last one.
 // The Gomoku leaf board is the root board plus the path moves (no Zobrist work: k_select stored
 // the leaf hash); Go replays its captures on lane 0 (go_build_leaf).
-__global__ __launch_bounds__(64) void k_expand_backup(TreeDev t, int mode) {
+__device__ __forceinline__ void expand_game(const TreeDev& t, int mode) {
     const int g = blockIdx.x;
     const int lane = threadIdx.x;
     __shared__ uint8_t board[AZ_MAXA];
@@ -1056,6 +1059,25 @@ __global__ __launch_bounds__(64) void k_expand_backup(TreeDev t, int mode) {
         if (sim) { cnt[CNT_SIMS] = c_sims + 1; cnt[CNT_BYTES_EXP] = c_bytes + kb; }
     }
     tstamp(t, g, 1, 7);
+}
+
+__global__ __launch_bounds__(64) void k_expand_backup(TreeDev t, int mode) { expand_game(t, mode); }
+
+// K3 of simulation step i and K1 of step i+1 in one launch: a game's expansion / backup and its
+// next selection are the same wave's consecutive work (no other game is involved), so one
+// kernel boundary per step goes (the wave's own global stores are visible to its later loads
+// after the block barrier's release / acquire).  te: step i's batch maps, ts: the search's.
+template <int IT>
+__global__ __launch_bounds__(64) void k_expand_select(TreeDev te, TreeDev ts) {
+    expand_game(te, MODE_SIM);
+    __syncthreads();
+    select_game<IT>(ts, MODE_SIM);
+}
+
+void az_launch_expand_select(const TreeDev& te, const TreeDev& ts, hipStream_t st) {
+    if (ts.NA <= 128) hipLaunchKernelGGL(k_expand_select<2>, dim3(ts.G), dim3(64), 0, st, te, ts);
+    else if (ts.NA <= 256) hipLaunchKernelGGL(k_expand_select<4>, dim3(ts.G), dim3(64), 0, st, te, ts);
+    else hipLaunchKernelGGL(k_expand_select<(AZ_MAXNA + 63) / 64>, dim3(ts.G), dim3(64), 0, st, te, ts);
 }
 
 // K4: visit distribution, action choice and root value per game.
