@@ -837,7 +837,7 @@ int search_apply_dev(az_search* s, int* terminal, int* result) {
     std::vector<int> acts(G);
     HIPCHK(hipMemcpyAsync(acts.data(), s->d_actions, G * 4, hipMemcpyDeviceToHost, st));
     hipLaunchKernelGGL(k_apply, dim3(G), dim3(64), 0, st, s->t, s->d_actions, s->d_term, s->d_res);
-    hipLaunchKernelGGL(k_compact, dim3(G), dim3(64), 0, st, s->t, s->arena[s->cur ^ 1], s->d_src_of);
+    hipLaunchKernelGGL(k_compact, dim3(G), dim3(256), 0, st, s->t, s->arena[s->cur ^ 1], s->d_src_of);
     HIPCHK(hipGetLastError());
     s->cur ^= 1;
     s->t.nd = s->arena[s->cur];

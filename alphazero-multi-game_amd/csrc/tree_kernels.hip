@@ -1232,16 +1232,25 @@ __global__ __launch_bounds__(64) void k_apply(TreeDev t, const int* actions, int
 }
 
 // K6: copy the subtree of the (new) root into the other arena, breadth first.
-__global__ __launch_bounds__(64) void k_compact(TreeDev t, Nodes dst, int* src_of) {
+// Subtree reuse: BFS copy of the new root's subtree into the other arena (children of a node stay
+// contiguous and in order; node k of the copy came from src_of[k]).  One 256-thread block per game
+// takes 256 queued nodes per round: a block prefix sum of their child counts places every child,
+// and all the round's children are copied in parallel, each thread finding its parent by binary
+// search over the prefix (one dependent round of loads per round instead of one per parent).
+__global__ __launch_bounds__(256) void k_compact(TreeDev t, Nodes dst, int* src_of) {
+    constexpr int NT = 256;
+    __shared__ int s_inc[NT];     // inclusive prefix of this round's child counts
+    __shared__ int s_fs[NT];      // first child (source arena) of each queued node
+    __shared__ int s_wsum[NT / 64];
     const int g = blockIdx.x;
-    const int lane = threadIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     if (g >= t.G) return;
     const size_t base = (size_t)g * t.ncap;
     GamePtrs s = game_nodes(t.nd, base);
     GamePtrs d = game_nodes(dst, base);
     int* so = src_of + base;
     const int root = t.rnode[g];
-    if (lane == 0) {
+    if (tid == 0) {
         d.N[0] = s.N[root]; d.W[0] = s.W[root]; d.VL[0] = s.VL[root]; d.P[0] = s.P[root];
         d.act[0] = s.act[root]; d.cnt[0] = s.cnt[root]; d.flag[0] = s.flag[root]; d.first[0] = -1;
         so[0] = root;
@@ -1249,34 +1258,43 @@ __global__ __launch_bounds__(64) void k_compact(TreeDev t, Nodes dst, int* src_o
     __syncthreads();
     int j = 0, top = 1;
     while (j < top) {
-        const int k = j + lane;
-        const bool valid = k < top;
+        const int m = min(NT, top - j);
+        const int k = j + tid;
+        const bool valid = tid < m;
         const int sn = valid ? so[k] : 0;
         const int nc = valid ? (int)s.cnt[sn] : 0;
-        const int incl = wave_incl_scan(nc, lane);
-        const int tot = __shfl(incl, 63);
-        const int nf = top + incl - nc;
-        if (valid) d.first[k] = nc ? nf : -1;
-        const int fsrc = valid && nc ? s.first[sn] : 0;
-        const int m = min(64, top - j);
-        for (int e = 0; e < m; ++e) {
-            const int ce = __shfl(nc, e);
-            if (ce == 0) continue;
-            const int fs = __shfl(fsrc, e);
-            const int fd = __shfl(nf, e);
-            if (fd + ce > t.ncap) { if (lane == 0) atomicOr(t.err, ERR_NODES); return; }
-            for (int i = lane; i < ce; i += 64) {
-                const int a = fs + i, b = fd + i;
-                d.N[b] = s.N[a]; d.W[b] = s.W[a]; d.VL[b] = s.VL[a]; d.P[b] = s.P[a];
-                d.act[b] = s.act[a]; d.cnt[b] = s.cnt[a]; d.flag[b] = s.flag[a]; d.first[b] = -1;
-                so[b] = a;
-            }
-        }
+        const int fs = valid && nc ? s.first[sn] : 0;
+        // block inclusive scan of nc
+        const int wincl = wave_incl_scan(nc, lane);
+        if (lane == 63) s_wsum[wave] = wincl;
         __syncthreads();
+        int off = 0;
+#pragma unroll
+        for (int w = 0; w < NT / 64; ++w) off += w < wave ? s_wsum[w] : 0;
+        const int incl = off + wincl;
+        s_inc[tid] = incl;
+        s_fs[tid] = fs;
+        const int tot = s_wsum[0] + s_wsum[1] + s_wsum[2] + s_wsum[3];
+        if (valid) d.first[k] = nc ? top + incl - nc : -1;
+        __syncthreads();
+        if (top + tot > t.ncap) { if (tid == 0) atomicOr(t.err, ERR_NODES); return; }
+        for (int c = tid; c < tot; c += NT) {
+            int lo = 0, hi = m - 1;                // smallest p with s_inc[p] > c
+            while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                if (s_inc[mid] > c) hi = mid; else lo = mid + 1;
+            }
+            const int ex = lo ? s_inc[lo - 1] : 0;
+            const int a = s_fs[lo] + (c - ex), b = top + c;
+            d.N[b] = s.N[a]; d.W[b] = s.W[a]; d.VL[b] = s.VL[a]; d.P[b] = s.P[a];
+            d.act[b] = s.act[a]; d.cnt[b] = s.cnt[a]; d.flag[b] = s.flag[a]; d.first[b] = -1;
+            so[b] = a;
+        }
+        __syncthreads();                           // so[] of this round visible to the next (same CU)
         j += m;
         top += tot;
     }
-    if (lane == 0) { t.rnode[g] = 0; t.atop[g] = top; }
+    if (tid == 0) { t.rnode[g] = 0; t.atop[g] = top; }
 }
 
 // releaseMemory(visitThreshold) (parallel_mcts.cpp:1481-1496; MCTSNode::pruneTree mcts_node.cpp:451-477):
