@@ -331,12 +331,27 @@ class ParallelMCTS:
         check(lib().az_selfplay_step(self.h, ctypes.byref(cfg), ctypes.byref(moves), ctypes.byref(evals)))
         return moves.value, evals.value
 
-    def stepMoves(self):
-        """MoveData of the last selfplayStep: [(slot, MoveData)] for every game that moved."""
+    def stepMoves(self, materialize=True):
+        """MoveData of the last selfplayStep: [(slot, MoveData)] for every game that moved.
+        materialize=False returns the engine's own records as they are (the C++-assembled
+        az_move_rec array, as a numpy structured view valid until the next step, and the slots)
+        without building Python objects."""
         mv = ctypes.POINTER(_lib_MoveRec)()
         sl = ctypes.POINTER(ctypes.c_int)()
         n = ctypes.c_int()
         check(lib().az_selfplay_step_moves(self.h, ctypes.byref(mv), ctypes.byref(sl), ctypes.byref(n)))
+        if not materialize:
+            if n.value == 0:
+                return None, None
+            import numpy as np
+            R = _lib_MoveRec
+            dt = np.dtype({"names": ["action", "value", "n_children", "policy", "child_actions", "thinking_time_ms"],
+                           "formats": ["<i4", "<f4", "<i4", "<u8", "<u8", "<i8"],
+                           "offsets": [R.action.offset, R.value.offset, R.n_children.offset, R.policy.offset,
+                                       R.child_actions.offset, R.thinking_time_ms.offset],
+                           "itemsize": ctypes.sizeof(R)})
+            raw = (ctypes.c_char * (n.value * ctypes.sizeof(R))).from_address(ctypes.addressof(mv.contents))
+            return np.frombuffer(raw, dtype=dt), np.ctypeslib.as_array(sl, shape=(n.value,))
         out = []
         for i in range(n.value):
             r = mv[i]

@@ -755,7 +755,7 @@ int search_noise(az_search* s, float alpha, float eps, const uint8_t* mask) {
             s->h_mask[g] = 1;
         }
     };
-    const int nt = std::max(1, std::min({host_threads(), G / 32}));
+    const int nt = std::max(1, std::min({host_threads(), G / 16}));
     if (nt == 1) {
         draw(0, G);
     } else {
