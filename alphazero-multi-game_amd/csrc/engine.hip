@@ -107,6 +107,8 @@ struct az_net {
     size_t act_elems = 0;   // elements of every 16-bit activation buffer before its zeroed tail
     size_t nparams = 0;
     Layer in, pconv, vconv, pfc, vfc1, vfc2;
+    Layer hconv;              // [pconv; vconv] as one 1x1 conv (2 HC outputs): both heads in one GEMM
+    float* hpv = nullptr;     // its output [B * P * P][2 HC] (policy channels, then value)
     std::vector<Layer> blk;   // 2 per block
     // activations (max_batch samples)
     float *x0 = nullptr, *h0 = nullptr, *h1 = nullptr, *t = nullptr, *pool = nullptr;
@@ -260,6 +262,7 @@ int net_load(az_net* n, const float* blob) {
     // policy head: 1x1 conv + BN, FC over the flattened (c, y, x) pooled map
     fold_conv(pc, HC, F, 1, F, d.conv_bias, W, b);
     if (int r = upload_layer(n->pconv, W, b, HC, F, 1, F, false)) return r;
+    std::vector<float> hW = W, hb = b;                 // the combined head conv, policy rows first
     auto fc_perm = [&](int out, int hc, int pp, std::vector<float>& Wt, std::vector<float>& bt) {
         // torch flattens NCHW (index c*pp + px); our pooled head map is [px][c].
         const float* w = pc.take((size_t)out * hc * pp);
@@ -274,6 +277,9 @@ int net_load(az_net* n, const float* blob) {
     if (int r = upload_layer(n->pfc, W, b, d.action_size, HC * PP, 1, HC * PP, false)) return r;
     fold_conv(pc, HC, F, 1, F, d.conv_bias, W, b);
     if (int r = upload_layer(n->vconv, W, b, HC, F, 1, F, false)) return r;
+    hW.insert(hW.end(), W.begin(), W.end());
+    hb.insert(hb.end(), b.begin(), b.end());
+    if (int r = upload_layer(n->hconv, hW, hb, 2 * HC, F, 1, F, false)) return r;
     fc_perm(d.fc_hidden, HC, PP, W, b);
     if (int r = upload_layer(n->vfc1, W, b, d.fc_hidden, HC * PP, 1, HC * PP, false)) return r;
     {
@@ -307,7 +313,8 @@ static int fc_splits(int B, int K) {
     return s;
 }
 
-int net_heads_fc(az_net* n, int B, const int* nb, float* logits, float* value, hipStream_t st);
+int net_heads_fc(az_net* n, int B, const int* nb, float* logits, float* value, hipStream_t st,
+                 const float* pp = nullptr, const float* vp = nullptr, int xs = 0);
 
 // How the forward reads its input planes: NET_IN_SMALL (k_smallnet), NET_IN_G8 (k_to_g8 + the
 // g8 input conv) -- both can build board b's planes from the search's leaf record gidx[b]
@@ -505,20 +512,30 @@ int net_forward(az_net* n, const float* x0, int B, const int* nb, float* logits,
     }
     if (ev1) HIPCHK(hipEventRecord(ev1, st));
     if (!g8) az_launch_pool(h, n->pool, B, H, W, F, P, nb, st);
-    az_launch_gemm_f32(gemm_args(n->pconv, n->pool, F, n->pp, d.head_channels, nullptr, B * PP, 1, 1, nb, PP), ACT_RELU, false, st);
-    az_launch_gemm_f32(gemm_args(n->vconv, n->pool, F, n->vp, d.head_channels, nullptr, B * PP, 1, 1, nb, PP), ACT_RELU, false, st);
+    const int HC = d.head_channels, HK = HC * PP;
+    if (HK % 32 == 0 && n->hpv) {
+        // both head 1x1 convs as one GEMM (2 HC outputs; every output is the same k-ordered fp32
+        // chain as in two launches), read by the FC heads with a 2 HC cell stride
+        az_launch_gemm_f32(gemm_args(n->hconv, n->pool, F, n->hpv, 2 * HC, nullptr, B * PP, 1, 1, nb, PP), ACT_RELU, false, st);
+        return net_heads_fc(n, B, nb, logits, value, st, n->hpv, n->hpv + HC, 2 * HC);
+    }
+    az_launch_gemm_f32(gemm_args(n->pconv, n->pool, F, n->pp, HC, nullptr, B * PP, 1, 1, nb, PP), ACT_RELU, false, st);
+    az_launch_gemm_f32(gemm_args(n->vconv, n->pool, F, n->vp, HC, nullptr, B * PP, 1, 1, nb, PP), ACT_RELU, false, st);
     return net_heads_fc(n, B, nb, logits, value, st);
 }
 
-// The FC layers of both heads from the head feature maps pp / vp ([B][P*P][HC]).
-int net_heads_fc(az_net* n, int B, const int* nb, float* logits, float* value, hipStream_t st) {
+// The FC layers of both heads from the head feature maps pp / vp ([B][P*P][HC]; cell stride xs,
+// default HC: pp / vp may be the two halves of the combined head-conv output).
+int net_heads_fc(az_net* n, int B, const int* nb, float* logits, float* value, hipStream_t st, const float* pp,
+                 const float* vp, int xs) {
     const az_net_desc& d = n->d;
     const int PP = n->P2;
     const int HK = d.head_channels * PP;
+    if (!pp) { pp = n->pp; vp = n->vp; xs = d.head_channels; }
     // Both FC heads: k_fc_heads (split-K partials of both FCs in one GEMM) + k_fc_finish (per board)
     if (HK % 32 == 0 && HK % 4 == 0) {
         FcHeadArgs fa{};
-        fa.pp = n->pp; fa.vp = n->vp;
+        fa.pp = pp; fa.vp = vp; fa.hc = d.head_channels; fa.xs = xs;
         fa.Wp = n->pfc.W; fa.bp = n->pfc.b; fa.Wv1 = n->vfc1.W; fa.bv1 = n->vfc1.b; fa.wv2 = n->vfc2.W; fa.bv2 = n->vfc2.b;
         fa.logits = logits; fa.hid = n->v1; fa.value = value;
         fa.part = n->ws; fa.m_limit = nb;
@@ -530,6 +547,7 @@ int net_heads_fc(az_net* n, int B, const int* nb, float* logits, float* value, h
     }
     // generic shapes: split-K partials (deterministic reductions); the value head's FC1 partials
     // are reduced, ReLU'd and dotted with FC2 by one kernel per board
+    if (xs != d.head_channels) return az_fail(AZ_ERR_ARG, "net_heads_fc: strided head maps need k_fc_heads");
     GemmArgs pf = gemm_args(n->pfc, n->pp, HK, logits, d.action_size, nullptr, B, 1, 1, nb, 1);
     GemmArgs v1 = gemm_args(n->vfc1, n->vp, HK, n->v1, d.fc_hidden, nullptr, B, 1, 1, nb, 1);
     const int splits = fc_splits(d.max_batch, HK);
@@ -942,6 +960,7 @@ int az_net_create(az_engine* e, const az_net_desc* d, az_net** out) {
     }
     A_(&n->pool, B * n->P2 * F);
     A_(&n->pp, B * n->P2 * d->head_channels); A_(&n->vp, B * n->P2 * d->head_channels);
+    A_(&n->hpv, B * n->P2 * 2 * d->head_channels);
     A_(&n->v1, B * d->fc_hidden);
     {   // split-K workspace: gemm_f32 partials, or k_fc_heads' [<= 16 slices][B padded to 64][64-column tiles]
         const size_t nc = (size_t)((d->action_size + 63) / 64 + (d->fc_hidden + 63) / 64) * 64;
@@ -962,10 +981,10 @@ void az_net_destroy(az_net* n) {
     if (!n) return;
     hipSetDevice(n->e->device);
     auto F = [](void* p) { if (p) hipFree(p); };
-    std::vector<Layer*> ls = {&n->in, &n->pconv, &n->vconv, &n->pfc, &n->vfc1, &n->vfc2};
+    std::vector<Layer*> ls = {&n->in, &n->pconv, &n->vconv, &n->hconv, &n->pfc, &n->vfc1, &n->vfc2};
     for (auto& l : n->blk) ls.push_back(&l);
     for (Layer* l : ls) { F(l->W); F(l->b); F(l->Whi); F(l->Wlo); F(l->Wh16); F(l->Wbk_bf); F(l->Wbk_h); }
-    for (void* p : {(void*)n->x0, (void*)n->h0, (void*)n->h1, (void*)n->t, (void*)n->pool, (void*)n->pp, (void*)n->vp,
+    for (void* p : {(void*)n->x0, (void*)n->h0, (void*)n->h1, (void*)n->t, (void*)n->pool, (void*)n->pp, (void*)n->vp, (void*)n->hpv,
                     (void*)n->v1, (void*)n->ws, (void*)n->logits, (void*)n->value, (void*)n->soft, (void*)n->in_nchw, (void*)n->d_nb,
                     (void*)n->hh[0], (void*)n->hh[1], (void*)n->hl[0], (void*)n->hl[1], (void*)n->th, (void*)n->tl,
                     (void*)n->zero, (void*)n->sm_W, (void*)n->sm_b})

@@ -76,6 +76,7 @@ struct FcHeadArgs {
     float* part;                                // split-K workspace [S][B64][NT * 64]
     const int* m_limit;
     int B, K, A, H, S;
+    int hc, xs;                                 // head channels; cell stride of pp / vp (xs == hc: contiguous [B][K])
 };
 int az_fc_heads_splits(int B, int K, int A, int H);
 void az_launch_fc_heads(const FcHeadArgs& a, hipStream_t st);

@@ -326,7 +326,9 @@ __global__ __launch_bounds__(256) void k_fc_heads(FcHeadArgs p) {
         for (int h = 0; h < 2; ++h) {
             const int r = tid >> 2, c4 = (tid & 3) + 4 * h, k = kc + 4 * c4;
             const int m = m0 + r, n = n0 + r;
-            ra[h] = m < mlim ? *reinterpret_cast<const f32x4n*>(X + (size_t)m * p.K + k) : f32x4n{0.f, 0.f, 0.f, 0.f};
+            // element k of board m's head map: cell k / hc, channel k % hc (cell stride xs)
+            const size_t xo = ((size_t)m * (p.K / p.hc) + k / p.hc) * p.xs + k % p.hc;
+            ra[h] = m < mlim ? *reinterpret_cast<const f32x4n*>(X + xo) : f32x4n{0.f, 0.f, 0.f, 0.f};
             rb[h] = n < NO ? *reinterpret_cast<const f32x4n*>(Wt + (size_t)n * p.K + k) : f32x4n{0.f, 0.f, 0.f, 0.f};
         }
     };
