@@ -71,14 +71,40 @@ def gomoku_net_desc(board_size=15, channels=256, blocks=20, precision=AZ_PREC_F3
                    residual, conv_bias, precision, max_batch)
 
 
+def randwire_net_desc(board_size=15, channels=128, blocks=20, in_planes=11, max_batch=256, action_size=None):
+    """DDWRandWireResNet(in_planes, action_size, channels, blocks) of src/nn/ddw_randwire_resnet.cpp:387-468
+    (the reference's defaults: 128 channels, 20 blocks; heads 32 channels, 8x8 pool, 256 hidden)."""
+    return NetDesc(board_size, in_planes, channels, blocks, action_size or board_size * board_size, 32,
+                   min(8, board_size), 256, 0, 0, AZ_PREC_F32, max_batch)
+
+
+def createDDWRandWireResNet(engine, input_channels, output_size, channels=128, num_blocks=20, board_size=15,
+                            max_batch=256):
+    """TorchNeuralNetwork::createDDWRandWireResNet (torch_neural_network.cpp:799-814) on the device engine."""
+    d = randwire_net_desc(board_size, channels, num_blocks, input_channels, max_batch, output_size)
+    return HipNeuralNetwork(engine, d, randwire=True)
+
+
+def randwire_graph(block):
+    """Host-side wiring of rand-wire block `block` (az_randwire_graph): dict like the reference dump."""
+    order, topo, ins, outs = ((ctypes.c_int * 32)() for _ in range(4))
+    nin, nout = ctypes.c_int(), ctypes.c_int()
+    off = (ctypes.c_int * 33)()
+    preds = (ctypes.c_int * 256)()
+    check(lib().az_randwire_graph(block, order, topo, ins, ctypes.byref(nin), outs, ctypes.byref(nout), off, preds, 256))
+    return {"nodes": list(order), "topo": list(topo), "input_nodes": list(ins)[:nin.value],
+            "output_nodes": list(outs)[:nout.value], "preds": {v: list(preds[off[v]:off[v + 1]]) for v in range(32)}}
+
+
 class HipNeuralNetwork:
     """NeuralNetwork plugin on the MI355X ConvNet kernels."""
 
-    def __init__(self, engine, desc):
+    def __init__(self, engine, desc, randwire=False):
         self.engine = engine
         self.desc = desc
         h = ctypes.c_void_p()
-        check(lib().az_net_create(engine.h, ctypes.byref(desc), ctypes.byref(h)))
+        create = lib().az_net_create_randwire if randwire else lib().az_net_create
+        check(create(engine.h, ctypes.byref(desc), ctypes.byref(h)))
         self.h = h
         n = ctypes.c_size_t()
         check(lib().az_net_num_params(self.h, ctypes.byref(n)))

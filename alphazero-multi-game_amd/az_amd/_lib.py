@@ -49,6 +49,9 @@ EXPORTS = {
     "az_engine_destroy": (None, [vp]),
     "az_engine_device_name": (c_int, [vp, ctypes.c_char_p, c_int]),
     "az_net_create": (c_int, [vp, P(NetDesc), P(vp)]),
+    "az_net_create_randwire": (c_int, [vp, P(NetDesc), P(vp)]),
+    "az_randwire_graph": (c_int, [c_int, P(c_int), P(c_int), P(c_int), P(c_int), P(c_int), P(c_int), P(c_int), P(c_int),
+                                  c_int]),
     "az_net_destroy": (None, [vp]),
     "az_net_num_params": (c_int, [vp, P(c_size_t)]),
     "az_net_load_weights": (c_int, [vp, P(c_float), c_size_t]),

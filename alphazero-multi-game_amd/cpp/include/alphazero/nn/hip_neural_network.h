@@ -18,6 +18,7 @@ struct NetShape {
     int boardSize = 15, inPlanes = 11, channels = 256, blocks = 20, actionSize = 225;
     int headChannels = 32, pool = 8, fcHidden = 256, residual = 1, convBias = 0;
     int precision = AZ_PREC_FP16, maxBatch = 2048;
+    int randWire = 0;   // 1: DDWRandWireResNet trunk (az_net_create_randwire; not part of the .azw header)
 };
 
 class HipNeuralNetwork : public NeuralNetwork {
@@ -32,6 +33,12 @@ class HipNeuralNetwork : public NeuralNetwork {
     void setPrecision(int precision);
     // .azw file: "AZW1", 12 int32 NetShape fields, uint64 count, float32[count]
     static std::unique_ptr<HipNeuralNetwork> load(const std::string& path, int device = -1);
+    // TorchNeuralNetwork::createDDWRandWireResNet (torch_neural_network.cpp:799-814): the
+    // DDW-RandWire net (ddw_randwire_resnet.cpp:387-468) on the device engine, fp32 path
+    static std::unique_ptr<HipNeuralNetwork> createDDWRandWireResNet(int inputChannels, int outputSize,
+                                                                     int channels = 128, int numBlocks = 20,
+                                                                     int boardSize = 15, int maxBatch = 256,
+                                                                     int device = -1);
     void save(const std::string& path) const;
 
     std::pair<std::vector<float>, float> predict(const core::IGameState& state) override;

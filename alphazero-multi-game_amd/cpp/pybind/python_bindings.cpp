@@ -196,6 +196,16 @@ PYBIND11_MODULE(_alphazero_cpp, m) {
         .def("setPrecision", &nn::HipNeuralNetwork::setPrecision)
         .def("save", &nn::HipNeuralNetwork::save)
         .def_static("load", &nn::HipNeuralNetwork::load, py::arg("path"), py::arg("device") = -1);
+    // TorchNeuralNetwork::createDDWRandWireResNet / DDWRandWireResNetCpp(input_channels, output_size,
+    // channels=128, num_blocks=20) (reference python_bindings.cpp:168-173) on the device engine
+    m.def("createDDWRandWireResNet",
+          [](int input_channels, int output_size, int channels, int num_blocks, int board_size, int max_batch,
+             int device) {
+              return nn::HipNeuralNetwork::createDDWRandWireResNet(input_channels, output_size, channels, num_blocks,
+                                                                   board_size, max_batch, device);
+          },
+          py::arg("input_channels"), py::arg("output_size"), py::arg("channels") = 128, py::arg("num_blocks") = 20,
+          py::arg("board_size") = 15, py::arg("max_batch") = 256, py::arg("device") = -1);
 
     py::class_<nn::RandomPolicyNetwork, nn::NeuralNetwork>(m, "RandomPolicyNetwork")
         .def(py::init<core::GameType, int, unsigned int>(), py::arg("gameType"), py::arg("boardSize") = 0,

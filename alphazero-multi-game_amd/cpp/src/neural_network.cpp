@@ -1,5 +1,6 @@
 // NeuralNetwork plugins of the host API: HipNeuralNetwork (the MI355X ConvNet behind
 // az_net_*), RandomPolicyNetwork, the factory, and the per-device engine registry.
+#include <algorithm>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -46,7 +47,8 @@ static az_net_desc toDesc(const NetShape& s) {
 HipNeuralNetwork::HipNeuralNetwork(const NetShape& shape, int device) : shape_(shape) {
     eng_ = engineForDevice(device);
     az_net_desc d = toDesc(shape_);
-    check(az_net_create(eng_, &d, &net_), "az_net_create");
+    if (shape_.randWire) check(az_net_create_randwire(eng_, &d, &net_), "az_net_create_randwire");
+    else check(az_net_create(eng_, &d, &net_), "az_net_create");
     check(az_net_num_params(net_, &params_), "az_net_num_params");
 }
 
@@ -93,7 +95,18 @@ std::unique_ptr<HipNeuralNetwork> HipNeuralNetwork::load(const std::string& path
     return net;
 }
 
+std::unique_ptr<HipNeuralNetwork> HipNeuralNetwork::createDDWRandWireResNet(int inputChannels, int outputSize,
+                                                                           int channels, int numBlocks, int boardSize,
+                                                                           int maxBatch, int device) {
+    NetShape s;
+    s.boardSize = boardSize; s.inPlanes = inputChannels; s.channels = channels; s.blocks = numBlocks;
+    s.actionSize = outputSize; s.headChannels = 32; s.pool = std::min(8, boardSize); s.fcHidden = 256;
+    s.residual = 0; s.convBias = 0; s.precision = AZ_PREC_F32; s.maxBatch = maxBatch; s.randWire = 1;
+    return std::make_unique<HipNeuralNetwork>(s, device);
+}
+
 void HipNeuralNetwork::save(const std::string& path) const {
+    if (shape_.randWire) throw std::runtime_error("save: the .azw header has no rand-wire field; keep the blob");
     if (blob_.empty()) throw std::runtime_error("save: weights were not loaded from a blob");
     std::ofstream f(path, std::ios::binary);
     const NetShape& s = shape_;

@@ -24,6 +24,7 @@
 #include "net.h"
 #include "tree.h"
 #include "leaf_planes.h"
+#include "randwire.h"
 
 // kernels (tree_kernels.hip)
 void az_launch_select(const TreeDev& t, int mode, hipStream_t st);
@@ -99,6 +100,18 @@ struct Layer {            // one implicit-GEMM layer, BN folded
     int N = 0, K = 0, Kpad = 0, taps = 1, C = 0;
 };
 
+// One DDW-RandWire node (row f4): its router (only used with >1 predecessors), the residual
+// block's two 3x3 convs (BN folded) and the SE block's two linear layers.
+struct RwNode {
+    Layer router, c1, c2;
+    float *w1 = nullptr, *b1 = nullptr, *w2 = nullptr, *b2 = nullptr;   // SE: [R][C], [R], [C][R], [C]
+};
+struct RwBlock {
+    azrw::Plan plan;
+    std::vector<RwNode> node;   // by node id
+    Layer out_router;           // when the block has more than one sink
+};
+
 struct az_net {
     az_engine* e = nullptr;
     az_net_desc d{};
@@ -121,6 +134,11 @@ struct az_net {
     // k_smallnet (64-filter fp16 nets): [2*blocks+1][9][64][64] fp16 trunk weights incl. the input conv, biases
     uint16_t* sm_W = nullptr;
     float* sm_b = nullptr;
+    // DDW-RandWire trunk (az_net_create_randwire): d.blocks rand-wire blocks of 32 nodes
+    bool rw = false;
+    std::vector<RwBlock> rwb;
+    std::vector<float*> rw_out;       // node outputs [B*HW][F], by node id
+    float *rw_t2 = nullptr, *rw_in = nullptr;   // conv2 output, router output
     bool loaded = false;
     std::vector<float> host_blob;   // canonical blob of the loaded weights (az_net_get_weights)
     // profiling: HIP events bracketing the 3x3 trunk of every forward (on the launch stream)
@@ -160,6 +178,30 @@ size_t count_params(const az_net_desc& d) {
     n += (size_t)d.fc_hidden * HC * PP + d.fc_hidden;
     n += (size_t)d.fc_hidden + 1;
     return n;
+}
+
+// Blob layout of a rand-wire net: (count, init kind, fan_in) per state entry in the reference's
+// state_dict order (oracle/randwire_oracle.param_shapes; kinds as az_net_init_random).
+struct PSpec { size_t n; int kind; int fan_in; };
+std::vector<PSpec> rw_spec(const az_net_desc& d, const std::vector<RwBlock>& rwb) {
+    const int C = d.channels, R = C / 16, HC = d.head_channels, PP = d.pool * d.pool;
+    std::vector<PSpec> s;
+    auto conv = [&](int co, int ci, int k) { s.push_back({(size_t)co * ci * k * k, 0, ci * k * k}); };
+    auto bn = [&](int co) { for (int kd = 2; kd <= 5; ++kd) s.push_back({(size_t)co, kd, 1}); };
+    auto lin = [&](int o, int i) { s.push_back({(size_t)o * i, 0, i}); s.push_back({(size_t)o, 1, i}); };
+    conv(C, d.in_planes, 3); bn(C);
+    for (const RwBlock& b : rwb) {
+        for (int v : b.plan.order)
+            if (!b.plan.preds[v].empty()) { conv(C, (int)b.plan.preds[v].size() * C, 1); bn(C); }
+        for (size_t k = 0; k < b.plan.order.size(); ++k) {
+            conv(C, C, 3); bn(C); conv(C, C, 3); bn(C);
+            lin(R, C); lin(C, R);
+        }
+        if (b.plan.outputs.size() > 1) { conv(C, (int)b.plan.outputs.size() * C, 1); bn(C); }
+    }
+    conv(HC, C, 1); bn(HC); lin(d.action_size, HC * PP);
+    conv(HC, C, 1); bn(HC); lin(d.fc_hidden, HC * PP); lin(1, d.fc_hidden);
+    return s;
 }
 
 uint16_t f2bf(float f) {   // round to nearest even
@@ -223,6 +265,8 @@ int upload_layer(Layer& L, const std::vector<float>& W, const std::vector<float>
     return 0;
 }
 
+int load_heads(az_net* n, ParamCursor& pc);
+
 int net_load(az_net* n, const float* blob) {
     const az_net_desc& d = n->d;
     ParamCursor pc{blob};
@@ -259,7 +303,17 @@ int net_load(az_net* n, const float* blob) {
         HIPCHK(hipMemcpy(n->sm_W, smw.data(), smw.size() * 2, hipMemcpyHostToDevice));
         HIPCHK(hipMemcpy(n->sm_b, smb.data(), smb.size() * 4, hipMemcpyHostToDevice));
     }
-    // policy head: 1x1 conv + BN, FC over the flattened (c, y, x) pooled map
+    if (int r = load_heads(n, pc)) return r;
+    if (pc.off != n->nparams) return az_fail(AZ_ERR_ARG, "parameter blob size mismatch (%zu vs %zu)", pc.off, n->nparams);
+    n->loaded = true;
+    return 0;
+}
+
+// policy head: 1x1 conv + BN, FC over the flattened (c, y, x) pooled map; value head likewise
+int load_heads(az_net* n, ParamCursor& pc) {
+    const az_net_desc& d = n->d;
+    const int F = d.channels, HC = d.head_channels, PP = d.pool * d.pool;
+    std::vector<float> W, b;
     fold_conv(pc, HC, F, 1, F, d.conv_bias, W, b);
     if (int r = upload_layer(n->pconv, W, b, HC, F, 1, F, false)) return r;
     std::vector<float> hW = W, hb = b;                 // the combined head conv, policy rows first
@@ -289,6 +343,49 @@ int net_load(az_net* n, const float* blob) {
         b.assign(bb, bb + 1);
         if (int r = upload_layer(n->vfc2, W, b, 1, d.fc_hidden, 1, d.fc_hidden, false)) return r;
     }
+    return 0;
+}
+
+// DDW-RandWire blob (rw_spec order): input conv, per block the routers (nodes() order, in-degree
+// > 0), the nodes' residual blocks incl. SE, the output router; then the heads.
+int net_load_rw(az_net* n, const float* blob) {
+    const az_net_desc& d = n->d;
+    const int F = d.channels, R = F / 16;
+    ParamCursor pc{blob};
+    std::vector<float> W, b;
+    fold_conv(pc, F, d.in_planes, 3, n->cin_pad, false, W, b);
+    if (int r = upload_layer(n->in, W, b, F, 9 * n->cin_pad, 9, n->cin_pad, false)) return r;
+    auto raw = [&](float** dst, size_t cnt) -> int {
+        if (!*dst) DALLOC(*dst, cnt);
+        HIPCHK(hipMemcpy(*dst, pc.take(cnt), cnt * 4, hipMemcpyHostToDevice));
+        return 0;
+    };
+    for (RwBlock& blk : n->rwb) {
+        const azrw::Plan& pl = blk.plan;
+        for (int v : pl.order) {
+            const int deg = (int)pl.preds[v].size();
+            if (!deg) continue;
+            fold_conv(pc, F, deg * F, 1, deg * F, false, W, b);
+            if (int r = upload_layer(blk.node[v].router, W, b, F, deg * F, 1, deg * F, false)) return r;
+        }
+        for (int v : pl.order) {
+            RwNode& nd = blk.node[v];
+            fold_conv(pc, F, F, 3, F, false, W, b);
+            if (int r = upload_layer(nd.c1, W, b, F, 9 * F, 9, F, false)) return r;
+            fold_conv(pc, F, F, 3, F, false, W, b);
+            if (int r = upload_layer(nd.c2, W, b, F, 9 * F, 9, F, false)) return r;
+            if (int r = raw(&nd.w1, (size_t)R * F)) return r;
+            if (int r = raw(&nd.b1, R)) return r;
+            if (int r = raw(&nd.w2, (size_t)F * R)) return r;
+            if (int r = raw(&nd.b2, F)) return r;
+        }
+        const int no = (int)pl.outputs.size();
+        if (no > 1) {
+            fold_conv(pc, F, no * F, 1, no * F, false, W, b);
+            if (int r = upload_layer(blk.out_router, W, b, F, no * F, 1, no * F, false)) return r;
+        }
+    }
+    if (int r = load_heads(n, pc)) return r;
     if (pc.off != n->nparams) return az_fail(AZ_ERR_ARG, "parameter blob size mismatch (%zu vs %zu)", pc.off, n->nparams);
     n->loaded = true;
     return 0;
@@ -334,6 +431,62 @@ int net_input_path(const az_net* n) {
 struct LeafRecs {                 // the search's leaf records: sample b = record gidx[b] (n records)
     const uint8_t* rec; const int* gidx; int go; int n;
 };
+
+// Router of a rand-wire node: relu(BN(conv1x1(concat(ins)))) as one K-slice GEMM per input
+// (K = F each, weight columns [j F, (j+1) F) of the folded [F][deg F] matrix), accumulated in
+// place; bias and ReLU on the last slice.
+void rw_router(const az_net* n, const Layer& L, const std::vector<const float*>& ins, float* out, int rows, const int* nb,
+               hipStream_t st) {
+    const int F = n->d.channels, H = n->d.board_size;
+    for (size_t j = 0; j < ins.size(); ++j) {
+        const bool last = j + 1 == ins.size();
+        GemmArgs p{};
+        p.A = ins[j]; p.lda = F; p.B = L.W + j * F; p.ldb = L.K; p.C = out; p.ldc = F;
+        p.bias = last ? L.b : nullptr; p.res = j ? out : nullptr;
+        p.M = rows; p.N = F; p.K = F; p.Kpad = (F + 31) / 32 * 32; p.taps = 1; p.Cch = F; p.H = H; p.W = H;
+        p.m_limit = nb; p.rows_per_sample = n->HW;
+        az_launch_gemm_f32(p, last ? ACT_RELU : ACT_NONE, j > 0, st);
+    }
+}
+
+// DDW-RandWire trunk (ddw_randwire_resnet.cpp:321-384 per block): input nodes on the block input,
+// the others in topological order on their router's output (or their single predecessor's
+// output), the block output (output router or the single sink) into the h0 / h1 ping-pong.
+float* rw_trunk(az_net* n, int B, const int* nb, hipStream_t st) {
+    const az_net_desc& d = n->d;
+    const int F = d.channels, H = d.board_size, HW = n->HW, rows = B * HW, R = F / 16;
+    float* x = n->h0;
+    std::vector<const float*> ins;
+    for (const RwBlock& blk : n->rwb) {
+        const azrw::Plan& pl = blk.plan;
+        auto node = [&](int v, const float* in) {
+            const RwNode& nd = blk.node[v];
+            az_launch_gemm_f32(gemm_args(nd.c1, in, F, n->t, F, nullptr, rows, H, H, nb, HW), ACT_RELU, false, st);
+            az_launch_gemm_f32(gemm_args(nd.c2, n->t, F, n->rw_t2, F, nullptr, rows, H, H, nb, HW), ACT_NONE, false, st);
+            az_launch_se_residual(n->rw_t2, in, n->rw_out[v], nd.w1, nd.b1, nd.w2, nd.b2, B, HW, F, R, nb, st);
+        };
+        for (int v : pl.inputs) node(v, x);
+        for (int v : pl.topo) {
+            const auto& pr = pl.preds[v];
+            if (pr.empty() || std::find(pl.inputs.begin(), pl.inputs.end(), v) != pl.inputs.end()) continue;
+            if (pr.size() == 1) { node(v, n->rw_out[pr[0]]); continue; }
+            ins.clear();
+            for (int u : pr) ins.push_back(n->rw_out[u]);
+            rw_router(n, blk.node[v].router, ins, n->rw_in, rows, nb, st);
+            node(v, n->rw_in);
+        }
+        float* y = x == n->h0 ? n->h1 : n->h0;
+        if (pl.outputs.size() > 1) {
+            ins.clear();
+            for (int u : pl.outputs) ins.push_back(n->rw_out[u]);
+            rw_router(n, blk.out_router, ins, y, rows, nb, st);
+        } else {
+            (void)hipMemcpyAsync(y, n->rw_out[pl.outputs[0]], (size_t)rows * F * 4, hipMemcpyDeviceToDevice, st);
+        }
+        x = y;
+    }
+    return x;
+}
 
 // Forward of B samples (B = capacity; *nb = active samples, device side) from the
 // NHWC16 input x0 -> logits [B][A], value [B].  lr (optional; only where
@@ -428,7 +581,9 @@ int net_forward(az_net* n, const float* x0, int B, const int* nb, float* logits,
         n->evused += 2;
         HIPCHK(hipEventRecord(ev0, st));
     }
-    if (!bf) {
+    if (n->rw) {
+        h = rw_trunk(n, B, nb, st);
+    } else if (!bf) {
         for (int i = 0; i < d.blocks; ++i) {
             az_launch_gemm_f32(gemm_args(n->blk[2 * i], h, F, n->t, F, nullptr, rows, H, W, nb, HW), ACT_RELU, false, st);
             az_launch_gemm_f32(gemm_args(n->blk[2 * i + 1], n->t, F, other, F, d.residual ? h : nullptr, rows, H, W, nb, HW),
@@ -922,7 +1077,7 @@ static int check_precision(const az_net_desc& d, int precision) {
     return 0;
 }
 
-int az_net_create(az_engine* e, const az_net_desc* d, az_net** out) {
+static int net_create(az_engine* e, const az_net_desc* d, az_net** out, bool rw) {
     if (!e || !d || !out) return az_fail(AZ_ERR_ARG, "null argument");
     if (d->board_size < 2 || d->board_size * d->board_size > AZ_MAXA || d->in_planes < 1 || d->in_planes > 128 ||
         d->channels < 4 || d->channels % 4 || d->blocks < 0 || d->action_size < 1 || d->action_size > 8192 ||
@@ -941,7 +1096,18 @@ int az_net_create(az_engine* e, const az_net_desc* d, az_net** out) {
     // pad to 32 so the v6 conv takes the input layer as whole 32-channel chunks
     n->cin_pad = (d->in_planes + 15) / 16 * 16;
     if (n->cin_pad > 16 && d->channels % 128 == 0) n->cin_pad = (d->in_planes + 31) / 32 * 32;
-    n->nparams = count_params(*d);
+    n->rw = rw;
+    if (rw) {
+        n->rwb.resize(d->blocks);
+        for (int i = 0; i < d->blocks; ++i) {
+            n->rwb[i].plan = azrw::plan(i);
+            n->rwb[i].node.resize(n->rwb[i].plan.preds.size());
+        }
+        n->nparams = 0;
+        for (const PSpec& ps : rw_spec(*d, n->rwb)) n->nparams += ps.n;
+    } else {
+        n->nparams = count_params(*d);
+    }
     const size_t B = d->max_batch, rows = B * n->HW, F = d->channels;
     n->act_elems = rows * F;
     int r = 0;
@@ -968,6 +1134,11 @@ int az_net_create(az_engine* e, const az_net_desc* d, az_net** out) {
     }
     A_(&n->logits, B * d->action_size); A_(&n->value, B); A_(&n->soft, B * d->action_size);
     A_(&n->in_nchw, B * d->in_planes * n->HW);
+    if (rw) {
+        n->rw_out.assign(n->rwb.empty() ? 0 : n->rwb[0].node.size(), nullptr);
+        for (float*& p : n->rw_out) A_(&p, rows * F);
+        A_(&n->rw_t2, rows * F); A_(&n->rw_in, rows * F);
+    }
     if (!r) r = dalloc(&n->d_nb, 1);
     if (!r) r = dalloc(&n->zero, 128);
     if (!r && hipMemset(n->zero, 0, 256) != hipSuccess) r = az_fail(AZ_ERR_HIP, "memset");
@@ -977,12 +1148,56 @@ int az_net_create(az_engine* e, const az_net_desc* d, az_net** out) {
     return 0;
 }
 
+int az_net_create(az_engine* e, const az_net_desc* d, az_net** out) { return net_create(e, d, out, false); }
+
+int az_net_create_randwire(az_engine* e, const az_net_desc* d, az_net** out) {
+    if (!d) return az_fail(AZ_ERR_ARG, "null argument");
+    if (d->precision != AZ_PREC_F32) return az_fail(AZ_ERR_ARG, "rand-wire nets run the fp32 path (AZ_PREC_F32)");
+    if (d->conv_bias) return az_fail(AZ_ERR_ARG, "rand-wire convolutions carry no bias (conv_bias = 0)");
+    if (d->channels % 16 || d->channels > 1024) return az_fail(AZ_ERR_ARG, "rand-wire channels: a multiple of 16, <= 1024");
+    if (d->pool != std::min(8, d->board_size)) return az_fail(AZ_ERR_ARG, "rand-wire heads pool to min(8, board)");
+    return net_create(e, d, out, true);
+}
+
+int az_randwire_graph(int block, int* order, int* topo, int* inputs, int* n_inputs, int* outputs, int* n_outputs,
+                      int* pred_off, int* preds, int preds_cap) {
+    if (block < 0 || !order || !topo || !inputs || !n_inputs || !outputs || !n_outputs || !pred_off || !preds)
+        return az_fail(AZ_ERR_ARG, "null argument / negative block");
+    const azrw::Plan pl = azrw::plan(block);
+    const int nn = (int)pl.order.size();
+    std::copy(pl.order.begin(), pl.order.end(), order);
+    std::copy(pl.topo.begin(), pl.topo.end(), topo);
+    std::copy(pl.inputs.begin(), pl.inputs.end(), inputs);
+    std::copy(pl.outputs.begin(), pl.outputs.end(), outputs);
+    *n_inputs = (int)pl.inputs.size();
+    *n_outputs = (int)pl.outputs.size();
+    int k = 0;
+    for (int v = 0; v < nn; ++v) {
+        pred_off[v] = k;
+        for (int u : pl.preds[v]) {
+            if (k >= preds_cap) return az_fail(AZ_ERR_CAPACITY, "preds_cap %d too small", preds_cap);
+            preds[k++] = u;
+        }
+    }
+    pred_off[nn] = k;
+    return 0;
+}
+
 void az_net_destroy(az_net* n) {
     if (!n) return;
     hipSetDevice(n->e->device);
     auto F = [](void* p) { if (p) hipFree(p); };
     std::vector<Layer*> ls = {&n->in, &n->pconv, &n->vconv, &n->hconv, &n->pfc, &n->vfc1, &n->vfc2};
     for (auto& l : n->blk) ls.push_back(&l);
+    for (auto& blk : n->rwb) {
+        ls.push_back(&blk.out_router);
+        for (auto& nd : blk.node) {
+            ls.push_back(&nd.router); ls.push_back(&nd.c1); ls.push_back(&nd.c2);
+            F(nd.w1); F(nd.b1); F(nd.w2); F(nd.b2);
+        }
+    }
+    for (float* p : n->rw_out) F(p);
+    F(n->rw_t2); F(n->rw_in);
     for (Layer* l : ls) { F(l->W); F(l->b); F(l->Whi); F(l->Wlo); F(l->Wh16); F(l->Wbk_bf); F(l->Wbk_h); }
     for (void* p : {(void*)n->x0, (void*)n->h0, (void*)n->h1, (void*)n->t, (void*)n->pool, (void*)n->pp, (void*)n->vp, (void*)n->hpv,
                     (void*)n->v1, (void*)n->ws, (void*)n->logits, (void*)n->value, (void*)n->soft, (void*)n->in_nchw, (void*)n->d_nb,
@@ -1003,7 +1218,7 @@ int az_net_load_weights(az_net* n, const float* blob, size_t count) {
     if (count != n->nparams) return az_fail(AZ_ERR_ARG, "expected %zu parameters, got %zu", n->nparams, count);
     std::lock_guard<std::mutex> lk(n->mu);
     HIPCHK(hipSetDevice(n->e->device));
-    if (int r = net_load(n, blob)) return r;
+    if (int r = n->rw ? net_load_rw(n, blob) : net_load(n, blob)) return r;
     n->host_blob.assign(blob, blob + count);
     return 0;
 }
@@ -1043,6 +1258,11 @@ int az_net_init_random(az_net* n, uint64_t seed) {
         off += cnt;
         ++tensor;
     };
+    if (n->rw) {
+        for (const PSpec& ps : rw_spec(d, n->rwb)) fill(ps.n, ps.kind, ps.fan_in);
+        if (off != n->nparams) return az_fail(AZ_ERR_STATE, "init size mismatch");
+        return az_net_load_weights(n, blob.data(), blob.size());
+    }
     const int F = d.channels, HC = d.head_channels, PP = d.pool * d.pool;
     auto conv = [&](int co, int ci, int k) {
         fill((size_t)co * ci * k * k, 0, ci * k * k);
@@ -1062,6 +1282,7 @@ int az_net_init_random(az_net* n, uint64_t seed) {
 
 int az_net_set_precision(az_net* n, int precision) {
     if (!n) return az_fail(AZ_ERR_ARG, "null net");
+    if (n->rw && precision != AZ_PREC_F32) return az_fail(AZ_ERR_ARG, "rand-wire nets run the fp32 path (AZ_PREC_F32)");
     if (int r = check_precision(n->d, precision)) return r;
     n->d.precision = precision;
     return 0;

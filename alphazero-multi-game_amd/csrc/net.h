@@ -85,3 +85,7 @@ void az_launch_value_head(const float* part, int splits, const float* b1, const 
 void az_launch_pool(const float* in, float* out, int B, int H, int W, int C, int P, const int* m_limit, hipStream_t st);
 void az_launch_pack_input(const float* in, float* out, int B, int Cin, int HW, int Cp, hipStream_t st);
 void az_launch_softmax_rows(const float* logits, float* out, int B, int A, hipStream_t st);
+
+// DDW-RandWire node tail: out = relu(y * SE(y) + x) (k_se_residual; C % 16 == 0, C <= 1024, R = C / 16 <= 64)
+void az_launch_se_residual(const float* y, const float* x, float* out, const float* W1, const float* b1, const float* W2,
+                           const float* b2, int B, int HW, int C, int R, const int* m_limit, hipStream_t st);

@@ -194,6 +194,54 @@ __global__ __launch_bounds__(256) void gemm_f32(GemmArgs p) {
         }
 }
 
+// Squeeze-and-excitation + residual + ReLU of a DDW-RandWire node (row f4;
+// ddw_randwire_resnet.cpp:10-32 SEBlock, :53-61 ResidualBlock::forward):
+//   s = sigmoid(W2 relu(W1 mean_hw(y) + b1) + b2),  out = relu(y * s + x)
+// One 256-thread block per board: the per-channel means, the two tiny FCs and the gates stay
+// in LDS; y and x are read once more for the scaled residual (both L2-resident right after the
+// producing conv).  C <= 1024, R = C / 16.
+__global__ __launch_bounds__(256) void k_se_residual(const float* y, const float* x, float* out, const float* W1,
+                                                     const float* b1, const float* W2, const float* b2, int HW, int C,
+                                                     int R, const int* m_limit) {
+    __shared__ float mean[1024], hid[64], gate[1024];
+    const int b = blockIdx.x;
+    if (m_limit && b >= *m_limit) return;
+    const size_t base = (size_t)b * HW * C;
+    const float inv = 1.0f / (float)HW;
+    for (int c = threadIdx.x; c < C; c += 256) {
+        float s = 0.0f;
+        for (int p = 0; p < HW; ++p) s += y[base + (size_t)p * C + c];
+        mean[c] = s * inv;
+    }
+    __syncthreads();
+    for (int r = threadIdx.x; r < R; r += 256) {
+        float s = b1[r];
+        for (int c = 0; c < C; ++c) s += W1[(size_t)r * C + c] * mean[c];
+        hid[r] = s > 0.0f ? s : 0.0f;
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < C; c += 256) {
+        float s = b2[c];
+        for (int r = 0; r < R; ++r) s += W2[(size_t)c * R + r] * hid[r];
+        gate[c] = 1.0f / (1.0f + expf(-s));
+    }
+    __syncthreads();
+    const int n4 = HW * C / 4;   // C % 16 == 0: float4 items never straddle a pixel
+    const float4* y4 = reinterpret_cast<const float4*>(y + base);
+    const float4* x4 = reinterpret_cast<const float4*>(x + base);
+    float4* o4 = reinterpret_cast<float4*>(out + base);
+    for (int i = threadIdx.x; i < n4; i += 256) {
+        const int c = (i * 4) % C;
+        const float4 a = y4[i], r = x4[i];
+        float4 o;
+        o.x = fmaxf(a.x * gate[c] + r.x, 0.0f);
+        o.y = fmaxf(a.y * gate[c + 1] + r.y, 0.0f);
+        o.z = fmaxf(a.z * gate[c + 2] + r.z, 0.0f);
+        o.w = fmaxf(a.w * gate[c + 3] + r.w, 0.0f);
+        o4[i] = o;
+    }
+}
+
 // adaptive_avg_pool2d(x, (P, P)) on NHWC: out[b][oy][ox][c]
 __global__ void k_adaptive_pool(const float* in, float* out, int B, int H, int W, int C, int P, const int* m_limit) {
     const int idx = blockIdx.x;           // b * P*P + oy*P + ox
@@ -476,4 +524,9 @@ void az_launch_pack_input(const float* in, float* out, int B, int Cin, int HW, i
 
 void az_launch_softmax_rows(const float* logits, float* out, int B, int A, hipStream_t st) {
     hipLaunchKernelGGL(k_softmax_rows, dim3(B), dim3(256), 0, st, logits, out, A);
+}
+
+void az_launch_se_residual(const float* y, const float* x, float* out, const float* W1, const float* b1, const float* W2,
+                           const float* b2, int B, int HW, int C, int R, const int* m_limit, hipStream_t st) {
+    hipLaunchKernelGGL(k_se_residual, dim3(B), dim3(256), 0, st, y, x, out, W1, b1, W2, b2, HW, C, R, m_limit);
 }

@@ -78,6 +78,21 @@ typedef struct az_net_desc {
 } az_net_desc;
 
 int az_net_create(az_engine* e, const az_net_desc* desc, az_net** out);
+/* DDW-RandWire network: DDWRandWireResNet(in_planes, action_size, channels,
+ * blocks) of src/nn/ddw_randwire_resnet.cpp:387-468 (TorchNeuralNetwork::createDDWRandWireResNet,
+ * torch_neural_network.cpp:799-814).  Each of `blocks` rand-wire blocks is RandWireBlock(channels,
+ * 32 nodes, p = 0.75, seed = block index) (:399): 32 SE residual blocks wired by a rewired
+ * Watts-Strogatz graph with routers.  desc: conv_bias 0, precision AZ_PREC_F32, pool = min(8, board)
+ * (the reference: head_channels 32, fc_hidden 256); residual is ignored.  The blob is the
+ * reference module's state_dict order (num_batches_tracked dropped); every other az_net_* call and
+ * the search take the handle as for az_net_create. */
+int az_net_create_randwire(az_engine* e, const az_net_desc* desc, az_net** out);
+/* Host only (no device needed): the wiring of rand-wire block `block` (RandWireBlock::_generate_graph,
+ * :248-319, with the duplicate-edge test evaluated as written -- DESIGN.md §5c).  order[32] = nodes()
+ * order (router / block registration order), topo[32], inputs / outputs (in-/out-degree 0), the
+ * predecessors of node v in preds[pred_off[v] .. pred_off[v+1]) (pred_off[33]; preds_cap entries). */
+int az_randwire_graph(int block, int* order, int* topo, int* inputs, int* n_inputs, int* outputs, int* n_outputs,
+                      int* pred_off, int* preds, int preds_cap);
 void az_net_destroy(az_net* n);
 /* Number of floats of the canonical parameter blob (torch state_dict order, BN in
  * eval form: weight, bias, running_mean, running_var per BN). */

@@ -1,0 +1,149 @@
+"""Row f4: the DDW-RandWire network (src/nn/ddw_randwire_resnet.cpp) on the device engine
+(az_net_create_randwire: f32 MFMA GEMMs for the 3x3 convs and routers, k_se_residual for
+SE + residual + ReLU), against
+
+* the reference C++ module's own outputs (tests/golden/randwire_golden.npz), tolerance 1e-4
+  (BASELINE.json north_star);
+* the oracle restatement (pinned to those goldens) at the reference's default width and depth
+  (128 channels, 20 rand-wire blocks = 640 SE residual blocks), relative to the output scale;
+* itself: a board's outputs do not depend on its batch position or batch size (bitwise);
+* the search: a self-play game whose leaves the rand-wire net evaluates replays bit for bit
+  through the CPU restatement of the search, and every logged evaluation matches the oracle."""
+import types
+
+import numpy as np
+import pytest
+
+GOLD_CASES = ["c16_b1_h9", "c32_b2_h15", "c16_b3_h8"]
+
+
+def _net(eng, bs, ch, nb, B, inp=11):
+    import az_amd
+    return az_amd.HipNeuralNetwork(eng, az_amd.randwire_net_desc(bs, ch, nb, inp, B), randwire=True)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", GOLD_CASES)
+def test_gpu_randwire_matches_reference_module(case):
+    import os
+    import az_amd
+    import randwire_oracle as RW
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "randwire_golden.npz"))
+    inp, bs, ch, nb, B, seed = (int(v) for v in g[case + "_cfg"])
+    eng = az_amd.Engine(0)
+    net = _net(eng, bs, ch, nb, B, inp)
+    graphs = RW.load_graphs()
+    blob = RW.init_blob(net.desc, graphs, seed)
+    assert net.num_params == blob.size
+    net.init_random(seed)                      # az_net_init_random over the rand-wire blob order
+    assert np.array_equal(net.get_weights().view(np.uint32), blob.view(np.uint32))
+    lo, v = net.forward(g[case + "_planes"])
+    dl = np.abs(lo - g[case + "_logits"]).max()
+    dv = np.abs(v - g[case + "_value"]).max()
+    print(f"{case}: max|dlogit| {dl:.3g} max|dvalue| {dv:.3g}")
+    assert dl <= 1e-4 and dv <= 1e-4
+    p, pv = net.predictBatch(g[case + "_planes"])
+    import net_oracle
+    assert np.abs(p - net_oracle.softmax_policy(g[case + "_logits"])).max() <= 1e-4
+    net.close()
+    eng.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("bs,ch,nb,B", [(15, 128, 20, 2), (15, 128, 2, 24), (9, 64, 3, 7)])
+def test_gpu_randwire_matches_oracle(bs, ch, nb, B):
+    import az_amd
+    import randwire_oracle as RW
+    eng = az_amd.Engine(0)
+    net = _net(eng, bs, ch, nb, B)
+    graphs = RW.load_graphs()
+    net.init_random(100 + nb)
+    blob = net.get_weights()
+    rng = np.random.default_rng(nb)
+    planes = (rng.random((B, 11, bs, bs)) < 0.3).astype(np.float32)
+    lo, v = net.forward(planes)
+    rl, rv = RW.forward(net.desc, graphs, blob, planes)
+    scale = max(1.0, float(np.abs(rl).max()))
+    dl, dv = np.abs(lo - rl).max(), np.abs(v - rv).max()
+    print(f"{bs}x{bs} {ch}ch {nb} blocks B={B}: |logit| max {np.abs(rl).max():.3g}, max|dlogit| {dl:.3g}, "
+          f"max|dvalue| {dv:.3g}")
+    assert dl <= 1e-4 * scale and dv <= 1e-4
+    # batch position / size independence (bitwise)
+    sub = [B - 1, 0] if B > 1 else [0]
+    lo2, v2 = net.forward(planes[sub])
+    assert np.array_equal(lo2.view(np.uint32), lo[sub].view(np.uint32))
+    assert np.array_equal(v2.view(np.uint32), v[sub].view(np.uint32))
+    net.close()
+    eng.close()
+
+
+@pytest.mark.gpu
+def test_gpu_randwire_selfplay_replay():
+    import az_amd
+    import az_oracle as O
+    import net_oracle
+    import randwire_oracle as RW
+    bs, sims, G, moves, logged = 9, 40, 3, 5, 1
+    eng = az_amd.Engine(0)
+    net = _net(eng, bs, 16, 1, G)
+    net.init_random(5)
+    blob = net.get_weights()
+    m = az_amd.ParallelMCTS(eng, n_games=G, board_size=bs, num_simulations=sims, evaluator=az_amd.AZ_EVAL_NET,
+                            net=net, noise_seed=42, noise_seed_stride=1)
+    cap = (sims + 2) * (moves + 1)
+    m.enableEvalLog(logged, cap)
+    m.newGames()
+    m.addDirichletNoise(0.03, 0.25)
+    dev = []
+    for ply in range(moves):
+        m.search()
+        act, val, probs, cact, nch = m.select(True, 1.0)
+        a, N, VL, W, P = m.rootChildren(logged)
+        dev.append(dict(action=int(act[logged]), value=float(val[logged]), N=N.tolist(), W=W.view(np.uint32).tolist(),
+                        P=P.view(np.uint32).tolist(), probs=probs[logged, :nch[logged]].view(np.uint32).tolist()))
+        term, _ = m.updateWithMove(act)
+        if ply % 2 == 0:
+            m.addDirichletNoise(0.03, 0.25)
+        if term[logged]:
+            break
+    pol, valv, planes = m.readEvalLog(cap)
+    assert len(pol) > sims
+    k = [0]
+
+    def replay(game, x):
+        i = k[0]
+        k[0] += 1
+        assert np.array_equal(x, planes[i]), f"feature planes differ at evaluation {i}"
+        return pol[i], float(valv[i])
+
+    ref = O.play(bs=bs, sims=sims, max_moves=len(dev), eval_kind=O.EVAL_REPLAY, evaluator=replay,
+                 noise_seed=42 + logged)[0]
+    assert k[0] == len(pol)
+    for ply, (d, r) in enumerate(zip(dev, ref["moves"])):
+        kids = r["children"]
+        assert d["N"] == [c[1] for c in kids], ply
+        assert d["W"] == [c[3] for c in kids] and d["P"] == [c[4] for c in kids], ply
+        assert d["probs"] == r["probs"] and d["action"] == r["action"], ply
+    rl, rv = RW.forward(net.desc, RW.load_graphs(), blob, planes)
+    assert np.abs(valv - rv).max() <= 1e-4
+    assert np.abs(pol - net_oracle.softmax_policy(rl)).max() <= 1e-4
+    m.close()
+    net.close()
+    eng.close()
+
+
+@pytest.mark.gpu
+def test_gpu_randwire_rejects_bad_desc():
+    import az_amd
+    eng = az_amd.Engine(0)
+    for kw in (dict(precision=az_amd.AZ_PREC_FP16), dict(conv_bias=1), dict(channels=24), dict(pool=4)):
+        d = az_amd.randwire_net_desc(9, 16, 1, 11, 4)
+        for k, v in kw.items():
+            setattr(d, k, v)
+        with pytest.raises(az_amd.AzError):
+            az_amd.HipNeuralNetwork(eng, d, randwire=True)
+    net = _net(eng, 9, 16, 1, 4)
+    with pytest.raises(az_amd.AzError):
+        net.set_precision(az_amd.AZ_PREC_BF16)
+    net.close()
+    eng.close()
