@@ -19,6 +19,8 @@ struct GemmArgs {
     int rows_per_sample;            // rows of one sample (H*W, P*P or 1)
     float* part;                    // split-K workspace [splits][M][N] (FC layers) or null
     int splits;                     // K slices when part != null
+    const float* const* Am;         // taps == 1 only: K spans Cch-wide slices of several inputs,
+                                    // slice j from Am[j] (device array; a rand-wire router's concat)
 };
 
 // bf16 trunk conv: activations stored as bf16 hi (+ lo) planes, NHWC.

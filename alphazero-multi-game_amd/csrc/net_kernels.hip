@@ -87,6 +87,9 @@ __global__ __launch_bounds__(256) void gemm_f32(GemmArgs p) {
                     const int y = arow_y[i] + dy, x = arow_x[i] + dx;
                     if (y >= 0 && y < p.H && x >= 0 && x < p.W)
                         src = p.A + ((size_t)(arow_b[i] * p.H + y) * p.W + x) * p.lda + c;
+                } else if (p.Am) {
+                    const int j = k / p.Cch;
+                    src = p.Am[j] + (size_t)(m0 + r0 + 32 * i) * p.lda + (k - j * p.Cch);
                 } else {
                     src = p.A + (size_t)(m0 + r0 + 32 * i) * p.lda + c;
                 }
@@ -206,12 +209,28 @@ __global__ __launch_bounds__(256) void k_se_residual(const float* y, const float
     __shared__ float mean[1024], hid[64], gate[1024];
     const int b = blockIdx.x;
     if (m_limit && b >= *m_limit) return;
+    __shared__ float4 part[256];
     const size_t base = (size_t)b * HW * C;
     const float inv = 1.0f / (float)HW;
-    for (int c = threadIdx.x; c < C; c += 256) {
-        float s = 0.0f;
-        for (int p = 0; p < HW; ++p) s += y[base + (size_t)p * C + c];
-        mean[c] = s * inv;
+    {   // channel quads over 256 / (C/4) pixel groups, then the groups summed in order per channel
+        const int C4 = C / 4, G = 256 / C4, t = threadIdx.x;
+        const int q = t % C4, g = t / C4;
+        float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (g < G) {
+            const float4* y4 = reinterpret_cast<const float4*>(y + base) + q;
+            for (int p = g; p < HW; p += G) {
+                const float4 v = y4[(size_t)p * C4];
+                s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+            }
+        }
+        part[t] = s;
+        __syncthreads();
+        for (int c = t; c < C; c += 256) {
+            const float* pf = reinterpret_cast<const float*>(part);
+            float a = 0.0f;
+            for (int k = 0; k < G; ++k) a += pf[(k * C4 + c / 4) * 4 + c % 4];
+            mean[c] = a * inv;
+        }
     }
     __syncthreads();
     for (int r = threadIdx.x; r < R; r += 256) {
