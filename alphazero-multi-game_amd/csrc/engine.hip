@@ -104,12 +104,14 @@ struct Layer {            // one implicit-GEMM layer, BN folded
 // block's two 3x3 convs (BN folded) and the SE block's two linear layers.
 struct RwNode {
     Layer router, c1, c2;
+    const float** ins = nullptr;   // device: the predecessors' output buffers (the router's concat)
     float *w1 = nullptr, *b1 = nullptr, *w2 = nullptr, *b2 = nullptr;   // SE: [R][C], [R], [C][R], [C]
 };
 struct RwBlock {
     azrw::Plan plan;
     std::vector<RwNode> node;   // by node id
     Layer out_router;           // when the block has more than one sink
+    const float** outs = nullptr;   // device: the sinks' output buffers
 };
 
 struct az_net {
@@ -139,6 +141,8 @@ struct az_net {
     std::vector<RwBlock> rwb;
     std::vector<float*> rw_out;       // node outputs [B*HW][F], by node id
     float *rw_t2 = nullptr, *rw_in = nullptr;   // conv2 output, router output
+    int rw_splits = 1;                // K slices of the node convs (from the capacity: batch-size independent)
+    float* rw_ws = nullptr;           // their split-K partials [rw_splits][rows][F]
     bool loaded = false;
     std::vector<float> host_blob;   // canonical blob of the loaded weights (az_net_get_weights)
     // profiling: HIP events bracketing the 3x3 trunk of every forward (on the launch stream)
@@ -432,21 +436,17 @@ struct LeafRecs {                 // the search's leaf records: sample b = recor
     const uint8_t* rec; const int* gidx; int go; int n;
 };
 
-// Router of a rand-wire node: relu(BN(conv1x1(concat(ins)))) as one K-slice GEMM per input
-// (K = F each, weight columns [j F, (j+1) F) of the folded [F][deg F] matrix), accumulated in
-// place; bias and ReLU on the last slice.
-void rw_router(const az_net* n, const Layer& L, const std::vector<const float*>& ins, float* out, int rows, const int* nb,
+// Router of a rand-wire node: relu(BN(conv1x1(concat(ins)))) as ONE GEMM over K = deg F whose
+// k-slice j is read straight from input j's buffer (the device table `dins`, same k order as the
+// reference's torch::cat); BN folded into the weights and bias.
+void rw_router(const az_net* n, const Layer& L, const float* const* dins, float* out, int rows, const int* nb,
                hipStream_t st) {
     const int F = n->d.channels, H = n->d.board_size;
-    for (size_t j = 0; j < ins.size(); ++j) {
-        const bool last = j + 1 == ins.size();
-        GemmArgs p{};
-        p.A = ins[j]; p.lda = F; p.B = L.W + j * F; p.ldb = L.K; p.C = out; p.ldc = F;
-        p.bias = last ? L.b : nullptr; p.res = j ? out : nullptr;
-        p.M = rows; p.N = F; p.K = F; p.Kpad = (F + 31) / 32 * 32; p.taps = 1; p.Cch = F; p.H = H; p.W = H;
-        p.m_limit = nb; p.rows_per_sample = n->HW;
-        az_launch_gemm_f32(p, last ? ACT_RELU : ACT_NONE, j > 0, st);
-    }
+    GemmArgs p{};
+    p.Am = dins; p.lda = F; p.B = L.W; p.ldb = L.K; p.C = out; p.ldc = F; p.bias = L.b;
+    p.M = rows; p.N = F; p.K = L.K; p.Kpad = L.Kpad; p.taps = 1; p.Cch = F; p.H = H; p.W = H;
+    p.m_limit = nb; p.rows_per_sample = n->HW;
+    az_launch_gemm_f32(p, ACT_RELU, false, st);
 }
 
 // DDW-RandWire trunk (ddw_randwire_resnet.cpp:321-384 per block): input nodes on the block input,
@@ -456,13 +456,15 @@ float* rw_trunk(az_net* n, int B, const int* nb, hipStream_t st) {
     const az_net_desc& d = n->d;
     const int F = d.channels, H = d.board_size, HW = n->HW, rows = B * HW, R = F / 16;
     float* x = n->h0;
-    std::vector<const float*> ins;
     for (const RwBlock& blk : n->rwb) {
         const azrw::Plan& pl = blk.plan;
         auto node = [&](int v, const float* in) {
             const RwNode& nd = blk.node[v];
-            az_launch_gemm_f32(gemm_args(nd.c1, in, F, n->t, F, nullptr, rows, H, H, nb, HW), ACT_RELU, false, st);
-            az_launch_gemm_f32(gemm_args(nd.c2, n->t, F, n->rw_t2, F, nullptr, rows, H, H, nb, HW), ACT_NONE, false, st);
+            GemmArgs g1 = gemm_args(nd.c1, in, F, n->t, F, nullptr, rows, H, H, nb, HW);
+            GemmArgs g2 = gemm_args(nd.c2, n->t, F, n->rw_t2, F, nullptr, rows, H, H, nb, HW);
+            if (n->rw_ws) { g1.part = g2.part = n->rw_ws; g1.splits = g2.splits = n->rw_splits; }
+            az_launch_gemm_f32(g1, ACT_RELU, false, st);
+            az_launch_gemm_f32(g2, ACT_NONE, false, st);
             az_launch_se_residual(n->rw_t2, in, n->rw_out[v], nd.w1, nd.b1, nd.w2, nd.b2, B, HW, F, R, nb, st);
         };
         for (int v : pl.inputs) node(v, x);
@@ -470,16 +472,12 @@ float* rw_trunk(az_net* n, int B, const int* nb, hipStream_t st) {
             const auto& pr = pl.preds[v];
             if (pr.empty() || std::find(pl.inputs.begin(), pl.inputs.end(), v) != pl.inputs.end()) continue;
             if (pr.size() == 1) { node(v, n->rw_out[pr[0]]); continue; }
-            ins.clear();
-            for (int u : pr) ins.push_back(n->rw_out[u]);
-            rw_router(n, blk.node[v].router, ins, n->rw_in, rows, nb, st);
+            rw_router(n, blk.node[v].router, blk.node[v].ins, n->rw_in, rows, nb, st);
             node(v, n->rw_in);
         }
         float* y = x == n->h0 ? n->h1 : n->h0;
         if (pl.outputs.size() > 1) {
-            ins.clear();
-            for (int u : pl.outputs) ins.push_back(n->rw_out[u]);
-            rw_router(n, blk.out_router, ins, y, rows, nb, st);
+            rw_router(n, blk.out_router, blk.outs, y, rows, nb, st);
         } else {
             (void)hipMemcpyAsync(y, n->rw_out[pl.outputs[0]], (size_t)rows * F * 4, hipMemcpyDeviceToDevice, st);
         }
@@ -1138,6 +1136,28 @@ static int net_create(az_engine* e, const az_net_desc* d, az_net** out, bool rw)
         n->rw_out.assign(n->rwb.empty() ? 0 : n->rwb[0].node.size(), nullptr);
         for (float*& p : n->rw_out) A_(&p, rows * F);
         A_(&n->rw_t2, rows * F); A_(&n->rw_in, rows * F);
+        // Small capacities leave most CUs idle (one 128 x 128 f32 tile of a K = 9F conv is ~60 us
+        // of one CU): split K so the node convs cover the chip.  Chosen from max_batch, so a
+        // board's summation order never depends on the batch it arrives in.
+        {
+            const int bn = F <= 64 ? 64 : 128, nk = (int)((9 * F + 31) / 32);
+            const long tiles = (long)((rows + 127) / 128) * (long)((F + bn - 1) / bn);
+            while (n->rw_splits < 8 && tiles * n->rw_splits < 256 && nk / (2 * n->rw_splits) >= 4) n->rw_splits *= 2;
+            if (n->rw_splits > 1) A_(&n->rw_ws, (size_t)n->rw_splits * rows * F);
+        }
+        // routers read their inputs straight from the node buffers: per router a device table
+        auto table = [&](const std::vector<int>& ids, const float*** dst) {
+            if (r || ids.size() < 2) return;
+            std::vector<const float*> t;
+            for (int u : ids) t.push_back(n->rw_out[u]);
+            if (hipMalloc((void**)dst, t.size() * sizeof(float*)) != hipSuccess ||
+                hipMemcpy((void*)*dst, t.data(), t.size() * sizeof(float*), hipMemcpyHostToDevice) != hipSuccess)
+                r = az_fail(AZ_ERR_OOM, "router input table");
+        };
+        for (RwBlock& blk : n->rwb) {
+            for (size_t v = 0; v < blk.node.size(); ++v) table(blk.plan.preds[v], &blk.node[v].ins);
+            table(blk.plan.outputs, &blk.outs);
+        }
     }
     if (!r) r = dalloc(&n->d_nb, 1);
     if (!r) r = dalloc(&n->zero, 128);
@@ -1191,13 +1211,14 @@ void az_net_destroy(az_net* n) {
     for (auto& l : n->blk) ls.push_back(&l);
     for (auto& blk : n->rwb) {
         ls.push_back(&blk.out_router);
+        F((void*)blk.outs);
         for (auto& nd : blk.node) {
             ls.push_back(&nd.router); ls.push_back(&nd.c1); ls.push_back(&nd.c2);
-            F(nd.w1); F(nd.b1); F(nd.w2); F(nd.b2);
+            F(nd.w1); F(nd.b1); F(nd.w2); F(nd.b2); F((void*)nd.ins);
         }
     }
     for (float* p : n->rw_out) F(p);
-    F(n->rw_t2); F(n->rw_in);
+    F(n->rw_t2); F(n->rw_in); F(n->rw_ws);
     for (Layer* l : ls) { F(l->W); F(l->b); F(l->Whi); F(l->Wlo); F(l->Wh16); F(l->Wbk_bf); F(l->Wbk_h); }
     for (void* p : {(void*)n->x0, (void*)n->h0, (void*)n->h1, (void*)n->t, (void*)n->pool, (void*)n->pp, (void*)n->vp, (void*)n->hpv,
                     (void*)n->v1, (void*)n->ws, (void*)n->logits, (void*)n->value, (void*)n->soft, (void*)n->in_nchw, (void*)n->d_nb,

@@ -10,6 +10,7 @@
 //              AZ_PREC_F32 path and the head layers of every precision.
 //   (bf16 MFMA trunk kernels live in conv_bf16.hip.)
 #include <hip/hip_runtime.h>
+#include <algorithm>
 #include <stdint.h>
 #include "net.h"
 #include "leaf_planes.h"
@@ -202,7 +203,8 @@ __global__ __launch_bounds__(256) void gemm_f32(GemmArgs p) {
 //   s = sigmoid(W2 relu(W1 mean_hw(y) + b1) + b2),  out = relu(y * s + x)
 // One 256-thread block per board: the per-channel means, the two tiny FCs and the gates stay
 // in LDS; y and x are read once more for the scaled residual (both L2-resident right after the
-// producing conv).  C <= 1024, R = C / 16.
+// producing conv).  C <= 1024, R = C / 16.  gridDim.y blocks share a board at small batches: each
+// computes the (identical) gates and scales its own slice of the board.
 __global__ __launch_bounds__(256) void k_se_residual(const float* y, const float* x, float* out, const float* W1,
                                                      const float* b1, const float* W2, const float* b2, int HW, int C,
                                                      int R, const int* m_limit) {
@@ -249,7 +251,7 @@ __global__ __launch_bounds__(256) void k_se_residual(const float* y, const float
     const float4* y4 = reinterpret_cast<const float4*>(y + base);
     const float4* x4 = reinterpret_cast<const float4*>(x + base);
     float4* o4 = reinterpret_cast<float4*>(out + base);
-    for (int i = threadIdx.x; i < n4; i += 256) {
+    for (int i = blockIdx.y * 256 + threadIdx.x; i < n4; i += 256 * gridDim.y) {
         const int c = (i * 4) % C;
         const float4 a = y4[i], r = x4[i];
         float4 o;
@@ -547,5 +549,6 @@ void az_launch_softmax_rows(const float* logits, float* out, int B, int A, hipSt
 
 void az_launch_se_residual(const float* y, const float* x, float* out, const float* W1, const float* b1, const float* W2,
                            const float* b2, int B, int HW, int C, int R, const int* m_limit, hipStream_t st) {
-    hipLaunchKernelGGL(k_se_residual, dim3(B), dim3(256), 0, st, y, x, out, W1, b1, W2, b2, HW, C, R, m_limit);
+    const int S = B >= 256 ? 1 : std::min(8, 256 / B);   // blocks per board: cover the CUs at small batches
+    hipLaunchKernelGGL(k_se_residual, dim3(B, S), dim3(256), 0, st, y, x, out, W1, b1, W2, b2, HW, C, R, m_limit);
 }
