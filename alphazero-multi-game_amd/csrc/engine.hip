@@ -374,10 +374,11 @@ int net_load_rw(az_net* n, const float* blob) {
         }
         for (int v : pl.order) {
             RwNode& nd = blk.node[v];
+            const bool h16 = F % 32 == 0;   // 16-bit weight copies: the fp16 node convs (conv3x3_v4)
             fold_conv(pc, F, F, 3, F, false, W, b);
-            if (int r = upload_layer(nd.c1, W, b, F, 9 * F, 9, F, false)) return r;
+            if (int r = upload_layer(nd.c1, W, b, F, 9 * F, 9, F, h16)) return r;
             fold_conv(pc, F, F, 3, F, false, W, b);
-            if (int r = upload_layer(nd.c2, W, b, F, 9 * F, 9, F, false)) return r;
+            if (int r = upload_layer(nd.c2, W, b, F, 9 * F, 9, F, h16)) return r;
             if (int r = raw(&nd.w1, (size_t)R * F)) return r;
             if (int r = raw(&nd.b1, R)) return r;
             if (int r = raw(&nd.w2, (size_t)F * R)) return r;
@@ -425,6 +426,7 @@ enum { NET_IN_GEMM = 0, NET_IN_SMALL = 1, NET_IN_G8 = 2 };
 int net_input_path(const az_net* n) {
     const az_net_desc& d = n->d;
     const int H = d.board_size, F = d.channels, prec = d.precision;
+    if (n->rw) return NET_IN_GEMM;   // rand-wire: f32 input conv on x0
     if (n->sm_W && prec == AZ_PREC_FP16 && d.blocks > 0) return NET_IN_SMALL;
     const bool bf = (prec == AZ_PREC_BF16 || prec == AZ_PREC_FP16) && F % 32 == 0;
     if (bf && az_conv_g8_supported(H, H, F, F) && n->in.Wbk_h != nullptr && az_conv_g8_supported(H, H, n->cin_pad, F))
@@ -460,6 +462,22 @@ float* rw_trunk(az_net* n, int B, const int* nb, hipStream_t st) {
         const azrw::Plan& pl = blk.plan;
         auto node = [&](int v, const float* in) {
             const RwNode& nd = blk.node[v];
+            if (d.precision == AZ_PREC_FP16) {
+                // fp16 operands, fp32 accumulation (conv3x3_v4): conv1 -> fp16 t, conv2 -> fp32 y;
+                // the residual stream, routers and SE stay fp32
+                az_launch_to_f16(in, n->hh[0], (size_t)rows * F, nb, HW, F, st);
+                ConvBf16Args a{};
+                a.Ahi = n->hh[0]; a.Bhi = nd.c1.Wh16; a.Bblk = nd.c1.Wbk_h; a.Chi = n->th; a.bias = nd.c1.b;
+                a.M = rows; a.N = F; a.C = F; a.H = H; a.W = H; a.m_limit = nb; a.rows_per_sample = HW; a.relu = 1;
+                a.zero = n->zero; a.stamp = -1;
+                az_conv_v4_launch(a, 2, st);
+                ConvBf16Args c = a;
+                c.Ahi = n->th; c.Bhi = nd.c2.Wh16; c.Bblk = nd.c2.Wbk_h; c.Chi = n->hh[1]; c.Cf = n->rw_t2; c.bias = nd.c2.b;
+                c.relu = 0;
+                az_conv_v4_launch(c, 2, st);
+                az_launch_se_residual(n->rw_t2, in, n->rw_out[v], nd.w1, nd.b1, nd.w2, nd.b2, B, HW, F, R, nb, st);
+                return;
+            }
             GemmArgs g1 = gemm_args(nd.c1, in, F, n->t, F, nullptr, rows, H, H, nb, HW);
             GemmArgs g2 = gemm_args(nd.c2, n->t, F, n->rw_t2, F, nullptr, rows, H, H, nb, HW);
             if (n->rw_ws) { g1.part = g2.part = n->rw_ws; g1.splits = g2.splits = n->rw_splits; }
@@ -498,7 +516,7 @@ int net_forward(az_net* n, const float* x0, int B, const int* nb, float* logits,
     const bool bf = (prec == AZ_PREC_BF16X3 || prec == AZ_PREC_BF16 || prec == AZ_PREC_FP16) && F % 32 == 0;
     const bool f16 = prec == AZ_PREC_FP16;
     // g8 path (v5 / v6 conv, fp16/bf16): input conv, trunk and pool all on 16-bit channel-blocked rows
-    const bool g8 = bf && prec != AZ_PREC_BF16X3 && az_conv_g8_supported(H, W, F, F);
+    const bool g8 = !n->rw && bf && prec != AZ_PREC_BF16X3 && az_conv_g8_supported(H, W, F, F);
     const int mode = f16 ? 2 : 1;
     int8_t* hq[2] = {reinterpret_cast<int8_t*>(n->hl[0]), reinterpret_cast<int8_t*>(n->hl[1])};
     const int inpath = net_input_path(n);
@@ -1170,9 +1188,17 @@ static int net_create(az_engine* e, const az_net_desc* d, az_net** out, bool rw)
 
 int az_net_create(az_engine* e, const az_net_desc* d, az_net** out) { return net_create(e, d, out, false); }
 
+// Rand-wire precisions: AZ_PREC_F32 (the reference module's arithmetic), or AZ_PREC_FP16 node convs
+// (conv3x3_v4: 15x15 boards, channels % 64 == 0) with the fp32 residual stream, routers and SE.
+static int check_rw_precision(const az_net_desc& d, int precision) {
+    if (precision == AZ_PREC_F32) return 0;
+    if (precision == AZ_PREC_FP16 && az_conv_v4_supported(d.board_size, d.board_size, d.channels, d.channels)) return 0;
+    return az_fail(AZ_ERR_ARG, "rand-wire nets: AZ_PREC_F32, or AZ_PREC_FP16 on 15x15 with channels %% 64 == 0");
+}
+
 int az_net_create_randwire(az_engine* e, const az_net_desc* d, az_net** out) {
     if (!d) return az_fail(AZ_ERR_ARG, "null argument");
-    if (d->precision != AZ_PREC_F32) return az_fail(AZ_ERR_ARG, "rand-wire nets run the fp32 path (AZ_PREC_F32)");
+    if (int r = check_rw_precision(*d, d->precision)) return r;
     if (d->conv_bias) return az_fail(AZ_ERR_ARG, "rand-wire convolutions carry no bias (conv_bias = 0)");
     if (d->channels % 16 || d->channels > 1024) return az_fail(AZ_ERR_ARG, "rand-wire channels: a multiple of 16, <= 1024");
     if (d->pool != std::min(8, d->board_size)) return az_fail(AZ_ERR_ARG, "rand-wire heads pool to min(8, board)");
@@ -1303,7 +1329,7 @@ int az_net_init_random(az_net* n, uint64_t seed) {
 
 int az_net_set_precision(az_net* n, int precision) {
     if (!n) return az_fail(AZ_ERR_ARG, "null net");
-    if (n->rw && precision != AZ_PREC_F32) return az_fail(AZ_ERR_ARG, "rand-wire nets run the fp32 path (AZ_PREC_F32)");
+    if (n->rw && check_rw_precision(n->d, precision)) return AZ_ERR_ARG;
     if (int r = check_precision(n->d, precision)) return r;
     n->d.precision = precision;
     return 0;
@@ -1335,6 +1361,7 @@ int az_net_trunk_kernel(az_net* n, char* name, int len) {
     const int prec = d.precision, F = d.channels, H = d.board_size;
     const bool bf = (prec == AZ_PREC_BF16X3 || prec == AZ_PREC_BF16 || prec == AZ_PREC_FP16) && F % 32 == 0;
     const bool f16 = prec == AZ_PREC_FP16;
+    if (n->rw) { snprintf(name, len, f16 ? "conv3x3_v4<2, 128, 1>" : "gemm_f32"); return 0; }
     if (!bf || d.blocks < 1) { snprintf(name, len, "gemm_f32"); return 0; }
     if (f16 && az_smallnet_supported(H, F, n->cin_pad, d.pool, d.head_channels) && d.blocks <= az_smallnet_max_blocks()) {
         snprintf(name, len, "k_smallnet<%d>", H);

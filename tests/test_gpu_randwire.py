@@ -147,3 +147,29 @@ def test_gpu_randwire_rejects_bad_desc():
         net.set_precision(az_amd.AZ_PREC_BF16)
     net.close()
     eng.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nb,B", [(2, 16), (20, 3)])
+def test_gpu_randwire_fp16_error(nb, B):
+    """AZ_PREC_FP16 rand-wire (node convs on conv3x3_v4 with fp16 operands and fp32 accumulation;
+    routers, SE and the residual stream fp32): a throughput mode.  Its error against the fp32
+    reference arithmetic is measured and bounded here; the parity precision is AZ_PREC_F32."""
+    import az_amd
+    import randwire_oracle as RW
+    eng = az_amd.Engine(0)
+    net = _net(eng, 15, 128, nb, B)
+    net.set_precision(az_amd.AZ_PREC_FP16)
+    net.init_random(300 + nb)
+    blob = net.get_weights()
+    planes = (np.random.default_rng(nb).random((B, 11, 15, 15)) < 0.3).astype(np.float32)
+    lo, v = net.forward(planes)
+    rl, rv = RW.forward(net.desc, RW.load_graphs(), blob, planes)
+    dl, dv = float(np.abs(lo - rl).max()), float(np.abs(v - rv).max())
+    print(f"fp16 rand-wire 128ch {nb} blocks B={B}: |logit| max {np.abs(rl).max():.3g}, max|dlogit| {dl:.3g}, "
+          f"max|dvalue| {dv:.3g}")
+    assert dl <= 1e-2 * max(1.0, float(np.abs(rl).max())) and dv <= 1e-2
+    lo2, v2 = net.forward(planes[[B - 1, 0]])
+    assert np.array_equal(lo2.view(np.uint32), lo[[B - 1, 0]].view(np.uint32))
+    net.close()
+    eng.close()
