@@ -448,7 +448,8 @@ void rw_router(const az_net* n, const Layer& L, const float* const* dins, float*
     p.Am = dins; p.lda = F; p.B = L.W; p.ldb = L.K; p.C = out; p.ldc = F; p.bias = L.b;
     p.M = rows; p.N = F; p.K = L.K; p.Kpad = L.Kpad; p.taps = 1; p.Cch = F; p.H = H; p.W = H;
     p.m_limit = nb; p.rows_per_sample = n->HW;
-    az_launch_gemm_f32(p, ACT_RELU, false, st);
+    if (n->d.precision == AZ_PREC_FP16) az_launch_gemm_h16_relu(p, st);   // fp16 operands, fp32 accumulation
+    else az_launch_gemm_f32(p, ACT_RELU, false, st);
 }
 
 // DDW-RandWire trunk (ddw_randwire_resnet.cpp:321-384 per block): input nodes on the block input,

@@ -91,3 +91,6 @@ void az_launch_softmax_rows(const float* logits, float* out, int B, int A, hipSt
 // DDW-RandWire node tail: out = relu(y * SE(y) + x) (k_se_residual; C % 16 == 0, C <= 1024, R = C / 16 <= 64)
 void az_launch_se_residual(const float* y, const float* x, float* out, const float* W1, const float* b1, const float* W2,
                            const float* b2, int B, int HW, int C, int R, const int* m_limit, hipStream_t st);
+// 1x1 GEMM with fp16 operands (rounded from fp32 on load), fp32 accumulation, bias + ReLU
+// (gemm_h16_relu: the fp16 rand-wire routers; taps == 1, K % 4 == 0, Am slices or A)
+void az_launch_gemm_h16_relu(const GemmArgs& p, hipStream_t st);

@@ -198,6 +198,112 @@ __global__ __launch_bounds__(256) void gemm_f32(GemmArgs p) {
         }
 }
 
+// 1x1-conv GEMM with fp16 operands and fp32 accumulation (v_mfma_f32_32x32x16_f16): the routers of
+// an AZ_PREC_FP16 rand-wire net.  out[m][n] = relu(sum_k A(m,k) W[n][k] + bias[n]), taps == 1,
+// A from p.Am slices (or p.A), fp32 in memory and rounded to fp16 on the way into LDS, W fp32
+// [N][ldb] likewise.  Tile 128 x 128, BK = 32, 2 x 2 waves of 64 x 64 (2 x 2 MFMA tiles); LDS rows
+// [m][k] / [n][k] of 32 halves + 8 pad (80 B), each lane's operand (8 consecutive k: A[r][8h + j])
+// one ds_read_b128.
+typedef _Float16 half4_t __attribute__((ext_vector_type(4)));
+typedef _Float16 half8_t __attribute__((ext_vector_type(8)));
+__global__ __launch_bounds__(256) void gemm_h16_relu(GemmArgs p) {
+    constexpr int BM = 128, BN = 128, BK = 32, LD = BK + 8;
+    __shared__ __attribute__((aligned(16))) _Float16 As[2][BM * LD];
+    __shared__ __attribute__((aligned(16))) _Float16 Bs[2][BN * LD];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave >> 1, wn = wave & 1;
+    const int nbm = (p.M + BM - 1) / BM;
+    const int bm = blockIdx.x % nbm, bn = blockIdx.x / nbm;
+    const int m0 = bm * BM, n0 = bn * BN;
+    const int Mact = p.m_limit ? min(p.M, *p.m_limit * p.rows_per_sample) : p.M;
+    if (m0 >= Mact) return;
+    const int kq = tid & 7, r0 = tid >> 3;     // float4 column kq of rows r0 + 32 i
+    const int nk = (p.Kpad + BK - 1) / BK;
+    float4 ra[4], rb[4];
+    auto load_stage = [&](int kt) {
+        const int k = kt * BK + kq * 4;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int m = m0 + r0 + 32 * i;
+            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (m < Mact && k < p.K) {
+                const float* src;
+                if (p.Am) { const int j = k / p.Cch; src = p.Am[j] + (size_t)m * p.lda + (k - j * p.Cch); }
+                else src = p.A + (size_t)m * p.lda + k;
+                v = *reinterpret_cast<const float4*>(src);
+            }
+            ra[i] = v;
+            const int n = n0 + r0 + 32 * i;
+            float4 w = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (n < p.N && k < p.K) w = *reinterpret_cast<const float4*>(p.B + (size_t)n * p.ldb + k);
+            rb[i] = w;
+        }
+    };
+    auto store_stage = [&](int buf) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int r = r0 + 32 * i;
+            half4_t a = {(_Float16)ra[i].x, (_Float16)ra[i].y, (_Float16)ra[i].z, (_Float16)ra[i].w};
+            half4_t b = {(_Float16)rb[i].x, (_Float16)rb[i].y, (_Float16)rb[i].z, (_Float16)rb[i].w};
+            *reinterpret_cast<half4_t*>(&As[buf][r * LD + kq * 4]) = a;
+            *reinterpret_cast<half4_t*>(&Bs[buf][r * LD + kq * 4]) = b;
+        }
+    };
+    floatx16 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
+    load_stage(0);
+    store_stage(0);
+    __syncthreads();
+    const int kh = lane >> 5, l32 = lane & 31;
+    for (int kt = 0; kt < nk; ++kt) {
+        const int buf = kt & 1;
+        if (kt + 1 < nk) load_stage(kt + 1);
+        const _Float16* as = As[buf];
+        const _Float16* bs = Bs[buf];
+#pragma unroll
+        for (int kk = 0; kk < BK / 16; ++kk) {
+            half8_t a[2], b[2];
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+                a[i] = *reinterpret_cast<const half8_t*>(&as[(wm * 64 + i * 32 + l32) * LD + kk * 16 + kh * 8]);
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+                b[j] = *reinterpret_cast<const half8_t*>(&bs[(wn * 64 + j * 32 + l32) * LD + kk * 16 + kh * 8]);
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[i], b[j], acc[i][j], 0, 0, 0);
+        }
+        if (kt + 1 < nk) store_stage(buf ^ 1);
+        __syncthreads();
+    }
+    // C/D map: col = lane & 31 (n), row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5) (m)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int n = n0 + wn * 64 + j * 32 + l32;
+            if (n >= p.N) continue;
+            const float bias = p.bias ? p.bias[n] : 0.0f;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int m = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * kh;
+                if (m < Mact) p.C[(size_t)m * p.ldc + n] = fmaxf(acc[i][j][r] + bias, 0.0f);
+            }
+        }
+}
+
+void az_launch_gemm_h16_relu(const GemmArgs& p, hipStream_t st) {
+    const int nbm = (p.M + 127) / 128, nbn = (p.N + 127) / 128;
+    hipLaunchKernelGGL(gemm_h16_relu, dim3(nbm * nbn), dim3(256), 0, st, p);
+}
+
 // Squeeze-and-excitation + residual + ReLU of a DDW-RandWire node (row f4;
 // ddw_randwire_resnet.cpp:10-32 SEBlock, :53-61 ResidualBlock::forward):
 //   s = sigmoid(W2 relu(W1 mean_hw(y) + b1) + b2),  out = relu(y * s + x)
