@@ -246,3 +246,35 @@ def test_host_api_script_matches_reference():
                for a, ch in zip(r.actions, r.children)]
         assert got == op["children"], (k, op["op"])
     assert "Node: V=" in m.getRootNode().toString(1)
+
+
+@pytest.mark.gpu
+def test_host_create_ddw_randwire():
+    """createDDWRandWireResNet (TorchNeuralNetwork::createDDWRandWireResNet,
+    torch_neural_network.cpp:799-814) through the host module: predictBatch on GomokuStates ==
+    softmax of the rand-wire oracle (pinned to the reference C++ module), and ParallelMCTS searches
+    with it."""
+    import az_amd
+    import net_oracle
+    import randwire_oracle as RW
+    net = az.createDDWRandWireResNet(11, 81, channels=16, num_blocks=2, board_size=9, max_batch=4)
+    net.initRandom(5)
+    desc = az_amd.randwire_net_desc(9, 16, 2, 11, 4)
+    blob = RW.init_blob(desc, RW.load_graphs(), 5)
+    states = []
+    rng = np.random.default_rng(3)
+    for i in range(4):
+        s = az.GomokuState(9)
+        for _ in range(i * 5):
+            s.makeMove(int(rng.choice(s.getLegalMoves())))
+        states.append(s)
+    pol, val = net.predictBatch(states)
+    x = np.stack([np.asarray(s.getEnhancedTensorRepresentation(), np.float32) for s in states])
+    rl, rv = RW.forward(desc, RW.load_graphs(), blob, x)
+    assert np.abs(np.asarray(pol) - net_oracle.softmax_policy(rl)).max() <= 1e-4
+    assert np.abs(np.asarray(val) - rv).max() <= 1e-4
+    m = az.ParallelMCTS(az.GomokuState(9), net, None, 1, 64, 1.5, 0.0, 3)
+    m.setDeterministicMode(True)
+    m.search()
+    probs = np.asarray(m.getActionProbabilities(1.0), np.float64)
+    assert abs(probs.sum() - 1.0) < 1e-5 and m.selectAction(True, 1.0) in az.GomokuState(9).getLegalMoves()
