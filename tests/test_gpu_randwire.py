@@ -149,12 +149,56 @@ def test_gpu_randwire_rejects_bad_desc():
     eng.close()
 
 
+def _scale_heads(desc, blob, factors):
+    """Trained-scale outputs: head FC weights scaled (|logit| ~5-10, value away from 0)."""
+    import randwire_oracle as RW
+    blob = blob.copy()
+    off = 0
+    for name, shape, _, _ in RW.param_shapes(desc, RW.load_graphs()):
+        n = int(np.prod(shape))
+        if name in factors:
+            blob[off:off + n] *= np.float32(factors[name])
+        off += n
+    return blob
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("prec", ["f32", "fp16"])
+def test_gpu_randwire_trained_scale(prec):
+    """Logits of order 5-10 (head FC weights scaled): the fp32 path stays within 1e-4 relative to
+    the logit scale; the fp16 throughput mode's error is reported and bounded."""
+    import az_amd
+    import randwire_oracle as RW
+    eng = az_amd.Engine(0)
+    B = 8
+    net = _net(eng, 15, 128, 3, B)
+    if prec == "fp16":
+        net.set_precision(az_amd.AZ_PREC_FP16)
+    net.init_random(77)
+    blob = _scale_heads(net.desc, net.get_weights(), {"policy_fc.weight": 100.0, "value_fc1.weight": 8.0})
+    net.load_weights(blob)
+    planes = (np.random.default_rng(77).random((B, 11, 15, 15)) < 0.3).astype(np.float32)
+    lo, v = net.forward(planes)
+    rl, rv = RW.forward(net.desc, RW.load_graphs(), blob, planes)
+    scale = float(np.abs(rl).max())
+    dl, dv = float(np.abs(lo - rl).max()), float(np.abs(v - rv).max())
+    print(f"trained-scale rand-wire {prec}: |logit| max {scale:.3g}, |value| max {np.abs(rv).max():.3g}, "
+          f"max|dlogit| {dl:.3g}, max|dvalue| {dv:.3g}")
+    assert scale > 3.0
+    if prec == "f32":
+        assert dl <= 1e-4 * scale and dv <= 1e-4
+    else:
+        assert dl <= 1e-2 * scale and dv <= 1e-2
+    net.close()
+    eng.close()
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("nb,B", [(2, 16), (20, 3)])
 def test_gpu_randwire_fp16_error(nb, B):
-    """AZ_PREC_FP16 rand-wire (node convs on conv3x3_v4 with fp16 operands and fp32 accumulation;
-    routers, SE and the residual stream fp32): a throughput mode.  Its error against the fp32
-    reference arithmetic is measured and bounded here; the parity precision is AZ_PREC_F32."""
+    """AZ_PREC_FP16 rand-wire (node convs on conv3x3_v4, routers on gemm_h16_relu: fp16 operands,
+    fp32 accumulation; SE and the residual stream fp32): a throughput mode.  Its error against the
+    fp32 reference arithmetic is measured and bounded here; the parity precision is AZ_PREC_F32."""
     import az_amd
     import randwire_oracle as RW
     eng = az_amd.Engine(0)
