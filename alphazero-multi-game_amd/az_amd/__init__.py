@@ -99,12 +99,26 @@ def randwire_graph(block):
 class HipNeuralNetwork:
     """NeuralNetwork plugin on the MI355X ConvNet kernels."""
 
-    def __init__(self, engine, desc, randwire=False):
+    def __init__(self, engine, desc, randwire=False, graphs=None):
+        """randwire: the DDW-RandWire net with the reference C++ wiring; graphs: explicit wiring per
+        block (dicts with "nodes" (registration order), "preds" {node: [...]}, "output_nodes")."""
         self.engine = engine
         self.desc = desc
         h = ctypes.c_void_p()
-        create = lib().az_net_create_randwire if randwire else lib().az_net_create
-        check(create(engine.h, ctypes.byref(desc), ctypes.byref(h)))
+        if graphs is not None:
+            flat = []
+            for g in graphs[:desc.blocks]:
+                n = len(g["nodes"])
+                flat += [n] + list(g["nodes"])
+                for v in range(n):
+                    p = list(g["preds"][v])
+                    flat += [len(p)] + p
+                flat += [len(g["output_nodes"])] + list(g["output_nodes"])
+            arr = (ctypes.c_int * max(1, len(flat)))(*flat)
+            check(lib().az_net_create_randwire_graphs(engine.h, ctypes.byref(desc), arr, len(flat), ctypes.byref(h)))
+        else:
+            create = lib().az_net_create_randwire if randwire else lib().az_net_create
+            check(create(engine.h, ctypes.byref(desc), ctypes.byref(h)))
         self.h = h
         n = ctypes.c_size_t()
         check(lib().az_net_num_params(self.h, ctypes.byref(n)))

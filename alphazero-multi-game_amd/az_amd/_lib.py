@@ -50,6 +50,7 @@ EXPORTS = {
     "az_engine_device_name": (c_int, [vp, ctypes.c_char_p, c_int]),
     "az_net_create": (c_int, [vp, P(NetDesc), P(vp)]),
     "az_net_create_randwire": (c_int, [vp, P(NetDesc), P(vp)]),
+    "az_net_create_randwire_graphs": (c_int, [vp, P(NetDesc), P(c_int), c_size_t, P(vp)]),
     "az_randwire_graph": (c_int, [c_int, P(c_int), P(c_int), P(c_int), P(c_int), P(c_int), P(c_int), P(c_int), P(c_int),
                                   c_int]),
     "az_net_destroy": (None, [vp]),

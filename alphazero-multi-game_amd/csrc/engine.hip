@@ -1094,7 +1094,8 @@ static int check_precision(const az_net_desc& d, int precision) {
     return 0;
 }
 
-static int net_create(az_engine* e, const az_net_desc* d, az_net** out, bool rw) {
+static int net_create(az_engine* e, const az_net_desc* d, az_net** out, bool rw,
+                      const std::vector<azrw::Plan>* plans = nullptr) {
     if (!e || !d || !out) return az_fail(AZ_ERR_ARG, "null argument");
     if (d->board_size < 2 || d->board_size * d->board_size > AZ_MAXA || d->in_planes < 1 || d->in_planes > 128 ||
         d->channels < 4 || d->channels % 4 || d->blocks < 0 || d->action_size < 1 || d->action_size > 8192 ||
@@ -1117,7 +1118,7 @@ static int net_create(az_engine* e, const az_net_desc* d, az_net** out, bool rw)
     if (rw) {
         n->rwb.resize(d->blocks);
         for (int i = 0; i < d->blocks; ++i) {
-            n->rwb[i].plan = azrw::plan(i);
+            n->rwb[i].plan = plans ? (*plans)[i] : azrw::plan(i);
             n->rwb[i].node.resize(n->rwb[i].plan.preds.size());
         }
         n->nparams = 0;
@@ -1152,7 +1153,9 @@ static int net_create(az_engine* e, const az_net_desc* d, az_net** out, bool rw)
     A_(&n->logits, B * d->action_size); A_(&n->value, B); A_(&n->soft, B * d->action_size);
     A_(&n->in_nchw, B * d->in_planes * n->HW);
     if (rw) {
-        n->rw_out.assign(n->rwb.empty() ? 0 : n->rwb[0].node.size(), nullptr);
+        size_t nodes = 0;
+        for (const RwBlock& blk : n->rwb) nodes = std::max(nodes, blk.node.size());
+        n->rw_out.assign(nodes, nullptr);
         for (float*& p : n->rw_out) A_(&p, rows * F);
         A_(&n->rw_t2, rows * F); A_(&n->rw_in, rows * F);
         // Small capacities leave most CUs idle (one 128 x 128 f32 tile of a K = 9F conv is ~60 us
@@ -1204,6 +1207,58 @@ int az_net_create_randwire(az_engine* e, const az_net_desc* d, az_net** out) {
     if (d->channels % 16 || d->channels > 1024) return az_fail(AZ_ERR_ARG, "rand-wire channels: a multiple of 16, <= 1024");
     if (d->pool != std::min(8, d->board_size)) return az_fail(AZ_ERR_ARG, "rand-wire heads pool to min(8, board)");
     return net_create(e, d, out, true);
+}
+
+// Explicit wiring (e.g. the Python DDWRandWireResNet's networkx graphs, python/alphazero/models/
+// ddw_randwire.py:56-116): per block  n, order[n], then for node v = 0..n-1: deg_v, preds[deg_v],
+// then n_out, outputs[n_out].  Inputs are the in-degree-0 nodes in `order`; the compute order is
+// any topological order (a node's output depends only on its inputs).
+int az_net_create_randwire_graphs(az_engine* e, const az_net_desc* d, const int* g, size_t n_ints, az_net** out) {
+    if (!d || !g) return az_fail(AZ_ERR_ARG, "null argument");
+    if (int r = check_rw_precision(*d, d->precision)) return r;
+    std::vector<azrw::Plan> plans(std::max(0, d->blocks));
+    size_t k = 0;
+    auto next = [&](int& v) { if (k >= n_ints) return false; v = g[k++]; return true; };
+    for (int b = 0; b < d->blocks; ++b) {
+        azrw::Plan& pl = plans[b];
+        int n = 0;
+        if (!next(n) || n < 1 || n > 1024) return az_fail(AZ_ERR_ARG, "block %d: bad node count", b);
+        pl.order.resize(n);
+        std::vector<char> seen(n, 0);
+        for (int& v : pl.order) {
+            if (!next(v) || v < 0 || v >= n || seen[v]) return az_fail(AZ_ERR_ARG, "block %d: order is not a permutation", b);
+            seen[v] = 1;
+        }
+        pl.preds.assign(n, {});
+        std::vector<int> indeg(n, 0);
+        std::vector<std::vector<int>> succ(n);
+        for (int v = 0; v < n; ++v) {
+            int deg = 0;
+            if (!next(deg) || deg < 0 || deg > 64) return az_fail(AZ_ERR_ARG, "block %d node %d: bad degree", b, v);
+            for (int j = 0; j < deg; ++j) {
+                int u = 0;
+                if (!next(u) || u < 0 || u >= n) return az_fail(AZ_ERR_ARG, "block %d node %d: bad predecessor", b, v);
+                pl.preds[v].push_back(u);
+                succ[u].push_back(v);
+            }
+            indeg[v] = deg;
+        }
+        int no = 0;
+        if (!next(no) || no < 1 || no > n) return az_fail(AZ_ERR_ARG, "block %d: bad output count", b);
+        pl.outputs.resize(no);
+        for (int& v : pl.outputs)
+            if (!next(v) || v < 0 || v >= n) return az_fail(AZ_ERR_ARG, "block %d: bad output node", b);
+        for (int v : pl.order)
+            if (pl.preds[v].empty()) pl.inputs.push_back(v);
+        std::vector<int> q = pl.inputs;   // Kahn over `order`
+        for (size_t h = 0; h < q.size(); ++h)
+            for (int w : succ[q[h]])
+                if (--indeg[w] == 0) q.push_back(w);
+        if ((int)q.size() != n) return az_fail(AZ_ERR_ARG, "block %d: the wiring has a cycle", b);
+        pl.topo = q;
+    }
+    if (k != n_ints) return az_fail(AZ_ERR_ARG, "graph description: %zu ints read, %zu given", k, n_ints);
+    return net_create(e, d, out, true, &plans);
 }
 
 int az_randwire_graph(int block, int* order, int* topo, int* inputs, int* n_inputs, int* outputs, int* n_outputs,

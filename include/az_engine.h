@@ -87,6 +87,13 @@ int az_net_create(az_engine* e, const az_net_desc* desc, az_net** out);
  * reference module's state_dict order (num_batches_tracked dropped); every other az_net_* call and
  * the search take the handle as for az_net_create. */
 int az_net_create_randwire(az_engine* e, const az_net_desc* desc, az_net** out);
+/* The same net with explicit wiring, e.g. the graphs of a Python DDWRandWireResNet
+ * (python/alphazero/models/ddw_randwire.py:56-116, networkx Watts-Strogatz + DiGraph): per block
+ * n, order[n] (router / block registration order), for node v = 0..n-1: deg_v, preds[deg_v]
+ * (concat order), n_out, outputs[n_out] (output-router concat order); n_ints in total.  Inputs
+ * are the in-degree-0 nodes in `order`.  AZ_ERR_ARG on a malformed or cyclic wiring. */
+int az_net_create_randwire_graphs(az_engine* e, const az_net_desc* desc, const int* graphs, size_t n_ints,
+                                  az_net** out);
 /* Host only (no device needed): the wiring of rand-wire block `block` (RandWireBlock::_generate_graph,
  * :248-319, with the duplicate-edge test evaluated as written -- DESIGN.md §5c).  order[32] = nodes()
  * order (router / block registration order), topo[32], inputs / outputs (in-/out-degree 0), the

@@ -217,3 +217,71 @@ def test_gpu_randwire_fp16_error(nb, B):
     assert np.array_equal(lo2.view(np.uint32), lo[[B - 1, 0]].view(np.uint32))
     net.close()
     eng.close()
+
+
+def _custom_graph(n, seed):
+    """A Python-DDWRandWireResNet-like wiring (networkx DiGraph semantics: no duplicate edges,
+    nodes in edge-insertion order, predecessors in insertion order): edges low -> high id."""
+    rng = np.random.default_rng(seed)
+    edges = []
+    for v in range(1, n):
+        for u in rng.choice(v, size=min(v, int(rng.integers(1, 4))), replace=False):
+            edges.append((int(u), v))
+    rng.shuffle(edges)
+    order, preds = [], {v: [] for v in range(n)}
+    for u, v in edges:
+        for w in (u, v):
+            if w not in order:
+                order.append(w)
+        preds[v].append(u)
+    for v in range(n):
+        if v not in order:
+            order.append(v)
+    succ = {v: [] for v in range(n)}
+    for u, v in edges:
+        succ[u].append(v)
+    inputs = [v for v in order if not preds[v]]
+    outputs = [v for v in order if not succ[v]]
+    indeg = {v: len(preds[v]) for v in range(n)}
+    topo = list(inputs)
+    for u in topo:
+        for w in succ[u]:
+            indeg[w] -= 1
+            if indeg[w] == 0:
+                topo.append(w)
+    return {"nodes": order, "preds": preds, "input_nodes": inputs, "output_nodes": outputs, "topo": topo}
+
+
+@pytest.mark.gpu
+def test_gpu_randwire_explicit_graphs():
+    """az_net_create_randwire_graphs: the reference wiring passed explicitly reproduces
+    az_net_create_randwire bit for bit; a networkx-style custom wiring (12 and 20 nodes, several
+    sinks) matches the oracle; a cyclic wiring is refused."""
+    import az_amd
+    import randwire_oracle as RW
+    eng = az_amd.Engine(0)
+    B = 5
+    planes = (np.random.default_rng(9).random((B, 11, 9, 9)) < 0.3).astype(np.float32)
+    ref = _net(eng, 9, 32, 2, B)
+    ref.init_random(21)
+    lo0, v0 = ref.forward(planes)
+    exp = az_amd.HipNeuralNetwork(eng, az_amd.randwire_net_desc(9, 32, 2, 11, B), graphs=RW.load_graphs())
+    assert exp.num_params == ref.num_params
+    exp.load_weights(ref.get_weights())
+    lo1, v1 = exp.forward(planes)
+    assert np.array_equal(lo0.view(np.uint32), lo1.view(np.uint32)) and np.array_equal(v0.view(np.uint32), v1.view(np.uint32))
+    graphs = [_custom_graph(12, 1), _custom_graph(20, 2)]
+    assert all(len(g["output_nodes"]) > 1 for g in graphs)
+    d = az_amd.randwire_net_desc(9, 32, 2, 11, B)
+    net = az_amd.HipNeuralNetwork(eng, d, graphs=graphs)
+    blob = RW.init_blob(d, graphs, 4)
+    net.load_weights(blob)
+    lo, v = net.forward(planes)
+    rl, rv = RW.forward(d, graphs, blob, planes)
+    assert np.abs(lo - rl).max() <= 1e-4 and np.abs(v - rv).max() <= 1e-4
+    bad = [dict(graphs[0], preds={**graphs[0]["preds"], 0: [graphs[0]["topo"][-1]]}), graphs[1]]
+    with pytest.raises(az_amd.AzError):
+        az_amd.HipNeuralNetwork(eng, d, graphs=bad)
+    for x in (ref, exp, net):
+        x.close()
+    eng.close()
