@@ -82,8 +82,10 @@ int az_net_create(az_engine* e, const az_net_desc* desc, az_net** out);
  * blocks) of src/nn/ddw_randwire_resnet.cpp:387-468 (TorchNeuralNetwork::createDDWRandWireResNet,
  * torch_neural_network.cpp:799-814).  Each of `blocks` rand-wire blocks is RandWireBlock(channels,
  * 32 nodes, p = 0.75, seed = block index) (:399): 32 SE residual blocks wired by a rewired
- * Watts-Strogatz graph with routers.  desc: conv_bias 0, precision AZ_PREC_F32, pool = min(8, board)
- * (the reference: head_channels 32, fc_hidden 256); residual is ignored.  The blob is the
+ * Watts-Strogatz graph with routers.  desc: conv_bias 0, pool = min(8, board), precision AZ_PREC_F32
+ * (the module's arithmetic; parity mode) or AZ_PREC_FP16 (15x15, channels % 64 == 0: fp16-operand node
+ * convs and routers, fp32 SE / residual stream; throughput mode); the reference's heads are
+ * head_channels 32, fc_hidden 256; residual is ignored.  The blob is the
  * reference module's state_dict order (num_batches_tracked dropped); every other az_net_* call and
  * the search take the handle as for az_net_create. */
 int az_net_create_randwire(az_engine* e, const az_net_desc* desc, az_net** out);
