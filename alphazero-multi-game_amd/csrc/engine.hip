@@ -479,6 +479,25 @@ float* rw_trunk(az_net* n, int B, const int* nb, hipStream_t st) {
                 az_launch_se_residual(n->rw_t2, in, n->rw_out[v], nd.w1, nd.b1, nd.w2, nd.b2, B, HW, F, R, nb, st);
                 return;
             }
+            if (d.precision == AZ_PREC_BF16X3 && d.max_batch >= 128) {
+                // fp32-faithful: operands split into bf16 hi + lo, three MFMAs per product, fp32
+                // accumulation (conv3x3_v4 mode 0); conv1 -> split t, conv2 -> fp32 y.  Below 128
+                // boards of capacity v4 has too few tiles (one per two boards) and the K-split f32
+                // GEMM below is faster (chosen by capacity: batch-size independent)
+                az_launch_split_bf16(in, n->hh[0], n->hl[0], (size_t)rows * F, nb, HW, F, st);
+                ConvBf16Args a{};
+                a.Ahi = n->hh[0]; a.Alo = n->hl[0]; a.Bhi = nd.c1.Whi; a.Blo = nd.c1.Wlo; a.Bblk = nd.c1.Wbk_bf;
+                a.Chi = n->th; a.Clo = n->tl; a.bias = nd.c1.b;
+                a.M = rows; a.N = F; a.C = F; a.H = H; a.W = H; a.m_limit = nb; a.rows_per_sample = HW; a.relu = 1;
+                a.zero = n->zero; a.stamp = -1;
+                az_conv_v4_launch(a, 0, st);
+                ConvBf16Args c = a;
+                c.Ahi = n->th; c.Alo = n->tl; c.Bhi = nd.c2.Whi; c.Blo = nd.c2.Wlo; c.Bblk = nd.c2.Wbk_bf;
+                c.Chi = n->hh[1]; c.Clo = n->hl[1]; c.Cf = n->rw_t2; c.bias = nd.c2.b; c.relu = 0;
+                az_conv_v4_launch(c, 0, st);
+                az_launch_se_residual(n->rw_t2, in, n->rw_out[v], nd.w1, nd.b1, nd.w2, nd.b2, B, HW, F, R, nb, st);
+                return;
+            }
             GemmArgs g1 = gemm_args(nd.c1, in, F, n->t, F, nullptr, rows, H, H, nb, HW);
             GemmArgs g2 = gemm_args(nd.c2, n->t, F, n->rw_t2, F, nullptr, rows, H, H, nb, HW);
             if (n->rw_ws) { g1.part = g2.part = n->rw_ws; g1.splits = g2.splits = n->rw_splits; }
@@ -1192,12 +1211,16 @@ static int net_create(az_engine* e, const az_net_desc* d, az_net** out, bool rw,
 
 int az_net_create(az_engine* e, const az_net_desc* d, az_net** out) { return net_create(e, d, out, false); }
 
-// Rand-wire precisions: AZ_PREC_F32 (the reference module's arithmetic), or AZ_PREC_FP16 node convs
-// (conv3x3_v4: 15x15 boards, channels % 64 == 0) with the fp32 residual stream, routers and SE.
+// Rand-wire precisions: AZ_PREC_F32 (the reference module's arithmetic, any shape), or on 15x15
+// with channels % 64 == 0 the conv3x3_v4 node convs: AZ_PREC_BF16X3 (fp32-faithful split operands,
+// fp32 routers) or AZ_PREC_FP16 (fp16 operands, fp16-operand routers); SE and the residual stream
+// stay fp32 in every mode.
 static int check_rw_precision(const az_net_desc& d, int precision) {
     if (precision == AZ_PREC_F32) return 0;
-    if (precision == AZ_PREC_FP16 && az_conv_v4_supported(d.board_size, d.board_size, d.channels, d.channels)) return 0;
-    return az_fail(AZ_ERR_ARG, "rand-wire nets: AZ_PREC_F32, or AZ_PREC_FP16 on 15x15 with channels %% 64 == 0");
+    if ((precision == AZ_PREC_FP16 || precision == AZ_PREC_BF16X3) &&
+        az_conv_v4_supported(d.board_size, d.board_size, d.channels, d.channels))
+        return 0;
+    return az_fail(AZ_ERR_ARG, "rand-wire nets: AZ_PREC_F32, or AZ_PREC_BF16X3 / AZ_PREC_FP16 on 15x15 with channels %% 64 == 0");
 }
 
 int az_net_create_randwire(az_engine* e, const az_net_desc* d, az_net** out) {
@@ -1417,7 +1440,10 @@ int az_net_trunk_kernel(az_net* n, char* name, int len) {
     const int prec = d.precision, F = d.channels, H = d.board_size;
     const bool bf = (prec == AZ_PREC_BF16X3 || prec == AZ_PREC_BF16 || prec == AZ_PREC_FP16) && F % 32 == 0;
     const bool f16 = prec == AZ_PREC_FP16;
-    if (n->rw) { snprintf(name, len, f16 ? "conv3x3_v4<2, 128, 1>" : "gemm_f32"); return 0; }
+    if (n->rw) {
+        snprintf(name, len, f16 ? "conv3x3_v4<2, 128, 1>" : prec == AZ_PREC_BF16X3 ? "conv3x3_v4<0, 128, 0>" : "gemm_f32");
+        return 0;
+    }
     if (!bf || d.blocks < 1) { snprintf(name, len, "gemm_f32"); return 0; }
     if (f16 && az_smallnet_supported(H, F, n->cin_pad, d.pool, d.head_channels) && d.blocks <= az_smallnet_max_blocks()) {
         snprintf(name, len, "k_smallnet<%d>", H);

@@ -22,6 +22,9 @@ def _net(eng, bs, ch, nb, B, inp=11):
     return az_amd.HipNeuralNetwork(eng, az_amd.randwire_net_desc(bs, ch, nb, inp, B), randwire=True)
 
 
+BF16X3_CAP = 128   # the bf16x3 node convs run on conv3x3_v4 from this capacity up (below: f32 K-split)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("case", GOLD_CASES)
 def test_gpu_randwire_matches_reference_module(case):
@@ -163,7 +166,34 @@ def _scale_heads(desc, blob, factors):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("prec", ["f32", "fp16"])
+@pytest.mark.parametrize("nb,B", [(20, 2), (2, 24)])
+def test_gpu_randwire_bf16x3_matches_oracle(nb, B):
+    """AZ_PREC_BF16X3: node convs on conv3x3_v4 with fp32-faithful split bf16 operands (three MFMAs
+    per product), fp32 routers / SE / residual stream -- the fast parity mode, held to the same
+    1e-4 tolerance as the f32 path, batch-position independent bitwise."""
+    import az_amd
+    import randwire_oracle as RW
+    eng = az_amd.Engine(0)
+    net = _net(eng, 15, 128, nb, BF16X3_CAP)
+    net.set_precision(az_amd.AZ_PREC_BF16X3)
+    net.init_random(500 + nb)
+    blob = net.get_weights()
+    planes = (np.random.default_rng(nb + 1).random((B, 11, 15, 15)) < 0.3).astype(np.float32)
+    lo, v = net.forward(planes)
+    rl, rv = RW.forward(net.desc, RW.load_graphs(), blob, planes)
+    scale = max(1.0, float(np.abs(rl).max()))
+    dl, dv = float(np.abs(lo - rl).max()), float(np.abs(v - rv).max())
+    print(f"bf16x3 rand-wire 128ch {nb} blocks B={B}: |logit| max {np.abs(rl).max():.3g}, max|dlogit| {dl:.3g}, "
+          f"max|dvalue| {dv:.3g}")
+    assert dl <= 1e-4 * scale and dv <= 1e-4
+    lo2, _ = net.forward(planes[[B - 1, 0]])
+    assert np.array_equal(lo2.view(np.uint32), lo[[B - 1, 0]].view(np.uint32))
+    net.close()
+    eng.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("prec", ["f32", "bf16x3", "fp16"])
 def test_gpu_randwire_trained_scale(prec):
     """Logits of order 5-10 (head FC weights scaled): the fp32 path stays within 1e-4 relative to
     the logit scale; the fp16 throughput mode's error is reported and bounded."""
@@ -171,9 +201,9 @@ def test_gpu_randwire_trained_scale(prec):
     import randwire_oracle as RW
     eng = az_amd.Engine(0)
     B = 8
-    net = _net(eng, 15, 128, 3, B)
-    if prec == "fp16":
-        net.set_precision(az_amd.AZ_PREC_FP16)
+    net = _net(eng, 15, 128, 3, BF16X3_CAP if prec == "bf16x3" else B)
+    if prec != "f32":
+        net.set_precision(az_amd.AZ_PREC_FP16 if prec == "fp16" else az_amd.AZ_PREC_BF16X3)
     net.init_random(77)
     blob = _scale_heads(net.desc, net.get_weights(), {"policy_fc.weight": 100.0, "value_fc1.weight": 8.0})
     net.load_weights(blob)
@@ -185,7 +215,7 @@ def test_gpu_randwire_trained_scale(prec):
     print(f"trained-scale rand-wire {prec}: |logit| max {scale:.3g}, |value| max {np.abs(rv).max():.3g}, "
           f"max|dlogit| {dl:.3g}, max|dvalue| {dv:.3g}")
     assert scale > 3.0
-    if prec == "f32":
+    if prec != "fp16":
         assert dl <= 1e-4 * scale and dv <= 1e-4
     else:
         assert dl <= 1e-2 * scale and dv <= 1e-2

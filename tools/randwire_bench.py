@@ -4,8 +4,9 @@ channels=128, num_blocks=20) on 15x15 (src/nn/ddw_randwire_resnet.cpp:387-468) a
 az_net_forward (device-resident weights; planes in / logits + value out over PCIe, small).
 Prints one JSON line: ms per forward (wall, synchronous), boards/s, and the algorithmic FLOP rate
 of the whole forward against the MFMA peak of the precision (MI355X_MICROARCH.md): f32-input MFMA
-157.3 TFLOP/s for --precision f32 (the reference module's arithmetic), dense fp16 2.5 PFLOP/s for
---precision fp16 (node convs on conv3x3_v4; routers, SE and the residual stream stay fp32).  FLOPs counted: every 3x3 conv and router /
+157.3 TFLOP/s for --precision f32 (the reference module's arithmetic), dense bf16 / fp16 2.5 PFLOP/s
+for --precision bf16x3 (fp32-faithful split operands: three MFMAs per product, FLOPs counted once)
+and --precision fp16 (node convs on conv3x3_v4; SE and the residual stream stay fp32).  FLOPs counted: every 3x3 conv and router /
 output-router 1x1 conv (2 * K * N per pixel), the input conv; heads and SE excluded (< 0.1 %)."""
 import argparse
 import json
@@ -42,12 +43,12 @@ def main():
     ap.add_argument("--blocks", type=int, default=20)
     ap.add_argument("--board", type=int, default=15)
     ap.add_argument("--iters", type=int, default=5)
-    ap.add_argument("--precision", default="f32", choices=["f32", "fp16"])
+    ap.add_argument("--precision", default="f32", choices=["f32", "bf16x3", "fp16"])
     a = ap.parse_args()
     eng = az_amd.Engine(int(os.environ.get("LOCAL_RANK", 0)))
     net = az_amd.createDDWRandWireResNet(eng, 11, a.board * a.board, a.channels, a.blocks, a.board, a.batch)
-    if a.precision == "fp16":
-        net.set_precision(az_amd.AZ_PREC_FP16)
+    if a.precision != "f32":
+        net.set_precision(az_amd.AZ_PREC_FP16 if a.precision == "fp16" else az_amd.AZ_PREC_BF16X3)
     net.init_random(7)
     x = (np.random.default_rng(0).random((a.batch, 11, a.board, a.board)) < 0.2).astype(np.float32)
     net.forward(x)
