@@ -83,8 +83,10 @@ int az_net_create(az_engine* e, const az_net_desc* desc, az_net** out);
  * torch_neural_network.cpp:799-814).  Each of `blocks` rand-wire blocks is RandWireBlock(channels,
  * 32 nodes, p = 0.75, seed = block index) (:399): 32 SE residual blocks wired by a rewired
  * Watts-Strogatz graph with routers.  desc: conv_bias 0, pool = min(8, board), precision AZ_PREC_F32
- * (the module's arithmetic; parity mode) or AZ_PREC_FP16 (15x15, channels % 64 == 0: fp16-operand node
- * convs and routers, fp32 SE / residual stream; throughput mode); the reference's heads are
+ * (the module's arithmetic; parity mode), or on 15x15 with channels % 64 == 0 AZ_PREC_BF16X3
+ * (fp32-faithful split-operand node convs from 128 boards of capacity; parity mode) or AZ_PREC_FP16
+ * (fp16-operand node convs and routers; throughput mode) -- SE and the residual stream stay fp32;
+ * the reference's heads are
  * head_channels 32, fc_hidden 256; residual is ignored.  The blob is the
  * reference module's state_dict order (num_batches_tracked dropped); every other az_net_* call and
  * the search take the handle as for az_net_create. */
