@@ -75,3 +75,27 @@ def test_randwire_graph_bad_block():
     import az_amd
     with pytest.raises(az_amd.AzError):
         az_amd.randwire_graph(-1)
+
+
+def test_randwire_explicit_graph_parsing_errors():
+    """az_net_create_randwire_graphs validates the wiring on the host before touching a device:
+    a non-permutation order, a bad predecessor, a cycle and trailing ints are refused by name."""
+    import ctypes
+    import az_amd
+    from az_amd import _lib
+    L = _lib.lib()
+    d = az_amd.randwire_net_desc(9, 16, 1, 11, 4)
+
+    def err(ints):
+        arr = (ctypes.c_int * len(ints))(*ints)
+        h = ctypes.c_void_p()
+        rc = L.az_net_create_randwire_graphs(None, ctypes.byref(d), arr, len(ints), ctypes.byref(h))
+        return rc, L.az_last_error().decode()
+
+    ok = [3, 0, 1, 2, 0, 1, 0, 2, 0, 1, 1, 2]   # 0 -> 1, {0, 1} -> 2, sink 2
+    rc, msg = err(ok)
+    assert rc == -1 and "null argument" in msg          # valid wiring: fails only at the null engine
+    assert "permutation" in err([3, 0, 0, 2] + ok[4:])[1]
+    assert "predecessor" in err([3, 0, 1, 2, 0, 1, 7, 2, 0, 1, 1, 2])[1]
+    assert "cycle" in err([3, 0, 1, 2, 1, 2, 1, 0, 1, 1, 1, 2])[1]
+    assert "ints read" in err(ok + [5])[1]
