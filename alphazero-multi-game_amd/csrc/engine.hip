@@ -1441,7 +1441,8 @@ int az_net_trunk_kernel(az_net* n, char* name, int len) {
     const bool bf = (prec == AZ_PREC_BF16X3 || prec == AZ_PREC_BF16 || prec == AZ_PREC_FP16) && F % 32 == 0;
     const bool f16 = prec == AZ_PREC_FP16;
     if (n->rw) {
-        snprintf(name, len, f16 ? "conv3x3_v4<2, 128, 1>" : prec == AZ_PREC_BF16X3 ? "conv3x3_v4<0, 128, 0>" : "gemm_f32");
+        const bool v4x3 = prec == AZ_PREC_BF16X3 && d.max_batch >= 128;   // as rw_trunk dispatches
+        snprintf(name, len, f16 ? "conv3x3_v4<2, 128, 1>" : v4x3 ? "conv3x3_v4<0, 128, 0>" : "gemm_f32");
         return 0;
     }
     if (!bf || d.blocks < 1) { snprintf(name, len, "gemm_f32"); return 0; }
