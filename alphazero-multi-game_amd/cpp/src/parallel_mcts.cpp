@@ -151,7 +151,14 @@ void ParallelMCTS::rebuild() {
         if (!g || g->getKomi() != 7.5f || !g->isChineseRules() || !g->isEnforcingSuperko())
             throw std::invalid_argument("ParallelMCTS: the device Go rules are komi 7.5, Chinese rules, superko");
     }
-    if (s_) { az_search_destroy(s_); s_ = nullptr; }
+    // rng_ survives the rebuild (the reference's setters leave it alone): carried over whole
+    std::vector<uint32_t> rng;
+    if (s_) {
+        rng.resize(AZ_RNG_STATE_WORDS);
+        check(az_search_get_rng(s_, 0, rng.data()), "az_search_get_rng");
+        az_search_destroy(s_);
+        s_ = nullptr;
+    }
     const DeviceEvaluator ev = deviceEvaluator(nn_);
     const az_search_cfg c = deviceConfig();
     check(az_search_create(ev.engine, ev.net, &c, &s_), "az_search_create");
@@ -163,6 +170,7 @@ void ParallelMCTS::rebuild() {
         int t = 0, r = 0;
         check(az_search_apply(s_, &a, &t, &r), "az_search_apply");
     }
+    if (!rng.empty()) check(az_search_set_rng(s_, 0, rng.data()), "az_search_set_rng");
     searched_ = false;
 }
 

@@ -1536,6 +1536,36 @@ __global__ void k_to_g8(const float* in, uint16_t* hi, int8_t* q, int C, int HW,
     }
 }
 
+// fp32 NHWC [B*HW][C] -> g8 bf16 hi + lo planes (AZ_PREC_BF16X3: hi = bf16(x), lo = bf16(x - hi))
+__global__ void k_to_g8x3(const float* in, uint16_t* hi, uint16_t* lo, int C, int HW, const int* m_limit, int maxB) {
+    const int G = C / 8;
+    const int B = m_limit ? min(*m_limit, maxB) : maxB;
+    const size_t total = (size_t)B * G * HW;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+        const int pix = (int)(i % HW);
+        const size_t bg = i / HW;
+        const int g = (int)(bg % G);
+        const size_t b = bg / G;
+        const float* src = in + (b * HW + pix) * C + g * 8;
+        const float4 v0 = *reinterpret_cast<const float4*>(src);
+        const float4 v1 = *reinterpret_cast<const float4*>(src + 4);
+        const float f[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+        uint16_t h[8], l[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            h[e] = Half16<1>::from_f(f[e]);
+            l[e] = Half16<1>::from_f(f[e] - Half16<1>::to_f(h[e]));
+        }
+        *reinterpret_cast<uint4*>(hi + i * 8) = *reinterpret_cast<const uint4*>(h);
+        *reinterpret_cast<uint4*>(lo + i * 8) = *reinterpret_cast<const uint4*>(l);
+    }
+}
+
+void az_launch_to_g8x3(const float* in, uint16_t* hi, uint16_t* lo, int C, int HW, const int* m_limit, int maxB,
+                       hipStream_t st) {
+    hipLaunchKernelGGL(k_to_g8x3, dim3(2048), dim3(256), 0, st, in, hi, lo, C, HW, m_limit, maxB);
+}
+
 void az_launch_to_g8(const float* in, uint16_t* hi, int8_t* q, int C, int HW, const int* m_limit, int maxB, int mode,
                      hipStream_t st) {
     if (mode == 2) hipLaunchKernelGGL(k_to_g8<2>, dim3(2048), dim3(256), 0, st, in, hi, q, C, HW, m_limit, maxB);
@@ -1580,6 +1610,7 @@ void az_launch_rec_to_g8(const uint8_t* rec, const int* gidx, uint16_t* hi, int 
 // H*W x 32 values are read once, coalesced per 8-channel group, joined to fp32 in LDS (row stride
 // 36 floats: conflict-free 16-byte writes; H*W*144 B of dynamic LDS), then every output sums its
 // window from LDS in the same order as before (y-major, then x; / kh / kw).
+// MODE 0 (AZ_PREC_BF16X3): q is the bf16 lo plane (uint16 elements), x = hi + lo.
 template <int MODE>
 __global__ __launch_bounds__(256) void k_pool_g8(const uint16_t* hi, const int8_t* q, float* out, int C, int H, int P,
                                                  const int* m_limit, int maxB) {
@@ -1593,12 +1624,19 @@ __global__ __launch_bounds__(256) void k_pool_g8(const uint16_t* hi, const int8_
         const int gl = idx / HW, pix = idx - gl * HW;
         const size_t e = ((size_t)(b * G + sl * 4 + gl) * HW + pix) * 8;
         uint16_t h[8];
-        int8_t r[8];
-        *reinterpret_cast<uint4*>(h) = *reinterpret_cast<const uint4*>(hi + e);
-        *reinterpret_cast<uint2*>(r) = *reinterpret_cast<const uint2*>(q + e);
         float v[8];
+        *reinterpret_cast<uint4*>(h) = *reinterpret_cast<const uint4*>(hi + e);
+        if constexpr (MODE == 0) {
+            uint16_t l[8];
+            *reinterpret_cast<uint4*>(l) = *reinterpret_cast<const uint4*>(reinterpret_cast<const uint16_t*>(q) + e);
 #pragma unroll
-        for (int k = 0; k < 8; ++k) v[k] = Half16<MODE>::join(h[k], r[k]);
+            for (int k = 0; k < 8; ++k) v[k] = Half16<1>::to_f(h[k]) + Half16<1>::to_f(l[k]);
+        } else {
+            int8_t r[8];
+            *reinterpret_cast<uint2*>(r) = *reinterpret_cast<const uint2*>(q + e);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) v[k] = Half16<MODE>::join(h[k], r[k]);
+        }
         float* d = f + pix * SL + gl * 8;
         *reinterpret_cast<float4*>(d) = make_float4(v[0], v[1], v[2], v[3]);
         *reinterpret_cast<float4*>(d + 4) = make_float4(v[4], v[5], v[6], v[7]);
@@ -1630,6 +1668,7 @@ void az_launch_pool_g8(const uint16_t* hi, const int8_t* q, float* out, int B, i
     const int grid = B * (C / 32);
     const size_t lds = (size_t)H * H * 36 * sizeof(float);
     if (mode == 2) hipLaunchKernelGGL(k_pool_g8<2>, dim3(grid), dim3(256), lds, st, hi, q, out, C, H, P, m_limit, B);
+    else if (mode == 0) hipLaunchKernelGGL(k_pool_g8<0>, dim3(grid), dim3(256), lds, st, hi, q, out, C, H, P, m_limit, B);
     else hipLaunchKernelGGL(k_pool_g8<1>, dim3(grid), dim3(256), lds, st, hi, q, out, C, H, P, m_limit, B);
 }
 

@@ -85,7 +85,11 @@ __device__ __forceinline__ void wait_vm(int n) {      // s_waitcnt vmcnt(n), n w
         case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
         case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
         case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
-        default: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+        case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+        case 9: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
+        case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
+        case 11: asm volatile("s_waitcnt vmcnt(11)" ::: "memory"); break;
+        default: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
     }
 }
 
@@ -398,6 +402,309 @@ __global__ __launch_bounds__(256, 2) void conv3x3_v7(ConvBf16Args p) {
     }
 }
 
+// conv3x3_v7x3: the fp32-faithful trunk conv (AZ_PREC_BF16X3) on the v7 tile.
+//
+// Every fp32 operand x is carried as two bf16 planes, hi = bf16(x) and lo = bf16(x - hi), each
+// in the g8 layout (activations) or the chunk-blocked layout (weights), and a product is
+// hi*hi + lo*hi + hi*lo: three v_mfma_f32_16x16x32_bf16 with fp32 accumulation (lo*lo, ~2^-18
+// of the product, is dropped) -- the arithmetic of conv3x3_v4<0>, on v7's geometry:
+//
+//  * tile 256 output rows x 128 channels per 256-thread block, wave tile 128 x 64 (as v7);
+//  * LDS 144 KB: the halo of a 32-channel chunk, hi and lo planes, double-buffered (2 x 40 KB),
+//    and a 4-slot ring of per-tap weight tiles, hi and lo (4 x 16 KB) -- one block per CU.
+//    A tap is 96 MFMAs per wave (3x v7's), so one wave per SIMD keeps the matrix pipe fed, and
+//    every fragment of tap s+1 (24 ds_read_b128: weights hi/lo, both row halves hi/lo) is read
+//    into a second register set during tap s's MFMAs, in three batches of 8 (each batch waits
+//    for the previous one, which is long done by then: never more than 8 LDS reads in flight);
+//  * MFMAs in six units of 16 (Bh*Ah, Bl*Ah, Bh*Al per row half): consecutive MFMAs never
+//    share an accumulator, so no unit waits on the previous one's result;
+//  * epilogue from registers: residual hi + lo joined in fp32, ReLU, re-split into hi / lo,
+//    streaming stores.
+// Input: p.Ahi / p.Alo (g8 hi / lo, both with zeroed tails at p.a_tail), p.Bblk / p.Bblk_lo,
+// residual p.Rhi / p.Rlo (optional), output p.Chi / p.Clo.
+template <int HB, int GEO>
+__global__ __launch_bounds__(256, 1) void conv3x3_v7x3(ConvBf16Args p) {
+    typedef Geom7<HB, GEO> GM;
+    typedef H16<1> H;
+    constexpr bool DENSE = GM::DENSE, SLIM = GM::SLIM;
+    typedef bf16x8 frag;
+    constexpr int BNT = 128, WG = GM::WG, HW = GM::HW, HROWS = GM::HROWS;
+    constexpr int A_PL = 4 * HROWS * 16;                  // one plane of a chunk's halo: 20 KB
+    constexpr int A_BUF = 2 * A_PL;                       // hi + lo: 40 KB
+    constexpr int B_PL = 4 * BNT * 16;                    // one plane of a tap's weights: 8 KB
+    constexpr int B_TAP = 2 * B_PL;                       // hi + lo: 16 KB
+    constexpr int LDS = 2 * A_BUF + 4 * B_TAP;            // 144 KB
+    __shared__ __attribute__((aligned(16))) uint8_t lds[LDS];
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave >> 1, wn = wave & 1;
+    const int nsplit = p.N / BNT;
+    const int xcd = blockIdx.x % 8, slot = blockIdx.x / 8;
+    const int nb = slot % nsplit, tile = (slot / nsplit) * 8 + xcd;   // a tile's channel halves share an XCD
+    const int n0 = nb * BNT;
+    const int nboards = p.m_limit ? *p.m_limit : p.M / HW;
+    if (DENSE ? tile * 256 >= nboards * HW : tile >= nboards) return;
+    const int C = p.C, GI = C / 8, GO = p.N / 8;
+    const int NCH = C / 32, NS = 9 * NCH;
+
+    const uint32_t a_bytes = (uint32_t)p.a_tail, b_bytes = (uint32_t)((size_t)9 * C * p.N * 2);
+    const __amdgpu_buffer_rsrc_t rsA =
+        __builtin_amdgcn_make_buffer_rsrc((void*)p.Ahi, (short)0, (int)(a_bytes + AZ_ACT_TAIL * 2), 0x00020000);
+    const __amdgpu_buffer_rsrc_t rsAl =
+        __builtin_amdgcn_make_buffer_rsrc((void*)p.Alo, (short)0, (int)(a_bytes + AZ_ACT_TAIL * 2), 0x00020000);
+    const __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc((void*)p.Bblk, (short)0, (int)b_bytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rsBl =
+        __builtin_amdgcn_make_buffer_rsrc((void*)p.Bblk_lo, (short)0, (int)b_bytes, 0x00020000);
+    const uint32_t PAD = a_bytes;                         // zeroed tails: padding rows
+
+    auto a_src = [&](int j, int ln) -> uint32_t {         // as conv3x3_v7: halo piece j of this wave
+        const int q = wave + 4 * j, rb = q % 5, g = q / 5;
+        const int hr = rb * 64 + ln;
+        int Y, X, b;
+        bool in;
+        if constexpr (DENSE) {
+            const int gpx = tile * 256 - (HB + 1) + hr;
+            b = gpx >= 0 ? gpx / HW : -1;
+            const int pix = gpx - b * HW;
+            Y = pix / HB + 1; X = pix - (Y - 1) * HB + 1;
+            in = hr < GM::TROWS && gpx >= 0;
+        } else {
+            Y = hr / WG; X = hr - Y * WG;
+            b = tile;
+            in = hr < GM::TROWS;
+        }
+        const bool ok = in && Y >= 1 && Y <= HB && X >= 1 && X <= HB && b < nboards;
+        return ok ? (uint32_t)((((size_t)b * GI + g) * HW + (Y - 1) * HB + (X - 1)) * 16) : PAD;
+    };
+    int b_src[2], b_dst[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const int q = wave + 4 * j, rb = q & 1, g = q >> 1;
+        b_src[j] = (((g >> 1) * 18 + (g & 1)) * p.N + n0 + rb * 64) * 16;
+        b_dst[j] = g * (BNT * 16) + rb * 1024;
+    }
+    const uint32_t lane16 = lane * 16;
+    uint8_t* abuf = lds;
+    uint8_t* bbuf = lds + 2 * A_BUF;
+    auto issueA = [&](int j, int c, int buf) {            // piece j of chunk c's halo, hi and lo planes
+        const int q = wave + 4 * j, rb = q % 5, g = q / 5;
+        int ln = lane;
+        asm volatile("" : "+v"(ln));
+        const uint32_t vo = a_src(j, ln);
+        const int so = __builtin_amdgcn_readfirstlane(c * (4 * HW * 16));
+        uint8_t* dst = abuf + buf * A_BUF + g * (HROWS * 16) + rb * 1024;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (lds_void_t*)dst, 16, (int)vo, so, 0, 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsAl, (lds_void_t*)(dst + A_PL), 16, (int)vo, so, 0, 0);
+    };
+    auto issueB = [&](int s, int slot) {                  // the wave's four pieces of tap s's weights
+        const int c = s / 9, t = s - 9 * c;
+        const int so = __builtin_amdgcn_readfirstlane((36 * c + 2 * t) * p.N * 16);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            uint8_t* dst = bbuf + slot * B_TAP + b_dst[j];
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, (lds_void_t*)dst, 16, (int)lane16, so + b_src[j], 0, 0);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsBl, (lds_void_t*)(dst + B_PL), 16, (int)lane16, so + b_src[j], 0, 0);
+        }
+    };
+
+    f32x4v acc[8][4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const float4 bv = *reinterpret_cast<const float4*>(p.bias + n0 + wn * 64 + j * 16 + 4 * (lane >> 4));
+#pragma unroll
+        for (int i = 0; i < 8; ++i) acc[i][j] = f32x4v{bv.x, bv.y, bv.z, bv.w};
+    }
+
+    const int l16 = lane & 15, lg = lane >> 4;
+    const uint32_t a_lane = lds_addr(abuf) + lg * (HROWS * 16) + (wm * 128 + l16) * 16;
+    const uint32_t b_lane = lds_addr(bbuf) + lg * (BNT * 16) + (wn * 64 + l16) * 16;
+    uint32_t mbits = 0;
+    if constexpr (DENSE) {
+#pragma unroll
+        for (int f = 0; f < 8; ++f) {
+            const int gq = tile * 256 + wm * 128 + f * 16 + l16;
+            const int pix = gq % HW, y = pix / HB, x = pix - y * HB;
+            mbits |= ((x == 0 ? 1u : 0u) | (x == HB - 1 ? 2u : 0u) | (y == 0 ? 4u : 0u) | (y == HB - 1 ? 8u : 0u)) << (4 * f);
+        }
+    }
+
+    // prologue: halo of chunk 0 (hi + lo), weights of taps 0..3
+#pragma unroll
+    for (int j = 0; j < 5; ++j) issueA(j, 0, 0);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) issueB(s, s);
+    wait_vm(12);                                          // A(0), B(0) landed; B(1..3) may fly
+    __builtin_amdgcn_s_barrier();
+
+    // fragment registers, double-buffered by tap parity: a[buf][row half][plane][i], bw[buf][plane][j]
+    frag a[2][2][2][4], bw[2][2][4];
+    auto maskA = [&](frag (&x)[4], int half, int dy, int dx) {
+        if constexpr (DENSE) {
+            const uint32_t test = (dy == 0 ? 4u : dy == 2 ? 8u : 0u) | (dx == 0 ? 1u : dx == 2 ? 2u : 0u);
+            if (test) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    if (mbits & (test << (4 * (half * 4 + i)))) x[i] = frag{};
+            }
+        }
+    };
+    const uint32_t z16 = (SLIM && wm == 1) ? 16 * 16 : 0;  // SLIM: 16th fragment reads all-zero halo rows
+    auto loadA = [&](frag (&x)[4], uint32_t ab, auto tc, auto hc, auto pc) {
+        constexpr int t = decltype(tc)::value, half = decltype(hc)::value, pl = decltype(pc)::value;
+        constexpr int sh = (t / 3) * WG + (t % 3);
+        static_for<0, 4>([&](auto ic) {
+            constexpr int i = decltype(ic)::value;
+            if constexpr (SLIM && half == 1 && i == 3) ds_rd<pl * A_PL + ((half * 4 + i) * 16 + sh) * 16>(x[i], ab + z16);
+            else ds_rd<pl * A_PL + ((half * 4 + i) * 16 + sh) * 16>(x[i], ab);
+        });
+    };
+    auto loadB = [&](frag (&x)[4], uint32_t bs, auto pc) {
+        constexpr int pl = decltype(pc)::value;
+        static_for<0, 4>([&](auto jc) {
+            constexpr int j = decltype(jc)::value;
+            ds_rd<pl * B_PL + j * 256>(x[j], bs);
+        });
+    };
+    auto mma = [&](const frag (&x)[4], const frag (&b)[4], int half) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                acc[half * 4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], x[i], acc[half * 4 + i][j], 0, 0, 0);
+        }
+    };
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
+    // fragments of tap 0 of chunk 0, in batches of 8 LDS reads
+    loadB(bw[0][0], b_lane, I0{});
+    loadB(bw[0][1], b_lane, I1{});
+    lgkm<0>(bw[0][0]);
+    loadA(a[0][0][0], a_lane, I0{}, I0{}, I0{});
+    loadA(a[0][0][1], a_lane, I0{}, I0{}, I1{});
+    lgkm<0>(a[0][0][0]);
+    loadA(a[0][1][0], a_lane, I0{}, I1{}, I0{});
+    loadA(a[0][1][1], a_lane, I0{}, I1{}, I1{});
+
+    // Two chunks per iteration (18 taps, register sets alternate by tap parity).  DMA as conv3x3_v7
+    // with twice the pieces: a halo piece pair at taps 0..4, four weight pieces per tap; the weights
+    // of tap s+1 were issued in tap s-3, followed by the pieces of taps s-2 and s-1.
+    for (int c2 = 0; c2 < NCH; c2 += 2) {
+        static_for<0, 18>([&](auto tc18) {
+            constexpr int T = decltype(tc18)::value;
+            constexpr int t = T % 9, cur = T & 1, nxt = cur ^ 1;
+            constexpr int allow = 2 * (t >= 2 && t - 2 < 5 ? 1 : 0) + 2 * (t >= 1 && t - 1 < 5 ? 1 : 0) + 8;
+            constexpr int tn = (t + 1) % 9;
+            using TN = std::integral_constant<int, tn>;
+            const int c = c2 + T / 9;
+            const int s = 9 * c + t;
+            if constexpr (DENSE) asm volatile("" : "+v"(mbits));
+            // every fragment of tap s is in registers (the last batch was read before the previous
+            // tap's last MFMA units): required before the barrier frees tap s's weight slot
+            lgkm<0>(a[cur][1][0]);
+            lgkm<0>(a[cur][1][1]);
+            wait_vm(allow);                               // weights of tap s+1 (and at t == 8 the next halo) landed
+            __builtin_amdgcn_s_barrier();
+            __builtin_amdgcn_sched_barrier(0);
+            if constexpr (t < 5) issueA(t, c + 1 < NCH ? c + 1 : c, (c + 1) & 1);
+            issueB(s + 4 < NS ? s + 4 : NS - 1, (s + 4) & 3);
+            // batch 1: the weights of tap s+1 (certified by the barrier above)
+            const uint32_t bn = b_lane + ((s + 1) & 3) * B_TAP;
+            loadB(bw[nxt][0], bn, I0{});
+            loadB(bw[nxt][1], bn, I1{});
+            __builtin_amdgcn_sched_barrier(0);
+            maskA(a[cur][0][0], 0, t / 3, t % 3);
+            maskA(a[cur][0][1], 0, t / 3, t % 3);
+            mma(a[cur][0][0], bw[cur][0], 0);             // hi x hi, row half 0
+            __builtin_amdgcn_sched_barrier(0);
+            lgkm<0>(bw[nxt][0]);
+            lgkm<0>(bw[nxt][1]);
+            // batch 2: row half 0 of tap s+1
+            const uint32_t an = a_lane + ((t == 8 ? c + 1 : c) & 1) * A_BUF;
+            loadA(a[nxt][0][0], an, TN{}, I0{}, I0{});
+            loadA(a[nxt][0][1], an, TN{}, I0{}, I1{});
+            __builtin_amdgcn_sched_barrier(0);
+            mma(a[cur][0][0], bw[cur][1], 0);             // hi(act) x lo(weights)
+            __builtin_amdgcn_sched_barrier(0);
+            mma(a[cur][0][1], bw[cur][0], 0);             // lo(act) x hi(weights)
+            __builtin_amdgcn_sched_barrier(0);
+            lgkm<0>(a[nxt][0][0]);
+            lgkm<0>(a[nxt][0][1]);
+            // batch 3: row half 1 of tap s+1
+            loadA(a[nxt][1][0], an, TN{}, I1{}, I0{});
+            loadA(a[nxt][1][1], an, TN{}, I1{}, I1{});
+            __builtin_amdgcn_sched_barrier(0);
+            maskA(a[cur][1][0], 1, t / 3, t % 3);
+            maskA(a[cur][1][1], 1, t / 3, t % 3);
+            mma(a[cur][1][0], bw[cur][0], 1);
+            __builtin_amdgcn_sched_barrier(0);
+            mma(a[cur][1][0], bw[cur][1], 1);
+            __builtin_amdgcn_sched_barrier(0);
+            mma(a[cur][1][1], bw[cur][0], 1);
+            __builtin_amdgcn_sched_barrier(0);
+        });
+    }
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+
+    // epilogue from the accumulators: residual hi + lo joined in fp32, ReLU, split, streaming stores
+    const __amdgpu_buffer_rsrc_t rh = __builtin_amdgcn_make_buffer_rsrc((void*)p.Rhi, (short)0, 0x7fffffff, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rl = __builtin_amdgcn_make_buffer_rsrc((void*)p.Rlo, (short)0, 0x7fffffff, 0x00020000);
+    const int chl = n0 + wn * 64 + 4 * lg;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const int q = wm * 128 + i * 16 + l16;
+        int b, pix;
+        bool live;
+        if constexpr (DENSE) {
+            const int gq = tile * 256 + q;
+            b = gq / HW;
+            pix = gq - b * HW;
+            live = b < nboards;
+        } else {
+            const int y = q / WG, x = q - y * WG;
+            b = tile;
+            pix = y * HB + x;
+            live = y < HB && x < HB;
+        }
+        if (!live) continue;
+        u32x2_t hv[4], lv[4];
+        if (p.Rhi) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int ch = chl + j * 16;
+                const size_t e = (((size_t)b * GO + (ch >> 3)) * HW + pix) * 8 + (ch & 7);
+                hv[j] = __builtin_amdgcn_raw_buffer_load_b64(rh, (int)(e * 2), 0, 2);
+                lv[j] = __builtin_amdgcn_raw_buffer_load_b64(rl, (int)(e * 2), 0, 2);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int ch = chl + j * 16;
+            const size_t e = (((size_t)b * GO + (ch >> 3)) * HW + pix) * 8 + (ch & 7);
+            float o[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+            if (p.Rhi) {
+                uint16_t hh[4], ll[4];
+                __builtin_memcpy(hh, &hv[j], 8);
+                __builtin_memcpy(ll, &lv[j], 8);
+#pragma unroll
+                for (int k = 0; k < 4; ++k) o[k] += H::to_f(hh[k]) + H::to_f(ll[k]);
+            }
+            uint16_t oh[4], ol[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                o[k] = __builtin_amdgcn_fmed3f(o[k], 0.0f, 3.0e38f);   // ReLU
+                oh[k] = H::from_f(o[k]);
+                ol[k] = H::from_f(o[k] - H::to_f(oh[k]));
+            }
+            u32x2_t hs, ls;
+            __builtin_memcpy(&hs, oh, 8);
+            __builtin_memcpy(&ls, ol, 8);
+            asm volatile("global_store_dwordx2 %0, %1, off nt" ::"v"(p.Chi + e), "v"(hs) : "memory");
+            asm volatile("global_store_dwordx2 %0, %1, off nt" ::"v"(p.Clo + e), "v"(ls) : "memory");
+        }
+    }
+}
+
 // Host side ----------------------------------------------------------------------------------
 template <int HB, int GEO>
 static void v7_launch_g(const ConvBf16Args& a, int mode, hipStream_t st) {
@@ -417,6 +724,38 @@ bool az_conv_v7_supported(const ConvBf16Args& a) {
     // the padding offset walks C/32 chunk steps into the zeroed tail; 32-bit buffer ranges
     return a.a_tail + AZ_ACT_TAIL * 2 < ((size_t)1 << 31) && (size_t)(a.C / 32) * 4 * HW * 16 + 16 <= AZ_ACT_TAIL * 2 &&
            (size_t)9 * a.C * a.N * 2 < ((size_t)1 << 31);
+}
+
+// conv3x3_v7x3 (AZ_PREC_BF16X3 on the g8 hi / lo planes): same shapes as conv3x3_v7, plus the lo
+// planes of the input and the weights and both output planes; a residual needs both of its planes
+bool az_conv_v7x3_supported(const ConvBf16Args& a) {
+    if (a.H != a.W || a.C % 64 || a.N % 128 || !a.relu || a.Cf || a.Cq || a.Rq) return false;
+    if (!a.Ahi || !a.Alo || !a.Bblk || !a.Bblk_lo || !a.Chi || !a.Clo || (!a.Rhi) != (!a.Rlo)) return false;
+    const int HB = a.H;
+    if (HB != 8 && HB != 9 && HB != 13 && HB != 15 && HB != 19) return false;
+    const size_t HW = (size_t)HB * HB;
+    return a.a_tail >= (size_t)a.M * a.C * 2 && a.a_tail + AZ_ACT_TAIL * 2 < ((size_t)1 << 31) &&
+           (size_t)(a.C / 32) * 4 * HW * 16 + 16 <= AZ_ACT_TAIL * 2 && (size_t)9 * a.C * a.N * 2 < ((size_t)1 << 31);
+}
+
+template <int HB, int GEO>
+static void v7x3_launch_g(const ConvBf16Args& a, hipStream_t st) {
+    const int boards = a.M / (HB * HB);
+    const int tiles = GEO == GEO_DENSE ? (boards * HB * HB + 255) / 256 : boards;
+    const int grid = (tiles + 7) / 8 * 8 * (a.N / 128);
+    hipLaunchKernelGGL((conv3x3_v7x3<HB, GEO>), dim3(grid), dim3(256), 0, st, a);
+}
+
+// 15x15 boards on the SLIM tile, every other board DENSE (as conv3x3_v7's defaults)
+int az_conv_v7x3_launch(const ConvBf16Args& a, hipStream_t st) {
+    if (!az_conv_v7x3_supported(a)) return -1;
+    switch (a.H) {
+        case 8: v7x3_launch_g<8, GEO_DENSE>(a, st); return 0;
+        case 9: v7x3_launch_g<9, GEO_DENSE>(a, st); return 0;
+        case 13: v7x3_launch_g<13, GEO_DENSE>(a, st); return 0;
+        case 19: v7x3_launch_g<19, GEO_DENSE>(a, st); return 0;
+        default: v7x3_launch_g<15, GEO_SLIM>(a, st); return 0;
+    }
 }
 
 // geo15: the 15x15 tile geometry (GEO_PAD / GEO_SLIM / GEO_DENSE); other boards are DENSE

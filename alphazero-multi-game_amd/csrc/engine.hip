@@ -12,6 +12,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
+#include <sstream>
 #include <chrono>
 #include <random>
 #include <string>
@@ -59,6 +60,10 @@ void az_launch_rec_planes(const uint8_t* rec, float* dst, const int* eval_games,
                           hipStream_t st);
 void az_launch_pool_g8(const uint16_t* hi, const int8_t* q, float* out, int B, int C, int H, int P, const int* m_limit,
                        int mode, hipStream_t st);
+void az_launch_to_g8x3(const float* in, uint16_t* hi, uint16_t* lo, int C, int HW, const int* m_limit, int maxB,
+                       hipStream_t st);
+bool az_conv_v7x3_supported(const ConvBf16Args& a);
+int az_conv_v7x3_launch(const ConvBf16Args& a, hipStream_t st);
 void az_launch_to_f16(const float* in, uint16_t* out, size_t n, const int* m_limit, int rows_per_sample, int C,
                       hipStream_t st);
 void az_launch_split_bf16(const float* in, uint16_t* hi, uint16_t* lo, size_t n, const int* m_limit, int rows_per_sample,
@@ -96,6 +101,7 @@ struct Layer {            // one implicit-GEMM layer, BN folded
     uint16_t* Whi = nullptr; uint16_t* Wlo = nullptr;   // bf16 split copies (3x3 trunk)
     uint16_t* Wh16 = nullptr;                           // fp16 copy (3x3 trunk, AZ_PREC_FP16)
     uint16_t* Wbk_bf = nullptr; uint16_t* Wbk_h = nullptr;  // chunk-blocked bf16 / fp16 copies (v5 conv)
+    uint16_t* Wbk_lo = nullptr;                         // chunk-blocked bf16 lo parts (conv3x3_v7x3, AZ_PREC_BF16X3)
     float* b = nullptr;   // [N]
     int N = 0, K = 0, Kpad = 0, taps = 1, C = 0;
 };
@@ -253,17 +259,18 @@ int upload_layer(Layer& L, const std::vector<float>& W, const std::vector<float>
         HIPCHK(hipMemcpy(L.Wh16, h16.data(), h16.size() * 2, hipMemcpyHostToDevice));
         if (taps == 9 && C % 16 == 0) {
             // [N][9][C] -> [C/16][9][2][N][8]: one 64-row piece of a chunk/tap/half is 1 KiB contiguous
-            std::vector<uint16_t> bb(W.size()), bh(W.size());
+            std::vector<uint16_t> bb(W.size()), bh(W.size()), bl(W.size());
             for (int o = 0; o < N; ++o)
                 for (int t = 0; t < 9; ++t)
                     for (int c = 0; c < C; ++c) {
                         const size_t src = ((size_t)o * 9 + t) * C + c;
                         const size_t dst = ((((size_t)(c / 16) * 9 + t) * 2 + (c / 8) % 2) * N + o) * 8 + c % 8;
-                        bb[dst] = hi[src]; bh[dst] = h16[src];
+                        bb[dst] = hi[src]; bh[dst] = h16[src]; bl[dst] = lo[src];
                     }
-            if (!L.Wbk_bf) { DALLOC(L.Wbk_bf, W.size()); DALLOC(L.Wbk_h, W.size()); }
+            if (!L.Wbk_bf) { DALLOC(L.Wbk_bf, W.size()); DALLOC(L.Wbk_h, W.size()); DALLOC(L.Wbk_lo, W.size()); }
             HIPCHK(hipMemcpy(L.Wbk_bf, bb.data(), bb.size() * 2, hipMemcpyHostToDevice));
             HIPCHK(hipMemcpy(L.Wbk_h, bh.data(), bh.size() * 2, hipMemcpyHostToDevice));
+            HIPCHK(hipMemcpy(L.Wbk_lo, bl.data(), bl.size() * 2, hipMemcpyHostToDevice));
         }
     }
     return 0;
@@ -418,6 +425,34 @@ static int fc_splits(int B, int K) {
 int net_heads_fc(az_net* n, int B, const int* nb, float* logits, float* value, hipStream_t st,
                  const float* pp = nullptr, const float* vp = nullptr, int xs = 0);
 
+// Trunk conv i (0: first conv of a block, 1: second) of an AZ_PREC_BF16X3 net on the g8 hi / lo
+// planes (conv3x3_v7x3): input / output / residual plane pairs by ping-pong index `cur`.
+ConvBf16Args x3_conv_args(const az_net* n, const Layer& L, int second, int cur, int B, const int* nb) {
+    const az_net_desc& d = n->d;
+    ConvBf16Args a{};
+    a.Ahi = second ? n->th : n->hh[cur]; a.Alo = second ? n->tl : n->hl[cur];
+    a.Bblk = L.Wbk_bf; a.Bblk_lo = L.Wbk_lo;
+    a.Chi = second ? n->hh[cur ^ 1] : n->th; a.Clo = second ? n->hl[cur ^ 1] : n->tl;
+    if (second && d.residual) { a.Rhi = n->hh[cur]; a.Rlo = n->hl[cur]; }
+    a.bias = L.b;
+    a.M = B * n->HW; a.N = d.channels; a.C = d.channels; a.H = d.board_size; a.W = d.board_size;
+    a.m_limit = nb; a.rows_per_sample = n->HW; a.relu = 1;
+    a.a_tail = n->act_elems * 2;
+    a.zero = n->zero;
+    a.stamp = -1;
+    return a;
+}
+// true when an AZ_PREC_BF16X3 net runs its trunk on conv3x3_v7x3 (else the NHWC split path,
+// conv3x3_v4<0>): decided by the shapes alone (the chunk-blocked hi / lo weights exist for every
+// 3x3 layer of a net with channels % 32 == 0 once it is loaded)
+bool x3_trunk(const az_net* n) {
+    const az_net_desc& d = n->d;
+    if (n->rw || d.precision != AZ_PREC_BF16X3 || d.blocks < 1 || !n->hh[0] || d.channels % 32) return false;
+    Layer probe;
+    probe.Wbk_bf = probe.Wbk_lo = n->zero;   // stand-ins for the shape check
+    return az_conv_v7x3_supported(x3_conv_args(n, probe, 1, 0, d.max_batch, nullptr));
+}
+
 // How the forward reads its input planes: NET_IN_SMALL (k_smallnet), NET_IN_G8 (k_to_g8 + the
 // g8 input conv) -- both can build board b's planes from the search's leaf record gidx[b]
 // (leaf_planes.h), so the search hands its leaves over without a plane batch -- or NET_IN_GEMM
@@ -537,6 +572,7 @@ int net_forward(az_net* n, const float* x0, int B, const int* nb, float* logits,
     const bool f16 = prec == AZ_PREC_FP16;
     // g8 path (v5 / v6 conv, fp16/bf16): input conv, trunk and pool all on 16-bit channel-blocked rows
     const bool g8 = !n->rw && bf && prec != AZ_PREC_BF16X3 && az_conv_g8_supported(H, W, F, F);
+    const bool g8x3 = x3_trunk(n);   // AZ_PREC_BF16X3 on the g8 hi / lo planes
     const int mode = f16 ? 2 : 1;
     int8_t* hq[2] = {reinterpret_cast<int8_t*>(n->hl[0]), reinterpret_cast<int8_t*>(n->hl[1])};
     const int inpath = net_input_path(n);
@@ -626,6 +662,22 @@ int net_forward(az_net* n, const float* x0, int B, const int* nb, float* logits,
                                ACT_RELU, d.residual != 0, st);
             std::swap(h, other);
         }
+    } else if (g8x3) {
+        // fp32-faithful trunk: every activation as g8 bf16 hi + lo planes, three MFMAs per product
+        az_launch_to_g8x3(h, n->hh[0], n->hl[0], F, HW, nb, B, st);
+        int cur = 0;
+        for (int i = 0; i < d.blocks; ++i) {
+            ConvBf16Args a = x3_conv_args(n, n->blk[2 * i], 0, cur, B, nb);
+            a.stamp = 2 * i;
+            if (az_conv_v7x3_launch(a, st)) return az_fail(AZ_ERR_ARG, "bf16x3 trunk conv: unsupported shape");
+            ConvBf16Args b2 = x3_conv_args(n, n->blk[2 * i + 1], 1, cur, B, nb);
+            b2.stamp = 2 * i + 1;
+            if (az_conv_v7x3_launch(b2, st)) return az_fail(AZ_ERR_ARG, "bf16x3 trunk conv: unsupported shape");
+            cur ^= 1;
+        }
+        if (ev1) HIPCHK(hipEventRecord(ev1, st));
+        ev1 = nullptr;
+        az_launch_pool_g8(n->hh[cur], reinterpret_cast<const int8_t*>(n->hl[cur]), n->pool, B, F, H, P, nb, 0, st);
     } else {
         const bool split = prec == AZ_PREC_BF16X3;
         if (g8) {
@@ -702,7 +754,7 @@ int net_forward(az_net* n, const float* x0, int B, const int* nb, float* logits,
         }
     }
     if (ev1) HIPCHK(hipEventRecord(ev1, st));
-    if (!g8) az_launch_pool(h, n->pool, B, H, W, F, P, nb, st);
+    if (!g8 && !g8x3) az_launch_pool(h, n->pool, B, H, W, F, P, nb, st);
     const int HC = d.head_channels, HK = HC * PP;
     if (HK % 32 == 0 && n->hpv) {
         // both head 1x1 convs as one GEMM (2 HC outputs; every output is the same k-ordered fp32
@@ -1223,12 +1275,21 @@ static int check_rw_precision(const az_net_desc& d, int precision) {
     return az_fail(AZ_ERR_ARG, "rand-wire nets: AZ_PREC_F32, or AZ_PREC_BF16X3 / AZ_PREC_FP16 on 15x15 with channels %% 64 == 0");
 }
 
+// Every rand-wire create path: the precision, then the shapes the node kernels assume
+// (k_se_residual: C % 16 == 0 for its float4 channel quads, C <= 1024 and R = C / 16 <= 64 for
+// its fixed LDS arrays; no conv bias; the reference's adaptive pool to min(8, board)).
+static int check_rw_desc(const az_net_desc& d) {
+    if (int r = check_rw_precision(d, d.precision)) return r;
+    if (d.conv_bias) return az_fail(AZ_ERR_ARG, "rand-wire convolutions carry no bias (conv_bias = 0)");
+    if (d.channels < 16 || d.channels % 16 || d.channels > 1024)
+        return az_fail(AZ_ERR_ARG, "rand-wire channels: a multiple of 16 in [16, 1024]");
+    if (d.pool != std::min(8, d.board_size)) return az_fail(AZ_ERR_ARG, "rand-wire heads pool to min(8, board)");
+    return 0;
+}
+
 int az_net_create_randwire(az_engine* e, const az_net_desc* d, az_net** out) {
     if (!d) return az_fail(AZ_ERR_ARG, "null argument");
-    if (int r = check_rw_precision(*d, d->precision)) return r;
-    if (d->conv_bias) return az_fail(AZ_ERR_ARG, "rand-wire convolutions carry no bias (conv_bias = 0)");
-    if (d->channels % 16 || d->channels > 1024) return az_fail(AZ_ERR_ARG, "rand-wire channels: a multiple of 16, <= 1024");
-    if (d->pool != std::min(8, d->board_size)) return az_fail(AZ_ERR_ARG, "rand-wire heads pool to min(8, board)");
+    if (int r = check_rw_desc(*d)) return r;
     return net_create(e, d, out, true);
 }
 
@@ -1238,7 +1299,7 @@ int az_net_create_randwire(az_engine* e, const az_net_desc* d, az_net** out) {
 // any topological order (a node's output depends only on its inputs).
 int az_net_create_randwire_graphs(az_engine* e, const az_net_desc* d, const int* g, size_t n_ints, az_net** out) {
     if (!d || !g) return az_fail(AZ_ERR_ARG, "null argument");
-    if (int r = check_rw_precision(*d, d->precision)) return r;
+    if (int r = check_rw_desc(*d)) return r;
     std::vector<azrw::Plan> plans(std::max(0, d->blocks));
     size_t k = 0;
     auto next = [&](int& v) { if (k >= n_ints) return false; v = g[k++]; return true; };
@@ -1324,7 +1385,7 @@ void az_net_destroy(az_net* n) {
     }
     for (float* p : n->rw_out) F(p);
     F(n->rw_t2); F(n->rw_in); F(n->rw_ws);
-    for (Layer* l : ls) { F(l->W); F(l->b); F(l->Whi); F(l->Wlo); F(l->Wh16); F(l->Wbk_bf); F(l->Wbk_h); }
+    for (Layer* l : ls) { F(l->W); F(l->b); F(l->Whi); F(l->Wlo); F(l->Wh16); F(l->Wbk_bf); F(l->Wbk_h); F(l->Wbk_lo); }
     for (void* p : {(void*)n->x0, (void*)n->h0, (void*)n->h1, (void*)n->t, (void*)n->pool, (void*)n->pp, (void*)n->vp, (void*)n->hpv,
                     (void*)n->v1, (void*)n->ws, (void*)n->logits, (void*)n->value, (void*)n->soft, (void*)n->in_nchw, (void*)n->d_nb,
                     (void*)n->hh[0], (void*)n->hh[1], (void*)n->hl[0], (void*)n->hl[1], (void*)n->th, (void*)n->tl,
@@ -1454,6 +1515,10 @@ int az_net_trunk_kernel(az_net* n, char* name, int len) {
     ConvBf16Args a{};
     a.M = d.max_batch * n->HW; a.N = F; a.C = F; a.H = H; a.W = H; a.rows_per_sample = n->HW; a.relu = 1;
     a.a_tail = n->act_elems * 2;
+    if (x3_trunk(n)) {
+        snprintf(name, len, "conv3x3_v7x3<%d, %s>", H, H == 15 ? "SLIM" : "DENSE");
+        return 0;
+    }
     const bool g8 = prec != AZ_PREC_BF16X3 && az_conv_g8_supported(H, H, F, F);
     const int r = g8 ? az_conv_g8_name(a, f16 ? 2 : 1, name, len)
                      : az_conv_bf16_name(a, f16 ? 2 : prec == AZ_PREC_BF16X3 ? 0 : 1, name, len);
@@ -1830,6 +1895,31 @@ int az_search_seed(az_search* s, int game, uint32_t seed) {
     if (!s || game < 0 || game >= s->c.n_games) return az_fail(AZ_ERR_ARG, "bad argument");
     std::lock_guard<std::mutex> lk(s->mu);
     s->rng[game].seed(seed);
+    return 0;
+}
+
+// std::mt19937's state through its stream operators (libstdc++: the 624 state words, then the
+// position), as 625 uint32
+int az_search_get_rng(az_search* s, int game, uint32_t* state) {
+    if (!s || !state || game < 0 || game >= s->c.n_games) return az_fail(AZ_ERR_ARG, "bad argument");
+    std::lock_guard<std::mutex> lk(s->mu);
+    std::ostringstream os;
+    os << s->rng[game];
+    std::istringstream is(os.str());
+    for (int i = 0; i < AZ_RNG_STATE_WORDS; ++i)
+        if (!(is >> state[i])) return az_fail(AZ_ERR_ARG, "rng state: unexpected serialisation");
+    return 0;
+}
+
+int az_search_set_rng(az_search* s, int game, const uint32_t* state) {
+    if (!s || !state || game < 0 || game >= s->c.n_games) return az_fail(AZ_ERR_ARG, "bad argument");
+    std::lock_guard<std::mutex> lk(s->mu);
+    std::ostringstream os;
+    for (int i = 0; i < AZ_RNG_STATE_WORDS; ++i) os << state[i] << (i + 1 < AZ_RNG_STATE_WORDS ? " " : "");
+    std::istringstream is(os.str());
+    std::mt19937 r;
+    if (!(is >> r) || state[AZ_RNG_STATE_WORDS - 1] > 624) return az_fail(AZ_ERR_ARG, "rng state: not an mt19937 state");
+    s->rng[game] = r;
     return 0;
 }
 

@@ -31,6 +31,7 @@ struct ConvBf16Args {
     const uint16_t* Ahi; const uint16_t* Alo;   // [rows][C] bf16 (Alo null for plain bf16)
     const uint16_t* Bhi; const uint16_t* Blo;   // [N][9*C] bf16
     const uint16_t* Bblk;                       // chunk-blocked [C/16][9][2][N][8] (v5; same type as Ahi)
+    const uint16_t* Bblk_lo;                    // conv3x3_v7x3: the bf16 lo parts of Bblk, same layout
     uint16_t* Chi; uint16_t* Clo;               // outputs (split for the next layer)
     float* Cf;                                  // optional fp32 output [rows][N]
     const float* bias;

@@ -227,6 +227,13 @@ int az_search_set_params(az_search* s, const az_search_cfg* cfg);
 /* Reseed game's rng_ (ParallelMCTS::setDeterministicMode, parallel_mcts.cpp:1263-1274: 42, or
  * std::random_device): the std::mt19937 of the Dirichlet draws and of az_search_select_action. */
 int az_search_seed(az_search* s, int game, uint32_t seed);
+/* The full state of game's rng_ (std::mt19937: 624 words + the position, 625 uint32), read and
+ * restored so that a host object that rebuilds its handle (a new evaluator or table) keeps
+ * drawing from the same generator, as the reference's ParallelMCTS keeps rng_ across
+ * setNeuralNetwork / setTranspositionTable (parallel_mcts.h:172-182). */
+#define AZ_RNG_STATE_WORDS 625
+int az_search_get_rng(az_search* s, int game, uint32_t* state);
+int az_search_set_rng(az_search* s, int game, const uint32_t* state);
 /* Root node flags of one game: 1 expanded (MCTSNode::isExpanded), 2 terminal, bits 2..3 the
  * GameResult of a terminal root. */
 #define AZ_NODE_EXPANDED 1

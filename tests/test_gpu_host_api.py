@@ -278,3 +278,29 @@ def test_host_create_ddw_randwire():
     m.search()
     probs = np.asarray(m.getActionProbabilities(1.0), np.float64)
     assert abs(probs.sum() - 1.0) < 1e-5 and m.selectAction(True, 1.0) in az.GomokuState(9).getLegalMoves()
+
+
+@pytest.mark.gpu
+def test_host_rng_survives_rebuild():
+    """setNeuralNetwork / setTranspositionTable rebuild the device handle; rng_ carries over whole
+    (az_search_get_rng / az_search_set_rng), as the reference's setters leave rng_ alone: after
+    three stochastic draws and a rebuild, the next draws equal those of an object never rebuilt
+    (same root, same fresh-evaluator search)."""
+    bs, sims = 9, 64
+    draws = []
+    for rebuild in (False, True):
+        cfg = az.MCTSConfig()
+        cfg.numSimulations = sims
+        net = az.RandomPolicyNetwork(az.GameType.GOMOKU, bs, 7)
+        m = az.ParallelMCTS(az.GomokuState(bs), cfg, net, az.TranspositionTable(1 << 16))
+        m.setDeterministicMode(True)
+        cfg2 = az.MCTSConfig()
+        cfg2.numSimulations = sims
+        cfg2.useBatchInference = False
+        m.setConfig(cfg2)
+        first = [m.selectAction(True, 1.0) for _ in range(3)]
+        if rebuild:
+            m.setNeuralNetwork(net)                   # new handle: tree reset, rng_ kept
+            m.setTranspositionTable(az.TranspositionTable(1 << 16))
+        draws.append((first, [m.selectAction(True, 1.0) for _ in range(8)]))
+    assert draws[0] == draws[1]

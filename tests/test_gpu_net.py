@@ -143,6 +143,45 @@ def test_gpu_c3_net_error_over_many_positions(engine, prec):
     net.close()
 
 
+X3_CASES = [  # (board, in_planes, action_size, channels, blocks, residual, B): conv3x3_v7x3 geometries
+    (15, 11, 225, 128, 2, 1, 9),     # SLIM tile, one board per tile
+    (15, 11, 225, 128, 2, 0, 3),     # plain stack (no residual planes)
+    (19, 8, 362, 128, 2, 1, 5),      # Go: DENSE tiles spanning boards, ragged last tile
+    (9, 11, 81, 256, 1, 1, 7),       # 9x9 DENSE, both channel halves
+    (13, 8, 170, 128, 2, 1, 4),      # 13x13 DENSE
+    (8, 111, 4672, 128, 1, 1, 6),    # Chess shape: the 111-plane input conv on the f32 GEMM
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", X3_CASES, ids=[str(c) for c in X3_CASES])
+def test_gpu_bf16x3_v7x3_geometries(engine, case):
+    """The fp32-faithful trunk (AZ_PREC_BF16X3 on conv3x3_v7x3, g8 hi / lo planes) on every tile
+    geometry it is instantiated for: within 1e-4 of the fp32 reference, and a board's outputs
+    bitwise the same whatever its batch position and tile-mates."""
+    import az_amd
+    import net_oracle
+    bs, ci, A, ch, blocks, res, B = case
+    desc = az_amd.NetDesc(bs, ci, ch, blocks, A, 32, 8, 256, res, 0, az_amd.AZ_PREC_BF16X3, B)
+    net = az_amd.HipNeuralNetwork(engine, desc)
+    if ch % 64 == 0:
+        assert net.trunk_kernel().startswith("conv3x3_v7x3<")
+    blob = net_oracle.init_blob(desc, seed=31)
+    net.load_weights(blob)
+    x = _rand_planes(B, ci, bs, seed=40 + bs, p=0.05 if ci > 16 else 0.25)
+    lo, v = net.forward(x)
+    rl, rv = net_oracle.forward(desc, blob, x)
+    el, ev = float(np.abs(lo - rl).max()), float(np.abs(v - rv).max())
+    print(f"{case} bf16x3: max|dlogit|={el:.3e} (|logit|max {np.abs(rl).max():.3f}) max|dvalue|={ev:.3e}")
+    assert el <= TOL and ev <= TOL
+    perm = np.random.default_rng(bs).permutation(B)
+    lo2, v2 = net.forward(x[perm])
+    assert np.array_equal(lo2, lo[perm]) and np.array_equal(v2, v[perm])
+    lo3, v3 = net.forward(x[B - 2:])
+    assert np.array_equal(lo3, lo[B - 2:]) and np.array_equal(v3, v[B - 2:])
+    net.close()
+
+
 G8_CASES = [  # (board, in_planes, action_size, channels, blocks, B): the g8 conv3x3_v6 board geometries
     (19, 8, 362, 128, 2, 5),      # Go shape (C4: 8 planes, 361 + pass); flattened tiles span boards
     (8, 111, 4672, 128, 2, 9),    # Chess shape (C5: 111 planes, 4672 moves); flattened tiles, v6 input conv
@@ -263,7 +302,9 @@ def test_gpu_c5_net_full_batch(engine):
     ((15, 11, 256, 20, 225, "fp16", 256), "conv3x3_v6<2, 15>"),          # C3 shard at N = 8
     ((15, 11, 64, 6, 225, "fp16", 256), "k_smallnet<15>"),               # C2: the fused 64-filter forward
     ((15, 11, 64, 6, 225, "bf16x3", 256), "conv3x3_v4<0, 64>"),
-    ((15, 11, 256, 20, 225, "bf16x3", 64), "conv3x3_v4<0, 128>"),
+    ((15, 11, 256, 20, 225, "bf16x3", 64), "conv3x3_v7x3<15, SLIM>"),   # the parity precision at C3
+    ((15, 11, 256, 20, 225, "bf16x3", 2048), "conv3x3_v7x3<15, SLIM>"),
+    ((19, 8, 256, 20, 362, "bf16x3", 1024), "conv3x3_v7x3<19, DENSE>"),
     ((19, 8, 256, 20, 362, "fp16", 1024), "conv3x3_v6<2, 19, DENSE>"),   # C4
     ((15, 11, 32, 2, 225, "f32", 4), "gemm_f32"),
 ])

@@ -139,12 +139,19 @@ def test_gpu_randwire_selfplay_replay():
 def test_gpu_randwire_rejects_bad_desc():
     import az_amd
     eng = az_amd.Engine(0)
-    for kw in (dict(precision=az_amd.AZ_PREC_FP16), dict(conv_bias=1), dict(channels=24), dict(pool=4)):
+    import randwire_oracle as RW
+    graphs = RW.load_graphs()
+    for kw in (dict(precision=az_amd.AZ_PREC_FP16), dict(conv_bias=1), dict(channels=24), dict(channels=2048),
+               dict(pool=4)):
         d = az_amd.randwire_net_desc(9, 16, 1, 11, 4)
         for k, v in kw.items():
             setattr(d, k, v)
         with pytest.raises(az_amd.AzError):
             az_amd.HipNeuralNetwork(eng, d, randwire=True)
+        # the explicit-wiring entry point validates the same desc (k_se_residual's fixed LDS arrays,
+        # float4 channel quads; no conv bias; pool min(8, board))
+        with pytest.raises(az_amd.AzError):
+            az_amd.HipNeuralNetwork(eng, d, graphs=graphs)
     net = _net(eng, 9, 16, 1, 4)
     with pytest.raises(az_amd.AzError):
         net.set_precision(az_amd.AZ_PREC_BF16)
