@@ -4,6 +4,7 @@
 // The product path never falls back to the CPU: without a HIP device every entry
 // point fails with AZ_ERR_HIP.
 #include <hip/hip_runtime.h>
+#include <sched.h>
 
 #include <algorithm>
 #include <cmath>
@@ -975,11 +976,14 @@ int search_sims(az_search* s, int n) {
     return 0;
 }
 
-// Host worker threads for per-game host work: the CPU share (OMP_NUM_THREADS where set, as on the
-// GPU boxes, where hardware_concurrency reports the whole machine), at most 16.
+// Host worker threads for per-game host work: the process's CPU share -- its affinity mask (a
+// multi-GPU bench rank runs on its own slice of the host, bench.py), capped by OMP_NUM_THREADS
+// where set (the GPU boxes, where hardware_concurrency reports the whole machine) and by 16.
 int host_threads() {
     static const int n = [] {
         int h = (int)std::thread::hardware_concurrency();
+        cpu_set_t cs;
+        if (sched_getaffinity(0, sizeof(cs), &cs) == 0 && CPU_COUNT(&cs) > 0) h = std::min(h, (int)CPU_COUNT(&cs));
         if (const char* e = getenv("OMP_NUM_THREADS")) if (atoi(e) > 0) h = std::min(h, atoi(e));
         return std::max(1, std::min(16, h));
     }();

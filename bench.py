@@ -41,6 +41,16 @@ if PKG not in sys.path:
 import numpy as np  # noqa: E402
 
 METRIC = "self-play positions/sec (+ NN evals/sec) at 800 sims/move, 1/2/4/8 GPU"
+# Measured error of each trunk precision against the fp32 network (profiles/r02b_trained_scale.txt,
+# profiles/r03a_x3_net_parity.log: heads scaled to |logit|max 8, |value| 0.9, the magnitudes of a trained net)
+PREC_NOTE = {
+    "fp16": "fp16 MFMA operands, fp32 accumulation (the reference's opt-in useFp16, torch_neural_network.h:29); "
+            "trained-scale max|dlogit| 1.3e-3 (C3), 1.9e-3 (C4) vs the fp32 net: outside the 1e-4 parity "
+            "tolerance, see parity_mode for the fp32-faithful rate",
+    "bf16x3": "fp32-faithful: bf16 hi + lo operands, three MFMAs per product, fp32 accumulation; trained-scale "
+              "max|dlogit| 3.4e-5 (C3), 3.7e-5 (C4) vs the fp32 net: within the 1e-4 parity tolerance",
+    "f32": "f32 MFMA (exact fp32 products)",
+}
 PEAK_TFLOPS = {"bf16x3": 2500.0, "bf16": 2500.0, "fp16": 2500.0, "f32": 157.3}   # dense MFMA peaks, MI355X_MICROARCH.md
 PREC = {"f32": 0, "bf16x3": 1, "bf16": 2, "fp16": 3}
 # BASELINE.json configs: game, board, blocks, channels, sims/move, global games
@@ -77,6 +87,12 @@ def parse(argv=None):
     ap.add_argument("--cpu-window", type=float, default=20.0, help="seconds of the CPU baseline's timed window")
     ap.add_argument("--cpu-workers", type=int, default=0, help="CPU baseline processes (0: the host's CPU share, <=16)")
     ap.add_argument("--seed", type=int, default=1234)
+    ap.add_argument("--parity-steps", type=int, default=1,
+                    help="N=1: also time this many moves of the same workload with the fp32-faithful bf16x3 trunk "
+                         "(the parity precision), reported as parity_mode; 0 disables")
+    ap.add_argument("--parity-warmup", type=int, default=1)
+    ap.add_argument("--dist-timeout", type=float, default=600.0,
+                    help="seconds a rank waits in a collective / barrier before the bench fails (N>1)")
     a = ap.parse_args(argv)
     cfg = a.config or ("c4" if a.game == "go" else "c3")
     c = CONFIGS[cfg]
@@ -156,6 +172,14 @@ class GpuWorkload:
     def sync(self):
         pass                           # selfplayStep returns after a stream synchronize
 
+    def close(self):
+        """Free the device search and net (the parity-mode run allocates a workload of the same size)."""
+        if self.mcts is not None:
+            self.mcts.close()
+            self.mcts = None
+        self.net.close()
+        self.eng.close()
+
 
 def run_rank(a, rank, world, dist, make_workload, coll_device):
     """One rank of the bench: shard, weights (rank 0 init + broadcast), warmup, timed steps between
@@ -195,6 +219,9 @@ def run_rank(a, rank, world, dist, make_workload, coll_device):
     barrier()
     trunk_ms, launches, _ = net.profile_read()
     tree = wl.mcts.profile_read()
+    kernel = net.trunk_kernel()      # the kernel the library dispatches for this net (engine's own choice)
+    if hasattr(wl, "close"):
+        wl.close()
     my_evals = evals
     tot_moves, tot_evals = moves, evals
     if dist is not None:
@@ -202,7 +229,6 @@ def run_rank(a, rank, world, dist, make_workload, coll_device):
     if rank != 0:
         return None
 
-    kernel = net.trunk_kernel()      # the kernel the library dispatches for this net (engine's own choice)
     HW = a.board * a.board
     conv_flops_per_eval = 2 * a.blocks * 2.0 * 9 * a.channels * a.channels * HW
     boards_per_launch = my_evals * 2 * a.blocks / max(1, launches)        # rank 0's own launches and boards
@@ -223,6 +249,7 @@ def run_rank(a, rank, world, dist, make_workload, coll_device):
         "scaling": "strong" if strong else "weak",
         "vs_baseline": None,
         "dtype": a.precision,
+        "dtype_note": PREC_NOTE.get(a.precision, ""),
         "data": "synthetic: self-play from empty boards, counter-based random-init weights of the named net",
         "config": {"workload": f"{a.workload_name}, {a.global_games if strong else a.global_games * world} games"
                                f"{' sharded' if strong else ''} over {world} GPU(s), {a.sims} sims/move",
@@ -368,7 +395,10 @@ def cpu_baseline(a, workers, window):
 
 def cpu_baseline_line(a, raw, evals_per_move):
     go = a.game == "go"
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else None
     return {"value": raw["evals_per_s"] / evals_per_move, "unit": "positions/s", "cores": raw["cores"],
+            "cores_from": f"min(16, affinity {aff}, OMP_NUM_THREADS {os.environ.get('OMP_NUM_THREADS')}); "
+                          f"nproc {os.cpu_count()}",
             "kind": "port", "evals_per_s": raw["evals_per_s"],
             "sample": f"{raw['cores']} worker processes x 1 thread, one {'Go' if go else 'Gomoku'} {a.board}x{a.board} "
                       f"game each from the empty board (oracle/ Mode S search, {a.sims} sims/move, fp32 "
@@ -377,8 +407,41 @@ def cpu_baseline_line(a, raw, evals_per_move):
                       f"{evals_per_move:.1f} evaluations per move (measured on the GPU run of the same workload)"}
 
 
+def parity_mode(a, make_workload, dev):
+    """The same workload with the fp32-faithful trunk (bf16x3), a short timed run in the same process
+    (N=1, after the headline run has freed its device memory): positions/s and its own roofline."""
+    import copy
+    b = copy.copy(a)
+    b.precision, b.steps, b.warmup = "bf16x3", a.parity_steps, a.parity_warmup
+    out = run_rank(b, 0, 1, None, make_workload, dev)
+    keys = ("value", "unit", "steps", "warmup", "ms_per_step", "dtype", "dtype_note", "nn_evals_per_s",
+            "evals_per_move", "roofline")
+    pm = {k: out[k] for k in keys}
+    rf = pm["roofline"]
+    rf["mfma_issue_frac"] = 3 * rf["frac"]      # three MFMAs per algorithmic product
+    pm["note"] = ("same workload and weights, trunk in the parity precision; roofline FLOPs counted once "
+                  "(algorithmic), so frac <= 1/3 and mfma_issue_frac = 3 x frac")
+    return pm
+
+
+def split_affinity(local, local_world):
+    """Give rank `local` its own slice of the host's CPUs (the engine sizes its host threads from the
+    affinity mask), so N ranks do not oversubscribe the CPU share."""
+    if not hasattr(os, "sched_getaffinity") or local_world < 2:
+        return None
+    cpus = sorted(os.sched_getaffinity(0))
+    per = len(cpus) // local_world
+    if per < 1:
+        return None
+    mine = cpus[local * per:(local + 1) * per]
+    os.sched_setaffinity(0, mine)
+    return mine
+
+
 # ------------------------------------------------------------------------------- main
-def main(argv=None):
+def main(argv=None, make_workload=None, backend=None):
+    """make_workload / backend: test hooks (a stand-in workload over gloo); the product run uses the
+    device workload over RCCL."""
     argv = sys.argv[1:] if argv is None else argv
     a = parse(argv)
     if "WORLD_SIZE" not in os.environ and a.gpus > 1:
@@ -392,23 +455,33 @@ def main(argv=None):
     raw_cpu = None
     if a.cpu_baseline and world == 1:
         raw_cpu = cpu_baseline(a, a.cpu_workers or cpu_share(), a.cpu_window)
+    make_workload = make_workload or GpuWorkload
     dist = None
     dev = "cpu"
     if world > 1:
+        import datetime
         import torch
         import torch.distributed as dist
-        if torch.cuda.device_count() <= local:
-            print(f"bench.py: LOCAL_RANK {local} but {torch.cuda.device_count()} GPU(s) visible", file=sys.stderr)
-            return 2
-        torch.cuda.set_device(local)
-        dev = f"cuda:{local}"
-        dist.init_process_group("nccl", init_method="env://")
-    out = run_rank(a, rank, world, dist, GpuWorkload, dev)
-    if out is not None:
-        out["cpu_baseline"] = cpu_baseline_line(a, raw_cpu, out["evals_per_move"]) if raw_cpu else None
-        print(json.dumps(out), flush=True)
-    if dist is not None:
-        dist.destroy_process_group()
+        split_affinity(local, int(os.environ.get("LOCAL_WORLD_SIZE", str(world))))
+        if backend is None:
+            if torch.cuda.device_count() <= local:
+                print(f"bench.py: LOCAL_RANK {local} but {torch.cuda.device_count()} GPU(s) visible", file=sys.stderr)
+                return 2
+            torch.cuda.set_device(local)
+            dev = f"cuda:{local}"
+        # a rank that dies leaves the others in a collective: they fail after dist_timeout, not hang
+        dist.init_process_group(backend or "nccl", init_method="env://",
+                                timeout=datetime.timedelta(seconds=a.dist_timeout))
+    try:
+        out = run_rank(a, rank, world, dist, make_workload, dev)
+        if out is not None:
+            out["cpu_baseline"] = cpu_baseline_line(a, raw_cpu, out["evals_per_move"]) if raw_cpu else None
+            if world == 1 and a.parity_steps > 0 and a.precision != "bf16x3" and a.channels % 64 == 0:
+                out["parity_mode"] = parity_mode(a, make_workload, dev)
+            print(json.dumps(out), flush=True)
+    finally:
+        if dist is not None:
+            dist.destroy_process_group()
     return 0
 
 

@@ -164,3 +164,48 @@ def test_cpu_baseline_workers_window():
     line = bench.cpu_baseline_line(a, raw, 20.0)
     assert line["kind"] == "port" and line["cores"] == 2
     assert abs(line["value"] - raw["evals_per_s"] / 20.0) < 1e-9
+
+
+class _DyingWorkload(_Workload):
+    """Rank 1's stand-in dies in its second timed step (a crashed GPU process)."""
+
+    def step(self):
+        if self.steps == 2:
+            raise RuntimeError("rank 1: simulated device failure")
+        return super().step()
+
+
+def _rank_main(rank, world, port, q):
+    import time
+    import bench
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), LOCAL_RANK=str(rank), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_WORLD_SIZE=str(world))
+    t0 = time.time()
+
+    def make(a_, local, shard):
+        return (_DyingWorkload if rank == 1 else _Workload)(a_, local, shard)
+    try:
+        bench.main(["--gpus", str(world), "--steps", "3", "--warmup", "1", "--cpu-baseline", "0",
+                    "--dist-timeout", "15"], make_workload=make, backend="gloo")
+        q.put((rank, "returned", time.time() - t0))
+    except BaseException as e:        # noqa: BLE001 -- reported to the parent, then re-raised
+        q.put((rank, type(e).__name__, time.time() - t0))
+        raise
+
+
+@pytest.mark.timeout(240)
+def test_bench_rank_death_fails_loudly_gloo_world2():
+    """One rank raising mid-run makes bench.py fail on every rank within --dist-timeout (no hang,
+    no JSON line from rank 0): the surviving rank's barrier raises, both processes exit non-zero."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank_main, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted((q.get(timeout=200) for _ in procs), key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+    assert res[1][1] == "RuntimeError"
+    assert res[0][1] != "returned" and res[0][2] < 15 + 60
+    assert all(p.exitcode not in (0, None) for p in procs)

@@ -69,19 +69,26 @@ def test_gpu_net_selfplay_matches_oracle_replay(prec, logged):
     net.close()
 
 
-def _full_size_replay(bs, sims, G, moves, logged, channels, blocks):
-    """Play `moves` moves of G games at a BASELINE.json size with the fp16 trunk, log game `logged`
-    and replay it through the CPU restatement bit for bit; check a sample of its logged network
-    outputs against the fp32 reference network (1e-4) and size-independent properties of every
-    game's root (one child per empty cell, visit sum, probability sum, value range)."""
+def _full_size_replay(bs, sims, G, moves, logged, channels, blocks, prec=None, trained=False):
+    """Play `moves` moves of G games at a BASELINE.json size (fp16 trunk unless `prec`), log game
+    `logged` and replay it through the CPU restatement bit for bit; check a sample of its logged
+    network outputs against the fp32 reference network (1e-4) and size-independent properties of
+    every game's root (one child per empty cell, visit sum, probability sum, value range).
+    trained: heads scaled to a trained net's output magnitudes (|logit|max 8, |value| ~0.9,
+    test_gpu_trained_scale.trained_scale_blob), and the raw logits of a full B = G forward of the
+    logged leaves checked against the fp32 network too."""
     import az_amd
     import az_oracle as O
     import net_oracle
     eng = az_amd.Engine(0)
-    desc = az_amd.gomoku_net_desc(board_size=bs, channels=channels, blocks=blocks, precision=az_amd.AZ_PREC_FP16,
-                                  max_batch=G)
+    desc = az_amd.gomoku_net_desc(board_size=bs, channels=channels, blocks=blocks,
+                                  precision=az_amd.AZ_PREC_FP16 if prec is None else prec, max_batch=G)
     net = az_amd.HipNeuralNetwork(eng, desc)
-    blob = net_oracle.init_blob(desc, seed=1234)
+    if trained:
+        from test_gpu_trained_scale import _planes as ts_planes, trained_scale_blob
+        blob = trained_scale_blob(desc, 1234, ts_planes("c3", 16, seed=17))
+    else:
+        blob = net_oracle.init_blob(desc, seed=1234)
     net.load_weights(blob)
     m = az_amd.ParallelMCTS(eng, n_games=G, board_size=bs, num_simulations=sims, evaluator=az_amd.AZ_EVAL_NET,
                             net=net, noise_seed=42, noise_seed_stride=1)
@@ -129,6 +136,15 @@ def _full_size_replay(bs, sims, G, moves, logged, channels, blocks):
     rl, rv = net_oracle.forward(desc, blob, planes[idx])
     assert np.abs(valv[idx] - rv).max() <= 1e-4
     assert np.abs(pol[idx] - net_oracle.softmax_policy(rl)).max() <= 1e-4
+    if trained:
+        # raw logits and values of a full-capacity forward (B = G boards: the logged leaves, cycled)
+        xb = planes[np.arange(G) % len(planes)]
+        lo, v = net.forward(xb)
+        keep = idx < G                                   # xb[i] == planes[i] for i < G
+        el = float(np.abs(lo[idx[keep]] - rl[keep]).max())
+        ev = float(np.abs(v[idx[keep]] - rv[keep]).max())
+        print(f"full-size trained-scale: |logit|max {np.abs(rl).max():.3f} max|dlogit|={el:.3e} max|dvalue|={ev:.3e}")
+        assert np.abs(rl).max() > 2.0 and el <= 1e-4 and ev <= 1e-4
     m.close()
     net.close()
 
@@ -138,6 +154,16 @@ def test_gpu_c3_full_size_replay():
     """C3 at full size (BASELINE.json configs[2]: 2048 games, 15x15, 800 sims, the 20 x 256 net):
     the first two moves of every game, game 1337 (in the middle of the batch) replayed."""
     _full_size_replay(bs=15, sims=800, G=2048, moves=2, logged=1337, channels=256, blocks=20)
+
+
+@pytest.mark.gpu
+def test_gpu_c3_full_size_replay_bf16x3():
+    """C3 at full size in the parity precision (AZ_PREC_BF16X3, conv3x3_v7x3) with trained-scale
+    heads: two moves of all 2048 games, game 1337 replayed bit for bit, sampled logits / values of
+    the logged leaves and of a B = 2048 forward within 1e-4 of the fp32 network."""
+    import az_amd
+    _full_size_replay(bs=15, sims=800, G=2048, moves=2, logged=1337, channels=256, blocks=20,
+                      prec=az_amd.AZ_PREC_BF16X3, trained=True)
 
 
 @pytest.mark.gpu
