@@ -33,6 +33,14 @@ class HipNeuralNetwork : public NeuralNetwork {
     void setPrecision(int precision);
     // .azw file: "AZW1", 12 int32 NetShape fields, uint64 count, float32[count]
     static std::unique_ptr<HipNeuralNetwork> load(const std::string& path, int device = -1);
+    // The reference's own model file: a TorchScript archive of its plain ResNet (SimplifiedModel /
+    // the exporter fallback; torch_neural_network.cpp:90 loads it with torch::jit::load), read
+    // without executing it (alphazero/nn/torchscript_reader.h).  precision: AZ_PREC_* of the trunk
+    // (-1: AZ_PREC_BF16X3 where the trunk has 16-bit kernels -- fp32-faithful, the reference's
+    // default fp32 inference -- else AZ_PREC_F32); boardSize <= 0: from the policy size.
+    static std::unique_ptr<HipNeuralNetwork> loadTorchScript(const std::string& path, core::GameType type,
+                                                             int boardSize = 0, int precision = -1,
+                                                             int maxBatch = 2048, int device = -1);
     // TorchNeuralNetwork::createDDWRandWireResNet (torch_neural_network.cpp:799-814): the
     // DDW-RandWire net (ddw_randwire_resnet.cpp:387-468) on the device engine, fp32 path
     static std::unique_ptr<HipNeuralNetwork> createDDWRandWireResNet(int inputChannels, int outputSize,

@@ -30,8 +30,10 @@ class NeuralNetwork {
     virtual void enableDebugMode(bool enable) = 0;
     virtual void printModelSummary() const = 0;
 
-    // modelPath: an .azw weight file (tools/export_azw.py) -> HipNeuralNetwork on the MI355X
-    // engine; "random" / "" -> RandomPolicyNetwork.  useGpu=false is refused (no CPU path).
+    // modelPath: an .azw weight file (tools/export_azw.py), or the reference's TorchScript model
+    // file of its plain ResNet (read without executing it, HipNeuralNetwork::loadTorchScript) ->
+    // HipNeuralNetwork on the MI355X engine; "random" / "" -> RandomPolicyNetwork.  useGpu=false
+    // is refused (no CPU path).
     static std::unique_ptr<NeuralNetwork> create(const std::string& modelPath, core::GameType gameType,
                                                  int boardSize = 0, bool useGpu = true);
 };

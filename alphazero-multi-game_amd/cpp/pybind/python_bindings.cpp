@@ -7,6 +7,7 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include "alphazero/nn/torchscript_reader.h"
 #include "alphazero/games/go/go_state.h"
 #include "alphazero/games/gomoku/gomoku_state.h"
 #include "alphazero/mcts/parallel_mcts.h"
@@ -195,7 +196,33 @@ PYBIND11_MODULE(_alphazero_cpp, m) {
         .def("initRandom", &nn::HipNeuralNetwork::initRandom)
         .def("setPrecision", &nn::HipNeuralNetwork::setPrecision)
         .def("save", &nn::HipNeuralNetwork::save)
-        .def_static("load", &nn::HipNeuralNetwork::load, py::arg("path"), py::arg("device") = -1);
+        .def_static("load", &nn::HipNeuralNetwork::load, py::arg("path"), py::arg("device") = -1)
+        .def_static("loadTorchScript", &nn::HipNeuralNetwork::loadTorchScript, py::arg("path"), py::arg("gameType"),
+                    py::arg("boardSize") = 0, py::arg("precision") = -1, py::arg("maxBatch") = 2048,
+                    py::arg("device") = -1);
+    // host-only reader of a TorchScript archive's tensors (no code executed): [(name, array)] in
+    // state_dict order, and the plain-ResNet shape + canonical blob the engine loads
+    m.def("readTorchScript", [](const std::string& path) {
+        py::list out;
+        for (auto& t : nn::readTorchScript(path)) {
+            std::vector<py::ssize_t> shape(t.shape.begin(), t.shape.end());
+            py::array_t<float> a(shape);
+            std::copy(t.data.begin(), t.data.end(), a.mutable_data());
+            out.append(py::make_tuple(t.name, a));
+        }
+        return out;
+    }, py::arg("path"));
+    m.def("torchScriptResNet", [](const std::string& path, core::GameType type, int boardSize) {
+        nn::NetShape s;
+        std::vector<float> blob = nn::torchScriptResNet(path, type, boardSize, s);
+        py::dict d;
+        d["board"] = s.boardSize; d["in_planes"] = s.inPlanes; d["channels"] = s.channels; d["blocks"] = s.blocks;
+        d["action_size"] = s.actionSize; d["head_channels"] = s.headChannels; d["pool"] = s.pool;
+        d["fc_hidden"] = s.fcHidden; d["residual"] = s.residual; d["conv_bias"] = s.convBias;
+        py::array_t<float> a((py::ssize_t)blob.size());
+        std::copy(blob.begin(), blob.end(), a.mutable_data());
+        return py::make_tuple(d, a);
+    }, py::arg("path"), py::arg("gameType"), py::arg("boardSize") = 0);
     // TorchNeuralNetwork::createDDWRandWireResNet / DDWRandWireResNetCpp(input_channels, output_size,
     // channels=128, num_blocks=20) (reference python_bindings.cpp:168-173) on the device engine
     m.def("createDDWRandWireResNet",

@@ -14,6 +14,7 @@
 #include "alphazero/games/go/go_state.h"
 #include "alphazero/games/gomoku/gomoku_state.h"
 #include "alphazero/nn/hip_neural_network.h"
+#include "alphazero/nn/torchscript_reader.h"
 #include "alphazero/nn/random_policy_network.h"
 
 namespace alphazero {
@@ -90,6 +91,18 @@ std::unique_ptr<HipNeuralNetwork> HipNeuralNetwork::load(const std::string& path
     std::vector<float> blob(count);
     f.read(reinterpret_cast<char*>(blob.data()), (std::streamsize)(count * 4));
     if (!f) throw std::runtime_error(path + ": truncated weight file");
+    auto net = std::make_unique<HipNeuralNetwork>(s, device);
+    net->loadWeights(blob);
+    return net;
+}
+
+std::unique_ptr<HipNeuralNetwork> HipNeuralNetwork::loadTorchScript(const std::string& path, core::GameType type,
+                                                                   int boardSize, int precision, int maxBatch, int device) {
+    NetShape s;
+    s.maxBatch = maxBatch;
+    s.precision = precision;
+    std::vector<float> blob = torchScriptResNet(path, type, boardSize, s);
+    if (precision < 0) s.precision = s.channels % 32 == 0 ? AZ_PREC_BF16X3 : AZ_PREC_F32;
     auto net = std::make_unique<HipNeuralNetwork>(s, device);
     net->loadWeights(blob);
     return net;
@@ -238,6 +251,7 @@ std::unique_ptr<NeuralNetwork> NeuralNetwork::create(const std::string& path, co
     if (type == core::GameType::CHESS) throw std::invalid_argument("Chess networks are created from .azw files only");
     if (path.empty() || path == "random") return std::make_unique<RandomPolicyNetwork>(type, bs, 0);
     if (!useGpu) throw std::invalid_argument("the engine has no CPU network path (useGpu=false)");
+    if (isZipArchive(path)) return HipNeuralNetwork::loadTorchScript(path, type, bs);   // the reference's .pt
     auto net = HipNeuralNetwork::load(path);
     if (bs > 0 && net->shape().boardSize != bs) throw std::invalid_argument("weight file board size mismatch");
     return net;

@@ -40,6 +40,8 @@ if PKG not in sys.path:
 
 import numpy as np  # noqa: E402
 
+T_START = time.perf_counter()
+
 METRIC = "self-play positions/sec (+ NN evals/sec) at 800 sims/move, 1/2/4/8 GPU"
 # Measured error of each trunk precision against the fp32 network (profiles/r02b_trained_scale.txt,
 # profiles/r03a_x3_net_parity.log: heads scaled to |logit|max 8, |value| 0.9, the magnitudes of a trained net)
@@ -91,6 +93,9 @@ def parse(argv=None):
                     help="N=1: also time this many moves of the same workload with the fp32-faithful bf16x3 trunk "
                          "(the parity precision), reported as parity_mode; 0 disables")
     ap.add_argument("--parity-warmup", type=int, default=1)
+    ap.add_argument("--time-budget", type=float, default=560.0,
+                    help="seconds: parity_mode is skipped (and says so) when the run so far plus its estimated "
+                         "time would exceed this (the driver's run limit is 600 s)")
     ap.add_argument("--dist-timeout", type=float, default=600.0,
                     help="seconds a rank waits in a collective / barrier before the bench fails (N>1)")
     a = ap.parse_args(argv)
@@ -477,7 +482,14 @@ def main(argv=None, make_workload=None, backend=None):
         if out is not None:
             out["cpu_baseline"] = cpu_baseline_line(a, raw_cpu, out["evals_per_move"]) if raw_cpu else None
             if world == 1 and a.parity_steps > 0 and a.precision != "bf16x3" and a.channels % 64 == 0:
-                out["parity_mode"] = parity_mode(a, make_workload, dev)
+                # bf16x3 moves take ~2.7x the fp16 trunk's (1.31 vs 0.485 ms per launch), plus setup
+                est = (a.parity_steps + a.parity_warmup) * out["ms_per_step"] / 1e3 * 2.8 + 20.0
+                spent = time.perf_counter() - T_START
+                if spent + est <= a.time_budget:
+                    out["parity_mode"] = parity_mode(a, make_workload, dev)
+                else:
+                    out["parity_mode"] = {"skipped": f"time budget: {spent:.0f} s spent + ~{est:.0f} s estimated > "
+                                                     f"{a.time_budget:.0f} s"}
             print(json.dumps(out), flush=True)
     finally:
         if dist is not None:

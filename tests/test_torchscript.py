@@ -1,0 +1,182 @@
+"""The reference's model file format at the boundary: a TorchScript archive (torch.jit.save of a traced
+module -- python/scripts/self_play.py:139-193 exports it, TorchNeuralNetwork loads it with
+torch::jit::load, torch_neural_network.cpp:90) read by the host API without executing anything
+(cpp/src/torchscript_reader.cpp: zip directory + restricted pickle machine).
+
+The archives are traced here from modules with the reference's two plain-ResNet layouts -- the
+parameter names, shapes and order of python/simple_export.py:12-66 SimplifiedModel (res_blocks.*,
+conv biases, residual blocks) and of the exporter fallback python/scripts/simple_export.py:40-96
+(middle_layers.*, no conv bias, plain stack, adaptive 8x8 pool) -- whose forward is the arithmetic
+net_oracle restates (pinned to the reference classes by tests/test_nn_golden.py).  CPU: every tensor
+read back bit for bit in state_dict order, the inferred net shape, and net_oracle on the read blob
+equal to the traced module's own output; a refused global.  GPU: createNeuralNetwork on the .pt
+file predicts what the traced module predicts (1e-4)."""
+import io
+import os
+import pickle
+import zipfile
+
+import numpy as np
+import pytest
+import torch
+
+az = pytest.importorskip("_alphazero_cpp", reason="build the host module: make -C alphazero-multi-game_amd")
+
+
+def _module(desc, residual):
+    nn = torch.nn
+    F, Ci, HC, A, Hd, P = (desc.channels, desc.in_planes, desc.head_channels, desc.action_size, desc.fc_hidden,
+                           desc.pool)
+    bias = bool(desc.conv_bias)
+
+    class Net(nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.input_conv = nn.Conv2d(Ci, F, 3, padding=1, bias=bias)
+            self.input_bn = nn.BatchNorm2d(F)
+            blocks = [nn.Sequential(nn.Conv2d(F, F, 3, padding=1, bias=bias), nn.BatchNorm2d(F), nn.ReLU(),
+                                    nn.Conv2d(F, F, 3, padding=1, bias=bias), nn.BatchNorm2d(F),
+                                    *([] if residual else [nn.ReLU()])) for _ in range(desc.blocks)]
+            if residual:
+                self.res_blocks = nn.ModuleList(blocks)
+            else:
+                self.middle_layers = nn.Sequential(*blocks)
+            self.policy_conv = nn.Conv2d(F, HC, 1, bias=bias)
+            self.policy_bn = nn.BatchNorm2d(HC)
+            self.policy_fc = nn.Linear(HC * P * P, A)
+            self.value_conv = nn.Conv2d(F, HC, 1, bias=bias)
+            self.value_bn = nn.BatchNorm2d(HC)
+            self.value_fc1 = nn.Linear(HC * P * P, Hd)
+            self.value_fc2 = nn.Linear(Hd, 1)
+
+        def forward(self, x):
+            x = torch.relu(self.input_bn(self.input_conv(x)))
+            if residual:
+                for b in self.res_blocks:
+                    x = torch.relu(b(x) + x)
+            else:
+                x = self.middle_layers(x)
+            x = torch.nn.functional.adaptive_avg_pool2d(x, (P, P))
+            p = torch.relu(self.policy_bn(self.policy_conv(x))).flatten(1)
+            v = torch.relu(self.value_bn(self.value_conv(x))).flatten(1)
+            return self.policy_fc(p), torch.tanh(self.value_fc2(torch.relu(self.value_fc1(v))))
+    return Net().eval()
+
+
+def _traced(tmp_path, desc, residual, seed, name):
+    """A traced archive of the layout with the counter-based weights of net_oracle.init_blob."""
+    import net_oracle
+    m = _module(desc, residual)
+    blob = net_oracle.init_blob(desc, seed)
+    sd = m.state_dict()
+    keys = [k for k in sd if not k.endswith("num_batches_tracked")]
+    shapes = net_oracle.param_shapes(desc)
+    assert [tuple(sd[k].shape) for k in keys] == [tuple(s) for _, s, _, _ in shapes]
+    off, new = 0, {}
+    for k in sd:
+        if k.endswith("num_batches_tracked"):
+            new[k] = torch.tensor(7)
+            continue
+        n = sd[k].numel()
+        new[k] = torch.from_numpy(blob[off:off + n].reshape(tuple(sd[k].shape)).copy())
+        off += n
+    m.load_state_dict(new)
+    x = torch.zeros(1, desc.in_planes, desc.board_size, desc.board_size)
+    path = str(tmp_path / name)
+    torch.jit.trace(m, x).save(path)
+    return m, blob, path
+
+
+LAYOUTS = [  # (board, channels, blocks, residual, conv_bias): SimplifiedModel and the exporter fallback
+    (8, 16, 2, 1, 1),
+    (15, 32, 2, 0, 0),
+]
+
+
+@pytest.mark.parametrize("case", LAYOUTS, ids=["simplified8", "fallback15"])
+def test_torchscript_reader_matches_module(tmp_path, case):
+    import az_amd
+    import az_oracle as O
+    import net_oracle
+    bs, ch, blocks, res, bias = case
+    desc = az_amd.gomoku_net_desc(board_size=bs, channels=ch, blocks=blocks, residual=res, conv_bias=bias, max_batch=4)
+    m, blob, path = _traced(tmp_path, desc, res, seed=5, name="m.pt")
+    # every tensor, in state_dict order, bit for bit (num_batches_tracked as a float)
+    got = az.readTorchScript(path)
+    sd = m.state_dict()
+    assert [k for k, _ in got] == list(sd)
+    for (k, a), v in zip(got, sd.values()):
+        assert np.array_equal(np.asarray(a, np.float32), v.float().numpy()), k
+    # the engine's shape and canonical blob
+    shape, b = az.torchScriptResNet(path, az.GameType.GOMOKU)
+    assert shape == dict(board=bs, in_planes=11, channels=ch, blocks=blocks, action_size=bs * bs, head_channels=32,
+                         pool=8, fc_hidden=256, residual=res, conv_bias=bias)
+    assert np.array_equal(np.asarray(b), blob)
+    # the arithmetic the engine implements (net_oracle) on the read weights == the traced module
+    rng = np.random.default_rng(1)
+    x = np.stack([O.position(bs, rng.permutation(bs * bs)[:k].tolist())[0] for k in (0, 5, 17)])
+    rl, rv = net_oracle.forward(desc, np.asarray(b), x)
+    with torch.no_grad():
+        tl, tv = torch.jit.load(path)(torch.from_numpy(x))
+    assert np.abs(rl - tl.numpy()).max() <= 1e-5 and np.abs(rv - tv.numpy().ravel()).max() <= 1e-5
+
+
+def test_torchscript_reader_refuses_foreign_globals(tmp_path):
+    """A data.pkl that names anything outside the allow-list is refused before it is used."""
+    for payload in (b"\x80\x02cos\nsystem\nq\x00X\x02\x00\x00\x00lsq\x01\x85q\x02Rq\x03.",
+                    b"\x80\x02cbuiltins\neval\nq\x00."):
+        p = tmp_path / "evil.pt"
+        with zipfile.ZipFile(p, "w", zipfile.ZIP_STORED) as z:
+            z.writestr("evil/data.pkl", payload)
+            z.writestr("evil/version", "3\n")
+        with pytest.raises(ValueError, match="refusing global"):
+            az.readTorchScript(str(p))
+    # a layout that is not the reference's plain ResNet
+    lin = torch.jit.trace(torch.nn.Linear(3, 2), torch.zeros(1, 3))
+    lin.save(str(tmp_path / "lin.pt"))
+    assert [k for k, _ in az.readTorchScript(str(tmp_path / "lin.pt"))] == ["weight", "bias"]
+    with pytest.raises(ValueError, match="unrecognised module layout"):
+        az.torchScriptResNet(str(tmp_path / "lin.pt"), az.GameType.GOMOKU)
+
+
+def test_export_azw_accepts_torchscript(tmp_path):
+    """tools/export_azw.py converts the reference's .pt into the .azw weight file."""
+    import struct
+    import subprocess
+    import sys
+    import az_amd
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    desc = az_amd.gomoku_net_desc(board_size=15, channels=32, blocks=2, residual=0, conv_bias=0, max_batch=4)
+    _, blob, path = _traced(tmp_path, desc, 0, seed=8, name="fb.pt")
+    dst = tmp_path / "fb.azw"
+    subprocess.run([sys.executable, os.path.join(root, "tools", "export_azw.py"), path, str(dst), "--max-batch", "4"],
+                   check=True, capture_output=True)
+    raw = dst.read_bytes()
+    assert struct.unpack("<12i", raw[4:52]) == (15, 11, 32, 2, 225, 32, 8, 256, 0, 0, 3, 4)
+    assert np.array_equal(np.frombuffer(raw[60:], np.float32), blob)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", LAYOUTS, ids=["simplified8", "fallback15"])
+def test_create_network_from_torchscript(tmp_path, case):
+    """createNeuralNetwork(<the reference's .pt>) -> HipNeuralNetwork (bf16x3 trunk where it has one):
+    predictBatch on GomokuStates == softmax / value of the traced module within 1e-4."""
+    import az_amd
+    import net_oracle
+    bs, ch, blocks, res, bias = case
+    desc = az_amd.gomoku_net_desc(board_size=bs, channels=ch, blocks=blocks, residual=res, conv_bias=bias, max_batch=4)
+    m, blob, path = _traced(tmp_path, desc, res, seed=6, name="m.pt")
+    net = az.createNeuralNetwork(path, az.GameType.GOMOKU, bs, True)
+    rng = np.random.default_rng(2)
+    states = []
+    for k in (0, 3, 9, 14):
+        s = az.GomokuState(bs)
+        for _ in range(k):
+            s.makeMove(int(rng.choice(s.getLegalMoves())))
+        states.append(s)
+    pol, val = net.predictBatch(states)
+    x = np.stack([np.asarray(s.getEnhancedTensorRepresentation(), np.float32) for s in states])
+    with torch.no_grad():
+        tl, tv = m(torch.from_numpy(x))
+    assert np.abs(np.asarray(pol) - net_oracle.softmax_policy(tl.numpy())).max() <= 1e-4
+    assert np.abs(np.asarray(val) - tv.numpy().ravel()).max() <= 1e-4
