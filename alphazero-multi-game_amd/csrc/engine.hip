@@ -1259,7 +1259,6 @@ static int net_create(az_engine* e, const az_net_desc* d, az_net** out, bool rw,
     if (!r) r = dalloc(&n->d_nb, 1);
     if (!r) r = dalloc(&n->zero, 128);
     if (!r && hipMemset(n->zero, 0, 256) != hipSuccess) r = az_fail(AZ_ERR_HIP, "memset");
-    if (const char* v = getenv("AZ_CONV_FLAGS")) az_diag_set_conv_flags(atoi(v));
     if (r) { az_net_destroy(n); return r; }
     *out = n;
     return 0;

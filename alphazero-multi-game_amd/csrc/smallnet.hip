@@ -102,6 +102,13 @@ __device__ __forceinline__ void certify_frags(F (&a)[JA], F (&b)[JB]) {
 
 }  // namespace
 
+// measurement only (tools/sm_check.sh): 4 = one wave per SIMD instead of the default 8-wave block
+static int g_sm_waves = 8;
+extern "C" int az_diag_set_smallnet_waves(int nw) {
+    g_sm_waves = nw == 4 ? 4 : 8;
+    return 0;
+}
+
 extern "C" int az_diag_smallnet_stamps(unsigned long long* out, int n) {
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sm_stamps), sizeof(unsigned long long) * (n < 128 ? n : 128)) == hipSuccess ? 0 : -1;
 }
@@ -438,8 +445,7 @@ int az_smallnet_launch(const SmallNetArgs& a, int B, hipStream_t st) {
         default: break;
     }
 #endif
-    static const int nw = getenv("AZ_SM_WAVES") ? atoi(getenv("AZ_SM_WAVES")) : 8;
-    if (nw == 4) hipLaunchKernelGGL((k_smallnet<15, 0, 4>), dim3(B), dim3(256), 0, st, a);
+    if (g_sm_waves == 4) hipLaunchKernelGGL((k_smallnet<15, 0, 4>), dim3(B), dim3(256), 0, st, a);
     else hipLaunchKernelGGL((k_smallnet<15, 0, 8>), dim3(B), dim3(512), 0, st, a);
     return 0;
 }

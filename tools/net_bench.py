@@ -32,6 +32,12 @@ def main():
     ap.add_argument("--game", default="gomoku15", choices=list(GAMES))
     a = ap.parse_args()
     bs, planes, actions = GAMES[a.game]
+    if os.environ.get("AZ_SM_WAVES"):      # measurement-only kernel variants (diag entry points)
+        from az_amd import _lib as _l
+        _l.lib().az_diag_set_smallnet_waves(int(os.environ["AZ_SM_WAVES"]))
+    if os.environ.get("AZ_CONV_FLAGS"):
+        from az_amd import _lib as _l
+        _l.lib().az_diag_set_conv_flags(int(os.environ["AZ_CONV_FLAGS"], 0))
     eng = az_amd.Engine(int(os.environ.get("LOCAL_RANK", 0)))
     desc = az_amd.NetDesc(bs, planes, a.channels, a.blocks, actions, 32, 8, 256, 1, 0, PREC[a.precision], a.batch)
     net = az_amd.HipNeuralNetwork(eng, desc)

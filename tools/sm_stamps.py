@@ -13,6 +13,12 @@ import az_amd  # noqa: E402
 from az_amd import _lib  # noqa: E402
 
 B, blocks = int(sys.argv[1]) if len(sys.argv) > 1 else 256, 6
+if os.environ.get("AZ_SM_WAVES"):      # measurement-only kernel variant (diag entry point)
+    from az_amd import _lib as _l
+    _l.lib().az_diag_set_smallnet_waves(int(os.environ["AZ_SM_WAVES"]))
+if os.environ.get("AZ_CONV_FLAGS"):
+    from az_amd import _lib as _l
+    _l.lib().az_diag_set_conv_flags(int(os.environ["AZ_CONV_FLAGS"], 0))
 eng = az_amd.Engine(0)
 net = az_amd.HipNeuralNetwork(eng, az_amd.NetDesc(15, 11, 64, blocks, 225, 32, 8, 256, 1, 0, az_amd.AZ_PREC_FP16, B))
 net.init_random(1)
