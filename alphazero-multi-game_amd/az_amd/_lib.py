@@ -79,6 +79,8 @@ EXPORTS = {
     "az_search_root_flags": (c_int, [vp, c_int, P(c_int)]),
     "az_search_seed": (c_int, [vp, c_int, c_uint32]),
     "az_search_get_rng": (c_int, [vp, c_int, vp]),
+    "az_search_set_net": (c_int, [vp, vp]),
+    "az_search_clear_tt": (c_int, [vp]),
     "az_search_set_rng": (c_int, [vp, c_int, vp]),
     "az_search_set_evaluator": (c_int, [vp, EVAL_FN, vp]),
     "az_search_set_params": (c_int, [vp, P(SearchCfg)]),

@@ -289,8 +289,30 @@ void ParallelMCTS::setNumSimulations(int n) { config_.numSimulations = n; applyC
 void ParallelMCTS::setCPuct(float c) { config_.cPuct = c; applyConfig(); }
 void ParallelMCTS::setFpuReduction(float f) { config_.fpuReduction = f; applyConfig(); }
 void ParallelMCTS::setVirtualLoss(int v) { config_.virtualLoss = v; applyConfig(); }
-void ParallelMCTS::setNeuralNetwork(nn::NeuralNetwork* nn) { nn_ = nn; rebuild(); }
-void ParallelMCTS::setTranspositionTable(TranspositionTable* tt) { tt_ = tt; rebuild(); }
+// parallel_mcts.cpp:1190-1222: the setters replace nn_ / tt_ and keep the tree.  On the device: a
+// device net of the same shape is swapped in place (az_search_set_net), a host evaluator
+// (AZ_EVAL_CALLBACK) is read through nn_ at every leaf batch anyway, and a new table of the same
+// size empties the device table (az_search_clear_tt); any other change (evaluator kind, random
+// network seed, table size) needs a new handle: the history is replayed and the tree rebuilt.
+void ParallelMCTS::setNeuralNetwork(nn::NeuralNetwork* nn) {
+    const DeviceEvaluator cur = deviceEvaluator(nn_), nxt = deviceEvaluator(nn);
+    nn_ = nn;
+    if (s_ && cur.kind == AZ_EVAL_NET && nxt.kind == AZ_EVAL_NET && cur.engine == nxt.engine &&
+        az_search_set_net(s_, nxt.net) == 0)
+        return;
+    if (s_ && cur.kind == AZ_EVAL_CALLBACK && nxt.kind == AZ_EVAL_CALLBACK) return;
+    rebuild();
+}
+void ParallelMCTS::setTranspositionTable(TranspositionTable* tt) {
+    const az_search_cfg before = deviceConfig();
+    TranspositionTable* old = tt_;
+    tt_ = tt;
+    if (s_ && deviceConfig().tt_log2 == before.tt_log2) {
+        if (tt != old) check(az_search_clear_tt(s_), "az_search_clear_tt");
+        return;
+    }
+    rebuild();
+}
 void ParallelMCTS::setConfig(const MCTSConfig& config) { config_ = config; applyConfig(); }
 // parallel_mcts.cpp:1263-1274: useBatchInference = enable; rng_ seeded 42, or from std::random_device
 void ParallelMCTS::setDeterministicMode(bool enable) {

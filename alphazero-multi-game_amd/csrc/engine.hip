@@ -1870,6 +1870,41 @@ int az_search_set_evaluator(az_search* s, az_eval_fn fn, void* user) {
     return 0;
 }
 
+// A new device net for a handle created with AZ_EVAL_NET, the tree kept (ParallelMCTS::
+// setNeuralNetwork only swaps nn_, parallel_mcts.cpp:1190-1207): same engine, board, planes and
+// action space, a batch capacity covering the handle's games, weights loaded.
+int az_search_set_net(az_search* s, az_net* net) {
+    if (!s || !net) return az_fail(AZ_ERR_ARG, "null argument");
+    if (s->c.eval_kind != AZ_EVAL_NET) return az_fail(AZ_ERR_STATE, "the handle was not created with AZ_EVAL_NET");
+    if (net->e != s->e) return az_fail(AZ_ERR_ARG, "the network lives on another engine");
+    const int bs = s->c.board_size, NA = s->t.NA;
+    const bool go = s->c.game == AZ_GAME_GO;
+    if (net->d.board_size != bs || net->d.action_size != NA || net->d.in_planes != (go ? 8 : 11))
+        return az_fail(AZ_ERR_ARG, "network shape does not match the board");
+    if (net->d.max_batch < s->c.n_games) return az_fail(AZ_ERR_ARG, "network max_batch < n_games");
+    if (!net->loaded) return az_fail(AZ_ERR_STATE, "network weights not loaded");
+    std::lock_guard<std::mutex> lk(s->mu);
+    s->net = net;
+    return 0;
+}
+
+// Empty every game's transposition table (a new TranspositionTable object: ParallelMCTS::
+// setTranspositionTable, parallel_mcts.cpp:1209-1222); trees and counters kept.
+int az_search_clear_tt(az_search* s) {
+    if (!s) return az_fail(AZ_ERR_ARG, "null search");
+    std::lock_guard<std::mutex> lk(s->mu);
+    HIPCHK(hipSetDevice(s->e->device));
+    const int G = s->c.n_games;
+    std::vector<int> g(G);
+    for (int i = 0; i < G; ++i) g[i] = i;
+    hipStream_t st = s->e->stream;
+    HIPCHK(hipMemcpyAsync(s->d_games, g.data(), (size_t)G * 4, hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(k_tt_clear, dim3(64, G), dim3(256), 0, st, s->t, s->d_games, G);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(st));
+    return 0;
+}
+
 int az_search_set_params(az_search* s, const az_search_cfg* c) {
     if (!s || !c) return az_fail(AZ_ERR_ARG, "null argument");
     std::lock_guard<std::mutex> lk(s->mu);

@@ -224,6 +224,13 @@ int az_search_root_node(az_search* s, int game, int* N, int* VL, float* W);
  * fpu_reduction, virtual_loss, the Dirichlet fields and the noise seeds of later new games.
  * Shape, evaluator and table changes need a new handle (AZ_ERR_ARG). */
 int az_search_set_params(az_search* s, const az_search_cfg* cfg);
+/* Swap the device net of an AZ_EVAL_NET handle in place, trees kept (ParallelMCTS::
+ * setNeuralNetwork, parallel_mcts.cpp:1190-1207, only replaces nn_): same engine, board, planes
+ * and action space, max_batch >= n_games, weights loaded; else AZ_ERR_ARG / AZ_ERR_STATE. */
+int az_search_set_net(az_search* s, az_net* net);
+/* Empty every game's transposition table, trees kept (ParallelMCTS::setTranspositionTable with a
+ * new table, parallel_mcts.cpp:1209-1222). */
+int az_search_clear_tt(az_search* s);
 /* Reseed game's rng_ (ParallelMCTS::setDeterministicMode, parallel_mcts.cpp:1263-1274: 42, or
  * std::random_device): the std::mt19937 of the Dirichlet draws and of az_search_select_action. */
 int az_search_seed(az_search* s, int game, uint32_t seed);

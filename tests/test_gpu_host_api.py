@@ -304,3 +304,37 @@ def test_host_rng_survives_rebuild():
             m.setTranspositionTable(az.TranspositionTable(1 << 16))
         draws.append((first, [m.selectAction(True, 1.0) for _ in range(8)]))
     assert draws[0] == draws[1]
+
+
+@pytest.mark.gpu
+def test_host_setters_keep_the_tree():
+    """setNeuralNetwork / setTranspositionTable keep the tree, as the reference's setters only
+    replace nn_ / tt_ (parallel_mcts.cpp:1190-1222): a device net of the same shape is swapped into
+    the handle, a new table of the same size empties the device table; the next search adds its
+    simulations to the same root."""
+    bs, sims = 9, 48
+    a = az.HipNeuralNetwork(boardSize=bs, channels=32, blocks=1, precision=0, maxBatch=4)
+    a.initRandom(1)
+    b = az.HipNeuralNetwork(boardSize=bs, channels=32, blocks=1, precision=0, maxBatch=4)
+    b.initRandom(2)
+    cfg = az.MCTSConfig()
+    cfg.numSimulations = sims
+    m = az.ParallelMCTS(az.GomokuState(bs), cfg, a, az.TranspositionTable(1 << 16))
+    m.setDeterministicMode(True)
+    m.search()
+    n0 = m.getRootNode().visitCount
+    kids0 = [c.visitCount for c in m.getRootNode().children]
+    m.setNeuralNetwork(b)
+    assert m.getRootNode().visitCount == n0 and [c.visitCount for c in m.getRootNode().children] == kids0
+    m.setTranspositionTable(az.TranspositionTable(1 << 16))
+    assert m.getRootNode().visitCount == n0
+    m.search()
+    assert m.getRootNode().visitCount == n0 + sims
+    # another trunk of the same board swaps in too; another evaluator kind needs a new handle
+    # (history replayed, fresh tree)
+    c = az.HipNeuralNetwork(boardSize=bs, channels=64, blocks=2, precision=0, maxBatch=1)
+    c.initRandom(3)
+    m.setNeuralNetwork(c)
+    assert m.getRootNode().visitCount == n0 + sims
+    m.setNeuralNetwork(az.RandomPolicyNetwork(az.GameType.GOMOKU, bs, 3))
+    assert m.getRootNode().visitCount == 0
