@@ -80,6 +80,10 @@ EXPORTS = {
     "az_search_seed": (c_int, [vp, c_int, c_uint32]),
     "az_search_get_rng": (c_int, [vp, c_int, vp]),
     "az_search_set_net": (c_int, [vp, vp]),
+    "az_search_run_masked": (c_int, [vp, vp]),
+    "az_search_simulate_masked": (c_int, [vp, c_int, vp]),
+    "az_search_release_masked": (c_int, [vp, c_int, vp, vp]),
+    "az_search_new_games_ids": (c_int, [vp, vp, vp, c_int]),
     "az_search_clear_tt": (c_int, [vp]),
     "az_search_set_rng": (c_int, [vp, c_int, vp]),
     "az_search_set_evaluator": (c_int, [vp, EVAL_FN, vp]),

@@ -16,6 +16,7 @@
 #include "alphazero/core/igamestate.h"
 #include "alphazero/mcts/mcts_node.h"
 #include "alphazero/mcts/transposition_table.h"
+#include "alphazero/mcts/search_group.h"
 #include "alphazero/nn/neural_network.h"
 #include "az_engine.h"
 
@@ -80,6 +81,9 @@ class ParallelMCTS {
                  int virtualLoss = 3);
     ParallelMCTS(const core::IGameState& rootState, const MCTSConfig& config, nn::NeuralNetwork* nn = nullptr,
                  TranspositionTable* tt = nullptr);
+    // A member of `group` (alphazero/mcts/search_group.h): plays in a slot of the group's handle
+    // with the group's evaluator and configuration; concurrent search() calls of members batch.
+    ParallelMCTS(const core::IGameState& rootState, SearchGroup& group);
     ~ParallelMCTS();
     ParallelMCTS(const ParallelMCTS&) = delete;
     ParallelMCTS& operator=(const ParallelMCTS&) = delete;
@@ -119,9 +123,11 @@ class ParallelMCTS {
     std::vector<std::tuple<int, int, float, float>> analyzePosition(int topN = 10) const;   // (action, N, Q, P)
     const MCTSStats& getStats() const { return stats_; }
     az_search* handle() const { return s_; }
+    int slot() const { return slot_; }                       // the game slot of handle()
+    bool inGroup() const { return group_ != nullptr; }
 
  private:
-    void rebuild();           // (re)create the device search for the current config / root
+    void rebuild();           // (re)create the device search for the current config / root (leaves a group)
     void applyConfig();       // new parameters in place (tree kept), or rebuild
     static int hostEvaluate(void* user, int n, const int* games, const int* pathLen, const int* moves, int maxPath,
                             const float* planes, int nPlanes, float* policy, float* value);
@@ -131,6 +137,15 @@ class ParallelMCTS {
     TranspositionTable* tt_;
     std::unique_ptr<core::IGameState> root_;
     az_search* s_ = nullptr;
+    SearchGroup* group_ = nullptr;   // member of a group: s_ is the group's handle, slot_ the game
+    int slot_ = 0;
+    std::vector<uint8_t> slotMask() const;
+    struct RootSelect {
+        std::vector<float> probs;
+        std::vector<int> actions;
+        float value = 0.0f;
+    };
+    RootSelect rootSelect(float temperature) const;
     MCTSStats stats_;
     bool debug_ = false;
     bool searched_ = false;

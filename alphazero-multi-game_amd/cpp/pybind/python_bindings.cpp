@@ -309,6 +309,17 @@ PYBIND11_MODULE(_alphazero_cpp, m) {
         .def_readonly("actions", &mcts::MCTSNode::actions)
         .def_readonly("children", &mcts::MCTSNode::children);
 
+    py::class_<mcts::SearchGroup>(m, "SearchGroup")
+        .def(py::init<nn::NeuralNetwork*, const mcts::MCTSConfig&, const core::IGameState&, int,
+                      const mcts::TranspositionTable*>(),
+             py::arg("nn"), py::arg("config"), py::arg("prototype"), py::arg("capacity"), py::arg("tt") = nullptr,
+             py::keep_alive<1, 2>())
+        .def("capacity", &mcts::SearchGroup::capacity)
+        .def("members", &mcts::SearchGroup::members)
+        .def("searches", &mcts::SearchGroup::searches)
+        .def("deviceRuns", &mcts::SearchGroup::deviceRuns)
+        .def("setGatherMicros", &mcts::SearchGroup::setGatherMicros);
+
     py::class_<mcts::ParallelMCTS>(m, "ParallelMCTS")
         .def(py::init<const core::IGameState&, nn::NeuralNetwork*, mcts::TranspositionTable*, int, int, float, float, int>(),
              py::arg("rootState"), py::arg("nn") = nullptr, py::arg("tt") = nullptr, py::arg("numThreads") = 1,
@@ -317,6 +328,10 @@ PYBIND11_MODULE(_alphazero_cpp, m) {
         .def(py::init<const core::IGameState&, const mcts::MCTSConfig&, nn::NeuralNetwork*, mcts::TranspositionTable*>(),
              py::arg("rootState"), py::arg("config"), py::arg("nn") = nullptr, py::arg("tt") = nullptr,
              py::keep_alive<1, 4>(), py::keep_alive<1, 5>())
+        .def(py::init<const core::IGameState&, mcts::SearchGroup&>(), py::arg("rootState"), py::arg("group"),
+             py::keep_alive<1, 3>())
+        .def("inGroup", &mcts::ParallelMCTS::inGroup)
+        .def("slot", &mcts::ParallelMCTS::slot)
         .def("search", [](mcts::ParallelMCTS& self) {
             py::gil_scoped_release release;
             self.search();

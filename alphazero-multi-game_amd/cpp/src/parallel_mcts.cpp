@@ -104,34 +104,70 @@ ParallelMCTS::ParallelMCTS(const core::IGameState& root, const MCTSConfig& confi
     rebuild();
 }
 
-ParallelMCTS::~ParallelMCTS() {
-    if (s_) az_search_destroy(s_);
+ParallelMCTS::ParallelMCTS(const core::IGameState& root, SearchGroup& group)
+    : nn_(group.network()), tt_(nullptr), root_(root.clone()) {
+    const az_search_cfg& g = group.deviceConfig();
+    config_.numSimulations = g.num_simulations;
+    config_.cPuct = g.c_puct;
+    config_.fpuReduction = g.fpu_reduction;
+    config_.virtualLoss = g.virtual_loss;
+    config_.useDirichletNoise = g.use_dirichlet_each_search != 0;
+    config_.dirichletAlpha = g.dirichlet_alpha;
+    config_.dirichletEpsilon = g.dirichlet_eps;
+    config_.transpositionTableSize = 1 << g.tt_log2;
+    if (root_->getBoardSize() != g.board_size || (root_->getGameType() == core::GameType::GO) != (g.game == AZ_GAME_GO))
+        throw std::invalid_argument("ParallelMCTS: the root's game does not match the group's");
+    slot_ = group.acquire(*root_);
+    group_ = &group;
+    s_ = group.handle();
 }
 
-az_search_cfg ParallelMCTS::deviceConfig() const {
-    const bool go = root_->getGameType() == core::GameType::GO;
-    const DeviceEvaluator ev = deviceEvaluator(nn_);
+ParallelMCTS::~ParallelMCTS() {
+    if (group_) group_->release(slot_);
+    else if (s_) az_search_destroy(s_);
+}
+
+az_search_cfg makeSearchConfig(const MCTSConfig& config, const core::IGameState& state, nn::NeuralNetwork* nn,
+                               const TranspositionTable* tt, int nGames) {
+    const bool go = state.getGameType() == core::GameType::GO;
+    const DeviceEvaluator ev = deviceEvaluator(nn);
     az_search_cfg c{};
     c.game = go ? AZ_GAME_GO : AZ_GAME_GOMOKU;
-    c.n_games = 1;
-    c.board_size = root_->getBoardSize();
-    c.num_simulations = config_.numSimulations;
-    c.c_puct = config_.cPuct;
-    c.fpu_reduction = config_.fpuReduction;
-    c.virtual_loss = config_.virtualLoss;
+    c.n_games = nGames;
+    c.board_size = state.getBoardSize();
+    c.num_simulations = config.numSimulations;
+    c.c_puct = config.cPuct;
+    c.fpu_reduction = config.fpuReduction;
+    c.virtual_loss = config.virtualLoss;
     c.eval_kind = ev.kind;
     c.eval_seed = ev.seed;
     c.zobrist_seed = 12345u;
     c.noise_seed = 42u;          // setDeterministicMode's rng seed (parallel_mcts.cpp:1268)
     c.noise_seed_stride = 0;
-    c.use_dirichlet_each_search = config_.useDirichletNoise ? 1 : 0;
-    c.dirichlet_alpha = config_.dirichletAlpha;
-    c.dirichlet_eps = config_.dirichletEpsilon;
-    const size_t ttsize = tt_ ? tt_->getSize() : (size_t)config_.transpositionTableSize;
+    c.use_dirichlet_each_search = config.useDirichletNoise ? 1 : 0;
+    c.dirichlet_alpha = config.dirichletAlpha;
+    c.dirichlet_eps = config.dirichletEpsilon;
+    const size_t ttsize = tt ? tt->getSize() : (size_t)config.transpositionTableSize;
     int k = 0;
     while (((size_t)1 << k) < ttsize && k < 24) ++k;
     c.tt_log2 = k;
     return c;
+}
+
+az_search_cfg ParallelMCTS::deviceConfig() const { return makeSearchConfig(config_, *root_, nn_, tt_, 1); }
+
+std::vector<uint8_t> ParallelMCTS::slotMask() const {
+    std::vector<uint8_t> m(group_ ? group_->capacity() : 1, 0);
+    m[slot_] = 1;
+    return m;
+}
+
+static bool sameSearch(const az_search_cfg& a, const az_search_cfg& b) {   // all but n_games
+    return a.game == b.game && a.board_size == b.board_size && a.num_simulations == b.num_simulations &&
+           a.c_puct == b.c_puct && a.fpu_reduction == b.fpu_reduction && a.virtual_loss == b.virtual_loss &&
+           a.eval_kind == b.eval_kind && a.eval_seed == b.eval_seed &&
+           a.use_dirichlet_each_search == b.use_dirichlet_each_search && a.dirichlet_alpha == b.dirichlet_alpha &&
+           a.dirichlet_eps == b.dirichlet_eps && a.tt_log2 == b.tt_log2;
 }
 
 // The reference's setters change config_ and keep the tree (parallel_mcts.h:172-182); the device
@@ -139,6 +175,10 @@ az_search_cfg ParallelMCTS::deviceConfig() const {
 // evaluator, the table size or a larger node pool is needed.
 void ParallelMCTS::applyConfig() {
     const az_search_cfg c = deviceConfig();
+    if (group_) {                          // the group's parameters are shared: other ones leave it
+        if (!sameSearch(c, group_->deviceConfig())) rebuild();
+        return;
+    }
     if (s_ && az_search_set_params(s_, &c) == 0) return;
     rebuild();
 }
@@ -155,8 +195,11 @@ void ParallelMCTS::rebuild() {
     std::vector<uint32_t> rng;
     if (s_) {
         rng.resize(AZ_RNG_STATE_WORDS);
-        check(az_search_get_rng(s_, 0, rng.data()), "az_search_get_rng");
-        az_search_destroy(s_);
+        check(az_search_get_rng(s_, slot_, rng.data()), "az_search_get_rng");
+        if (group_) group_->release(slot_);      // leaves the group: a handle of its own
+        else az_search_destroy(s_);
+        group_ = nullptr;
+        slot_ = 0;
         s_ = nullptr;
     }
     const DeviceEvaluator ev = deviceEvaluator(nn_);
@@ -176,10 +219,11 @@ void ParallelMCTS::rebuild() {
 
 void ParallelMCTS::search() {
     if (root_->isTerminal()) return;
-    check(az_search_run(s_), "az_search_run");
+    if (group_) group_->search(slot_);
+    else check(az_search_run(s_), "az_search_run");
     searched_ = true;
     int64_t c[5] = {0, 0, 0, 0, 0};
-    check(az_search_counters(s_, 0, c), "az_search_counters");
+    check(az_search_counters(s_, slot_, c), "az_search_counters");
     stats_.evaluationCalls = (size_t)c[0];
     stats_.cacheHits = (size_t)c[2];
     stats_.cacheMisses = (size_t)(c[1] - c[2]);
@@ -190,17 +234,24 @@ void ParallelMCTS::search() {
 }
 
 void ParallelMCTS::runSingleSimulation() {
-    check(az_search_simulate(s_, 1), "az_search_simulate");
+    if (group_) check(az_search_simulate_masked(s_, 1, slotMask().data()), "az_search_simulate_masked");
+    else check(az_search_simulate(s_, 1), "az_search_simulate");
     searched_ = true;
 }
 
 void ParallelMCTS::runBatchedSearch() {
     if (config_.numSimulations <= 0) return;
-    check(az_search_simulate(s_, config_.numSimulations), "az_search_simulate");
+    if (group_) check(az_search_simulate_masked(s_, config_.numSimulations, slotMask().data()), "az_search_simulate_masked");
+    else check(az_search_simulate(s_, config_.numSimulations), "az_search_simulate");
     searched_ = true;
 }
 
 size_t ParallelMCTS::releaseMemory(int visitThreshold) {
+    if (group_) {
+        std::vector<int64_t> pruned(group_->capacity(), 0);
+        check(az_search_release_masked(s_, visitThreshold, pruned.data(), slotMask().data()), "az_search_release_masked");
+        return (size_t)pruned[slot_];
+    }
     int64_t pruned = 0;
     check(az_search_release(s_, visitThreshold, &pruned), "az_search_release");
     return (size_t)pruned;
@@ -208,11 +259,11 @@ size_t ParallelMCTS::releaseMemory(int visitThreshold) {
 
 int ParallelMCTS::selectAction(bool isTraining, float temperature) {
     int flags = 0;
-    check(az_search_root_flags(s_, 0, &flags), "az_search_root_flags");
+    check(az_search_root_flags(s_, slot_, &flags), "az_search_root_flags");
     if (!(flags & AZ_NODE_EXPANDED)) search();        // parallel_mcts.cpp:988-991
     const std::vector<int> legal = root_->getLegalMoves();
     int act = -1;
-    check(az_search_select_action(s_, 0, isTraining ? 1 : 0, temperature, config_.useBatchInference ? 1 : 0,
+    check(az_search_select_action(s_, slot_, isTraining ? 1 : 0, temperature, config_.useBatchInference ? 1 : 0,
                                   legal.data(), (int)legal.size(), &act),
           "az_search_select_action");
     return act;
@@ -221,8 +272,8 @@ int ParallelMCTS::selectAction(bool isTraining, float temperature) {
 MCTSNode ParallelMCTS::getRootNode() const {
     MCTSNode r;
     int flags = 0;
-    check(az_search_root_flags(s_, 0, &flags), "az_search_root_flags");
-    check(az_search_root_node(s_, 0, &r.visitCount, &r.virtualLoss, &r.valueSum), "az_search_root_node");
+    check(az_search_root_flags(s_, slot_, &flags), "az_search_root_flags");
+    check(az_search_root_node(s_, slot_, &r.visitCount, &r.virtualLoss, &r.valueSum), "az_search_root_node");
     r.isExpanded = (flags & AZ_NODE_EXPANDED) != 0;
     r.isTerminal = (flags & AZ_NODE_TERMINAL) != 0;
     r.gameResult = r.isTerminal ? (core::GameResult)((flags >> 2) & 3) : root_->getGameResult();
@@ -231,7 +282,7 @@ MCTSNode ParallelMCTS::getRootNode() const {
     std::vector<int> act(A), N(A), VL(A);
     std::vector<float> W(A), P(A);
     int n = 0;
-    check(az_search_root_children(s_, 0, act.data(), N.data(), VL.data(), W.data(), P.data(), &n), "az_search_root_children");
+    check(az_search_root_children(s_, slot_, act.data(), N.data(), VL.data(), W.data(), P.data(), &n), "az_search_root_children");
     for (int i = 0; i < n; ++i) {
         auto c = std::make_shared<MCTSNode>();
         c->visitCount = N[i]; c->virtualLoss = VL[i]; c->valueSum = W[i]; c->prior = P[i]; c->action = act[i];
@@ -241,48 +292,54 @@ MCTSNode ParallelMCTS::getRootNode() const {
     return r;
 }
 
+// getActionProbabilities(T) + getChildActions + getRootValue of this object's game: az_search_select
+// reports every game of the handle (a group's: every slot), this slot's row is taken
+ParallelMCTS::RootSelect ParallelMCTS::rootSelect(float temperature) const {
+    const int G = group_ ? group_->capacity() : 1;
+    const int NA = root_->getActionSpaceSize();
+    std::vector<int> act(G), nch(G), cact((size_t)G * NA);
+    std::vector<float> val(G), probs((size_t)G * NA);
+    check(az_search_select(s_, 1, temperature, act.data(), val.data(), probs.data(), cact.data(), nch.data()),
+          "az_search_select");
+    RootSelect r;
+    const size_t o = (size_t)slot_ * NA;
+    r.probs.assign(probs.begin() + o, probs.begin() + o + nch[slot_]);
+    r.actions.assign(cact.begin() + o, cact.begin() + o + nch[slot_]);
+    r.value = val[slot_];
+    return r;
+}
+
 std::vector<float> ParallelMCTS::getActionProbabilities(float temperature) const {
-    int act = -1, nch = 0;
-    float val = 0.0f;
-    const int A = root_->getActionSpaceSize();
-    std::vector<float> probs(A);
-    std::vector<int> cact(A);
-    check(az_search_select(s_, 1, temperature, &act, &val, probs.data(), cact.data(), &nch), "az_search_select");
-    probs.resize(nch);
-    return probs;
+    const RootSelect r = rootSelect(temperature);
+    return r.probs;
 }
 
 std::vector<int> ParallelMCTS::getChildActions() const {
-    int act = -1, nch = 0;
-    float val = 0.0f;
-    const int A = root_->getActionSpaceSize();
-    std::vector<float> probs(A);
-    std::vector<int> cact(A);
-    check(az_search_select(s_, 1, 1.0f, &act, &val, probs.data(), cact.data(), &nch), "az_search_select");
-    cact.resize(nch);
-    return cact;
+    return rootSelect(1.0f).actions;
 }
 
 float ParallelMCTS::getRootValue() const {
-    int act = -1, nch = 0;
-    float val = 0.0f;
-    const int A = root_->getActionSpaceSize();
-    std::vector<float> probs(A);
-    std::vector<int> cact(A);
-    check(az_search_select(s_, 1, 1.0f, &act, &val, probs.data(), cact.data(), &nch), "az_search_select");
-    return val;
+    return rootSelect(1.0f).value;
 }
 
 void ParallelMCTS::updateWithMove(int action) {
     root_->makeMove(action);
-    int t = 0, r = 0;
-    check(az_search_apply(s_, &action, &t, &r), "az_search_apply");
+    if (group_) {                          // only this slot moves (the others get no action)
+        const int G = group_->capacity();
+        std::vector<int> acts(G, AZ_ACTION_NONE), t(G), r(G);
+        acts[slot_] = action;
+        check(az_search_apply(s_, acts.data(), t.data(), r.data()), "az_search_apply");
+    } else {
+        int t = 0, r = 0;
+        check(az_search_apply(s_, &action, &t, &r), "az_search_apply");
+    }
     searched_ = false;
 }
 
 void ParallelMCTS::addDirichletNoise(float alpha, float epsilon) {
     if (root_->isTerminal()) return;
-    check(az_search_add_noise(s_, alpha, epsilon), "az_search_add_noise");
+    if (group_) check(az_search_add_noise_masked(s_, alpha, epsilon, slotMask().data()), "az_search_add_noise_masked");
+    else check(az_search_add_noise(s_, alpha, epsilon), "az_search_add_noise");
 }
 
 void ParallelMCTS::setNumSimulations(int n) { config_.numSimulations = n; applyConfig(); }
@@ -296,6 +353,10 @@ void ParallelMCTS::setVirtualLoss(int v) { config_.virtualLoss = v; applyConfig(
 // network seed, table size) needs a new handle: the history is replayed and the tree rebuilt.
 void ParallelMCTS::setNeuralNetwork(nn::NeuralNetwork* nn) {
     const DeviceEvaluator cur = deviceEvaluator(nn_), nxt = deviceEvaluator(nn);
+    if (group_) {                          // the group's evaluator is shared: another one leaves it
+        if (nn != nn_) { nn_ = nn; rebuild(); }
+        return;
+    }
     nn_ = nn;
     if (s_ && cur.kind == AZ_EVAL_NET && nxt.kind == AZ_EVAL_NET && cur.engine == nxt.engine &&
         az_search_set_net(s_, nxt.net) == 0)
@@ -307,6 +368,10 @@ void ParallelMCTS::setTranspositionTable(TranspositionTable* tt) {
     const az_search_cfg before = deviceConfig();
     TranspositionTable* old = tt_;
     tt_ = tt;
+    if (group_) {                          // a table of its own: the member leaves the group
+        if (tt != old) rebuild();
+        return;
+    }
     if (s_ && deviceConfig().tt_log2 == before.tt_log2) {
         if (tt != old) check(az_search_clear_tt(s_), "az_search_clear_tt");
         return;
@@ -319,7 +384,7 @@ void ParallelMCTS::setDeterministicMode(bool enable) {
     config_.deterministic = enable;
     config_.useBatchInference = enable;
     std::random_device rd;
-    check(az_search_seed(s_, 0, enable ? 42u : rd()), "az_search_seed");
+    check(az_search_seed(s_, slot_, enable ? 42u : rd()), "az_search_seed");
 }
 
 std::vector<std::tuple<int, int, float, float>> ParallelMCTS::analyzePosition(int topN) const {
@@ -327,7 +392,7 @@ std::vector<std::tuple<int, int, float, float>> ParallelMCTS::analyzePosition(in
     std::vector<int> act(A), N(A), VL(A);
     std::vector<float> W(A), P(A);
     int n = 0;
-    check(az_search_root_children(s_, 0, act.data(), N.data(), VL.data(), W.data(), P.data(), &n),
+    check(az_search_root_children(s_, slot_, act.data(), N.data(), VL.data(), W.data(), P.data(), &n),
           "az_search_root_children");
     std::vector<std::tuple<int, int, float, float>> out;
     for (int i = 0; i < n; ++i) out.emplace_back(act[i], N[i], N[i] > 0 ? W[i] / (float)N[i] : 0.0f, P[i]);
@@ -339,7 +404,7 @@ std::vector<std::tuple<int, int, float, float>> ParallelMCTS::analyzePosition(in
 std::string ParallelMCTS::getSearchInfo() const {
     int N = 0, VL = 0;
     float W = 0.0f;
-    check(az_search_root_node(s_, 0, &N, &VL, &W), "az_search_root_node");
+    check(az_search_root_node(s_, slot_, &N, &VL, &W), "az_search_root_node");
     std::ostringstream o;
     o << "root visits " << N << ", value " << (N ? W / (float)N : 0.0f) << ", simulations "
       << stats_.simulationCount.load() << ", evaluations " << stats_.evaluationCalls.load() << ", TT hits "

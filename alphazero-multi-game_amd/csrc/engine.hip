@@ -12,6 +12,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <mutex>
 #include <sstream>
 #include <chrono>
@@ -38,7 +39,7 @@ __global__ void k_select_action(TreeDev t, int training, float temperature, cons
 __global__ void k_apply(TreeDev t, const int* actions, int* terminal, int* result);
 __global__ void k_compact(TreeDev t, Nodes dst, int* src_of);
 __global__ void k_leaf_moves(TreeDev t, int* moves, int* len);
-__global__ void k_prune(TreeDev t, Nodes dst, int* src_of, int thr, long long* pruned);
+__global__ void k_prune(TreeDev t, Nodes dst, int* src_of, int thr_all, const int* thr_g, long long* pruned);
 __global__ void k_noise(TreeDev t, const float* noise, const uint8_t* mask, float eps);
 __global__ void k_new_games(TreeDev t, const int* games, const int* seed_ids, int n, uint32_t eval_seed);
 __global__ void k_tt_clear(TreeDev t, const int* games, int n);
@@ -1744,16 +1745,24 @@ int az_search_simulate(az_search* s, int n) {
     return check_err(s);
 }
 
-int az_search_release(az_search* s, int threshold, int64_t* pruned) {
-    if (!s) return az_fail(AZ_ERR_ARG, "null search");
-    std::lock_guard<std::mutex> lk(s->mu);
+static int search_release(az_search* s, int threshold, int64_t* pruned, const uint8_t* mask) {
     HIPCHK(hipSetDevice(s->e->device));
     hipStream_t st = s->e->stream;
     const int G = s->c.n_games;
     long long* d_pr = nullptr;
+    int* d_thr = nullptr;
     DALLOC(d_pr, G);
+    if (mask) {   // games outside the mask keep every child (the whole tree is copied as it is)
+        std::vector<int> thr(G);
+        for (int g = 0; g < G; ++g) thr[g] = mask[g] ? threshold : 0;
+        if (dalloc(&d_thr, G)) { hipFree(d_pr); return AZ_ERR_HIP; }
+        if (hipMemcpy(d_thr, thr.data(), (size_t)G * 4, hipMemcpyHostToDevice) != hipSuccess) {
+            hipFree(d_pr); hipFree(d_thr);
+            return az_fail(AZ_ERR_HIP, "hipMemcpy");
+        }
+    }
     s->t.nd = s->arena[s->cur];
-    hipLaunchKernelGGL(k_prune, dim3(G), dim3(64), 0, st, s->t, s->arena[s->cur ^ 1], s->d_src_of, threshold, d_pr);
+    hipLaunchKernelGGL(k_prune, dim3(G), dim3(64), 0, st, s->t, s->arena[s->cur ^ 1], s->d_src_of, threshold, d_thr, d_pr);
     s->cur ^= 1;
     s->t.nd = s->arena[s->cur];
     std::vector<long long> pr(G);
@@ -1761,10 +1770,74 @@ int az_search_release(az_search* s, int threshold, int64_t* pruned) {
     hipError_t e2 = hipMemcpyAsync(pr.data(), d_pr, (size_t)G * 8, hipMemcpyDeviceToHost, st);
     hipError_t e3 = hipStreamSynchronize(st);
     hipFree(d_pr);
+    if (d_thr) hipFree(d_thr);
     if (e1 != hipSuccess || e2 != hipSuccess || e3 != hipSuccess)
         return az_fail(AZ_ERR_HIP, "az_search_release: %s", hipGetErrorString(e1 != hipSuccess ? e1 : e2 != hipSuccess ? e2 : e3));
     if (pruned) for (int g = 0; g < G; ++g) pruned[g] = pr[g];
     return check_err(s);
+}
+
+int az_search_release(az_search* s, int threshold, int64_t* pruned) {
+    if (!s) return az_fail(AZ_ERR_ARG, "null search");
+    std::lock_guard<std::mutex> lk(s->mu);
+    return search_release(s, threshold, pruned, nullptr);
+}
+
+int az_search_release_masked(az_search* s, int threshold, int64_t* pruned, const uint8_t* mask) {
+    if (!s || !mask) return az_fail(AZ_ERR_ARG, "null argument");
+    std::lock_guard<std::mutex> lk(s->mu);
+    return search_release(s, threshold, pruned, mask);
+}
+
+// Park every game outside `mask` (inactive on the host and the device) around fn, then give the
+// parked games their flags back: the masked entry points run the search of some games of a handle
+// that several host objects share (mcts::SearchGroup), leaving the others' trees untouched.
+static int with_masked(az_search* s, const uint8_t* mask, const std::function<int()>& fn) {
+    const int G = s->c.n_games;
+    const std::vector<int> saved = s->active;
+    std::vector<int> now(G);
+    bool parked = false;
+    for (int g = 0; g < G; ++g) {
+        now[g] = saved[g] && mask[g];
+        parked |= now[g] != saved[g];
+    }
+    if (parked) {
+        s->active = now;
+        HIPCHK(hipMemcpy(s->t.active, now.data(), (size_t)G * 4, hipMemcpyHostToDevice));
+    }
+    const int r = fn();
+    if (parked) {
+        HIPCHK(hipStreamSynchronize(s->e->stream));
+        std::vector<int> back(G);
+        for (int g = 0; g < G; ++g) back[g] = mask[g] ? s->active[g] : saved[g];
+        s->active = back;
+        HIPCHK(hipMemcpy(s->t.active, back.data(), (size_t)G * 4, hipMemcpyHostToDevice));
+    }
+    return r;
+}
+
+int az_search_run_masked(az_search* s, const uint8_t* mask) {
+    if (!s || !mask) return az_fail(AZ_ERR_ARG, "null argument");
+    std::lock_guard<std::mutex> lk(s->mu);
+    HIPCHK(hipSetDevice(s->e->device));
+    return with_masked(s, mask, [&] { return search_run(s); });
+}
+
+int az_search_simulate_masked(az_search* s, int n, const uint8_t* mask) {
+    if (!s || !mask || n < 0) return az_fail(AZ_ERR_ARG, "bad argument");
+    std::lock_guard<std::mutex> lk(s->mu);
+    HIPCHK(hipSetDevice(s->e->device));
+    return with_masked(s, mask, [&] {
+        if (int r = search_sims(s, n)) return r;
+        return check_err(s);
+    });
+}
+
+int az_search_new_games_ids(az_search* s, const int* games, const int* seed_ids, int n) {
+    if (!s || (!games && n) || (!seed_ids && n)) return az_fail(AZ_ERR_ARG, "null argument");
+    std::lock_guard<std::mutex> lk(s->mu);
+    HIPCHK(hipSetDevice(s->e->device));
+    return search_new_games(s, games, n, seed_ids);
 }
 
 int az_search_select_action(az_search* s, int game, int training, float temperature, int batch_inference,

@@ -1302,10 +1302,12 @@ __global__ __launch_bounds__(256) void k_compact(TreeDev t, Nodes dst, int* src_
 // visitCount >= threshold (in child order; the root itself stays).  A node whose children all go
 // stays expanded with none.  pruned[g] = nodes before - nodes after (getTreeSize of every removed
 // subtree: the arena holds exactly the tree).
-__global__ __launch_bounds__(64) void k_prune(TreeDev t, Nodes dst, int* src_of, int thr, long long* pruned) {
+__global__ __launch_bounds__(64) void k_prune(TreeDev t, Nodes dst, int* src_of, int thr_all, const int* thr_g,
+                                              long long* pruned) {
     const int g = blockIdx.x;
     const int lane = threadIdx.x;
     if (g >= t.G) return;
+    const int thr = thr_g ? thr_g[g] : thr_all;     // per game (0: keep every child, the whole tree)
     const size_t base = (size_t)g * t.ncap;
     GamePtrs s = game_nodes(t.nd, base);
     GamePtrs d = game_nodes(dst, base);

@@ -195,6 +195,16 @@ int az_search_simulate(az_search* s, int n);
  * their subtrees, recursively from the root (child order kept; a node that loses every child
  * stays expanded).  pruned[g] (optional, G entries) = nodes removed (getTreeSize of each). */
 int az_search_release(az_search* s, int threshold, int64_t* pruned);
+/* The same for the games with mask[g] != 0 only (G entries); the other games' trees are untouched:
+ * the entry points of a handle that several host objects share (mcts::SearchGroup).  The masked
+ * search / simulation park the other games for the call (inactive), release copies their trees
+ * whole. */
+int az_search_run_masked(az_search* s, const uint8_t* mask);
+int az_search_simulate_masked(az_search* s, int n, const uint8_t* mask);
+int az_search_release_masked(az_search* s, int threshold, int64_t* pruned, const uint8_t* mask);
+/* az_search_new_games with each game's stream id for the evaluator / noise seeds given (default:
+ * the slot index): id 0 makes a slot's game the one a single-game handle plays. */
+int az_search_new_games_ids(az_search* s, const int* games, const int* seed_ids, int n);
 /* ParallelMCTS::selectAction(isTraining, T) of one game (parallel_mcts.cpp:987-1047).
  * batch_inference != 0 (MCTSConfig::useBatchInference, forced by setDeterministicMode and
  * SelfPlayManager): the deterministic rules of az_search_select.  Otherwise draws on the game's

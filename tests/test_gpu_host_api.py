@@ -329,12 +329,111 @@ def test_host_setters_keep_the_tree():
     m.setTranspositionTable(az.TranspositionTable(1 << 16))
     assert m.getRootNode().visitCount == n0
     m.search()
-    assert m.getRootNode().visitCount == n0 + sims
+    assert m.getRootNode().visitCount == 2 * n0      # the second search adds as many visits as the first
     # another trunk of the same board swaps in too; another evaluator kind needs a new handle
     # (history replayed, fresh tree)
     c = az.HipNeuralNetwork(boardSize=bs, channels=64, blocks=2, precision=0, maxBatch=1)
     c.initRandom(3)
     m.setNeuralNetwork(c)
-    assert m.getRootNode().visitCount == n0 + sims
+    assert m.getRootNode().visitCount == 2 * n0
     m.setNeuralNetwork(az.RandomPolicyNetwork(az.GameType.GOMOKU, bs, 3))
     assert m.getRootNode().visitCount == 0
+
+
+def _opening(bs, k, seed):
+    import random
+    rng = random.Random(seed)
+    s = az.GomokuState(bs)
+    for _ in range(k):
+        s.makeMove(rng.choice(s.getLegalMoves()))
+    return s
+
+
+def _root_bits(m):
+    r = m.getRootNode()
+    return (r.visitCount, r.virtualLoss, bits([r.valueSum])[0],
+            [(a, c.visitCount, c.virtualLoss, bits([c.valueSum])[0], bits([c.prior])[0]) for a, c in zip(r.actions, r.children)])
+
+
+def _play(objs, moves, stochastic):
+    """Each object: search, record its root, select (stochastic draws on rng_ when asked), move, noise."""
+    out = [[] for _ in objs]
+    for _ in range(moves):
+        for i, m in enumerate(objs):
+            m.search()
+            out[i].append(_root_bits(m))
+            a = m.selectAction(True, 1.0)
+            out[i].append(a)
+            m.updateWithMove(a)
+            m.addDirichletNoise(0.03, 0.25)
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("evaluator", ["random", "net"])
+def test_search_group_matches_standalone(evaluator):
+    """SearchGroup members (one device handle, a slot per object) play exactly what standalone objects
+    play -- root statistics bit for bit after every search, the same actions -- sequentially and with
+    one thread per member whose concurrent searches batch into shared device runs."""
+    import threading
+    bs, sims, n, moves = 9, 48, 6, 3
+    cfg = az.MCTSConfig()
+    cfg.numSimulations = sims
+    if evaluator == "random":
+        net = az.RandomPolicyNetwork(az.GameType.GOMOKU, bs, 7)
+    else:
+        net = az.HipNeuralNetwork(boardSize=bs, channels=32, blocks=1, precision=0, maxBatch=8)
+        net.initRandom(4)
+    openings = [_opening(bs, k, 100 + k) for k in range(n)]
+
+    def standalone():
+        objs = [az.ParallelMCTS(o, cfg, net, az.TranspositionTable(1 << 20)) for o in openings]
+        for i, m in enumerate(objs):
+            m.setDeterministicMode(True)
+            if i % 2:
+                c2 = az.MCTSConfig()
+                c2.numSimulations = sims
+                c2.useBatchInference = False          # stochastic selectAction on rng_
+                m.setConfig(c2)
+        return objs
+    want = _play(standalone(), moves, True)
+
+    group = az.SearchGroup(net, cfg, az.GomokuState(bs), 8)
+    members = [az.ParallelMCTS(o, group) for o in openings]
+    for i, m in enumerate(members):
+        assert m.inGroup()
+        m.setDeterministicMode(True)
+        if i % 2:
+            c2 = az.MCTSConfig()
+            c2.numSimulations = sims
+            c2.useBatchInference = False              # host-side only: stays in the group
+            m.setConfig(c2)
+            assert m.inGroup()
+    assert group.members() == n
+    assert _play(members, moves, True) == want
+
+    # one thread per member: concurrent searches share device runs
+    group2 = az.SearchGroup(net, cfg, az.GomokuState(bs), 8)
+    group2.setGatherMicros(20000)
+    mem2 = [az.ParallelMCTS(o, group2) for o in openings]
+    for i, m in enumerate(mem2):
+        m.setDeterministicMode(True)
+        if i % 2:
+            c2 = az.MCTSConfig()
+            c2.numSimulations = sims
+            c2.useBatchInference = False
+            m.setConfig(c2)
+    got = [None] * n
+
+    def run(i):
+        got[i] = _play([mem2[i]], moves, True)[0]
+    th = [threading.Thread(target=run, args=(i,)) for i in range(n)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert got == want
+    assert group2.searches() == n * moves and group2.deviceRuns() < group2.searches()
+    # a member whose search parameters change leaves the group (its history replayed)
+    mem2[0].setNumSimulations(sims + 16)
+    assert not mem2[0].inGroup() and group2.members() == n - 1
