@@ -1,0 +1,38 @@
+#!/usr/bin/env python3
+"""Progress of a search under rocprofv3 --pmc (tools/pmc_hang_probe.sh): a handle sized for
+--cap-sims simulations per move (node pool, prior ring), --games games, the C3 net cut to --blocks
+blocks; then --run-sims simulations in chunks of --chunk, a timestamped line after each (flushed),
+so a killed pass shows where it stopped."""
+import argparse
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "alphazero-multi-game_amd"))
+import az_amd  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--games", type=int, default=256)
+ap.add_argument("--cap-sims", type=int, default=800)
+ap.add_argument("--run-sims", type=int, default=800)
+ap.add_argument("--chunk", type=int, default=50)
+ap.add_argument("--blocks", type=int, default=2)
+a = ap.parse_args()
+t0 = time.perf_counter()
+eng = az_amd.Engine(0)
+net = az_amd.HipNeuralNetwork(eng, az_amd.gomoku_net_desc(board_size=15, channels=256, blocks=a.blocks,
+                                                          precision=az_amd.AZ_PREC_FP16, max_batch=a.games))
+net.init_random(1234)
+m = az_amd.ParallelMCTS(eng, net=net, n_games=a.games, board_size=15, num_simulations=a.cap_sims,
+                        evaluator=az_amd.AZ_EVAL_NET, noise_seed=42, noise_seed_stride=1)
+m.newGames()
+m.addDirichletNoise(0.03, 0.25)
+print(f"{time.perf_counter() - t0:8.2f} s  created ({a.games} games, capacity {a.cap_sims} sims)", flush=True)
+done = 0
+while done < a.run_sims:
+    k = min(a.chunk, a.run_sims - done)
+    m.runSingleSimulation(k)
+    done += k
+    print(f"{time.perf_counter() - t0:8.2f} s  {done} sims", flush=True)
+print("finished", flush=True)
