@@ -53,8 +53,10 @@ class SearchGroup {
     int members() const;
     size_t searches() const;       // member search() calls served
     size_t deviceRuns() const;     // masked device searches that served them
-    // A search() that finds no run in progress waits this long for other members' requests before
-    // it starts (default 0: requests that arrive during a run are batched into the next one).
+    // A search() that finds no run in progress waits up to this long for every live member's request
+    // before it starts (default 2000 us: one thread per member issues its next search a few host calls
+    // after the last run; a single-threaded caller pays the wait once per search); 0: requests that
+    // arrive during a run are batched into the next one only.
     void setGatherMicros(int us);
 
  private:
@@ -76,7 +78,7 @@ class SearchGroup {
     std::set<int> pending_, inflight_;
     std::map<int, std::string> errors_;
     bool running_ = false;
-    int gatherUs_ = 0;
+    int gatherUs_ = 2000;
     size_t searches_ = 0, runs_ = 0;
 };
 

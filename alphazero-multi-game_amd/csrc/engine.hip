@@ -829,6 +829,8 @@ struct az_search {
     float* d_noise = nullptr; uint8_t* d_mask = nullptr;
     int* d_actions = nullptr; float* d_values = nullptr; float* d_probs = nullptr; int* d_cact = nullptr; int* d_nch = nullptr;
     int* d_term = nullptr; int* d_res = nullptr; int* d_games = nullptr; int* d_seed_ids = nullptr;
+    // scratch allocated once: one game's root-children readback, per-game prune thresholds / counts
+    int* d_rc = nullptr; float* d_rcf = nullptr; int* d_thr = nullptr; long long* d_pruned = nullptr;
     float* d_temps = nullptr;
     // host mirrors
     std::vector<int> stones, active, fresh, ply, expanded;
@@ -1625,6 +1627,7 @@ int az_search_create(az_engine* e, az_net* net, const az_search_cfg* c, az_searc
     if (c->eval_kind == AZ_EVAL_CALLBACK) { SA(s->d_lmoves, (size_t)G * AZ_DMAX); SA(s->d_llen, G); }
     SA(s->d_noise, (size_t)G * NA); SA(s->d_mask, G); SA(s->d_actions, G); SA(s->d_values, G); SA(s->d_probs, (size_t)G * NA);
     SA(s->d_cact, (size_t)G * NA); SA(s->d_nch, G); SA(s->d_term, G); SA(s->d_res, G); SA(s->d_games, G); SA(s->d_seed_ids, G); SA(s->d_temps, G);
+    SA(s->d_rc, 4 * (size_t)NA + 8); SA(s->d_rcf, 2 * (size_t)NA + 4); SA(s->d_thr, G); SA(s->d_pruned, G);
 #undef SA
     if (r) { az_search_destroy(s); return r; }
     t.zpiece = zp; t.zplayer = zpl; t.fresh_order = fo; t.zko = zko;
@@ -1696,7 +1699,8 @@ void az_search_destroy(az_search* s) {
                           (const void*)s->d_src_of, (const void*)s->d_batch, (const void*)s->d_id, (const void*)s->d_logits,
                           (const void*)s->d_value, (const void*)s->d_noise, (const void*)s->d_mask, (const void*)s->d_actions,
                           (const void*)s->d_values, (const void*)s->d_probs, (const void*)s->d_cact, (const void*)s->d_nch,
-                          (const void*)s->d_term, (const void*)s->d_res, (const void*)s->d_games, (const void*)s->d_seed_ids, (const void*)s->d_temps})
+                          (const void*)s->d_term, (const void*)s->d_res, (const void*)s->d_games, (const void*)s->d_seed_ids, (const void*)s->d_temps,
+                          (const void*)s->d_rc, (const void*)s->d_rcf, (const void*)s->d_thr, (const void*)s->d_pruned})
         F(p);
     delete s;
 }
@@ -1749,17 +1753,13 @@ static int search_release(az_search* s, int threshold, int64_t* pruned, const ui
     HIPCHK(hipSetDevice(s->e->device));
     hipStream_t st = s->e->stream;
     const int G = s->c.n_games;
-    long long* d_pr = nullptr;
+    long long* d_pr = s->d_pruned;
     int* d_thr = nullptr;
-    DALLOC(d_pr, G);
     if (mask) {   // games outside the mask keep every child (the whole tree is copied as it is)
         std::vector<int> thr(G);
         for (int g = 0; g < G; ++g) thr[g] = mask[g] ? threshold : 0;
-        if (dalloc(&d_thr, G)) { hipFree(d_pr); return AZ_ERR_HIP; }
-        if (hipMemcpy(d_thr, thr.data(), (size_t)G * 4, hipMemcpyHostToDevice) != hipSuccess) {
-            hipFree(d_pr); hipFree(d_thr);
-            return az_fail(AZ_ERR_HIP, "hipMemcpy");
-        }
+        d_thr = s->d_thr;
+        HIPCHK(hipMemcpy(d_thr, thr.data(), (size_t)G * 4, hipMemcpyHostToDevice));
     }
     s->t.nd = s->arena[s->cur];
     hipLaunchKernelGGL(k_prune, dim3(G), dim3(64), 0, st, s->t, s->arena[s->cur ^ 1], s->d_src_of, threshold, d_thr, d_pr);
@@ -1769,8 +1769,6 @@ static int search_release(az_search* s, int threshold, int64_t* pruned, const ui
     hipError_t e1 = hipGetLastError();
     hipError_t e2 = hipMemcpyAsync(pr.data(), d_pr, (size_t)G * 8, hipMemcpyDeviceToHost, st);
     hipError_t e3 = hipStreamSynchronize(st);
-    hipFree(d_pr);
-    if (d_thr) hipFree(d_thr);
     if (e1 != hipSuccess || e2 != hipSuccess || e3 != hipSuccess)
         return az_fail(AZ_ERR_HIP, "az_search_release: %s", hipGetErrorString(e1 != hipSuccess ? e1 : e2 != hipSuccess ? e2 : e3));
     if (pruned) for (int g = 0; g < G; ++g) pruned[g] = pr[g];
@@ -1875,10 +1873,8 @@ int az_search_select_action(az_search* s, int game, int training, float temperat
     std::vector<float> W(NA), P(NA);
     int n = 0;
     s->t.nd = s->arena[s->cur];
-    int* d_tmp = nullptr;
-    DALLOC(d_tmp, 4 * (size_t)NA + 8);
-    float* d_f = nullptr;
-    if (int r = dalloc(&d_f, 2 * (size_t)NA + 4)) { hipFree(d_tmp); return r; }
+    int* d_tmp = s->d_rc;
+    float* d_f = s->d_rcf;
     hipStream_t st = s->e->stream;
     hipLaunchKernelGGL(k_root_children, dim3(1), dim3(64), 0, st, s->t, game, d_tmp, d_tmp + NA, d_tmp + 2 * NA, d_f,
                        d_f + NA, d_tmp + 3 * NA, d_tmp + 3 * NA + 1, d_f + 2 * NA);
@@ -1886,7 +1882,6 @@ int az_search_select_action(az_search* s, int game, int training, float temperat
     hipError_t e2 = hipMemcpyAsync(N.data(), d_tmp + NA, NA * 4, hipMemcpyDeviceToHost, st);
     hipError_t e3 = hipMemcpyAsync(&n, d_tmp + 3 * NA, 4, hipMemcpyDeviceToHost, st);
     hipError_t e4 = hipStreamSynchronize(st);
-    hipFree(d_tmp); hipFree(d_f);
     if (e1 != hipSuccess || e2 != hipSuccess || e3 != hipSuccess || e4 != hipSuccess)
         return az_fail(AZ_ERR_HIP, "az_search_sample_action: root children readback failed");
     int mx = 0;

@@ -47,7 +47,7 @@ def main():
     ap.add_argument("--channels", type=int, default=64)
     ap.add_argument("--blocks", type=int, default=6)
     ap.add_argument("--standalone-games", type=int, default=8)
-    ap.add_argument("--gather-us", type=int, default=0)
+    ap.add_argument("--gather-us", type=int, default=2000)
     a = ap.parse_args()
     bs, G = 15, a.games
     cfg = az.MCTSConfig()
