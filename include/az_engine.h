@@ -85,7 +85,9 @@ int az_net_create(az_engine* e, const az_net_desc* desc, az_net** out);
  * Watts-Strogatz graph with routers.  desc: conv_bias 0, pool = min(8, board), precision AZ_PREC_F32
  * (the module's arithmetic; parity mode), or on 15x15 with channels % 64 == 0 AZ_PREC_BF16X3
  * (fp32-faithful split-operand node convs from 128 boards of capacity; parity mode) or AZ_PREC_FP16
- * (fp16-operand node convs and routers; throughput mode) -- SE and the residual stream stay fp32;
+ * (fp16-operand node convs and routers; throughput mode: node inputs are rounded to fp16 with no
+ * range guard, so a net whose trunk activations exceed 65504 overflows to inf -- keep such nets on
+ * AZ_PREC_F32 / AZ_PREC_BF16X3) -- SE and the residual stream stay fp32;
  * the reference's heads are
  * head_channels 32, fc_hidden 256; residual is ignored.  The blob is the
  * reference module's state_dict order (num_batches_tracked dropped); every other az_net_* call and
