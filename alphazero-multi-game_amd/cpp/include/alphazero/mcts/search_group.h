@@ -53,10 +53,12 @@ class SearchGroup {
     int members() const;
     size_t searches() const;       // member search() calls served
     size_t deviceRuns() const;     // masked device searches that served them
-    // A search() that finds no run in progress waits up to this long for every live member's request
-    // before it starts (default 2000 us: one thread per member issues its next search a few host calls
-    // after the last run; a single-threaded caller pays the wait once per search); 0: requests that
-    // arrive during a run are batched into the next one only.
+    // A search() that finds no run in progress gathers the other live members' requests before it
+    // starts: until every live member has one in, or no new one has arrived for this long (a sliding
+    // window, at most 64 windows in all).  Default 2000 us: one thread per member issues its next
+    // search a few host calls (selectAction, updateWithMove, noise: each a short device call on the
+    // shared handle) after the last run; a single-threaded caller pays one window per search.
+    // 0: requests that arrive during a run are batched into the next one only.
     void setGatherMicros(int us);
 
  private:

@@ -1,6 +1,7 @@
 // search_group.cpp -- mcts::SearchGroup (alphazero/mcts/search_group.h).
 #include "alphazero/mcts/search_group.h"
 
+#include <algorithm>
 #include <chrono>
 #include <stdexcept>
 
@@ -108,10 +109,23 @@ void SearchGroup::search(int slot) {
         }
         running_ = true;
         if (gatherUs_ > 0) {
-            const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(gatherUs_);
+            // sliding window: every new request extends it by gatherUs_, up to 64 windows in all
+            using clk = std::chrono::steady_clock;
+            const auto win = std::chrono::microseconds(gatherUs_);
+            const auto cap = clk::now() + 64 * win;
+            auto until = clk::now() + win;
+            size_t seen = pending_.size();
             int live = 0;
             for (char u : used_) live += u != 0;
-            cv_.wait_until(lk, until, [&] { return (int)pending_.size() >= live; });
+            while ((int)pending_.size() < live) {
+                const auto t = clk::now();
+                if (t >= until || t >= cap) break;
+                cv_.wait_until(lk, std::min(until, cap));
+                if (pending_.size() != seen) {
+                    seen = pending_.size();
+                    until = clk::now() + win;
+                }
+            }
         }
         std::vector<uint8_t> mask(capacity_, 0);
         for (int g : pending_) mask[g] = 1;

@@ -96,6 +96,9 @@ def parse(argv=None):
     ap.add_argument("--time-budget", type=float, default=560.0,
                     help="seconds: parity_mode is skipped (and says so) when the run so far plus its estimated "
                          "time would exceed this (the driver's run limit is 600 s)")
+    ap.add_argument("--kernel-timing", type=int, default=1,
+                    help="HIP events around sampled trunk / tree launches (the roofline); 0 for rocprofv3 --pmc "
+                         "passes: a search that records events hangs under counter collection (tools/pmc_hang_probe2.sh)")
     ap.add_argument("--dist-timeout", type=float, default=600.0,
                     help="seconds a rank waits in a collective / barrier before the bench fails (N>1)")
     a = ap.parse_args(argv)
@@ -211,8 +214,9 @@ def run_rank(a, rank, world, dist, make_workload, coll_device):
         if dist is not None:
             dist.barrier()
     barrier()
-    net.profile(True)
-    wl.mcts.profile(True)
+    if a.kernel_timing:
+        net.profile(True)
+        wl.mcts.profile(True)
     t0 = time.perf_counter()
     moves = evals = 0
     for _ in range(a.steps):

@@ -1,25 +1,26 @@
-# rocprofv3 HBM traffic of the tree kernels (k_select, k_expand_backup, k_scan) and the record ->
-# g8 input kernel (k_rec_to_g8) over one full C3 move (2048 games, 800 sims): a kernel-trace pass,
-# then FETCH_SIZE and WRITE_SIZE in separate passes.  The net is cut to 2 residual blocks (tree
-# traffic does not depend on the trunk's depth): counters over the full 20-block run's 64k trunk
-# dispatches crash rocprofv3 on the host, and so does --kernel-include-regex (SIGSEGV in the
-# profiler's launch hook at the first conv dispatch).
+# rocprofv3 HBM traffic of the tree kernels (k_select, k_expand_backup, the fused k_expand_select,
+# k_scan) and the record -> g8 input kernel (k_rec_to_g8) over one full C3 move (2048 games, 800
+# sims, BLOCKS residual blocks, default 20 = the bench config): a kernel-trace pass (bench.py's own
+# HIP-event timing on, so its JSON line carries the kernels' algorithmic bytes), then FETCH_SIZE and
+# WRITE_SIZE in separate passes with --kernel-timing 0: a search that records HIP events hangs under
+# counter collection (round 3, tools/pmc_hang_probe2.sh; the round-2 "800-sim hang").
+# --kernel-include-regex is not used (round 2: SIGSEGV in the profiler's launch hook).
 set -o pipefail
 export TMPDIR=/tmp
 O=gpurun_out/${TAG:-tree}
 mkdir -p $O
-CMD="python3 bench.py --cpu-baseline 0 --steps 1 --warmup 0 --sims ${SIMS:-800} --blocks ${BLOCKS:-2}"
+CMD="python3 bench.py --cpu-baseline 0 --parity-steps 0 --steps 1 --warmup 0 --sims ${SIMS:-800} --blocks ${BLOCKS:-20}"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o run -- $CMD > $O/trace.log 2>&1 || { echo FAIL trace; tail -3 $O/trace.log; exit 1; }
 ( while sleep 30; do echo "pmc pass running ($(date +%T))"; done ) &
 HB=$!
 trap "kill $HB 2>/dev/null" EXIT
-timeout -s KILL ${PMC_TIMEOUT:-240} rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/fetch -o run -- $CMD > $O/fetch.log 2>&1 || { echo FAIL fetch; tail -3 $O/fetch.log; exit 1; }
-timeout -s KILL ${PMC_TIMEOUT:-240} rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/write -o run -- $CMD > $O/write.log 2>&1 || { echo FAIL write; tail -3 $O/write.log; exit 1; }
+timeout -s KILL ${PMC_TIMEOUT:-240} rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/fetch -o run -- $CMD --kernel-timing 0 > $O/fetch.log 2>&1 || { echo FAIL fetch; tail -3 $O/fetch.log; exit 1; }
+timeout -s KILL ${PMC_TIMEOUT:-240} rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/write -o run -- $CMD --kernel-timing 0 > $O/write.log 2>&1 || { echo FAIL write; tail -3 $O/write.log; exit 1; }
 kill $HB 2>/dev/null
-O=$O SIMS=${SIMS:-800} BLOCKS=${BLOCKS:-2} python3 - <<'PY'
+O=$O SIMS=${SIMS:-800} BLOCKS=${BLOCKS:-20} python3 - <<'PY'
 import collections, csv, glob, json, os, re
 O = os.environ["O"]
-K = ["k_select", "k_expand_backup", "k_scan", "k_rec_to_g8"]
+K = ["k_select", "k_expand_backup", "k_expand_select", "k_scan", "k_rec_to_g8"]
 def key(name):
     for k in K:
         if re.search(r"\b" + k + r"\b", name):
@@ -39,13 +40,23 @@ for f in glob.glob(f"{O}/trace/**/*kernel_stats.csv", recursive=True):
         k = key(r["Name"])
         if k:
             dur[k] = float(r["AverageNs"])
-out = {"workload": f"python3 bench.py --cpu-baseline 0 --steps 1 --warmup 0 --sims {os.environ['SIMS']} --blocks {os.environ['BLOCKS']} (C3 games: 2048, 15x15, 256-filter fp16 net cut to {os.environ['BLOCKS']} blocks; one full move)",
-       "note": "per dispatch: FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE (KiB -> bytes); average duration from the kernel-trace pass (all dispatches incl. the per-move root steps)"}
+out = {"workload": f"python3 bench.py --cpu-baseline 0 --parity-steps 0 --steps 1 --warmup 0 --sims {os.environ['SIMS']} --blocks {os.environ['BLOCKS']} (C3 games: 2048, 15x15, 256-filter fp16 net with {os.environ['BLOCKS']} blocks; one full move)",
+       "note": "per dispatch: FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE (KiB -> bytes), counter passes with --kernel-timing 0; average duration from the kernel-trace pass (all dispatches incl. the per-move root steps); algorithmic bytes: the bench line of the trace pass (kernel-counted, sampled steps)"}
+bl = [l for l in open(f"{O}/trace.log") if l.startswith('{"metric"')]
+if bl:
+    tk = json.loads(bl[-1]).get("tree_kernels", {})
+    alg = {k: tk[k]["bytes_per_launch"] for k in ("k_select", "k_expand_backup") if k in tk}
+    if len(alg) == 2:
+        alg["k_expand_select"] = alg["k_select"] + alg["k_expand_backup"]
+    out["algorithmic_bytes_per_launch"] = alg
 for k in K:
     if k in fe and k in wr and k in dur:
         rd, w = fe[k][0] * 1024 * 2, wr[k][0] * 1024
         out[k] = {"dispatches": fe[k][1], "avg_duration_us": dur[k] / 1e3, "hbm_read_bytes": rd, "hbm_write_bytes": w,
                   "hbm_GB_per_s": (rd + w) / dur[k], "frac_of_hbm_peak": (rd + w) / dur[k] / 8000.0}
+        a = out.get("algorithmic_bytes_per_launch", {}).get(k)
+        if a:
+            out[k]["traffic_over_algorithmic"] = (rd + w) / a
 json.dump(out, open(f"{O}/tree_pmc.json", "w"), indent=1)
 print(json.dumps(out, indent=1))
 PY
