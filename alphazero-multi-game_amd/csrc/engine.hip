@@ -606,8 +606,7 @@ int net_forward(az_net* n, const float* x0, int B, const int* nb, float* logits,
         sa.Wpc = n->pconv.W; sa.bpc = n->pconv.b; sa.Wvc = n->vconv.W; sa.bvc = n->vconv.b;
         sa.pp = n->pp; sa.vp = n->vp;
         sa.H = H; sa.blocks = d.blocks; sa.residual = d.residual; sa.HC = d.head_channels; sa.P = P;
-        static const int stamps = getenv("AZ_SM_STAMPS") ? atoi(getenv("AZ_SM_STAMPS")) : 0;   // diagnostic phase stamps
-        sa.stamps = stamps;
+        sa.stamps = az_smallnet_stamps_mode();   // diagnostic phase stamps (az_diag_set_smallnet_stamps)
         if (az_smallnet_launch(sa, B, st)) return az_fail(AZ_ERR_ARG, "smallnet: unsupported shape");
         if (e1) HIPCHK(hipEventRecord(e1, st));
         return net_heads_fc(n, B, nb, logits, value, st);

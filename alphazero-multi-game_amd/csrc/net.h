@@ -65,6 +65,7 @@ struct SmallNetArgs {
 bool az_smallnet_supported(int H, int C, int cin_pad, int pool, int head_channels);
 int az_smallnet_max_blocks();
 int az_smallnet_launch(const SmallNetArgs& a, int B, hipStream_t st);
+int az_smallnet_stamps_mode();        // az_diag_set_smallnet_stamps (0: off)
 
 void az_launch_gemm_f32(const GemmArgs& p, int act, bool res, hipStream_t st);
 void az_launch_gemm_f32_partials(const GemmArgs& p, hipStream_t st);

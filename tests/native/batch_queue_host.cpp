@@ -237,7 +237,7 @@ int main(int argc, char** argv) {
         nn::BatchQueueConfig cfg;
         cfg.batchSize = 4;
         cfg.timeoutMs = 2;
-        cfg.adaptiveBatchInterval = 1;
+        cfg.adaptiveBatchInterval = 0;              // adapt before every batch (timing-independent)
         cfg.maxAdaptiveBatchSize = 12;
         nn::BatchQueue q(&net, cfg);
         net.close_gate();

@@ -316,3 +316,32 @@ def test_gpu_trunk_kernel_name(engine, case):
     net = az_amd.HipNeuralNetwork(engine, az_amd.NetDesc(bs, ci, ch, blocks, A, 32, 8, 256, 1, 0, p, B))
     assert net.trunk_kernel() == want
     net.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("residual", [1, 0])
+@pytest.mark.parametrize("B", [256, 37])
+def test_gpu_smallnet_matches_round2_kernel(engine, residual, B):
+    """k_smallnet (round 3: offset-addressed fragments, 6-slot ring, layer pairs, med3 epilogue) runs
+    the round-2 kernel's arithmetic: the same MFMA sequence, residual stream and fp16 rounding, so
+    both kernels (and both wave shapes) give bitwise equal outputs on C2-shape nets."""
+    import az_amd
+    from az_amd import _lib
+    d = az_amd.NetDesc(15, 11, 64, 6, 225, 32, 8, 256, residual, 0, az_amd.AZ_PREC_FP16, 256)
+    net = az_amd.HipNeuralNetwork(engine, d)
+    net.init_random(77 + residual)
+    x = _rand_planes(B, 11, 15, 5 + B)
+    outs = {}
+    try:
+        for k, w in ((1, 8), (0, 8), (0, 4), (1, 4)):
+            _lib.lib().az_diag_set_smallnet_kernel(k)
+            _lib.lib().az_diag_set_smallnet_waves(w)
+            outs[(k, w)] = net.forward(x)
+    finally:
+        _lib.lib().az_diag_set_smallnet_kernel(0)
+        _lib.lib().az_diag_set_smallnet_waves(8)
+    ref_p, ref_v = outs[(1, 8)]
+    assert np.isfinite(ref_p).all() and np.abs(ref_p).max() > 0
+    for kw, (pl, v) in outs.items():
+        np.testing.assert_array_equal(pl, ref_p, err_msg=f"kernel {kw}")
+        np.testing.assert_array_equal(v, ref_v, err_msg=f"kernel {kw}")

@@ -29,6 +29,8 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--flags", default="", help="comma list of conv variant flag sets to A/B (alternating rounds)")
     ap.add_argument("--rounds", type=int, default=4)
+    ap.add_argument("--sm-kernels", default="", help="comma list of k_smallnet kernels to A/B (0 = current, 1 = round 2; "
+                                                     "optionally :4 / :8 waves, e.g. 0:8,0:4,1:8)")
     ap.add_argument("--game", default="gomoku15", choices=list(GAMES))
     a = ap.parse_args()
     bs, planes, actions = GAMES[a.game]
@@ -44,6 +46,27 @@ def main():
     net.init_random(1234)
     x = (np.random.default_rng(0).random((a.batch, planes, bs, bs)) < (0.05 if planes > 16 else 0.2)).astype(np.float32)
     net.forward(x)
+    if a.sm_kernels:
+        from az_amd import _lib
+        sets = a.sm_kernels.split(",")
+        res = {f: [] for f in sets}
+        flops = a.batch * 2 * 9 * a.channels * a.channels * bs * bs
+        for _ in range(a.rounds):
+            for f in sets:
+                k, _, w = f.partition(":")
+                _lib.lib().az_diag_set_smallnet_kernel(int(k))
+                _lib.lib().az_diag_set_smallnet_waves(int(w or 8))
+                net.forward(x)
+                net.profile(True)
+                for _ in range(a.iters):
+                    net.forward(x)
+                ms, launches, fw = net.profile_read()
+                res[f].append(ms / fw)
+        for f in sets:
+            v = np.array(res[f])
+            print(f"k_smallnet kernel {f}: {1e3 * np.median(v):.1f} us/forward (min {1e3 * v.min():.1f} max {1e3 * v.max():.1f}), "
+                  f"{2 * a.blocks * flops / np.median(v) / 1e9:.1f} TFLOP/s trunk")
+        return
     if a.flags:
         from az_amd import _lib
         sets = [int(f, 0) for f in a.flags.split(",")]

@@ -6,7 +6,6 @@ import sys
 
 import numpy as np
 
-os.environ.setdefault("AZ_SM_STAMPS", "1")
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "alphazero-multi-game_amd"))
 import az_amd  # noqa: E402
@@ -19,6 +18,9 @@ if os.environ.get("AZ_SM_WAVES"):      # measurement-only kernel variant (diag e
 if os.environ.get("AZ_CONV_FLAGS"):
     from az_amd import _lib as _l
     _l.lib().az_diag_set_conv_flags(int(os.environ["AZ_CONV_FLAGS"], 0))
+_lib.lib().az_diag_set_smallnet_stamps(int(os.environ.get("AZ_SM_STAMPS", "1")))
+if os.environ.get("AZ_SM_KERNEL"):
+    _lib.lib().az_diag_set_smallnet_kernel(int(os.environ["AZ_SM_KERNEL"]))
 eng = az_amd.Engine(0)
 net = az_amd.HipNeuralNetwork(eng, az_amd.NetDesc(15, 11, 64, blocks, 225, 32, 8, 256, 1, 0, az_amd.AZ_PREC_FP16, B))
 net.init_random(1)
