@@ -42,6 +42,7 @@ __global__ void k_leaf_moves(TreeDev t, int* moves, int* len);
 __global__ void k_prune(TreeDev t, Nodes dst, int* src_of, int thr_all, const int* thr_g, long long* pruned);
 __global__ void k_noise(TreeDev t, const float* noise, const uint8_t* mask, float eps);
 __global__ void k_new_games(TreeDev t, const int* games, const int* seed_ids, int n, uint32_t eval_seed);
+__global__ void k_init_slots(TreeDev t, Nodes other);
 __global__ void k_tt_clear(TreeDev t, const int* games, int n);
 __global__ void k_root_nchild(TreeDev t, int* out);
 __global__ void k_root_children(TreeDev t, int g, int* act, int* N, int* VL, float* W, float* P, int* n, int* rootinfo,
@@ -143,6 +144,7 @@ struct az_net {
     uint16_t* zero = nullptr;   // 256 zero bytes: glds source for the board edge
     // k_smallnet (64-filter fp16 nets): [2*blocks+1][9][64][64] fp16 trunk weights incl. the input conv, biases
     uint16_t* sm_W = nullptr;
+    uint16_t* sm_Wf = nullptr;                  // the same weights fragment-major (k_smallnet's register path)
     float* sm_b = nullptr;
     // DDW-RandWire trunk (az_net_create_randwire): d.blocks rand-wire blocks of 32 nodes
     bool rw = false;
@@ -161,6 +163,14 @@ struct az_net {
     long long prof_tick = 0, prof_sampled = 0;    // events on every prof_every()-th forward only
     std::mutex mu;
 };
+
+// diagnostic: the game whose k_select / k_expand_backup write phase stamps (tools/tree_stamps.py),
+// read at search creation; -1 off
+static int g_tree_stamp_game = -1;
+extern "C" int az_diag_set_tree_stamps(int game) {
+    g_tree_stamp_game = game;
+    return 0;
+}
 
 // Profiling events are recorded on one simulation step / forward in AZ_PROF_EVERY (default 16):
 // each hipEventRecord leaves a ~6 us gap on the queue, which at C2 (a ~140 us simulation step)
@@ -312,8 +322,23 @@ int net_load(az_net* n, const float* blob) {
         if (sm) sm_add(W, b, F);
     }
     if (sm) {
-        if (!n->sm_W) { DALLOC(n->sm_W, smw.size()); DALLOC(n->sm_b, smb.size()); }
+        if (!n->sm_W) { DALLOC(n->sm_W, smw.size()); DALLOC(n->sm_Wf, smw.size()); DALLOC(n->sm_b, smb.size()); }
         HIPCHK(hipMemcpy(n->sm_W, smw.data(), smw.size() * 2, hipMemcpyHostToDevice));
+        // fragment-major: [layer][tap][32-channel chunk kk][16-channel block J][lane][8] -- one MFMA
+        // A operand (rows 16 J + lane % 16, channels 32 kk + 8 (lane / 16) ..) is 1 KB contiguous
+        std::vector<uint16_t> smwf(smw.size());
+        const size_t nl = smw.size() / ((size_t)9 * F * F);
+        for (size_t l = 0; l < nl; ++l)
+            for (int t = 0; t < 9; ++t)
+                for (int kk = 0; kk < F / 32; ++kk)
+                    for (int J = 0; J < F / 16; ++J)
+                        for (int ln = 0; ln < 64; ++ln)
+                            for (int e = 0; e < 8; ++e) {
+                                const int nn = 16 * J + (ln & 15), c = 32 * kk + 8 * (ln >> 4) + e;
+                                smwf[((((l * 9 + t) * (F / 32) + kk) * (F / 16) + J) * 64 + ln) * 8 + e] =
+                                    smw[((l * 9 + t) * F + nn) * F + c];
+                            }
+        HIPCHK(hipMemcpy(n->sm_Wf, smwf.data(), smwf.size() * 2, hipMemcpyHostToDevice));
         HIPCHK(hipMemcpy(n->sm_b, smb.data(), smb.size() * 4, hipMemcpyHostToDevice));
     }
     if (int r = load_heads(n, pc)) return r;
@@ -602,7 +627,7 @@ int net_forward(az_net* n, const float* x0, int B, const int* nb, float* logits,
         if (lr) {
             if (lr->go) return az_fail(AZ_ERR_ARG, "smallnet: Gomoku leaf records only");
             sa.x0 = nullptr; sa.rec = lr->rec; sa.gidx = lr->gidx; sa.rec_n = lr->n;
-        } sa.W = n->sm_W; sa.bias = n->sm_b;
+        } sa.W = n->sm_W; sa.Wf = n->sm_Wf; sa.bias = n->sm_b;
         sa.Wpc = n->pconv.W; sa.bpc = n->pconv.b; sa.Wvc = n->vconv.W; sa.bvc = n->vconv.b;
         sa.pp = n->pp; sa.vp = n->vp;
         sa.H = H; sa.blocks = d.blocks; sa.residual = d.residual; sa.HC = d.head_channels; sa.P = P;
@@ -938,7 +963,7 @@ int search_step(az_search* s, int mode, bool pre = false, bool fuse_next = false
         bool identity = mode == MODE_SIM && s->d_id != nullptr;
         for (int g = 0; identity && g < G; ++g) identity = s->active[g] != 0;
         if (identity) {
-            tt.eval_slot = s->d_id; tt.eval_games = s->d_id; tt.n_eval = s->d_id + G;
+            tt.eval_slot = s->d_id; tt.eval_games = s->d_id; tt.n_eval = s->d_id + G; tt.eval_identity = 1;
         } else {
             hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, st, s->t);
         }
@@ -1394,7 +1419,7 @@ void az_net_destroy(az_net* n) {
     for (void* p : {(void*)n->x0, (void*)n->h0, (void*)n->h1, (void*)n->t, (void*)n->pool, (void*)n->pp, (void*)n->vp, (void*)n->hpv,
                     (void*)n->v1, (void*)n->ws, (void*)n->logits, (void*)n->value, (void*)n->soft, (void*)n->in_nchw, (void*)n->d_nb,
                     (void*)n->hh[0], (void*)n->hh[1], (void*)n->hl[0], (void*)n->hl[1], (void*)n->th, (void*)n->tl,
-                    (void*)n->zero, (void*)n->sm_W, (void*)n->sm_b})
+                    (void*)n->zero, (void*)n->sm_W, (void*)n->sm_Wf, (void*)n->sm_b})
         F(p);
     delete n;
 }
@@ -1587,6 +1612,8 @@ int az_search_create(az_engine* e, az_net* net, const az_search_cfg* c, az_searc
     auto* s = new az_search();
     s->e = e; s->net = net; s->c = *c;
     const int ncap = c->node_capacity > 0 ? c->node_capacity : 3 * std::max(64, c->num_simulations) * NA + 8 * NA + 64;
+    if (c->prior_ring > 0 && c->prior_ring < NA)
+        return az_fail(AZ_ERR_ARG, "prior_ring %d is smaller than one policy (%d entries)", c->prior_ring, NA);
     const int ring = c->prior_ring > 0 ? c->prior_ring : std::max(1 << 16, 12 * std::max(64, c->num_simulations) * NA);
     s->c.node_capacity = ncap; s->c.prior_ring = ring;
     TreeDev& t = s->t;
@@ -1594,7 +1621,7 @@ int az_search_create(az_engine* e, az_net* net, const az_search_cfg* c, az_searc
     t.hmax = go ? 2048 : 0; t.vl = c->virtual_loss; t.cpuct = c->c_puct; t.fpu = c->fpu_reduction;
     t.eval_kind = c->eval_kind; t.tt_slots = 1 << c->tt_log2; t.tt_mask = (uint64_t)t.tt_slots - 1; t.ring = ring;
     t.log_game = -1; t.log_cap = 0;
-    t.stamp_game = getenv("AZ_TREE_STAMPS") ? atoi(getenv("AZ_TREE_STAMPS")) : -1;   // diagnostic phase stamps
+    t.stamp_game = g_tree_stamp_game;   // diagnostic phase stamps (az_diag_set_tree_stamps)
     const size_t NG = (size_t)G * ncap;
     int r = 0;
 #define SA(p, n) do { if (!r) r = dalloc(&(p), (size_t)(n)); } while (0)
@@ -1607,7 +1634,7 @@ int az_search_create(az_engine* e, az_net* net, const az_search_cfg* c, az_searc
     SA(t.rhash, G); SA(t.rfresh, G); SA(t.rnode, G); SA(t.active, G); SA(t.gresult, G);
     uint64_t* zko = nullptr;
     if (go) { SA(t.rko, G); SA(t.rpass, G); SA(t.rposh, (size_t)G * t.hmax); SA(t.rnposh, G); SA(zko, A + 1); }
-    SA(t.path, (size_t)G * AZ_DMAX); SA(t.pact, (size_t)G * AZ_DMAX); SA(t.plen, G); SA(t.lstatus, G); SA(t.lvalue, G); SA(t.lhash, G); SA(t.ttstore, G);
+    SA(t.path, (size_t)G * AZ_DMAX); SA(t.pact, (size_t)G * AZ_DMAX); SA(t.pstat, (size_t)G * AZ_DMAX); SA(t.plen, G); SA(t.lstatus, G); SA(t.lvalue, G); SA(t.lhash, G); SA(t.ttstore, G);
     SA(t.ttref, G); SA(t.tthslot, G); SA(t.need_eval, G); SA(t.eval_slot, G); SA(t.eval_games, G); SA(t.n_eval, 1);
     SA(t.leafrec, (size_t)G * AZ_REC_BYTES);
     SA(t.tt_hash, (size_t)G * t.tt_slots); SA(t.tt_visits, (size_t)G * t.tt_slots); SA(t.tt_value, (size_t)G * t.tt_slots);
@@ -1666,7 +1693,11 @@ int az_search_create(az_engine* e, az_net* net, const az_search_cfg* c, az_searc
         HIPCHK(hipMemcpy(fo, order.data(), A * 4, hipMemcpyHostToDevice));
     }
     HIPCHK(hipMemset(t.err, 0, 4));
-    HIPCHK(hipMemset(t.active, 0, G * 4));
+    // every slot an idle game with a valid root until k_new_games starts it
+    t.nd = s->arena[0];
+    hipLaunchKernelGGL(k_init_slots, dim3((G + 255) / 256), dim3(256), 0, e->stream, t, s->arena[1]);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(e->stream));
     s->stones.assign(G, 0); s->active.assign(G, 0); s->fresh.assign(G, 1); s->ply.assign(G, 0); s->expanded.assign(G, 0);
     s->rng.resize(G);
     s->hist.assign(G, {});
@@ -1686,6 +1717,7 @@ void az_search_destroy(az_search* s) {
     for (const void* p : {(const void*)t.atop, (const void*)t.rboard, (const void*)t.rhist, (const void*)t.rplayer,
                           (const void*)t.rstones, (const void*)t.rply, (const void*)t.rhash, (const void*)t.rfresh,
                           (const void*)t.rnode, (const void*)t.active, (const void*)t.gresult, (const void*)t.path, (const void*)t.pact,
+                          (const void*)t.pstat,
                           (const void*)t.plen, (const void*)t.lstatus, (const void*)t.lvalue, (const void*)t.lhash,
                           (const void*)t.ttstore, (const void*)t.ttref, (const void*)t.tthslot, (const void*)t.need_eval,
                           (const void*)t.eval_slot, (const void*)t.eval_games, (const void*)t.n_eval, (const void*)t.leafrec,

@@ -55,6 +55,7 @@ struct SmallNetArgs {
     int rec_n;                      // with rec: records (games); gidx entries are clamped to it
     const int* m_limit;             // device: active boards
     const uint16_t* W;              // [2*blocks+1][9][64 n][64 c] fp16, BN folded; layer 0 = input conv (c >= planes zero)
+    const uint16_t* Wf;             // the same, fragment-major [layer][tap][kk][J][64 lanes][8] (engine.hip)
     const float* bias;              // [2*blocks+1][64]
     const float* Wpc; const float* bpc;   // policy 1x1 conv [HC][64], [HC] (BN folded)
     const float* Wvc; const float* bvc;   // value 1x1 conv

@@ -103,7 +103,8 @@ __device__ __forceinline__ void certify_frags(F (&a)[JA], F (&b)[JB]) {
 }  // namespace
 
 // measurement only (tools/sm_check.sh, tools/net_bench.py): 4 = one wave per SIMD instead of the
-// default 8-wave block; kernel 1 = the round-2 kernel (k_smallnet_r2, A/B against k_smallnet)
+// default 8-wave block.  Kernel 0 (default) = k_smallnet_g (weights streamed into registers), 1 = the
+// round-2 kernel (k_smallnet_r2), 2 = k_smallnet (weights through the LDS ring); A/B only
 static int g_sm_waves = 8;
 static int g_sm_kernel = 0;
 static int g_sm_stamp_mode = 0;
@@ -119,7 +120,7 @@ extern "C" int az_diag_set_smallnet_waves(int nw) {
     return 0;
 }
 extern "C" int az_diag_set_smallnet_kernel(int k) {
-    g_sm_kernel = k == 1 ? 1 : 0;
+    g_sm_kernel = k == 1 || k == 2 ? k : 0;
     return 0;
 }
 
@@ -465,7 +466,7 @@ namespace {
 // chunk minor), fp32 residual stream in registers, fp16 activations rounded to nearest even.
 constexpr int RS = 160;          // activation row stride, bytes (64 fp16 channels + 32 B pad)
 
-template <int HB, int NW>
+template <int HB, int NW, int BAR = 1>
 struct Sm2 {
     static constexpr int WG = HB + 2, HW = HB * HB, GRID = HB * WG;
     static constexpr int NFRAG = (GRID + 15) / 16;       // 16-row pixel fragments (wave wp: wp + 4 i)
@@ -475,7 +476,11 @@ struct Sm2 {
     static constexpr int IR = NFRAG * 16 + 2 * WG + 2;   // halo rows the last fragment's taps read
     static constexpr int IMG = IR * RS;
     static constexpr int WT = SF * SF * 2;               // one tap's weight tile [64 n][64 c] fp16
-    static constexpr int NSLOT = 6, DIST = 5;
+    // ring: tile s + DIST lands in the slot of tile s + DIST - NSLOT, which every wave has consumed
+    // once waves are at most BAR taps apart (one barrier per BAR taps); each barrier certifies the
+    // tiles the next BAR taps read (one tap ahead), leaving DIST - BAR - 1 tiles in flight
+    static constexpr int NSLOT = 6, DIST = NSLOT - BAR, INFLIGHT = DIST - BAR - 1;
+    static_assert(INFLIGHT >= 0, "ring too small for BAR taps per barrier");
     static constexpr int WPT = 512 / NT;                 // 16-B DMA pieces per thread per tile
     static constexpr int MAXL = 32;                      // bias rows (L <= 31: the epilogue reads row L)
     static constexpr int OX = 0, OY = IMG, OW = 2 * IMG, OB = OW + NSLOT * WT;
@@ -509,11 +514,47 @@ __device__ __forceinline__ uint32_t pack_f16(float a, float b) {
 template <int V> using IC = std::integral_constant<int, V>;
 enum { ROLE_IN = 0, ROLE_ODD = 1, ROLE_EVEN = 2 };
 
+// adaptive average pool of the fp32 stream xs ([HW][64], xs_off layout) to P x P cells (torch
+// adaptive_avg_pool2d bins, y-major sums from 0, / count): item i = (c4 = i / PP, cell = i % PP), so
+// consecutive lanes write consecutive cells of pooled [64 c][64 cells].  PC = P at compile time (the
+// bins become constants) or 0 (runtime P); bins of at most 3 x 3 issue every load before the sums.
+template <int HB, int PC, int NT>
+__device__ __forceinline__ void pool_cells(const uint8_t* xs, float* pooled, int tid, int Prt = 0) {
+    const int P = PC ? PC : Prt, PP = P * P;
+    for (int i = tid; i < PP * (SF / 4); i += NT) {
+        const int c4 = i / PP, cell = i - c4 * PP, oy = cell / P, ox = cell - oy * P;
+        const int y0 = (oy * HB) / P, y1 = ((oy + 1) * HB + P - 1) / P;
+        const int xa = (ox * HB) / P, xb = ((ox + 1) * HB + P - 1) / P;
+        f32x4v sum = {0.0f, 0.0f, 0.0f, 0.0f};
+        if (y1 - y0 <= 3 && xb - xa <= 3) {
+            f32x4v v[3][3];
+#pragma unroll
+            for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+                for (int dx = 0; dx < 3; ++dx) {
+                    const int y = min(y0 + dy, HB - 1), x = min(xa + dx, HB - 1);
+                    v[dy][dx] = *reinterpret_cast<const f32x4v*>(xs + xs_off(y * HB + x, c4));
+                }
+#pragma unroll
+            for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+                for (int dx = 0; dx < 3; ++dx)
+                    if (y0 + dy < y1 && xa + dx < xb) sum += v[dy][dx];
+        } else {
+            for (int y = y0; y < y1; ++y)
+                for (int x = xa; x < xb; ++x) sum += *reinterpret_cast<const f32x4v*>(xs + xs_off(y * HB + x, c4));
+        }
+        const float cnt = (float)((y1 - y0) * (xb - xa));
+#pragma unroll
+        for (int e = 0; e < 4; ++e) pooled[(4 * c4 + e) * 64 + cell] = sum[e] / cnt;
+    }
+}
+
 }  // namespace
 
-template <int HB, int NW, bool RES>
+template <int HB, int NW, bool RES, int BAR = 1>
 __global__ __launch_bounds__(64 * NW, 1) void k_smallnet(SmallNetArgs p) {
-    typedef Sm2<HB, NW> G;
+    typedef Sm2<HB, NW, BAR> G;
     constexpr int NT = G::NT, WG = G::WG, HW = G::HW, FPW = G::FPW, JN = G::JN, WPT = G::WPT;
     constexpr int NSLOT = G::NSLOT, DIST = G::DIST, WT = G::WT;
     __shared__ __attribute__((aligned(16))) uint8_t lds[G::LDS];
@@ -546,11 +587,11 @@ __global__ __launch_bounds__(64 * NW, 1) void k_smallnet(SmallNetArgs p) {
 
     // global loads the prologue consumes (head 1x1 weights, biases), issued before the weight DMA
     // so the compiler's waits for them do not drain it
-    constexpr int HWT = SF * SF / NT;
+    constexpr int HWT = SF * SF / NT;                    // element (c, o) = tid + NT k, o fastest
     float wpre[HWT];
 #pragma unroll
     for (int k = 0; k < HWT; ++k) {
-        const int i = tid + NT * k, o = i / SF, c = i - o * SF;
+        const int i = tid + NT * k, c = i / SF, o = i - c * SF;
         wpre[k] = o < p.HC ? p.Wpc[o * SF + c] : p.Wvc[(o - p.HC) * SF + c];
     }
     constexpr int BPT = (G::MAXL * SF + NT - 1) / NT;
@@ -622,8 +663,8 @@ __global__ __launch_bounds__(64 * NW, 1) void k_smallnet(SmallNetArgs p) {
             if (i < L * SF) bsm[i] = bpre[k];
         }
     }
-    // tiles 0 and 1 landed (2..DIST-1 stay in flight), every prologue store done
-    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"i"((DIST - 2) * WPT) : "memory");
+    // the tiles the first BAR taps read landed (INFLIGHT stay in flight), every prologue store done
+    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"i"(G::INFLIGHT * WPT) : "memory");
     sm_stamp(p, 1);
 
     // per-lane bases: activation fragment reads, epilogue writes, weight fragment reads, biases
@@ -709,9 +750,9 @@ __global__ __launch_bounds__(64 * NW, 1) void k_smallnet(SmallNetArgs p) {
                     });
                     read_bias(layer + 1);                // row L (past the last layer) is never used
                     if (layer == 5) sm_stamp(p, 53);
-                    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"i"((DIST - 2) * WPT) : "memory");
-                } else {
-                    asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"i"((DIST - 2) * WPT) : "memory");
+                    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"i"(G::INFLIGHT * WPT) : "memory");
+                } else if constexpr ((t + 1) % BAR == 0) {
+                    asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"i"(G::INFLIGHT * WPT) : "memory");
                 }
             }
         });
@@ -745,44 +786,15 @@ __global__ __launch_bounds__(64 * NW, 1) void k_smallnet(SmallNetArgs p) {
     float* pooled = reinterpret_cast<float*>(lds + G::OW);   // [64 c][64 cells] (cells >= PP zero)
     float* wt = pooled + SF * 64;                        // [64 c][HO o] (policy outputs, then value)
 #pragma unroll
-    for (int k = 0; k < HWT; ++k) {
-        const int i = tid + NT * k, o = i / SF, c = i - o * SF;
-        wt[c * HO + o] = wpre[k];
-    }
+    for (int k = 0; k < HWT; ++k) wt[tid + NT * k] = wpre[k];   // [c][o]: consecutive lanes, consecutive o
     for (int i = tid; i < SF * (64 - PP); i += NT) {
         const int c = i / (64 - PP), cell = PP + (i - c * (64 - PP));
         pooled[c * 64 + cell] = 0.0f;
     }
     __syncthreads();
     sm_stamp(p, 40);
-    for (int i = tid; i < PP * (SF / 4); i += NT) {
-        const int cell = i / (SF / 4), c4 = i - cell * (SF / 4), oy = cell / P, ox = cell - oy * P;
-        const int y0 = (oy * HB) / P, y1 = ((oy + 1) * HB + P - 1) / P;
-        const int xa = (ox * HB) / P, xb = ((ox + 1) * HB + P - 1) / P;
-        f32x4v sum = {0.0f, 0.0f, 0.0f, 0.0f};
-        if (y1 - y0 <= 3 && xb - xa <= 3) {
-            // bins of at most 3 x 3 (P >= HB / 2): every load in flight before the sums
-            f32x4v v[3][3];
-#pragma unroll
-            for (int dy = 0; dy < 3; ++dy)
-#pragma unroll
-                for (int dx = 0; dx < 3; ++dx) {
-                    const int y = min(y0 + dy, HB - 1), x = min(xa + dx, HB - 1);
-                    v[dy][dx] = *reinterpret_cast<const f32x4v*>(xs + xs_off(y * HB + x, c4));
-                }
-#pragma unroll
-            for (int dy = 0; dy < 3; ++dy)
-#pragma unroll
-                for (int dx = 0; dx < 3; ++dx)
-                    if (y0 + dy < y1 && xa + dx < xb) sum += v[dy][dx];
-        } else {
-            for (int y = y0; y < y1; ++y)
-                for (int x = xa; x < xb; ++x) sum += *reinterpret_cast<const f32x4v*>(xs + xs_off(y * HB + x, c4));
-        }
-        const float cnt = (float)((y1 - y0) * (xb - xa));
-#pragma unroll
-        for (int e = 0; e < 4; ++e) pooled[(4 * c4 + e) * 64 + cell] = sum[e] / cnt;
-    }
+    if (P == 8) pool_cells<HB, 8, NT>(xs, pooled, tid);
+    else pool_cells<HB, 0, NT>(xs, pooled, tid, P);
     __syncthreads();
     sm_stamp(p, 41);
     // head 1x1 convs on the f32 MFMA (v_mfma_f32_16x16x4_f32: an exact k-ordered fmaf chain, as
@@ -802,6 +814,280 @@ __global__ __launch_bounds__(64 * NW, 1) void k_smallnet(SmallNetArgs p) {
 #pragma unroll
             for (int j = 0; j < JN; ++j) {
                 const int o = 16 * (J0 + j) + 4 * lg;   // 4 consecutive outputs, all policy or all value
+                const bool pol = o < HC;
+                const int oc = pol ? o : o - HC;
+                const float* bias = (pol ? p.bpc : p.bvc) + oc;
+                f32x4v v;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const float t = hacc[j][e] + bias[e];
+                    v[e] = t > 0.0f ? t : 0.0f;
+                }
+                *reinterpret_cast<f32x4v*>((pol ? p.pp : p.vp) + ((size_t)b * PP + cell) * HC + oc) = v;
+            }
+        }
+    }
+    sm_stamp(p, 42);
+}
+
+namespace {
+// k_smallnet_g: k_smallnet with the weights streamed from L1 / L2 straight into registers instead of
+// through an LDS ring.  Per 32-channel step a wave loads its JN weight fragments (1 KB each,
+// fragment-major Wf: one coalesced global_load_dwordx4 per lane) PW = 6 steps ahead into a 6-deep
+// register ring whose slot is the step's global index mod 6 (compile-time: layer 0 has 9 steps, a
+// trunk layer 18, so every trunk layer starts at slot 3).  The LDS then carries only activation
+// fragments (4 ds_read_b128 per step instead of 6, and no 8 KB tile DMA per tap), and a layer has
+// one barrier, at its end.  Waves of a pixel group share their weight fragments through the CU's
+// L1.  Arithmetic identical to k_smallnet (same MFMA order, epilogue).
+template <int HB, int NW>
+struct SmG {
+    typedef Sm2<HB, NW> B;
+    static constexpr int PW = 6;                         // weight prefetch distance = ring depth (steps)
+    static constexpr int OX = 0, OY = B::IMG, OB = 2 * B::IMG;
+    static constexpr int OS = OB;                        // pool / head staging (after the trunk, over the biases)
+    static constexpr int LDS = OB + 2 * SF * SF * 4 > OB + B::MAXL * SF * 4 ? OB + 2 * SF * SF * 4 : OB + B::MAXL * SF * 4;
+    static_assert(LDS <= 160 * 1024, "");
+    static_assert(9 % 3 == 0 && 18 % PW == 0 && 9 % PW == 3, "trunk layers start at ring slot 3");
+};
+
+}  // namespace
+
+template <int HB, int NW, bool RES>
+__global__ __launch_bounds__(64 * NW, 1) void k_smallnet_g(SmallNetArgs p) {
+    typedef Sm2<HB, NW> G;
+    typedef SmG<HB, NW> H;
+    constexpr int NT = G::NT, WG = G::WG, HW = G::HW, FPW = G::FPW, JN = G::JN, PW = H::PW;
+    __shared__ __attribute__((aligned(16))) uint8_t lds[H::LDS];
+    const uint32_t L0 = (uint32_t)(uintptr_t)lds;
+    const int b = blockIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int gq = tid, gy = gq / WG, gx = gq - gy * WG;
+    const bool glive = gq < G::NFRAG * 16 && gy < HB && gx < HB;
+    int rv = 0;
+    int meta[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (p.rec) {
+        const int gi = min(max(p.gidx[b], 0), p.rec_n - 1);
+        const uint8_t* rec = p.rec + (size_t)gi * AZ_REC_BYTES;
+        rv = glive ? rec[gy * HB + gx] : 0;
+        const int4 m0 = *reinterpret_cast<const int4*>(rec + AZ_REC_META);
+        const int4 m1 = *reinterpret_cast<const int4*>(rec + AZ_REC_META + 16);
+        meta[0] = m0.x; meta[1] = m0.y; meta[2] = m0.z; meta[3] = m0.w;
+        meta[4] = m1.x; meta[5] = m1.y; meta[6] = m1.z; meta[7] = m1.w;
+    }
+    if (p.m_limit && b >= *p.m_limit) return;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wp = wave & 3;
+    const int J0 = (wave >> 2) * JN;
+    const int l16 = lane & 15, lg = lane >> 4;
+    const int L = 2 * p.blocks + 1;
+    const int NFR = L * 18;                              // weight fragment groups (layer, tap, kk)
+    sm_stamp(p, 0);
+
+    constexpr int HWT = SF * SF / NT;
+    float wpre[HWT];
+#pragma unroll
+    for (int k = 0; k < HWT; ++k) {
+        const int i = tid + NT * k, c = i / SF, o = i - c * SF;
+        wpre[k] = o < p.HC ? p.Wpc[o * SF + c] : p.Wvc[(o - p.HC) * SF + c];
+    }
+    constexpr int BPT = (G::MAXL * SF + NT - 1) / NT;
+    float bpre[BPT];
+#pragma unroll
+    for (int k = 0; k < BPT; ++k) {
+        const int i = tid + NT * k;
+        bpre[k] = i < L * SF ? p.bias[i] : 0.0f;
+    }
+    // weight register ring: fw[slot][j] = fragment group fg's block J0 + j
+    f16x8 fw[PW][JN];
+    const f16x8* wsrc = reinterpret_cast<const f16x8*>(p.Wf) + J0 * 64 + lane;
+    auto wload = [&](auto slotc, int fg) {
+        constexpr int slot = decltype(slotc)::value;
+        const f16x8* src = wsrc + (size_t)min(fg, NFR - 1) * (4 * 64);
+        static_for<0, JN>([&](auto jc) { fw[slot][decltype(jc)::value] = src[64 * decltype(jc)::value]; });
+    };
+    // layer 0 reads chunk kk = 0 of each tap: fragment group 2 t
+    static_for<0, PW>([&](auto xc) { wload(xc, 2 * decltype(xc)::value); });
+
+    {
+        constexpr int TOP = WG + 1, BOT0 = G::NFRAG * 16 + WG + 1, NPAD = TOP + (G::IR - BOT0);
+        for (int i = tid; i < 2 * NPAD * 8; i += NT) {
+            const int img = i / (NPAD * 8), k = i - img * NPAD * 8, r = k >> 3, c = k & 7;
+            const int row = r < TOP ? r : BOT0 + (r - TOP);
+            *reinterpret_cast<uint4*>(lds + (img ? H::OY : H::OX) + row * RS + c * 16) = uint4{0, 0, 0, 0};
+        }
+        if (tid < G::NFRAG * 16) {
+            float c[16];
+#pragma unroll
+            for (int k = 0; k < 16; ++k) c[k] = 0.0f;
+            if (glive) {
+                const int px = gy * HB + gx;
+                if (p.rec) {
+                    az_leaf_planes_v(rv, 0, meta, 0, HB, px, c);
+                } else {
+                    const float* x0 = p.x0 + ((size_t)b * HW + px) * 16;
+#pragma unroll
+                    for (int k = 0; k < 16; k += 4) {
+                        const float4 u = *reinterpret_cast<const float4*>(x0 + k);
+                        c[k] = u.x; c[k + 1] = u.y; c[k + 2] = u.z; c[k + 3] = u.w;
+                    }
+                }
+            }
+            uint8_t* dst = lds + H::OY + (gq + WG + 1) * RS;
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const uint4 v = {pack_f16(c[8 * h], c[8 * h + 1]), pack_f16(c[8 * h + 2], c[8 * h + 3]),
+                                 pack_f16(c[8 * h + 4], c[8 * h + 5]), pack_f16(c[8 * h + 6], c[8 * h + 7])};
+                *reinterpret_cast<uint4*>(dst + 16 * h) = v;
+                *reinterpret_cast<uint4*>(dst + 32 + 16 * h) = uint4{0, 0, 0, 0};
+            }
+        }
+        float* bsm = reinterpret_cast<float*>(lds + H::OB);
+#pragma unroll
+        for (int k = 0; k < BPT; ++k) {
+            const int i = tid + NT * k;
+            if (i < L * SF) bsm[i] = bpre[k];
+        }
+    }
+    __syncthreads();
+    sm_stamp(p, 1);
+
+    const uint32_t aX = L0 + H::OX + (16 * wp + l16) * RS + 16 * lg, aY = aX + H::OY;
+    const uint32_t eX = L0 + H::OX + (16 * wp + l16 + WG + 1) * RS + 32 * J0 + 8 * lg, eY = eX + H::OY;
+    const uint32_t bb = L0 + H::OB + (16 * J0 + 4 * lg) * 4;
+    float mlive[FPW];
+#pragma unroll
+    for (int i = 0; i < FPW; ++i) {
+        const int q = 16 * (wp + 4 * i) + l16, y = q / WG, x = q - y * WG;
+        mlive[i] = (y < HB && x < HB) ? __builtin_inff() : 0.0f;
+    }
+
+    f32x4v acc[FPW][JN];
+    f32x4v xr[FPW][JN];
+    f32x4v bn[JN];
+    f16x8 fb[3][FPW];                                    // activation fragments (reads PF steps ahead)
+    auto read_bias = [&](int layer) {
+        const uint32_t a = bb + layer * (SF * 4);
+        static_for<0, JN>([&](auto jc) { ds_rd<64 * decltype(jc)::value>(bn[decltype(jc)::value], a); });
+    };
+    read_bias(0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+
+    // ROLE, NCH chunks per tap, R0 = ring slot of the layer's step 0 (0 for layer 0, 3 otherwise);
+    // NNCH = chunks per tap of the next layer (its fragment groups are prefetched here)
+    auto run_layer = [&](int layer, auto rolec, auto nchc, auto r0c) {
+        constexpr int ROLE = decltype(rolec)::value, NCH = decltype(nchc)::value, R0 = decltype(r0c)::value;
+        constexpr int NSTEP = 9 * NCH, PF = NCH == 1 ? 1 : 2, NB = PF + 1;
+        const uint32_t src = ROLE == ROLE_ODD ? aX : aY;
+        const uint32_t dst = ROLE == ROLE_ODD ? eY : eX;
+        const int fg0 = layer * 18;                      // this layer's first fragment group
+        static_for<0, FPW>([&](auto ic) {
+            static_for<0, JN>([&](auto jc) { acc[decltype(ic)::value][decltype(jc)::value] = bn[decltype(jc)::value]; });
+        });
+        auto aload = [&](auto bufc, auto xc) {
+            constexpr int buf = decltype(bufc)::value, x = decltype(xc)::value;
+            constexpr int t = x / NCH, kk = x % NCH, sh = (t / 3) * WG + (t % 3);
+            static_for<0, FPW>([&](auto ic) {
+                constexpr int i = decltype(ic)::value;
+                ds_rd<64 * RS * i + RS * sh + 64 * kk>(fb[buf][i], src);
+            });
+        };
+        static_for<0, PF>([&](auto xc) { aload(IC<decltype(xc)::value % NB>{}, xc); });
+        static_for<0, NSTEP>([&](auto qc) {
+            constexpr int q = decltype(qc)::value, t = q / NCH, kk = q % NCH, r = q % NB, ws = (R0 + q) % PW;
+            if constexpr (q + PF < NSTEP) aload(IC<(q + PF) % NB>{}, IC<q + PF>{});
+            constexpr int ahead = (NSTEP - 1 - q) < PF ? (NSTEP - 1 - q) : PF;
+            certify_frags<(ahead * FPW > 15 ? 15 : ahead * FPW)>(fw[ws], fb[r]);
+            __builtin_amdgcn_sched_barrier(0);
+            static_for<0, FPW>([&](auto ic) {
+                static_for<0, JN>([&](auto jc) {
+                    constexpr int i = decltype(ic)::value, j = decltype(jc)::value;
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fw[ws][j], fb[r][i], acc[i][j], 0, 0, 0);
+                });
+            });
+            __builtin_amdgcn_sched_barrier(0);
+            // the ring slot just consumed takes the fragment group PW steps ahead (possibly the next
+            // layer's: 2 chunks per tap from layer 1 on)
+            {
+                constexpr int ahead_step = q + PW;
+                if constexpr (ahead_step < NSTEP) {
+                    wload(IC<ws>{}, fg0 + (ahead_step / NCH) * 2 + ahead_step % NCH);
+                } else {
+                    wload(IC<ws>{}, fg0 + 18 + (ahead_step - NSTEP));   // next layer: 2 chunks per tap
+                }
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            if constexpr (kk == NCH - 1) {
+                if (layer == 5) sm_stamp(p, 43 + t);
+                if constexpr (t == 8) {
+                    static_for<0, FPW>([&](auto ic) {
+                        static_for<0, JN>([&](auto jc) {
+                            constexpr int i = decltype(ic)::value, j = decltype(jc)::value;
+                            f32x4v v = acc[i][j];
+                            if constexpr (ROLE == ROLE_EVEN && RES) v += xr[i][j];
+#pragma unroll
+                            for (int e = 0; e < 4; ++e) v[e] = __builtin_amdgcn_fmed3f(v[e], 0.0f, mlive[i]);
+                            if constexpr (ROLE != ROLE_ODD) xr[i][j] = v;
+                            ds_wr64<64 * RS * i + 32 * j>(dst, pack_f16(v[0], v[1]), pack_f16(v[2], v[3]));
+                        });
+                    });
+                    read_bias(layer + 1);
+                    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+                }
+            }
+        });
+    };
+    run_layer(0, IC<ROLE_IN>{}, IC<1>{}, IC<0>{});
+    sm_stamp(p, 2);
+    for (int layer = 1; layer < L; layer += 2) {
+        run_layer(layer, IC<ROLE_ODD>{}, IC<2>{}, IC<3>{});
+        sm_stamp(p, 2 + layer);
+        run_layer(layer + 1, IC<ROLE_EVEN>{}, IC<2>{}, IC<3>{});
+        sm_stamp(p, 3 + layer);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // the ring's trailing (clamped) loads
+    __syncthreads();
+
+    uint8_t* xs = lds;
+    static_for<0, FPW>([&](auto ic) {
+        constexpr int i = decltype(ic)::value;
+        const int q = 16 * (wp + 4 * i) + l16, y = q / WG, x = q - y * WG;
+        if (y < HB && x < HB)
+            static_for<0, JN>([&](auto jc) {
+                constexpr int j = decltype(jc)::value;
+                *reinterpret_cast<f32x4v*>(xs + xs_off(y * HB + x, (16 * (J0 + j) + 4 * lg) >> 2)) = xr[i][j];
+            });
+    });
+    const int P = p.P, PP = P * P, HC = p.HC;
+    constexpr int HO = SF;
+    float* pooled = reinterpret_cast<float*>(lds + H::OS);
+    float* wt = pooled + SF * 64;
+#pragma unroll
+    for (int k = 0; k < HWT; ++k) wt[tid + NT * k] = wpre[k];
+    for (int i = tid; i < SF * (64 - PP); i += NT) {
+        const int c = i / (64 - PP), cell = PP + (i - c * (64 - PP));
+        pooled[c * 64 + cell] = 0.0f;
+    }
+    __syncthreads();
+    sm_stamp(p, 40);
+    if (P == 8) pool_cells<HB, 8, NT>(xs, pooled, tid);
+    else pool_cells<HB, 0, NT>(xs, pooled, tid, P);
+    __syncthreads();
+    sm_stamp(p, 41);
+    {
+        const int cell = 16 * wp + l16;
+        f32x4v hacc[JN] = {};
+#pragma unroll 4
+        for (int kb = 0; kb < SF / 4; ++kb) {
+            const int c = 4 * kb + lg;
+            const float bv = pooled[c * 64 + cell];
+#pragma unroll
+            for (int j = 0; j < JN; ++j)
+                hacc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(wt[c * HO + 16 * (J0 + j) + l16], bv, hacc[j], 0, 0, 0);
+        }
+        if (cell < PP) {
+#pragma unroll
+            for (int j = 0; j < JN; ++j) {
+                const int o = 16 * (J0 + j) + 4 * lg;
                 const bool pol = o < HC;
                 const int oc = pol ? o : o - HC;
                 const float* bias = (pol ? p.bpc : p.bvc) + oc;
@@ -841,6 +1127,11 @@ int az_smallnet_launch(const SmallNetArgs& a, int B, hipStream_t st) {
     if (g_sm_kernel == 1) {
         if (g_sm_waves == 4) hipLaunchKernelGGL((k_smallnet_r2<15, 0, 4>), dim3(B), dim3(256), 0, st, a);
         else hipLaunchKernelGGL((k_smallnet_r2<15, 0, 8>), dim3(B), dim3(512), 0, st, a);
+        return 0;
+    }
+    if (g_sm_kernel == 0) {                              // default: weights streamed into registers
+        if (a.residual) hipLaunchKernelGGL((k_smallnet_g<15, 8, true>), dim3(B), dim3(512), 0, st, a);
+        else hipLaunchKernelGGL((k_smallnet_g<15, 8, false>), dim3(B), dim3(512), 0, st, a);
         return 0;
     }
     if (g_sm_waves == 4) {

@@ -40,19 +40,81 @@ __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
 __device__ __forceinline__ float seq_sum_lds(const float* x, int n) {
     float s = 0.0f;
     const float4* q = reinterpret_cast<const float4*>(x);
-    for (int j = 0; j < (n + 15) / 16; ++j) {
-        const float4 a = q[4 * j], b = q[4 * j + 1], c = q[4 * j + 2], d = q[4 * j + 3];
+    const int nq = (n + 15) / 16;
+    if (nq <= 0) return s;
+    // the next 16 values are read while the current 16 are added (the add chain, not the LDS
+    // latency, is then the critical path)
+    float4 a = q[0], b = q[1], c = q[2], d = q[3];
+    for (int j = 0; j < nq; ++j) {
+        float4 na = a, nb = b, nc = c, nd = d;
+        if (j + 1 < nq) { na = q[4 * j + 4]; nb = q[4 * j + 5]; nc = q[4 * j + 6]; nd = q[4 * j + 7]; }
         s += a.x; s += a.y; s += a.z; s += a.w;
         s += b.x; s += b.y; s += b.z; s += b.w;
         s += c.x; s += c.y; s += c.z; s += c.w;
         s += d.x; s += d.y; s += d.z; s += d.w;
+        a = na; b = nb; c = nc; d = nd;
     }
     return s;
 }
 
+// Cross-lane reductions without the LDS crossbar: DPP moves inside each 16-lane row (xor 1, xor 2,
+// half-mirror, mirror: after the four steps every lane of a row holds the row's result), then the
+// four rows' results read into scalars.  A __shfl_xor butterfly is six dependent ds_bpermute round
+// trips; this is four DPP VALU steps and four v_readlane.  The combine is a total order, so the
+// result does not depend on the combining order.
+template <int CTRL>
+__device__ __forceinline__ int dpp_mov(int v) { return __builtin_amdgcn_mov_dpp(v, CTRL, 0xF, 0xF, false); }
+constexpr int DPP_XOR1 = 0xB1, DPP_XOR2 = 0x4E, DPP_HALF_MIRROR = 0x141, DPP_MIRROR = 0x140;
+
+// (r0 + i) mod ring for r0 < ring and i < ring (search creation checks ring >= NA)
+__device__ __forceinline__ uint32_t ring_wrap(uint32_t x, int ring) {
+    return x >= (uint32_t)ring ? x - (uint32_t)ring : x;
+}
+
 __device__ __forceinline__ float wave_max(float v) {
-    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
-    return v;
+    v = fmaxf(v, __int_as_float(dpp_mov<DPP_XOR1>(__float_as_int(v))));
+    v = fmaxf(v, __int_as_float(dpp_mov<DPP_XOR2>(__float_as_int(v))));
+    v = fmaxf(v, __int_as_float(dpp_mov<DPP_HALF_MIRROR>(__float_as_int(v))));
+    v = fmaxf(v, __int_as_float(dpp_mov<DPP_MIRROR>(__float_as_int(v))));
+    const float r0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0));
+    const float r1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 16));
+    const float r2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32));
+    const float r3 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48));
+    return fmaxf(fmaxf(r0, r1), fmaxf(r2, r3));
+}
+
+// first-max argmax over the wave: the largest score, ties to the smallest index (the reference's
+// sequential first-max scan); returns wave-uniform (best, index)
+__device__ __forceinline__ bool argmax_better(float s, int i, float bs, int bi) {
+    return s > bs || (s == bs && i < bi);
+}
+template <int CTRL>
+__device__ __forceinline__ void argmax_step(float& best, int& bi) {
+    const float ob = __int_as_float(dpp_mov<CTRL>(__float_as_int(best)));
+    const int oi = dpp_mov<CTRL>(bi);
+    if (argmax_better(ob, oi, best, bi)) { best = ob; bi = oi; }
+}
+__device__ __forceinline__ void wave_argmax(float& best, int& bi) {
+    argmax_step<DPP_XOR1>(best, bi);
+    argmax_step<DPP_XOR2>(best, bi);
+    argmax_step<DPP_HALF_MIRROR>(best, bi);
+    argmax_step<DPP_MIRROR>(best, bi);
+    float b = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(best), 0));
+    int i = __builtin_amdgcn_readlane(bi, 0);
+#pragma unroll
+    for (int r = 1; r < 4; ++r) {
+        const float ob = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(best), 16 * r));
+        const int oi = __builtin_amdgcn_readlane(bi, 16 * r);
+        if (argmax_better(ob, oi, b, i)) { b = ob; i = oi; }
+    }
+    best = b; bi = i;
+}
+// v from a wave-uniform lane (v_readlane, no LDS round trip)
+__device__ __forceinline__ int lane_bcast(int v, int src) {
+    return __builtin_amdgcn_readlane(v, __builtin_amdgcn_readfirstlane(src));
+}
+__device__ __forceinline__ float lane_bcast(float v, int src) {
+    return __int_as_float(lane_bcast(__float_as_int(v), src));
 }
 
 // inclusive prefix sum across the wave
@@ -468,29 +530,65 @@ __device__ int go_legal(const TreeDev& t, int g, int lane, const uint8_t* b, con
 // descent is ONE dependent round trip to memory: each lane loads all IT of its child records in
 // full (N, W, VL, P and the child's own header first / cnt / flag / act) before the PUCT scores,
 // and the winner's record is broadcast from its lane, so the next level needs no header load.
+// The selection's per-game inputs: the root state (not changed by an expansion) and the root
+// node's header and statistics.  k_expand_select issues these loads before the expansion runs; the
+// expansion then hands over what its backup / root expansion changed (RootHint), so the selection
+// starts its descent without a round trip.
+constexpr int AZ_SEL_BK = (AZ_MAXA + 63) / 64;
+struct SelPre {
+    int active, root;
+    uint8_t rb[AZ_SEL_BK];
+    int p0, rstones, gres, rhist;
+    uint64_t rhash, zpl0, zpl1;
+    long long c_look, c_hits, c_bytes;
+    int rN, rVL, rfirst, rcnt;
+    float rW;
+    uint8_t rflag;
+};
+struct RootHint {
+    int valid;                   // the expansion's backup updated the root's statistics
+    int N, VL; float W;
+    int hdr;                     // the expansion expanded the root: first / cnt / flag below
+    int first, cnt, flag;
+};
+__device__ __forceinline__ void select_pre(const TreeDev& t, int g, int lane, SelPre& p) {
+    const int A = t.A;
+    p.active = t.active[g];
+    p.root = t.rnode[g];
+#pragma unroll
+    for (int k = 0; k < AZ_SEL_BK; ++k) p.rb[k] = lane + 64 * k < A ? t.rboard[(size_t)g * A + lane + 64 * k] : 0;
+    p.p0 = t.rplayer[g]; p.rstones = t.rstones[g]; p.gres = t.gresult[g];
+    p.rhash = t.rhash[g]; p.zpl0 = t.zplayer[0]; p.zpl1 = t.zplayer[1];
+    p.rhist = lane < 6 ? t.rhist[g * 6 + lane] : -1;
+    const long long* cnt = t.cnt + (size_t)g * AZ_NCNT;
+    p.c_look = cnt[CNT_LOOKUPS]; p.c_hits = cnt[CNT_HITS]; p.c_bytes = cnt[CNT_BYTES_SEL];
+    const GamePtrs nd = game_nodes(t.nd, (size_t)g * t.ncap);
+    p.rN = nd.N[p.root]; p.rVL = nd.VL[p.root]; p.rW = nd.W[p.root];
+    p.rfirst = nd.first[p.root]; p.rcnt = nd.cnt[p.root]; p.rflag = nd.flag[p.root];
+}
+
 template <int IT>
-__device__ __forceinline__ void select_game(const TreeDev& t, int mode) {
+__device__ __forceinline__ void select_game(const TreeDev& t, int mode, const SelPre& pre, const RootHint* hint) {
     const int g = blockIdx.x;
     const int lane = threadIdx.x;
     __shared__ uint8_t board[AZ_MAXA];
     __shared__ int spath[AZ_DMAX];
     __shared__ int sact[AZ_DMAX];
+    __shared__ int sN[AZ_DMAX], sVL[AZ_DMAX];
+    __shared__ float sW[AZ_DMAX];
     __shared__ GoLds gl;
     const bool go = t.game == GAME_GO;
     if (g >= t.G) return;
-    // per-game inputs that do not depend on the tree, loaded before anything waits
-    constexpr int BK = (AZ_MAXA + 63) / 64;
+    constexpr int BK = AZ_SEL_BK;
     const int A = t.A;
-    const int active = t.active[g];
-    const int root = t.rnode[g];
-    uint8_t rb[BK];
-#pragma unroll
-    for (int k = 0; k < BK; ++k) rb[k] = lane + 64 * k < A ? t.rboard[(size_t)g * A + lane + 64 * k] : 0;
-    const int p0 = t.rplayer[g], rstones = t.rstones[g], gres = t.gresult[g];
-    const uint64_t rhash = t.rhash[g], zpl0 = t.zplayer[0], zpl1 = t.zplayer[1];
-    const int rhist = lane < 6 ? t.rhist[g * 6 + lane] : -1;
+    const int active = pre.active;
+    const int root = pre.root;
+    const uint8_t* rb = pre.rb;
+    const int p0 = pre.p0, rstones = pre.rstones, gres = pre.gres;
+    const uint64_t rhash = pre.rhash, zpl0 = pre.zpl0, zpl1 = pre.zpl1;
+    const int rhist = pre.rhist;
     long long* cnt = t.cnt + (size_t)g * AZ_NCNT;
-    const long long c_look = cnt[CNT_LOOKUPS], c_hits = cnt[CNT_HITS], c_bytes = cnt[CNT_BYTES_SEL];
+    const long long c_look = pre.c_look, c_hits = pre.c_hits, c_bytes = pre.c_bytes;
     tstamp(t, g, 0, 0);
     if (!active) {
         if (lane == 0) { t.lstatus[g] = ST_NONE; t.need_eval[g] = 0; }
@@ -504,7 +602,9 @@ __device__ __forceinline__ void select_game(const TreeDev& t, int mode) {
     int status = ST_NONE;
     float value = 0.0f;
     long long scanned = 0;       // child records read by the PUCT scans (25 B each)
-    uint8_t nflag = nd.flag[root];   // flag of the current node (the leaf's after the descent)
+    const bool hv = hint && hint->valid, hh = hint && hint->hdr;
+    // flag of the current node (the leaf's after the descent)
+    uint8_t nflag = hh ? (uint8_t)hint->flag : pre.rflag;
 
     if (mode != MODE_SIM) {
         // Root expansion: expandNode (noise) / search() root branch.
@@ -515,9 +615,9 @@ __device__ __forceinline__ void select_game(const TreeDev& t, int mode) {
         if (lane == 0) spath[0] = root;
     } else {
         // selectLeafWithPath: VL on the root, then PUCT descent.
-        int rN = nd.N[root], rVL = nd.VL[root];
-        float rW = nd.W[root];
-        int fc = nd.first[root], nc = nd.cnt[root];
+        int rN = hv ? hint->N : pre.rN, rVL = hv ? hint->VL : pre.rVL;
+        float rW = hv ? hint->W : pre.rW;
+        int fc = hh ? hint->first : pre.rfirst, nc = hh ? hint->cnt : pre.rcnt;
         rN += t.vl; rVL += t.vl; rW = rW - (float)t.vl;           // addVirtualLoss (root, first)
         if (lane == 0) spath[0] = root;
         tstamp(t, g, 0, 1);
@@ -550,34 +650,38 @@ __device__ __forceinline__ void select_game(const TreeDev& t, int mode) {
 #pragma unroll
             for (int k = 1; k < IT; ++k)
                 if (bk == k) { bN = cN[k]; bVL = cVL[k]; bF = cF[k]; bC = cC[k]; bA = cA[k]; bFl = cFl[k]; bW = cW[k]; }
-            for (int o = 32; o > 0; o >>= 1) {
-                float ob = __shfl_xor(best, o);
-                int oi = __shfl_xor(bi, o);
-                if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
-            }
+            wave_argmax(best, bi);
             if (bi == INT_MAX) break;
             if (depth + 1 >= AZ_DMAX) { if (lane == 0) atomicOr(t.err, ERR_PATH); break; }
             const int src = bi & 63;
-            pN = __shfl(bN, src); pVL = __shfl(bVL, src); pW = __shfl(bW, src);
-            nflag = (uint8_t)__shfl(bFl, src);
-            const int act = __shfl(bA, src);
+            pN = lane_bcast(bN, src); pVL = lane_bcast(bVL, src); pW = lane_bcast(bW, src);
+            nflag = (uint8_t)lane_bcast(bFl, src);
+            const int act = lane_bcast(bA, src);
             node = fc + bi;
-            fc = __shfl(bF, src); nc = __shfl(bC, src);
+            fc = lane_bcast(bF, src); nc = lane_bcast(bC, src);
             ++depth;
-            if (lane == 0) { spath[depth] = node; sact[depth] = act; }
+            // the node's statistics as loaded: its virtual loss below needs no second read
+            if (lane == 0) { spath[depth] = node; sact[depth] = act; sN[depth] = pN; sVL[depth] = pVL; sW[depth] = pW; }
             // its piece key lands while the next level's records load (no extra round trip)
             if (!go) zx ^= t.zpiece[(size_t)((depth & 1) ? p0 - 1 : 2 - p0) * A + act];
         }
         tstamp(t, g, 0, 2);
-        // addVirtualLoss on every path node, root a second time (parallel_mcts.cpp:293-295)
+        // addVirtualLoss on every path node, root a second time (parallel_mcts.cpp:293-295), on the
+        // statistics the descent loaded (the wave is the tree's only writer); the post-VL values also
+        // go to the path record (pstat), which the expansion's backup reads instead of the nodes
+        int4* ps = t.pstat + (size_t)g * AZ_DMAX;
         if (lane == 0) {
             rN += t.vl; rVL += t.vl; rW = rW - (float)t.vl;
             nd.N[root] = rN; nd.VL[root] = rVL; nd.W[root] = rW;
+            ps[0] = int4{rN, rVL, __float_as_int(rW), depth == 0 ? (int)nflag : 0};
         }
         __syncthreads();
         for (int i = 1 + lane; i <= depth; i += 64) {
             const int n = spath[i];
-            nd.N[n] += t.vl; nd.VL[n] += t.vl; nd.W[n] = nd.W[n] - (float)t.vl;
+            const int N = sN[i] + t.vl, VL = sVL[i] + t.vl;
+            const float W = sW[i] - (float)t.vl;
+            nd.N[n] = N; nd.VL[n] = VL; nd.W[n] = W;
+            ps[i] = int4{N, VL, __float_as_int(W), i == depth ? (int)nflag : 0};   // .w: the leaf's flag
         }
     }
     __syncthreads();
@@ -599,7 +703,7 @@ __device__ __forceinline__ void select_game(const TreeDev& t, int mode) {
         player = (depth & 1) ? 3 - p0 : p0;
         stones = rstones + depth;
         hash = rhash ^ zx ^ (p0 == 1 ? zpl0 : zpl1) ^ (player == 1 ? zpl0 : zpl1);
-        for (int i = 0; i < 6; ++i) hist6[i] = i < depth ? sact[depth - i] : __shfl(rhist, i - depth);
+        for (int i = 0; i < 6; ++i) hist6[i] = i < depth ? sact[depth - i] : lane_bcast(rhist, i - depth);
         __syncthreads();
     }
     tstamp(t, g, 0, 3);
@@ -623,7 +727,7 @@ __device__ __forceinline__ void select_game(const TreeDev& t, int mode) {
                 if (gpass >= 2) {
                     int r = 0;
                     if (lane == 0) r = go_result_seq(t, board, gl);
-                    result = __shfl(r, 0);
+                    result = lane_bcast(r, 0);
                 }
             } else {
                 const int a = sact[depth];
@@ -723,7 +827,12 @@ __device__ __forceinline__ void select_game(const TreeDev& t, int mode) {
 }
 
 template <int IT>
-__global__ __launch_bounds__(64) void k_select(TreeDev t, int mode) { select_game<IT>(t, mode); }
+__global__ __launch_bounds__(64) void k_select(TreeDev t, int mode) {
+    if (blockIdx.x >= t.G) return;
+    SelPre pre;
+    select_pre(t, blockIdx.x, threadIdx.x, pre);
+    select_game<IT>(t, mode, pre, nullptr);
+}
 
 extern "C" int az_diag_tree_stamps(unsigned long long* out, int n) {
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_tree_stamps), sizeof(unsigned long long) * (n < 128 ? n : 128)) == hipSuccess ? 0 : -1;
@@ -778,9 +887,10 @@ __global__ __launch_bounds__(1024) void k_scan(TreeDev t) {
 // then the leaf's network outputs and the path nodes' statistics -- the second and last one.
 // The Gomoku leaf board is the root board plus the path moves (no Zobrist work: k_select stored
 // the leaf hash); Go replays its captures on lane 0 (go_build_leaf).
-__device__ __forceinline__ void expand_game(const TreeDev& t, int mode) {
+__device__ __forceinline__ void expand_game(const TreeDev& t, int mode, RootHint* hint = nullptr) {
     const int g = blockIdx.x;
     const int lane = threadIdx.x;
+    if (hint && lane == 0) { hint->valid = 0; hint->hdr = 0; }
     __shared__ uint8_t board[AZ_MAXA];
     __shared__ int spath[AZ_DMAX];
     __shared__ int sact[AZ_DMAX];
@@ -801,10 +911,27 @@ __device__ __forceinline__ void expand_game(const TreeDev& t, int mode) {
     const int plen = t.plen[g];
     const float lvalue = t.lvalue[g];
     const uint64_t lhash = t.lhash[g];
-    const int slot = t.eval_slot[g];
+    const int slot = t.eval_identity ? g : t.eval_slot[g];
     const int pth0 = t.path[pb + lane], pac0 = t.pact[pb + lane];
     const int pth1 = lane < AZ_DMAX - 64 ? t.path[pb + 64 + lane] : 0;
     const int pac1 = lane < AZ_DMAX - 64 ? t.pact[pb + 64 + lane] : -1;
+    // the path nodes' statistics as k_select left them (pstat; entries past the path are stale and
+    // unused) and, with an identity batch, the leaf's network outputs: no second round trip
+    const bool sim = mode == MODE_SIM;
+    int4 ps0 = int4{0, 0, 0, 0}, ps1 = int4{0, 0, 0, 0};
+    if (sim) {
+        ps0 = t.pstat[pb + lane];
+        if (lane < AZ_DMAX - 64) ps1 = t.pstat[pb + 64 + lane];
+    }
+    const bool lg_early = t.eval_identity && (t.eval_kind == 0 || t.eval_kind == 4);
+    float lg[PK];
+    float netv = 0.0f;
+    if (lg_early) {
+        const float* src = t.net_logits + (size_t)g * NA;
+#pragma unroll
+        for (int k = 0; k < PK; ++k) lg[k] = lane + 64 * k < NA ? src[lane + 64 * k] : 0.0f;
+        netv = t.net_value[g];
+    }
     uint8_t rb[BK];
 #pragma unroll
     for (int k = 0; k < BK; ++k) rb[k] = lane + 64 * k < A ? t.rboard[(size_t)g * A + lane + 64 * k] : 0;
@@ -819,21 +946,16 @@ __device__ __forceinline__ void expand_game(const TreeDev& t, int mode) {
     const size_t base = (size_t)g * t.ncap;
     GamePtrs nd = game_nodes(t.nd, base);
     const int depth = plen - 1;
-    // ---- round trip 2: the leaf's network outputs and the path statistics of the backup
+    // ---- round trip 2 (batches that are not the identity): the leaf's network outputs
     const bool net_in = status == ST_EVAL && (t.eval_kind == 0 || t.eval_kind == 4);
-    float lg[PK];
-    float netv = 0.0f;
-    if (net_in) {
+    if (net_in && !lg_early) {
         const float* src = t.net_logits + (size_t)slot * NA;
 #pragma unroll
         for (int k = 0; k < PK; ++k) lg[k] = lane + 64 * k < NA ? src[lane + 64 * k] : 0.0f;
         netv = t.net_value[slot];
     }
-    const bool sim = mode == MODE_SIM;
-    int bN0 = 0, bVL0 = 0, bN1 = 0, bVL1 = 0;
-    float bW0 = 0.0f, bW1 = 0.0f;
-    if (sim && lane <= depth) { bN0 = nd.N[pth0]; bVL0 = nd.VL[pth0]; bW0 = nd.W[pth0]; }
-    if (sim && lane + 64 <= depth) { bN1 = nd.N[pth1]; bVL1 = nd.VL[pth1]; bW1 = nd.W[pth1]; }
+    const int bN0 = ps0.x, bVL0 = ps0.y, bN1 = ps1.x, bVL1 = ps1.y;
+    const float bW0 = __int_as_float(ps0.z), bW1 = __int_as_float(ps1.z);
 
     spath[lane] = pth0; sact[lane] = pac0;
     if (lane < AZ_DMAX - 64) { spath[64 + lane] = pth1; sact[64 + lane] = pac1; }
@@ -893,7 +1015,8 @@ __device__ __forceinline__ void expand_game(const TreeDev& t, int mode) {
             // gather is redone over the current legal set, as the reference does with entry.policy
             if (ring_cur - ttref > (uint64_t)t.ring) { if (lane == 0) atomicOr(t.err, ERR_RING); return; }
             const float* rbuf = t.ring_buf + (size_t)g * t.ring;
-            for (int a = lane; a < NA; a += 64) pol[a] = rbuf[(ttref + a) % (uint64_t)t.ring];
+            const uint32_t r0 = (uint32_t)(ttref % (uint64_t)t.ring);
+            for (int a = lane; a < NA; a += 64) pol[a] = rbuf[ring_wrap(r0 + a, t.ring)];
             __syncthreads();
           } else {
             ev_add = 1;
@@ -996,7 +1119,8 @@ __device__ __forceinline__ void expand_game(const TreeDev& t, int mode) {
             // the cached policy over the same legal set (same position => same order).
             if (ring_cur - ttref > (uint64_t)t.ring) { if (lane == 0) atomicOr(t.err, ERR_RING); return; }
             const float* rbuf = t.ring_buf + (size_t)g * t.ring;
-            for (int i = lane; i < n; i += 64) lp[i] = rbuf[(ttref + i) % (uint64_t)t.ring];
+            const uint32_t r0 = (uint32_t)(ttref % (uint64_t)t.ring);
+            for (int i = lane; i < n; i += 64) lp[i] = rbuf[ring_wrap(r0 + i, t.ring)];
         }
         __syncthreads();
         // TT store (new entry) + prior ring
@@ -1004,7 +1128,8 @@ __device__ __forceinline__ void expand_game(const TreeDev& t, int mode) {
             float* rbuf = t.ring_buf + (size_t)g * t.ring;
             const int len = go ? NA : n;            // Go keeps the policy, Gomoku the children priors
             const float* src = go ? pol : lp;
-            for (int i = lane; i < len; i += 64) rbuf[(ring_cur + i) % (uint64_t)t.ring] = src[i];
+            const uint32_t r0 = (uint32_t)(ring_cur % (uint64_t)t.ring);
+            for (int i = lane; i < len; i += 64) rbuf[ring_wrap(r0 + i, t.ring)] = src[i];
             if (lane == 0) {
                 const size_t tb = (size_t)g * t.tt_slots + tthslot;
                 t.tt_hash[tb] = hash; t.tt_visits[tb] = 1; t.tt_value[tb] = value; t.tt_ref[tb] = ring_cur;
@@ -1019,10 +1144,14 @@ __device__ __forceinline__ void expand_game(const TreeDev& t, int mode) {
             nd.N[c] = 0; nd.W[c] = 0.0f; nd.VL[c] = 0; nd.P[c] = lp[i];
             nd.first[c] = -1; nd.act[c] = (int16_t)legal[i]; nd.cnt[c] = 0; nd.flag[c] = 0;
         }
+        // the leaf's flag: k_select left it in the path record (a simulation step), else from the node
+        const int lfw = lane_bcast(depth < 64 ? ps0.w : ps1.w, depth & 63);
         if (lane == 0) {
             t.atop[g] = first + n;
-            nd.first[leaf] = first; nd.cnt[leaf] = (int16_t)n; nd.flag[leaf] = (uint8_t)(nd.flag[leaf] | FL_EXPANDED);
+            const uint8_t fl = (uint8_t)((sim ? (uint8_t)lfw : nd.flag[leaf]) | FL_EXPANDED);
+            nd.first[leaf] = first; nd.cnt[leaf] = (int16_t)n; nd.flag[leaf] = fl;
             cnt[CNT_NODES] = first + n;
+            if (hint && depth == 0) { hint->hdr = 1; hint->first = first; hint->cnt = (int16_t)n; hint->flag = fl; }
         }
         kb += 25LL * n + 7 + 4LL * n + (status == ST_EVAL ? 4LL * NA + 4 + 24 : 0);
         tstamp(t, g, 1, 6);
@@ -1043,6 +1172,7 @@ __device__ __forceinline__ void expand_game(const TreeDev& t, int mode) {
             N += 1;
             W = W + v;
             nd.N[pth0] = N; nd.VL[pth0] = VL; nd.W[pth0] = W;
+            if (hint && lane == 0) { hint->valid = 1; hint->N = N; hint->VL = VL; hint->W = W; }   // path[0]: the root
         }
         if (lane + 64 <= depth) {
             const float v = ((depth - lane - 64) & 1) ? -value : value;
@@ -1069,9 +1199,13 @@ __global__ __launch_bounds__(64) void k_expand_backup(TreeDev t, int mode) { exp
 // after the block barrier's release / acquire).  te: step i's batch maps, ts: the search's.
 template <int IT>
 __global__ __launch_bounds__(64) void k_expand_select(TreeDev te, TreeDev ts) {
-    expand_game(te, MODE_SIM);
+    if (blockIdx.x >= ts.G) return;
+    __shared__ RootHint hint;
+    SelPre pre;
+    select_pre(ts, blockIdx.x, threadIdx.x, pre);        // lands while the expansion runs
+    expand_game(te, MODE_SIM, &hint);
     __syncthreads();
-    select_game<IT>(ts, MODE_SIM);
+    select_game<IT>(ts, MODE_SIM, pre, &hint);
 }
 
 void az_launch_expand_select(const TreeDev& te, const TreeDev& ts, hipStream_t st) {
@@ -1407,6 +1541,22 @@ __global__ __launch_bounds__(64) void k_new_games(TreeDev t, const int* games, c
             for (int i = 1; i < 624; ++i) st[i] = 1812433253u * (st[i - 1] ^ (st[i - 1] >> 30)) + (uint32_t)i;
             st[624] = 624;
         }
+    }
+}
+
+// Every slot of a new handle as an idle game: a valid root (node 0 of both arenas, no children),
+// inactive.  Kernels that run over every slot (k_apply, k_compact, k_prune copy every game's tree
+// when the arenas flip) then never read an uninitialised root index; k_new_games starts a game.
+__global__ void k_init_slots(TreeDev t, Nodes other) {
+    const int g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= t.G) return;
+    t.rnode[g] = 0; t.atop[g] = 1; t.active[g] = 0; t.gresult[g] = R_ONGOING; t.ring_cur[g] = 0;
+    t.rplayer[g] = 1; t.rstones[g] = 0; t.rply[g] = 0; t.rfresh[g] = 1; t.rhash[g] = 0;
+    const Nodes* ar[2] = {&t.nd, &other};
+    for (int k = 0; k < 2; ++k) {
+        GamePtrs nd = game_nodes(*ar[k], (size_t)g * t.ncap);
+        nd.N[0] = 0; nd.W[0] = 0.0f; nd.VL[0] = 0; nd.P[0] = 0.0f; nd.first[0] = -1; nd.act[0] = -1;
+        nd.cnt[0] = 0; nd.flag[0] = 0;
     }
 }
 

@@ -333,7 +333,7 @@ def test_gpu_smallnet_matches_round2_kernel(engine, residual, B):
     x = _rand_planes(B, 11, 15, 5 + B)
     outs = {}
     try:
-        for k, w in ((1, 8), (0, 8), (0, 4), (1, 4)):
+        for k, w in ((1, 8), (0, 8), (1, 4), (2, 8), (2, 4)):
             _lib.lib().az_diag_set_smallnet_kernel(k)
             _lib.lib().az_diag_set_smallnet_waves(w)
             outs[(k, w)] = net.forward(x)

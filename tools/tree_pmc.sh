@@ -9,7 +9,15 @@ set -o pipefail
 export TMPDIR=/tmp
 O=gpurun_out/${TAG:-tree}
 mkdir -p $O
-CMD="python3 bench.py --cpu-baseline 0 --parity-steps 0 --steps 1 --warmup 0 --sims ${SIMS:-800} --blocks ${BLOCKS:-20}"
+# CONFIG=c2: BASELINE configs[1] as the bench runs it (256 games, 400 sims, the 6x64 net: every
+# kernel at its own bench config); default c3 with BLOCKS (20: the PMC passes of a full 20-block move
+# crash the profiler's host thread, SIGSEGV, profiles/r03g_tree_pmc_c3_20b_crash.txt -- BLOCKS=2
+# keeps the tree kernels' config, 2048 games x 800 sims, with a shorter trunk)
+if [ "${CONFIG:-c3}" = c2 ]; then
+  CMD="python3 bench.py --config c2 --cpu-baseline 0 --parity-steps 0 --steps 1 --warmup 0"
+else
+  CMD="python3 bench.py --cpu-baseline 0 --parity-steps 0 --steps 1 --warmup 0 --sims ${SIMS:-800} --blocks ${BLOCKS:-20}"
+fi
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o run -- $CMD > $O/trace.log 2>&1 || { echo FAIL trace; tail -3 $O/trace.log; exit 1; }
 ( while sleep 30; do echo "pmc pass running ($(date +%T))"; done ) &
 HB=$!
@@ -17,7 +25,7 @@ trap "kill $HB 2>/dev/null" EXIT
 timeout -s KILL ${PMC_TIMEOUT:-240} rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/fetch -o run -- $CMD --kernel-timing 0 > $O/fetch.log 2>&1 || { echo FAIL fetch; tail -3 $O/fetch.log; exit 1; }
 timeout -s KILL ${PMC_TIMEOUT:-240} rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/write -o run -- $CMD --kernel-timing 0 > $O/write.log 2>&1 || { echo FAIL write; tail -3 $O/write.log; exit 1; }
 kill $HB 2>/dev/null
-O=$O SIMS=${SIMS:-800} BLOCKS=${BLOCKS:-20} python3 - <<'PY'
+O=$O SIMS=${SIMS:-800} BLOCKS=${BLOCKS:-20} CONFIG=${CONFIG:-c3} python3 - <<'PY'
 import collections, csv, glob, json, os, re
 O = os.environ["O"]
 K = ["k_select", "k_expand_backup", "k_expand_select", "k_scan", "k_rec_to_g8"]
@@ -40,7 +48,9 @@ for f in glob.glob(f"{O}/trace/**/*kernel_stats.csv", recursive=True):
         k = key(r["Name"])
         if k:
             dur[k] = float(r["AverageNs"])
-out = {"workload": f"python3 bench.py --cpu-baseline 0 --parity-steps 0 --steps 1 --warmup 0 --sims {os.environ['SIMS']} --blocks {os.environ['BLOCKS']} (C3 games: 2048, 15x15, 256-filter fp16 net with {os.environ['BLOCKS']} blocks; one full move)",
+wl = ("bench.py --config c2 (C2: 256 games, 400 sims, 6x64 fp16 net; one full move)" if os.environ["CONFIG"] == "c2" else
+      f"bench.py --sims {os.environ['SIMS']} --blocks {os.environ['BLOCKS']} (C3 games: 2048, 15x15, 256-filter fp16 net with {os.environ['BLOCKS']} blocks; one full move)")
+out = {"workload": wl,
        "note": "per dispatch: FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE (KiB -> bytes), counter passes with --kernel-timing 0; average duration from the kernel-trace pass (all dispatches incl. the per-move root steps); algorithmic bytes: the bench line of the trace pass (kernel-counted, sampled steps)"}
 bl = [l for l in open(f"{O}/trace.log") if l.startswith('{"metric"')]
 if bl:

@@ -6,7 +6,6 @@ import ctypes
 import os
 import sys
 
-os.environ.setdefault("AZ_TREE_STAMPS", "137")
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "alphazero-multi-game_amd"))
 import az_amd  # noqa: E402
@@ -15,6 +14,7 @@ from az_amd import _lib  # noqa: E402
 G = int(sys.argv[1]) if len(sys.argv) > 1 else 256
 sims = int(sys.argv[2]) if len(sys.argv) > 2 else 400
 moves = int(sys.argv[3]) if len(sys.argv) > 3 else 3
+_lib.lib().az_diag_set_tree_stamps(int(os.environ.get("AZ_TREE_STAMPS", "137")))
 eng = az_amd.Engine(0)
 net = az_amd.HipNeuralNetwork(eng, az_amd.gomoku_net_desc(board_size=15, channels=64, blocks=6, max_batch=G))
 net.init_random(1)
