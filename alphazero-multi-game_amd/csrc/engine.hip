@@ -1634,7 +1634,7 @@ int az_search_create(az_engine* e, az_net* net, const az_search_cfg* c, az_searc
     SA(t.rhash, G); SA(t.rfresh, G); SA(t.rnode, G); SA(t.active, G); SA(t.gresult, G);
     uint64_t* zko = nullptr;
     if (go) { SA(t.rko, G); SA(t.rpass, G); SA(t.rposh, (size_t)G * t.hmax); SA(t.rnposh, G); SA(zko, A + 1); }
-    SA(t.path, (size_t)G * AZ_DMAX); SA(t.pact, (size_t)G * AZ_DMAX); SA(t.pstat, (size_t)G * AZ_DMAX); SA(t.plen, G); SA(t.lstatus, G); SA(t.lvalue, G); SA(t.lhash, G); SA(t.ttstore, G);
+    SA(t.path, (size_t)G * AZ_DMAX); SA(t.pact, (size_t)G * AZ_DMAX); SA(t.pstat, (size_t)G * AZ_DMAX); SA(t.rhdr, G); SA(t.plen, G); SA(t.lstatus, G); SA(t.lvalue, G); SA(t.lhash, G); SA(t.ttstore, G);
     SA(t.ttref, G); SA(t.tthslot, G); SA(t.need_eval, G); SA(t.eval_slot, G); SA(t.eval_games, G); SA(t.n_eval, 1);
     SA(t.leafrec, (size_t)G * AZ_REC_BYTES);
     SA(t.tt_hash, (size_t)G * t.tt_slots); SA(t.tt_visits, (size_t)G * t.tt_slots); SA(t.tt_value, (size_t)G * t.tt_slots);
@@ -1717,7 +1717,7 @@ void az_search_destroy(az_search* s) {
     for (const void* p : {(const void*)t.atop, (const void*)t.rboard, (const void*)t.rhist, (const void*)t.rplayer,
                           (const void*)t.rstones, (const void*)t.rply, (const void*)t.rhash, (const void*)t.rfresh,
                           (const void*)t.rnode, (const void*)t.active, (const void*)t.gresult, (const void*)t.path, (const void*)t.pact,
-                          (const void*)t.pstat,
+                          (const void*)t.pstat, (const void*)t.rhdr,
                           (const void*)t.plen, (const void*)t.lstatus, (const void*)t.lvalue, (const void*)t.lhash,
                           (const void*)t.ttstore, (const void*)t.ttref, (const void*)t.tthslot, (const void*)t.need_eval,
                           (const void*)t.eval_slot, (const void*)t.eval_games, (const void*)t.n_eval, (const void*)t.leafrec,

@@ -49,7 +49,8 @@ struct TreeDev {
     int* path; int* plen;        // [G][AZ_DMAX], [G]
     int* pact;                   // [G][AZ_DMAX] action of every path node (pact[0] unused)
     int* lstatus; float* lvalue; uint64_t* lhash; int* ttstore; uint64_t* ttref; int* tthslot;
-    int4* pstat;                 // [G][AZ_DMAX] path nodes' statistics after k_select's virtual loss {N, VL, W bits, 0}
+    int4* pstat;                 // [G][AZ_DMAX] path nodes' statistics after k_select's virtual loss {N, VL, W bits, leaf flag}
+    int4* rhdr;                  // [G] the root's header {first, cnt, flag} as the last simulation's k_select ended
     int* need_eval; int* eval_slot; int* eval_games; int* n_eval;
     int eval_identity;           // 1: the batch maps are the identity (eval_slot[g] == g): no slot load
     uint8_t* leafrec;            // [G][AZ_REC_BYTES] leaf records (leaf_planes.h): the planes' inputs (NET)

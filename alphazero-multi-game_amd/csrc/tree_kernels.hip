@@ -109,9 +109,13 @@ __device__ __forceinline__ void wave_argmax(float& best, int& bi) {
     }
     best = b; bi = i;
 }
-// v from a wave-uniform lane (v_readlane, no LDS round trip)
+// v from a wave-uniform lane (v_readlane, no LDS round trip), returned in a VGPR: these values
+// live across the descent, where scalar registers are the kernel's tight resource (spills)
 __device__ __forceinline__ int lane_bcast(int v, int src) {
-    return __builtin_amdgcn_readlane(v, __builtin_amdgcn_readfirstlane(src));
+    const int x = __builtin_amdgcn_readlane(v, __builtin_amdgcn_readfirstlane(src));
+    int r;
+    asm("v_mov_b32 %0, %1" : "=v"(r) : "s"(x));
+    return r;
 }
 __device__ __forceinline__ float lane_bcast(float v, int src) {
     return __int_as_float(lane_bcast(__float_as_int(v), src));
@@ -530,45 +534,18 @@ __device__ int go_legal(const TreeDev& t, int g, int lane, const uint8_t* b, con
 // descent is ONE dependent round trip to memory: each lane loads all IT of its child records in
 // full (N, W, VL, P and the child's own header first / cnt / flag / act) before the PUCT scores,
 // and the winner's record is broadcast from its lane, so the next level needs no header load.
-// The selection's per-game inputs: the root state (not changed by an expansion) and the root
-// node's header and statistics.  k_expand_select issues these loads before the expansion runs; the
-// expansion then hands over what its backup / root expansion changed (RootHint), so the selection
-// starts its descent without a round trip.
-constexpr int AZ_SEL_BK = (AZ_MAXA + 63) / 64;
-struct SelPre {
-    int active, root;
-    uint8_t rb[AZ_SEL_BK];
-    int p0, rstones, gres, rhist;
-    uint64_t rhash, zpl0, zpl1;
-    long long c_look, c_hits, c_bytes;
-    int rN, rVL, rfirst, rcnt;
-    float rW;
-    uint8_t rflag;
-};
+// What an expansion hands to the selection that follows it in the same wave (k_expand_select):
+// the root's statistics after the backup and its header (first child, count, flag: from the
+// root-header record k_select keeps, or as the expansion just set them), so the selection starts
+// its descent without a round trip for the root.
 struct RootHint {
-    int valid;                   // the expansion's backup updated the root's statistics
+    int valid;                   // the expansion's backup ran: the fields below are current
     int N, VL; float W;
-    int hdr;                     // the expansion expanded the root: first / cnt / flag below
     int first, cnt, flag;
 };
-__device__ __forceinline__ void select_pre(const TreeDev& t, int g, int lane, SelPre& p) {
-    const int A = t.A;
-    p.active = t.active[g];
-    p.root = t.rnode[g];
-#pragma unroll
-    for (int k = 0; k < AZ_SEL_BK; ++k) p.rb[k] = lane + 64 * k < A ? t.rboard[(size_t)g * A + lane + 64 * k] : 0;
-    p.p0 = t.rplayer[g]; p.rstones = t.rstones[g]; p.gres = t.gresult[g];
-    p.rhash = t.rhash[g]; p.zpl0 = t.zplayer[0]; p.zpl1 = t.zplayer[1];
-    p.rhist = lane < 6 ? t.rhist[g * 6 + lane] : -1;
-    const long long* cnt = t.cnt + (size_t)g * AZ_NCNT;
-    p.c_look = cnt[CNT_LOOKUPS]; p.c_hits = cnt[CNT_HITS]; p.c_bytes = cnt[CNT_BYTES_SEL];
-    const GamePtrs nd = game_nodes(t.nd, (size_t)g * t.ncap);
-    p.rN = nd.N[p.root]; p.rVL = nd.VL[p.root]; p.rW = nd.W[p.root];
-    p.rfirst = nd.first[p.root]; p.rcnt = nd.cnt[p.root]; p.rflag = nd.flag[p.root];
-}
 
 template <int IT>
-__device__ __forceinline__ void select_game(const TreeDev& t, int mode, const SelPre& pre, const RootHint* hint) {
+__device__ __forceinline__ void select_game(const TreeDev& t, int mode, const RootHint* hint) {
     const int g = blockIdx.x;
     const int lane = threadIdx.x;
     __shared__ uint8_t board[AZ_MAXA];
@@ -579,16 +556,19 @@ __device__ __forceinline__ void select_game(const TreeDev& t, int mode, const Se
     __shared__ GoLds gl;
     const bool go = t.game == GAME_GO;
     if (g >= t.G) return;
-    constexpr int BK = AZ_SEL_BK;
+    // per-game inputs that do not depend on the tree, loaded before anything waits
+    constexpr int BK = (AZ_MAXA + 63) / 64;
     const int A = t.A;
-    const int active = pre.active;
-    const int root = pre.root;
-    const uint8_t* rb = pre.rb;
-    const int p0 = pre.p0, rstones = pre.rstones, gres = pre.gres;
-    const uint64_t rhash = pre.rhash, zpl0 = pre.zpl0, zpl1 = pre.zpl1;
-    const int rhist = pre.rhist;
+    const int active = t.active[g];
+    const int root = t.rnode[g];
+    uint8_t rb[BK];
+#pragma unroll
+    for (int k = 0; k < BK; ++k) rb[k] = lane + 64 * k < A ? t.rboard[(size_t)g * A + lane + 64 * k] : 0;
+    const int p0 = t.rplayer[g], rstones = t.rstones[g], gres = t.gresult[g];
+    const uint64_t rhash = t.rhash[g], zpl0 = t.zplayer[0], zpl1 = t.zplayer[1];
+    const int rhist = lane < 6 ? t.rhist[g * 6 + lane] : -1;
     long long* cnt = t.cnt + (size_t)g * AZ_NCNT;
-    const long long c_look = pre.c_look, c_hits = pre.c_hits, c_bytes = pre.c_bytes;
+    const long long c_look = cnt[CNT_LOOKUPS], c_hits = cnt[CNT_HITS], c_bytes = cnt[CNT_BYTES_SEL];
     tstamp(t, g, 0, 0);
     if (!active) {
         if (lane == 0) { t.lstatus[g] = ST_NONE; t.need_eval[g] = 0; }
@@ -602,9 +582,9 @@ __device__ __forceinline__ void select_game(const TreeDev& t, int mode, const Se
     int status = ST_NONE;
     float value = 0.0f;
     long long scanned = 0;       // child records read by the PUCT scans (25 B each)
-    const bool hv = hint && hint->valid, hh = hint && hint->hdr;
-    // flag of the current node (the leaf's after the descent)
-    uint8_t nflag = hh ? (uint8_t)hint->flag : pre.rflag;
+    const bool hv = hint && hint->valid;
+    int4 rhdr0 = int4{0, 0, 0, 0};
+    uint8_t nflag = hv ? (uint8_t)hint->flag : nd.flag[root];   // flag of the current node (the leaf's after the descent)
 
     if (mode != MODE_SIM) {
         // Root expansion: expandNode (noise) / search() root branch.
@@ -615,9 +595,10 @@ __device__ __forceinline__ void select_game(const TreeDev& t, int mode, const Se
         if (lane == 0) spath[0] = root;
     } else {
         // selectLeafWithPath: VL on the root, then PUCT descent.
-        int rN = hv ? hint->N : pre.rN, rVL = hv ? hint->VL : pre.rVL;
-        float rW = hv ? hint->W : pre.rW;
-        int fc = hh ? hint->first : pre.rfirst, nc = hh ? hint->cnt : pre.rcnt;
+        int rN = hv ? hint->N : nd.N[root], rVL = hv ? hint->VL : nd.VL[root];
+        float rW = hv ? hint->W : nd.W[root];
+        int fc = hv ? hint->first : nd.first[root], nc = hv ? hint->cnt : nd.cnt[root];
+        rhdr0 = int4{fc, nc, (int)nflag, 0};            // the root's header (its flag as it ends below)
         rN += t.vl; rVL += t.vl; rW = rW - (float)t.vl;           // addVirtualLoss (root, first)
         if (lane == 0) spath[0] = root;
         tstamp(t, g, 0, 1);
@@ -738,6 +719,7 @@ __device__ __forceinline__ void select_game(const TreeDev& t, int mode, const Se
                 status = ST_TERMINAL;
                 value = convert_value(result, player);
                 if (lane == 0) nd.flag[leaf] = (uint8_t)(f | FL_TERMINAL | (result << 2));
+                if (depth == 0) rhdr0.z = (int)(uint8_t)(f | FL_TERMINAL | (result << 2));
             } else if (f & FL_EXPANDED) {
                 // an expanded leaf: a childless node (releaseMemory pruned its children) or the depth
                 // cap.  runSingleSimulation still looks it up in the TT (parallel_mcts.cpp:319-335) and
@@ -806,6 +788,7 @@ __device__ __forceinline__ void select_game(const TreeDev& t, int mode, const Se
         t.tthslot[g] = hslot;
         t.plen[g] = depth + 1;
         t.need_eval[g] = (status == ST_EVAL && (t.eval_kind == 0 || t.eval_kind == 4)) ? 1 : 0;
+        if (mode == MODE_SIM) t.rhdr[g] = rhdr0;        // the root-header record (the next expansion's hint)
     }
     for (int i = lane; i <= depth; i += 64) {
         t.path[(size_t)g * AZ_DMAX + i] = spath[i];
@@ -827,12 +810,7 @@ __device__ __forceinline__ void select_game(const TreeDev& t, int mode, const Se
 }
 
 template <int IT>
-__global__ __launch_bounds__(64) void k_select(TreeDev t, int mode) {
-    if (blockIdx.x >= t.G) return;
-    SelPre pre;
-    select_pre(t, blockIdx.x, threadIdx.x, pre);
-    select_game<IT>(t, mode, pre, nullptr);
-}
+__global__ __launch_bounds__(64) void k_select(TreeDev t, int mode) { select_game<IT>(t, mode, nullptr); }
 
 extern "C" int az_diag_tree_stamps(unsigned long long* out, int n) {
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_tree_stamps), sizeof(unsigned long long) * (n < 128 ? n : 128)) == hipSuccess ? 0 : -1;
@@ -890,7 +868,7 @@ __global__ __launch_bounds__(1024) void k_scan(TreeDev t) {
 __device__ __forceinline__ void expand_game(const TreeDev& t, int mode, RootHint* hint = nullptr) {
     const int g = blockIdx.x;
     const int lane = threadIdx.x;
-    if (hint && lane == 0) { hint->valid = 0; hint->hdr = 0; }
+    if (hint && lane == 0) hint->valid = 0;
     __shared__ uint8_t board[AZ_MAXA];
     __shared__ int spath[AZ_DMAX];
     __shared__ int sact[AZ_DMAX];
@@ -923,6 +901,8 @@ __device__ __forceinline__ void expand_game(const TreeDev& t, int mode, RootHint
         ps0 = t.pstat[pb + lane];
         if (lane < AZ_DMAX - 64) ps1 = t.pstat[pb + 64 + lane];
     }
+    const int4 rh = sim ? t.rhdr[g] : int4{0, 0, 0, 0};   // the root's header as k_select left it
+    int rfirst = rh.x, rcnt = rh.y, rflag = rh.z;
     const bool lg_early = t.eval_identity && (t.eval_kind == 0 || t.eval_kind == 4);
     float lg[PK];
     float netv = 0.0f;
@@ -1024,7 +1004,9 @@ __device__ __forceinline__ void expand_game(const TreeDev& t, int mode, RootHint
                 float mx = -FLT_MAX;
 #pragma unroll
                 for (int k = 0; k < PK; ++k) if (lane + 64 * k < NA) { pol[lane + 64 * k] = lg[k]; mx = fmaxf(mx, lg[k]); }
+                tstamp(t, g, 1, 8);
                 mx = wave_max(mx);
+                tstamp(t, g, 1, 9);
                 float e[PK];
 #pragma unroll
                 for (int k = 0; k < PK; ++k) {
@@ -1032,8 +1014,10 @@ __device__ __forceinline__ void expand_game(const TreeDev& t, int mode, RootHint
                     pol[lane + 64 * k] = e[k];                 // +0.0f past NA
                 }
                 __syncthreads();
+                tstamp(t, g, 1, 10);
                 if (lane == 0) s_scalar[0] = seq_sum_lds(pol, NA);
                 __syncthreads();
+                tstamp(t, g, 1, 11);
                 const float sum = s_scalar[0];
 #pragma unroll
                 for (int k = 0; k < PK; ++k)
@@ -1106,8 +1090,10 @@ __device__ __forceinline__ void expand_game(const TreeDev& t, int mode, RootHint
 #pragma unroll
             for (int k = 0; k < PK; ++k) lp[lane + 64 * k] = gv[k];   // +0.0f past n
             __syncthreads();
+            tstamp(t, g, 1, 12);
             if (lane == 0) s_scalar[0] = seq_sum_lds(lp, n);
             __syncthreads();
+            tstamp(t, g, 1, 13);
             const float ps = s_scalar[0];
             const float u = 1.0f / (float)n;
 #pragma unroll
@@ -1151,7 +1137,7 @@ __device__ __forceinline__ void expand_game(const TreeDev& t, int mode, RootHint
             const uint8_t fl = (uint8_t)((sim ? (uint8_t)lfw : nd.flag[leaf]) | FL_EXPANDED);
             nd.first[leaf] = first; nd.cnt[leaf] = (int16_t)n; nd.flag[leaf] = fl;
             cnt[CNT_NODES] = first + n;
-            if (hint && depth == 0) { hint->hdr = 1; hint->first = first; hint->cnt = (int16_t)n; hint->flag = fl; }
+            if (depth == 0) { rfirst = first; rcnt = n; rflag = fl; }   // the root was the leaf
         }
         kb += 25LL * n + 7 + 4LL * n + (status == ST_EVAL ? 4LL * NA + 4 + 24 : 0);
         tstamp(t, g, 1, 6);
@@ -1172,7 +1158,10 @@ __device__ __forceinline__ void expand_game(const TreeDev& t, int mode, RootHint
             N += 1;
             W = W + v;
             nd.N[pth0] = N; nd.VL[pth0] = VL; nd.W[pth0] = W;
-            if (hint && lane == 0) { hint->valid = 1; hint->N = N; hint->VL = VL; hint->W = W; }   // path[0]: the root
+            if (hint && lane == 0) {                    // path[0]: the root
+                hint->valid = 1; hint->N = N; hint->VL = VL; hint->W = W;
+                hint->first = rfirst; hint->cnt = rcnt; hint->flag = rflag;
+            }
         }
         if (lane + 64 <= depth) {
             const float v = ((depth - lane - 64) & 1) ? -value : value;
@@ -1197,21 +1186,23 @@ __global__ __launch_bounds__(64) void k_expand_backup(TreeDev t, int mode) { exp
 // next selection are the same wave's consecutive work (no other game is involved), so one
 // kernel boundary per step goes (the wave's own global stores are visible to its later loads
 // after the block barrier's release / acquire).  te: step i's batch maps, ts: the search's.
+// One TreeDev argument (the kernel's scalar registers are the tight resource): the expansion's
+// batch map differs from the search's only in eval_slot / eval_identity.
 template <int IT>
-__global__ __launch_bounds__(64) void k_expand_select(TreeDev te, TreeDev ts) {
-    if (blockIdx.x >= ts.G) return;
+__global__ __launch_bounds__(64) void k_expand_select(TreeDev ts, const int* eval_slot, int eval_identity) {
     __shared__ RootHint hint;
-    SelPre pre;
-    select_pre(ts, blockIdx.x, threadIdx.x, pre);        // lands while the expansion runs
+    TreeDev te = ts;
+    te.eval_slot = const_cast<int*>(eval_slot);
+    te.eval_identity = eval_identity;
     expand_game(te, MODE_SIM, &hint);
     __syncthreads();
-    select_game<IT>(ts, MODE_SIM, pre, &hint);
+    select_game<IT>(ts, MODE_SIM, &hint);
 }
 
 void az_launch_expand_select(const TreeDev& te, const TreeDev& ts, hipStream_t st) {
-    if (ts.NA <= 128) hipLaunchKernelGGL(k_expand_select<2>, dim3(ts.G), dim3(64), 0, st, te, ts);
-    else if (ts.NA <= 256) hipLaunchKernelGGL(k_expand_select<4>, dim3(ts.G), dim3(64), 0, st, te, ts);
-    else hipLaunchKernelGGL(k_expand_select<(AZ_MAXNA + 63) / 64>, dim3(ts.G), dim3(64), 0, st, te, ts);
+    if (ts.NA <= 128) hipLaunchKernelGGL(k_expand_select<2>, dim3(ts.G), dim3(64), 0, st, ts, te.eval_slot, te.eval_identity);
+    else if (ts.NA <= 256) hipLaunchKernelGGL(k_expand_select<4>, dim3(ts.G), dim3(64), 0, st, ts, te.eval_slot, te.eval_identity);
+    else hipLaunchKernelGGL(k_expand_select<(AZ_MAXNA + 63) / 64>, dim3(ts.G), dim3(64), 0, st, ts, te.eval_slot, te.eval_identity);
 }
 
 // K4: visit distribution, action choice and root value per game.

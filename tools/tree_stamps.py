@@ -30,15 +30,18 @@ names = {0: ["prologue loads issued", "root record", "descent", "leaf board", "t
              "planes + outputs", "counters / end"],
          1: ["prologue loads issued", "status", "leaf board", "legal moves", "softmax", "prior gather",
              "TT store + children", "backup / end"]}
+extra = {1: {8: "  (softmax: logits in, max)", 9: "  (wave max)", 10: "  (exp, stores, barrier)", 11: "  (sequential sum)",
+             12: "  (gather, stores, barrier)", 13: "  (sequential sum)"}}
 for k, kname in ((0, "k_select"), (1, "k_expand_backup")):
     row = st[64 * k: 64 * k + 64]
     print(kname)
+    marks = [(row[i], i, n) for i, n in enumerate(names[k]) if row[i]]
+    marks += [(row[i], i, n) for i, n in extra.get(k, {}).items() if row[i]]
+    marks.sort()
     prev = None
-    for i, n in enumerate(names[k]):
-        if row[i] == 0:
-            continue
+    for ts, i, n in marks:
         if prev is not None:
-            dt = (row[i] - row[prev]) / 100.0
+            dt = (ts - row[prev]) / 100.0
             cyc = row[32 + i] - row[32 + prev]
-            print(f"  {n:24s} {dt:7.2f} us {cyc:7d} cyc")
+            print(f"  {n:28s} {dt:7.2f} us {cyc:7d} cyc")
         prev = i
