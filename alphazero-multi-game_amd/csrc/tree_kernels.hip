@@ -922,6 +922,12 @@ __device__ __forceinline__ void expand_game(const TreeDev& t, int mode, RootHint
     const long long c_ev = cnt[CNT_EVALS], c_evt = cnt[CNT_EVALS_TOTAL], c_sims = cnt[CNT_SIMS], c_bytes = cnt[CNT_BYTES_EXP];
     tstamp(t, g, 1, 0);
     if (status == ST_NONE) return;
+    // the identity batch's logits were loaded in round trip 1: land them in LDS now, so their wait is
+    // that round trip's (the compiler would otherwise sink the loads to the softmax)
+    if (lg_early && status == ST_EVAL) {
+#pragma unroll
+        for (int k = 0; k < PK; ++k) if (lane + 64 * k < NA) pol[lane + 64 * k] = lg[k];
+    }
     tstamp(t, g, 1, 1);
     const size_t base = (size_t)g * t.ncap;
     GamePtrs nd = game_nodes(t.nd, base);
@@ -1003,7 +1009,7 @@ __device__ __forceinline__ void expand_game(const TreeDev& t, int mode, RootHint
             if (t.eval_kind == 0) {
                 float mx = -FLT_MAX;
 #pragma unroll
-                for (int k = 0; k < PK; ++k) if (lane + 64 * k < NA) { pol[lane + 64 * k] = lg[k]; mx = fmaxf(mx, lg[k]); }
+                for (int k = 0; k < PK; ++k) if (lane + 64 * k < NA) mx = fmaxf(mx, lg[k]);
                 tstamp(t, g, 1, 8);
                 mx = wave_max(mx);
                 tstamp(t, g, 1, 9);
@@ -1125,10 +1131,14 @@ __device__ __forceinline__ void expand_game(const TreeDev& t, int mode, RootHint
         // create children (include/alphazero/mcts/mcts_node.h: N=W=VL=0, prior, action)
         if (atop + n > t.ncap) { if (lane == 0) atomicOr(t.err, ERR_NODES); return; }
         const int first = atop;
-        for (int i = lane; i < n; i += 64) {
-            const int c = first + i;
-            nd.N[c] = 0; nd.W[c] = 0.0f; nd.VL[c] = 0; nd.P[c] = lp[i];
-            nd.first[c] = -1; nd.act[c] = (int16_t)legal[i]; nd.cnt[c] = 0; nd.flag[c] = 0;
+#pragma unroll
+        for (int k = 0; k < PK; ++k) {                 // unrolled: the LDS reads of every chunk before the stores
+            const int i = lane + 64 * k;
+            if (i < n) {
+                const int c = first + i;
+                nd.N[c] = 0; nd.W[c] = 0.0f; nd.VL[c] = 0; nd.P[c] = lp[i];
+                nd.first[c] = -1; nd.act[c] = (int16_t)legal[i]; nd.cnt[c] = 0; nd.flag[c] = 0;
+            }
         }
         // the leaf's flag: k_select left it in the path record (a simulation step), else from the node
         const int lfw = lane_bcast(depth < 64 ? ps0.w : ps1.w, depth & 63);
