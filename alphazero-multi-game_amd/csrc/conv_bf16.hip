@@ -467,20 +467,7 @@ __device__ __forceinline__ uint16_t v4_store(float f) {
     return f2bf(f);
 }
 
-#ifdef AZ_V4_STAMPS
-// diagnostic build only: per-block s_memrealtime (100 MHz) at start / end of main loop / end,
-// slot p.stamp (the engine numbers the trunk launches of a forward 0..2*blocks-1)
-constexpr int V4_SLOTS = 48, V4_MAXBLK = 4096;
-__device__ unsigned long long g_v4_stamps[V4_SLOTS * V4_MAXBLK * 8];
-#define V4_STAMP(k) do { if (threadIdx.x == 0 && blockIdx.x < V4_MAXBLK && p.stamp >= 0 && p.stamp < V4_SLOTS) { \
-    g_v4_stamps[((size_t)p.stamp * V4_MAXBLK + blockIdx.x) * 8 + (k)] = __builtin_amdgcn_s_memrealtime(); \
-    if ((k) < 2) g_v4_stamps[((size_t)p.stamp * V4_MAXBLK + blockIdx.x) * 8 + 5 + (k)] = __builtin_amdgcn_s_memtime(); } } while (0)
-extern "C" int az_diag_v4_stamps(unsigned long long* out, int n) {
-    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_v4_stamps), sizeof(unsigned long long) * (size_t)n);
-}
-#else
 #define V4_STAMP(k) do { } while (0)
-#endif
 
 template <int MODE, int BNT, int SCHED>
 __global__ __launch_bounds__(512, 1) void conv3x3_v4(ConvBf16Args p) {
@@ -873,20 +860,11 @@ __global__ __launch_bounds__(512, 1) void conv3x3_v5(ConvBf16Args p) {
     const int q0 = (wm * TM) % 256;
     const uint32_t a_lane = lds_addr(abuf) + bd_w * A_PLANE + lh * (V4_HROWS * 16) + (q0 + l32) * 16;
     const uint32_t b_lane = lds_addr(bbuf) + lh * BNT * 16 + (wn * (BNT / WN) + l32) * 16;
-#ifdef AZ_V4_STAMPS
-    unsigned long long t_wait = 0, t_issue = 0;
-#endif
     for (int c = 0; c < NCH; ++c) {
-#ifdef AZ_V4_STAMPS
-        const unsigned long long tw0 = __builtin_amdgcn_s_memtime();
-#endif
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __builtin_amdgcn_sched_barrier(0);
         __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_sched_barrier(0);
-#ifdef AZ_V4_STAMPS
-        t_wait += __builtin_amdgcn_s_memtime() - tw0;
-#endif
         const uint32_t ab = a_lane + (c & 1) * A_BUF;
         const uint32_t bb = b_lane + (c & 1) * B_BUF;
         auto load = [&](int tap, frag (&a)[FM], frag (&b)[FN]) {
@@ -899,32 +877,20 @@ __global__ __launch_bounds__(512, 1) void conv3x3_v5(ConvBf16Args p) {
         auto mma = [&](frag (&a)[FM], frag (&b)[FN], int tap) {
 #pragma unroll
             for (int i = 0; i < FM; ++i) {
-#ifndef AZ_V5_NOLOAD
                 // next chunk's LDS-DMA pieces ride between this chunk's MFMAs, one per tap (two per
                 // tap early in the chunk, or staggered between SIMD-mate waves, measured no better)
                 const int pk = tap * PPT + (PPT == 1 ? 0 : i / 2);
                 if ((PPT == 1 ? i == FM / 2 : (i & 1)) && c + 1 < NCH && pk < PAX + PBX) {
                     __builtin_amdgcn_sched_barrier(0);
-#ifdef AZ_V4_STAMPS
-                    const unsigned long long ti0 = __builtin_amdgcn_s_memtime();
-#endif
                     issue_piece(pk, c + 1);
-#ifdef AZ_V4_STAMPS
-                    t_issue += __builtin_amdgcn_s_memtime() - ti0;
-#endif
                     __builtin_amdgcn_sched_barrier(0);
                 }
-#endif
 #pragma unroll
                 for (int j = 0; j < FN; ++j) {
-#ifdef AZ_V5_NOMFMA
-                    acc[i][j][0] += (float)a[i][0] * (float)b[j][0];
-#else
                     if constexpr (MODE == 2)
                         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[i], b[j], acc[i][j], 0, 0, 0);
                     else
                         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
-#endif
                 }
             }
         };
@@ -946,12 +912,6 @@ __global__ __launch_bounds__(512, 1) void conv3x3_v5(ConvBf16Args p) {
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __syncthreads();
     V4_STAMP(1);
-#ifdef AZ_V4_STAMPS
-    if (threadIdx.x == 0 && blockIdx.x < V4_MAXBLK && p.stamp >= 0 && p.stamp < V4_SLOTS)
-        g_v4_stamps[((size_t)p.stamp * V4_MAXBLK + blockIdx.x) * 8 + 3] = t_wait;   // shader cycles in wait+barrier
-    if (threadIdx.x == 0 && blockIdx.x < V4_MAXBLK && p.stamp >= 0 && p.stamp < V4_SLOTS)
-        g_v4_stamps[((size_t)p.stamp * V4_MAXBLK + blockIdx.x) * 8 + 4] = t_issue;
-#endif
 
     // epilogue in two column passes (acc[.][j], j = 0, 1), both boards at once: the staged
     // fp32 tile is [2 boards][225 pixels][64 + 4], so the other pass's accumulators are the only
@@ -1101,7 +1061,7 @@ struct G8Geom {
 
 typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
-template <int MODE, int HB = 15, bool DENSE = false, int DV = 0>   // DV: timing-only variants (AZ_V6_DIAG)
+template <int MODE, int HB = 15, bool DENSE = false>
 __global__ __launch_bounds__(512, 1) void conv3x3_v6(ConvBf16Args p) {
     static_assert(MODE == 1 || MODE == 2, "v6: single-plane modes");
     typedef Half16<MODE> H16;
@@ -1137,11 +1097,6 @@ __global__ __launch_bounds__(512, 1) void conv3x3_v6(ConvBf16Args p) {
     const int b0 = pair * BOARDS;                        // FLAT: pair is the tile index
     if (GM::FLAT ? pair * 512 >= nboards * GM::S : b0 >= nboards) return;
     V4_STAMP(3);
-#ifdef AZ_V4_STAMPS
-    if (threadIdx.x == 0 && blockIdx.x < V4_MAXBLK && p.stamp >= 0 && p.stamp < V4_SLOTS)
-        g_v4_stamps[((size_t)p.stamp * V4_MAXBLK + blockIdx.x) * 8 + 7] =
-            (unsigned long long)__builtin_amdgcn_s_getreg(0xF804) | ((unsigned long long)__builtin_amdgcn_s_getreg(0xF814) << 32);
-#endif
     const int C = p.C, GI = C / 8, GO = p.N / 8;
     const int NCH = C / 32, NS = NCH * 3;
 
@@ -1155,23 +1110,10 @@ __global__ __launch_bounds__(512, 1) void conv3x3_v6(ConvBf16Args p) {
         __builtin_amdgcn_make_buffer_rsrc((void*)p.Ahi, (short)0, (int)(a_bytes + AZ_ACT_TAIL * 2), 0x00020000);
     const __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc((void*)p.Bblk, (short)0, (int)b_bytes, 0x00020000);
     const uint32_t PAD = a_bytes;
-#ifdef AZ_V6_DIAG
-    // timing-only variants (tools/net_bench.py --flags): 16/32 = zero-record B/A descriptor (loads
-    // dropped by the range check, instruction stream unchanged); 64/128 = B/A pieces not issued
-    const __amdgpu_buffer_rsrc_t rsA_d =
-        __builtin_amdgcn_make_buffer_rsrc((void*)p.Ahi, (short)0, (p.flags & 32) ? 0 : (int)(a_bytes + AZ_ACT_TAIL * 2), 0x00020000);
-    const __amdgpu_buffer_rsrc_t rsB_d =
-        __builtin_amdgcn_make_buffer_rsrc((void*)p.Bblk, (short)0, (p.flags & 16) ? 0 : (int)b_bytes, 0x00020000);
-#define AZ_RSA rsA_d
-#define AZ_RSB rsB_d
-#define AZ_SKIP_A if (p.flags & 128) return;
-#define AZ_SKIP_B if (p.flags & 64) return;
-#else
 #define AZ_RSA rsA
 #define AZ_RSB rsB
 #define AZ_SKIP_A
 #define AZ_SKIP_B
-#endif
     uint32_t a_vo[PA];
     int a_off[PA];
 #pragma unroll
@@ -1276,7 +1218,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_v6(ConvBf16Args p) {
         else allow = issued(s - 1) + (s >= 2 && ((s - 2) % 3) == 0 && (s - 2) / 3 + 1 < NCH ? pa_w : 0);
         wait_vm(allow);
         __builtin_amdgcn_sched_barrier(0);
-        if constexpr (!(DV & 2)) __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_sched_barrier(0);
         const uint32_t ab = a_lane + (c & 1) * A_BUF;
         const uint32_t bb = b_lane + (s % 3) * B_STAGE;
@@ -1331,9 +1273,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_v6(ConvBf16Args p) {
                 }
 #pragma unroll
                 for (int j = 0; j < FN; ++j) {
-                    if constexpr (DV & 1)
-                        asm volatile("" : "+v"(acc[half * 4 + i][j]) : "v"(a[i]), "v"(b[j]));
-                    else if constexpr (MODE == 2)
+                    if constexpr (MODE == 2)
                         acc[half * 4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[i], b[j], acc[half * 4 + i][j], 0, 0, 0);
                     else
                         acc[half * 4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[half * 4 + i][j], 0, 0, 0);
@@ -1411,11 +1351,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_v6(ConvBf16Args p) {
         }
         return it;
     };
-#ifdef AZ_V6_DIAG
-    const bool d_noload = (p.flags >> 20) & 1, d_nostore = (p.flags >> 21) & 1;   // timing-only epilogue variants
-#else
     constexpr bool d_noload = false, d_nostore = false;
-#endif
     auto fetch = [&](int pp, int v) {
         Res rr{};
         const Item it = item(v);
@@ -1692,15 +1628,6 @@ static void v6_launch_g(const ConvBf16Args& a, int mode, hipStream_t st) {
     const int boards = a.M / GM::HW;
     const int groups = GM::FLAT ? (boards * GM::S + 511) / 512 : (boards + GM::BOARDS - 1) / GM::BOARDS;
     const int grid = (groups + 7) / 8 * 8 * (a.N / 128);   // XCD-aware group/half mapping: whole groups of 8
-#ifdef AZ_V6_DIAG
-    if (HB == 15 && !DENSE && mode == 2 && (a.flags >> 24) & 3) {
-        switch ((a.flags >> 24) & 3) {
-            case 1: hipLaunchKernelGGL((conv3x3_v6<2, 15, false, 1>), dim3(grid), dim3(512), 0, st, a); return;
-            case 2: hipLaunchKernelGGL((conv3x3_v6<2, 15, false, 2>), dim3(grid), dim3(512), 0, st, a); return;
-            default: hipLaunchKernelGGL((conv3x3_v6<2, 15, false, 3>), dim3(grid), dim3(512), 0, st, a); return;
-        }
-    }
-#endif
     if (mode == 2) hipLaunchKernelGGL((conv3x3_v6<2, HB, DENSE>), dim3(grid), dim3(512), 0, st, a);
     else hipLaunchKernelGGL((conv3x3_v6<1, HB, DENSE>), dim3(grid), dim3(512), 0, st, a);
 }

@@ -103,14 +103,13 @@ __device__ __forceinline__ void certify_frags(F (&a)[JA], F (&b)[JB]) {
 }  // namespace
 
 // measurement only (tools/sm_check.sh, tools/net_bench.py): 4 = one wave per SIMD instead of the
-// default 8-wave block.  Kernel 0 (default) = k_smallnet_g (weights streamed into registers), 1 = the
-// round-2 kernel (k_smallnet_r2), 2 = k_smallnet (weights through the LDS ring); A/B only
+// default 8-wave block of the round-2 kernel.  Kernel 0 (default) = k_smallnet_g (weights streamed
+// into registers), 1 = the round-2 kernel (k_smallnet_r2: A/B and the bitwise-equality test)
 static int g_sm_waves = 8;
 static int g_sm_kernel = 0;
 static int g_sm_stamp_mode = 0;
 int az_smallnet_stamps_mode() { return g_sm_stamp_mode; }
-// phase stamps of block 0 (tools/sm_stamps.py): 1 = on; with the -DAZ_SM_DIAG build, 2..8 select the
-// round-2 kernel's timing-only variants (their outputs are wrong)
+// phase stamps of block 0 (tools/sm_stamps.py): nonzero = on
 extern "C" int az_diag_set_smallnet_stamps(int mode) {
     g_sm_stamp_mode = mode;
     return 0;
@@ -120,7 +119,7 @@ extern "C" int az_diag_set_smallnet_waves(int nw) {
     return 0;
 }
 extern "C" int az_diag_set_smallnet_kernel(int k) {
-    g_sm_kernel = k == 1 || k == 2 ? k : 0;
+    g_sm_kernel = k == 1 ? 1 : 0;
     return 0;
 }
 
@@ -128,16 +127,15 @@ extern "C" int az_diag_smallnet_stamps(unsigned long long* out, int n) {
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sm_stamps), sizeof(unsigned long long) * (n < 128 ? n : 128)) == hipSuccess ? 0 : -1;
 }
 
-// DV: timing-only variants (build with -DAZ_SM_DIAG, AZ_SM_STAMPS=<DV+1>): 1 = no per-tap barriers
-// (waits only), 2 = no MFMAs, 3 = neither, 4 = no fragment reads after a layer's first steps
-// (MFMAs on stale registers), 8 = no weight DMA in the layers.  Their outputs are wrong.
+// The round-2 kernel (A/B and the bitwise-equality test of k_smallnet_g; its timing-only
+// variants are gone, their measurements are in profiles/r03e_smallnet_diag_variants.txt).
 // NW = 4: one wave per SIMD, each wave all 64 output channels of its 4 pixel fragments.  NW = 8
 // (default; AZ_SM_WAVES=4 selects the other): two waves per SIMD, wave w owns the pixel fragments
 // of group w & 3 and output channels 32 (w >> 2) .. +31.  Measured (phase stamps, 256 boards): the
 // layers take the same 11.3k cycles either way -- every layer ends in a block-wide epilogue and
 // barrier that no MFMA can overlap, one board per CU -- while the prologue, pool and head convs
 // are 2.4 us shorter with 8 waves.
-template <int HB, int DV = 0, int NW = 4>
+template <int HB, int NW = 4>
 __global__ __launch_bounds__(64 * NW, 1) void k_smallnet_r2(SmallNetArgs p) {
     typedef SmGeom<HB, NW> GM;
     constexpr int NT = 64 * NW;                          // threads
@@ -326,13 +324,13 @@ __global__ __launch_bounds__(64 * NW, 1) void k_smallnet_r2(SmallNetArgs p) {
         // tap before the loop.  A step's reads are certified once at most the younger batches are
         // outstanding.  Tile (tap) t+1 is certified before tap t starts, so reads one tap ahead are legal.
         constexpr int NSTEP = 9 * NCH;
-        auto LD = [](int x) constexpr { return x < NSTEP && !((DV & 4) && x > 2); };
+        auto LD = [](int x) constexpr { return x < NSTEP; };
         load(0, src, s0, std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{});
         if constexpr (LD(1))
             load(1, src, s0 + 1 / NCH, std::integral_constant<int, 1 / NCH>{}, std::integral_constant<int, 1 % NCH>{});
         static_for<0, NSTEP>([&](auto qc) {
             constexpr int q = decltype(qc)::value, t = q / NCH, kk = q % NCH, r = q % 3;
-            if constexpr (kk == 0 && !(DV & 8)) issue_w(s0 + t + DIST);   // its slot was last read at tap s - 3
+            if constexpr (kk == 0) issue_w(s0 + t + DIST);   // its slot was last read at tap s - 3
             if constexpr (LD(q + 2))
                 load((q + 2) % 3, src, s0 + (q + 2) / NCH, std::integral_constant<int, (q + 2) / NCH>{},
                      std::integral_constant<int, (q + 2) % NCH>{});
@@ -340,7 +338,7 @@ __global__ __launch_bounds__(64 * NW, 1) void k_smallnet_r2(SmallNetArgs p) {
             certify(std::integral_constant<int, r>{}, std::integral_constant<int, (younger > 15 ? 15 : younger)>{});   // lgkmcnt <= 15
             // pin the order: the next steps' reads are in flight while this step's MFMAs issue
             __builtin_amdgcn_sched_barrier(0);
-            if constexpr (!(DV & 2)) mma(r);
+            mma(r);
             __builtin_amdgcn_sched_barrier(0);
             if constexpr (kk == NCH - 1) {
                 // tile s+2 landed (s+3..s+DIST stay in flight: no __syncthreads, whose vmcnt(0) would
@@ -351,8 +349,6 @@ __global__ __launch_bounds__(64 * NW, 1) void k_smallnet_r2(SmallNetArgs p) {
                     epilogue(layer, dst);
                     if (layer == 5) sm_stamp(p, 53);             // epilogue issued
                     asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"i"((DIST - 2) * WPT) : "memory");
-                } else if constexpr (DV & 1) {
-                    asm volatile("s_waitcnt vmcnt(%0)" ::"i"((DIST - 2) * WPT) : "memory");
                 } else {
                     if (layer == 5) sm_stamp(p, 43 + t);         // tap t's MFMAs issued (before the wait)
                     asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"i"((DIST - 2) * WPT) : "memory");
@@ -442,32 +438,32 @@ __global__ __launch_bounds__(64 * NW, 1) void k_smallnet_r2(SmallNetArgs p) {
 
 namespace {
 // ------------------------------------------------------------------------------------------------
-// k_smallnet (round 3): the same fused forward, rebuilt around what the round-2 kernel's phase
-// stamps measured (profiles/r03e_smallnet_diag_variants.txt, r03f_*): its 18 steps of a layer ran
-// at ~2x the MFMA time, and each layer paid ~2.4k cycles of epilogue on top.  The fixes:
+// k_smallnet_g (round 3, the shipped kernel): the same fused forward, rebuilt around what the
+// round-2 kernel's phase stamps measured (profiles/r03e_smallnet_diag_variants.txt, r03f_*): its 18
+// steps of a layer ran at ~2x the MFMA time, and each layer paid ~2.4k cycles of epilogue on top.
 //  * operand addresses are a per-lane base plus a compile-time offset (ds_read_b128 offset:imm), so
-//    a step issues its 6 fragment reads and 8 MFMAs with no address VALU (the round-2 kernel
+//    a step issues its fragment reads and 8 MFMAs with no address VALU (the round-2 kernel
 //    recomputed 6 XOR-swizzled addresses per step: ~40 VALU, more issue cycles than its MFMAs at
 //    two waves per SIMD).  Activation rows are padded to RS = 160 B instead of swizzled: every tap
 //    shift of a fragment is then a constant offset, and the 16-lane groups of ds_read_b128 still
-//    hit 16 distinct 16-B bank slots (10 r + c mod 16 over a group's rows r and chunks c; 144 and
-//    192 B strides conflict).  Weight tiles keep the chunk ^ (row & 7) swizzle, whose row is fixed
-//    per lane: one base per 32-channel chunk;
-//  * a ring of 6 weight tiles, which divides the 18 taps of a layer pair: the slot of every tap is
-//    a compile-time constant (tap 0 of an even layer lands in slot 0, of an odd layer in slot 3),
-//    loaded 5 taps ahead, certified one tap ahead;
+//    hit 16 distinct 16-B bank slots (10 r + c mod 16 over a group's rows r and chunks c; 128, 144
+//    and 192 B strides conflict);
+//  * the weights stream from L1 / L2 straight into registers (below), so the LDS carries only
+//    activations and a layer has one barrier (a variant with an LDS weight ring and compile-time
+//    slots over layer pairs measured 57.9 vs 55.7 us per forward, profiles/r03f_smallnet_ab.txt);
 //  * layers run in pairs (first / second conv of a residual block) with the role compile-time: no
 //    runtime selects in the epilogue, which is one v_med3 per value (ReLU and the dead-row mask in
 //    one: med3(v, 0, +inf) on live rows, med3(v, 0, 0) = 0 on the grid's dead columns, which land
 //    on the halo's zero padding) plus the fp16 pack and one ds_write_b64;
-//  * the prologue zeroes only the halo rows no epilogue writes and waits for the first two weight
-//    tiles only; the adaptive pool issues all its loads before the y-major sums.
+//  * the prologue zeroes only the halo rows no epilogue writes; the adaptive pool issues all its
+//    loads before the y-major sums.
 // Arithmetic is the round-2 kernel's: the same MFMAs in the same order (tap-major, 32-channel
-// chunk minor), fp32 residual stream in registers, fp16 activations rounded to nearest even.
+// chunk minor), fp32 residual stream in registers, fp16 activations rounded to nearest even
+// (tests/test_gpu_net.py::test_gpu_smallnet_matches_round2_kernel: bitwise equal).
 constexpr int RS = 160;          // activation row stride, bytes (64 fp16 channels + 32 B pad)
 
-template <int HB, int NW, int BAR = 1>
-struct Sm2 {
+template <int HB, int NW>
+struct Sm2 {                                             // the board's geometry in k_smallnet_g
     static constexpr int WG = HB + 2, HW = HB * HB, GRID = HB * WG;
     static constexpr int NFRAG = (GRID + 15) / 16;       // 16-row pixel fragments (wave wp: wp + 4 i)
     static constexpr int FPW = NFRAG / 4;
@@ -475,23 +471,10 @@ struct Sm2 {
     static constexpr int NT = 64 * NW;
     static constexpr int IR = NFRAG * 16 + 2 * WG + 2;   // halo rows the last fragment's taps read
     static constexpr int IMG = IR * RS;
-    static constexpr int WT = SF * SF * 2;               // one tap's weight tile [64 n][64 c] fp16
-    // ring: tile s + DIST lands in the slot of tile s + DIST - NSLOT, which every wave has consumed
-    // once waves are at most BAR taps apart (one barrier per BAR taps); each barrier certifies the
-    // tiles the next BAR taps read (one tap ahead), leaving DIST - BAR - 1 tiles in flight
-    static constexpr int NSLOT = 6, DIST = NSLOT - BAR, INFLIGHT = DIST - BAR - 1;
-    static_assert(INFLIGHT >= 0, "ring too small for BAR taps per barrier");
-    static constexpr int WPT = 512 / NT;                 // 16-B DMA pieces per thread per tile
     static constexpr int MAXL = 32;                      // bias rows (L <= 31: the epilogue reads row L)
-    static constexpr int OX = 0, OY = IMG, OW = 2 * IMG, OB = OW + NSLOT * WT;
-    static constexpr int LDS = OB + MAXL * SF * 4;
     static_assert(NFRAG % 4 == 0, "four pixel groups of FPW fragments");
-    static_assert(LDS <= 160 * 1024, "board does not fit the CU's LDS");
     static_assert(HW * SF * 4 <= 2 * IMG, "fp32 stream does not fit over the images");
     static_assert(64 * RS * (FPW - 1) + RS * (2 * WG + 2) + 64 < 65536, "activation offsets fit offset:imm");
-    static_assert((NSLOT - 1) * WT + 3 * 2048 < 65536, "weight offsets fit offset:imm");
-    static_assert(18 % NSLOT == 0 && 9 % NSLOT == 3, "tap 0 of even layers in slot 0, of odd layers in slot 3");
-    static_assert(2 * SF * SF <= NSLOT * WT, "pool + head staging fits the ring");
 };
 
 template <int OFF, typename T>
@@ -551,284 +534,6 @@ __device__ __forceinline__ void pool_cells(const uint8_t* xs, float* pooled, int
 }
 
 }  // namespace
-
-template <int HB, int NW, bool RES, int BAR = 1>
-__global__ __launch_bounds__(64 * NW, 1) void k_smallnet(SmallNetArgs p) {
-    typedef Sm2<HB, NW, BAR> G;
-    constexpr int NT = G::NT, WG = G::WG, HW = G::HW, FPW = G::FPW, JN = G::JN, WPT = G::WPT;
-    constexpr int NSLOT = G::NSLOT, DIST = G::DIST, WT = G::WT;
-    __shared__ __attribute__((aligned(16))) uint8_t lds[G::LDS];
-    const uint32_t L0 = (uint32_t)(uintptr_t)lds;
-    const int b = blockIdx.x;
-    const int tid = threadIdx.x, lane = tid & 63;
-    // threads 0..NFRAG*16-1 own one output-grid row each in the prologue: the record byte of its
-    // pixel and the meta ints, fetched first
-    const int gq = tid, gy = gq / WG, gx = gq - gy * WG;
-    const bool glive = gq < G::NFRAG * 16 && gy < HB && gx < HB;
-    int rv = 0;
-    int meta[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (p.rec) {
-        const int gi = min(max(p.gidx[b], 0), p.rec_n - 1);
-        const uint8_t* rec = p.rec + (size_t)gi * AZ_REC_BYTES;
-        rv = glive ? rec[gy * HB + gx] : 0;
-        const int4 m0 = *reinterpret_cast<const int4*>(rec + AZ_REC_META);
-        const int4 m1 = *reinterpret_cast<const int4*>(rec + AZ_REC_META + 16);
-        meta[0] = m0.x; meta[1] = m0.y; meta[2] = m0.z; meta[3] = m0.w;
-        meta[4] = m1.x; meta[5] = m1.y; meta[6] = m1.z; meta[7] = m1.w;
-    }
-    if (p.m_limit && b >= *p.m_limit) return;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int wp = wave & 3;                             // pixel group: fragments wp + 4 i
-    const int J0 = (wave >> 2) * JN;                     // first 16-channel output block of this wave
-    const int l16 = lane & 15, lg = lane >> 4;
-    const int L = 2 * p.blocks + 1;
-    const int S = 9 * L;                                 // weight tiles streamed: (layer, tap)
-    sm_stamp(p, 0);
-
-    // global loads the prologue consumes (head 1x1 weights, biases), issued before the weight DMA
-    // so the compiler's waits for them do not drain it
-    constexpr int HWT = SF * SF / NT;                    // element (c, o) = tid + NT k, o fastest
-    float wpre[HWT];
-#pragma unroll
-    for (int k = 0; k < HWT; ++k) {
-        const int i = tid + NT * k, c = i / SF, o = i - c * SF;
-        wpre[k] = o < p.HC ? p.Wpc[o * SF + c] : p.Wvc[(o - p.HC) * SF + c];
-    }
-    constexpr int BPT = (G::MAXL * SF + NT - 1) / NT;
-    float bpre[BPT];
-#pragma unroll
-    for (int k = 0; k < BPT; ++k) {
-        const int i = tid + NT * k;
-        bpre[k] = i < L * SF ? p.bias[i] : 0.0f;
-    }
-    // weight tile s -> slot: 512 pieces of 16 B; LDS position (row n, physical chunk pc) holds
-    // logical chunk pc ^ (n & 7) (swizzle applied at the source).  Past the last tile the last one
-    // is reloaded into the free slot, so every tap issues the same loads (constant vmcnt budget).
-    int woff[WPT];
-#pragma unroll
-    for (int j = 0; j < WPT; ++j) {
-        const int P = j * NT + tid, n = P >> 3, pc = P & 7;
-        woff[j] = n * SF + 8 * (pc ^ (n & 7));
-    }
-    auto issue_w = [&](int s, auto slotc) {
-        constexpr int slot = decltype(slotc)::value;
-        const uint16_t* src = p.W + (size_t)min(s, S - 1) * (SF * SF);
-#pragma unroll
-        for (int j = 0; j < WPT; ++j)
-            __builtin_amdgcn_global_load_lds((const void*)(src + woff[j]),
-                                             (lds_void_t*)(lds + G::OW + slot * WT + (j * NT + wave * 64) * 16), 16, 0, 0);
-    };
-    static_for<0, DIST>([&](auto sc) { issue_w(decltype(sc)::value, IC<decltype(sc)::value % NSLOT>{}); });
-
-    // halo rows no epilogue writes: X and Y rows [0, WG+1) and [NFRAG*16 + WG + 1, IR), all 8
-    // chunks; Y's band rows: the input planes (channels 0..15) and zeros (16..31: the input conv
-    // reads one 32-channel chunk), from the threads that own the grid rows
-    {
-        constexpr int TOP = WG + 1, BOT0 = G::NFRAG * 16 + WG + 1, NPAD = TOP + (G::IR - BOT0);
-        for (int i = tid; i < 2 * NPAD * 8; i += NT) {
-            const int img = i / (NPAD * 8), k = i - img * NPAD * 8, r = k >> 3, c = k & 7;
-            const int row = r < TOP ? r : BOT0 + (r - TOP);
-            *reinterpret_cast<uint4*>(lds + (img ? G::OY : G::OX) + row * RS + c * 16) = uint4{0, 0, 0, 0};
-        }
-        if (tid < G::NFRAG * 16) {
-            float c[16];
-#pragma unroll
-            for (int k = 0; k < 16; ++k) c[k] = 0.0f;
-            if (glive) {
-                const int px = gy * HB + gx;
-                if (p.rec) {
-                    az_leaf_planes_v(rv, 0, meta, 0, HB, px, c);
-                } else {
-                    const float* x0 = p.x0 + ((size_t)b * HW + px) * 16;
-#pragma unroll
-                    for (int k = 0; k < 16; k += 4) {
-                        const float4 u = *reinterpret_cast<const float4*>(x0 + k);
-                        c[k] = u.x; c[k + 1] = u.y; c[k + 2] = u.z; c[k + 3] = u.w;
-                    }
-                }
-            }
-            uint8_t* dst = lds + G::OY + (gq + WG + 1) * RS;
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                const uint4 v = {pack_f16(c[8 * h], c[8 * h + 1]), pack_f16(c[8 * h + 2], c[8 * h + 3]),
-                                 pack_f16(c[8 * h + 4], c[8 * h + 5]), pack_f16(c[8 * h + 6], c[8 * h + 7])};
-                *reinterpret_cast<uint4*>(dst + 16 * h) = v;
-                *reinterpret_cast<uint4*>(dst + 32 + 16 * h) = uint4{0, 0, 0, 0};
-            }
-        }
-        float* bsm = reinterpret_cast<float*>(lds + G::OB);
-#pragma unroll
-        for (int k = 0; k < BPT; ++k) {
-            const int i = tid + NT * k;
-            if (i < L * SF) bsm[i] = bpre[k];
-        }
-    }
-    // the tiles the first BAR taps read landed (INFLIGHT stay in flight), every prologue store done
-    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"i"(G::INFLIGHT * WPT) : "memory");
-    sm_stamp(p, 1);
-
-    // per-lane bases: activation fragment reads, epilogue writes, weight fragment reads, biases
-    const uint32_t aX = L0 + G::OX + (16 * wp + l16) * RS + 16 * lg, aY = aX + G::OY;
-    const uint32_t eX = L0 + G::OX + (16 * wp + l16 + WG + 1) * RS + 32 * J0 + 8 * lg, eY = eX + G::OY;
-    uint32_t wb[2];
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) wb[kk] = L0 + G::OW + (16 * J0 + l16) * 128 + 16 * ((4 * kk + lg) ^ (l16 & 7));
-    const uint32_t bb = L0 + G::OB + (16 * J0 + 4 * lg) * 4;
-    float mlive[FPW];                                    // +inf on live output rows, 0 on dead ones
-#pragma unroll
-    for (int i = 0; i < FPW; ++i) {
-        const int q = 16 * (wp + 4 * i) + l16, y = q / WG, x = q - y * WG;
-        mlive[i] = (y < HB && x < HB) ? __builtin_inff() : 0.0f;
-    }
-
-    f32x4v acc[FPW][JN];
-    f32x4v xr[FPW][JN];                                  // fp32 residual stream (the lane's outputs)
-    f32x4v bn[JN];                                       // the next layer's biases
-    f16x8 fa[3][JN], fb[3][FPW];                         // operand fragments (up to 3 buffers)
-    auto read_bias = [&](int layer) {
-        const uint32_t a = bb + layer * (SF * 4);
-        static_for<0, JN>([&](auto jc) { ds_rd<64 * decltype(jc)::value>(bn[decltype(jc)::value], a); });
-    };
-    read_bias(0);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-
-    // one layer: ROLE (input / first / second conv of a residual block), NCH 32-channel chunks per
-    // tap, SB the ring slot of its tap 0.  Step x = (tap x / NCH, chunk x % NCH); its fragments are
-    // read PF steps ahead (buffer x % (PF + 1)); tile t + 1 is certified before tap t starts.
-    auto run_layer = [&](int layer, auto rolec, auto nchc, auto sbc) {
-        constexpr int ROLE = decltype(rolec)::value, NCH = decltype(nchc)::value, SB = decltype(sbc)::value;
-        constexpr int NSTEP = 9 * NCH, PF = NCH == 1 ? 1 : 2, NB = PF + 1;
-        const uint32_t src = ROLE == ROLE_ODD ? aX : aY;
-        const uint32_t dst = ROLE == ROLE_ODD ? eY : eX;
-        const int s0 = 9 * layer;
-        static_for<0, FPW>([&](auto ic) {
-            static_for<0, JN>([&](auto jc) { acc[decltype(ic)::value][decltype(jc)::value] = bn[decltype(jc)::value]; });
-        });
-        auto load = [&](auto bufc, auto xc) {
-            constexpr int buf = decltype(bufc)::value, x = decltype(xc)::value;
-            constexpr int t = x / NCH, kk = x % NCH, slot = (SB + t) % NSLOT, sh = (t / 3) * WG + (t % 3);
-            static_for<0, JN>([&](auto jc) {
-                constexpr int j = decltype(jc)::value;
-                ds_rd<slot * WT + j * 2048>(fa[buf][j], wb[kk]);
-            });
-            static_for<0, FPW>([&](auto ic) {
-                constexpr int i = decltype(ic)::value;
-                ds_rd<64 * RS * i + RS * sh + 64 * kk>(fb[buf][i], src);
-            });
-        };
-        static_for<0, PF>([&](auto xc) { load(IC<decltype(xc)::value % NB>{}, xc); });
-        static_for<0, NSTEP>([&](auto qc) {
-            constexpr int q = decltype(qc)::value, t = q / NCH, kk = q % NCH, r = q % NB;
-            if constexpr (kk == 0) issue_w(s0 + t + DIST, IC<(SB + t + DIST) % NSLOT>{});
-            if constexpr (q + PF < NSTEP) load(IC<(q + PF) % NB>{}, IC<q + PF>{});
-            constexpr int ahead = (NSTEP - 1 - q) < PF ? (NSTEP - 1 - q) : PF;
-            constexpr int younger = ahead * (JN + FPW);
-            certify_frags<(younger > 15 ? 15 : younger)>(fa[r], fb[r]);
-            __builtin_amdgcn_sched_barrier(0);
-            static_for<0, FPW>([&](auto ic) {
-                static_for<0, JN>([&](auto jc) {
-                    constexpr int i = decltype(ic)::value, j = decltype(jc)::value;
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[r][j], fb[r][i], acc[i][j], 0, 0, 0);
-                });
-            });
-            __builtin_amdgcn_sched_barrier(0);
-            if constexpr (kk == NCH - 1) {
-                if (layer == 5) sm_stamp(p, 43 + t);
-                if constexpr (t == 8) {
-                    // epilogue from registers: lane holds channels 16 (J0 + j) + 4 lg + e of grid row
-                    // 16 (wp + 4 i) + l16
-                    static_for<0, FPW>([&](auto ic) {
-                        static_for<0, JN>([&](auto jc) {
-                            constexpr int i = decltype(ic)::value, j = decltype(jc)::value;
-                            f32x4v v = acc[i][j];
-                            if constexpr (ROLE == ROLE_EVEN && RES) v += xr[i][j];
-#pragma unroll
-                            for (int e = 0; e < 4; ++e) v[e] = __builtin_amdgcn_fmed3f(v[e], 0.0f, mlive[i]);
-                            if constexpr (ROLE != ROLE_ODD) xr[i][j] = v;
-                            ds_wr64<64 * RS * i + 32 * j>(dst, pack_f16(v[0], v[1]), pack_f16(v[2], v[3]));
-                        });
-                    });
-                    read_bias(layer + 1);                // row L (past the last layer) is never used
-                    if (layer == 5) sm_stamp(p, 53);
-                    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"i"(G::INFLIGHT * WPT) : "memory");
-                } else if constexpr ((t + 1) % BAR == 0) {
-                    asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"i"(G::INFLIGHT * WPT) : "memory");
-                }
-            }
-        });
-    };
-    run_layer(0, IC<ROLE_IN>{}, IC<1>{}, IC<0>{});
-    sm_stamp(p, 2);
-    for (int layer = 1; layer < L; layer += 2) {
-        run_layer(layer, IC<ROLE_ODD>{}, IC<2>{}, IC<3>{});
-        sm_stamp(p, 2 + layer);
-        run_layer(layer + 1, IC<ROLE_EVEN>{}, IC<2>{}, IC<0>{});
-        sm_stamp(p, 3 + layer);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // the ring's trailing reloads landed
-    __syncthreads();
-
-    // the fp32 stream to LDS (over the two images), adaptive average pool to P x P cells (torch
-    // adaptive_avg_pool2d bins, y-major sums), then the policy / value 1x1 convs (BN folded,
-    // k-ordered fp32 FMA chain + bias, ReLU); the 1x1 weights staged transposed ([c][o]) in the ring
-    uint8_t* xs = lds;
-    static_for<0, FPW>([&](auto ic) {
-        constexpr int i = decltype(ic)::value;
-        const int q = 16 * (wp + 4 * i) + l16, y = q / WG, x = q - y * WG;
-        if (y < HB && x < HB)
-            static_for<0, JN>([&](auto jc) {
-                constexpr int j = decltype(jc)::value;
-                *reinterpret_cast<f32x4v*>(xs + xs_off(y * HB + x, (16 * (J0 + j) + 4 * lg) >> 2)) = xr[i][j];
-            });
-    });
-    const int P = p.P, PP = P * P, HC = p.HC;
-    constexpr int HO = SF;                               // 2 * HC head outputs
-    float* pooled = reinterpret_cast<float*>(lds + G::OW);   // [64 c][64 cells] (cells >= PP zero)
-    float* wt = pooled + SF * 64;                        // [64 c][HO o] (policy outputs, then value)
-#pragma unroll
-    for (int k = 0; k < HWT; ++k) wt[tid + NT * k] = wpre[k];   // [c][o]: consecutive lanes, consecutive o
-    for (int i = tid; i < SF * (64 - PP); i += NT) {
-        const int c = i / (64 - PP), cell = PP + (i - c * (64 - PP));
-        pooled[c * 64 + cell] = 0.0f;
-    }
-    __syncthreads();
-    sm_stamp(p, 40);
-    if (P == 8) pool_cells<HB, 8, NT>(xs, pooled, tid);
-    else pool_cells<HB, 0, NT>(xs, pooled, tid, P);
-    __syncthreads();
-    sm_stamp(p, 41);
-    // head 1x1 convs on the f32 MFMA (v_mfma_f32_16x16x4_f32: an exact k-ordered fmaf chain, as
-    // gemm_f32): D[o][cell] = sum_c W[o][c] pooled[cell][c]; wave w: cells 16 (w & 3) .., outputs 16 (J0 + j) ..
-    {
-        const int cell = 16 * wp + l16;
-        f32x4v hacc[JN] = {};
-#pragma unroll 4
-        for (int kb = 0; kb < SF / 4; ++kb) {
-            const int c = 4 * kb + lg;
-            const float bv = pooled[c * 64 + cell];
-#pragma unroll
-            for (int j = 0; j < JN; ++j)
-                hacc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(wt[c * HO + 16 * (J0 + j) + l16], bv, hacc[j], 0, 0, 0);
-        }
-        if (cell < PP) {
-#pragma unroll
-            for (int j = 0; j < JN; ++j) {
-                const int o = 16 * (J0 + j) + 4 * lg;   // 4 consecutive outputs, all policy or all value
-                const bool pol = o < HC;
-                const int oc = pol ? o : o - HC;
-                const float* bias = (pol ? p.bpc : p.bvc) + oc;
-                f32x4v v;
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    const float t = hacc[j][e] + bias[e];
-                    v[e] = t > 0.0f ? t : 0.0f;
-                }
-                *reinterpret_cast<f32x4v*>((pol ? p.pp : p.vp) + ((size_t)b * PP + cell) * HC + oc) = v;
-            }
-        }
-    }
-    sm_stamp(p, 42);
-}
 
 namespace {
 // k_smallnet_g: k_smallnet with the weights streamed from L1 / L2 straight into registers instead of
@@ -1112,34 +817,12 @@ int az_smallnet_max_blocks() { return (SmGeom<15>::MAXL - 1) / 2; }
 
 int az_smallnet_launch(const SmallNetArgs& a, int B, hipStream_t st) {
     if (!az_smallnet_supported(a.H, SF, 16, a.P, a.HC)) return -1;
-#ifdef AZ_SM_DIAG
-    switch (a.stamps) {
-        case 2: hipLaunchKernelGGL((k_smallnet_r2<15, 1>), dim3(B), dim3(256), 0, st, a); return 0;
-        case 3: hipLaunchKernelGGL((k_smallnet_r2<15, 2>), dim3(B), dim3(256), 0, st, a); return 0;
-        case 4: hipLaunchKernelGGL((k_smallnet_r2<15, 3>), dim3(B), dim3(256), 0, st, a); return 0;
-        case 5: hipLaunchKernelGGL((k_smallnet_r2<15, 4>), dim3(B), dim3(256), 0, st, a); return 0;
-        case 6: hipLaunchKernelGGL((k_smallnet_r2<15, 5>), dim3(B), dim3(256), 0, st, a); return 0;
-        case 7: hipLaunchKernelGGL((k_smallnet_r2<15, 12>), dim3(B), dim3(256), 0, st, a); return 0;
-        case 8: hipLaunchKernelGGL((k_smallnet_r2<15, 8>), dim3(B), dim3(256), 0, st, a); return 0;
-        default: break;
-    }
-#endif
-    if (g_sm_kernel == 1) {
-        if (g_sm_waves == 4) hipLaunchKernelGGL((k_smallnet_r2<15, 0, 4>), dim3(B), dim3(256), 0, st, a);
-        else hipLaunchKernelGGL((k_smallnet_r2<15, 0, 8>), dim3(B), dim3(512), 0, st, a);
+    if (g_sm_kernel == 1) {                              // A/B only: the round-2 kernel
+        if (g_sm_waves == 4) hipLaunchKernelGGL((k_smallnet_r2<15, 4>), dim3(B), dim3(256), 0, st, a);
+        else hipLaunchKernelGGL((k_smallnet_r2<15, 8>), dim3(B), dim3(512), 0, st, a);
         return 0;
     }
-    if (g_sm_kernel == 0) {                              // default: weights streamed into registers
-        if (a.residual) hipLaunchKernelGGL((k_smallnet_g<15, 8, true>), dim3(B), dim3(512), 0, st, a);
-        else hipLaunchKernelGGL((k_smallnet_g<15, 8, false>), dim3(B), dim3(512), 0, st, a);
-        return 0;
-    }
-    if (g_sm_waves == 4) {
-        if (a.residual) hipLaunchKernelGGL((k_smallnet<15, 4, true>), dim3(B), dim3(256), 0, st, a);
-        else hipLaunchKernelGGL((k_smallnet<15, 4, false>), dim3(B), dim3(256), 0, st, a);
-    } else {
-        if (a.residual) hipLaunchKernelGGL((k_smallnet<15, 8, true>), dim3(B), dim3(512), 0, st, a);
-        else hipLaunchKernelGGL((k_smallnet<15, 8, false>), dim3(B), dim3(512), 0, st, a);
-    }
+    if (a.residual) hipLaunchKernelGGL((k_smallnet_g<15, 8, true>), dim3(B), dim3(512), 0, st, a);
+    else hipLaunchKernelGGL((k_smallnet_g<15, 8, false>), dim3(B), dim3(512), 0, st, a);
     return 0;
 }

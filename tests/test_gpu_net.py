@@ -322,9 +322,10 @@ def test_gpu_trunk_kernel_name(engine, case):
 @pytest.mark.parametrize("residual", [1, 0])
 @pytest.mark.parametrize("B", [256, 37])
 def test_gpu_smallnet_matches_round2_kernel(engine, residual, B):
-    """k_smallnet (round 3: offset-addressed fragments, 6-slot ring, layer pairs, med3 epilogue) runs
-    the round-2 kernel's arithmetic: the same MFMA sequence, residual stream and fp16 rounding, so
-    both kernels (and both wave shapes) give bitwise equal outputs on C2-shape nets."""
+    """k_smallnet_g (round 3: offset-addressed activation fragments, weights streamed into registers,
+    layer pairs, med3 epilogue) runs the round-2 kernel's arithmetic: the same MFMA sequence,
+    residual stream and fp16 rounding, so both kernels (and both of the round-2 kernel's wave
+    shapes) give bitwise equal outputs on C2-shape nets."""
     import az_amd
     from az_amd import _lib
     d = az_amd.NetDesc(15, 11, 64, 6, 225, 32, 8, 256, residual, 0, az_amd.AZ_PREC_FP16, 256)
@@ -333,7 +334,7 @@ def test_gpu_smallnet_matches_round2_kernel(engine, residual, B):
     x = _rand_planes(B, 11, 15, 5 + B)
     outs = {}
     try:
-        for k, w in ((1, 8), (0, 8), (1, 4), (2, 8), (2, 4)):
+        for k, w in ((1, 8), (0, 8), (1, 4)):
             _lib.lib().az_diag_set_smallnet_kernel(k)
             _lib.lib().az_diag_set_smallnet_waves(w)
             outs[(k, w)] = net.forward(x)
