@@ -1644,7 +1644,6 @@ static void v6_launch(const ConvBf16Args& a, int mode, hipStream_t st) {
 }
 
 bool az_conv_v7_supported(const ConvBf16Args& a);
-bool az_conv_v8_applies(const ConvBf16Args& a);
 int az_conv_v7_launch(const ConvBf16Args& a, int mode, int geo15, hipStream_t st);
 
 // Which kernel az_conv_g8_launch takes for a layer (a.flags already set): 0 none (unsupported),
@@ -1711,8 +1710,7 @@ int az_conv_g8_name(const ConvBf16Args& a_in, int mode, char* out, int len) {
     int geo = 0;
     static const char* g7[3] = {"PAD", "SLIM", "DENSE"};
     switch (g8_choice(a, &geo)) {
-        case 1: snprintf(out, len, "conv3x3_v%d<%d, %d, %s>", az_conv_v8_applies(a) ? 8 : 7, mode, a.H, g7[a.H == 15 ? geo : 2]);
-            return 0;
+        case 1: snprintf(out, len, "conv3x3_v7<%d, %d, %s>", mode, a.H, g7[a.H == 15 ? geo : 2]); return 0;
         case 2: snprintf(out, len, "conv3x3_v6<%d, %d%s>", mode, a.H, geo ? ", DENSE" : ""); return 0;
         case 3: snprintf(out, len, "conv3x3_v5<%d, 8>", mode); return 0;
         default: return -1;

@@ -402,310 +402,6 @@ __global__ __launch_bounds__(256, 2) void conv3x3_v7(ConvBf16Args p) {
     }
 }
 
-// conv3x3_v8: the v7 tile widened to every output channel.  A 256-thread block (4 waves) owns a
-// 256-row output tile x 256 channels; a wave 128 rows x 128 channels (32 accumulator tiles of
-// 16 x 16, 256 registers, one wave per SIMD, one block per CU with 104 KB of LDS: the halo of a
-// 32-channel chunk double-buffered, 2 x 20 KB, and a 7-slot ring of per-tap weight tiles, 7 x 16 KB).
-// Against v7 (wave tile 128 x 64, two blocks per CU, each channel half of a tile in its own block):
-//  * a tap reads 16 fragments for 64 MFMAs (v7: 12 for 32): a third fewer LDS bytes per MFMA --
-//    the chip runs the trunk at its power cap, so energy per MFMA is the lever (v7x3, whose tap is
-//    24 fragments for 96 MFMAs, issues 49.7 % of the MFMA peak against v7's 44 %);
-//  * each tile's halo is fetched once (v7: once per channel half, 1.23x the algorithmic HBM bytes);
-//  * with one wave per SIMD nothing hides the issue cost of the LDS-DMA pieces and fragment reads
-//    (MI355X_MICROARCH.md: an LDS-DMA piece costs the issuing wave 60 cycles among bare MFMAs, 100+
-//    in a burst), so every one is threaded between the tap's MFMAs: the DMA pieces and the next
-//    tap's weight reads between the low half's 32, the next tap's activation reads between the
-//    high half's; the weights of a tap are fetched five taps ahead.
-// Same products, same accumulation order (chunk-major, tap-minor, the MFMA's internal K order):
-// bit-identical to conv3x3_v7 / v6.  Requires N % 256 == 0 (otherwise v7 runs).
-template <int N, typename F>
-__device__ __forceinline__ void lgkm12(F (&x)[8], F (&y)[4]) {
-    asm volatile("s_waitcnt lgkmcnt(%12)" : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(x[4]), "+v"(x[5]),
-                 "+v"(x[6]), "+v"(x[7]), "+v"(y[0]), "+v"(y[1]), "+v"(y[2]), "+v"(y[3]) : "i"(N) : "memory");
-}
-
-template <int MODE, int HB, int GEO>
-__global__ __launch_bounds__(256, 1) void conv3x3_v8(ConvBf16Args p) {
-    typedef H16<MODE> H;
-    typedef Geom7<HB, GEO> GM;
-    constexpr bool DENSE = GM::DENSE, SLIM = GM::SLIM;
-    typedef typename std::conditional<MODE == 2, f16x8, bf16x8>::type frag;
-    constexpr int BNT = 256, WG = GM::WG, HW = GM::HW, HROWS = GM::HROWS;
-    constexpr int A_BUF = 4 * HROWS * 16;                 // one chunk: [4 groups][320 rows][16 B] = 20 KB
-    constexpr int B_TAP = 4 * BNT * 16;                   // one tap: [4 groups][256 ch][16 B] = 16 KB
-    constexpr int NSLOT = 7;                              // weight ring: slot of tap s = s % 7
-    constexpr int LDS = 2 * A_BUF + NSLOT * B_TAP;        // 152 KB
-    __shared__ __attribute__((aligned(16))) uint8_t lds[LDS];
-
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int wm = wave >> 1, wn = wave & 1;             // 128 pixels x 128 channels per wave
-    const int nsplit = p.N / BNT;
-    const int nb = blockIdx.x % nsplit, tile = blockIdx.x / nsplit;
-    const int n0 = nb * BNT;
-    const int nboards = p.m_limit ? *p.m_limit : p.M / HW;
-    if (DENSE ? tile * 256 >= nboards * HW : tile >= nboards) return;
-    const int C = p.C, GI = C / 8, GO = p.N / 8;
-    const int NCH = C / 32, NS = 9 * NCH;
-
-    const uint32_t a_bytes = (uint32_t)p.a_tail, b_bytes = (uint32_t)((size_t)9 * C * p.N * 2);
-    const __amdgpu_buffer_rsrc_t rsA =
-        __builtin_amdgcn_make_buffer_rsrc((void*)p.Ahi, (short)0, (int)(a_bytes + AZ_ACT_TAIL * 2), 0x00020000);
-    const __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc((void*)p.Bblk, (short)0, (int)b_bytes, 0x00020000);
-    const uint32_t PAD = a_bytes;                         // zeroed tail: padding rows
-
-    auto a_src = [&](int j, int ln) -> uint32_t {         // as conv3x3_v7: halo piece j of this wave
-        const int q = wave + 4 * j, rb = q % 5, g = q / 5;
-        const int hr = rb * 64 + ln;
-        int Y, X, b;
-        bool in;
-        if constexpr (DENSE) {
-            const int gpx = tile * 256 - (HB + 1) + hr;
-            b = gpx >= 0 ? gpx / HW : -1;
-            const int pix = gpx - b * HW;
-            Y = pix / HB + 1; X = pix - (Y - 1) * HB + 1;
-            in = hr < GM::TROWS && gpx >= 0;
-        } else {
-            Y = hr / WG; X = hr - Y * WG;
-            b = tile;
-            in = hr < GM::TROWS;
-        }
-        const bool ok = in && Y >= 1 && Y <= HB && X >= 1 && X <= HB && b < nboards;
-        return ok ? (uint32_t)((((size_t)b * GI + g) * HW + (Y - 1) * HB + (X - 1)) * 16) : PAD;
-    };
-    // weight pieces: q = wave + 4j (j < 4) -> (group g = q / 4, 64-channel block rb = q % 4)
-    int b_src[4], b_dst[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const int q = wave + 4 * j, rb = q & 3, g = q >> 2;
-        b_src[j] = (((g >> 1) * 18 + (g & 1)) * p.N + n0 + rb * 64) * 16;
-        b_dst[j] = g * (BNT * 16) + rb * 1024;
-    }
-    const uint32_t lane16 = lane * 16;
-    uint8_t* abuf = lds;
-    uint8_t* bbuf = lds + 2 * A_BUF;
-    auto issueA = [&](int j, int c, int buf) {            // piece j of chunk c's halo into A buffer `buf`
-        const int q = wave + 4 * j, rb = q % 5, g = q / 5;
-        int ln = lane;
-        asm volatile("" : "+v"(ln));
-        const uint32_t vo = a_src(j, ln);
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (lds_void_t*)(abuf + buf * A_BUF + g * (HROWS * 16) + rb * 1024),
-                                                 16, (int)vo, __builtin_amdgcn_readfirstlane(c * (4 * HW * 16)), 0, 0);
-    };
-    auto issueB = [&](int s, int slot, int j) {           // the wave's piece j (< 4) of tap s's weights
-        const int c = s / 9, t = s - 9 * c;
-        const int so = __builtin_amdgcn_readfirstlane((36 * c + 2 * t) * p.N * 16);
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, (lds_void_t*)(bbuf + slot * B_TAP + b_dst[j]), 16,
-                                                 (int)lane16, so + b_src[j], 0, 0);
-    };
-
-    f32x4v acc[8][8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {                         // the bias seeds the accumulators
-        const float4 bv = *reinterpret_cast<const float4*>(p.bias + n0 + wn * 128 + j * 16 + 4 * (lane >> 4));
-#pragma unroll
-        for (int i = 0; i < 8; ++i) acc[i][j] = f32x4v{bv.x, bv.y, bv.z, bv.w};
-    }
-    // The 256 accumulator registers fill the AGPR file: with the builtin the allocator renames the
-    // accumulators at every MFMA and carries half of them through VGPRs (copies, s_nop stalls,
-    // scratch spills), so the MFMAs are issued as inline asm with the accumulator tied in place.
-    // The hazards the compiler no longer sees are covered by hand: s_nop after the accumulator
-    // writes of the bias seed and the VALU writes of the edge mask, and before the epilogue reads.
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) asm volatile("" : "+a"(acc[i][j]));
-    asm volatile("s_nop 7\n s_nop 7\n s_nop 7" ::: "memory");
-
-    const int l16 = lane & 15, lg = lane >> 4;
-    const uint32_t a_lane = lds_addr(abuf) + lg * (HROWS * 16) + (wm * 128 + l16) * 16;
-    const uint32_t b_lane = lds_addr(bbuf) + lg * (BNT * 16) + (wn * 128 + l16) * 16;
-    uint32_t mbits = 0;                                   // DENSE: board-edge bits of the lane's 8 pixels
-    if constexpr (DENSE) {
-#pragma unroll
-        for (int f = 0; f < 8; ++f) {
-            const int gq = tile * 256 + wm * 128 + f * 16 + l16;
-            const int pix = gq % HW, y = pix / HB, x = pix - y * HB;
-            mbits |= ((x == 0 ? 1u : 0u) | (x == HB - 1 ? 2u : 0u) | (y == 0 ? 4u : 0u) | (y == HB - 1 ? 8u : 0u)) << (4 * f);
-        }
-    }
-
-    // prologue: halo of chunk 0, weights of taps 0..5
-#pragma unroll
-    for (int j = 0; j < 5; ++j) issueA(j, 0, 0);
-#pragma unroll
-    for (int s = 0; s < 6; ++s)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) issueB(s, s, j);
-    wait_vm(20);                                          // A(0), B(0) landed; B(1..5) may fly
-    __builtin_amdgcn_s_barrier();
-
-    frag a[2][2][4], bw[2][8];                            // fragment registers, double-buffered by tap parity
-    auto maskA = [&](frag (&x)[4], int half, int dy, int dx) {
-        if constexpr (DENSE) {
-            const uint32_t test = (dy == 0 ? 4u : dy == 2 ? 8u : 0u) | (dx == 0 ? 1u : dx == 2 ? 2u : 0u);
-            if (test) {
-#pragma unroll
-                for (int i = 0; i < 4; ++i)
-                    if (mbits & (test << (4 * (half * 4 + i)))) x[i] = frag{};
-#pragma unroll
-                for (int i = 0; i < 4; ++i) asm volatile("" : "+v"(x[i]));
-                asm volatile("s_nop 4" ::: "memory");
-            }
-        }
-    };
-    const uint32_t z16 = (SLIM && wm == 1) ? 16 * 16 : 0;  // SLIM: 16th fragment reads all-zero halo rows
-    auto loadA = [&](frag (&x)[4], uint32_t ab, auto tc, auto hc) {
-        constexpr int t = decltype(tc)::value, half = decltype(hc)::value;
-        constexpr int sh = (t / 3) * WG + (t % 3);
-        static_for<0, 4>([&](auto ic) {
-            constexpr int i = decltype(ic)::value;
-            if constexpr (SLIM && half == 1 && i == 3) ds_rd<((half * 4 + i) * 16 + sh) * 16>(x[i], ab + z16);
-            else ds_rd<((half * 4 + i) * 16 + sh) * 16>(x[i], ab);
-        });
-    };
-    auto loadB = [&](frag (&x)[8], uint32_t bs) {
-        static_for<0, 8>([&](auto jc) {
-            constexpr int j = decltype(jc)::value;
-            ds_rd<j * 256>(x[j], bs);
-        });
-    };
-    auto mma1 = [&](const frag& x, const frag& b, f32x4v& d) {
-        if constexpr (MODE == 2) asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, %0" : "+a"(d) : "v"(b), "v"(x));
-        else asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(d) : "v"(b), "v"(x));
-    };
-    using I0 = std::integral_constant<int, 0>;
-    using I1 = std::integral_constant<int, 1>;
-    // tap 0 of chunk 0 (the loop's waits count these 16 reads as a tap's)
-    loadB(bw[0], b_lane);
-    loadA(a[0][0], a_lane, I0{}, I0{});
-    loadA(a[0][1], a_lane, I0{}, I1{});
-
-    // Two chunks per iteration: 18 taps, the register sets alternate by tap parity.  At tap s the
-    // barrier certifies the weights of tap s+1 (and at t == 8 the next chunk's halo); the wave then
-    // issues a halo piece of the next chunk (t < 5, into the buffer chunk c-1 used, last read at its
-    // tap 7) and the weights of tap s+6 into the slot of tap s-1 (read during tap s-2, before every
-    // wave's barrier s).  Past the end the pieces are harmless reloads into free buffers, so the vmcnt
-    // budget is a compile-time function of t: after the weights of tap s+1 (issued at tap s-5) come
-    // the pieces of taps s-4 .. s-1 -- 16 weight pieces and a halo piece per tap with t < 5 -- and at
-    // t == 8 the halo's last piece (issued at t = 4) is followed by exactly 16.  LDS reads of a tap,
-    // in order: weights of tap s+1 (8), activations of tap s+1 low half (4), high half (4).
-    for (int c2 = 0; c2 < NCH; c2 += 2) {
-        static_for<0, 18>([&](auto tc18) {
-            constexpr int T = decltype(tc18)::value;
-            constexpr int t = T % 9, cur = T & 1, nxt = cur ^ 1;
-            constexpr int nA = ((t + 8) % 9 < 5) + ((t + 7) % 9 < 5) + ((t + 6) % 9 < 5) + ((t + 5) % 9 < 5);
-            constexpr int allow = t == 8 ? 16 : 16 + nA;
-            constexpr int tn = (t + 1) % 9;
-            using TN = std::integral_constant<int, tn>;
-            const int c = c2 + T / 9;
-            const int s = 9 * c + t;
-            const int sl1 = (s + 1) % NSLOT, sl6 = (s + 6) % NSLOT;
-            if constexpr (DENSE) asm volatile("" : "+v"(mbits));
-            wait_vm(allow);
-            __builtin_amdgcn_s_barrier();
-            const uint32_t bn = b_lane + sl1 * B_TAP;
-            const int cn = c + 1 < NCH ? c + 1 : c, sb = s + 6 < NS ? s + 6 : NS - 1;
-            lgkm12<4>(bw[cur], a[cur][0]);                // younger: this tap's high half (4)
-            maskA(a[cur][0], 0, t / 3, t % 3);
-            // low half: after MFMA 2n+1 the n-th of [halo piece (t < 5)], R0 B0 R1 B1 R2 B2 R3 B3 R4 .. R7
-            // (Rj: ds_read of the next tap's weight fragment j, Bj: LDS-DMA weight piece j of tap s+6)
-            static_for<0, 32>([&](auto kc) {
-                constexpr int k = decltype(kc)::value;
-                mma1(a[cur][0][k / 8], bw[cur][k % 8], acc[k / 8][k % 8]);
-                if constexpr (k % 2 == 1) {
-                    constexpr int m = k / 2 - (t < 5 ? 1 : 0);
-                    if constexpr (m == -1) issueA(t, cn, (c + 1) & 1);
-                    else if constexpr (m >= 0 && m < 8 && m % 2 == 0) ds_rd<(m / 2) * 256>(bw[nxt][m / 2], bn);
-                    else if constexpr (m >= 0 && m < 8) issueB(sb, sl6, m / 2);
-                    else if constexpr (m >= 8 && m < 12) ds_rd<(m - 4) * 256>(bw[nxt][m - 4], bn);
-                }
-            });
-            const uint32_t an = a_lane + ((t == 8 ? c + 1 : c) & 1) * A_BUF;
-            lgkm<8>(a[cur][1]);                           // younger: the next tap's weights (8)
-            maskA(a[cur][1], 1, t / 3, t % 3);
-            // high half: after MFMA 3n+2 the n-th activation read of the next tap (low half, high half)
-            static_for<0, 32>([&](auto kc) {
-                constexpr int k = decltype(kc)::value;
-                mma1(a[cur][1][k / 8], bw[cur][k % 8], acc[4 + k / 8][k % 8]);
-                if constexpr (k % 3 == 2 && k / 3 < 8) {
-                    constexpr int n = k / 3, hh = n / 4, ii = n % 4;
-                    constexpr int sh = (tn / 3) * WG + (tn % 3);
-                    constexpr int off = ((hh * 4 + ii) * 16 + sh) * 16;
-                    if constexpr (SLIM && hh == 1 && ii == 3) ds_rd<off>(a[nxt][hh][ii], an + z16);
-                    else ds_rd<off>(a[nxt][hh][ii], an);
-                }
-            });
-        });
-    }
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n s_nop 7\n s_nop 7\n s_nop 7" ::: "memory");
-
-    // epilogue (as conv3x3_v7), straight from the accumulators: lane holds channels 4*(l >> 4) + e of
-    // pixel l16 of every 16 x 16 tile; residual join, ReLU, 16-bit + int8 split, streaming stores
-    const __amdgpu_buffer_rsrc_t rh = __builtin_amdgcn_make_buffer_rsrc((void*)p.Rhi, (short)0, 0x7fffffff, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rq = __builtin_amdgcn_make_buffer_rsrc((void*)p.Rq, (short)0, 0x7fffffff, 0x00020000);
-    const int chl = n0 + wn * 128 + 4 * lg;               // first channel of the lane in tile j = 0
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        const int q = wm * 128 + i * 16 + l16;            // output grid row of the tile
-        int b, pix;
-        bool live;
-        if constexpr (DENSE) {
-            const int gq = tile * 256 + q;
-            b = gq / HW;
-            pix = gq - b * HW;
-            live = b < nboards;
-        } else {
-            const int y = q / WG, x = q - y * WG;
-            b = tile;
-            pix = y * HB + x;
-            live = y < HB && x < HB;
-        }
-        if (!live) continue;
-        u32x2_t hv[8];
-        uint32_t qv[8];
-        if (p.Rhi) {
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const int ch = chl + j * 16;
-                const size_t e = (((size_t)b * GO + (ch >> 3)) * HW + pix) * 8 + (ch & 7);
-                hv[j] = __builtin_amdgcn_raw_buffer_load_b64(rh, (int)(e * 2), 0, 2);
-                qv[j] = __builtin_amdgcn_raw_buffer_load_b32(rq, (int)e, 0, 2);
-            }
-        }
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const int ch = chl + j * 16;
-            const size_t e = (((size_t)b * GO + (ch >> 3)) * HW + pix) * 8 + (ch & 7);
-            float o[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-            if (p.Rhi) {
-                uint16_t hh[4];
-                int8_t qq[4];
-                __builtin_memcpy(hh, &hv[j], 8);
-                __builtin_memcpy(qq, &qv[j], 4);
-#pragma unroll
-                for (int k = 0; k < 4; ++k) o[k] += H::join(hh[k], qq[k]);
-            }
-            uint16_t oh[4];
-            int8_t oq[4];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                o[k] = __builtin_amdgcn_fmed3f(o[k], 0.0f, 3.0e38f);   // ReLU
-                if (p.Cq) H::split(o[k], oh[k], oq[k]);
-                else oh[k] = H::from_f(o[k]);
-            }
-            u32x2_t hs;
-            __builtin_memcpy(&hs, oh, 8);
-            asm volatile("global_store_dwordx2 %0, %1, off nt" ::"v"(p.Chi + e), "v"(hs) : "memory");
-            if (p.Cq) {
-                uint32_t qs;
-                __builtin_memcpy(&qs, oq, 4);
-                asm volatile("global_store_dword %0, %1, off nt" ::"v"(p.Cq + e), "v"(qs) : "memory");
-            }
-        }
-    }
-}
-
 // conv3x3_v7x3: the fp32-faithful trunk conv (AZ_PREC_BF16X3) on the v7 tile.
 //
 // Every fp32 operand x is carried as two bf16 planes, hi = bf16(x) and lo = bf16(x - hi), each
@@ -1063,33 +759,8 @@ int az_conv_v7x3_launch(const ConvBf16Args& a, hipStream_t st) {
 }
 
 // geo15: the 15x15 tile geometry (GEO_PAD / GEO_SLIM / GEO_DENSE); other boards are DENSE
-template <int HB, int GEO>
-static void v8_launch_g(const ConvBf16Args& a, int mode, hipStream_t st) {
-    const int boards = a.M / (HB * HB);
-    const int tiles = GEO == GEO_DENSE ? (boards * HB * HB + 255) / 256 : boards;
-    const int grid = tiles * (a.N / 256);
-    if (mode == 2) hipLaunchKernelGGL((conv3x3_v8<2, HB, GEO>), dim3(grid), dim3(256), 0, st, a);
-    else hipLaunchKernelGGL((conv3x3_v8<1, HB, GEO>), dim3(grid), dim3(256), 0, st, a);
-}
-
-// conv3x3_v8 takes the v7 layers whose N is a multiple of 256 (flag 0x20000: v7, A/B measurement)
-bool az_conv_v8_applies(const ConvBf16Args& a) { return a.N % 256 == 0 && !(a.flags & 0x20000); }
-
 int az_conv_v7_launch(const ConvBf16Args& a, int mode, int geo15, hipStream_t st) {
     if (!az_conv_v7_supported(a)) return -1;
-    if (az_conv_v8_applies(a)) {
-        switch (a.H) {
-            case 8: v8_launch_g<8, GEO_DENSE>(a, mode, st); return 0;
-            case 9: v8_launch_g<9, GEO_DENSE>(a, mode, st); return 0;
-            case 13: v8_launch_g<13, GEO_DENSE>(a, mode, st); return 0;
-            case 19: v8_launch_g<19, GEO_DENSE>(a, mode, st); return 0;
-            default:
-                if (geo15 == GEO_DENSE) v8_launch_g<15, GEO_DENSE>(a, mode, st);
-                else if (geo15 == GEO_PAD) v8_launch_g<15, GEO_PAD>(a, mode, st);
-                else v8_launch_g<15, GEO_SLIM>(a, mode, st);
-                return 0;
-        }
-    }
     switch (a.H) {
         case 8: v7_launch_g<8, GEO_DENSE>(a, mode, st); return 0;
         case 9: v7_launch_g<9, GEO_DENSE>(a, mode, st); return 0;

@@ -1,6 +1,5 @@
-"""conv3x3_v8 / conv3x3_v7 (csrc/conv_v7.hip: v7 = two 256-thread blocks per CU, swapped MFMA operands,
-epilogue from registers; v8 = the same tile over all 256 channels in one block, one wave per SIMD; the
-defaults for batches of >= 1024 boards on 15x15, v8 wherever N % 256 == 0) against conv3x3_v6 (csrc/conv_bf16.hip): same products in the same accumulation order,
+"""conv3x3_v7 (csrc/conv_v7.hip: two 256-thread blocks per CU, swapped MFMA operands, epilogue from
+registers; the default for batches of >= 1024 boards on 15x15) against conv3x3_v6 (csrc/conv_bf16.hip): same products in the same accumulation order,
 so every output of the whole network must be BITWISE equal -- on the SLIM and padded 15x15 tiles, on DENSE
 tiles of every board, for ragged batches and in both 16-bit modes.  Both kernels are also pinned to
 the fp32 reference by tests/test_gpu_net.py (v7 is the default kernel there)."""
@@ -28,10 +27,7 @@ CASES = [  # board, in_planes, actions, channels, blocks, B, flags selecting v7 
     (19, 8, 362, 256, 2, 13, 0x804),      # DENSE 19x19 (Go)
     (9, 11, 81, 128, 2, 29, 0x804),       # DENSE 9x9
     (13, 8, 170, 256, 1, 7, 0x804),       # DENSE 13x13
-    (8, 111, 4672, 256, 2, 33, 0x804),    # DENSE 8x8 chess: the 128-channel input conv runs on v8 too
-    (15, 11, 225, 256, 2, 37, 0x20a04),   # v7 on N = 256 (flag 0x20000 keeps those layers off v8)
-    (15, 11, 225, 256, 2, 37, 0x20a0c),   # v7 DENSE 15x15
-    (19, 8, 362, 256, 2, 13, 0x20804),    # v7 DENSE 19x19
+    (8, 111, 4672, 256, 2, 33, 0x804),    # DENSE 8x8 chess: the 128-channel input conv runs on v7 too
 ]
 
 
