@@ -226,7 +226,7 @@ def run_rank(a, rank, world, dist, make_workload, coll_device):
     wl.sync()
     elapsed = time.perf_counter() - t0
     barrier()
-    trunk_ms, launches, _ = net.profile_read()
+    trunk_ms, launches, forwards = net.profile_read()
     tree = wl.mcts.profile_read()
     kernel = net.trunk_kernel()      # the kernel the library dispatches for this net (engine's own choice)
     if hasattr(wl, "close"):
@@ -271,7 +271,10 @@ def run_rank(a, rank, world, dist, make_workload, coll_device):
                      "bound": "mfma",
                      "achieved": achieved, "peak": peak, "unit": "TFLOP/s", "frac": achieved / peak, "traffic": None,
                      "launches": launches, "avg_launch_ms": per_launch_ms, "boards_per_launch": boards_per_launch,
-                     "flops_per_launch": per_launch_flops},
+                     "flops_per_launch": per_launch_flops,
+                     # launches are trunk-conv equivalents (2 x blocks per forward); a fused forward (k_smallnet)
+                     # is one kernel launch per forward, whose rocprofv3 average is avg_forward_ms
+                     "forwards": forwards, "avg_forward_ms": trunk_ms / max(1, forwards)},
     }
     steps = max(1, tree["sim_steps"])
     out["tree_kernels"] = {
