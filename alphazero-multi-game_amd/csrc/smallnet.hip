@@ -503,6 +503,43 @@ enum { ROLE_IN = 0, ROLE_ODD = 1, ROLE_EVEN = 2 };
 // bins become constants) or 0 (runtime P); bins of at most 3 x 3 issue every load before the sums.
 template <int HB, int PC, int NT>
 __device__ __forceinline__ void pool_cells(const uint8_t* xs, float* pooled, int tid, int Prt = 0) {
+    if constexpr (PC > 0 && (HB + PC - 1) / PC + 1 <= 3) {
+        // compile-time bins of at most 3 x 3: the loads of all the thread's items are issued before
+        // any sum or store (the stores to pooled would otherwise fence the next item's loads)
+        constexpr int PP = PC * PC, NI = (PP * (SF / 4) + NT - 1) / NT;
+        f32x4v v[NI][3][3];
+#pragma unroll
+        for (int k = 0; k < NI; ++k) {
+            const int i = tid + NT * k, ii = i < PP * (SF / 4) ? i : 0;
+            const int c4 = ii / PP, cell = ii - c4 * PP, oy = cell / PC, ox = cell - oy * PC;
+            const int y0 = (oy * HB) / PC, xa = (ox * HB) / PC;
+#pragma unroll
+            for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+                for (int dx = 0; dx < 3; ++dx) {
+                    const int y = min(y0 + dy, HB - 1), x = min(xa + dx, HB - 1);
+                    v[k][dy][dx] = *reinterpret_cast<const f32x4v*>(xs + xs_off(y * HB + x, c4));
+                }
+        }
+#pragma unroll
+        for (int k = 0; k < NI; ++k) {
+            const int i = tid + NT * k;
+            if (i >= PP * (SF / 4)) break;
+            const int c4 = i / PP, cell = i - c4 * PP, oy = cell / PC, ox = cell - oy * PC;
+            const int y0 = (oy * HB) / PC, y1 = ((oy + 1) * HB + PC - 1) / PC;
+            const int xa = (ox * HB) / PC, xb = ((ox + 1) * HB + PC - 1) / PC;
+            f32x4v sum = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+            for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+                for (int dx = 0; dx < 3; ++dx)
+                    if (y0 + dy < y1 && xa + dx < xb) sum += v[k][dy][dx];
+            const float cnt = (float)((y1 - y0) * (xb - xa));
+#pragma unroll
+            for (int e = 0; e < 4; ++e) pooled[(4 * c4 + e) * 64 + cell] = sum[e] / cnt;
+        }
+        return;
+    }
     const int P = PC ? PC : Prt, PP = P * P;
     for (int i = tid; i < PP * (SF / 4); i += NT) {
         const int c4 = i / PP, cell = i - c4 * PP, oy = cell / P, ox = cell - oy * P;
@@ -750,7 +787,9 @@ __global__ __launch_bounds__(64 * NW, 1) void k_smallnet_g(SmallNetArgs p) {
         sm_stamp(p, 3 + layer);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // the ring's trailing (clamped) loads
+    sm_stamp(p, 54);
     __syncthreads();
+    sm_stamp(p, 55);
 
     uint8_t* xs = lds;
     static_for<0, FPW>([&](auto ic) {
@@ -764,6 +803,16 @@ __global__ __launch_bounds__(64 * NW, 1) void k_smallnet_g(SmallNetArgs p) {
     });
     const int P = p.P, PP = P * P, HC = p.HC;
     constexpr int HO = SF;
+    // the head biases (global loads) in flight during the staging and the pool
+    const int cell = 16 * wp + l16;
+    f32x4v hbias[JN];
+#pragma unroll
+    for (int j = 0; j < JN; ++j) {
+        const int o = 16 * (J0 + j) + 4 * lg;
+        const float* bias = o < HC ? p.bpc + o : p.bvc + (o - HC);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) hbias[j][e] = bias[e];
+    }
     float* pooled = reinterpret_cast<float*>(lds + H::OS);
     float* wt = pooled + SF * 64;
 #pragma unroll
@@ -772,34 +821,40 @@ __global__ __launch_bounds__(64 * NW, 1) void k_smallnet_g(SmallNetArgs p) {
         const int c = i / (64 - PP), cell = PP + (i - c * (64 - PP));
         pooled[c * 64 + cell] = 0.0f;
     }
+    sm_stamp(p, 56);
     __syncthreads();
     sm_stamp(p, 40);
     if (P == 8) pool_cells<HB, 8, NT>(xs, pooled, tid);
     else pool_cells<HB, 0, NT>(xs, pooled, tid, P);
+    sm_stamp(p, 57);
     __syncthreads();
     sm_stamp(p, 41);
     {
-        const int cell = 16 * wp + l16;
+        // every operand read before the first MFMA (one LDS round trip), then the k-ordered chain
         f32x4v hacc[JN] = {};
-#pragma unroll 4
+        float pv[SF / 4], wv[SF / 4][JN];
+#pragma unroll
         for (int kb = 0; kb < SF / 4; ++kb) {
             const int c = 4 * kb + lg;
-            const float bv = pooled[c * 64 + cell];
+            pv[kb] = pooled[c * 64 + cell];
 #pragma unroll
-            for (int j = 0; j < JN; ++j)
-                hacc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(wt[c * HO + 16 * (J0 + j) + l16], bv, hacc[j], 0, 0, 0);
+            for (int j = 0; j < JN; ++j) wv[kb][j] = wt[c * HO + 16 * (J0 + j) + l16];
         }
+#pragma unroll
+        for (int kb = 0; kb < SF / 4; ++kb)
+#pragma unroll
+            for (int j = 0; j < JN; ++j) hacc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(wv[kb][j], pv[kb], hacc[j], 0, 0, 0);
+        sm_stamp(p, 58);
         if (cell < PP) {
 #pragma unroll
             for (int j = 0; j < JN; ++j) {
                 const int o = 16 * (J0 + j) + 4 * lg;
                 const bool pol = o < HC;
                 const int oc = pol ? o : o - HC;
-                const float* bias = (pol ? p.bpc : p.bvc) + oc;
                 f32x4v v;
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
-                    const float t = hacc[j][e] + bias[e];
+                    const float t = hacc[j][e] + hbias[j][e];
                     v[e] = t > 0.0f ? t : 0.0f;
                 }
                 *reinterpret_cast<f32x4v*>((pol ? p.pp : p.vp) + ((size_t)b * PP + cell) * HC + oc) = v;

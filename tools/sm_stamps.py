@@ -32,6 +32,9 @@ _lib.lib().az_diag_smallnet_stamps(buf, 128)
 st = list(buf)
 t0 = st[0]
 names = {1: "prologue"} | {2 + i: f"layer {i}" for i in range(2 * blocks + 1)} | {40: "stream->LDS, wt", 41: "pool", 42: "head convs"}
+if os.environ.get("SM_TAIL"):    # the tail: ring drain, barrier, stream / weight staging, pool, head MFMAs
+    names = {2 * blocks + 2: f"layer {2 * blocks}", 54: "ring drained", 55: "barrier", 56: "stream + wt to LDS",
+             40: "barrier", 57: "pool", 41: "barrier", 58: "head MFMAs", 42: "head stores"}
 if os.environ.get("SM_INNER"):   # inside layer 5: from the end of layer 4, each tap's MFMAs issued, the epilogue
     names = {6: "layer 4 end"} | {43 + t: f"L5 tap {t} issued" for t in range(8)} | {52: "L5 tap 8 issued", 53: "L5 epilogue", 7: "L5 end"}
 prev, prevk = t0, 0
