@@ -498,6 +498,7 @@ int net_input_path(const az_net* n) {
 
 struct LeafRecs {                 // the search's leaf records: sample b = record gidx[b] (n records)
     const uint8_t* rec; const int* gidx; int go; int n;
+    int identity;                 // gidx[b] == b (the identity batch): the fused forward skips that load
 };
 
 // Router of a rand-wire node: relu(BN(conv1x1(concat(ins)))) as ONE GEMM over K = deg F whose
@@ -626,7 +627,7 @@ int net_forward(az_net* n, const float* x0, int B, const int* nb, float* logits,
         sa.x0 = x0; sa.m_limit = nb;
         if (lr) {
             if (lr->go) return az_fail(AZ_ERR_ARG, "smallnet: Gomoku leaf records only");
-            sa.x0 = nullptr; sa.rec = lr->rec; sa.gidx = lr->gidx; sa.rec_n = lr->n;
+            sa.x0 = nullptr; sa.rec = lr->rec; sa.gidx = lr->gidx; sa.rec_n = lr->n; sa.rec_identity = lr->identity;
         } sa.W = n->sm_W; sa.Wf = n->sm_Wf; sa.bias = n->sm_b;
         sa.Wpc = n->pconv.W; sa.bpc = n->pconv.b; sa.Wvc = n->vconv.W; sa.bvc = n->vconv.b;
         sa.pp = n->pp; sa.vp = n->vp;
@@ -970,7 +971,7 @@ int search_step(az_search* s, int mode, bool pre = false, bool fuse_next = false
         // the net's input stage builds the leaves' planes from their records (record eval_games[b])
         // where it can; otherwise a dense fp32 plane batch is built first
         const bool in_place = net_input_path(s->net) != NET_IN_GEMM;
-        const LeafRecs lr{tt.leafrec, tt.eval_games, tt.game == GAME_GO, G};
+        const LeafRecs lr{tt.leafrec, tt.eval_games, tt.game == GAME_GO, G, identity ? 1 : 0};
         if (!in_place) az_launch_rec_planes(tt.leafrec, s->d_batch, tt.eval_games, tt.n_eval, lr.go, tt.bs, G, st);
         const bool prof = s->net->prof;
         if (mode != MODE_SIM) s->net->prof = false;   // time only the simulation batches

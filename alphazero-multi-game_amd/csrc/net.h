@@ -53,6 +53,7 @@ struct SmallNetArgs {
     const uint8_t* rec;             // or: leaf records (leaf_planes.h, Gomoku), board b = record gidx[b]
     const int* gidx;                // with rec: the batch's games
     int rec_n;                      // with rec: records (games); gidx entries are clamped to it
+    int rec_identity;               // with rec: gidx[b] == b (the search's identity batch): gidx not read
     const int* m_limit;             // device: active boards
     const uint16_t* W;              // [2*blocks+1][9][64 n][64 c] fp16, BN folded; layer 0 = input conv (c >= planes zero)
     const uint16_t* Wf;             // the same, fragment-major [layer][tap][kk][J][64 lanes][8] (engine.hip)

@@ -155,7 +155,7 @@ __global__ __launch_bounds__(64 * NW, 1) void k_smallnet_r2(SmallNetArgs p) {
     int rv = 0;
     int meta[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     if (p.rec) {
-        const int gi = min(max(p.gidx[b], 0), p.rec_n - 1);
+        const int gi = p.rec_identity ? min(b, p.rec_n - 1) : min(max(p.gidx[b], 0), p.rec_n - 1);
         const uint8_t* rec = p.rec + (size_t)gi * AZ_REC_BYTES;
         rv = tid < HW ? rec[tid] : 0;
         const int4 m0 = *reinterpret_cast<const int4*>(rec + AZ_REC_META);
@@ -608,7 +608,7 @@ __global__ __launch_bounds__(64 * NW, 1) void k_smallnet_g(SmallNetArgs p) {
     int rv = 0;
     int meta[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     if (p.rec) {
-        const int gi = min(max(p.gidx[b], 0), p.rec_n - 1);
+        const int gi = p.rec_identity ? min(b, p.rec_n - 1) : min(max(p.gidx[b], 0), p.rec_n - 1);
         const uint8_t* rec = p.rec + (size_t)gi * AZ_REC_BYTES;
         rv = glive ? rec[gy * HB + gx] : 0;
         const int4 m0 = *reinterpret_cast<const int4*>(rec + AZ_REC_META);
