@@ -1539,7 +1539,7 @@ int az_net_trunk_kernel(az_net* n, char* name, int len) {
     }
     if (!bf || d.blocks < 1) { snprintf(name, len, "gemm_f32"); return 0; }
     if (f16 && az_smallnet_supported(H, F, n->cin_pad, d.pool, d.head_channels) && d.blocks <= az_smallnet_max_blocks()) {
-        snprintf(name, len, "k_smallnet<%d>", H);
+        snprintf(name, len, "k_smallnet_g<%d, 8, %s>", H, d.residual ? "true" : "false");   // as rocprofv3 names it
         return 0;
     }
     // the trunk's second conv of a block, as net_forward builds it at the net's capacity

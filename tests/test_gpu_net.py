@@ -300,7 +300,7 @@ def test_gpu_c5_net_full_batch(engine):
     # (board, in_planes, channels, blocks, actions, precision, max_batch) -> trunk kernel prefix
     ((15, 11, 256, 20, 225, "fp16", 2048), "conv3x3_v7<2, 15, SLIM>"),   # C3 at N = 1, 2
     ((15, 11, 256, 20, 225, "fp16", 256), "conv3x3_v6<2, 15>"),          # C3 shard at N = 8
-    ((15, 11, 64, 6, 225, "fp16", 256), "k_smallnet<15>"),               # C2: the fused 64-filter forward
+    ((15, 11, 64, 6, 225, "fp16", 256), "k_smallnet_g<15, 8, true>"),    # C2: the fused 64-filter forward
     ((15, 11, 64, 6, 225, "bf16x3", 256), "conv3x3_v4<0, 64>"),
     ((15, 11, 256, 20, 225, "bf16x3", 64), "conv3x3_v7x3<15, SLIM>"),   # the parity precision at C3
     ((15, 11, 256, 20, 225, "bf16x3", 2048), "conv3x3_v7x3<15, SLIM>"),
