@@ -722,9 +722,6 @@ __global__ __launch_bounds__(64 * NW, 1) void k_smallnet_g(SmallNetArgs p) {
         const uint32_t src = ROLE == ROLE_ODD ? aX : aY;
         const uint32_t dst = ROLE == ROLE_ODD ? eY : eX;
         const int fg0 = layer * 18;                      // this layer's first fragment group
-        static_for<0, FPW>([&](auto ic) {
-            static_for<0, JN>([&](auto jc) { acc[decltype(ic)::value][decltype(jc)::value] = bn[decltype(jc)::value]; });
-        });
         auto aload = [&](auto bufc, auto xc) {
             constexpr int buf = decltype(bufc)::value, x = decltype(xc)::value;
             constexpr int t = x / NCH, kk = x % NCH, sh = (t / 3) * WG + (t % 3);
@@ -737,13 +734,18 @@ __global__ __launch_bounds__(64 * NW, 1) void k_smallnet_g(SmallNetArgs p) {
         static_for<0, NSTEP>([&](auto qc) {
             constexpr int q = decltype(qc)::value, t = q / NCH, kk = q % NCH, r = q % NB, ws = (R0 + q) % PW;
             if constexpr (q + PF < NSTEP) aload(IC<(q + PF) % NB>{}, IC<q + PF>{});
+            // the next layer's biases, mid-layer: bn's last reads (step 0's MFMAs) are long done,
+            // and the reads land long before the epilogue's wait (the certify waits below count
+            // them as younger reads: at most a wait for more than needed)
+            if constexpr (q == NSTEP / 2) read_bias(layer + 1);
             constexpr int ahead = (NSTEP - 1 - q) < PF ? (NSTEP - 1 - q) : PF;
             certify_frags<(ahead * FPW > 15 ? 15 : ahead * FPW)>(fw[ws], fb[r]);
             __builtin_amdgcn_sched_barrier(0);
             static_for<0, FPW>([&](auto ic) {
                 static_for<0, JN>([&](auto jc) {
                     constexpr int i = decltype(ic)::value, j = decltype(jc)::value;
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fw[ws][j], fb[r][i], acc[i][j], 0, 0, 0);
+                    // step 0 accumulates onto the bias registers (no copies into the accumulators)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fw[ws][j], fb[r][i], q == 0 ? bn[j] : acc[i][j], 0, 0, 0);
                 });
             });
             __builtin_amdgcn_sched_barrier(0);
@@ -772,7 +774,6 @@ __global__ __launch_bounds__(64 * NW, 1) void k_smallnet_g(SmallNetArgs p) {
                             ds_wr64<64 * RS * i + 32 * j>(dst, pack_f16(v[0], v[1]), pack_f16(v[2], v[3]));
                         });
                     });
-                    read_bias(layer + 1);
                     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
                 }
             }
