@@ -748,8 +748,8 @@ __global__ __launch_bounds__(64 * NW, 1) void k_smallnet_g(SmallNetArgs p) {
                     acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fw[ws][j], fb[r][i], q == 0 ? bn[j] : acc[i][j], 0, 0, 0);
                 });
             });
-            // the last step's MFMAs are left free to interleave with the epilogue's VALU
-            if constexpr (q != NSTEP - 1) __builtin_amdgcn_sched_barrier(0);
+            // the MFMAs are left free to interleave with the ring refill (global loads) and, in the
+            // last step, with the epilogue's VALU
             // the ring slot just consumed takes the fragment group PW steps ahead (possibly the next
             // layer's: 2 chunks per tap from layer 1 on)
             {
@@ -760,7 +760,6 @@ __global__ __launch_bounds__(64 * NW, 1) void k_smallnet_g(SmallNetArgs p) {
                     wload(IC<ws>{}, fg0 + 18 + (ahead_step - NSTEP));   // next layer: 2 chunks per tap
                 }
             }
-            if constexpr (q != NSTEP - 1) __builtin_amdgcn_sched_barrier(0);
             if constexpr (kk == NCH - 1) {
                 if constexpr (t < 8) if (layer == 5) sm_stamp(p, 43 + t);
                 if constexpr (t == 8) {
