@@ -320,12 +320,17 @@ def pmc_traffic(a, kernel, boards_per_launch):
 
 
 def _same_kernel(profiled, name):
-    """rocprof's demangled name ("void conv3x3_v7<2, 15, 1>(ConvBf16Args)") vs the library's label
-    ("conv3x3_v7<2, 15, SLIM>"): same template and first two template arguments."""
+    """rocprof's demangled name ("void conv3x3_v7<2, 15, 1>(ConvBf16Args)", "void
+    conv3x3_v7x3<15, 1>(...)") vs the library's label ("conv3x3_v7<2, 15, SLIM>", "conv3x3_v7x3<15,
+    SLIM>"): same template and every template argument but the last (the tile geometry, an enum
+    that rocprof prints as a number)."""
     import re
-    m1 = re.search(r"(conv3x3_v\d+)<(\d+), ?(\d+)", profiled)
-    m2 = re.search(r"(conv3x3_v\d+)<(\d+), ?(\d+)", name)
-    return bool(m1 and m2 and m1.groups() == m2.groups())
+
+    def parts(s):
+        m = re.search(r"(conv3x3_v[0-9a-z]+)<([^>]*)>", s)
+        return (m.group(1), [x.strip() for x in m.group(2).split(",")][:-1]) if m else None
+    p1, p2 = parts(profiled), parts(name)
+    return bool(p1 and p2 and p1 == p2)
 
 
 # ------------------------------------------------------------------------------- CPU baseline
