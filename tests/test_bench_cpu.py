@@ -209,3 +209,22 @@ def test_bench_rank_death_fails_loudly_gloo_world2():
     assert res[1][1] == "RuntimeError"
     assert res[0][1] != "returned" and res[0][2] < 15 + 60
     assert all(p.exitcode not in (0, None) for p in procs)
+
+
+def test_pmc_traffic_matches_each_trunk_kernel():
+    """roofline.traffic comes from the committed PMC summary of the SAME kernel and precision: the
+    fp16 v7 line and parity_mode's bf16x3 v7x3 line each find theirs, and neither takes the other's."""
+    import types
+    import bench
+    assert bench._same_kernel("void conv3x3_v7<2, 15, 1>(ConvBf16Args)", "conv3x3_v7<2, 15, SLIM>")
+    assert bench._same_kernel("void conv3x3_v7x3<15, 1>(ConvBf16Args)", "conv3x3_v7x3<15, SLIM>")
+    assert not bench._same_kernel("void conv3x3_v7<2, 15, 1>(ConvBf16Args)", "conv3x3_v7x3<15, SLIM>")
+    assert not bench._same_kernel("void conv3x3_v6<2, 15, 1>(ConvBf16Args)", "conv3x3_v7<2, 15, SLIM>")
+    assert not bench._same_kernel("void conv3x3_v7<1, 15, 1>(ConvBf16Args)", "conv3x3_v7<2, 15, SLIM>")
+    net = dict(board=15, channels=256, blocks=20)
+    fp16 = bench.pmc_traffic(types.SimpleNamespace(precision="fp16", **net), "conv3x3_v7<2, 15, SLIM>", 2048.0)
+    x3 = bench.pmc_traffic(types.SimpleNamespace(precision="bf16x3", **net), "conv3x3_v7x3<15, SLIM>", 2048.0)
+    assert fp16 and x3 and "v7x3" in x3["traffic_source"] and "v7x3" not in fp16["traffic_source"]
+    assert x3["traffic"] > fp16["traffic"] > 0
+    half = bench.pmc_traffic(types.SimpleNamespace(precision="fp16", **net), "conv3x3_v7<2, 15, SLIM>", 1024.0)
+    assert half["traffic"] == pytest.approx(fp16["traffic"] / 2)
