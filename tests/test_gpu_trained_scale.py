@@ -95,3 +95,29 @@ def test_gpu_trained_scale_outputs(engine, shape, prec):
     else:
         assert el <= TOL and ev <= TOL
     net.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape,B", [("c4", 1024), ("c5", 1024)])
+def test_gpu_trained_scale_production_batch_bf16x3(engine, shape, B):
+    """The parity precision at the BASELINE configs' production batch (C4 / C5: 1024 boards per
+    forward, the batch the self-play search hands the net), trained-scale heads: 16 sampled boards
+    (first, last, and 14 in between) against the fp32 oracle within the north-star 1e-4.  (C3's
+    2048-board batch: tests/test_gpu_selfplay_net.py::test_gpu_c3_full_size_replay_bf16x3.)"""
+    import az_amd
+    import net_oracle
+    bs, ci, ch, blocks, A = NETS[shape]
+    desc = az_amd.NetDesc(bs, ci, ch, blocks, A, 32, 8, 256, 1, 0, az_amd.AZ_PREC_BF16X3, B)
+    x = _planes(shape, B, seed=29)
+    pick = np.unique(np.concatenate([[0, B - 1], np.random.default_rng(5).choice(B, 14, replace=False)]))
+    blob = trained_scale_blob(desc, 4321, x[pick])
+    net = az_amd.HipNeuralNetwork(engine, desc)
+    net.load_weights(blob)
+    lo, v = net.forward(x)
+    rl, rv = net_oracle.forward(desc, blob, x[pick])
+    lmax = float(np.abs(rl).max())
+    el, ev = float(np.abs(lo[pick] - rl).max()), float(np.abs(v[pick] - rv).max())
+    print(f"{shape} bf16x3 B={B}: |logit|max {lmax:.3f} max|dlogit|={el:.3e} max|dvalue|={ev:.3e}")
+    assert 7.9 < lmax < 8.1
+    assert el <= TOL and ev <= TOL
+    net.close()
