@@ -469,11 +469,14 @@ __device__ __forceinline__ uint16_t v4_store(float f) {
 
 #define V4_STAMP(k) do { } while (0)
 
-template <int MODE, int BNT, int SCHED>
-__global__ __launch_bounds__(512, 1) void conv3x3_v4(ConvBf16Args p) {
+// BOARDS boards per block, 4 waves per board (BOARDS = 1: 256 threads, two blocks per CU by LDS --
+// the small-batch bf16x3 layers of the 64-channel C2 net, whose 256 boards would fill only half the
+// CUs two per block).  Every output's MFMA chain is the same for either BOARDS.
+template <int MODE, int BNT, int SCHED, int BOARDS = 2>
+__global__ __launch_bounds__(256 * BOARDS, 1) void conv3x3_v4(ConvBf16Args p) {
     constexpr bool SPLIT = MODE == 0;
     constexpr int NPL = SPLIT ? 2 : 1;
-    constexpr int BOARDS = 2;
+    constexpr int NT = 256 * BOARDS, NW = NT / 64;
     constexpr int A_PLANE = 2 * V4_HROWS * 16;             // one board, one plane, 16 channels: 10 KB
     constexpr int A_BUF = BOARDS * NPL * A_PLANE;
     constexpr int B_TAP = NPL * 2 * BNT * 16;
@@ -484,10 +487,10 @@ __global__ __launch_bounds__(512, 1) void conv3x3_v4(ConvBf16Args p) {
     constexpr int LDS = LDS_MAIN > LDS_EPI ? LDS_MAIN : LDS_EPI;
     constexpr int A_INS = BOARDS * NPL * 2 * (V4_HROWS / 64);   // 1 KiB pieces per A chunk
     constexpr int B_INS = 3 * NPL * 2 * (BNT / 64);             // per step
-    constexpr int PAX = (A_INS + 7) / 8, PBX = (B_INS + 7) / 8;
+    constexpr int PAX = (A_INS + NW - 1) / NW, PBX = (B_INS + NW - 1) / NW;
     constexpr int WN = BNT >= 128 ? BNT / 64 : 1;
-    constexpr int WM = 8 / WN;
-    constexpr int TM = 512 / WM;
+    constexpr int WM = NW / WN;
+    constexpr int TM = NT / WM;
     constexpr int FM = TM / 32, FN = BNT / WN / 32;
     typedef typename std::conditional<MODE == 2, f16x8, bf16x8>::type frag;
     __shared__ __attribute__((aligned(16))) uint8_t lds[LDS];
@@ -503,13 +506,13 @@ __global__ __launch_bounds__(512, 1) void conv3x3_v4(ConvBf16Args p) {
     if (b0 >= nboards) return;
     const int C = p.C, HW = p.H * p.W, K = 9 * C;
     const int NCH = C / 16, NS = NCH * 3;
-    const int PA = (A_INS - wave + 7) / 8, PB = (B_INS - wave + 7) / 8;   // this wave's pieces
+    const int PA = (A_INS - wave + NW - 1) / NW, PB = (B_INS - wave + NW - 1) / NW;   // this wave's pieces
 
     const uint16_t* a_src[PAX];
     int a_ch[PAX], a_off[PAX];
 #pragma unroll
     for (int j = 0; j < PAX; ++j) {
-        const int q = wave + 8 * j;
+        const int q = wave + NW * j;
         const int rb = q % 5, ch = (q / 5) % 2, plane = (q / 10) % NPL, bd = q / (10 * NPL);
         const int hr = rb * 64 + lane;
         const int Y = hr / 17, X = hr - Y * 17;
@@ -524,7 +527,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_v4(ConvBf16Args p) {
     int b_off[PBX];
 #pragma unroll
     for (int j = 0; j < PBX; ++j) {
-        const int q = min(wave + 8 * j, B_INS - 1);
+        const int q = min(wave + NW * j, B_INS - 1);
         constexpr int RB = BNT / 64;
         const int rb = q % RB, ch = (q / RB) % 2, plane = (q / (2 * RB)) % NPL, t = q / (2 * RB * NPL);
         const int n = n0 + rb * 64 + lane;
@@ -656,7 +659,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_v4(ConvBf16Args p) {
         const int b = b0 + bd;
         constexpr int VPR = BNT / 8;
         if (b < nboards) {
-            for (int v = tid; v < 225 * VPR; v += 512) {
+            for (int v = tid; v < 225 * VPR; v += NT) {
                 const int pix = v / VPR, cv = (v % VPR) * 8;
                 const int y = pix / 15, x = pix - y * 15;
                 const int row = y * 17 + x;
@@ -1743,6 +1746,10 @@ static void v4_launch(const ConvBf16Args& a, int mode, int grid, hipStream_t st)
 void az_conv_v4_launch(const ConvBf16Args& a, int mode, hipStream_t st) {
     const int boards = a.M / 225;
     const int bnt = a.N % 128 == 0 ? 128 : 64;
+    if (mode == 0 && bnt == 64 && boards <= 512) {   // one board per block: fill the CUs at small batches
+        hipLaunchKernelGGL((conv3x3_v4<0, 64, 0, 1>), dim3(boards * (a.N / 64)), dim3(256), 0, st, a);
+        return;
+    }
     const int grid = (boards + 1) / 2 * (a.N / bnt);
     if (bnt == 128) v4_launch<128>(a, mode, grid, st);
     else v4_launch<64>(a, mode, grid, st);
