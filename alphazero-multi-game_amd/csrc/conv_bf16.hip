@@ -472,11 +472,11 @@ __device__ __forceinline__ uint16_t v4_store(float f) {
 // BOARDS boards per block, 4 waves per board (BOARDS = 1: 256 threads, two blocks per CU by LDS --
 // the small-batch bf16x3 layers of the 64-channel C2 net, whose 256 boards would fill only half the
 // CUs two per block).  Every output's MFMA chain is the same for either BOARDS.
-template <int MODE, int BNT, int SCHED, int BOARDS = 2>
-__global__ __launch_bounds__(256 * BOARDS, 1) void conv3x3_v4(ConvBf16Args p) {
+template <int MODE, int BNT, int SCHED, int BOARDS = 2, int NT = 256 * BOARDS>
+__global__ __launch_bounds__(NT, 1) void conv3x3_v4(ConvBf16Args p) {
     constexpr bool SPLIT = MODE == 0;
     constexpr int NPL = SPLIT ? 2 : 1;
-    constexpr int NT = 256 * BOARDS, NW = NT / 64;
+    constexpr int NW = NT / 64;
     constexpr int A_PLANE = 2 * V4_HROWS * 16;             // one board, one plane, 16 channels: 10 KB
     constexpr int A_BUF = BOARDS * NPL * A_PLANE;
     constexpr int B_TAP = NPL * 2 * BNT * 16;
@@ -490,7 +490,7 @@ __global__ __launch_bounds__(256 * BOARDS, 1) void conv3x3_v4(ConvBf16Args p) {
     constexpr int PAX = (A_INS + NW - 1) / NW, PBX = (B_INS + NW - 1) / NW;
     constexpr int WN = BNT >= 128 ? BNT / 64 : 1;
     constexpr int WM = NW / WN;
-    constexpr int TM = NT / WM;
+    constexpr int TM = BOARDS * 256 / WM;              // output rows per wave
     constexpr int FM = TM / 32, FN = BNT / WN / 32;
     typedef typename std::conditional<MODE == 2, f16x8, bf16x8>::type frag;
     __shared__ __attribute__((aligned(16))) uint8_t lds[LDS];
@@ -1747,7 +1747,7 @@ void az_conv_v4_launch(const ConvBf16Args& a, int mode, hipStream_t st) {
     const int boards = a.M / 225;
     const int bnt = a.N % 128 == 0 ? 128 : 64;
     if (mode == 0 && bnt == 64 && boards <= 512) {   // one board per block: fill the CUs at small batches
-        hipLaunchKernelGGL((conv3x3_v4<0, 64, 0, 1>), dim3(boards * (a.N / 64)), dim3(256), 0, st, a);
+        hipLaunchKernelGGL((conv3x3_v4<0, 64, 0, 1, 512>), dim3(boards * (a.N / 64)), dim3(512), 0, st, a);
         return;
     }
     const int grid = (boards + 1) / 2 * (a.N / bnt);
