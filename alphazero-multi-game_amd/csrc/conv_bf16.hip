@@ -1747,7 +1747,7 @@ void az_conv_v4_launch(const ConvBf16Args& a, int mode, hipStream_t st) {
     const int boards = a.M / 225;
     const int bnt = a.N % 128 == 0 ? 128 : 64;
     if (mode == 0 && bnt == 64 && boards <= 512) {   // one board per block: fill the CUs at small batches
-        hipLaunchKernelGGL((conv3x3_v4<0, 64, 0, 1, 512>), dim3(boards * (a.N / 64)), dim3(512), 0, st, a);
+        hipLaunchKernelGGL((conv3x3_v4<0, 64, 1, 1, 512>), dim3(boards * (a.N / 64)), dim3(512), 0, st, a);
         return;
     }
     const int grid = (boards + 1) / 2 * (a.N / bnt);
