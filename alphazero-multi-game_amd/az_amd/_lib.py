@@ -5,7 +5,16 @@ import ctypes
 import os
 
 PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.environ.get("AZ_HIP_LIB") or os.path.join(PKG, "build", "libaz_hip.so")  # override: diagnostic builds
+LIB_PATH = os.path.join(PKG, "build", "libaz_hip.so")
+# Measurement tools (tools/ab_builds.sh) may load an in-tree diagnostic build of the same library,
+# named by AZ_DIAG_HIP_LIB; only PKG/build*/libaz_hip.so is accepted (never another library).
+_diag = os.environ.get("AZ_DIAG_HIP_LIB")
+if _diag:
+    _d = os.path.realpath(_diag)
+    if not (os.path.basename(_d) == "libaz_hip.so" and os.path.dirname(os.path.dirname(_d)) == os.path.realpath(PKG)
+            and os.path.basename(os.path.dirname(_d)).startswith("build")):
+        raise RuntimeError(f"AZ_DIAG_HIP_LIB={_diag}: only an in-tree build (build*/libaz_hip.so) may be loaded")
+    LIB_PATH = _d
 
 c_int, c_float, c_size_t, c_uint32, c_uint64, c_int64 = (ctypes.c_int, ctypes.c_float, ctypes.c_size_t,
                                                           ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int64)

@@ -43,7 +43,7 @@ struct BatchQueueConfig {
     int timeoutMs = 10;                // how long a partial batch may wait for more requests
     int maxQueueSize = 1024;           // requests beyond this are answered uniformly (dropped)
     int numWorkerThreads = 1;
-    bool prioritizeBatchSize = true;   // a partial batch waits up to timeoutMs to fill (else only to minBatchSize)
+    bool prioritizeBatchSize = true;   // kept for the API; unused, as in the reference (batch_queue.cpp never reads it)
     int minBatchSize = 1;
     bool useAdaptiveBatching = true;
     int adaptiveBatchInterval = 100;   // ms
@@ -85,8 +85,9 @@ class BatchQueue {
     int getPendingRequests() const;
     const BatchQueueStats& getStats() const { return stats_; }
     void resetStats() { stats_.reset(); }
-    NeuralNetwork* getNeuralNetwork() const { return neuralNetwork_; }
-    void setNeuralNetwork(NeuralNetwork* neuralNetwork) { neuralNetwork_ = neuralNetwork; }
+    NeuralNetwork* getNeuralNetwork() const { return neuralNetwork_.load(); }
+    // takes effect from the next batch a worker evaluates (workers read the pointer once per batch)
+    void setNeuralNetwork(NeuralNetwork* neuralNetwork) { neuralNetwork_.store(neuralNetwork); }
     // batch target of the adaptive batching (== getBatchSize() without it)
     int getCurrentBatchSize() const;
 
@@ -106,7 +107,7 @@ class BatchQueue {
     void adapt();
     static Result uniform(const core::IGameState& s);
 
-    NeuralNetwork* neuralNetwork_;
+    std::atomic<NeuralNetwork*> neuralNetwork_;
     BatchQueueConfig config_;
     std::map<int, std::deque<Request>, std::greater<int>> queue_;   // by priority, highest first; FIFO inside
     size_t size_ = 0;

@@ -158,42 +158,45 @@ void BatchQueue::adapt() {
     int opt;
     if (q <= config_.minBatchSize) opt = config_.minBatchSize;
     else if (q > 2 * current_) opt = std::min(q / 2, config_.maxAdaptiveBatchSize);
-    else if (neuralNetwork_ && neuralNetwork_->isGpuAvailable()) opt = std::min(config_.batchSize * 2, config_.maxAdaptiveBatchSize);
+    else if (NeuralNetwork* nn = neuralNetwork_.load(); nn && nn->isGpuAvailable()) opt = std::min(config_.batchSize * 2, config_.maxAdaptiveBatchSize);
     else opt = config_.batchSize;
     if (opt > current_) current_ = std::min(opt, current_ + 2);
     else if (opt < current_) current_ = std::max(opt, current_ - 1);
     current_ = std::max(config_.minBatchSize, std::min(current_, config_.maxAdaptiveBatchSize));
 }
 
-// Up to the batch target from the highest priority down.  A batch below minBatchSize -- or, with
-// prioritizeBatchSize, below the target -- waits up to timeoutMs for more requests; a batch that
-// leaves at the deadline still short of the target counts as timed out.
+// batch_queue.cpp:219-265: up to the batch target from the highest priority down.  The batch
+// runs as soon as the queue is drained and it holds at least minBatchSize requests (the reference
+// never reads prioritizeBatchSize); below minBatchSize it waits timeoutMs / 4 for more and then
+// runs with what it has.  Past timeoutMs of collecting, a batch of at least minBatchSize stops
+// taking requests.  Either early stop counts as a timed-out batch.
 std::vector<BatchQueue::Request> BatchQueue::takeBatch(std::unique_lock<std::mutex>& lk, bool& timedOut) {
     std::vector<Request> batch;
-    const auto deadline = Clock::now() + std::chrono::milliseconds(std::max(0, config_.timeoutMs));
-    for (;;) {
-        const size_t target = (size_t)std::max(1, current_);
-        while (batch.size() < target && size_ > 0) {
-            auto it = queue_.begin();
-            batch.push_back(std::move(it->second.front()));
-            it->second.pop_front();
-            if (it->second.empty()) queue_.erase(it);
-            --size_;
+    const auto start = Clock::now();
+    const auto limit = std::chrono::milliseconds(config_.timeoutMs);
+    const size_t target = (size_t)std::max(1, current_);
+    const size_t minB = (size_t)std::max(0, config_.minBatchSize);
+    while (batch.size() < target && size_ > 0) {
+        if (Clock::now() - start >= limit && batch.size() >= minB) {
+            timedOut = true;
+            break;
         }
-        const size_t want = config_.prioritizeBatchSize ? target : (size_t)std::max(1, config_.minBatchSize);
-        if (batch.size() >= want || stop_) return batch;
-        if (!cv_.wait_until(lk, deadline, [&] { return size_ > 0 || stop_; })) {
-            timedOut = batch.size() < target;
-            if (batch.size() < (size_t)std::max(1, config_.minBatchSize)) {
-                // below the minimum: keep waiting for requests (the reference loops likewise)
-                if (!cv_.wait_for(lk, std::chrono::milliseconds(std::max(1, config_.timeoutMs / 4)),
-                                  [&] { return size_ > 0 || stop_; }))
-                    return batch;
-                continue;
+        auto it = queue_.begin();
+        batch.push_back(std::move(it->second.front()));
+        it->second.pop_front();
+        if (it->second.empty()) queue_.erase(it);
+        --size_;
+        if (size_ == 0 && batch.size() < minB) {
+            const bool more = cv_.wait_for(lk, std::chrono::milliseconds(std::max(1, config_.timeoutMs / 4)),
+                                           [&] { return size_ > 0 || stop_; });
+            if (stop_) break;
+            if (!more && !batch.empty()) {
+                timedOut = true;
+                break;
             }
-            return batch;
         }
     }
+    return batch;
 }
 
 void BatchQueue::worker() {
@@ -233,7 +236,7 @@ void BatchQueue::evaluate(std::vector<Request>& batch) {
     for (const Request& r : batch) states.push_back(std::cref(*r.state));
     std::vector<std::vector<float>> policies;
     std::vector<float> values;
-    NeuralNetwork* nn = neuralNetwork_;
+    NeuralNetwork* nn = neuralNetwork_.load();
     bool ok = true;
     try {
         if (!nn) throw std::runtime_error("BatchQueue: no network");

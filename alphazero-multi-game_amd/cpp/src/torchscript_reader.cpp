@@ -40,33 +40,45 @@ struct Zip {
         if (count == 0xffff || cd == 0xffffffffu) {            // zip64 end of central directory
             if (eocd < 20 || rd32(&buf[eocd - 20]) != 0x07064b50u) fail("zip64 locator missing");
             const uint64_t z = rd64(&buf[eocd - 20 + 8]);
-            if (z + 56 > n || rd32(&buf[z]) != 0x06064b50u) fail("zip64 record missing");
+            if (z > n || n - z < 56 || rd32(&buf[z]) != 0x06064b50u) fail("zip64 record missing");
             count = rd64(&buf[z + 32]);
             cd = rd64(&buf[z + 48]);
         }
+        if (cd > n) fail("central directory outside the file");
         size_t p = cd;
         for (uint64_t e = 0; e < count; ++e) {
-            if (p + 46 > n || rd32(&buf[p]) != 0x02014b50u) fail("bad central directory");
+            if (n - p < 46 || rd32(&buf[p]) != 0x02014b50u) fail("bad central directory");
             const uint16_t method = rd16(&buf[p + 10]);
             uint64_t csize = rd32(&buf[p + 20]), usize = rd32(&buf[p + 24]);
             const uint16_t nl = rd16(&buf[p + 28]), xl = rd16(&buf[p + 30]), cl = rd16(&buf[p + 32]);
             uint64_t loc = rd32(&buf[p + 42]);
+            if (n - p - 46 < (size_t)nl + xl + cl) fail("central directory entry past the end of the file");
             const std::string name(reinterpret_cast<const char*>(&buf[p + 46]), nl);
             // zip64 extra: the fields that overflowed, in the order usize, csize, offset
-            for (size_t x = p + 46 + nl; x + 4 <= p + 46 + nl + xl;) {
+            const size_t xend = p + 46 + nl + xl;
+            for (size_t x = p + 46 + nl; x + 4 <= xend;) {
                 const uint16_t id = rd16(&buf[x]), len = rd16(&buf[x + 2]);
+                if (xend - x - 4 < len) fail("zip extra field past its record");
                 if (id == 0x0001) {
                     size_t q = x + 4;
-                    if (usize == 0xffffffffu) { usize = rd64(&buf[q]); q += 8; }
-                    if (csize == 0xffffffffu) { csize = rd64(&buf[q]); q += 8; }
-                    if (loc == 0xffffffffu) loc = rd64(&buf[q]);
+                    const size_t qend = x + 4 + len;
+                    auto take = [&](uint64_t& f) {
+                        if (qend - q < 8) fail("short zip64 extra field");
+                        f = rd64(&buf[q]);
+                        q += 8;
+                    };
+                    if (usize == 0xffffffffu) take(usize);
+                    if (csize == 0xffffffffu) take(csize);
+                    if (loc == 0xffffffffu) take(loc);
                 }
                 x += 4 + len;
             }
-            if (loc + 30 > n || rd32(&buf[loc]) != 0x04034b50u) fail("bad local header of " + name);
-            const size_t data = loc + 30 + rd16(&buf[loc + 26]) + rd16(&buf[loc + 28]);
+            if (loc > n || n - loc < 30 || rd32(&buf[loc]) != 0x04034b50u) fail("bad local header of " + name);
+            const uint64_t hdr = 30 + (uint64_t)rd16(&buf[loc + 26]) + rd16(&buf[loc + 28]);
+            if (n - loc < hdr) fail("truncated local header of " + name);
+            const size_t data = loc + hdr;
             if (method == 0) {
-                if (data + usize > n) fail("truncated entry " + name);
+                if (usize > n - data) fail("truncated entry " + name);
                 entries[name] = {data, (size_t)usize};
             }
             p += 46 + nl + xl + cl;
@@ -103,7 +115,13 @@ VP unpickle(const uint8_t* p, size_t n) {
     std::map<uint64_t, VP> memo;
     size_t i = 0;
     auto need = [&](size_t k) { if (i + k > n) fail("truncated data.pkl"); };
-    auto pop = [&]() { if (st.empty()) fail("pickle stack underflow"); VP v = st.back(); st.pop_back(); return v; };
+    auto pop = [&]() {
+        if (st.empty()) fail("pickle stack underflow");
+        VP v = st.back();
+        st.pop_back();
+        if (!v) fail("null pickle value");
+        return v;
+    };
     auto pop_mark = [&]() {
         if (marks.empty()) fail("pickle mark underflow");
         const size_t m = marks.back();
@@ -190,8 +208,8 @@ VP unpickle(const uint8_t* p, size_t n) {
             case 'd': { VP d = mk(Val::DICT); setitems(d, pop_mark()); st.push_back(d); break; }
             case 's': { VP v = pop(), k = pop(); if (st.empty()) fail("SETITEM"); setitems(st.back(), {k, v}); break; }
             case 'u': { std::vector<VP> kv = pop_mark(); if (st.empty()) fail("SETITEMS"); setitems(st.back(), kv); break; }
-            case 'q': { need(1); memo[p[i]] = st.empty() ? nullptr : st.back(); i += 1; break; }
-            case 'r': { need(4); memo[rd32(p + i)] = st.empty() ? nullptr : st.back(); i += 4; break; }
+            case 'q': { need(1); if (st.empty()) fail("BINPUT on an empty stack"); memo[p[i]] = st.back(); i += 1; break; }
+            case 'r': { need(4); if (st.empty()) fail("LONG_BINPUT on an empty stack"); memo[rd32(p + i)] = st.back(); i += 4; break; }
             case 'h': { need(1); auto it = memo.find(p[i]); if (it == memo.end()) fail("BINGET of an unset memo"); st.push_back(it->second); i += 1; break; }
             case 'j': { need(4); auto it = memo.find(rd32(p + i)); if (it == memo.end()) fail("LONG_BINGET of an unset memo"); st.push_back(it->second); i += 4; break; }
             case 'c': {                                                         // GLOBAL: the allow-list
@@ -293,17 +311,27 @@ std::vector<NamedTensor> readTorchScript(const std::string& path) {
     const auto& d = z.get(prefix + "data.pkl");
     VP root = unpickle(z.buf.data() + d.first, d.second);
     std::vector<NamedTensor> out;
-    std::function<void(const VP&, const std::string&)> walk = [&](const VP& v, const std::string& pre) {
+    // module nesting is shallow in any real archive; a BUILD state that reaches its own object
+    // through the memo would otherwise recurse without bound
+    constexpr int MAX_DEPTH = 64;
+    std::function<void(const VP&, const std::string&, int)> walk = [&](const VP& v, const std::string& pre, int depth) {
+        if (depth > MAX_DEPTH) fail("module nesting deeper than 64 (cyclic BUILD state?)");
         for (auto& kv : v->dict) {
+            if (!kv.first || !kv.second) fail("null dictionary entry");
             if (kv.first->k != Val::STR) continue;
             const std::string name = pre + kv.first->s;
             const VP& x = kv.second;
             if (x->k == Val::OBJECT) {
-                walk(x, name + ".");
+                walk(x, name + ".", depth + 1);
             } else if (x->k == Val::TENSOR) {
                 NamedTensor t;
                 t.name = name;
                 t.shape = x->size;
+                if (!x->storage || x->size.size() != x->stride.size()) fail("tensor " + name + ": size / stride mismatch");
+                for (size_t a = 0; a < x->size.size(); ++a)
+                    if (x->size[a] < 0 || x->stride[a] < -((int64_t)1 << 40) || x->stride[a] > ((int64_t)1 << 40))
+                        fail("tensor " + name + ": size / stride out of range");
+                if (x->offset < 0 || x->offset > ((int64_t)1 << 40)) fail("tensor " + name + ": storage offset out of range");
                 const std::string& ty = x->storage->s;
                 const size_t es = ty == "DoubleStorage" || ty == "LongStorage" ? 8 : ty == "FloatStorage" || ty == "IntStorage" ? 4
                                   : ty == "HalfStorage" || ty == "BFloat16Storage" ? 2 : 0;
@@ -311,7 +339,10 @@ std::vector<NamedTensor> readTorchScript(const std::string& path) {
                 const auto& e = z.get(prefix + "data/" + x->storage->key);
                 const uint8_t* base = z.buf.data() + e.first;
                 int64_t numel = 1;
-                for (int64_t s : x->size) numel *= s;
+                for (int64_t s : x->size) {
+                    if (s && numel > ((int64_t)1 << 40) / s) fail("tensor " + name + " too large");
+                    numel *= s;
+                }
                 t.data.resize((size_t)numel);
                 const size_t nd = x->size.size();
                 for (int64_t lin = 0; lin < numel; ++lin) {
@@ -335,7 +366,7 @@ std::vector<NamedTensor> readTorchScript(const std::string& path) {
             }
         }
     };
-    if (root->k == Val::OBJECT || root->k == Val::DICT) walk(root, "");
+    if (root && (root->k == Val::OBJECT || root->k == Val::DICT)) walk(root, "", 0);
     else fail("data.pkl does not hold a module or a state dict");
     return out;
 }

@@ -469,9 +469,12 @@ __device__ __forceinline__ uint16_t v4_store(float f) {
 
 #define V4_STAMP(k) do { } while (0)
 
-// BOARDS boards per block, 4 waves per board (BOARDS = 1: 256 threads, two blocks per CU by LDS --
-// the small-batch bf16x3 layers of the 64-channel C2 net, whose 256 boards would fill only half the
-// CUs two per block).  Every output's MFMA chain is the same for either BOARDS.
+// BOARDS boards per block of NT threads (default 4 waves per board).  The small-batch bf16x3 layers
+// of the 64-channel C2 net launch conv3x3_v4<0, 64, 1, 1, 512>: ONE board per 512-thread block
+// (8 waves, two per SIMD, 32 output rows per wave), one block per CU by its LDS -- at 256 boards two
+// boards per block would fill only half the CUs, and one board per 256-thread block left a SIMD
+// with one wave and nothing to hide its fragment reads behind.  Every output's MFMA chain is the
+// same for any BOARDS / NT.
 template <int MODE, int BNT, int SCHED, int BOARDS = 2, int NT = 256 * BOARDS>
 __global__ __launch_bounds__(NT, 1) void conv3x3_v4(ConvBf16Args p) {
     constexpr bool SPLIT = MODE == 0;
@@ -1624,6 +1627,7 @@ static int g_conv_flags = 4 | 0x200;   // bit 2: v6 (16x16x32) at 15x15; 0x200: 
 // (a residual L2 prefetch during the main loop measured 0.6% slower and was removed; a cross-row
 // fragment prefetch and a mid-row barrier variant measured 1.5-2% slower)
 extern "C" int az_diag_set_conv_flags(int flags) { g_conv_flags = flags; return 0; }
+int az_conv_flags() { return g_conv_flags; }
 
 template <int HB, bool DENSE>
 static void v6_launch_g(const ConvBf16Args& a, int mode, hipStream_t st) {

@@ -67,6 +67,7 @@ void az_launch_to_g8x3(const float* in, uint16_t* hi, uint16_t* lo, int C, int H
                        hipStream_t st);
 bool az_conv_v7x3_supported(const ConvBf16Args& a);
 int az_conv_v7x3_launch(const ConvBf16Args& a, hipStream_t st);
+int az_conv_x3_name(const ConvBf16Args& a, char* out, int len);
 void az_launch_to_f16(const float* in, uint16_t* out, size_t n, const int* m_limit, int rows_per_sample, int C,
                       hipStream_t st);
 void az_launch_split_bf16(const float* in, uint16_t* hi, uint16_t* lo, size_t n, const int* m_limit, int rows_per_sample,
@@ -1547,8 +1548,9 @@ int az_net_trunk_kernel(az_net* n, char* name, int len) {
     a.M = d.max_batch * n->HW; a.N = F; a.C = F; a.H = H; a.W = H; a.rows_per_sample = n->HW; a.relu = 1;
     a.a_tail = n->act_elems * 2;
     if (x3_trunk(n)) {
-        snprintf(name, len, "conv3x3_v7x3<%d, %s>", H, H == 15 ? "SLIM" : "DENSE");
-        return 0;
+        Layer probe;
+        probe.Wbk_bf = probe.Wbk_lo = n->zero;
+        return az_conv_x3_name(x3_conv_args(n, probe, 1, 0, d.max_batch, nullptr), name, len) ? az_fail(AZ_ERR_ARG, "x3 name") : 0;
     }
     const bool g8 = prec != AZ_PREC_BF16X3 && az_conv_g8_supported(H, H, F, F);
     const int r = g8 ? az_conv_g8_name(a, f16 ? 2 : 1, name, len)
@@ -1608,13 +1610,13 @@ int az_search_create(az_engine* e, az_net* net, const az_search_cfg* c, az_searc
         if (net->d.max_batch < G) return az_fail(AZ_ERR_ARG, "network max_batch %d < n_games %d", net->d.max_batch, G);
         if (!net->loaded) return az_fail(AZ_ERR_STATE, "network weights not loaded");
     }
+    if (c->prior_ring > 0 && c->prior_ring < NA)
+        return az_fail(AZ_ERR_ARG, "prior_ring %d is smaller than one policy (%d entries)", c->prior_ring, NA);
     std::lock_guard<std::mutex> lk(e->mu);
     HIPCHK(hipSetDevice(e->device));
     auto* s = new az_search();
     s->e = e; s->net = net; s->c = *c;
     const int ncap = c->node_capacity > 0 ? c->node_capacity : 3 * std::max(64, c->num_simulations) * NA + 8 * NA + 64;
-    if (c->prior_ring > 0 && c->prior_ring < NA)
-        return az_fail(AZ_ERR_ARG, "prior_ring %d is smaller than one policy (%d entries)", c->prior_ring, NA);
     const int ring = c->prior_ring > 0 ? c->prior_ring : std::max(1 << 16, 12 * std::max(64, c->num_simulations) * NA);
     s->c.node_capacity = ncap; s->c.prior_ring = ring;
     TreeDev& t = s->t;

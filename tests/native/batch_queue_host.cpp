@@ -3,6 +3,7 @@
 // network whose outputs are a function of the state's hash, so every answer can be checked
 // against a direct predictBatch.  Prints "OK" and exits 0 when every check holds.
 #include <atomic>
+#include <chrono>
 #include <cmath>
 #include <condition_variable>
 #include <cstdio>
@@ -263,6 +264,43 @@ int main(int argc, char** argv) {
         std::vector<std::future<nn::BatchQueue::Result>> fut;
         for (int k = 0; k < 30; ++k) fut.push_back(q.enqueue(*position(k)));
         for (int k = 0; k < 30; ++k) CHECK(same(fut[k].get(), MockNeuralNetwork::out(*position(k))));
+    }
+    // latency (batch_queue.cpp:219-265): a lone caller's request runs as soon as the queue is
+    // drained -- it never waits timeoutMs for the batch to fill; below minBatchSize a batch waits
+    // timeoutMs / 4 for company and then runs anyway (a timed-out batch)
+    {
+        MockNeuralNetwork net;
+        nn::BatchQueueConfig cfg;
+        cfg.timeoutMs = 200;
+        nn::BatchQueue q(&net, cfg);
+        const auto t0 = std::chrono::steady_clock::now();
+        for (int k = 0; k < 20; ++k) CHECK(same(q.enqueue(*position(k)).get(), MockNeuralNetwork::out(*position(k))));
+        const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        CHECK(ms < 20 * 25.0);                        // a fill-wait would cost 20 x 200 ms
+        CHECK(q.getStats().totalTimedOutBatches == 0);
+        cfg.minBatchSize = 3;
+        nn::BatchQueue q3(&net, cfg);
+        const auto t1 = std::chrono::steady_clock::now();
+        CHECK(same(q3.enqueue(*position(3)).get(), MockNeuralNetwork::out(*position(3))));
+        const double ms3 = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t1).count();
+        CHECK(ms3 >= 40.0 && ms3 < 200.0);            // timeoutMs / 4 = 50 ms
+        CHECK(q3.getStats().totalTimedOutBatches == 1);
+    }
+    // the network may be swapped while workers run (the next batch uses the new one)
+    {
+        MockNeuralNetwork a, b;
+        nn::BatchQueue q(&a, 2, 2);
+        std::atomic<bool> done{false};
+        std::thread sw([&] {
+            for (int k = 0; !done.load(); ++k) {
+                q.setNeuralNetwork(k % 2 ? &a : &b);
+                std::this_thread::yield();
+            }
+        });
+        for (int k = 0; k < 40; ++k) CHECK(same(q.enqueue(*position(k)).get(), MockNeuralNetwork::out(*position(k))));
+        done = true;
+        sw.join();
+        CHECK(q.getNeuralNetwork() == &a || q.getNeuralNetwork() == &b);
     }
     // destruction with requests still queued returns (their futures report a broken promise)
     {

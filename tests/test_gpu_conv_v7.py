@@ -54,3 +54,43 @@ def test_gpu_v7_bitwise_equals_v6(engine, case, mode):
     print(f"{case} {mode}: max|v7 - v6| logits {np.abs(l7 - l6).max():.3e} value {np.abs(v7 - v6).max():.3e}")
     assert np.array_equal(l7, l6) and np.array_equal(v7, v6)
     net.close()
+
+
+X3W_CASES = [  # board, in_planes, actions, channels, blocks, residual, B: conv3x3_v9x3 geometries (N % 256 == 0)
+    (15, 11, 225, 256, 2, 1, 37),     # SLIM tile, ragged batch
+    (15, 11, 225, 256, 1, 1, 1),      # a single board
+    (15, 11, 225, 256, 2, 0, 5),      # plain stack (no residual planes)
+    (19, 8, 362, 256, 2, 1, 13),      # DENSE 19x19 (Go), tiles spanning boards
+    (9, 11, 81, 256, 1, 1, 29),       # DENSE 9x9
+    (13, 8, 170, 256, 1, 1, 7),       # DENSE 13x13
+    (8, 111, 4672, 256, 2, 1, 33),    # DENSE 8x8 chess shape
+    (15, 11, 225, 512, 1, 1, 3),      # two 256-channel output blocks per tile
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", X3W_CASES, ids=[str(c) for c in X3W_CASES])
+def test_gpu_v9x3_bitwise_equals_v7x3(engine, case):
+    """conv3x3_v9x3 (one 512-thread block per CU owning all 256 output channels of a tile) gives
+    every accumulator the same products in the same order as conv3x3_v7x3 (Bh*Ah, Bl*Ah, Bh*Al per
+    tap), so the whole bf16x3 network must be BITWISE equal on every geometry and batch shape."""
+    import az_amd
+    import net_oracle
+    bs, ci, A, ch, blocks, res, B = case
+    desc = az_amd.NetDesc(bs, ci, ch, blocks, A, 32, 8, 256, res, 0, az_amd.AZ_PREC_BF16X3, B)
+    net = az_amd.HipNeuralNetwork(engine, desc)
+    assert net.trunk_kernel().startswith("conv3x3_v9x3<")
+    net.load_weights(net_oracle.init_blob(desc, seed=57))
+    rng = np.random.default_rng(bs * 11 + B)
+    x = (rng.random((B, ci, bs, bs)) < (0.05 if ci > 16 else 0.25)).astype(np.float32)
+    try:
+        _flags(0x10000204)                # conv3x3_v7x3
+        l7, v7 = net.forward(x)
+        _flags(0x204)                     # the library default: conv3x3_v9x3
+        l9, v9 = net.forward(x)
+    finally:
+        _flags(0x204)
+    print(f"{case}: max|v9x3 - v7x3| logits {np.abs(l9 - l7).max():.3e} value {np.abs(v9 - v7).max():.3e}")
+    assert np.isfinite(l9).all() and np.abs(l9).max() > 0
+    assert np.array_equal(l9, l7) and np.array_equal(v9, v7)
+    net.close()

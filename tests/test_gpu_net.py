@@ -165,7 +165,7 @@ def test_gpu_bf16x3_v7x3_geometries(engine, case):
     desc = az_amd.NetDesc(bs, ci, ch, blocks, A, 32, 8, 256, res, 0, az_amd.AZ_PREC_BF16X3, B)
     net = az_amd.HipNeuralNetwork(engine, desc)
     if ch % 64 == 0:
-        assert net.trunk_kernel().startswith("conv3x3_v7x3<")
+        assert net.trunk_kernel().startswith("conv3x3_v9x3<" if ch % 256 == 0 else "conv3x3_v7x3<")
     blob = net_oracle.init_blob(desc, seed=31)
     net.load_weights(blob)
     x = _rand_planes(B, ci, bs, seed=40 + bs, p=0.05 if ci > 16 else 0.25)
@@ -302,9 +302,10 @@ def test_gpu_c5_net_full_batch(engine):
     ((15, 11, 256, 20, 225, "fp16", 256), "conv3x3_v6<2, 15>"),          # C3 shard at N = 8
     ((15, 11, 64, 6, 225, "fp16", 256), "k_smallnet_g<15, 8, true>"),    # C2: the fused 64-filter forward
     ((15, 11, 64, 6, 225, "bf16x3", 256), "conv3x3_v4<0, 64>"),
-    ((15, 11, 256, 20, 225, "bf16x3", 64), "conv3x3_v7x3<15, SLIM>"),   # the parity precision at C3
-    ((15, 11, 256, 20, 225, "bf16x3", 2048), "conv3x3_v7x3<15, SLIM>"),
-    ((19, 8, 256, 20, 362, "bf16x3", 1024), "conv3x3_v7x3<19, DENSE>"),
+    ((15, 11, 256, 20, 225, "bf16x3", 64), "conv3x3_v9x3<15, SLIM>"),   # the parity precision at C3
+    ((15, 11, 256, 20, 225, "bf16x3", 2048), "conv3x3_v9x3<15, SLIM>"),
+    ((15, 11, 128, 2, 225, "bf16x3", 64), "conv3x3_v7x3<15, SLIM>"),    # 128 channels: the v7 tile
+    ((19, 8, 256, 20, 362, "bf16x3", 1024), "conv3x3_v9x3<19, DENSE>"),
     ((19, 8, 256, 20, 362, "fp16", 1024), "conv3x3_v6<2, 19, DENSE>"),   # C4
     ((15, 11, 32, 2, 225, "f32", 4), "gemm_f32"),
 ])

@@ -139,6 +139,57 @@ def test_torchscript_reader_refuses_foreign_globals(tmp_path):
         az.torchScriptResNet(str(tmp_path / "lin.pt"), az.GameType.GOMOKU)
 
 
+def _archive(path, pkl, extra=()):
+    with zipfile.ZipFile(path, "w", zipfile.ZIP_STORED) as z:
+        z.writestr("arch/data.pkl", pkl)
+        z.writestr("arch/version", "3\n")
+        for name, data in extra:
+            z.writestr(name, data)
+    return str(path)
+
+
+def _tensor_pkl(size, stride):
+    """data.pkl of {'w': _rebuild_tensor_v2(FloatStorage '0' of 6 floats, 0, size, stride, False)}."""
+    def ints(v):
+        return b"(" + b"".join(b"K" + bytes([x]) for x in v) + b"t"
+    persid = b"(X\x07\x00\x00\x00storagectorch\nFloatStorage\nX\x01\x00\x00\x000X\x03\x00\x00\x00cpuK\x06tQ"
+    return (b"\x80\x02}X\x01\x00\x00\x00wctorch._utils\n_rebuild_tensor_v2\n(" + persid + b"K\x00" + ints(size) +
+            ints(stride) + b"\x89tRs.")
+
+
+def test_torchscript_reader_rejects_malformed_archives(tmp_path):
+    """Crafted archives fail with an error instead of reading past a buffer or recursing forever
+    (cpp/src/torchscript_reader.cpp): truncated files, a central-directory name running past the
+    end, a memo PUT on an empty stack, a module whose BUILD state holds itself, a tensor whose
+    stride tuple is shorter than its size tuple, and one that reaches past its storage."""
+    storage = [("arch/data/0", np.arange(6, dtype=np.float32).tobytes())]
+    good = _archive(tmp_path / "good.pt", _tensor_pkl((2, 3), (3, 1)), storage)
+    got = az.readTorchScript(good)
+    assert [k for k, _ in got] == ["w"] and np.array_equal(np.asarray(got[0][1], np.float32).ravel(), np.arange(6))
+    raw = open(good, "rb").read()
+    for cut in (10, 40, len(raw) // 2, len(raw) - 30, len(raw) - 5):
+        p = tmp_path / f"cut{cut}.pt"
+        p.write_bytes(raw[:cut])
+        with pytest.raises(ValueError):
+            az.readTorchScript(str(p))
+    # central-directory entry whose name length points past the end of the file
+    cd = raw.rfind(b"PK\x01\x02")
+    bad = bytearray(raw)
+    bad[cd + 28:cd + 30] = (0xfff0).to_bytes(2, "little")
+    (tmp_path / "name.pt").write_bytes(bytes(bad))
+    with pytest.raises(ValueError):
+        az.readTorchScript(str(tmp_path / "name.pt"))
+    cases = [
+        (b"\x80\x02q\x00.", "empty stack"),                                   # BINPUT with nothing to memoize
+        (b"\x80\x02c__torch__\nM\nq\x00)\x81q\x01}X\x01\x00\x00\x00ah\x01sb.", "nesting"),   # obj.a = obj
+        (_tensor_pkl((2, 3), (1,)), "size / stride"),
+        (_tensor_pkl((2, 3), (4, 1)), "exceeds its storage"),
+    ]
+    for i, (pkl, msg) in enumerate(cases):
+        with pytest.raises(ValueError, match=msg):
+            az.readTorchScript(_archive(tmp_path / f"bad{i}.pt", pkl, storage))
+
+
 def test_export_azw_accepts_torchscript(tmp_path):
     """tools/export_azw.py converts the reference's .pt into the .azw weight file."""
     import struct

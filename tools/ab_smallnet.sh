@@ -6,7 +6,7 @@ O=gpurun_out/${ABTAG:-smab}
 mkdir -p $O
 for r in $(seq 1 ${ROUNDS:-4}); do
   for lib in build_ab build; do
-    AZ_HIP_LIB=$PWD/alphazero-multi-game_amd/$lib/libaz_hip.so timeout -k 10 120 python3 tools/net_bench.py --game gomoku15 ${NBARGS:---channels 64 --blocks 6 --batch 256 --iters 30} > $O/$lib.$r.txt 2>&1 || { echo FAIL $lib; tail -3 $O/$lib.$r.txt; exit 1; }
+    AZ_DIAG_HIP_LIB=$PWD/alphazero-multi-game_amd/$lib/libaz_hip.so timeout -k 10 120 python3 tools/net_bench.py --game gomoku15 ${NBARGS:---channels 64 --blocks 6 --batch 256 --iters 30} > $O/$lib.$r.txt 2>&1 || { echo FAIL $lib; tail -3 $O/$lib.$r.txt; exit 1; }
     echo "$lib $(tail -1 $O/$lib.$r.txt | cut -c1-100)"
   done
 done

@@ -11,7 +11,7 @@ import sys
 import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-os.environ["AZ_HIP_LIB"] = os.path.join(ROOT, "alphazero-multi-game_amd", os.environ.get("AZ_DIAG_DIR", "build_diag"), "libaz_hip.so")
+os.environ["AZ_DIAG_HIP_LIB"] = os.path.join(ROOT, "alphazero-multi-game_amd", os.environ.get("AZ_DIAG_DIR", "build_diag"), "libaz_hip.so")
 sys.path.insert(0, os.path.join(ROOT, "alphazero-multi-game_amd"))
 import az_amd  # noqa: E402
 from az_amd import _lib  # noqa: E402
