@@ -1,9 +1,9 @@
 """the CPU restatement of Dataset::extractExamples + augmentExample
 (oracle/az_oracle.cpp az_oracle_dataset; src/selfplay/dataset.cpp:60-114,245-436).
 
-Pinning: dataset.cpp needs nlohmann_json, which is absent here, so the reference Dataset cannot be
-built and no reference test or fixture holds augmented examples.  The restatement
-is pinned by
+Pinning: since round 4 the restatement is pinned against the reference's own Dataset, built with
+only its JSON functions removed (oracle/build_ref_dataset.sh, tests/test_dataset_reference.py: every
+store bitwise).  Before that, and still checked here, it was pinned by
   * the reference goldens for its inputs: the records are the reference's own self-play games
     (tests/golden/ref_games.json.gz, ref_go_games.json.gz) and the original (s = 0) example of
     every position equals the reference-pinned feature planes of that position;

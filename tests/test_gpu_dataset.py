@@ -182,3 +182,44 @@ def test_gpu_bad_records_fail_loudly(engine):
     with pytest.raises(az_amd.AzError, match="game type"):
         az_amd.Dataset(engine, 2, 8)
     ds.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("augment", [1, 0])
+def test_gpu_dataset_matches_reference_build(engine, augment):
+    """k_dataset_extract + the device store against the REFERENCE Dataset's own output
+    (tests/golden/ref_dataset.npz from oracle/build_ref_dataset.sh; see test_dataset_reference.py):
+    every board group, same rng_ seed, shuffle included -- bitwise; and the getBatch /
+    getRandomSubset / shuffle sequence of the 9x9 group."""
+    import az_amd
+    from test_dataset_reference import REF, groups, same_rows, store
+    for bs, games in groups():
+        ds = az_amd.Dataset(engine, 0, bs, seed=1000 + bs)
+        for r in to_records(records_of(games), bs):
+            ds.addGameRecord(r)
+        E = ds.extractExamples(bool(augment))
+        ref = store(f"b{bs}_a{augment}")
+        assert E == len(ref[0])
+        same_rows(ds.gather(np.arange(E)), ref)
+        ds.close()
+    if not augment:
+        return
+    bs = 9
+    ds = az_amd.Dataset(engine, 0, bs, seed=1234)
+    for r in to_records(records_of(dict(groups())[bs]), bs):
+        ds.addGameRecord(r)
+    E = ds.extractExamples(True)
+    s0 = store("ops_s0")
+    same_rows(ds.gather(np.arange(E)), s0)
+    st, pols, va = ds.getBatch(37)
+    want = tuple(x[REF["ops_batch_idx"]] for x in s0)
+    np.testing.assert_array_equal(bits(st), bits(want[0]))
+    np.testing.assert_array_equal(bits(va), bits(want[3]))
+    for i, p in enumerate(pols):
+        np.testing.assert_array_equal(bits(p), bits(want[1][i, :want[2][i]]))
+    sub = ds.getRandomSubset(5)
+    for i, e in enumerate(sub):
+        np.testing.assert_array_equal(bits(e.state), bits(s0[0][REF["ops_subset_idx"][i]]))
+    ds.shuffle()
+    same_rows(ds.gather(np.arange(E)), tuple(x[REF["ops_shuffled_idx"]] for x in s0))
+    ds.close()
