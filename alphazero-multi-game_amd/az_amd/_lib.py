@@ -138,11 +138,16 @@ def lib():
     return _lib
 
 
+AZ_ERR_ARG, AZ_ERR_HIP, AZ_ERR_OOM, AZ_ERR_CAPACITY, AZ_ERR_STATE, AZ_ERR_RANGE = -1, -2, -3, -4, -5, -6
+
+
 class AzError(RuntimeError):
-    pass
+    def __init__(self, msg, code=0):
+        super().__init__(msg)
+        self.code = code
 
 
 def check(rc):
     if rc != 0:
-        raise AzError(f"az error {rc}: {lib().az_last_error().decode()}")
+        raise AzError(f"az error {rc}: {lib().az_last_error().decode()}", rc)
     return rc

@@ -646,6 +646,7 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_v4(ConvBf16Args p) {
     __syncthreads();
     V4_STAMP(1);
     float* ep = reinterpret_cast<float*>(lds);
+    float vmax = 0.0f;                                 // MODE 2: the largest |output| (the range guard)
     for (int bd = 0; bd < BOARDS; ++bd) {
         if (bd_w == bd) {
 #pragma unroll
@@ -692,6 +693,7 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_v4(ConvBf16Args p) {
                     else if (p.Rhi) val += v4_load<MODE>(rh[e]) + (SPLIT ? bf2f(rl[e]) : 0.0f);
                     if (p.relu) val = val > 0.0f ? val : 0.0f;
                     o[e] = val;
+                    if constexpr (MODE == 2) vmax = __builtin_fmaxf(vmax, __builtin_fabsf(val));
                     oh[e] = v4_store<MODE>(val);
                     if (SPLIT) ol[e] = f2bf(val - bf2f(oh[e]));
                 }
@@ -705,6 +707,7 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_v4(ConvBf16Args p) {
         }
         __syncthreads();
     }
+    if (MODE == 2 && !(vmax <= 65504.0f) && p.ovf) atomicOr(p.ovf, 1);   // fp16 overflow: the engine fails the forward
     V4_STAMP(2);
 }
 
@@ -1380,6 +1383,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_v6(ConvBf16Args p) {
 #pragma unroll
         for (int k = 0; k < ITER; ++k) rq[0][k] = fetch(0, tid + 512 * k);
     }
+    float vmax = 0.0f;                                // fp16: the largest |output| (the range guard)
 #pragma unroll
     for (int pp = 0; pp < 2; ++pp) {
         Res (&rres)[ITER] = rq[pp];
@@ -1420,6 +1424,10 @@ __global__ __launch_bounds__(512, 1) void conv3x3_v6(ConvBf16Args p) {
                 int8_t oq[8];
 #pragma unroll
                 for (int e = 0; e < 8; ++e) o[e] = __builtin_amdgcn_fmed3f(o[e], 0.0f, 3.0e38f);   // ReLU: every g8 conv has one
+                if constexpr (MODE == 2) {
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) vmax = __builtin_fmaxf(vmax, o[e]);
+                }
                 if (p.Cq) {                                // residual-stream output: 16-bit + int8 remainder
 #pragma unroll
                     for (int e = 0; e < 8; ++e) H16::split(o[e], oh[e], oq[e]);
@@ -1446,6 +1454,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_v6(ConvBf16Args p) {
         }
         __syncthreads();
     }
+    if (MODE == 2 && !(vmax <= 65504.0f) && p.ovf) atomicOr(p.ovf, 1);   // fp16 overflow: the engine fails the forward
     V4_STAMP(2);
 }
 
@@ -1725,15 +1734,21 @@ int az_conv_g8_name(const ConvBf16Args& a_in, int mode, char* out, int len) {
 }
 
 // fp32 -> fp16 activations (first trunk input, AZ_PREC_FP16)
-__global__ void k_to_f16(const float* in, uint16_t* out, size_t n, const int* m_limit, int rows_per_sample, int C) {
+__global__ void k_to_f16(const float* in, uint16_t* out, size_t n, const int* m_limit, int rows_per_sample, int C,
+                         int* ovf) {
     size_t lim = n;
     if (m_limit) lim = min(n, (size_t)(*m_limit) * rows_per_sample * C);
-    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < lim; i += (size_t)gridDim.x * blockDim.x)
-        out[i] = v4_store<2>(in[i]);
+    float vmax = 0.0f;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < lim; i += (size_t)gridDim.x * blockDim.x) {
+        const float v = in[i];
+        vmax = __builtin_fmaxf(vmax, __builtin_fabsf(v));
+        out[i] = v4_store<2>(v);
+    }
+    if (!(vmax <= 65504.0f) && ovf) atomicOr(ovf, 1);                // fp16 overflow: the engine fails the forward
 }
 void az_launch_to_f16(const float* in, uint16_t* out, size_t n, const int* m_limit, int rows_per_sample, int C,
-                      hipStream_t st) {
-    hipLaunchKernelGGL(k_to_f16, dim3(2048), dim3(256), 0, st, in, out, n, m_limit, rows_per_sample, C);
+                      hipStream_t st, int* ovf) {
+    hipLaunchKernelGGL(k_to_f16, dim3(2048), dim3(256), 0, st, in, out, n, m_limit, rows_per_sample, C, ovf);
 }
 
 // true when conv3x3_v4 handles this shape

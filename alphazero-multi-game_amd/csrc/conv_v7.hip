@@ -342,6 +342,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_v7(ConvBf16Args p) {
     const __amdgpu_buffer_rsrc_t rh = __builtin_amdgcn_make_buffer_rsrc((void*)p.Rhi, (short)0, 0x7fffffff, 0x00020000);
     const __amdgpu_buffer_rsrc_t rq = __builtin_amdgcn_make_buffer_rsrc((void*)p.Rq, (short)0, 0x7fffffff, 0x00020000);
     const int chl = n0 + wn * 64 + 4 * lg;                // first channel of the lane in tile j = 0
+    float vmax = 0.0f;                                    // fp16: the largest output (the range guard)
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
         const int q = wm * 128 + i * 16 + l16;            // output grid row of the tile
@@ -388,6 +389,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_v7(ConvBf16Args p) {
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 o[k] = __builtin_amdgcn_fmed3f(o[k], 0.0f, 3.0e38f);   // ReLU
+                if constexpr (MODE == 2) vmax = __builtin_fmaxf(vmax, o[k]);
                 if (p.Cq) H::split(o[k], oh[k], oq[k]);
                 else oh[k] = H::from_f(o[k]);
             }
@@ -401,6 +403,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_v7(ConvBf16Args p) {
             }
         }
     }
+    if (MODE == 2 && !(vmax <= 65504.0f) && p.ovf) atomicOr(p.ovf, 1);   // fp16 overflow: the engine fails the forward
 }
 
 // conv3x3_v7x3: the fp32-faithful trunk conv (AZ_PREC_BF16X3) on the v7 tile.
@@ -726,8 +729,10 @@ __global__ __launch_bounds__(256, 1) void conv3x3_v7x3(ConvBf16Args p) {
 //    read fragment by fragment as U2 / U3 release them (64 fragment VGPRs + 128 accumulators:
 //    two waves per SIMD fit the register file);
 //  * epilogue from registers as v7x3.
-template <int HB, int GEO>
+template <int HB, int GEO, int VAR>
 __global__ __launch_bounds__(512, 1) void conv3x3_v9x3(ConvBf16Args p) {
+    constexpr bool MID = VAR & 1;                         // the tap barrier after unit U0 (else at the tap start)
+    constexpr bool SKIP = (VAR & 2) && GEO == GEO_SLIM;   // waves 4-7 skip the SLIM tile's dead 16th fragment
     typedef Geom7<HB, GEO> GM;
     typedef H16<1> H;
     constexpr bool DENSE = GM::DENSE, SLIM = GM::SLIM;
@@ -856,100 +861,129 @@ __global__ __launch_bounds__(512, 1) void conv3x3_v9x3(ConvBf16Args p) {
             }
         }
     };
-    const uint32_t z16 = (SLIM && wm == 1) ? 16 * 16 : 0;  // SLIM: 16th fragment reads all-zero halo rows
-    auto loadA = [&](frag (&x)[4], uint32_t ab, auto tc, auto hc, auto pc) {
-        constexpr int t = decltype(tc)::value, half = decltype(hc)::value, pl = decltype(pc)::value;
-        constexpr int sh = (t / 3) * WG + (t % 3);
-        static_for<0, 4>([&](auto ic) {
-            constexpr int i = decltype(ic)::value;
-            if constexpr (SLIM && half == 1 && i == 3) ds_rd<pl * A_PL + ((half * 4 + i) * 16 + sh) * 16>(x[i], ab + z16);
-            else ds_rd<pl * A_PL + ((half * 4 + i) * 16 + sh) * 16>(x[i], ab);
-        });
-    };
-    auto loadB = [&](frag (&x)[4], uint32_t bs, auto pc) {
-        constexpr int pl = decltype(pc)::value;
-        static_for<0, 4>([&](auto jc) {
-            constexpr int j = decltype(jc)::value;
-            ds_rd<pl * B_PL + j * 256>(x[j], bs);
-        });
-    };
-    auto mma = [&](const frag (&x)[4], const frag (&b)[4], int half) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-                acc[half * 4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], x[i], acc[half * 4 + i][j], 0, 0, 0);
-        }
-    };
-    // row half 1 with the weights b, j-major: after fragment j's four MFMAs, b[j] is reloaded with
-    // plane pl of the next tap's weights (at bn)
-    auto mma_reload = [&](const frag (&x)[4], frag (&b)[4], uint32_t bn, auto pc) {
-        constexpr int pl = decltype(pc)::value;
-        static_for<0, 4>([&](auto jc) {
-            constexpr int j = decltype(jc)::value;
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-                acc[4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], x[i], acc[4 + i][j], 0, 0, 0);
-            __builtin_amdgcn_sched_barrier(0);
-            ds_rd<pl * B_PL + j * 256>(b[j], bn);
-            __builtin_amdgcn_sched_barrier(0);
-        });
-    };
     using I0 = std::integral_constant<int, 0>;
     using I1 = std::integral_constant<int, 1>;
-    loadB(bh, b_lane, I0{});
-    loadB(bl, b_lane, I1{});
-    loadA(aX, a_lane, I0{}, I0{}, I0{});
-
-    for (int c2 = 0; c2 < NCH; c2 += 2) {
-        static_for<0, 18>([&](auto tc18) {
-            constexpr int T = decltype(tc18)::value;
-            constexpr int t = T % 9, tn = (t + 1) % 9;
-            using TC = std::integral_constant<int, t>;
-            using TN = std::integral_constant<int, tn>;
-            const int c = c2 + T / 9;
-            const int s = 9 * c + t;
-            if constexpr (DENSE) asm volatile("" : "+v"(mbits));
-            // tap s's weights and U0's fragments are in registers (required before the barrier lets
-            // tap s+2's DMA into tap s's slot); tap s+1's weights (and at t == 8 the next halo) landed
-            lgkm<0>(aX);
-            lgkm<0>(bh);
-            lgkm<0>(bl);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __builtin_amdgcn_s_barrier();
-            __builtin_amdgcn_sched_barrier(0);
-            if constexpr (t < 3) issueA(t, c + 1 < NCH ? c + 1 : c, (c + 1) & 1);
+    // The main loop, compiled once per row half of the tile (WMC = wm): with SKIP the second half
+    // (waves 4-7) neither reads nor multiplies its 16th fragment, whose rows hold no live outputs
+    // on the SLIM grid -- 1/16 of a SIMD's MFMAs saved without a branch inside the loop.
+    auto main_loop = [&](auto wmc) {
+        constexpr int WMC = decltype(wmc)::value;
+        constexpr int NI1 = (SKIP && WMC == 1) ? 3 : 4;  // fragments of row half 1 this wave computes
+        const uint32_t z16 = (SLIM && wm == 1) ? 16 * 16 : 0;    // SLIM: 16th fragment reads all-zero halo rows
+        auto loadA = [&](frag (&x)[4], uint32_t ab, auto tc, auto hc, auto pc) {
+            constexpr int t = decltype(tc)::value, half = decltype(hc)::value, pl = decltype(pc)::value;
+            constexpr int sh = (t / 3) * WG + (t % 3);
+            static_for<0, 4>([&](auto ic) {
+                constexpr int i = decltype(ic)::value;
+                if constexpr (half == 1 && i >= NI1) return;
+                else if constexpr (SLIM && half == 1 && i == 3) ds_rd<pl * A_PL + ((half * 4 + i) * 16 + sh) * 16>(x[i], ab + z16);
+                else ds_rd<pl * A_PL + ((half * 4 + i) * 16 + sh) * 16>(x[i], ab);
+            });
+        };
+        auto loadB = [&](frag (&x)[4], uint32_t bs, auto pc) {
+            constexpr int pl = decltype(pc)::value;
+            static_for<0, 4>([&](auto jc) {
+                constexpr int j = decltype(jc)::value;
+                ds_rd<pl * B_PL + j * 256>(x[j], bs);
+            });
+        };
+        auto mma = [&](const frag (&x)[4], const frag (&b)[4], auto hc) {
+            constexpr int half = decltype(hc)::value, NI = half == 1 ? NI1 : 4;
+#pragma unroll
+            for (int i = 0; i < NI; ++i) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    acc[half * 4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], x[i], acc[half * 4 + i][j], 0, 0, 0);
+            }
+        };
+        // row half 1 with the weights b, j-major: after fragment j's MFMAs, b[j] is reloaded with
+        // plane pl of the next tap's weights (at bn)
+        auto mma_reload = [&](const frag (&x)[4], frag (&b)[4], uint32_t bn, auto pc) {
+            constexpr int pl = decltype(pc)::value;
+            static_for<0, 4>([&](auto jc) {
+                constexpr int j = decltype(jc)::value;
+#pragma unroll
+                for (int i = 0; i < NI1; ++i)
+                    acc[4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], x[i], acc[4 + i][j], 0, 0, 0);
+                __builtin_amdgcn_sched_barrier(0);
+                ds_rd<pl * B_PL + j * 256>(b[j], bn);
+                __builtin_amdgcn_sched_barrier(0);
+            });
+        };
+        // the tap's DMA: a halo piece pair of chunk c+1 at t < 3 (the last chunk reloads itself into
+        // the free buffer) and the weights of tap s+2 (clamped) into tap s's slot
+        auto dma = [&](int t, int c, int s) {
+            if (t < 3) issueA(t, c + 1 < NCH ? c + 1 : c, (c + 1) & 1);
             issueB(s + 2 < NS ? s + 2 : NS - 1, s & 1);
-            const uint32_t ac = a_lane + (c & 1) * A_BUF;
-            loadA(aY, ac, TC{}, I0{}, I1{});              // U1: lo, row half 0
-            __builtin_amdgcn_sched_barrier(0);
-            maskA(aX, 0, t / 3, t % 3);
-            mma(aX, bh, 0);                               // U0: hi x hi, hi(act) x lo(weights)
-            __builtin_amdgcn_sched_barrier(0);
-            mma(aX, bl, 0);
-            __builtin_amdgcn_sched_barrier(0);
-            lgkm<0>(aY);
-            loadA(aX, ac, TC{}, I1{}, I0{});              // U2: hi, row half 1
-            __builtin_amdgcn_sched_barrier(0);
-            maskA(aY, 0, t / 3, t % 3);
-            mma(aY, bh, 0);                               // U1: lo(act) x hi(weights)
-            __builtin_amdgcn_sched_barrier(0);
-            lgkm<0>(aX);
-            loadA(aY, ac, TC{}, I1{}, I1{});              // U3: lo, row half 1
-            __builtin_amdgcn_sched_barrier(0);
-            maskA(aX, 1, t / 3, t % 3);
-            mma(aX, bh, 1);                               // U2
-            __builtin_amdgcn_sched_barrier(0);
-            const uint32_t bn = b_lane + ((s + 1) & 1) * B_TAP;
-            mma_reload(aX, bl, bn, I1{});                 // U2, releasing bl to tap s+1
-            lgkm<4>(aY);                                  // U3's fragments (the 4 weight reads may fly)
-            const uint32_t an = a_lane + ((t == 8 ? c + 1 : c) & 1) * A_BUF;
-            loadA(aX, an, TN{}, I0{}, I0{});              // next tap's U0
-            __builtin_amdgcn_sched_barrier(0);
-            maskA(aY, 1, t / 3, t % 3);
-            mma_reload(aY, bh, bn, I0{});                 // U3, releasing bh to tap s+1
-        });
-    }
+        };
+        loadB(bh, b_lane, I0{});
+        loadB(bl, b_lane, I1{});
+        loadA(aX, a_lane, I0{}, I0{}, I0{});
+
+        for (int c2 = 0; c2 < NCH; c2 += 2) {
+            static_for<0, 18>([&](auto tc18) {
+                constexpr int T = decltype(tc18)::value;
+                constexpr int t = T % 9, tn = (t + 1) % 9;
+                using TC = std::integral_constant<int, t>;
+                using TN = std::integral_constant<int, tn>;
+                const int c = c2 + T / 9;
+                const int s = 9 * c + t;
+                if constexpr (DENSE) asm volatile("" : "+v"(mbits));
+                // tap s's weights and U0's fragments are in registers
+                lgkm<0>(aX);
+                lgkm<0>(bh);
+                lgkm<0>(bl);
+                if constexpr (!MID) {
+                    // barrier at the tap start: tap s's weight reads are done (its slot may take tap
+                    // s+2), tap s+1's weights (and at t == 8 the next halo) landed in every wave
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    __builtin_amdgcn_s_barrier();
+                    __builtin_amdgcn_sched_barrier(0);
+                    dma(t, c, s);
+                }
+                const uint32_t ac = a_lane + (c & 1) * A_BUF;
+                loadA(aY, ac, TC{}, I0{}, I1{});          // U1: lo, row half 0
+                __builtin_amdgcn_sched_barrier(0);
+                maskA(aX, 0, t / 3, t % 3);
+                mma(aX, bh, I0{});                        // U0: hi x hi, hi(act) x lo(weights)
+                __builtin_amdgcn_sched_barrier(0);
+                mma(aX, bl, I0{});
+                __builtin_amdgcn_sched_barrier(0);
+                lgkm<0>(aY);
+                if constexpr (MID) {
+                    // barrier after U0: every wave's reads of tap s's weights (issued at the end of
+                    // tap s-1) have completed behind U0's MFMAs, so tap s's slot may take tap s+2;
+                    // tap s+1's weights (and at t == 8 the next halo) landed in every wave
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    __builtin_amdgcn_s_barrier();
+                    __builtin_amdgcn_sched_barrier(0);
+                    dma(t, c, s);
+                }
+                loadA(aX, ac, TC{}, I1{}, I0{});          // U2: hi, row half 1
+                __builtin_amdgcn_sched_barrier(0);
+                maskA(aY, 0, t / 3, t % 3);
+                mma(aY, bh, I0{});                        // U1: lo(act) x hi(weights)
+                __builtin_amdgcn_sched_barrier(0);
+                lgkm<0>(aX);
+                loadA(aY, ac, TC{}, I1{}, I1{});          // U3: lo, row half 1
+                __builtin_amdgcn_sched_barrier(0);
+                maskA(aX, 1, t / 3, t % 3);
+                mma(aX, bh, I1{});                        // U2
+                __builtin_amdgcn_sched_barrier(0);
+                const uint32_t bn = b_lane + ((s + 1) & 1) * B_TAP;
+                mma_reload(aX, bl, bn, I1{});             // U2, releasing bl to tap s+1
+                if constexpr (NI1 == 4) lgkm<4>(aY);      // U3's fragments (the 4 weight reads may fly)
+                else asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(aY[0]), "+v"(aY[1]), "+v"(aY[2]) :: "memory");
+                const uint32_t an = a_lane + ((t == 8 ? c + 1 : c) & 1) * A_BUF;
+                loadA(aX, an, TN{}, I0{}, I0{});          // next tap's U0
+                __builtin_amdgcn_sched_barrier(0);
+                maskA(aY, 1, t / 3, t % 3);
+                mma_reload(aY, bh, bn, I0{});             // U3, releasing bh to tap s+1
+            });
+        }
+    };
+    if (SKIP && wm == 1) main_loop(I1{});
+    else main_loop(I0{});
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
 
     // epilogue from the accumulators: residual hi + lo joined in fp32, ReLU, split, streaming stores
@@ -1052,14 +1086,23 @@ static void v7x3_launch_g(const ConvBf16Args& a, hipStream_t st) {
     hipLaunchKernelGGL((conv3x3_v7x3<HB, GEO>), dim3(grid), dim3(256), 0, st, a);
 }
 
+int az_conv_flags();
+// conv3x3_v9x3 variants (A/B measurement): flag 0x20000000 puts the tap barrier at the tap start
+// instead of after unit U0, 0x40000000 keeps the SLIM tile's dead 16th fragment in waves 4-7
 template <int HB, int GEO>
 static void v9x3_launch_g(const ConvBf16Args& a, hipStream_t st) {
     const int boards = a.M / (HB * HB);
     const int tiles = GEO == GEO_DENSE ? (boards * HB * HB + 255) / 256 : boards;
-    hipLaunchKernelGGL((conv3x3_v9x3<HB, GEO>), dim3(tiles * (a.N / 256)), dim3(512), 0, st, a);
+    const int f = az_conv_flags(), var = ((f & 0x20000000) ? 0 : 1) | ((f & 0x40000000) ? 0 : 2);
+    const dim3 grid(tiles * (a.N / 256)), block(512);
+    switch (var) {
+        case 0: hipLaunchKernelGGL((conv3x3_v9x3<HB, GEO, 0>), grid, block, 0, st, a); break;
+        case 1: hipLaunchKernelGGL((conv3x3_v9x3<HB, GEO, 1>), grid, block, 0, st, a); break;
+        case 2: hipLaunchKernelGGL((conv3x3_v9x3<HB, GEO, 2>), grid, block, 0, st, a); break;
+        default: hipLaunchKernelGGL((conv3x3_v9x3<HB, GEO, 3>), grid, block, 0, st, a); break;
+    }
 }
 
-int az_conv_flags();
 // conv3x3_v9x3 takes every bf16x3 trunk layer with N % 256 == 0 unless conv flag 0x10000000
 // selects conv3x3_v7x3 (A/B measurement)
 static bool x3_wide(const ConvBf16Args& a) { return a.N % 256 == 0 && !(az_conv_flags() & 0x10000000); }

@@ -69,7 +69,7 @@ bool az_conv_v7x3_supported(const ConvBf16Args& a);
 int az_conv_v7x3_launch(const ConvBf16Args& a, hipStream_t st);
 int az_conv_x3_name(const ConvBf16Args& a, char* out, int len);
 void az_launch_to_f16(const float* in, uint16_t* out, size_t n, const int* m_limit, int rows_per_sample, int C,
-                      hipStream_t st);
+                      hipStream_t st, int* ovf);
 void az_launch_split_bf16(const float* in, uint16_t* hi, uint16_t* lo, size_t n, const int* m_limit, int rows_per_sample,
                           int C, hipStream_t st);
 
@@ -124,6 +124,32 @@ struct RwBlock {
     const float** outs = nullptr;   // device: the sinks' output buffers
 };
 
+// Sampled kernel timing (az_net_profile / az_search_profile, bench.py's roofline and tree-kernel
+// times): a one-wave kernel on the engine stream writes the 100 MHz device clock (s_memrealtime)
+// into the next slot of a device buffer; a timed interval is the difference of two stamps around
+// the kernels it brackets (same-stream order: each stamp runs after the previous kernel completes).
+// HIP events, used before round 4, never completed under rocprofv3 --pmc counter collection once a
+// selfplay step had recorded them (profiles/r03e_pmc_hang_probe.txt); stamps are ordinary dispatches.
+__global__ void k_clock_stamp(unsigned long long* out) {
+    if (threadIdx.x == 0) out[threadIdx.x] = __builtin_amdgcn_s_memrealtime();   // vector store (lane-indexed)
+}
+struct ProfClock {
+    static constexpr size_t CAP = 1 << 16;      // stamps per profiling session (bench: a few thousand)
+    unsigned long long* d = nullptr;
+    size_t used = 0;
+    bool room(size_t k) const { return d && used + k <= CAP; }
+    void stamp(hipStream_t st) { hipLaunchKernelGGL(k_clock_stamp, dim3(1), dim3(64), 0, st, d + used); ++used; }
+    // the stamps [0, used) on the host, in milliseconds (10 ns ticks)
+    std::vector<double> read_ms() const {
+        std::vector<unsigned long long> h(used);
+        if (used && hipMemcpy(h.data(), d, used * 8, hipMemcpyDeviceToHost) != hipSuccess) h.assign(used, 0);
+        std::vector<double> out(used);
+        for (size_t i = 0; i < used; ++i) out[i] = (double)h[i] * 1e-5;
+        return out;
+    }
+    void release() { if (d) (void)hipFree(d); d = nullptr; used = 0; }
+};
+
 struct az_net {
     az_engine* e = nullptr;
     az_net_desc d{};
@@ -142,10 +168,15 @@ struct az_net {
     float* ws = nullptr;                                // split-K workspace of the FC layers
     float* in_nchw = nullptr;
     int* d_nb = nullptr;
+    int* ovf = nullptr;         // set by the fp16 kernels when an activation leaves the fp16 range (sticky until read)
     uint16_t* zero = nullptr;   // 256 zero bytes: glds source for the board edge
     // k_smallnet (64-filter fp16 nets): [2*blocks+1][9][64][64] fp16 trunk weights incl. the input conv, biases
     uint16_t* sm_W = nullptr;
     uint16_t* sm_Wf = nullptr;                  // the same weights fragment-major (k_smallnet's register path)
+    uint16_t* sm_Wxh = nullptr;                 // bf16 hi / lo parts, fragment-major (k_smallnet_x3, AZ_PREC_BF16X3)
+    uint16_t* sm_Wxl = nullptr;
+    uint16_t* fcx_hi = nullptr;                 // both FC layers' bf16 hi / lo rows (k_fc_heads_x3)
+    uint16_t* fcx_lo = nullptr;
     float* sm_b = nullptr;
     // DDW-RandWire trunk (az_net_create_randwire): d.blocks rand-wire blocks of 32 nodes
     bool rw = false;
@@ -158,8 +189,7 @@ struct az_net {
     std::vector<float> host_blob;   // canonical blob of the loaded weights (az_net_get_weights)
     // profiling: HIP events bracketing the 3x3 trunk of every forward (on the launch stream)
     bool prof = false;
-    std::vector<hipEvent_t> evpool;
-    size_t evused = 0;
+    ProfClock pc;                 // sampled trunk timing (az_net_profile)
     long long prof_launches = 0, prof_forwards = 0;
     long long prof_tick = 0, prof_sampled = 0;    // events on every prof_every()-th forward only
     std::mutex mu;
@@ -173,9 +203,10 @@ extern "C" int az_diag_set_tree_stamps(int game) {
     return 0;
 }
 
-// Profiling events are recorded on one simulation step / forward in AZ_PROF_EVERY (default 16):
-// each hipEventRecord leaves a ~6 us gap on the queue, which at C2 (a ~140 us simulation step)
-// would otherwise inflate the timed loop by a fifth.  Reads scale the sampled times to all steps.
+// Profiling stamps (ProfClock) are recorded on one simulation step / forward in AZ_PROF_EVERY
+// (default 16): every marker on the queue leaves a gap of a few us (round 2 measured ~6 us per HIP
+// event), which at C2 (a ~140 us simulation step) would otherwise inflate the timed loop.  Reads
+// scale the sampled times to all steps.
 static int prof_every() {
     static const int p = getenv("AZ_PROF_EVERY") ? std::max(1, atoi(getenv("AZ_PROF_EVERY"))) : 16;
     return p;
@@ -297,20 +328,18 @@ int net_load(az_net* n, const float* blob) {
     const int F = d.channels, HC = d.head_channels, PP = d.pool * d.pool;
     std::vector<float> W, b;
     const bool split = F % 32 == 0;
-    // k_smallnet weights: every 3x3 layer as [tap][n][c] fp16 over 64 channels (input conv zero-padded)
-    const bool sm = d.precision == AZ_PREC_FP16 && az_smallnet_supported(d.board_size, F, n->cin_pad, d.pool, HC) &&
-                    d.blocks <= az_smallnet_max_blocks();
-    std::vector<uint16_t> smw;
+    // k_smallnet weights: every 3x3 layer as [tap][n][c] over 64 channels (input conv zero-padded):
+    // fp16 for k_smallnet_g, bf16 hi / lo parts for k_smallnet_x3 (AZ_PREC_BF16X3)
+    const bool sm = (d.precision == AZ_PREC_FP16 || d.precision == AZ_PREC_BF16X3) &&
+                    az_smallnet_supported(d.board_size, F, n->cin_pad, d.pool, HC) && d.blocks <= az_smallnet_max_blocks();
+    std::vector<float> smf;
     std::vector<float> smb;
     auto sm_add = [&](const std::vector<float>& Wl, const std::vector<float>& bl, int cl) {
-        const size_t o = smw.size();
-        smw.resize(o + (size_t)9 * F * F, 0);
+        const size_t o = smf.size();
+        smf.resize(o + (size_t)9 * F * F, 0.0f);
         for (int t = 0; t < 9; ++t)
             for (int nn = 0; nn < F; ++nn)
-                for (int c = 0; c < cl; ++c) {
-                    _Float16 h = (_Float16)Wl[((size_t)nn * 9 + t) * cl + c];
-                    std::memcpy(&smw[o + ((size_t)t * F + nn) * F + c], &h, 2);
-                }
+                for (int c = 0; c < cl; ++c) smf[o + ((size_t)t * F + nn) * F + c] = Wl[((size_t)nn * 9 + t) * cl + c];
         smb.insert(smb.end(), bl.begin(), bl.end());
     };
     fold_conv(pc, F, d.in_planes, 3, n->cin_pad, d.conv_bias, W, b);
@@ -323,23 +352,38 @@ int net_load(az_net* n, const float* blob) {
         if (sm) sm_add(W, b, F);
     }
     if (sm) {
-        if (!n->sm_W) { DALLOC(n->sm_W, smw.size()); DALLOC(n->sm_Wf, smw.size()); DALLOC(n->sm_b, smb.size()); }
-        HIPCHK(hipMemcpy(n->sm_W, smw.data(), smw.size() * 2, hipMemcpyHostToDevice));
+        const size_t ne = smf.size();
+        std::vector<uint16_t> smw(ne), smh(ne), sml(ne);
+        for (size_t i = 0; i < ne; ++i) {
+            _Float16 h = (_Float16)smf[i];
+            std::memcpy(&smw[i], &h, 2);
+            smh[i] = f2bf(smf[i]);
+            sml[i] = f2bf(smf[i] - bf2f(smh[i]));
+        }
+        if (!n->sm_W) {
+            DALLOC(n->sm_W, ne); DALLOC(n->sm_Wf, ne); DALLOC(n->sm_Wxh, ne); DALLOC(n->sm_Wxl, ne); DALLOC(n->sm_b, smb.size());
+        }
+        HIPCHK(hipMemcpy(n->sm_W, smw.data(), ne * 2, hipMemcpyHostToDevice));
         // fragment-major: [layer][tap][32-channel chunk kk][16-channel block J][lane][8] -- one MFMA
         // A operand (rows 16 J + lane % 16, channels 32 kk + 8 (lane / 16) ..) is 1 KB contiguous
-        std::vector<uint16_t> smwf(smw.size());
-        const size_t nl = smw.size() / ((size_t)9 * F * F);
-        for (size_t l = 0; l < nl; ++l)
-            for (int t = 0; t < 9; ++t)
-                for (int kk = 0; kk < F / 32; ++kk)
-                    for (int J = 0; J < F / 16; ++J)
-                        for (int ln = 0; ln < 64; ++ln)
-                            for (int e = 0; e < 8; ++e) {
-                                const int nn = 16 * J + (ln & 15), c = 32 * kk + 8 * (ln >> 4) + e;
-                                smwf[((((l * 9 + t) * (F / 32) + kk) * (F / 16) + J) * 64 + ln) * 8 + e] =
-                                    smw[((l * 9 + t) * F + nn) * F + c];
-                            }
-        HIPCHK(hipMemcpy(n->sm_Wf, smwf.data(), smwf.size() * 2, hipMemcpyHostToDevice));
+        auto frag_major = [&](const std::vector<uint16_t>& src) {
+            std::vector<uint16_t> out(ne);
+            const size_t nl = ne / ((size_t)9 * F * F);
+            for (size_t l = 0; l < nl; ++l)
+                for (int t = 0; t < 9; ++t)
+                    for (int kk = 0; kk < F / 32; ++kk)
+                        for (int J = 0; J < F / 16; ++J)
+                            for (int ln = 0; ln < 64; ++ln)
+                                for (int e = 0; e < 8; ++e) {
+                                    const int nn = 16 * J + (ln & 15), c = 32 * kk + 8 * (ln >> 4) + e;
+                                    out[((((l * 9 + t) * (F / 32) + kk) * (F / 16) + J) * 64 + ln) * 8 + e] =
+                                        src[((l * 9 + t) * F + nn) * F + c];
+                                }
+            return out;
+        };
+        HIPCHK(hipMemcpy(n->sm_Wf, frag_major(smw).data(), ne * 2, hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(n->sm_Wxh, frag_major(smh).data(), ne * 2, hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(n->sm_Wxl, frag_major(sml).data(), ne * 2, hipMemcpyHostToDevice));
         HIPCHK(hipMemcpy(n->sm_b, smb.data(), smb.size() * 4, hipMemcpyHostToDevice));
     }
     if (int r = load_heads(n, pc)) return r;
@@ -381,6 +425,30 @@ int load_heads(az_net* n, ParamCursor& pc) {
         W.assign(w, w + d.fc_hidden);
         b.assign(bb, bb + 1);
         if (int r = upload_layer(n->vfc2, W, b, 1, d.fc_hidden, 1, d.fc_hidden, false)) return r;
+    }
+    // both FC layers as one bf16 hi / lo matrix [NC][K] for k_fc_heads_x3: policy rows padded to a
+    // multiple of 64, then the value rows (the partial-column layout of k_fc_finish)
+    {
+        const int K = HC * PP, A = d.action_size, H = d.fc_hidden;
+        const int NTP = (A + 63) / 64, NTV = (H + 63) / 64, NC = (NTP + NTV) * 64;
+        std::vector<float> Wp((size_t)A * K), Wv((size_t)H * K);
+        HIPCHK(hipMemcpy(Wp.data(), n->pfc.W, Wp.size() * 4, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(Wv.data(), n->vfc1.W, Wv.size() * 4, hipMemcpyDeviceToHost));
+        std::vector<uint16_t> hi((size_t)NC * K, 0), lo((size_t)NC * K, 0);
+        auto put = [&](const std::vector<float>& Wm, int rows, int r0) {
+            for (int r = 0; r < rows; ++r)
+                for (int k = 0; k < K; ++k) {
+                    const float w = Wm[(size_t)r * K + k];
+                    const uint16_t h = f2bf(w);
+                    hi[(size_t)(r0 + r) * K + k] = h;
+                    lo[(size_t)(r0 + r) * K + k] = f2bf(w - bf2f(h));
+                }
+        };
+        put(Wp, A, 0);
+        put(Wv, H, NTP * 64);
+        if (!n->fcx_hi) { DALLOC(n->fcx_hi, hi.size()); DALLOC(n->fcx_lo, lo.size()); }
+        HIPCHK(hipMemcpy(n->fcx_hi, hi.data(), hi.size() * 2, hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(n->fcx_lo, lo.data(), lo.size() * 2, hipMemcpyHostToDevice));
     }
     return 0;
 }
@@ -466,7 +534,7 @@ ConvBf16Args x3_conv_args(const az_net* n, const Layer& L, int second, int cur, 
     a.M = B * n->HW; a.N = d.channels; a.C = d.channels; a.H = d.board_size; a.W = d.board_size;
     a.m_limit = nb; a.rows_per_sample = n->HW; a.relu = 1;
     a.a_tail = n->act_elems * 2;
-    a.zero = n->zero;
+    a.zero = n->zero; a.ovf = n->ovf;
     a.stamp = -1;
     return a;
 }
@@ -490,7 +558,7 @@ int net_input_path(const az_net* n) {
     const az_net_desc& d = n->d;
     const int H = d.board_size, F = d.channels, prec = d.precision;
     if (n->rw) return NET_IN_GEMM;   // rand-wire: f32 input conv on x0
-    if (n->sm_W && prec == AZ_PREC_FP16 && d.blocks > 0) return NET_IN_SMALL;
+    if (n->sm_W && (prec == AZ_PREC_FP16 || prec == AZ_PREC_BF16X3) && d.blocks > 0) return NET_IN_SMALL;
     const bool bf = (prec == AZ_PREC_BF16 || prec == AZ_PREC_FP16) && F % 32 == 0;
     if (bf && az_conv_g8_supported(H, H, F, F) && n->in.Wbk_h != nullptr && az_conv_g8_supported(H, H, n->cin_pad, F))
         return NET_IN_G8;
@@ -530,11 +598,11 @@ float* rw_trunk(az_net* n, int B, const int* nb, hipStream_t st) {
             if (d.precision == AZ_PREC_FP16) {
                 // fp16 operands, fp32 accumulation (conv3x3_v4): conv1 -> fp16 t, conv2 -> fp32 y;
                 // the residual stream, routers and SE stay fp32
-                az_launch_to_f16(in, n->hh[0], (size_t)rows * F, nb, HW, F, st);
+                az_launch_to_f16(in, n->hh[0], (size_t)rows * F, nb, HW, F, st, n->ovf);
                 ConvBf16Args a{};
                 a.Ahi = n->hh[0]; a.Bhi = nd.c1.Wh16; a.Bblk = nd.c1.Wbk_h; a.Chi = n->th; a.bias = nd.c1.b;
                 a.M = rows; a.N = F; a.C = F; a.H = H; a.W = H; a.m_limit = nb; a.rows_per_sample = HW; a.relu = 1;
-                a.zero = n->zero; a.stamp = -1;
+                a.zero = n->zero; a.ovf = n->ovf; a.stamp = -1;
                 az_conv_v4_launch(a, 2, st);
                 ConvBf16Args c = a;
                 c.Ahi = n->th; c.Bhi = nd.c2.Wh16; c.Bblk = nd.c2.Wbk_h; c.Chi = n->hh[1]; c.Cf = n->rw_t2; c.bias = nd.c2.b;
@@ -553,7 +621,7 @@ float* rw_trunk(az_net* n, int B, const int* nb, hipStream_t st) {
                 a.Ahi = n->hh[0]; a.Alo = n->hl[0]; a.Bhi = nd.c1.Whi; a.Blo = nd.c1.Wlo; a.Bblk = nd.c1.Wbk_bf;
                 a.Chi = n->th; a.Clo = n->tl; a.bias = nd.c1.b;
                 a.M = rows; a.N = F; a.C = F; a.H = H; a.W = H; a.m_limit = nb; a.rows_per_sample = HW; a.relu = 1;
-                a.zero = n->zero; a.stamp = -1;
+                a.zero = n->zero; a.ovf = n->ovf; a.stamp = -1;
                 az_conv_v4_launch(a, 0, st);
                 ConvBf16Args c = a;
                 c.Ahi = n->th; c.Alo = n->tl; c.Bhi = nd.c2.Whi; c.Blo = nd.c2.Wlo; c.Bblk = nd.c2.Wbk_bf;
@@ -608,34 +676,29 @@ int net_forward(az_net* n, const float* x0, int B, const int* nb, float* logits,
     if (lr && inpath == NET_IN_GEMM) return az_fail(AZ_ERR_ARG, "net_forward: this net cannot read leaf records");
     if (inpath == NET_IN_SMALL) {
         // one launch: input conv, trunk, pool and the two head 1x1 convs (smallnet.hip)
-        hipEvent_t e0 = nullptr, e1 = nullptr;
+        bool sampled = false;
         if (n->prof) {
             n->prof_launches += 2 * d.blocks;    // counted in trunk-conv equivalents (bench.py's per-conv rate)
             n->prof_forwards += 1;
         }
-        if (n->prof && n->prof_tick++ % prof_every() == 0) {
+        if (n->prof && n->prof_tick++ % prof_every() == 0 && n->pc.room(2)) {
             n->prof_sampled += 1;
-            while (n->evpool.size() < n->evused + 2) {
-                hipEvent_t ev;
-                HIPCHK(hipEventCreate(&ev));
-                n->evpool.push_back(ev);
-            }
-            e0 = n->evpool[n->evused]; e1 = n->evpool[n->evused + 1];
-            n->evused += 2;
-            HIPCHK(hipEventRecord(e0, st));
+            sampled = true;
+            n->pc.stamp(st);
         }
         SmallNetArgs sa{};
-        sa.x0 = x0; sa.m_limit = nb;
+        sa.x0 = x0; sa.m_limit = nb; sa.ovf = n->ovf;
         if (lr) {
             if (lr->go) return az_fail(AZ_ERR_ARG, "smallnet: Gomoku leaf records only");
             sa.x0 = nullptr; sa.rec = lr->rec; sa.gidx = lr->gidx; sa.rec_n = lr->n; sa.rec_identity = lr->identity;
         } sa.W = n->sm_W; sa.Wf = n->sm_Wf; sa.bias = n->sm_b;
+        if (prec == AZ_PREC_BF16X3) { sa.Wxh = n->sm_Wxh; sa.Wxl = n->sm_Wxl; }   // k_smallnet_x3
         sa.Wpc = n->pconv.W; sa.bpc = n->pconv.b; sa.Wvc = n->vconv.W; sa.bvc = n->vconv.b;
         sa.pp = n->pp; sa.vp = n->vp;
         sa.H = H; sa.blocks = d.blocks; sa.residual = d.residual; sa.HC = d.head_channels; sa.P = P;
         sa.stamps = az_smallnet_stamps_mode();   // diagnostic phase stamps (az_diag_set_smallnet_stamps)
         if (az_smallnet_launch(sa, B, st)) return az_fail(AZ_ERR_ARG, "smallnet: unsupported shape");
-        if (e1) HIPCHK(hipEventRecord(e1, st));
+        if (sampled) n->pc.stamp(st);
         return net_heads_fc(n, B, nb, logits, value, st);
     }
     if (inpath == NET_IN_G8) {
@@ -653,7 +716,7 @@ int net_forward(az_net* n, const float* x0, int B, const int* nb, float* logits,
         a.bias = n->in.b;
         a.M = rows; a.N = F; a.C = n->cin_pad; a.H = H; a.W = W; a.m_limit = nb; a.rows_per_sample = HW; a.relu = 1;
         a.a_tail = n->act_elems * 2;          // th's zeroed tail sits behind its full capacity
-        a.zero = n->zero;
+        a.zero = n->zero; a.ovf = n->ovf;
         a.stamp = -1;
         if (az_conv_g8_launch(a, mode, st)) return az_fail(AZ_ERR_ARG, "g8 input conv: unsupported shape");
     } else if (g8) {
@@ -665,21 +728,15 @@ int net_forward(az_net* n, const float* x0, int B, const int* nb, float* logits,
     }
     float* h = n->h0;
     float* other = n->h1;
-    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    bool ev1 = false;                    // a sampled forward: the trunk's closing stamp is pending
     if (n->prof && d.blocks > 0) {
         n->prof_launches += 2 * d.blocks;
         n->prof_forwards += 1;
     }
-    if (n->prof && d.blocks > 0 && n->prof_tick++ % prof_every() == 0) {
+    if (n->prof && d.blocks > 0 && n->prof_tick++ % prof_every() == 0 && n->pc.room(2)) {
         n->prof_sampled += 1;
-        while (n->evpool.size() < n->evused + 2) {
-            hipEvent_t ev;
-            HIPCHK(hipEventCreate(&ev));
-            n->evpool.push_back(ev);
-        }
-        ev0 = n->evpool[n->evused]; ev1 = n->evpool[n->evused + 1];
-        n->evused += 2;
-        HIPCHK(hipEventRecord(ev0, st));
+        ev1 = true;
+        n->pc.stamp(st);
     }
     if (n->rw) {
         h = rw_trunk(n, B, nb, st);
@@ -703,8 +760,8 @@ int net_forward(az_net* n, const float* x0, int B, const int* nb, float* logits,
             if (az_conv_v7x3_launch(b2, st)) return az_fail(AZ_ERR_ARG, "bf16x3 trunk conv: unsupported shape");
             cur ^= 1;
         }
-        if (ev1) HIPCHK(hipEventRecord(ev1, st));
-        ev1 = nullptr;
+        if (ev1) n->pc.stamp(st);
+        ev1 = false;
         az_launch_pool_g8(n->hh[cur], reinterpret_cast<const int8_t*>(n->hl[cur]), n->pool, B, F, H, P, nb, 0, st);
     } else {
         const bool split = prec == AZ_PREC_BF16X3;
@@ -721,7 +778,7 @@ int net_forward(az_net* n, const float* x0, int B, const int* nb, float* logits,
                 a.bias = L1.b;
                 a.M = rows; a.N = F; a.C = F; a.H = H; a.W = W; a.m_limit = nb; a.rows_per_sample = HW; a.relu = 1;
                 a.a_tail = n->act_elems * 2;
-                a.zero = n->zero;
+                a.zero = n->zero; a.ovf = n->ovf;
                 a.stamp = 2 * i;
                 if (az_conv_g8_launch(a, mode, st)) return az_fail(AZ_ERR_ARG, "g8 trunk conv: unsupported shape");
                 ConvBf16Args b2 = a;
@@ -734,11 +791,11 @@ int net_forward(az_net* n, const float* x0, int B, const int* nb, float* logits,
                 if (az_conv_g8_launch(b2, mode, st)) return az_fail(AZ_ERR_ARG, "g8 trunk conv: unsupported shape");
                 cur ^= 1;
             }
-            if (ev1) HIPCHK(hipEventRecord(ev1, st));
-            ev1 = nullptr;
+            if (ev1) n->pc.stamp(st);
+            ev1 = false;
             az_launch_pool_g8(n->hh[cur], hq[cur], n->pool, B, F, H, P, nb, mode, st);
         } else {
-        if (f16) az_launch_to_f16(h, n->hh[0], (size_t)rows * F, nb, HW, F, st);
+        if (f16) az_launch_to_f16(h, n->hh[0], (size_t)rows * F, nb, HW, F, st, n->ovf);
         else az_launch_split_bf16(h, n->hh[0], split ? n->hl[0] : nullptr, (size_t)rows * F, nb, HW, F, st);
         int cur = 0;
         for (int i = 0; i < d.blocks; ++i) {
@@ -750,7 +807,7 @@ int net_forward(az_net* n, const float* x0, int B, const int* nb, float* logits,
             a.Chi = n->th; a.Clo = split ? n->tl : nullptr; a.Cf = nullptr;
             a.bias = L1.b; a.Rhi = nullptr; a.Rlo = nullptr;
             a.M = rows; a.N = F; a.C = F; a.H = H; a.W = W; a.m_limit = nb; a.rows_per_sample = HW; a.relu = 1;
-            a.zero = n->zero;
+            a.zero = n->zero; a.ovf = n->ovf;
             a.stamp = 2 * i;
             a.Bblk = f16 ? L1.Wbk_h : L1.Wbk_bf;
             if (f16) a.Bhi = L1.Wh16;
@@ -781,7 +838,7 @@ int net_forward(az_net* n, const float* x0, int B, const int* nb, float* logits,
         if (d.blocks > 0 && !f16) h = other;
         }
     }
-    if (ev1) HIPCHK(hipEventRecord(ev1, st));
+    if (ev1) n->pc.stamp(st);
     if (!g8 && !g8x3) az_launch_pool(h, n->pool, B, H, W, F, P, nb, st);
     const int HC = d.head_channels, HK = HC * PP;
     if (HK % 32 == 0 && n->hpv) {
@@ -812,6 +869,10 @@ int net_heads_fc(az_net* n, int B, const int* nb, float* logits, float* value, h
         fa.part = n->ws; fa.m_limit = nb;
         fa.B = B; fa.K = HK; fa.A = d.action_size; fa.H = d.fc_hidden;
         fa.S = az_fc_heads_splits(d.max_batch, HK, d.action_size, d.fc_hidden);   // from the capacity: batch-size independent
+        if (d.precision != AZ_PREC_F32 && n->fcx_hi) {     // bf16x3 products (fp32-faithful)
+            fa.Wx_hi = n->fcx_hi; fa.Wx_lo = n->fcx_lo;
+            fa.S = az_fc_heads_splits_x3(d.max_batch, HK, d.action_size, d.fc_hidden);
+        }
         az_launch_fc_heads(fa, st);
         HIPCHK(hipGetLastError());
         return 0;
@@ -862,8 +923,7 @@ struct az_search {
     std::vector<int> stones, active, fresh, ply, expanded;
     // az_search_profile
     bool prof = false;
-    std::vector<hipEvent_t> evpool;
-    size_t evused = 0;
+    ProfClock pc;                 // sampled tree-kernel timing (az_search_profile)
     int64_t prof_steps = 0, prof_sampled = 0;
     std::vector<long long> prof_cnt0;
     std::vector<std::mt19937> rng;
@@ -877,24 +937,28 @@ struct az_search {
 
 namespace {
 
+// The fp16 range guard's flag of a net (sticky on the device until read here): AZ_ERR_RANGE once set.
+int check_ovf(az_net* n, int ovf) {
+    if (!ovf) return 0;
+    HIPCHK(hipMemsetAsync(n->ovf, 0, 4, n->e->stream));
+    HIPCHK(hipStreamSynchronize(n->e->stream));
+    return az_fail(AZ_ERR_RANGE, "fp16 activation overflow (|x| > 65504) in the network forward: its outputs are invalid; "
+                                 "use AZ_PREC_BF16X3 for nets with activations of this magnitude");
+}
+
 int check_err(az_search* s) {
-    int err = 0;
+    int err = 0, ovf = 0;
     HIPCHK(hipMemcpyAsync(&err, s->t.err, 4, hipMemcpyDeviceToHost, s->e->stream));
+    if (s->net && s->c.eval_kind == AZ_EVAL_NET) HIPCHK(hipMemcpyAsync(&ovf, s->net->ovf, 4, hipMemcpyDeviceToHost, s->e->stream));
     HIPCHK(hipStreamSynchronize(s->e->stream));
     if (err) return az_fail(AZ_ERR_CAPACITY, "device capacity exceeded (flags 0x%x: 1 node pool, 2 path, 4 prior ring)", err);
+    if (int r = check_ovf(s->net, ovf)) return r;
     return 0;
 }
 
 // One batched step over all games: select -> (network) -> expand/backup.
 // tree-kernel timing (az_search_profile): events around K1 and K3 of simulation steps
-static hipEvent_t prof_event(az_search* s) {
-    if (s->evused >= s->evpool.size()) {
-        hipEvent_t ev;
-        if (hipEventCreate(&ev) != hipSuccess) return nullptr;
-        s->evpool.push_back(ev);
-    }
-    return s->evpool[s->evused++];
-}
+// (clock stamps, ProfClock: four per sampled step -- before / after the selection and the expansion)
 
 // AZ_EVAL_CALLBACK: the leaves that need an evaluation go to the host evaluator as (game, moves
 // from the root, NCHW feature planes); its policies / values come back for k_expand_backup.
@@ -948,10 +1012,10 @@ int search_step(az_search* s, int mode, bool pre = false, bool fuse_next = false
     hipStream_t st = s->e->stream;
     const int G = s->c.n_games;
     s->t.nd = s->arena[s->cur];
-    const bool prof = s->prof && mode == MODE_SIM && s->prof_steps++ % prof_every() == 0;
-    if (prof) HIPCHK(hipEventRecord(prof_event(s), st));
+    const bool prof = s->prof && mode == MODE_SIM && s->prof_steps++ % prof_every() == 0 && s->pc.room(4);
+    if (prof) s->pc.stamp(st);
     if (!pre) az_launch_select(s->t, mode, st);
-    if (prof) HIPCHK(hipEventRecord(prof_event(s), st));
+    if (prof) s->pc.stamp(st);
     if (s->c.eval_kind == AZ_EVAL_CALLBACK) {
         if (int r = host_evaluate(s)) return r;
     }
@@ -981,10 +1045,10 @@ int search_step(az_search* s, int mode, bool pre = false, bool fuse_next = false
         s->net->prof = prof;
         if (r) return r;
     }
-    if (prof) HIPCHK(hipEventRecord(prof_event(s), st));
+    if (prof) s->pc.stamp(st);
     if (fuse_next) az_launch_expand_select(tt, s->t, st);
     else hipLaunchKernelGGL(k_expand_backup, dim3(G), dim3(64), 0, st, tt, mode);
-    if (prof) { HIPCHK(hipEventRecord(prof_event(s), st)); s->prof_sampled += 1; }
+    if (prof) { s->pc.stamp(st); s->prof_sampled += 1; }
     HIPCHK(hipGetLastError());
     return 0;
 }
@@ -1286,6 +1350,8 @@ static int net_create(az_engine* e, const az_net_desc* d, az_net** out, bool rw,
         }
     }
     if (!r) r = dalloc(&n->d_nb, 1);
+    if (!r) r = dalloc(&n->ovf, 1);
+    if (!r && hipMemset(n->ovf, 0, 4) != hipSuccess) r = az_fail(AZ_ERR_HIP, "memset");
     if (!r) r = dalloc(&n->zero, 128);
     if (!r && hipMemset(n->zero, 0, 256) != hipSuccess) r = az_fail(AZ_ERR_HIP, "memset");
     if (r) { az_net_destroy(n); return r; }
@@ -1419,10 +1485,11 @@ void az_net_destroy(az_net* n) {
     F(n->rw_t2); F(n->rw_in); F(n->rw_ws);
     for (Layer* l : ls) { F(l->W); F(l->b); F(l->Whi); F(l->Wlo); F(l->Wh16); F(l->Wbk_bf); F(l->Wbk_h); F(l->Wbk_lo); }
     for (void* p : {(void*)n->x0, (void*)n->h0, (void*)n->h1, (void*)n->t, (void*)n->pool, (void*)n->pp, (void*)n->vp, (void*)n->hpv,
-                    (void*)n->v1, (void*)n->ws, (void*)n->logits, (void*)n->value, (void*)n->soft, (void*)n->in_nchw, (void*)n->d_nb,
+                    (void*)n->v1, (void*)n->ws, (void*)n->logits, (void*)n->value, (void*)n->soft, (void*)n->in_nchw, (void*)n->d_nb, (void*)n->ovf,
                     (void*)n->hh[0], (void*)n->hh[1], (void*)n->hl[0], (void*)n->hl[1], (void*)n->th, (void*)n->tl,
-                    (void*)n->zero, (void*)n->sm_W, (void*)n->sm_Wf, (void*)n->sm_b})
+                    (void*)n->zero, (void*)n->sm_W, (void*)n->sm_Wf, (void*)n->sm_Wxh, (void*)n->sm_Wxl, (void*)n->sm_b, (void*)n->fcx_hi, (void*)n->fcx_lo})
         F(p);
+    n->pc.release();
     delete n;
 }
 
@@ -1523,8 +1590,10 @@ static int net_host_forward(az_net* n, const float* planes, int B, float* logits
     HIPCHK(hipGetLastError());
     if (logits) HIPCHK(hipMemcpyAsync(logits, pol, (size_t)B * A * 4, hipMemcpyDeviceToHost, st));
     if (value) HIPCHK(hipMemcpyAsync(value, n->value, (size_t)B * 4, hipMemcpyDeviceToHost, st));
+    int ovf = 0;
+    HIPCHK(hipMemcpyAsync(&ovf, n->ovf, 4, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
-    return 0;
+    return check_ovf(n, ovf);
 }
 
 int az_net_trunk_kernel(az_net* n, char* name, int len) {
@@ -1539,8 +1608,9 @@ int az_net_trunk_kernel(az_net* n, char* name, int len) {
         return 0;
     }
     if (!bf || d.blocks < 1) { snprintf(name, len, "gemm_f32"); return 0; }
-    if (f16 && az_smallnet_supported(H, F, n->cin_pad, d.pool, d.head_channels) && d.blocks <= az_smallnet_max_blocks()) {
-        snprintf(name, len, "k_smallnet_g<%d, 8, %s>", H, d.residual ? "true" : "false");   // as rocprofv3 names it
+    if ((f16 || prec == AZ_PREC_BF16X3) && az_smallnet_supported(H, F, n->cin_pad, d.pool, d.head_channels) &&
+        d.blocks <= az_smallnet_max_blocks()) {
+        snprintf(name, len, "%s<%d, 8, %s>", f16 ? "k_smallnet_g" : "k_smallnet_x3", H, d.residual ? "true" : "false");   // as rocprofv3 names it
         return 0;
     }
     // the trunk's second conv of a block, as net_forward builds it at the net's capacity
@@ -1562,7 +1632,11 @@ int az_net_profile(az_net* n, int enable) {
     if (!n) return az_fail(AZ_ERR_ARG, "null net");
     std::lock_guard<std::mutex> lk(n->mu);
     n->prof = enable != 0;
-    n->evused = 0; n->prof_launches = 0; n->prof_forwards = 0; n->prof_tick = 0; n->prof_sampled = 0;
+    if (n->prof && !n->pc.d) {
+        HIPCHK(hipSetDevice(n->e->device));
+        if (hipMalloc((void**)&n->pc.d, ProfClock::CAP * 8) != hipSuccess) { n->pc.d = nullptr; return az_fail(AZ_ERR_OOM, "profile clock buffer"); }
+    }
+    n->pc.used = 0; n->prof_launches = 0; n->prof_forwards = 0; n->prof_tick = 0; n->prof_sampled = 0;
     return 0;
 }
 
@@ -1572,11 +1646,8 @@ int az_net_profile_read(az_net* n, double* trunk_ms, int64_t* trunk_launches, in
     HIPCHK(hipSetDevice(n->e->device));
     HIPCHK(hipStreamSynchronize(n->e->stream));
     double ms = 0.0;
-    for (size_t i = 0; i + 1 < n->evused; i += 2) {
-        float t = 0.0f;
-        HIPCHK(hipEventElapsedTime(&t, n->evpool[i], n->evpool[i + 1]));
-        ms += t;
-    }
+    const std::vector<double> t = n->pc.read_ms();
+    for (size_t i = 0; i + 1 < t.size(); i += 2) ms += t[i + 1] - t[i];
     // the sampled forwards' trunk time scaled to every profiled forward
     if (trunk_ms) *trunk_ms = n->prof_sampled ? ms * (double)n->prof_forwards / (double)n->prof_sampled : 0.0;
     if (trunk_launches) *trunk_launches = n->prof_launches;
@@ -1711,7 +1782,7 @@ int az_search_create(az_engine* e, az_net* net, const az_search_cfg* c, az_searc
 }
 
 void az_search_destroy(az_search* s) {
-    if (s) for (hipEvent_t ev : s->evpool) (void)hipEventDestroy(ev);
+    if (s) s->pc.release();
     if (!s) return;
     hipSetDevice(s->e->device);
     auto F = [](const void* p) { if (p) hipFree((void*)p); };
@@ -2295,7 +2366,11 @@ int az_search_profile(az_search* s, int enable) {
     HIPCHK(hipSetDevice(s->e->device));
     HIPCHK(hipStreamSynchronize(s->e->stream));
     s->prof = enable != 0;
-    s->evused = 0;
+    if (s->prof && !s->pc.d && hipMalloc((void**)&s->pc.d, ProfClock::CAP * 8) != hipSuccess) {
+        s->pc.d = nullptr;
+        return az_fail(AZ_ERR_OOM, "profile clock buffer");
+    }
+    s->pc.used = 0;
     s->prof_steps = 0; s->prof_sampled = 0;
     s->prof_cnt0.assign((size_t)s->c.n_games * AZ_NCNT, 0);
     HIPCHK(hipMemcpy(s->prof_cnt0.data(), s->t.cnt, s->prof_cnt0.size() * 8, hipMemcpyDeviceToHost));
@@ -2309,12 +2384,10 @@ int az_search_profile_read(az_search* s, double* select_ms, double* expand_ms, i
     HIPCHK(hipSetDevice(s->e->device));
     HIPCHK(hipStreamSynchronize(s->e->stream));
     double sel = 0.0, exp = 0.0;
-    for (size_t i = 0; i + 3 < s->evused; i += 4) {
-        float a = 0.0f, b = 0.0f;
-        HIPCHK(hipEventElapsedTime(&a, s->evpool[i], s->evpool[i + 1]));
-        HIPCHK(hipEventElapsedTime(&b, s->evpool[i + 2], s->evpool[i + 3]));
-        sel += a;
-        exp += b;
+    const std::vector<double> t = s->pc.read_ms();
+    for (size_t i = 0; i + 3 < t.size(); i += 4) {
+        sel += t[i + 1] - t[i];
+        exp += t[i + 3] - t[i + 2];
     }
     std::vector<long long> c((size_t)s->c.n_games * AZ_NCNT);
     HIPCHK(hipMemcpy(c.data(), s->t.cnt, c.size() * 8, hipMemcpyDeviceToHost));

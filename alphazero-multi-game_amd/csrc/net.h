@@ -45,6 +45,7 @@ struct ConvBf16Args {
     const uint16_t* zero;                       // >= 64 zero bytes (padding source for glds)
     int stamp;                                  // diagnostic builds: launch slot for phase stamps
     int flags;                                  // kernel variant bits (az_diag_set_conv_flags; A/B tests)
+    int* ovf;                                   // fp16 outputs: set to 1 when a value leaves the fp16 range (or null)
 };
 
 // k_smallnet (smallnet.hip): the whole trunk + pool + head 1x1 convs of a 64-filter net, one board per block
@@ -63,6 +64,9 @@ struct SmallNetArgs {
     float* pp; float* vp;           // head feature maps [B][P*P][HC] fp32
     int H, blocks, residual, HC, P;
     int stamps;                     // diagnostic: block 0 writes phase stamps (az_diag_smallnet_stamps)
+    int* ovf;                       // set to 1 when an activation leaves the fp16 range
+    const uint16_t* Wxh;            // AZ_PREC_BF16X3 (k_smallnet_x3): bf16 hi / lo parts of the weights,
+    const uint16_t* Wxl;            // fragment-major as Wf; null = the fp16 kernel
 };
 bool az_smallnet_supported(int H, int C, int cin_pad, int pool, int head_channels);
 int az_smallnet_max_blocks();
@@ -83,8 +87,11 @@ struct FcHeadArgs {
     const int* m_limit;
     int B, K, A, H, S;
     int hc, xs;                                 // head channels; cell stride of pp / vp (xs == hc: contiguous [B][K])
+    const uint16_t* Wx_hi; const uint16_t* Wx_lo;   // bf16x3 (k_fc_heads_x3): [NC][K] hi / lo rows (policy padded
+                                                    // to a multiple of 64, then value), or null (f32 k_fc_heads)
 };
 int az_fc_heads_splits(int B, int K, int A, int H);
+int az_fc_heads_splits_x3(int B, int K, int A, int H);
 void az_launch_fc_heads(const FcHeadArgs& a, hipStream_t st);
 void az_launch_value_head(const float* part, int splits, const float* b1, const float* w2, const float* b2, float* hid,
                           float* value, int B, int H, const int* m_limit, hipStream_t st);

@@ -474,7 +474,7 @@ static void launch_f32(const GemmArgs& p, hipStream_t st) {
 // Both FC heads in two launches: k_fc_heads computes the split-K partials of the policy FC
 // (K -> A logits) and the value FC1 (K -> H hidden) as one GEMM over 64-column tiles of
 // [policy | value] (f32 MFMA v_mfma_f32_16x16x4_f32: every partial a k-ordered fmaf chain, as
-// gemm_f32); k_fc_finish (one block per board) sums the slices in order and finishes both heads
+// gemm_f32); k_fc_finish (one wave per board) sums the slices in order and finishes both heads
 // (bias, ReLU, value FC2, tanh).  Deterministic and batch-position independent.
 typedef float f32x4n __attribute__((ext_vector_type(4)));
 
@@ -538,11 +538,127 @@ __global__ __launch_bounds__(256) void k_fc_heads(FcHeadArgs p) {
         for (int e = 0; e < 4; ++e) part[(size_t)(m0 + 16 * wave + 4 * lg + e) * NC + nt * 64 + 16 * j + l16] = acc[j][e];
 }
 
-// Finish both heads, one block per board: K slices summed in slice order (loads unrolled), biases,
-// the value hidden layer (ReLU) and value = tanh(hid . w2 + b2) with a fixed-order block reduction.
+// k_fc_heads_x3: the same split-K partials as k_fc_heads in the fp32-faithful bf16x3 arithmetic
+// (the FP16 / BF16 / BF16X3 precisions): weights pre-split into bf16 hi / lo rows ([NC][K], policy
+// rows padded to 64, then the value rows; p.Wx_hi / p.Wx_lo), activations split on the fly, every
+// product hi*hi + lo*hi + hi*lo on v_mfma_f32_16x16x32_bf16 with fp32 accumulation -- 16 x the f32
+// MFMA's FLOP per cycle, three MFMAs per product.  256 threads = 4 waves of 32 boards x 32 outputs
+// of a 64 x 64 tile; operands go straight from global memory (L2) into registers, one K step of 32
+// ahead.  Writes k_fc_finish's partial layout.
+typedef __bf16 bf16x8n __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ uint32_t fc_bf16_rne(float f) {
+    uint32_t u = __float_as_uint(f);
+    u += 0x7fffu + ((u >> 16) & 1u);
+    return u >> 16;
+}
+__global__ __launch_bounds__(256) void k_fc_heads_x3(FcHeadArgs p) {
+    const int NTP = (p.A + 63) / 64, NTV = (p.H + 63) / 64, NT = NTP + NTV;
+    const int mt = blockIdx.x / NT, nt = blockIdx.x - mt * NT, sl = blockIdx.y, S = gridDim.y;
+    const int mlim = p.m_limit ? min(p.B, *p.m_limit) : p.B;
+    const int m0 = mt * 64;
+    if (m0 >= mlim) return;
+    const bool pol = nt < NTP;
+    const float* X = pol ? p.pp : p.vp;                // [B][K] (cell stride xs)
+    const int K = p.K, KS = K / S, k0 = sl * KS;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wm = wave >> 1, wn = wave & 1;
+    const int l16 = lane & 15, lg = lane >> 4;
+    // weight rows of the lane: output 16 j + l16 of the wave's 32 (rows of the padded [NC][K] matrices)
+    const uint16_t* wh[2];
+    const uint16_t* wl[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const size_t row = (size_t)nt * 64 + wn * 32 + 16 * j + l16;
+        wh[j] = p.Wx_hi + row * K + 8 * lg;
+        wl[j] = p.Wx_lo + row * K + 8 * lg;
+    }
+    // activation rows of the lane: board 16 i + l16 of the wave's 32 (zero past the batch)
+    const float* xr[2];
+    bool live[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int m = m0 + wm * 32 + 16 * i + l16;
+        live[i] = m < mlim;
+        xr[i] = X + (size_t)(live[i] ? m : 0) * (K / p.hc) * p.xs;
+    }
+    // element k of a board's head map: cell k / hc, channel k % hc (cell stride xs); a lane's 8
+    // consecutive k never straddle a cell (hc % 8 == 0)
+    const int gap = p.xs - p.hc;
+    auto xoff = [&](int k) { return (size_t)k + (size_t)(k / p.hc) * gap; };
+    typedef float f32x8n __attribute__((ext_vector_type(8)));
+    struct Ops { bf16x8n wh[2], wl[2]; f32x8n x[2]; };
+    auto fetch = [&](Ops& o, int k) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            o.wh[j] = *reinterpret_cast<const bf16x8n*>(wh[j] + k);
+            o.wl[j] = *reinterpret_cast<const bf16x8n*>(wl[j] + k);
+        }
+        const size_t xo = xoff(k + 8 * lg);
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const float4 u = *reinterpret_cast<const float4*>(xr[i] + xo), v = *reinterpret_cast<const float4*>(xr[i] + xo + 4);
+            o.x[i] = live[i] ? f32x8n{u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w} : f32x8n{};
+        }
+    };
+    f32x4n acc[2][2] = {};
+    auto step = [&](const Ops& o) {
+        bf16x8n xh[2], xl[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            uint32_t h[4], l[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const float a0 = o.x[i][2 * e], a1 = o.x[i][2 * e + 1];
+                const uint32_t b0 = fc_bf16_rne(a0), b1 = fc_bf16_rne(a1);
+                h[e] = b0 | (b1 << 16);
+                l[e] = fc_bf16_rne(a0 - __uint_as_float(b0 << 16)) | (fc_bf16_rne(a1 - __uint_as_float(b1 << 16)) << 16);
+            }
+            __builtin_memcpy(&xh[i], h, 16);
+            __builtin_memcpy(&xl[i], l, 16);
+        }
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(o.wh[j], xh[i], acc[i][j], 0, 0, 0);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(o.wl[j], xh[i], acc[i][j], 0, 0, 0);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(o.wh[j], xl[i], acc[i][j], 0, 0, 0);
+    };
+    // K steps of 32 in pairs (register double buffer with compile-time roles); KS / 32 is even
+    // except for KS = 32 (handled by the tail)
+    Ops A, B;
+    fetch(A, k0);
+    const int steps = KS / 32;
+    int st = 0;
+    for (; st + 2 <= steps; st += 2) {
+        fetch(B, k0 + 32 * (st + 1));
+        step(A);
+        if (st + 2 < steps) fetch(A, k0 + 32 * (st + 2));
+        step(B);
+    }
+    if (st < steps) step(A);
+    // acc[i][j][e] = partial of board 16 i + l16, output 16 j + 4 lg + e (of the wave's 32 x 32)
+    const int NC = NT * 64, BP = (p.B + 63) / 64 * 64;
+    float* part = p.part + (size_t)sl * BP * NC;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+            *reinterpret_cast<f32x4n*>(part + (size_t)(m0 + wm * 32 + 16 * i + l16) * NC + nt * 64 + wn * 32 + 16 * j + 4 * lg) = acc[i][j];
+}
+
+// Finish both heads, one wave per board (4 boards per block): K slices summed in slice order (loads
+// unrolled), biases, the value hidden layer (ReLU) and value = tanh(hid . w2 + b2), the dot product
+// reduced across the wave by a fixed xor butterfly (deterministic, no block barrier).
 __global__ __launch_bounds__(256) void k_fc_finish(FcHeadArgs p) {
-    const int b = blockIdx.x;
-    if (p.m_limit && b >= *p.m_limit) return;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int b = blockIdx.x * 4 + wave;
+    const int mlim = p.m_limit ? min(p.B, *p.m_limit) : p.B;
+    if (b >= mlim) return;                             // wave-uniform
     const int NTP = (p.A + 63) / 64, NTV = (p.H + 63) / 64, NC = (NTP + NTV) * 64, BP = (p.B + 63) / 64 * 64, S = p.S;
     const float* row = p.part + (size_t)b * NC;
     const size_t sstride = (size_t)BP * NC;
@@ -555,22 +671,26 @@ __global__ __launch_bounds__(256) void k_fc_finish(FcHeadArgs p) {
         for (int s = 0; s < 16; ++s) if (s < S) t += v[s];
         return t;
     };
-    for (int n = threadIdx.x; n < p.A; n += 256) p.logits[(size_t)b * p.A + n] = sum(n) + p.bp[n];
+    for (int n = lane; n < p.A; n += 64) p.logits[(size_t)b * p.A + n] = sum(n) + p.bp[n];
     float d = 0.0f;
-    for (int h = threadIdx.x; h < p.H; h += 256) {
+    for (int h = lane; h < p.H; h += 64) {
         float v = sum(NTP * 64 + h) + p.bv1[h];
         v = v > 0.0f ? v : 0.0f;
         p.hid[(size_t)b * p.H + h] = v;
         d = __builtin_fmaf(v, p.wv2[h], d);
     }
-    __shared__ float red[256];
-    red[threadIdx.x] = d;
-    __syncthreads();
-    for (int w = 128; w > 0; w >>= 1) {
-        if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) p.value[b] = tanhf(red[0] + p.bv2[0]);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) d += __shfl_xor(d, off);
+    if (lane == 0) p.value[b] = tanhf(d + p.bv2[0]);
+}
+
+// k_fc_heads_x3: its tiles run ~5x faster than the f32 ones, so fewer K slices (less partial
+// traffic for k_fc_finish): enough blocks to cover the CUs once, slices of >= 256 K
+int az_fc_heads_splits_x3(int B, int K, int A, int H) {
+    const int tiles = (B + 63) / 64 * ((A + 63) / 64 + (H + 63) / 64);
+    int s = 1;
+    while (s < 16 && tiles * s < 256 && K % (2 * s * 32) == 0 && K / (2 * s) >= 256) s *= 2;
+    return s;
 }
 
 int az_fc_heads_splits(int B, int K, int A, int H) {
@@ -582,8 +702,11 @@ int az_fc_heads_splits(int B, int K, int A, int H) {
 
 void az_launch_fc_heads(const FcHeadArgs& a, hipStream_t st) {
     const int NT = (a.A + 63) / 64 + (a.H + 63) / 64, MT = (a.B + 63) / 64;
-    hipLaunchKernelGGL(k_fc_heads, dim3(MT * NT, a.S), dim3(256), 0, st, a);
-    hipLaunchKernelGGL(k_fc_finish, dim3(a.B), dim3(256), 0, st, a);
+    if (a.Wx_hi && a.Wx_lo && a.hc % 8 == 0 && (a.K / a.S) % 32 == 0)
+        hipLaunchKernelGGL(k_fc_heads_x3, dim3(MT * NT, a.S), dim3(256), 0, st, a);
+    else
+        hipLaunchKernelGGL(k_fc_heads, dim3(MT * NT, a.S), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(k_fc_finish, dim3((a.B + 3) / 4), dim3(256), 0, st, a);
 }
 
 // split-K partial sums only (p.part, p.splits): the caller reduces them

@@ -493,6 +493,15 @@ __device__ __forceinline__ uint32_t pack_f16(float a, float b) {
     const f16x2 h = {(_Float16)a, (_Float16)b};
     return __builtin_bit_cast(uint32_t, h);
 }
+// two fp32 -> bf16, round to nearest even (finite inputs), low half = a
+__device__ __forceinline__ uint32_t pack_bf16(float a, float b) {
+    auto r = [](float f) {
+        uint32_t u = __float_as_uint(f);
+        u += 0x7fffu + ((u >> 16) & 1u);
+        return u >> 16;
+    };
+    return r(a) | (r(b) << 16);
+}
 
 template <int V> using IC = std::integral_constant<int, V>;
 enum { ROLE_IN = 0, ROLE_ODD = 1, ROLE_EVEN = 2 };
@@ -594,6 +603,87 @@ struct SmG {
 
 }  // namespace
 
+
+// The fused forward's tail, shared by k_smallnet_g and k_smallnet_x3: the fp32 residual stream
+// (registers xr) staged in LDS, the adaptive pool, and the two head 1x1 convs (f32 MFMA, exact f32
+// products) with bias + ReLU into pp / vp.  wpre: the transposed head weights prefetched at start.
+template <int HB, int NW, int FPW, int JN, int HWT>
+__device__ __forceinline__ void smallnet_tail(const SmallNetArgs& p, uint8_t* lds, int OS, const f32x4v (&xr)[FPW][JN],
+                                              const float (&wpre)[HWT], int b, int tid, int wp, int l16, int lg, int J0) {
+    typedef Sm2<HB, NW> G;
+    constexpr int NT = G::NT, WG = G::WG;
+    uint8_t* xs = lds;
+    static_for<0, FPW>([&](auto ic) {
+        constexpr int i = decltype(ic)::value;
+        const int q = 16 * (wp + 4 * i) + l16, y = q / WG, x = q - y * WG;
+        if (y < HB && x < HB)
+            static_for<0, JN>([&](auto jc) {
+                constexpr int j = decltype(jc)::value;
+                *reinterpret_cast<f32x4v*>(xs + xs_off(y * HB + x, (16 * (J0 + j) + 4 * lg) >> 2)) = xr[i][j];
+            });
+    });
+    const int P = p.P, PP = P * P, HC = p.HC;
+    constexpr int HO = SF;
+    // the head biases (global loads) in flight during the staging and the pool
+    const int cell = 16 * wp + l16;
+    f32x4v hbias[JN];
+#pragma unroll
+    for (int j = 0; j < JN; ++j) {
+        const int o = 16 * (J0 + j) + 4 * lg;
+        const float* bias = o < HC ? p.bpc + o : p.bvc + (o - HC);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) hbias[j][e] = bias[e];
+    }
+    float* pooled = reinterpret_cast<float*>(lds + OS);
+    float* wt = pooled + SF * 64;
+#pragma unroll
+    for (int k = 0; k < HWT; ++k) wt[tid + NT * k] = wpre[k];
+    for (int i = tid; i < SF * (64 - PP); i += NT) {
+        const int c = i / (64 - PP), cell = PP + (i - c * (64 - PP));
+        pooled[c * 64 + cell] = 0.0f;
+    }
+    sm_stamp(p, 56);
+    __syncthreads();
+    sm_stamp(p, 40);
+    if (P == 8) pool_cells<HB, 8, NT>(xs, pooled, tid);
+    else pool_cells<HB, 0, NT>(xs, pooled, tid, P);
+    sm_stamp(p, 57);
+    __syncthreads();
+    sm_stamp(p, 41);
+    {
+        // every operand read before the first MFMA (one LDS round trip), then the k-ordered chain
+        f32x4v hacc[JN] = {};
+        float pv[SF / 4], wv[SF / 4][JN];
+#pragma unroll
+        for (int kb = 0; kb < SF / 4; ++kb) {
+            const int c = 4 * kb + lg;
+            pv[kb] = pooled[c * 64 + cell];
+#pragma unroll
+            for (int j = 0; j < JN; ++j) wv[kb][j] = wt[c * HO + 16 * (J0 + j) + l16];
+        }
+#pragma unroll
+        for (int kb = 0; kb < SF / 4; ++kb)
+#pragma unroll
+            for (int j = 0; j < JN; ++j) hacc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(wv[kb][j], pv[kb], hacc[j], 0, 0, 0);
+        sm_stamp(p, 58);
+        if (cell < PP) {
+#pragma unroll
+            for (int j = 0; j < JN; ++j) {
+                const int o = 16 * (J0 + j) + 4 * lg;
+                const bool pol = o < HC;
+                const int oc = pol ? o : o - HC;
+                f32x4v v;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const float t = hacc[j][e] + hbias[j][e];
+                    v[e] = t > 0.0f ? t : 0.0f;
+                }
+                *reinterpret_cast<f32x4v*>((pol ? p.pp : p.vp) + ((size_t)b * PP + cell) * HC + oc) = v;
+            }
+        }
+    }
+}
+
 template <int HB, int NW, bool RES>
 __global__ __launch_bounds__(64 * NW, 1) void k_smallnet_g(SmallNetArgs p) {
     typedef Sm2<HB, NW> G;
@@ -605,6 +695,7 @@ __global__ __launch_bounds__(64 * NW, 1) void k_smallnet_g(SmallNetArgs p) {
     const int tid = threadIdx.x, lane = tid & 63;
     const int gq = tid, gy = gq / WG, gx = gq - gy * WG;
     const bool glive = gq < G::NFRAG * 16 && gy < HB && gx < HB;
+    float vmax = 0.0f;                             // largest fp16 activation written (the range guard)
     int rv = 0;
     int meta[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     if (p.rec) {
@@ -770,6 +861,8 @@ __global__ __launch_bounds__(64 * NW, 1) void k_smallnet_g(SmallNetArgs p) {
                             if constexpr (ROLE == ROLE_EVEN && RES) v += xr[i][j];
 #pragma unroll
                             for (int e = 0; e < 4; ++e) v[e] = __builtin_amdgcn_fmed3f(v[e], 0.0f, mlive[i]);
+#pragma unroll
+                            for (int e = 0; e < 4; ++e) vmax = __builtin_fmaxf(vmax, v[e]);
                             if constexpr (ROLE != ROLE_ODD) xr[i][j] = v;
                             ds_wr64<64 * RS * i + 32 * j>(dst, pack_f16(v[0], v[1]), pack_f16(v[2], v[3]));
                         });
@@ -788,81 +881,251 @@ __global__ __launch_bounds__(64 * NW, 1) void k_smallnet_g(SmallNetArgs p) {
         sm_stamp(p, 3 + layer);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // the ring's trailing (clamped) loads
+    if (!(vmax <= 65504.0f) && p.ovf) atomicOr(p.ovf, 1);   // fp16 overflow: the engine fails the forward
     sm_stamp(p, 54);
     __syncthreads();
     sm_stamp(p, 55);
 
-    uint8_t* xs = lds;
-    static_for<0, FPW>([&](auto ic) {
-        constexpr int i = decltype(ic)::value;
-        const int q = 16 * (wp + 4 * i) + l16, y = q / WG, x = q - y * WG;
-        if (y < HB && x < HB)
-            static_for<0, JN>([&](auto jc) {
-                constexpr int j = decltype(jc)::value;
-                *reinterpret_cast<f32x4v*>(xs + xs_off(y * HB + x, (16 * (J0 + j) + 4 * lg) >> 2)) = xr[i][j];
-            });
-    });
-    const int P = p.P, PP = P * P, HC = p.HC;
-    constexpr int HO = SF;
-    // the head biases (global loads) in flight during the staging and the pool
-    const int cell = 16 * wp + l16;
-    f32x4v hbias[JN];
-#pragma unroll
-    for (int j = 0; j < JN; ++j) {
-        const int o = 16 * (J0 + j) + 4 * lg;
-        const float* bias = o < HC ? p.bpc + o : p.bvc + (o - HC);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) hbias[j][e] = bias[e];
+    smallnet_tail<HB, NW>(p, lds, H::OS, xr, wpre, b, tid, wp, l16, lg, J0);
+    sm_stamp(p, 42);
+}
+
+// ------------------------------------------------------------------------------------------------
+// k_smallnet_x3: the fused forward in the fp32-faithful parity precision (AZ_PREC_BF16X3).
+// Every activation is carried as two bf16 planes, hi = bf16(x) and lo = bf16(x - hi), and every
+// weight likewise (fragment-major Wxh / Wxl); a product is hi*hi + lo*hi + hi*lo -- three
+// v_mfma_f32_16x16x32_bf16 per 32-channel step, fp32 accumulation (the arithmetic of conv3x3_v7x3 /
+// conv3x3_v4<0>).  The fp32 residual stream stays in registers as in k_smallnet_g, and the tail
+// (pool, head convs) is the same code.  What differs:
+//  * ONE activation image per plane (hi, lo: 2 x 46.7 KB), updated IN PLACE: a layer's outputs stay
+//    in the accumulators until every wave has read its last input fragment (barrier A), then the
+//    epilogue writes them over the input and barrier B certifies them for the next layer -- two
+//    images per plane (k_smallnet_g's X / Y) would need 187 KB;
+//  * per step a wave reads 2 x FPW activation fragments (hi, lo) one step ahead and holds a 3-step
+//    register ring of 2 x JN weight fragments (hi, lo; a step is 3x the MFMAs of the fp16 kernel,
+//    so three steps cover the L2 latency): 24 MFMAs per step in three sweeps (Wh*Ah, Wl*Ah, Wh*Al),
+//    so an accumulator is reused every JN * FPW = 8 MFMAs;
+//  * layer 0 (the 0/1 input planes, exact in bf16: lo = 0) runs the same three sweeps.
+template <int HB, int NW, bool RES>
+__global__ __launch_bounds__(64 * NW, 1) void k_smallnet_x3(SmallNetArgs p) {
+    typedef Sm2<HB, NW> G;
+    constexpr int NT = G::NT, WG = G::WG, HW = G::HW, FPW = G::FPW, JN = G::JN;
+    constexpr int PW = 3;                                // weight ring depth (steps): 9 and 18 are multiples
+    constexpr int OH = 0, OL = G::IMG, OB = 2 * G::IMG, OS = OB;
+    constexpr int LDS = OB + 2 * SF * SF * 4 > OB + G::MAXL * SF * 4 ? OB + 2 * SF * SF * 4 : OB + G::MAXL * SF * 4;
+    static_assert(LDS <= 160 * 1024, "");
+    typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+    __shared__ __attribute__((aligned(16))) uint8_t lds[LDS];
+    const uint32_t L0 = (uint32_t)(uintptr_t)lds;
+    const int b = blockIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int gq = tid, gy = gq / WG, gx = gq - gy * WG;
+    const bool glive = gq < G::NFRAG * 16 && gy < HB && gx < HB;
+    int rv = 0;
+    int meta[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (p.rec) {
+        const int gi = p.rec_identity ? min(b, p.rec_n - 1) : min(max(p.gidx[b], 0), p.rec_n - 1);
+        const uint8_t* rec = p.rec + (size_t)gi * AZ_REC_BYTES;
+        rv = glive ? rec[gy * HB + gx] : 0;
+        const int4 m0 = *reinterpret_cast<const int4*>(rec + AZ_REC_META);
+        const int4 m1 = *reinterpret_cast<const int4*>(rec + AZ_REC_META + 16);
+        meta[0] = m0.x; meta[1] = m0.y; meta[2] = m0.z; meta[3] = m0.w;
+        meta[4] = m1.x; meta[5] = m1.y; meta[6] = m1.z; meta[7] = m1.w;
     }
-    float* pooled = reinterpret_cast<float*>(lds + H::OS);
-    float* wt = pooled + SF * 64;
+    if (p.m_limit && b >= *p.m_limit) return;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wp = wave & 3;
+    const int J0 = (wave >> 2) * JN;
+    const int l16 = lane & 15, lg = lane >> 4;
+    const int L = 2 * p.blocks + 1;
+    const int NFR = L * 18;                              // weight fragment groups (layer, tap, kk)
+
+    constexpr int HWT = SF * SF / NT;
+    float wpre[HWT];
 #pragma unroll
-    for (int k = 0; k < HWT; ++k) wt[tid + NT * k] = wpre[k];
-    for (int i = tid; i < SF * (64 - PP); i += NT) {
-        const int c = i / (64 - PP), cell = PP + (i - c * (64 - PP));
-        pooled[c * 64 + cell] = 0.0f;
+    for (int k = 0; k < HWT; ++k) {
+        const int i = tid + NT * k, c = i / SF, o = i - c * SF;
+        wpre[k] = o < p.HC ? p.Wpc[o * SF + c] : p.Wvc[(o - p.HC) * SF + c];
     }
-    sm_stamp(p, 56);
-    __syncthreads();
-    sm_stamp(p, 40);
-    if (P == 8) pool_cells<HB, 8, NT>(xs, pooled, tid);
-    else pool_cells<HB, 0, NT>(xs, pooled, tid, P);
-    sm_stamp(p, 57);
-    __syncthreads();
-    sm_stamp(p, 41);
+    constexpr int BPT = (G::MAXL * SF + NT - 1) / NT;
+    float bpre[BPT];
+#pragma unroll
+    for (int k = 0; k < BPT; ++k) {
+        const int i = tid + NT * k;
+        bpre[k] = i < L * SF ? p.bias[i] : 0.0f;
+    }
+    // weight register ring: fwh / fwl[slot][j] = fragment group fg's block J0 + j, hi / lo
+    bf16x8 fwh[PW][JN], fwl[PW][JN];
+    const bf16x8* wsh = reinterpret_cast<const bf16x8*>(p.Wxh) + J0 * 64 + lane;
+    const bf16x8* wsl = reinterpret_cast<const bf16x8*>(p.Wxl) + J0 * 64 + lane;
+    auto wload = [&](auto slotc, int fg) {
+        constexpr int slot = decltype(slotc)::value;
+        const size_t o = (size_t)min(fg, NFR - 1) * (4 * 64);
+        static_for<0, JN>([&](auto jc) {
+            constexpr int j = decltype(jc)::value;
+            fwh[slot][j] = wsh[o + 64 * j];
+            fwl[slot][j] = wsl[o + 64 * j];
+        });
+    };
+    static_for<0, PW>([&](auto xc) { wload(xc, 2 * decltype(xc)::value); });   // layer 0: chunk 0 of taps 0..2
+
     {
-        // every operand read before the first MFMA (one LDS round trip), then the k-ordered chain
-        f32x4v hacc[JN] = {};
-        float pv[SF / 4], wv[SF / 4][JN];
-#pragma unroll
-        for (int kb = 0; kb < SF / 4; ++kb) {
-            const int c = 4 * kb + lg;
-            pv[kb] = pooled[c * 64 + cell];
-#pragma unroll
-            for (int j = 0; j < JN; ++j) wv[kb][j] = wt[c * HO + 16 * (J0 + j) + l16];
+        // zero the halo rows no epilogue writes (both planes), the lo plane of the input chunk, and
+        // write the input planes (0/1: exact in bf16) into the hi plane's first 32 channels
+        constexpr int TOP = WG + 1, BOT0 = G::NFRAG * 16 + WG + 1, NPAD = TOP + (G::IR - BOT0);
+        for (int i = tid; i < 2 * NPAD * 8; i += NT) {
+            const int pl = i / (NPAD * 8), k = i - pl * NPAD * 8, r = k >> 3, c = k & 7;
+            const int row = r < TOP ? r : BOT0 + (r - TOP);
+            *reinterpret_cast<uint4*>(lds + (pl ? OL : OH) + row * RS + c * 16) = uint4{0, 0, 0, 0};
         }
+        if (tid < G::NFRAG * 16) {
+            float c[16];
 #pragma unroll
-        for (int kb = 0; kb < SF / 4; ++kb)
+            for (int k = 0; k < 16; ++k) c[k] = 0.0f;
+            if (glive) {
+                const int px = gy * HB + gx;
+                if (p.rec) {
+                    az_leaf_planes_v(rv, 0, meta, 0, HB, px, c);
+                } else {
+                    const float* x0 = p.x0 + ((size_t)b * HW + px) * 16;
 #pragma unroll
-            for (int j = 0; j < JN; ++j) hacc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(wv[kb][j], pv[kb], hacc[j], 0, 0, 0);
-        sm_stamp(p, 58);
-        if (cell < PP) {
-#pragma unroll
-            for (int j = 0; j < JN; ++j) {
-                const int o = 16 * (J0 + j) + 4 * lg;
-                const bool pol = o < HC;
-                const int oc = pol ? o : o - HC;
-                f32x4v v;
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    const float t = hacc[j][e] + hbias[j][e];
-                    v[e] = t > 0.0f ? t : 0.0f;
+                    for (int k = 0; k < 16; k += 4) {
+                        const float4 u = *reinterpret_cast<const float4*>(x0 + k);
+                        c[k] = u.x; c[k + 1] = u.y; c[k + 2] = u.z; c[k + 3] = u.w;
+                    }
                 }
-                *reinterpret_cast<f32x4v*>((pol ? p.pp : p.vp) + ((size_t)b * PP + cell) * HC + oc) = v;
+            }
+            const int row = gq + WG + 1;
+            uint8_t* dh = lds + OH + row * RS;
+            uint8_t* dl = lds + OL + row * RS;
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const uint4 v = {pack_bf16(c[8 * h], c[8 * h + 1]), pack_bf16(c[8 * h + 2], c[8 * h + 3]),
+                                 pack_bf16(c[8 * h + 4], c[8 * h + 5]), pack_bf16(c[8 * h + 6], c[8 * h + 7])};
+                *reinterpret_cast<uint4*>(dh + 16 * h) = v;
+                *reinterpret_cast<uint4*>(dh + 32 + 16 * h) = uint4{0, 0, 0, 0};
+                *reinterpret_cast<uint4*>(dl + 16 * h) = uint4{0, 0, 0, 0};
+                *reinterpret_cast<uint4*>(dl + 32 + 16 * h) = uint4{0, 0, 0, 0};
             }
         }
+        float* bsm = reinterpret_cast<float*>(lds + OB);
+#pragma unroll
+        for (int k = 0; k < BPT; ++k) {
+            const int i = tid + NT * k;
+            if (i < L * SF) bsm[i] = bpre[k];
+        }
     }
-    sm_stamp(p, 42);
+    __syncthreads();
+
+    // fragment reads and epilogue writes through ordinary LDS pointers (compile-time offsets), so the
+    // compiler orders every read before its MFMA and every write before the barriers itself
+    const uint8_t* aH = lds + OH + (16 * wp + l16) * RS + 16 * lg;
+    const uint8_t* aL = aH + OL;
+    uint8_t* eH = lds + OH + (16 * wp + l16 + WG + 1) * RS + 32 * J0 + 8 * lg;
+    uint8_t* eL = eH + OL;
+    const float* bb = reinterpret_cast<const float*>(lds + OB) + 16 * J0 + 4 * lg;
+    float mlive[FPW];
+#pragma unroll
+    for (int i = 0; i < FPW; ++i) {
+        const int q = 16 * (wp + 4 * i) + l16, y = q / WG, x = q - y * WG;
+        mlive[i] = (y < HB && x < HB) ? __builtin_inff() : 0.0f;
+    }
+
+    f32x4v acc[FPW][JN];
+    f32x4v xr[FPW][JN];
+    f32x4v bn[JN];
+    bf16x8 fbh[2][FPW], fbl[2][FPW];                     // activation fragments (read one step ahead)
+    auto read_bias = [&](int layer) {
+        static_for<0, JN>([&](auto jc) {
+            constexpr int j = decltype(jc)::value;
+            bn[j] = *reinterpret_cast<const f32x4v*>(bb + layer * SF + 16 * j);
+        });
+    };
+    read_bias(0);
+
+    auto run_layer = [&](int layer, auto rolec, auto nchc) {
+        constexpr int ROLE = decltype(rolec)::value, NCH = decltype(nchc)::value;
+        constexpr int NSTEP = 9 * NCH;
+        const int fg0 = layer * 18;
+        auto aload = [&](auto bufc, auto xc) {           // activation fragments of step x, both planes
+            constexpr int buf = decltype(bufc)::value, x = decltype(xc)::value;
+            constexpr int t = x / NCH, kk = x % NCH, sh = (t / 3) * WG + (t % 3);
+            static_for<0, FPW>([&](auto ic) {
+                constexpr int i = decltype(ic)::value, off = 64 * RS * i + RS * sh + 64 * kk;
+                fbh[buf][i] = *reinterpret_cast<const bf16x8*>(aH + off);
+                fbl[buf][i] = *reinterpret_cast<const bf16x8*>(aL + off);
+            });
+        };
+        // sched_barriers keep every load where it is issued (one step ahead for the activation
+        // fragments, PW steps ahead for the weight ring): left alone, the scheduler sinks each load
+        // next to its first MFMA and every step waits out an L2 / LDS round trip
+        aload(IC<0>{}, IC<0>{});
+        static_for<0, NSTEP>([&](auto qc) {
+            constexpr int q = decltype(qc)::value, r = q % 2, ws = q % PW;
+            __builtin_amdgcn_sched_barrier(0);
+            if constexpr (q + 1 < NSTEP) aload(IC<(q + 1) % 2>{}, IC<q + 1>{});
+            if constexpr (q == NSTEP / 2) read_bias(layer + 1);
+            __builtin_amdgcn_sched_barrier(0);
+            static_for<0, FPW>([&](auto ic) {
+                static_for<0, JN>([&](auto jc) {
+                    constexpr int i = decltype(ic)::value, j = decltype(jc)::value;
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fwh[ws][j], fbh[r][i], q == 0 ? bn[j] : acc[i][j], 0, 0, 0);
+                });
+            });
+            static_for<0, FPW>([&](auto ic) {
+                static_for<0, JN>([&](auto jc) {
+                    constexpr int i = decltype(ic)::value, j = decltype(jc)::value;
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fwl[ws][j], fbh[r][i], acc[i][j], 0, 0, 0);
+                });
+            });
+            static_for<0, FPW>([&](auto ic) {
+                static_for<0, JN>([&](auto jc) {
+                    constexpr int i = decltype(ic)::value, j = decltype(jc)::value;
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fwh[ws][j], fbl[r][i], acc[i][j], 0, 0, 0);
+                });
+            });
+            __builtin_amdgcn_sched_barrier(0);
+            {
+                constexpr int ahead_step = q + PW;
+                if constexpr (ahead_step < NSTEP) wload(IC<ws>{}, fg0 + (ahead_step / NCH) * 2 + ahead_step % NCH);
+                else wload(IC<ws>{}, fg0 + 18 + (ahead_step - NSTEP));   // next layer: 2 chunks per tap
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            if constexpr (q == NSTEP - 1) {
+                // barrier A: every wave has read its last input fragment; the outputs go in place
+                __syncthreads();
+                static_for<0, FPW>([&](auto ic) {
+                    static_for<0, JN>([&](auto jc) {
+                        constexpr int i = decltype(ic)::value, j = decltype(jc)::value;
+                        f32x4v v = acc[i][j];
+                        if constexpr (ROLE == ROLE_EVEN && RES) v += xr[i][j];
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) v[e] = __builtin_amdgcn_fmed3f(v[e], 0.0f, mlive[i]);
+                        if constexpr (ROLE != ROLE_ODD) xr[i][j] = v;
+                        uint32_t h[2], l[2];
+#pragma unroll
+                        for (int e = 0; e < 2; ++e) {
+                            const float a0 = v[2 * e], a1 = v[2 * e + 1];
+                            h[e] = pack_bf16(a0, a1);
+                            l[e] = pack_bf16(a0 - __uint_as_float(h[e] << 16), a1 - __uint_as_float(h[e] & 0xffff0000u));
+                        }
+                        constexpr int off = 64 * RS * i + 32 * j;
+                        *reinterpret_cast<uint2*>(eH + off) = uint2{h[0], h[1]};
+                        *reinterpret_cast<uint2*>(eL + off) = uint2{l[0], l[1]};
+                    });
+                });
+                __syncthreads();                         // barrier B: the layer's outputs are in place
+            }
+        });
+    };
+    run_layer(0, IC<ROLE_IN>{}, IC<1>{});
+    for (int layer = 1; layer < L; layer += 2) {
+        run_layer(layer, IC<ROLE_ODD>{}, IC<2>{});
+        run_layer(layer + 1, IC<ROLE_EVEN>{}, IC<2>{});
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // the ring's trailing (clamped) loads
+    __syncthreads();
+    smallnet_tail<HB, NW>(p, lds, OS, xr, wpre, b, tid, wp, l16, lg, J0);
 }
 
 bool az_smallnet_supported(int H, int C, int cin_pad, int pool, int head_channels) {
@@ -876,6 +1139,12 @@ int az_smallnet_launch(const SmallNetArgs& a, int B, hipStream_t st) {
     if (g_sm_kernel == 1) {                              // A/B only: the round-2 kernel
         if (g_sm_waves == 4) hipLaunchKernelGGL((k_smallnet_r2<15, 4>), dim3(B), dim3(256), 0, st, a);
         else hipLaunchKernelGGL((k_smallnet_r2<15, 8>), dim3(B), dim3(512), 0, st, a);
+        return 0;
+    }
+    if (a.Wxh) {                                         // AZ_PREC_BF16X3
+        if (!a.Wxl) return -1;
+        if (a.residual) hipLaunchKernelGGL((k_smallnet_x3<15, 8, true>), dim3(B), dim3(512), 0, st, a);
+        else hipLaunchKernelGGL((k_smallnet_x3<15, 8, false>), dim3(B), dim3(512), 0, st, a);
         return 0;
     }
     if (a.residual) hipLaunchKernelGGL((k_smallnet_g<15, 8, true>), dim3(B), dim3(512), 0, st, a);

@@ -34,7 +34,9 @@ enum az_status {
     AZ_ERR_HIP = -2,       /* HIP runtime error (device missing, launch failure) */
     AZ_ERR_OOM = -3,       /* device allocation failed */
     AZ_ERR_CAPACITY = -4,  /* node pool / prior ring / batch capacity exceeded */
-    AZ_ERR_STATE = -5      /* call not valid in the current state */
+    AZ_ERR_STATE = -5,     /* call not valid in the current state */
+    AZ_ERR_RANGE = -6      /* an AZ_PREC_FP16 activation left the fp16 range (|x| > 65504): the
+                              outputs of that forward / search are invalid; use AZ_PREC_BF16X3 */
 };
 
 typedef struct az_engine az_engine;

@@ -68,6 +68,9 @@ X3W_CASES = [  # board, in_planes, actions, channels, blocks, residual, B: conv3
 ]
 
 
+V9_VARIANTS = [0x204, 0x20000204, 0x40000204, 0x60000204]   # default; tap-start barrier; no fragment skip; both
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("case", X3W_CASES, ids=[str(c) for c in X3W_CASES])
 def test_gpu_v9x3_bitwise_equals_v7x3(engine, case):
@@ -86,11 +89,14 @@ def test_gpu_v9x3_bitwise_equals_v7x3(engine, case):
     try:
         _flags(0x10000204)                # conv3x3_v7x3
         l7, v7 = net.forward(x)
-        _flags(0x204)                     # the library default: conv3x3_v9x3
-        l9, v9 = net.forward(x)
+        outs = {}
+        for fl in V9_VARIANTS:            # conv3x3_v9x3 (0x204: the library default) and its A/B variants
+            _flags(fl)
+            outs[fl] = net.forward(x)
     finally:
         _flags(0x204)
-    print(f"{case}: max|v9x3 - v7x3| logits {np.abs(l9 - l7).max():.3e} value {np.abs(v9 - v7).max():.3e}")
-    assert np.isfinite(l9).all() and np.abs(l9).max() > 0
-    assert np.array_equal(l9, l7) and np.array_equal(v9, v7)
+    for fl, (l9, v9) in outs.items():
+        print(f"{case} flags {fl:#x}: max|v9x3 - v7x3| logits {np.abs(l9 - l7).max():.3e} value {np.abs(v9 - v7).max():.3e}")
+        assert np.isfinite(l9).all() and np.abs(l9).max() > 0
+        assert np.array_equal(l9, l7) and np.array_equal(v9, v7), hex(fl)
     net.close()

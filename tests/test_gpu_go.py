@@ -190,4 +190,12 @@ def test_gpu_c4_full_size_replay(engine):
     idx = np.random.default_rng(1).choice(len(pol), 32, replace=False)
     rl, rv = net_oracle.forward(desc, blob, planes[idx])
     assert np.abs(net_oracle.softmax_policy(rl) - pol[idx]).max() <= 1e-4 and np.abs(rv - valv[idx]).max() <= 1e-4
+    # RAW logits / values of a full B = G forward of the logged leaves (cycled): 16 boards vs fp32
+    xb = planes[np.arange(G) % len(planes)]
+    lo, v = net.forward(xb)
+    jdx = np.unique(np.concatenate([[0, G - 1], np.random.default_rng(2).choice(G, 14, replace=False)]))
+    jl, jv = net_oracle.forward(desc, blob, xb[jdx])
+    el, ev = float(np.abs(lo[jdx] - jl).max()), float(np.abs(v[jdx] - jv).max())
+    print(f"C4 full-size raw outputs: |logit|max {np.abs(jl).max():.3f} max|dlogit|={el:.3e} max|dvalue|={ev:.3e}")
+    assert el <= 1e-4 and ev <= 1e-4
     net.close()

@@ -301,7 +301,7 @@ def test_gpu_c5_net_full_batch(engine):
     ((15, 11, 256, 20, 225, "fp16", 2048), "conv3x3_v7<2, 15, SLIM>"),   # C3 at N = 1, 2
     ((15, 11, 256, 20, 225, "fp16", 256), "conv3x3_v6<2, 15>"),          # C3 shard at N = 8
     ((15, 11, 64, 6, 225, "fp16", 256), "k_smallnet_g<15, 8, true>"),    # C2: the fused 64-filter forward
-    ((15, 11, 64, 6, 225, "bf16x3", 256), "conv3x3_v4<0, 64>"),
+    ((15, 11, 64, 6, 225, "bf16x3", 256), "k_smallnet_x3<15, 8, true>"),   # C2 in the parity precision
     ((15, 11, 256, 20, 225, "bf16x3", 64), "conv3x3_v9x3<15, SLIM>"),   # the parity precision at C3
     ((15, 11, 256, 20, 225, "bf16x3", 2048), "conv3x3_v9x3<15, SLIM>"),
     ((15, 11, 128, 2, 225, "bf16x3", 64), "conv3x3_v7x3<15, SLIM>"),    # 128 channels: the v7 tile
@@ -347,3 +347,33 @@ def test_gpu_smallnet_matches_round2_kernel(engine, residual, B):
     for kw, (pl, v) in outs.items():
         np.testing.assert_array_equal(pl, ref_p, err_msg=f"kernel {kw}")
         np.testing.assert_array_equal(v, ref_v, err_msg=f"kernel {kw}")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("residual", [1, 0])
+@pytest.mark.parametrize("B", [256, 37])
+def test_gpu_smallnet_x3_matches_oracle(engine, residual, B):
+    """k_smallnet_x3 (the fused 64-filter forward in the fp32-faithful bf16x3 precision: hi / lo
+    activation planes updated in place in LDS, three MFMAs per product) on C2-shape nets: within the
+    north-star 1e-4 of the fp32 network on sampled boards, and a board's outputs bitwise the same
+    whatever its batch position (permuted batch, a tail slice)."""
+    import az_amd
+    import net_oracle
+    d = az_amd.NetDesc(15, 11, 64, 6, 225, 32, 8, 256, residual, 0, az_amd.AZ_PREC_BF16X3, 256)
+    net = az_amd.HipNeuralNetwork(engine, d)
+    assert net.trunk_kernel() == f"k_smallnet_x3<15, 8, {'true' if residual else 'false'}>"
+    blob = net_oracle.init_blob(d, seed=91 + residual)
+    net.load_weights(blob)
+    x = _rand_planes(B, 11, 15, 15 + B)
+    lo, v = net.forward(x)
+    pick = np.unique(np.concatenate([[0, B - 1], np.random.default_rng(B).choice(B, 10, replace=False)]))
+    rl, rv = net_oracle.forward(d, blob, x[pick])
+    el, ev = float(np.abs(lo[pick] - rl).max()), float(np.abs(v[pick] - rv).max())
+    print(f"smallnet_x3 residual={residual} B={B}: max|dlogit|={el:.3e} max|dvalue|={ev:.3e}")
+    assert el <= TOL and ev <= TOL
+    perm = np.random.default_rng(3).permutation(B)
+    lo2, v2 = net.forward(x[perm])
+    assert np.array_equal(lo2, lo[perm]) and np.array_equal(v2, v[perm])
+    lo3, v3 = net.forward(x[B - 5:])
+    assert np.array_equal(lo3, lo[B - 5:]) and np.array_equal(v3, v[B - 5:])
+    net.close()

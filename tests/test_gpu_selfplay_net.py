@@ -136,15 +136,19 @@ def _full_size_replay(bs, sims, G, moves, logged, channels, blocks, prec=None, t
     rl, rv = net_oracle.forward(desc, blob, planes[idx])
     assert np.abs(valv[idx] - rv).max() <= 1e-4
     assert np.abs(pol[idx] - net_oracle.softmax_policy(rl)).max() <= 1e-4
+    # RAW logits and values of a full-capacity forward (B = G boards: the logged leaves, cycled) --
+    # post-softmax probabilities of ~1/A each would hide a logit error A times larger
+    xb = planes[np.arange(G) % len(planes)]
+    lo, v = net.forward(xb)
+    jdx = np.unique(np.concatenate([[0, G - 1], np.random.default_rng(1).choice(G, 14, replace=False)]))
+    jl, jv = net_oracle.forward(desc, blob, xb[jdx])
+    el = float(np.abs(lo[jdx] - jl).max())
+    ev = float(np.abs(v[jdx] - jv).max())
+    print(f"full-size raw outputs ({'trained-scale' if trained else 'init'} weights): |logit|max "
+          f"{np.abs(jl).max():.3f} max|dlogit|={el:.3e} max|dvalue|={ev:.3e} over {len(jdx)} boards of B = {G}")
+    assert el <= 1e-4 and ev <= 1e-4
     if trained:
-        # raw logits and values of a full-capacity forward (B = G boards: the logged leaves, cycled)
-        xb = planes[np.arange(G) % len(planes)]
-        lo, v = net.forward(xb)
-        keep = idx < G                                   # xb[i] == planes[i] for i < G
-        el = float(np.abs(lo[idx[keep]] - rl[keep]).max())
-        ev = float(np.abs(v[idx[keep]] - rv[keep]).max())
-        print(f"full-size trained-scale: |logit|max {np.abs(rl).max():.3f} max|dlogit|={el:.3e} max|dvalue|={ev:.3e}")
-        assert np.abs(rl).max() > 2.0 and el <= 1e-4 and ev <= 1e-4
+        assert np.abs(jl).max() > 2.0
     m.close()
     net.close()
 
@@ -172,3 +176,13 @@ def test_gpu_c2_full_size_replay():
     python/simple_export.py's shape family): the first four moves of every game (noise after plies
     0 and 2, subtree reuse across three moves), game 137 replayed."""
     _full_size_replay(bs=15, sims=400, G=256, moves=4, logged=137, channels=64, blocks=6)
+
+
+@pytest.mark.gpu
+def test_gpu_c2_full_size_replay_bf16x3():
+    """C2 at full size in the parity precision (AZ_PREC_BF16X3 on k_smallnet_x3, fed the search's
+    leaf records) with trained-scale heads: four moves of all 256 games, game 137 replayed bit for
+    bit, sampled outputs of the logged leaves and of a B = 256 forward within 1e-4 of fp32."""
+    import az_amd
+    _full_size_replay(bs=15, sims=400, G=256, moves=4, logged=137, channels=64, blocks=6,
+                      prec=az_amd.AZ_PREC_BF16X3, trained=True)

@@ -47,6 +47,65 @@ def trained_scale_blob(desc, seed, x, logit_max=8.0, value_pre_max=1.5):
     return blob
 
 
+def trunk_scaled_blob(desc, seed, x, act_max=64.0, spread=4.0, logit_max=8.0, value_pre_max=1.5):
+    """init_blob reshaped like a TRAINED trunk, not only trained heads: every
+    BN of the trunk gets per-channel output scales drawn log-uniform in [1/spread, spread] (channel
+    magnitudes a decade or two apart, so every dot product mixes large and small terms), and each
+    block's second BN a global gain calibrated on the fp32 network so that the largest activation
+    after block i grows geometrically from 4 to `act_max` over the trunk (O(10-100), the range of a
+    trained AlphaZero trunk; the init weights stay near 1-2).  Then the heads as trained_scale_blob
+    (|logit|max = logit_max, |pre-tanh value| = value_pre_max).  Returns (blob, largest trunk activation)."""
+    import torch
+    import torch.nn.functional as Fn
+    import net_oracle
+    blob = net_oracle.init_blob(desc, seed)
+    o = _offsets(desc)
+    rng = np.random.default_rng(seed + 7)
+    C = desc.channels
+    xt = torch.from_numpy(np.ascontiguousarray(x, np.float32))
+
+    def scale_bn(name, k):
+        for f in ("weight", "bias"):
+            a, n = o[f"{name}.{f}"]
+            blob[a:a + n] *= np.asarray(k, np.float32)
+
+    def conv_bn(h, conv, bn, pad):
+        p = net_oracle.unpack(desc, blob)
+        h = Fn.conv2d(h, p[conv + ".weight"], p.get(conv + ".bias"), padding=pad)
+        return Fn.batch_norm(h, p[bn + ".running_mean"], p[bn + ".running_var"], p[bn + ".weight"], p[bn + ".bias"],
+                             training=False, eps=1e-5)
+
+    spreadk = lambda: np.exp(rng.uniform(-np.log(spread), np.log(spread), C))
+    targets = np.geomspace(4.0, act_max, desc.blocks + 1)
+    amax = 0.0
+    with torch.no_grad():
+        scale_bn("input_bn", spreadk())
+        h = torch.relu(conv_bn(xt, "input_conv", "input_bn", 1))
+        scale_bn("input_bn", np.full(C, targets[0] / float(h.max())))
+        h = torch.relu(conv_bn(xt, "input_conv", "input_bn", 1))
+        amax = float(h.max())
+        for i in range(desc.blocks):
+            scale_bn(f"blocks.{i}.1", spreadk())
+            scale_bn(f"blocks.{i}.4", spreadk())
+            y = torch.relu(conv_bn(h, f"blocks.{i}.0", f"blocks.{i}.1", 1))
+            z = conv_bn(y, f"blocks.{i}.3", f"blocks.{i}.4", 1)
+            for _ in range(4):                     # gain g on the block's branch: max relu(g z + h) -> target
+                cur = float(torch.relu(z + h).max()) if desc.residual else float(torch.relu(z).max())
+                g = targets[i + 1] / max(cur, 1e-6)
+                scale_bn(f"blocks.{i}.4", np.full(C, g))
+                z = z * g
+            h = torch.relu(z + h) if desc.residual else torch.relu(z)
+            amax = max(amax, float(h.max()), float(y.max()))
+    rl, rv = net_oracle.forward(desc, blob, x)
+    kp = logit_max / float(np.abs(rl).max())
+    kv = value_pre_max / float(np.abs(np.arctanh(np.clip(rv, -0.999999, 0.999999))).max())
+    for name, k in (("policy_fc.weight", kp), ("policy_fc.bias", kp), ("value_fc2.weight", kv),
+                    ("value_fc2.bias", kv)):
+        a, n = o[name]
+        blob[a:a + n] *= np.float32(k)
+    return blob, amax
+
+
 def _planes(shape, B, seed):
     rng = np.random.default_rng(seed)
     if shape == "c3" or shape == "c2":
@@ -121,3 +180,90 @@ def test_gpu_trained_scale_production_batch_bf16x3(engine, shape, B):
     assert 7.9 < lmax < 8.1
     assert el <= TOL and ev <= TOL
     net.close()
+
+
+PROD_B = {"c2": 256, "c3": 2048, "c4": 1024, "c5": 1024}   # the BASELINE configs' batch per forward (one GPU)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("prec", ["bf16x3", "fp16"])
+@pytest.mark.parametrize("shape", list(NETS))
+def test_gpu_trunk_scaled_production_batch(engine, shape, prec):
+    """A trained-like TRUNK (trunk_scaled_blob: per-channel BN scales a decade apart, activations
+    growing to O(64) through the blocks) plus trained-scale heads, at each config's production batch
+    (C2 256 -- the bf16x3 64-channel trunk on conv3x3_v4<0, 64>'s one-board blocks --, C3 2048, C4 / C5
+    1024): 16 sampled boards (first, last, 14 between) against the fp32 oracle on RAW logits and
+    values.  bf16x3 must hold the north-star 1e-4; fp16's error is reported (its 11-bit operands
+    cannot hold 1e-4 at |logit| 8) and bounded relative to the largest logit."""
+    import az_amd
+    import net_oracle
+    bs, ci, ch, blocks, A = NETS[shape]
+    B = PROD_B[shape]
+    p = {"bf16x3": az_amd.AZ_PREC_BF16X3, "fp16": az_amd.AZ_PREC_FP16}[prec]
+    desc = az_amd.NetDesc(bs, ci, ch, blocks, A, 32, 8, 256, 1, 0, p, B)
+    x = _planes(shape, B, seed=31)
+    pick = np.unique(np.concatenate([[0, B - 1], np.random.default_rng(6).choice(B, 14, replace=False)]))
+    blob, amax = trunk_scaled_blob(desc, 2468, x[pick])
+    net = az_amd.HipNeuralNetwork(engine, desc)
+    net.load_weights(blob)
+    lo, v = net.forward(x)
+    rl, rv = net_oracle.forward(desc, blob, x[pick])
+    lmax = float(np.abs(rl).max())
+    el, ev = float(np.abs(lo[pick] - rl).max()), float(np.abs(v[pick] - rv).max())
+    print(f"{shape} {prec} B={B} trunk-scaled (max activation {amax:.1f}): |logit|max {lmax:.3f} "
+          f"max|dlogit|={el:.3e} ({el / lmax:.2e} of |logit|max) max|dvalue|={ev:.3e}")
+    assert amax > 30.0 and 7.9 < lmax < 8.1
+    if prec == "fp16":
+        assert el <= 2e-3 * lmax and ev <= 2e-3
+    else:
+        assert el <= TOL and ev <= TOL
+    net.close()
+
+
+OVF_CASES = [  # (board, in_planes, channels, blocks, actions, B, conv flags): every fp16 trunk kernel
+    (15, 11, 64, 2, 225, 8, 0x204),       # k_smallnet_g (C2 shape)
+    (15, 11, 256, 2, 225, 8, 0x204),      # conv3x3_v6 (below 1024 boards)
+    (15, 11, 256, 2, 225, 8, 0xa04),      # conv3x3_v7 (flag 0x800 forces it at any batch)
+    (19, 8, 256, 2, 362, 4, 0x204),       # conv3x3_v6 DENSE (Go)
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", OVF_CASES, ids=[str(c) for c in OVF_CASES])
+def test_gpu_fp16_overflow_fails_loudly(engine, case):
+    """The fp16 range guard: a trunk whose activations exceed the fp16 range (65504) must not
+    return silently wrong outputs -- the forward fails with AZ_ERR_RANGE (AzError) -- while the same
+    trunk at O(64) activations runs, the flag is cleared after it is reported, and the parity
+    precision (bf16x3) takes the overflowing trunk within 1e-4."""
+    import az_amd
+    import net_oracle
+    from az_amd import _lib
+    bs, ci, ch, blocks, A, B, fl = case
+    shape = "c4" if bs == 19 else "c3"
+    x = _planes(shape, B, seed=3)
+    try:
+        _lib.lib().az_diag_set_conv_flags(fl)
+        for act_max, ok in ((64.0, True), (3.0e5, False), (64.0, True)):
+            desc = az_amd.NetDesc(bs, ci, ch, blocks, A, 32, 8, 256, 1, 0, az_amd.AZ_PREC_FP16, B)
+            blob, amax = trunk_scaled_blob(desc, 99, x, act_max=act_max)
+            net = az_amd.HipNeuralNetwork(engine, desc)
+            net.load_weights(blob)
+            if ok:
+                lo, v = net.forward(x)
+                assert np.isfinite(lo).all() and np.isfinite(v).all()
+            else:
+                with pytest.raises(az_amd.AzError, match="fp16 activation overflow") as ei:
+                    net.forward(x)
+                assert ei.value.code == _lib.AZ_ERR_RANGE and amax > 65504
+                with pytest.raises(az_amd.AzError, match="fp16 activation overflow"):
+                    net.forward(x)                       # every overflowing forward is reported
+                dx = az_amd.NetDesc(bs, ci, ch, blocks, A, 32, 8, 256, 1, 0, az_amd.AZ_PREC_BF16X3, B)
+                n3 = az_amd.HipNeuralNetwork(engine, dx)
+                n3.load_weights(blob)
+                l3, v3 = n3.forward(x)
+                rl, rv = net_oracle.forward(dx, blob, x)
+                assert np.abs(l3 - rl).max() <= TOL and np.abs(v3 - rv).max() <= TOL
+                n3.close()
+            net.close()
+    finally:
+        _lib.lib().az_diag_set_conv_flags(0x204)

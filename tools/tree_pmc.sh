@@ -1,9 +1,11 @@
 # rocprofv3 HBM traffic of the tree kernels (k_select, k_expand_backup, the fused k_expand_select,
 # k_scan) and the record -> g8 input kernel (k_rec_to_g8) over one full C3 move (2048 games, 800
 # sims, BLOCKS residual blocks, default 20 = the bench config): a kernel-trace pass (bench.py's own
-# HIP-event timing on, so its JSON line carries the kernels' algorithmic bytes), then FETCH_SIZE and
-# WRITE_SIZE in separate passes with --kernel-timing 0: a search that records HIP events hangs under
-# counter collection (round 3, tools/pmc_hang_probe2.sh; the round-2 "800-sim hang").
+# kernel timing on, so its JSON line carries the kernels' algorithmic bytes), then FETCH_SIZE and
+# WRITE_SIZE in separate passes.  Rounds 2-3 had to pass --kernel-timing 0 there: a search that
+# recorded HIP events hung under counter collection (tools/pmc_hang_probe2.sh); since round 4 the
+# timing uses device clock-stamp kernels instead of events (engine.hip ProfClock), and KT (default 1)
+# keeps the bench's timing on in the counter passes too.
 # --kernel-include-regex is not used (round 2: SIGSEGV in the profiler's launch hook).
 set -o pipefail
 export TMPDIR=/tmp
@@ -22,8 +24,8 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/tra
 ( while sleep 30; do echo "pmc pass running ($(date +%T))"; done ) &
 HB=$!
 trap "kill $HB 2>/dev/null" EXIT
-timeout -s KILL ${PMC_TIMEOUT:-240} rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/fetch -o run -- $CMD --kernel-timing 0 > $O/fetch.log 2>&1 || { echo FAIL fetch; tail -3 $O/fetch.log; exit 1; }
-timeout -s KILL ${PMC_TIMEOUT:-240} rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/write -o run -- $CMD --kernel-timing 0 > $O/write.log 2>&1 || { echo FAIL write; tail -3 $O/write.log; exit 1; }
+timeout -s KILL ${PMC_TIMEOUT:-240} rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/fetch -o run -- $CMD --kernel-timing ${KT:-1} > $O/fetch.log 2>&1 || { echo FAIL fetch; tail -3 $O/fetch.log; exit 1; }
+timeout -s KILL ${PMC_TIMEOUT:-240} rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/write -o run -- $CMD --kernel-timing ${KT:-1} > $O/write.log 2>&1 || { echo FAIL write; tail -3 $O/write.log; exit 1; }
 kill $HB 2>/dev/null
 O=$O SIMS=${SIMS:-800} BLOCKS=${BLOCKS:-20} CONFIG=${CONFIG:-c3} python3 - <<'PY'
 import collections, csv, glob, json, os, re
@@ -51,7 +53,7 @@ for f in glob.glob(f"{O}/trace/**/*kernel_stats.csv", recursive=True):
 wl = ("bench.py --config c2 (C2: 256 games, 400 sims, 6x64 fp16 net; one full move)" if os.environ["CONFIG"] == "c2" else
       f"bench.py --sims {os.environ['SIMS']} --blocks {os.environ['BLOCKS']} (C3 games: 2048, 15x15, 256-filter fp16 net with {os.environ['BLOCKS']} blocks; one full move)")
 out = {"workload": wl,
-       "note": "per dispatch: FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE (KiB -> bytes), counter passes with --kernel-timing 0; average duration from the kernel-trace pass (all dispatches incl. the per-move root steps); algorithmic bytes: the bench line of the trace pass (kernel-counted, sampled steps)"}
+       "note": "per dispatch: FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE (KiB -> bytes), counter passes with the bench kernel timing as KT (1: clock-stamp kernels on); average duration from the kernel-trace pass (all dispatches incl. the per-move root steps); algorithmic bytes: the bench line of the trace pass (kernel-counted, sampled steps)"}
 bl = [l for l in open(f"{O}/trace.log") if l.startswith('{"metric"')]
 if bl:
     tk = json.loads(bl[-1]).get("tree_kernels", {})
