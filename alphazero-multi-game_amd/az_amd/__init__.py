@@ -18,12 +18,12 @@ from dataclasses import dataclass, field
 
 import numpy as np
 
-from ._lib import (AZ_EVAL_CALLBACK, AZ_EVAL_HASH, AZ_EVAL_NET, AZ_EVAL_RANDOM, AZ_EVAL_UNIFORM, EVAL_FN, AZ_PREC_BF16, AZ_PREC_BF16X3, AZ_PREC_F32, AZ_PREC_FP16, AzError,
+from ._lib import (AZ_EVAL_CALLBACK, AZ_EVAL_HASH, AZ_EVAL_NET, AZ_EVAL_RANDOM, AZ_EVAL_UNIFORM, EVAL_FN, AZ_PREC_BF16, AZ_PREC_BF16X3, AZ_PREC_F16X3, AZ_PREC_F32, AZ_PREC_FP16, AzError,
                    GAME_SINK, PROGRESS_FN, MoveRec as _lib_MoveRec, NetDesc, SearchCfg, SelfPlayCfg, check, lib)
 
 __all__ = ["Engine", "HipNeuralNetwork", "ParallelMCTS", "SelfPlayManager", "GameRecord", "MoveData", "AzError",
            "Dataset", "TrainingExample", "GAME_GOMOKU", "GAME_GO",
-           "AZ_PREC_F32", "AZ_PREC_BF16X3", "AZ_PREC_BF16", "AZ_PREC_FP16", "AZ_EVAL_NET", "AZ_EVAL_HASH", "AZ_EVAL_RANDOM", "AZ_EVAL_UNIFORM", "AZ_EVAL_CALLBACK",
+           "AZ_PREC_F32", "AZ_PREC_BF16X3", "AZ_PREC_F16X3", "AZ_PREC_BF16", "AZ_PREC_FP16", "AZ_EVAL_NET", "AZ_EVAL_HASH", "AZ_EVAL_RANDOM", "AZ_EVAL_UNIFORM", "AZ_EVAL_CALLBACK",
            "gomoku_net_desc"]
 
 _f = ctypes.POINTER(ctypes.c_float)

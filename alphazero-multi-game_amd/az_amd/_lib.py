@@ -21,7 +21,7 @@ c_int, c_float, c_size_t, c_uint32, c_uint64, c_int64 = (ctypes.c_int, ctypes.c_
 P = ctypes.POINTER
 vp = ctypes.c_void_p
 
-AZ_PREC_F32, AZ_PREC_BF16X3, AZ_PREC_BF16, AZ_PREC_FP16 = 0, 1, 2, 3
+AZ_PREC_F32, AZ_PREC_BF16X3, AZ_PREC_BF16, AZ_PREC_FP16, AZ_PREC_F16X3 = 0, 1, 2, 3, 4
 AZ_EVAL_NET, AZ_EVAL_HASH, AZ_EVAL_RANDOM, AZ_EVAL_UNIFORM, AZ_EVAL_CALLBACK = 0, 1, 2, 3, 4
 
 

@@ -1487,8 +1487,12 @@ __global__ void k_to_g8(const float* in, uint16_t* hi, int8_t* q, int C, int HW,
     }
 }
 
-// fp32 NHWC [B*HW][C] -> g8 bf16 hi + lo planes (AZ_PREC_BF16X3: hi = bf16(x), lo = bf16(x - hi))
-__global__ void k_to_g8x3(const float* in, uint16_t* hi, uint16_t* lo, int C, int HW, const int* m_limit, int maxB) {
+// fp32 NHWC [B*HW][C] -> g8 hi + lo planes: PT 1 bf16 pieces (AZ_PREC_BF16X3: hi = bf16(x), lo =
+// bf16(x - hi)), PT 2 fp16 pieces (AZ_PREC_F16X3, with the fp16 range guard)
+template <int PT>
+__global__ void k_to_g8x3(const float* in, uint16_t* hi, uint16_t* lo, int C, int HW, const int* m_limit, int maxB,
+                          int* ovf) {
+    float vmax = 0.0f;
     const int G = C / 8;
     const int B = m_limit ? min(*m_limit, maxB) : maxB;
     const size_t total = (size_t)B * G * HW;
@@ -1504,17 +1508,20 @@ __global__ void k_to_g8x3(const float* in, uint16_t* hi, uint16_t* lo, int C, in
         uint16_t h[8], l[8];
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-            h[e] = Half16<1>::from_f(f[e]);
-            l[e] = Half16<1>::from_f(f[e] - Half16<1>::to_f(h[e]));
+            h[e] = Half16<PT>::from_f(f[e]);
+            l[e] = Half16<PT>::from_f(f[e] - Half16<PT>::to_f(h[e]));
+            if (PT == 2) vmax = fmaxf(vmax, fabsf(f[e]));
         }
         *reinterpret_cast<uint4*>(hi + i * 8) = *reinterpret_cast<const uint4*>(h);
         *reinterpret_cast<uint4*>(lo + i * 8) = *reinterpret_cast<const uint4*>(l);
     }
+    if (PT == 2 && !(vmax <= 65504.0f) && ovf) atomicOr(ovf, 1);
 }
 
 void az_launch_to_g8x3(const float* in, uint16_t* hi, uint16_t* lo, int C, int HW, const int* m_limit, int maxB,
-                       hipStream_t st) {
-    hipLaunchKernelGGL(k_to_g8x3, dim3(2048), dim3(256), 0, st, in, hi, lo, C, HW, m_limit, maxB);
+                       hipStream_t st, int pt, int* ovf) {
+    if (pt == 2) hipLaunchKernelGGL(k_to_g8x3<2>, dim3(2048), dim3(256), 0, st, in, hi, lo, C, HW, m_limit, maxB, ovf);
+    else hipLaunchKernelGGL(k_to_g8x3<1>, dim3(2048), dim3(256), 0, st, in, hi, lo, C, HW, m_limit, maxB, ovf);
 }
 
 void az_launch_to_g8(const float* in, uint16_t* hi, int8_t* q, int C, int HW, const int* m_limit, int maxB, int mode,
@@ -1561,7 +1568,7 @@ void az_launch_rec_to_g8(const uint8_t* rec, const int* gidx, uint16_t* hi, int 
 // H*W x 32 values are read once, coalesced per 8-channel group, joined to fp32 in LDS (row stride
 // 36 floats: conflict-free 16-byte writes; H*W*144 B of dynamic LDS), then every output sums its
 // window from LDS in the same order as before (y-major, then x; / kh / kw).
-// MODE 0 (AZ_PREC_BF16X3): q is the bf16 lo plane (uint16 elements), x = hi + lo.
+// MODE 0 (AZ_PREC_BF16X3) / 3 (AZ_PREC_F16X3): q is the bf16 / fp16 lo plane (uint16 elements), x = hi + lo.
 template <int MODE>
 __global__ __launch_bounds__(256) void k_pool_g8(const uint16_t* hi, const int8_t* q, float* out, int C, int H, int P,
                                                  const int* m_limit, int maxB) {
@@ -1577,11 +1584,12 @@ __global__ __launch_bounds__(256) void k_pool_g8(const uint16_t* hi, const int8_
         uint16_t h[8];
         float v[8];
         *reinterpret_cast<uint4*>(h) = *reinterpret_cast<const uint4*>(hi + e);
-        if constexpr (MODE == 0) {
+        if constexpr (MODE == 0 || MODE == 3) {
+            constexpr int PM = MODE == 0 ? 1 : 2;
             uint16_t l[8];
             *reinterpret_cast<uint4*>(l) = *reinterpret_cast<const uint4*>(reinterpret_cast<const uint16_t*>(q) + e);
 #pragma unroll
-            for (int k = 0; k < 8; ++k) v[k] = Half16<1>::to_f(h[k]) + Half16<1>::to_f(l[k]);
+            for (int k = 0; k < 8; ++k) v[k] = Half16<PM>::to_f(h[k]) + Half16<PM>::to_f(l[k]);
         } else {
             int8_t r[8];
             *reinterpret_cast<uint2*>(r) = *reinterpret_cast<const uint2*>(q + e);
@@ -1620,6 +1628,7 @@ void az_launch_pool_g8(const uint16_t* hi, const int8_t* q, float* out, int B, i
     const size_t lds = (size_t)H * H * 36 * sizeof(float);
     if (mode == 2) hipLaunchKernelGGL(k_pool_g8<2>, dim3(grid), dim3(256), lds, st, hi, q, out, C, H, P, m_limit, B);
     else if (mode == 0) hipLaunchKernelGGL(k_pool_g8<0>, dim3(grid), dim3(256), lds, st, hi, q, out, C, H, P, m_limit, B);
+    else if (mode == 3) hipLaunchKernelGGL(k_pool_g8<3>, dim3(grid), dim3(256), lds, st, hi, q, out, C, H, P, m_limit, B);
     else hipLaunchKernelGGL(k_pool_g8<1>, dim3(grid), dim3(256), lds, st, hi, q, out, C, H, P, m_limit, B);
 }
 

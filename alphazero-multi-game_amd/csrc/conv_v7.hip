@@ -63,6 +63,22 @@ struct H16 {                                           // MODE 2: fp16, MODE 1: 
     }
 };
 
+// The split-operand (x3) kernels' piece type: PT 1 = bf16 pieces (AZ_PREC_BF16X3), PT 2 = fp16 pieces
+// (AZ_PREC_F16X3; weights per-output-channel power-of-2 scaled, undone in the epilogue by oscale)
+template <int PT> struct X3T;
+template <> struct X3T<1> {
+    typedef bf16x8 frag;
+    __device__ static f32x4v mma(const frag& b, const frag& a, const f32x4v& c) {
+        return __builtin_amdgcn_mfma_f32_16x16x32_bf16(b, a, c, 0, 0, 0);
+    }
+};
+template <> struct X3T<2> {
+    typedef f16x8 frag;
+    __device__ static f32x4v mma(const frag& b, const frag& a, const f32x4v& c) {
+        return __builtin_amdgcn_mfma_f32_16x16x32_f16(b, a, c, 0, 0, 0);
+    }
+};
+
 __device__ __forceinline__ uint32_t lds_addr(const void* p) { return (uint32_t)(uintptr_t)p; }
 
 template <int OFF, typename F>
@@ -426,12 +442,12 @@ __global__ __launch_bounds__(256, 2) void conv3x3_v7(ConvBf16Args p) {
 //    streaming stores.
 // Input: p.Ahi / p.Alo (g8 hi / lo, both with zeroed tails at p.a_tail), p.Bblk / p.Bblk_lo,
 // residual p.Rhi / p.Rlo (optional), output p.Chi / p.Clo.
-template <int HB, int GEO>
+template <int HB, int GEO, int PT>
 __global__ __launch_bounds__(256, 1) void conv3x3_v7x3(ConvBf16Args p) {
     typedef Geom7<HB, GEO> GM;
-    typedef H16<1> H;
+    typedef H16<PT> H;
     constexpr bool DENSE = GM::DENSE, SLIM = GM::SLIM;
-    typedef bf16x8 frag;
+    typedef typename X3T<PT>::frag frag;
     constexpr int BNT = 128, WG = GM::WG, HW = GM::HW, HROWS = GM::HROWS;
     constexpr int A_PL = 4 * HROWS * 16;                  // one plane of a chunk's halo: 20 KB
     constexpr int A_BUF = 2 * A_PL;                       // hi + lo: 40 KB
@@ -575,7 +591,7 @@ __global__ __launch_bounds__(256, 1) void conv3x3_v7x3(ConvBf16Args p) {
         for (int i = 0; i < 4; ++i) {
 #pragma unroll
             for (int j = 0; j < 4; ++j)
-                acc[half * 4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], x[i], acc[half * 4 + i][j], 0, 0, 0);
+                acc[half * 4 + i][j] = X3T<PT>::mma(b[j], x[i], acc[half * 4 + i][j]);
         }
     };
     using I0 = std::integral_constant<int, 0>;
@@ -654,6 +670,12 @@ __global__ __launch_bounds__(256, 1) void conv3x3_v7x3(ConvBf16Args p) {
     const __amdgpu_buffer_rsrc_t rh = __builtin_amdgcn_make_buffer_rsrc((void*)p.Rhi, (short)0, 0x7fffffff, 0x00020000);
     const __amdgpu_buffer_rsrc_t rl = __builtin_amdgcn_make_buffer_rsrc((void*)p.Rlo, (short)0, 0x7fffffff, 0x00020000);
     const int chl = n0 + wn * 64 + 4 * lg;
+    float4 osc[4];                                        // PT 2: the weights' per-channel scale, undone
+    if constexpr (PT == 2) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) osc[j] = *reinterpret_cast<const float4*>(p.oscale + chl + j * 16);
+    }
+    float vmax = 0.0f;                                    // PT 2: fp16 range guard
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
         const int q = wm * 128 + i * 16 + l16;
@@ -686,6 +708,9 @@ __global__ __launch_bounds__(256, 1) void conv3x3_v7x3(ConvBf16Args p) {
             const int ch = chl + j * 16;
             const size_t e = (((size_t)b * GO + (ch >> 3)) * HW + pix) * 8 + (ch & 7);
             float o[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+            if constexpr (PT == 2) {
+                o[0] *= osc[j].x; o[1] *= osc[j].y; o[2] *= osc[j].z; o[3] *= osc[j].w;
+            }
             if (p.Rhi) {
                 uint16_t hh[4], ll[4];
                 __builtin_memcpy(hh, &hv[j], 8);
@@ -697,6 +722,7 @@ __global__ __launch_bounds__(256, 1) void conv3x3_v7x3(ConvBf16Args p) {
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 o[k] = __builtin_amdgcn_fmed3f(o[k], 0.0f, 3.0e38f);   // ReLU
+                if constexpr (PT == 2) vmax = fmaxf(vmax, o[k]);
                 oh[k] = H::from_f(o[k]);
                 ol[k] = H::from_f(o[k] - H::to_f(oh[k]));
             }
@@ -707,6 +733,7 @@ __global__ __launch_bounds__(256, 1) void conv3x3_v7x3(ConvBf16Args p) {
             asm volatile("global_store_dwordx2 %0, %1, off nt" ::"v"(p.Clo + e), "v"(ls) : "memory");
         }
     }
+    if (PT == 2 && !(vmax <= 65504.0f) && p.ovf) atomicOr(p.ovf, 1);    // fp16 pieces: the engine fails the forward
 }
 
 // conv3x3_v9x3: the fp32-faithful trunk conv on a full-width tile (the default for AZ_PREC_BF16X3
@@ -729,14 +756,14 @@ __global__ __launch_bounds__(256, 1) void conv3x3_v7x3(ConvBf16Args p) {
 //    read fragment by fragment as U2 / U3 release them (64 fragment VGPRs + 128 accumulators:
 //    two waves per SIMD fit the register file);
 //  * epilogue from registers as v7x3.
-template <int HB, int GEO, int VAR>
+template <int HB, int GEO, int VAR, int PT>
 __global__ __launch_bounds__(512, 1) void conv3x3_v9x3(ConvBf16Args p) {
     constexpr bool MID = VAR & 1;                         // the tap barrier after unit U0 (else at the tap start)
     constexpr bool SKIP = (VAR & 2) && GEO == GEO_SLIM;   // waves 4-7 skip the SLIM tile's dead 16th fragment
     typedef Geom7<HB, GEO> GM;
-    typedef H16<1> H;
+    typedef H16<PT> H;
     constexpr bool DENSE = GM::DENSE, SLIM = GM::SLIM;
-    typedef bf16x8 frag;
+    typedef typename X3T<PT>::frag frag;
     constexpr int BNT = 256, WG = GM::WG, HW = GM::HW, HROWS = GM::HROWS;
     constexpr int A_PL = 4 * HROWS * 16;                  // one plane of a chunk's halo: 20 KB
     constexpr int A_BUF = 2 * A_PL;                       // hi + lo: 40 KB
@@ -893,7 +920,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_v9x3(ConvBf16Args p) {
             for (int i = 0; i < NI; ++i) {
 #pragma unroll
                 for (int j = 0; j < 4; ++j)
-                    acc[half * 4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], x[i], acc[half * 4 + i][j], 0, 0, 0);
+                    acc[half * 4 + i][j] = X3T<PT>::mma(b[j], x[i], acc[half * 4 + i][j]);
             }
         };
         // row half 1 with the weights b, j-major: after fragment j's MFMAs, b[j] is reloaded with
@@ -904,7 +931,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_v9x3(ConvBf16Args p) {
                 constexpr int j = decltype(jc)::value;
 #pragma unroll
                 for (int i = 0; i < NI1; ++i)
-                    acc[4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], x[i], acc[4 + i][j], 0, 0, 0);
+                    acc[4 + i][j] = X3T<PT>::mma(b[j], x[i], acc[4 + i][j]);
                 __builtin_amdgcn_sched_barrier(0);
                 ds_rd<pl * B_PL + j * 256>(b[j], bn);
                 __builtin_amdgcn_sched_barrier(0);
@@ -990,6 +1017,12 @@ __global__ __launch_bounds__(512, 1) void conv3x3_v9x3(ConvBf16Args p) {
     const __amdgpu_buffer_rsrc_t rh = __builtin_amdgcn_make_buffer_rsrc((void*)p.Rhi, (short)0, 0x7fffffff, 0x00020000);
     const __amdgpu_buffer_rsrc_t rl = __builtin_amdgcn_make_buffer_rsrc((void*)p.Rlo, (short)0, 0x7fffffff, 0x00020000);
     const int chl = n0 + wn * 64 + 4 * lg;
+    float4 osc[4];                                        // PT 2: the weights' per-channel scale, undone
+    if constexpr (PT == 2) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) osc[j] = *reinterpret_cast<const float4*>(p.oscale + chl + j * 16);
+    }
+    float vmax = 0.0f;                                    // PT 2: fp16 range guard
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
         const int q = wm * 128 + i * 16 + l16;
@@ -1022,6 +1055,9 @@ __global__ __launch_bounds__(512, 1) void conv3x3_v9x3(ConvBf16Args p) {
             const int ch = chl + j * 16;
             const size_t e = (((size_t)b * GO + (ch >> 3)) * HW + pix) * 8 + (ch & 7);
             float o[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+            if constexpr (PT == 2) {
+                o[0] *= osc[j].x; o[1] *= osc[j].y; o[2] *= osc[j].z; o[3] *= osc[j].w;
+            }
             if (p.Rhi) {
                 uint16_t hh[4], ll[4];
                 __builtin_memcpy(hh, &hv[j], 8);
@@ -1033,6 +1069,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_v9x3(ConvBf16Args p) {
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 o[k] = __builtin_amdgcn_fmed3f(o[k], 0.0f, 3.0e38f);   // ReLU
+                if constexpr (PT == 2) vmax = fmaxf(vmax, o[k]);
                 oh[k] = H::from_f(o[k]);
                 ol[k] = H::from_f(o[k] - H::to_f(oh[k]));
             }
@@ -1043,6 +1080,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_v9x3(ConvBf16Args p) {
             asm volatile("global_store_dwordx2 %0, %1, off nt" ::"v"(p.Clo + e), "v"(ls) : "memory");
         }
     }
+    if (PT == 2 && !(vmax <= 65504.0f) && p.ovf) atomicOr(p.ovf, 1);    // fp16 pieces: the engine fails the forward
 }
 
 // Host side ----------------------------------------------------------------------------------
@@ -1071,6 +1109,7 @@ bool az_conv_v7_supported(const ConvBf16Args& a) {
 bool az_conv_v7x3_supported(const ConvBf16Args& a) {
     if (a.H != a.W || a.C % 64 || a.N % 128 || !a.relu || a.Cf || a.Cq || a.Rq) return false;
     if (!a.Ahi || !a.Alo || !a.Bblk || !a.Bblk_lo || !a.Chi || !a.Clo || (!a.Rhi) != (!a.Rlo)) return false;
+    if (a.pt == 2 && !a.oscale) return false;             // fp16 pieces: the weights' per-channel scale
     const int HB = a.H;
     if (HB != 8 && HB != 9 && HB != 13 && HB != 15 && HB != 19) return false;
     const size_t HW = (size_t)HB * HB;
@@ -1083,23 +1122,29 @@ static void v7x3_launch_g(const ConvBf16Args& a, hipStream_t st) {
     const int boards = a.M / (HB * HB);
     const int tiles = GEO == GEO_DENSE ? (boards * HB * HB + 255) / 256 : boards;
     const int grid = (tiles + 7) / 8 * 8 * (a.N / 128);
-    hipLaunchKernelGGL((conv3x3_v7x3<HB, GEO>), dim3(grid), dim3(256), 0, st, a);
+    if (a.pt == 2) hipLaunchKernelGGL((conv3x3_v7x3<HB, GEO, 2>), dim3(grid), dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((conv3x3_v7x3<HB, GEO, 1>), dim3(grid), dim3(256), 0, st, a);
 }
 
 int az_conv_flags();
-// conv3x3_v9x3 variants (A/B measurement): flag 0x20000000 puts the tap barrier at the tap start
-// instead of after unit U0, 0x40000000 keeps the SLIM tile's dead 16th fragment in waves 4-7
+// conv3x3_v9x3 variants (A/B measurement, bf16 pieces): flag 0x20000000 puts the tap barrier at the
+// tap start instead of after unit U0, 0x40000000 keeps the SLIM tile's dead 16th fragment in waves
+// 4-7.  fp16 pieces (AZ_PREC_F16X3) run the default variant only.
 template <int HB, int GEO>
 static void v9x3_launch_g(const ConvBf16Args& a, hipStream_t st) {
     const int boards = a.M / (HB * HB);
     const int tiles = GEO == GEO_DENSE ? (boards * HB * HB + 255) / 256 : boards;
     const int f = az_conv_flags(), var = ((f & 0x20000000) ? 0 : 1) | ((f & 0x40000000) ? 0 : 2);
     const dim3 grid(tiles * (a.N / 256)), block(512);
+    if (a.pt == 2) {
+        hipLaunchKernelGGL((conv3x3_v9x3<HB, GEO, 3, 2>), grid, block, 0, st, a);
+        return;
+    }
     switch (var) {
-        case 0: hipLaunchKernelGGL((conv3x3_v9x3<HB, GEO, 0>), grid, block, 0, st, a); break;
-        case 1: hipLaunchKernelGGL((conv3x3_v9x3<HB, GEO, 1>), grid, block, 0, st, a); break;
-        case 2: hipLaunchKernelGGL((conv3x3_v9x3<HB, GEO, 2>), grid, block, 0, st, a); break;
-        default: hipLaunchKernelGGL((conv3x3_v9x3<HB, GEO, 3>), grid, block, 0, st, a); break;
+        case 0: hipLaunchKernelGGL((conv3x3_v9x3<HB, GEO, 0, 1>), grid, block, 0, st, a); break;
+        case 1: hipLaunchKernelGGL((conv3x3_v9x3<HB, GEO, 1, 1>), grid, block, 0, st, a); break;
+        case 2: hipLaunchKernelGGL((conv3x3_v9x3<HB, GEO, 2, 1>), grid, block, 0, st, a); break;
+        default: hipLaunchKernelGGL((conv3x3_v9x3<HB, GEO, 3, 1>), grid, block, 0, st, a); break;
     }
 }
 
@@ -1110,7 +1155,8 @@ static bool x3_wide(const ConvBf16Args& a) { return a.N % 256 == 0 && !(az_conv_
 // the kernel az_conv_v7x3_launch takes (bench.py's roofline label)
 int az_conv_x3_name(const ConvBf16Args& a, char* out, int len) {
     if (!az_conv_v7x3_supported(a)) return -1;
-    snprintf(out, len, "%s<%d, %s>", x3_wide(a) ? "conv3x3_v9x3" : "conv3x3_v7x3", a.H, a.H == 15 ? "SLIM" : "DENSE");
+    snprintf(out, len, "%s<%d, %s%s>", x3_wide(a) ? "conv3x3_v9x3" : "conv3x3_v7x3", a.H, a.H == 15 ? "SLIM" : "DENSE",
+             a.pt == 2 ? ", f16" : "");
     return 0;
 }
 

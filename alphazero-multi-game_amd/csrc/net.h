@@ -46,6 +46,8 @@ struct ConvBf16Args {
     int stamp;                                  // diagnostic builds: launch slot for phase stamps
     int flags;                                  // kernel variant bits (az_diag_set_conv_flags; A/B tests)
     int* ovf;                                   // fp16 outputs: set to 1 when a value leaves the fp16 range (or null)
+    int pt;                                     // x3 kernels (v7x3 / v9x3): pieces 1 = bf16 (0 reads as 1), 2 = fp16
+    const float* oscale;                        // pt 2: per-output-channel 2^-s undoing the weights' scale 2^s
 };
 
 // k_smallnet (smallnet.hip): the whole trunk + pool + head 1x1 convs of a 64-filter net, one board per block
@@ -65,8 +67,10 @@ struct SmallNetArgs {
     int H, blocks, residual, HC, P;
     int stamps;                     // diagnostic: block 0 writes phase stamps (az_diag_smallnet_stamps)
     int* ovf;                       // set to 1 when an activation leaves the fp16 range
-    const uint16_t* Wxh;            // AZ_PREC_BF16X3 (k_smallnet_x3): bf16 hi / lo parts of the weights,
+    const uint16_t* Wxh;            // AZ_PREC_BF16X3 / F16X3 (k_smallnet_x3): hi / lo pieces of the weights,
     const uint16_t* Wxl;            // fragment-major as Wf; null = the fp16 kernel
+    int pt;                         // k_smallnet_x3 pieces: 1 bf16, 2 fp16 (weights scaled by 2^s per output channel,
+    const float* osc;               // bias = b * 2^s; osc [L][64] = 2^-s)
 };
 bool az_smallnet_supported(int H, int C, int cin_pad, int pool, int head_channels);
 int az_smallnet_max_blocks();

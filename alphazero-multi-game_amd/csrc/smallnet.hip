@@ -503,6 +503,25 @@ __device__ __forceinline__ uint32_t pack_bf16(float a, float b) {
     return r(a) | (r(b) << 16);
 }
 
+template <int PT, typename F>
+__device__ __forceinline__ f32x4v x3_mma(const F& w, const F& a, const f32x4v& c) {
+    if constexpr (PT == 2) return __builtin_amdgcn_mfma_f32_16x16x32_f16(w, a, c, 0, 0, 0);
+    else return __builtin_amdgcn_mfma_f32_16x16x32_bf16(w, a, c, 0, 0, 0);
+}
+// two fp32 -> a hi pair and a lo pair (x - hi) of 16-bit pieces: PT 1 bf16, PT 2 fp16
+template <int PT>
+__device__ __forceinline__ void split_pair(float a, float b, uint32_t& h, uint32_t& l) {
+    if constexpr (PT == 1) {
+        h = pack_bf16(a, b);
+        l = pack_bf16(a - __uint_as_float(h << 16), b - __uint_as_float(h & 0xffff0000u));
+    } else {
+        typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+        const f16x2 x = {(_Float16)a, (_Float16)b};
+        h = __builtin_bit_cast(uint32_t, x);
+        l = pack_f16(a - (float)x[0], b - (float)x[1]);
+    }
+}
+
 template <int V> using IC = std::integral_constant<int, V>;
 enum { ROLE_IN = 0, ROLE_ODD = 1, ROLE_EVEN = 2 };
 
@@ -891,12 +910,14 @@ __global__ __launch_bounds__(64 * NW, 1) void k_smallnet_g(SmallNetArgs p) {
 }
 
 // ------------------------------------------------------------------------------------------------
-// k_smallnet_x3: the fused forward in the fp32-faithful parity precision (AZ_PREC_BF16X3).
-// Every activation is carried as two bf16 planes, hi = bf16(x) and lo = bf16(x - hi), and every
-// weight likewise (fragment-major Wxh / Wxl); a product is hi*hi + lo*hi + hi*lo -- three
-// v_mfma_f32_16x16x32_bf16 per 32-channel step, fp32 accumulation (the arithmetic of conv3x3_v7x3 /
-// conv3x3_v4<0>).  The fp32 residual stream stays in registers as in k_smallnet_g, and the tail
-// (pool, head convs) is the same code.  What differs:
+// k_smallnet_x3: the fused forward in the fp32-faithful parity precisions (PT 1: AZ_PREC_BF16X3,
+// PT 2: AZ_PREC_F16X3).  Every activation is carried as two 16-bit planes, hi = p(x) and lo =
+// p(x - hi) for the piece type p (bf16 or fp16), and every weight likewise (fragment-major Wxh / Wxl;
+// fp16 pieces of weights scaled by 2^s per output channel, the accumulators start at bias * 2^s and
+// the epilogue multiplies by p.osc = 2^-s); a product is hi*hi + lo*hi + hi*lo -- three MFMAs
+// (v_mfma_f32_16x16x32_bf16 / _f16) per 32-channel step, fp32 accumulation (the arithmetic of
+// conv3x3_v9x3 / v7x3).  The fp32 residual stream stays in registers as in k_smallnet_g, and the
+// tail (pool, head convs) is the same code.  What differs:
 //  * ONE activation image per plane (hi, lo: 2 x 46.7 KB), updated IN PLACE: a layer's outputs stay
 //    in the accumulators until every wave has read its last input fragment (barrier A), then the
 //    epilogue writes them over the input and barrier B certifies them for the next layer -- two
@@ -905,16 +926,18 @@ __global__ __launch_bounds__(64 * NW, 1) void k_smallnet_g(SmallNetArgs p) {
 //    register ring of 2 x JN weight fragments (hi, lo; a step is 3x the MFMAs of the fp16 kernel,
 //    so three steps cover the L2 latency): 24 MFMAs per step in three sweeps (Wh*Ah, Wl*Ah, Wh*Al),
 //    so an accumulator is reused every JN * FPW = 8 MFMAs;
-//  * layer 0 (the 0/1 input planes, exact in bf16: lo = 0) runs the same three sweeps.
-template <int HB, int NW, bool RES>
+//  * layer 0 reads the input planes split the same way (hi + lo) and runs the same three sweeps.
+template <int HB, int NW, bool RES, int PT>
 __global__ __launch_bounds__(64 * NW, 1) void k_smallnet_x3(SmallNetArgs p) {
     typedef Sm2<HB, NW> G;
     constexpr int NT = G::NT, WG = G::WG, HW = G::HW, FPW = G::FPW, JN = G::JN;
     constexpr int PW = 3;                                // weight ring depth (steps): 9 and 18 are multiples
     constexpr int OH = 0, OL = G::IMG, OB = 2 * G::IMG, OS = OB;
-    constexpr int LDS = OB + 2 * SF * SF * 4 > OB + G::MAXL * SF * 4 ? OB + 2 * SF * SF * 4 : OB + G::MAXL * SF * 4;
+    constexpr int OSC = OB + G::MAXL * SF * 4;           // PT 2: the per-channel scales [L][64] behind the biases
+    constexpr int LDS = OB + 2 * SF * SF * 4 > OB + 2 * G::MAXL * SF * 4 ? OB + 2 * SF * SF * 4 : OB + 2 * G::MAXL * SF * 4;
     static_assert(LDS <= 160 * 1024, "");
-    typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+    typedef typename std::conditional<PT == 2, _Float16, __bf16>::type piece_t;
+    typedef piece_t bf16x8 __attribute__((ext_vector_type(8)));
     __shared__ __attribute__((aligned(16))) uint8_t lds[LDS];
     const uint32_t L0 = (uint32_t)(uintptr_t)lds;
     const int b = blockIdx.x;
@@ -954,6 +977,10 @@ __global__ __launch_bounds__(64 * NW, 1) void k_smallnet_x3(SmallNetArgs p) {
         const int i = tid + NT * k;
         bpre[k] = i < L * SF ? p.bias[i] : 0.0f;
     }
+    if constexpr (PT == 2) {
+        float* ssm = reinterpret_cast<float*>(lds + OSC);
+        for (int i = tid; i < L * SF; i += NT) ssm[i] = p.osc[i];
+    }
     // weight register ring: fwh / fwl[slot][j] = fragment group fg's block J0 + j, hi / lo
     bf16x8 fwh[PW][JN], fwl[PW][JN];
     const bf16x8* wsh = reinterpret_cast<const bf16x8*>(p.Wxh) + J0 * 64 + lane;
@@ -970,8 +997,9 @@ __global__ __launch_bounds__(64 * NW, 1) void k_smallnet_x3(SmallNetArgs p) {
     static_for<0, PW>([&](auto xc) { wload(xc, 2 * decltype(xc)::value); });   // layer 0: chunk 0 of taps 0..2
 
     {
-        // zero the halo rows no epilogue writes (both planes), the lo plane of the input chunk, and
-        // write the input planes (0/1: exact in bf16) into the hi plane's first 32 channels
+        // zero the halo rows no epilogue writes (both planes) and write the input planes, split into
+        // hi + lo like every other operand (the coordinate planes are not exact in 16 bits), into the
+        // first 32 channels of both planes
         constexpr int TOP = WG + 1, BOT0 = G::NFRAG * 16 + WG + 1, NPAD = TOP + (G::IR - BOT0);
         for (int i = tid; i < 2 * NPAD * 8; i += NT) {
             const int pl = i / (NPAD * 8), k = i - pl * NPAD * 8, r = k >> 3, c = k & 7;
@@ -998,13 +1026,16 @@ __global__ __launch_bounds__(64 * NW, 1) void k_smallnet_x3(SmallNetArgs p) {
             const int row = gq + WG + 1;
             uint8_t* dh = lds + OH + row * RS;
             uint8_t* dl = lds + OL + row * RS;
+            uint32_t hp[8], lp[8];                       // hi / lo pairs
+#pragma unroll
+            for (int k = 0; k < 8; ++k) split_pair<PT>(c[2 * k], c[2 * k + 1], hp[k], lp[k]);
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
-                const uint4 v = {pack_bf16(c[8 * h], c[8 * h + 1]), pack_bf16(c[8 * h + 2], c[8 * h + 3]),
-                                 pack_bf16(c[8 * h + 4], c[8 * h + 5]), pack_bf16(c[8 * h + 6], c[8 * h + 7])};
+                const uint4 v = {hp[4 * h], hp[4 * h + 1], hp[4 * h + 2], hp[4 * h + 3]};
+                const uint4 w = {lp[4 * h], lp[4 * h + 1], lp[4 * h + 2], lp[4 * h + 3]};
                 *reinterpret_cast<uint4*>(dh + 16 * h) = v;
                 *reinterpret_cast<uint4*>(dh + 32 + 16 * h) = uint4{0, 0, 0, 0};
-                *reinterpret_cast<uint4*>(dl + 16 * h) = uint4{0, 0, 0, 0};
+                *reinterpret_cast<uint4*>(dl + 16 * h) = w;
                 *reinterpret_cast<uint4*>(dl + 32 + 16 * h) = uint4{0, 0, 0, 0};
             }
         }
@@ -1024,6 +1055,8 @@ __global__ __launch_bounds__(64 * NW, 1) void k_smallnet_x3(SmallNetArgs p) {
     uint8_t* eH = lds + OH + (16 * wp + l16 + WG + 1) * RS + 32 * J0 + 8 * lg;
     uint8_t* eL = eH + OL;
     const float* bb = reinterpret_cast<const float*>(lds + OB) + 16 * J0 + 4 * lg;
+    const float* sb = reinterpret_cast<const float*>(lds + OSC) + 16 * J0 + 4 * lg;
+    float vmax = 0.0f;                                   // PT 2: the fp16 range guard
     float mlive[FPW];
 #pragma unroll
     for (int i = 0; i < FPW; ++i) {
@@ -1069,19 +1102,19 @@ __global__ __launch_bounds__(64 * NW, 1) void k_smallnet_x3(SmallNetArgs p) {
             static_for<0, FPW>([&](auto ic) {
                 static_for<0, JN>([&](auto jc) {
                     constexpr int i = decltype(ic)::value, j = decltype(jc)::value;
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fwh[ws][j], fbh[r][i], q == 0 ? bn[j] : acc[i][j], 0, 0, 0);
+                    acc[i][j] = x3_mma<PT>(fwh[ws][j], fbh[r][i], q == 0 ? bn[j] : acc[i][j]);
                 });
             });
             static_for<0, FPW>([&](auto ic) {
                 static_for<0, JN>([&](auto jc) {
                     constexpr int i = decltype(ic)::value, j = decltype(jc)::value;
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fwl[ws][j], fbh[r][i], acc[i][j], 0, 0, 0);
+                    acc[i][j] = x3_mma<PT>(fwl[ws][j], fbh[r][i], acc[i][j]);
                 });
             });
             static_for<0, FPW>([&](auto ic) {
                 static_for<0, JN>([&](auto jc) {
                     constexpr int i = decltype(ic)::value, j = decltype(jc)::value;
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fwh[ws][j], fbl[r][i], acc[i][j], 0, 0, 0);
+                    acc[i][j] = x3_mma<PT>(fwh[ws][j], fbl[r][i], acc[i][j]);
                 });
             });
             __builtin_amdgcn_sched_barrier(0);
@@ -1098,17 +1131,18 @@ __global__ __launch_bounds__(64 * NW, 1) void k_smallnet_x3(SmallNetArgs p) {
                     static_for<0, JN>([&](auto jc) {
                         constexpr int i = decltype(ic)::value, j = decltype(jc)::value;
                         f32x4v v = acc[i][j];
+                        if constexpr (PT == 2) v *= *reinterpret_cast<const f32x4v*>(sb + layer * SF + 16 * j);
                         if constexpr (ROLE == ROLE_EVEN && RES) v += xr[i][j];
 #pragma unroll
                         for (int e = 0; e < 4; ++e) v[e] = __builtin_amdgcn_fmed3f(v[e], 0.0f, mlive[i]);
+                        if constexpr (PT == 2) {
+#pragma unroll
+                            for (int e = 0; e < 4; ++e) vmax = __builtin_fmaxf(vmax, v[e]);
+                        }
                         if constexpr (ROLE != ROLE_ODD) xr[i][j] = v;
                         uint32_t h[2], l[2];
 #pragma unroll
-                        for (int e = 0; e < 2; ++e) {
-                            const float a0 = v[2 * e], a1 = v[2 * e + 1];
-                            h[e] = pack_bf16(a0, a1);
-                            l[e] = pack_bf16(a0 - __uint_as_float(h[e] << 16), a1 - __uint_as_float(h[e] & 0xffff0000u));
-                        }
+                        for (int e = 0; e < 2; ++e) split_pair<PT>(v[2 * e], v[2 * e + 1], h[e], l[e]);
                         constexpr int off = 64 * RS * i + 32 * j;
                         *reinterpret_cast<uint2*>(eH + off) = uint2{h[0], h[1]};
                         *reinterpret_cast<uint2*>(eL + off) = uint2{l[0], l[1]};
@@ -1124,6 +1158,7 @@ __global__ __launch_bounds__(64 * NW, 1) void k_smallnet_x3(SmallNetArgs p) {
         run_layer(layer + 1, IC<ROLE_EVEN>{}, IC<2>{});
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // the ring's trailing (clamped) loads
+    if (PT == 2 && !(vmax <= 65504.0f) && p.ovf) atomicOr(p.ovf, 1);   // fp16 pieces: the engine fails the forward
     __syncthreads();
     smallnet_tail<HB, NW>(p, lds, OS, xr, wpre, b, tid, wp, l16, lg, J0);
 }
@@ -1141,10 +1176,15 @@ int az_smallnet_launch(const SmallNetArgs& a, int B, hipStream_t st) {
         else hipLaunchKernelGGL((k_smallnet_r2<15, 8>), dim3(B), dim3(512), 0, st, a);
         return 0;
     }
-    if (a.Wxh) {                                         // AZ_PREC_BF16X3
-        if (!a.Wxl) return -1;
-        if (a.residual) hipLaunchKernelGGL((k_smallnet_x3<15, 8, true>), dim3(B), dim3(512), 0, st, a);
-        else hipLaunchKernelGGL((k_smallnet_x3<15, 8, false>), dim3(B), dim3(512), 0, st, a);
+    if (a.Wxh) {                                         // AZ_PREC_BF16X3 (pt 1) / AZ_PREC_F16X3 (pt 2)
+        if (!a.Wxl || (a.pt == 2 && !a.osc)) return -1;
+        if (a.pt == 2) {
+            if (a.residual) hipLaunchKernelGGL((k_smallnet_x3<15, 8, true, 2>), dim3(B), dim3(512), 0, st, a);
+            else hipLaunchKernelGGL((k_smallnet_x3<15, 8, false, 2>), dim3(B), dim3(512), 0, st, a);
+            return 0;
+        }
+        if (a.residual) hipLaunchKernelGGL((k_smallnet_x3<15, 8, true, 1>), dim3(B), dim3(512), 0, st, a);
+        else hipLaunchKernelGGL((k_smallnet_x3<15, 8, false, 1>), dim3(B), dim3(512), 0, st, a);
         return 0;
     }
     if (a.residual) hipLaunchKernelGGL((k_smallnet_g<15, 8, true>), dim3(B), dim3(512), 0, st, a);

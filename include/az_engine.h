@@ -35,7 +35,7 @@ enum az_status {
     AZ_ERR_OOM = -3,       /* device allocation failed */
     AZ_ERR_CAPACITY = -4,  /* node pool / prior ring / batch capacity exceeded */
     AZ_ERR_STATE = -5,     /* call not valid in the current state */
-    AZ_ERR_RANGE = -6      /* an AZ_PREC_FP16 activation left the fp16 range (|x| > 65504): the
+    AZ_ERR_RANGE = -6      /* an AZ_PREC_FP16 / F16X3 activation left the fp16 range (|x| > 65504): the
                               outputs of that forward / search are invalid; use AZ_PREC_BF16X3 */
 };
 
@@ -59,10 +59,16 @@ int az_engine_device_name(az_engine* e, char* buf, int len);
  *   residual=0,conv_bias=0 : exporter fallback (python/scripts/simple_export.py:40-96)  */
 enum az_precision {
     AZ_PREC_F32 = 0,    /* fp32 operands, f32-input MFMA (exact f32 products)              */
-    AZ_PREC_BF16X3 = 1, /* fp32 split into bf16 hi+lo, 3 bf16 MFMAs per product (~2^-16)   */
+    AZ_PREC_BF16X3 = 1, /* fp32 split into bf16 hi+lo, 3 bf16 MFMAs per product (~2^-17;
+                           the full fp32 range)                                            */
     AZ_PREC_BF16 = 2,   /* plain bf16 operands, fp32 accumulate (throughput only)          */
-    AZ_PREC_FP16 = 3    /* fp16 operands, fp32 accumulate: TorchNeuralNetworkConfig::useFp16
+    AZ_PREC_FP16 = 3,   /* fp16 operands, fp32 accumulate: TorchNeuralNetworkConfig::useFp16
                            (include/alphazero/nn/torch_neural_network.h:29); 15x15, F%64==0   */
+    AZ_PREC_F16X3 = 4   /* fp32 split into fp16 hi+lo (weights scaled 2^s per output channel),
+                           3 fp16 MFMAs per product (~2^-21: the fp32 oracle's own error level);
+                           activations must stay within |x| <= 65504 (else AZ_ERR_RANGE; use
+                           AZ_PREC_BF16X3); 8/9/13/15/19 boards with channels % 128 == 0, or
+                           the 15x15 64-channel net                                        */
 };
 typedef struct az_net_desc {
     int board_size;     /* H = W */

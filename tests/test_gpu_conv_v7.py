@@ -72,15 +72,18 @@ V9_VARIANTS = [0x204, 0x20000204, 0x40000204, 0x60000204]   # default; tap-start
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("prec", ["bf16x3", "f16x3"])
 @pytest.mark.parametrize("case", X3W_CASES, ids=[str(c) for c in X3W_CASES])
-def test_gpu_v9x3_bitwise_equals_v7x3(engine, case):
+def test_gpu_v9x3_bitwise_equals_v7x3(engine, case, prec):
     """conv3x3_v9x3 (one 512-thread block per CU owning all 256 output channels of a tile) gives
     every accumulator the same products in the same order as conv3x3_v7x3 (Bh*Ah, Bl*Ah, Bh*Al per
-    tap), so the whole bf16x3 network must be BITWISE equal on every geometry and batch shape."""
+    tap), so the whole split-precision network must be BITWISE equal on every geometry and batch
+    shape, for bf16 pieces (and every v9x3 A/B variant) and fp16 pieces (the default variant)."""
     import az_amd
     import net_oracle
     bs, ci, A, ch, blocks, res, B = case
-    desc = az_amd.NetDesc(bs, ci, ch, blocks, A, 32, 8, 256, res, 0, az_amd.AZ_PREC_BF16X3, B)
+    p = {"bf16x3": az_amd.AZ_PREC_BF16X3, "f16x3": az_amd.AZ_PREC_F16X3}[prec]
+    desc = az_amd.NetDesc(bs, ci, ch, blocks, A, 32, 8, 256, res, 0, p, B)
     net = az_amd.HipNeuralNetwork(engine, desc)
     assert net.trunk_kernel().startswith("conv3x3_v9x3<")
     net.load_weights(net_oracle.init_blob(desc, seed=57))
@@ -90,7 +93,7 @@ def test_gpu_v9x3_bitwise_equals_v7x3(engine, case):
         _flags(0x10000204)                # conv3x3_v7x3
         l7, v7 = net.forward(x)
         outs = {}
-        for fl in V9_VARIANTS:            # conv3x3_v9x3 (0x204: the library default) and its A/B variants
+        for fl in (V9_VARIANTS if prec == "bf16x3" else V9_VARIANTS[:1]):   # 0x204: the library default
             _flags(fl)
             outs[fl] = net.forward(x)
     finally:

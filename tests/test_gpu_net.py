@@ -3,12 +3,19 @@ restatement (oracle/net_oracle.py), itself pinned to the reference's Python clas
 (tests/test_nn_golden.py).
 
 Tolerance (BASELINE.json north_star): |logit - ref| <= 1e-4 and |value - ref| <= 1e-4
-for the parity precisions (AZ_PREC_F32, AZ_PREC_BF16X3).  Plain bf16 is a throughput
-variant and only gets a loose sanity bound."""
+for the parity precisions (AZ_PREC_F32, AZ_PREC_F16X3, AZ_PREC_BF16X3) and the throughput
+precision AZ_PREC_FP16 on init-scale weights (trained scale: tests/test_gpu_trained_scale.py).
+Plain bf16 is a throughput variant and only gets a loose sanity bound."""
 import numpy as np
 import pytest
 
 TOL = 1e-4
+PREC = {"f32": 0, "bf16x3": 1, "bf16": 2, "fp16": 3, "f16x3": 4}
+
+
+def f16x3_ok(bs, ch, blocks):
+    """AZ_PREC_F16X3's kernels: conv3x3_v9x3 / v7x3 or the 15x15 64-channel k_smallnet_x3."""
+    return (bs in (8, 9, 13, 15, 19) and ch % 128 == 0) or (bs == 15 and ch == 64 and blocks <= 15)
 
 
 @pytest.fixture(scope="module")
@@ -39,19 +46,23 @@ CASES = [  # (board, channels, blocks, residual, conv_bias, B)
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("prec", ["f32", "bf16x3", "fp16"])
+@pytest.mark.parametrize("prec", ["f32", "f16x3", "bf16x3", "fp16"])
 @pytest.mark.parametrize("case", CASES, ids=[str(c) for c in CASES])
 def test_gpu_net_matches_fp32_reference(engine, case, prec):
     import az_amd
     import net_oracle
     bs, ch, blocks, res, bias, B = case
-    p = {"f32": az_amd.AZ_PREC_F32, "bf16x3": az_amd.AZ_PREC_BF16X3, "fp16": az_amd.AZ_PREC_FP16}[prec]
+    p = PREC[prec]
     if p != az_amd.AZ_PREC_F32 and ch % 32:
         pytest.skip("bf16 trunk needs channels % 32 == 0")
     if p == az_amd.AZ_PREC_FP16 and (bs != 15 or ch % 64):
         pytest.skip("fp16 trunk: 15x15 boards, channels % 64 == 0")
     desc = az_amd.gomoku_net_desc(board_size=bs, channels=ch, blocks=blocks, residual=res, conv_bias=bias,
                                   precision=p, max_batch=B)
+    if prec == "f16x3" and not f16x3_ok(bs, ch, blocks):
+        with pytest.raises(az_amd.AzError, match="AZ_PREC_F16X3"):     # refused at creation, not run elsewhere
+            az_amd.HipNeuralNetwork(engine, desc)
+        return
     net = az_amd.HipNeuralNetwork(engine, desc)
     blob = net_oracle.init_blob(desc, seed=11)
     net.load_weights(blob)
@@ -86,7 +97,7 @@ def test_gpu_net_bf16_sanity(engine):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("prec", [0, 1, 3])
+@pytest.mark.parametrize("prec", [0, 1, 3, 4])
 def test_gpu_net_batch_position_independent(engine, prec):
     """A sample's output does not depend on its position or batch-mates (bitwise)."""
     import az_amd
@@ -123,13 +134,13 @@ def test_gpu_net_init_random_matches_numpy(engine):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("prec", ["bf16x3", "fp16"])
+@pytest.mark.parametrize("prec", ["f16x3", "bf16x3", "fp16"])
 def test_gpu_c3_net_error_over_many_positions(engine, prec):
     """The C3 net (20 blocks x 256 filters) on 96 random positions: every logit and value
     within 1e-4 of the fp32 reference (the bench precisions)."""
     import az_amd
     import net_oracle
-    p = {"bf16x3": az_amd.AZ_PREC_BF16X3, "fp16": az_amd.AZ_PREC_FP16}[prec]
+    p = PREC[prec]
     desc = az_amd.gomoku_net_desc(board_size=15, channels=256, blocks=20, precision=p, max_batch=96)
     net = az_amd.HipNeuralNetwork(engine, desc)
     blob = net_oracle.init_blob(desc, seed=1234)      # bench.py's weights
@@ -154,15 +165,16 @@ X3_CASES = [  # (board, in_planes, action_size, channels, blocks, residual, B): 
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("prec", ["f16x3", "bf16x3"])
 @pytest.mark.parametrize("case", X3_CASES, ids=[str(c) for c in X3_CASES])
-def test_gpu_bf16x3_v7x3_geometries(engine, case):
-    """The fp32-faithful trunk (AZ_PREC_BF16X3 on conv3x3_v7x3, g8 hi / lo planes) on every tile
-    geometry it is instantiated for: within 1e-4 of the fp32 reference, and a board's outputs
-    bitwise the same whatever its batch position and tile-mates."""
+def test_gpu_x3_trunk_geometries(engine, case, prec):
+    """The split-precision trunks (AZ_PREC_F16X3 / BF16X3 on conv3x3_v7x3 / v9x3, g8 hi / lo planes)
+    on every tile geometry they are instantiated for: within 1e-4 of the fp32 reference, and a
+    board's outputs bitwise the same whatever its batch position and tile-mates."""
     import az_amd
     import net_oracle
     bs, ci, A, ch, blocks, res, B = case
-    desc = az_amd.NetDesc(bs, ci, ch, blocks, A, 32, 8, 256, res, 0, az_amd.AZ_PREC_BF16X3, B)
+    desc = az_amd.NetDesc(bs, ci, ch, blocks, A, 32, 8, 256, res, 0, PREC[prec], B)
     net = az_amd.HipNeuralNetwork(engine, desc)
     if ch % 64 == 0:
         assert net.trunk_kernel().startswith("conv3x3_v9x3<" if ch % 256 == 0 else "conv3x3_v7x3<")
@@ -172,7 +184,7 @@ def test_gpu_bf16x3_v7x3_geometries(engine, case):
     lo, v = net.forward(x)
     rl, rv = net_oracle.forward(desc, blob, x)
     el, ev = float(np.abs(lo - rl).max()), float(np.abs(v - rv).max())
-    print(f"{case} bf16x3: max|dlogit|={el:.3e} (|logit|max {np.abs(rl).max():.3f}) max|dvalue|={ev:.3e}")
+    print(f"{case} {prec}: max|dlogit|={el:.3e} (|logit|max {np.abs(rl).max():.3f}) max|dvalue|={ev:.3e}")
     assert el <= TOL and ev <= TOL
     perm = np.random.default_rng(bs).permutation(B)
     lo2, v2 = net.forward(x[perm])
@@ -301,11 +313,15 @@ def test_gpu_c5_net_full_batch(engine):
     ((15, 11, 256, 20, 225, "fp16", 2048), "conv3x3_v7<2, 15, SLIM>"),   # C3 at N = 1, 2
     ((15, 11, 256, 20, 225, "fp16", 256), "conv3x3_v6<2, 15>"),          # C3 shard at N = 8
     ((15, 11, 64, 6, 225, "fp16", 256), "k_smallnet_g<15, 8, true>"),    # C2: the fused 64-filter forward
-    ((15, 11, 64, 6, 225, "bf16x3", 256), "k_smallnet_x3<15, 8, true>"),   # C2 in the parity precision
-    ((15, 11, 256, 20, 225, "bf16x3", 64), "conv3x3_v9x3<15, SLIM>"),   # the parity precision at C3
+    ((15, 11, 64, 6, 225, "f16x3", 256), "k_smallnet_x3<15, 8, true, 2>"),   # C2 in the parity precision
+    ((15, 11, 64, 6, 225, "bf16x3", 256), "k_smallnet_x3<15, 8, true, 1>"),
+    ((15, 11, 256, 20, 225, "f16x3", 2048), "conv3x3_v9x3<15, SLIM, f16>"),   # the parity precision at C3
+    ((15, 11, 256, 20, 225, "bf16x3", 64), "conv3x3_v9x3<15, SLIM>"),
     ((15, 11, 256, 20, 225, "bf16x3", 2048), "conv3x3_v9x3<15, SLIM>"),
     ((15, 11, 128, 2, 225, "bf16x3", 64), "conv3x3_v7x3<15, SLIM>"),    # 128 channels: the v7 tile
+    ((15, 11, 128, 2, 225, "f16x3", 64), "conv3x3_v7x3<15, SLIM, f16>"),
     ((19, 8, 256, 20, 362, "bf16x3", 1024), "conv3x3_v9x3<19, DENSE>"),
+    ((19, 8, 256, 20, 362, "f16x3", 1024), "conv3x3_v9x3<19, DENSE, f16>"),
     ((19, 8, 256, 20, 362, "fp16", 1024), "conv3x3_v6<2, 19, DENSE>"),   # C4
     ((15, 11, 32, 2, 225, "f32", 4), "gemm_f32"),
 ])
@@ -313,7 +329,7 @@ def test_gpu_trunk_kernel_name(engine, case):
     """az_net_trunk_kernel names the kernel the trunk actually dispatches (bench.py's roofline label)."""
     import az_amd
     (bs, ci, ch, blocks, A, prec, B), want = case
-    p = {"f32": az_amd.AZ_PREC_F32, "bf16x3": az_amd.AZ_PREC_BF16X3, "fp16": az_amd.AZ_PREC_FP16}[prec]
+    p = PREC[prec]
     net = az_amd.HipNeuralNetwork(engine, az_amd.NetDesc(bs, ci, ch, blocks, A, 32, 8, 256, 1, 0, p, B))
     assert net.trunk_kernel() == want
     net.close()
@@ -350,18 +366,20 @@ def test_gpu_smallnet_matches_round2_kernel(engine, residual, B):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("prec", ["f16x3", "bf16x3"])
 @pytest.mark.parametrize("residual", [1, 0])
 @pytest.mark.parametrize("B", [256, 37])
-def test_gpu_smallnet_x3_matches_oracle(engine, residual, B):
-    """k_smallnet_x3 (the fused 64-filter forward in the fp32-faithful bf16x3 precision: hi / lo
-    activation planes updated in place in LDS, three MFMAs per product) on C2-shape nets: within the
-    north-star 1e-4 of the fp32 network on sampled boards, and a board's outputs bitwise the same
+def test_gpu_smallnet_x3_matches_oracle(engine, residual, B, prec):
+    """k_smallnet_x3 (the fused 64-filter forward in the split precisions: hi / lo activation planes
+    of fp16 or bf16 pieces updated in place in LDS, three MFMAs per product) on C2-shape nets: within
+    the north-star 1e-4 of the fp32 network on sampled boards, and a board's outputs bitwise the same
     whatever its batch position (permuted batch, a tail slice)."""
     import az_amd
     import net_oracle
-    d = az_amd.NetDesc(15, 11, 64, 6, 225, 32, 8, 256, residual, 0, az_amd.AZ_PREC_BF16X3, 256)
+    d = az_amd.NetDesc(15, 11, 64, 6, 225, 32, 8, 256, residual, 0, PREC[prec], 256)
     net = az_amd.HipNeuralNetwork(engine, d)
-    assert net.trunk_kernel() == f"k_smallnet_x3<15, 8, {'true' if residual else 'false'}>"
+    pt = 2 if prec == "f16x3" else 1
+    assert net.trunk_kernel() == f"k_smallnet_x3<15, 8, {'true' if residual else 'false'}, {pt}>"
     blob = net_oracle.init_blob(d, seed=91 + residual)
     net.load_weights(blob)
     x = _rand_planes(B, 11, 15, 15 + B)
@@ -369,7 +387,7 @@ def test_gpu_smallnet_x3_matches_oracle(engine, residual, B):
     pick = np.unique(np.concatenate([[0, B - 1], np.random.default_rng(B).choice(B, 10, replace=False)]))
     rl, rv = net_oracle.forward(d, blob, x[pick])
     el, ev = float(np.abs(lo[pick] - rl).max()), float(np.abs(v[pick] - rv).max())
-    print(f"smallnet_x3 residual={residual} B={B}: max|dlogit|={el:.3e} max|dvalue|={ev:.3e}")
+    print(f"smallnet_x3 {prec} residual={residual} B={B}: max|dlogit|={el:.3e} max|dvalue|={ev:.3e}")
     assert el <= TOL and ev <= TOL
     perm = np.random.default_rng(3).permutation(B)
     lo2, v2 = net.forward(x[perm])

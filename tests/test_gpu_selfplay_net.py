@@ -161,13 +161,14 @@ def test_gpu_c3_full_size_replay():
 
 
 @pytest.mark.gpu
-def test_gpu_c3_full_size_replay_bf16x3():
-    """C3 at full size in the parity precision (AZ_PREC_BF16X3, conv3x3_v7x3) with trained-scale
-    heads: two moves of all 2048 games, game 1337 replayed bit for bit, sampled logits / values of
-    the logged leaves and of a B = 2048 forward within 1e-4 of the fp32 network."""
-    import az_amd
+@pytest.mark.parametrize("prec", ["f16x3", "bf16x3"])
+def test_gpu_c3_full_size_replay_x3(prec):
+    """C3 at full size in the split precisions (AZ_PREC_F16X3 -- the parity precision -- and
+    AZ_PREC_BF16X3, both on conv3x3_v9x3) with trained-scale heads: two moves of all 2048 games, game
+    1337 replayed bit for bit, sampled logits / values of the logged leaves and of a B = 2048 forward
+    within 1e-4 of the fp32 network."""
     _full_size_replay(bs=15, sims=800, G=2048, moves=2, logged=1337, channels=256, blocks=20,
-                      prec=az_amd.AZ_PREC_BF16X3, trained=True)
+                      prec={"f16x3": 4, "bf16x3": 1}[prec], trained=True)
 
 
 @pytest.mark.gpu
@@ -179,10 +180,10 @@ def test_gpu_c2_full_size_replay():
 
 
 @pytest.mark.gpu
-def test_gpu_c2_full_size_replay_bf16x3():
-    """C2 at full size in the parity precision (AZ_PREC_BF16X3 on k_smallnet_x3, fed the search's
-    leaf records) with trained-scale heads: four moves of all 256 games, game 137 replayed bit for
-    bit, sampled outputs of the logged leaves and of a B = 256 forward within 1e-4 of fp32."""
-    import az_amd
+@pytest.mark.parametrize("prec", ["f16x3", "bf16x3"])
+def test_gpu_c2_full_size_replay_x3(prec):
+    """C2 at full size in the split precisions (k_smallnet_x3 with fp16 / bf16 pieces, fed the
+    search's leaf records) with trained-scale heads: four moves of all 256 games, game 137 replayed
+    bit for bit, sampled outputs of the logged leaves and of a B = 256 forward within 1e-4 of fp32."""
     _full_size_replay(bs=15, sims=400, G=256, moves=4, logged=137, channels=64, blocks=6,
-                      prec=az_amd.AZ_PREC_BF16X3, trained=True)
+                      prec={"f16x3": 4, "bf16x3": 1}[prec], trained=True)

@@ -17,7 +17,7 @@ import az_amd  # noqa: E402
 GAMES = {"gomoku15": (15, 11, 225), "go19": (19, 8, 362), "chess": (8, 111, 4672), "gomoku9": (9, 11, 81),
          "go13": (13, 8, 170), "go9": (9, 8, 82)}   # board, planes, actions
 PREC = {"f32": az_amd.AZ_PREC_F32, "bf16x3": az_amd.AZ_PREC_BF16X3, "bf16": az_amd.AZ_PREC_BF16,
-        "fp16": az_amd.AZ_PREC_FP16}
+        "fp16": az_amd.AZ_PREC_FP16, "f16x3": az_amd.AZ_PREC_F16X3}
 
 
 def main():
