@@ -81,6 +81,29 @@ template <> struct X3T<2> {
 
 __device__ __forceinline__ uint32_t lds_addr(const void* p) { return (uint32_t)(uintptr_t)p; }
 
+#ifdef AZ_V9_STAMPS
+// Diagnostic builds only (make EXTRA=-DAZ_V9_STAMPS OUT=build_stamps): wave 0 of every block of the
+// selected conv3x3_v9x3 launch (ConvBf16Args::stamp == g_v9_sel) records s_memrealtime (100 MHz) at
+// its start, after the prologue barrier, after the main loop, after the epilogue's stores issue and
+// after they complete, plus HW_ID / XCC_ID (tools/v9_stamps.py)
+constexpr int V9_MAXB = 8192;
+__device__ int g_v9_sel = -1;
+__device__ unsigned long long g_v9_st[V9_MAXB][5];
+__device__ unsigned g_v9_hw[V9_MAXB][2];
+#define V9_STAMP(k)                                                                                 \
+    do {                                                                                            \
+        if (p.stamp == g_v9_sel && tid == 0 && blockIdx.x < V9_MAXB) {                              \
+            g_v9_st[blockIdx.x][k] = __builtin_amdgcn_s_memrealtime();                              \
+            if (k == 0) {                                                                           \
+                g_v9_hw[blockIdx.x][0] = __builtin_amdgcn_s_getreg((31 << 11) | 4);                 \
+                g_v9_hw[blockIdx.x][1] = __builtin_amdgcn_s_getreg((31 << 11) | 20);                \
+            }                                                                                       \
+        }                                                                                           \
+    } while (0)
+#else
+#define V9_STAMP(k) do { } while (0)
+#endif
+
 template <int OFF, typename F>
 __device__ __forceinline__ void ds_rd(F& d, uint32_t addr) {
     asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(d) : "v"(addr), "i"(OFF) : "memory");
@@ -780,6 +803,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_v9x3(ConvBf16Args p) {
     const int n0 = nb * BNT;
     const int nboards = p.m_limit ? *p.m_limit : p.M / HW;
     if (DENSE ? tile * 256 >= nboards * HW : tile >= nboards) return;
+    V9_STAMP(0);
     const int C = p.C, GI = C / 8, GO = p.N / 8;
     const int NCH = C / 32, NS = 9 * NCH;
 
@@ -876,6 +900,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_v9x3(ConvBf16Args p) {
     issueB(1, 1);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
+    V9_STAMP(1);
 
     frag aX[4], aY[4], bh[4], bl[4];
     auto maskA = [&](frag (&x)[4], int half, int dy, int dx) {
@@ -1012,6 +1037,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_v9x3(ConvBf16Args p) {
     if (SKIP && wm == 1) main_loop(I1{});
     else main_loop(I0{});
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    V9_STAMP(2);
 
     // epilogue from the accumulators: residual hi + lo joined in fp32, ReLU, split, streaming stores
     const __amdgpu_buffer_rsrc_t rh = __builtin_amdgcn_make_buffer_rsrc((void*)p.Rhi, (short)0, 0x7fffffff, 0x00020000);
@@ -1080,10 +1106,36 @@ __global__ __launch_bounds__(512, 1) void conv3x3_v9x3(ConvBf16Args p) {
             asm volatile("global_store_dwordx2 %0, %1, off nt" ::"v"(p.Clo + e), "v"(ls) : "memory");
         }
     }
+#ifdef AZ_V9_STAMPS
+    V9_STAMP(3);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    V9_STAMP(4);
+#endif
     if (PT == 2 && !(vmax <= 65504.0f) && p.ovf) atomicOr(p.ovf, 1);    // fp16 pieces: the engine fails the forward
 }
 
 // Host side ----------------------------------------------------------------------------------
+// diagnostic: select the stamped conv3x3_v9x3 launch / read its stamps (AZ_V9_STAMPS builds; else -1)
+extern "C" int az_diag_v9_stamps(int sel, unsigned long long* st, unsigned* hw, int n) {
+#ifdef AZ_V9_STAMPS
+    if (sel >= -1) {
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_v9_sel), &sel, sizeof(int)) != hipSuccess) return -2;
+        static unsigned long long zero[V9_MAXB][5];
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_v9_st), zero, sizeof(zero)) != hipSuccess) return -2;
+    }
+    if (st && n > 0) {
+        n = n < V9_MAXB ? n : V9_MAXB;
+        if (hipDeviceSynchronize() != hipSuccess) return -2;
+        if (hipMemcpyFromSymbol(st, HIP_SYMBOL(g_v9_st), (size_t)n * 5 * 8) != hipSuccess) return -2;
+        if (hw && hipMemcpyFromSymbol(hw, HIP_SYMBOL(g_v9_hw), (size_t)n * 2 * 4) != hipSuccess) return -2;
+    }
+    return 0;
+#else
+    (void)sel; (void)st; (void)hw; (void)n;
+    return -1;
+#endif
+}
+
 template <int HB, int GEO>
 static void v7_launch_g(const ConvBf16Args& a, int mode, hipStream_t st) {
     const int boards = a.M / (HB * HB);

@@ -184,6 +184,9 @@ struct az_net {
     uint16_t* sm_Wxl = nullptr;
     uint16_t* fcx_hi = nullptr;                 // both FC layers' bf16 hi / lo rows (k_fc_heads_x3)
     uint16_t* fcx_lo = nullptr;
+    uint16_t* fcf_hi = nullptr;                 // the same rows scaled by 2^s, fp16 hi / lo (k_fc_heads_x3<2>, F16X3)
+    uint16_t* fcf_lo = nullptr;
+    float* fcf_rs = nullptr;                    // [NC] 2^-s
     float* sm_b = nullptr;
     // DDW-RandWire trunk (az_net_create_randwire): d.blocks rand-wire blocks of 32 nodes
     bool rw = false;
@@ -488,21 +491,38 @@ int load_heads(az_net* n, ParamCursor& pc) {
         std::vector<float> Wp((size_t)A * K), Wv((size_t)H * K);
         HIPCHK(hipMemcpy(Wp.data(), n->pfc.W, Wp.size() * 4, hipMemcpyDeviceToHost));
         HIPCHK(hipMemcpy(Wv.data(), n->vfc1.W, Wv.size() * 4, hipMemcpyDeviceToHost));
-        std::vector<uint16_t> hi((size_t)NC * K, 0), lo((size_t)NC * K, 0);
+        std::vector<uint16_t> hi((size_t)NC * K, 0), lo((size_t)NC * K, 0), fh((size_t)NC * K, 0), fl((size_t)NC * K, 0);
+        std::vector<float> rs(NC, 1.0f);
         auto put = [&](const std::vector<float>& Wm, int rows, int r0) {
-            for (int r = 0; r < rows; ++r)
+            for (int r = 0; r < rows; ++r) {
+                float m = 0.0f;
+                for (int k = 0; k < K; ++k) m = std::max(m, std::fabs(Wm[(size_t)r * K + k]));
+                const int s = m > 0.0f ? 13 - std::ilogb(m) : 0;      // max |row| * 2^s in [2^13, 2^14)
+                const float up = std::ldexp(1.0f, s);
+                rs[r0 + r] = std::ldexp(1.0f, -s);
                 for (int k = 0; k < K; ++k) {
                     const float w = Wm[(size_t)r * K + k];
                     const uint16_t h = f2bf(w);
                     hi[(size_t)(r0 + r) * K + k] = h;
                     lo[(size_t)(r0 + r) * K + k] = f2bf(w - bf2f(h));
+                    const float ws = w * up;
+                    const _Float16 ph = (_Float16)ws, pl = (_Float16)(ws - (float)ph);
+                    std::memcpy(&fh[(size_t)(r0 + r) * K + k], &ph, 2);
+                    std::memcpy(&fl[(size_t)(r0 + r) * K + k], &pl, 2);
                 }
+            }
         };
         put(Wp, A, 0);
         put(Wv, H, NTP * 64);
-        if (!n->fcx_hi) { DALLOC(n->fcx_hi, hi.size()); DALLOC(n->fcx_lo, lo.size()); }
+        if (!n->fcx_hi) {
+            DALLOC(n->fcx_hi, hi.size()); DALLOC(n->fcx_lo, lo.size());
+            DALLOC(n->fcf_hi, fh.size()); DALLOC(n->fcf_lo, fl.size()); DALLOC(n->fcf_rs, rs.size());
+        }
         HIPCHK(hipMemcpy(n->fcx_hi, hi.data(), hi.size() * 2, hipMemcpyHostToDevice));
         HIPCHK(hipMemcpy(n->fcx_lo, lo.data(), lo.size() * 2, hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(n->fcf_hi, fh.data(), fh.size() * 2, hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(n->fcf_lo, fl.data(), fl.size() * 2, hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(n->fcf_rs, rs.data(), rs.size() * 4, hipMemcpyHostToDevice));
     }
     return 0;
 }
@@ -939,13 +959,17 @@ int net_heads_fc(az_net* n, int B, const int* nb, float* logits, float* value, h
         fa.part = n->ws; fa.m_limit = nb;
         fa.B = B; fa.K = HK; fa.A = d.action_size; fa.H = d.fc_hidden;
         fa.S = az_fc_heads_splits(d.max_batch, HK, d.action_size, d.fc_hidden);   // from the capacity: batch-size independent
-        // the throughput precisions (fp16 / bf16 trunk) take the FC products in bf16x3 (fp32-faithful to
-        // ~2^-16 per product, 5x the f32 MFMA rate; their trunk error is 30x larger); the parity
-        // precisions keep exact f32 products: the bf16x3 FC adds ~2.5e-5 at trained-scale logits, a
-        // quarter of the 1e-4 budget (tests/test_gpu_trained_scale.py).  Conv flag 0x08000000 keeps the
-        // f32 k_fc_heads (A/B, diagnosis).
-        if ((d.precision == AZ_PREC_FP16 || d.precision == AZ_PREC_BF16) && n->fcx_hi && !(az_conv_flags() & 0x08000000)) {
-            fa.Wx_hi = n->fcx_hi; fa.Wx_lo = n->fcx_lo;
+        // split-operand FC products at 5x the f32 MFMA rate: the throughput precisions (fp16 / bf16
+        // trunk) in bf16 pieces (~2^-16 per product; their trunk error is 30x larger), AZ_PREC_F16X3 in
+        // scaled fp16 pieces (~2^-21, as its trunk).  AZ_PREC_BF16X3 and F32 keep exact f32 products
+        // (bf16 pieces would add ~2.5e-5 at trained-scale logits).  Conv flag 0x08000000 keeps the f32
+        // k_fc_heads (A/B, diagnosis).
+        const bool fx = !(az_conv_flags() & 0x08000000) && n->fcx_hi;
+        if (fx && (d.precision == AZ_PREC_FP16 || d.precision == AZ_PREC_BF16)) {
+            fa.Wx_hi = n->fcx_hi; fa.Wx_lo = n->fcx_lo; fa.pt = 1;
+            fa.S = az_fc_heads_splits_x3(d.max_batch, HK, d.action_size, d.fc_hidden);
+        } else if (fx && d.precision == AZ_PREC_F16X3) {
+            fa.Wx_hi = n->fcf_hi; fa.Wx_lo = n->fcf_lo; fa.pt = 2; fa.rs = n->fcf_rs; fa.ovf = n->ovf;
             fa.S = az_fc_heads_splits_x3(d.max_batch, HK, d.action_size, d.fc_hidden);
         }
         az_launch_fc_heads(fa, st);
@@ -1574,7 +1598,7 @@ void az_net_destroy(az_net* n) {
     for (void* p : {(void*)n->x0, (void*)n->h0, (void*)n->h1, (void*)n->t, (void*)n->pool, (void*)n->pp, (void*)n->vp, (void*)n->hpv,
                     (void*)n->v1, (void*)n->ws, (void*)n->logits, (void*)n->value, (void*)n->soft, (void*)n->in_nchw, (void*)n->d_nb, (void*)n->ovf,
                     (void*)n->hh[0], (void*)n->hh[1], (void*)n->hl[0], (void*)n->hl[1], (void*)n->th, (void*)n->tl,
-                    (void*)n->zero, (void*)n->sm_W, (void*)n->sm_Wf, (void*)n->sm_Wxh, (void*)n->sm_Wxl, (void*)n->sm_b, (void*)n->fcx_hi, (void*)n->fcx_lo,
+                    (void*)n->zero, (void*)n->sm_W, (void*)n->sm_Wf, (void*)n->sm_Wxh, (void*)n->sm_Wxl, (void*)n->sm_b, (void*)n->fcx_hi, (void*)n->fcx_lo, (void*)n->fcf_hi, (void*)n->fcf_lo, (void*)n->fcf_rs,
                     (void*)n->sm_Wfh, (void*)n->sm_Wfl, (void*)n->sm_bx, (void*)n->sm_sx})
         F(p);
     n->pc.release();

@@ -93,6 +93,9 @@ struct FcHeadArgs {
     int hc, xs;                                 // head channels; cell stride of pp / vp (xs == hc: contiguous [B][K])
     const uint16_t* Wx_hi; const uint16_t* Wx_lo;   // bf16x3 (k_fc_heads_x3): [NC][K] hi / lo rows (policy padded
                                                     // to a multiple of 64, then value), or null (f32 k_fc_heads)
+    int pt;                                     // k_fc_heads_x3 pieces: 1 bf16, 2 fp16 (rows scaled by 2^s,
+    const float* rs;                            // pt 2: [NC] 2^-s, applied by k_fc_finish to the slice sums)
+    int* ovf;                                   // pt 2: set to 1 when a head feature leaves the fp16 range
 };
 int az_fc_heads_splits(int B, int K, int A, int H);
 int az_fc_heads_splits_x3(int B, int K, int A, int H);

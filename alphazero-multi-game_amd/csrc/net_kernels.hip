@@ -11,6 +11,7 @@
 //   (bf16 MFMA trunk kernels live in conv_bf16.hip.)
 #include <hip/hip_runtime.h>
 #include <algorithm>
+#include <type_traits>
 #include <stdint.h>
 #include "net.h"
 #include "leaf_planes.h"
@@ -551,7 +552,12 @@ __device__ __forceinline__ uint32_t fc_bf16_rne(float f) {
     u += 0x7fffu + ((u >> 16) & 1u);
     return u >> 16;
 }
+// PT 2 (AZ_PREC_F16X3): fp16 pieces -- the rows pre-scaled by 2^s (k_fc_finish applies p.rs = 2^-s),
+// the features split in fp16 with the range guard (p.ovf); v_mfma_f32_16x16x32_f16, same shape.
+typedef _Float16 f16x8n __attribute__((ext_vector_type(8)));
+template <int PT>
 __global__ __launch_bounds__(256) void k_fc_heads_x3(FcHeadArgs p) {
+    typedef typename std::conditional<PT == 2, f16x8n, bf16x8n>::type frag;
     const int NTP = (p.A + 63) / 64, NTV = (p.H + 63) / 64, NT = NTP + NTV;
     const int mt = blockIdx.x / NT, nt = blockIdx.x - mt * NT, sl = blockIdx.y, S = gridDim.y;
     const int mlim = p.m_limit ? min(p.B, *p.m_limit) : p.B;
@@ -585,12 +591,12 @@ __global__ __launch_bounds__(256) void k_fc_heads_x3(FcHeadArgs p) {
     const int gap = p.xs - p.hc;
     auto xoff = [&](int k) { return (size_t)k + (size_t)(k / p.hc) * gap; };
     typedef float f32x8n __attribute__((ext_vector_type(8)));
-    struct Ops { bf16x8n wh[2], wl[2]; f32x8n x[2]; };
+    struct Ops { frag wh[2], wl[2]; f32x8n x[2]; };
     auto fetch = [&](Ops& o, int k) {
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
-            o.wh[j] = *reinterpret_cast<const bf16x8n*>(wh[j] + k);
-            o.wl[j] = *reinterpret_cast<const bf16x8n*>(wl[j] + k);
+            o.wh[j] = *reinterpret_cast<const frag*>(wh[j] + k);
+            o.wl[j] = *reinterpret_cast<const frag*>(wl[j] + k);
         }
         const size_t xo = xoff(k + 8 * lg);
 #pragma unroll
@@ -600,33 +606,48 @@ __global__ __launch_bounds__(256) void k_fc_heads_x3(FcHeadArgs p) {
         }
     };
     f32x4n acc[2][2] = {};
+    float vmax = 0.0f;
+    auto mma = [](const frag& w, const frag& x, const f32x4n& c) {
+        if constexpr (PT == 2) return __builtin_amdgcn_mfma_f32_16x16x32_f16(w, x, c, 0, 0, 0);
+        else return __builtin_amdgcn_mfma_f32_16x16x32_bf16(w, x, c, 0, 0, 0);
+    };
     auto step = [&](const Ops& o) {
-        bf16x8n xh[2], xl[2];
+        frag xh[2], xl[2];
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
-            uint32_t h[4], l[4];
+            if constexpr (PT == 2) {
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const float a0 = o.x[i][2 * e], a1 = o.x[i][2 * e + 1];
-                const uint32_t b0 = fc_bf16_rne(a0), b1 = fc_bf16_rne(a1);
-                h[e] = b0 | (b1 << 16);
-                l[e] = fc_bf16_rne(a0 - __uint_as_float(b0 << 16)) | (fc_bf16_rne(a1 - __uint_as_float(b1 << 16)) << 16);
+                for (int e = 0; e < 8; ++e) {
+                    const float a = o.x[i][e];
+                    vmax = fmaxf(vmax, fabsf(a));
+                    xh[i][e] = (_Float16)a;
+                    xl[i][e] = (_Float16)(a - (float)xh[i][e]);
+                }
+            } else {
+                uint32_t h[4], l[4];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const float a0 = o.x[i][2 * e], a1 = o.x[i][2 * e + 1];
+                    const uint32_t b0 = fc_bf16_rne(a0), b1 = fc_bf16_rne(a1);
+                    h[e] = b0 | (b1 << 16);
+                    l[e] = fc_bf16_rne(a0 - __uint_as_float(b0 << 16)) | (fc_bf16_rne(a1 - __uint_as_float(b1 << 16)) << 16);
+                }
+                __builtin_memcpy(&xh[i], h, 16);
+                __builtin_memcpy(&xl[i], l, 16);
             }
-            __builtin_memcpy(&xh[i], h, 16);
-            __builtin_memcpy(&xl[i], l, 16);
         }
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
-            for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(o.wh[j], xh[i], acc[i][j], 0, 0, 0);
+            for (int j = 0; j < 2; ++j) acc[i][j] = mma(o.wh[j], xh[i], acc[i][j]);
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
-            for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(o.wl[j], xh[i], acc[i][j], 0, 0, 0);
+            for (int j = 0; j < 2; ++j) acc[i][j] = mma(o.wl[j], xh[i], acc[i][j]);
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
-            for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(o.wh[j], xl[i], acc[i][j], 0, 0, 0);
+            for (int j = 0; j < 2; ++j) acc[i][j] = mma(o.wh[j], xl[i], acc[i][j]);
     };
     // K steps of 32 in pairs (register double buffer with compile-time roles); KS / 32 is even
     // except for KS = 32 (handled by the tail)
@@ -641,6 +662,7 @@ __global__ __launch_bounds__(256) void k_fc_heads_x3(FcHeadArgs p) {
         step(B);
     }
     if (st < steps) step(A);
+    if (PT == 2 && !(vmax <= 65504.0f) && p.ovf) atomicOr(p.ovf, 1);
     // acc[i][j][e] = partial of board 16 i + l16, output 16 j + 4 lg + e (of the wave's 32 x 32)
     const int NC = NT * 64, BP = (p.B + 63) / 64 * 64;
     float* part = p.part + (size_t)sl * BP * NC;
@@ -671,10 +693,12 @@ __global__ __launch_bounds__(256) void k_fc_finish(FcHeadArgs p) {
         for (int s = 0; s < 16; ++s) if (s < S) t += v[s];
         return t;
     };
-    for (int n = lane; n < p.A; n += 64) p.logits[(size_t)b * p.A + n] = sum(n) + p.bp[n];
+    // k_fc_heads_x3<2>: the rows' 2^s scale undone (exact) before the bias
+    auto scl = [&](int col) { return p.rs ? p.rs[col] : 1.0f; };
+    for (int n = lane; n < p.A; n += 64) p.logits[(size_t)b * p.A + n] = sum(n) * scl(n) + p.bp[n];
     float d = 0.0f;
     for (int h = lane; h < p.H; h += 64) {
-        float v = sum(NTP * 64 + h) + p.bv1[h];
+        float v = sum(NTP * 64 + h) * scl(NTP * 64 + h) + p.bv1[h];
         v = v > 0.0f ? v : 0.0f;
         p.hid[(size_t)b * p.H + h] = v;
         d = __builtin_fmaf(v, p.wv2[h], d);
@@ -702,11 +726,16 @@ int az_fc_heads_splits(int B, int K, int A, int H) {
 
 void az_launch_fc_heads(const FcHeadArgs& a, hipStream_t st) {
     const int NT = (a.A + 63) / 64 + (a.H + 63) / 64, MT = (a.B + 63) / 64;
-    if (a.Wx_hi && a.Wx_lo && a.hc % 8 == 0 && (a.K / a.S) % 32 == 0)
-        hipLaunchKernelGGL(k_fc_heads_x3, dim3(MT * NT, a.S), dim3(256), 0, st, a);
-    else
+    FcHeadArgs f = a;
+    if (a.Wx_hi && a.Wx_lo && a.hc % 8 == 0 && (a.K / a.S) % 32 == 0) {
+        if (a.pt == 2) hipLaunchKernelGGL(k_fc_heads_x3<2>, dim3(MT * NT, a.S), dim3(256), 0, st, a);
+        else hipLaunchKernelGGL(k_fc_heads_x3<1>, dim3(MT * NT, a.S), dim3(256), 0, st, a);
+        if (a.pt != 2) f.rs = nullptr;
+    } else {
         hipLaunchKernelGGL(k_fc_heads, dim3(MT * NT, a.S), dim3(256), 0, st, a);
-    hipLaunchKernelGGL(k_fc_finish, dim3((a.B + 3) / 4), dim3(256), 0, st, a);
+        f.rs = nullptr;                                   // unscaled f32 rows
+    }
+    hipLaunchKernelGGL(k_fc_finish, dim3((a.B + 3) / 4), dim3(256), 0, st, f);
 }
 
 // split-K partial sums only (p.part, p.splits): the caller reduces them

@@ -43,18 +43,23 @@ import numpy as np  # noqa: E402
 T_START = time.perf_counter()
 
 METRIC = "self-play positions/sec (+ NN evals/sec) at 800 sims/move, 1/2/4/8 GPU"
-# Measured error of each trunk precision against the fp32 network (profiles/r02b_trained_scale.txt,
-# profiles/r03a_x3_net_parity.log: heads scaled to |logit|max 8, |value| 0.9, the magnitudes of a trained net)
+# Measured error of each trunk precision against the fp32 network (profiles/r04_f16x3_net_parity.log:
+# tests/test_gpu_trained_scale.py, a trained-like trunk -- per-channel BN scales a decade apart,
+# activations growing to ~64 -- with heads scaled to |logit|max 8, |value| 0.9, at each config's batch)
 PREC_NOTE = {
     "fp16": "fp16 MFMA operands, fp32 accumulation (the reference's opt-in useFp16, torch_neural_network.h:29); "
-            "trained-scale max|dlogit| 1.3e-3 (C3), 1.9e-3 (C4) vs the fp32 net: outside the 1e-4 parity "
-            "tolerance, see parity_mode for the fp32-faithful rate",
-    "bf16x3": "fp32-faithful: bf16 hi + lo operands, three MFMAs per product, fp32 accumulation; trained-scale "
-              "max|dlogit| 3.4e-5 (C3), 3.7e-5 (C4) vs the fp32 net: within the 1e-4 parity tolerance",
+            "trained-like max|dlogit| 4.9e-3 (C3), 4.6e-3 (C4), 7.0e-3 (C5) vs the fp32 net: outside the 1e-4 "
+            "parity tolerance, see parity_mode for the fp32-faithful rate",
+    "f16x3": "fp32-faithful: fp16 hi + lo operands (weights scaled 2^s per output channel), three MFMAs per "
+             "product, fp32 accumulation; trained-like max|dlogit| 1.0e-5 (C3), 1.0e-5 (C4), 1.7e-5 (C5) vs "
+             "the fp32 net: within the 1e-4 parity tolerance (activations |x| <= 65504, guarded)",
+    "bf16x3": "bf16 hi + lo operands, three MFMAs per product, fp32 accumulation (the full fp32 range); "
+              "trained-like max|dlogit| 7.5e-5 (C3), 5.6e-5 (C4), 1.4e-4 (C5) vs the fp32 net",
     "f32": "f32 MFMA (exact fp32 products)",
 }
-PEAK_TFLOPS = {"bf16x3": 2500.0, "bf16": 2500.0, "fp16": 2500.0, "f32": 157.3}   # dense MFMA peaks, MI355X_MICROARCH.md
-PREC = {"f32": 0, "bf16x3": 1, "bf16": 2, "fp16": 3}
+PEAK_TFLOPS = {"f16x3": 2500.0, "bf16x3": 2500.0, "bf16": 2500.0, "fp16": 2500.0, "f32": 157.3}   # dense MFMA peaks, MI355X_MICROARCH.md
+PREC = {"f32": 0, "bf16x3": 1, "bf16": 2, "fp16": 3, "f16x3": 4}
+PARITY_PREC = "f16x3"    # the parity precision parity_mode times
 # BASELINE.json configs: game, board, blocks, channels, sims/move, global games
 CONFIGS = {
     "c2": dict(game="gomoku", board=15, blocks=6, channels=64, sims=400, games=256,
@@ -84,21 +89,23 @@ def parse(argv=None):
     ap.add_argument("--blocks", type=int, default=None)
     ap.add_argument("--precision", default="fp16", choices=list(PREC),
                     help="trunk precision: fp16 = the reference useFp16 option (fp16 MFMA operands, fp32 accumulate, "
-                         "2^-20 residual stream), bf16x3 = fp32-faithful (three bf16 MFMAs per product)")
+                         "2^-20 residual stream), f16x3 = fp32-faithful (fp16 hi + lo pieces, three MFMAs per "
+                         "product), bf16x3 = bf16 hi + lo pieces (the full fp32 range, ~2^-17)")
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU restatement on rank 0 at N=1")
     ap.add_argument("--cpu-window", type=float, default=20.0, help="seconds of the CPU baseline's timed window")
     ap.add_argument("--cpu-workers", type=int, default=0, help="CPU baseline processes (0: the host's CPU share, <=16)")
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--parity-steps", type=int, default=1,
-                    help="N=1: also time this many moves of the same workload with the fp32-faithful bf16x3 trunk "
+                    help="N=1: also time this many moves of the same workload with the fp32-faithful f16x3 trunk "
                          "(the parity precision), reported as parity_mode; 0 disables")
     ap.add_argument("--parity-warmup", type=int, default=1)
     ap.add_argument("--time-budget", type=float, default=560.0,
                     help="seconds: parity_mode is skipped (and says so) when the run so far plus its estimated "
                          "time would exceed this (the driver's run limit is 600 s)")
     ap.add_argument("--kernel-timing", type=int, default=1,
-                    help="HIP events around sampled trunk / tree launches (the roofline); 0 for rocprofv3 --pmc "
-                         "passes: a search that records events hangs under counter collection (tools/pmc_hang_probe2.sh)")
+                    help="device clock stamps (s_memrealtime, 100 MHz) around sampled trunk / tree launches (the "
+                         "roofline); 0 disables (round 3's HIP-event timing hung under rocprofv3 --pmc; the "
+                         "stamps do not)")
     ap.add_argument("--dist-timeout", type=float, default=600.0,
                     help="seconds a rank waits in a collective / barrier before the bench fails (N>1)")
     a = ap.parse_args(argv)
@@ -328,7 +335,12 @@ def _same_kernel(profiled, name):
 
     def parts(s):
         m = re.search(r"(conv3x3_v[0-9a-z]+)<([^>]*)>", s)
-        return (m.group(1), [x.strip() for x in m.group(2).split(",")][:-1]) if m else None
+        if not m:
+            return None
+        args = [x.strip() for x in m.group(2).split(",")]
+        # the split-operand kernels (v7x3 / v9x3: <board, geometry[, variant], piece type> in rocprof,
+        # <board, SLIM|DENSE[, f16]> as labelled): the board; the piece type is the precision's
+        return (m.group(1), args[:1] if m.group(1).endswith("x3") else args[:-1])
     p1, p2 = parts(profiled), parts(name)
     return bool(p1 and p2 and p1 == p2)
 
@@ -425,11 +437,11 @@ def cpu_baseline_line(a, raw, evals_per_move):
 
 
 def parity_mode(a, make_workload, dev):
-    """The same workload with the fp32-faithful trunk (bf16x3), a short timed run in the same process
+    """The same workload with the fp32-faithful trunk (f16x3), a short timed run in the same process
     (N=1, after the headline run has freed its device memory): positions/s and its own roofline."""
     import copy
     b = copy.copy(a)
-    b.precision, b.steps, b.warmup = "bf16x3", a.parity_steps, a.parity_warmup
+    b.precision, b.steps, b.warmup = PARITY_PREC, a.parity_steps, a.parity_warmup
     out = run_rank(b, 0, 1, None, make_workload, dev)
     keys = ("value", "unit", "steps", "warmup", "ms_per_step", "dtype", "dtype_note", "nn_evals_per_s",
             "evals_per_move", "roofline")
@@ -493,8 +505,8 @@ def main(argv=None, make_workload=None, backend=None):
         out = run_rank(a, rank, world, dist, make_workload, dev)
         if out is not None:
             out["cpu_baseline"] = cpu_baseline_line(a, raw_cpu, out["evals_per_move"]) if raw_cpu else None
-            if world == 1 and a.parity_steps > 0 and a.precision != "bf16x3" and a.channels % 64 == 0:
-                # bf16x3 moves take ~2.7x the fp16 trunk's (1.31 vs 0.485 ms per launch), plus setup
+            if world == 1 and a.parity_steps > 0 and a.precision not in ("f16x3", "bf16x3") and a.channels % 64 == 0:
+                # f16x3 moves take ~2.5x the fp16 trunk's (1.19 vs 0.485 ms per launch), plus setup
                 est = (a.parity_steps + a.parity_warmup) * out["ms_per_step"] / 1e3 * 2.8 + 20.0
                 spent = time.perf_counter() - T_START
                 if spent + est <= a.time_budget:

@@ -221,6 +221,11 @@ def test_pmc_traffic_matches_each_trunk_kernel():
     assert not bench._same_kernel("void conv3x3_v7<2, 15, 1>(ConvBf16Args)", "conv3x3_v7x3<15, SLIM>")
     assert not bench._same_kernel("void conv3x3_v6<2, 15, 1>(ConvBf16Args)", "conv3x3_v7<2, 15, SLIM>")
     assert not bench._same_kernel("void conv3x3_v7<1, 15, 1>(ConvBf16Args)", "conv3x3_v7<2, 15, SLIM>")
+    # the split-operand kernels: rocprof <board, geometry, variant, piece type> vs the label
+    assert bench._same_kernel("void conv3x3_v9x3<15, 1, 3, 2>(ConvBf16Args)", "conv3x3_v9x3<15, SLIM, f16>")
+    assert bench._same_kernel("void conv3x3_v9x3<19, 2, 3, 1>(ConvBf16Args)", "conv3x3_v9x3<19, DENSE>")
+    assert not bench._same_kernel("void conv3x3_v9x3<15, 1, 3, 2>(ConvBf16Args)", "conv3x3_v7x3<15, SLIM, f16>")
+    assert not bench._same_kernel("void conv3x3_v9x3<15, 1, 3, 2>(ConvBf16Args)", "conv3x3_v9x3<19, DENSE, f16>")
     net = dict(board=15, channels=256, blocks=20)
     fp16 = bench.pmc_traffic(types.SimpleNamespace(precision="fp16", **net), "conv3x3_v7<2, 15, SLIM>", 2048.0)
     x3 = bench.pmc_traffic(types.SimpleNamespace(precision="bf16x3", **net), "conv3x3_v7x3<15, SLIM>", 2048.0)

@@ -6,7 +6,7 @@ OUT=$1; TO=$2; shift 2
 for i in $(seq 1 ${RETRIES:-12}); do
   /usr/local/graft/bin/gpurun --timeout "$TO" -- "$@" > "$OUT" 2>&1
   rc=$?
-  if [ $rc -eq 3 ] || { grep -q "status=transient" "$OUT" && grep -q "run 0.0s" "$OUT"; }; then
+  if [ $rc -eq 3 ] || { grep -q "status=transient" "$OUT" && grep -qE "run 0.0s|run Nones|backing off" "$OUT"; }; then
     echo "attempt $i: no box ($(date +%T)), retrying" >> "$OUT.retries"
     sleep ${RETRY_SLEEP:-90}
     continue

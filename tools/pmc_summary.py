@@ -61,8 +61,8 @@ def main():
     rd = c["FETCH_SIZE"] * 1024 * 2
     wr = c["WRITE_SIZE"] * 1024
     B, C, HW = a.boards, a.channels, a.board * a.board
-    x3 = a.precision == "bf16x3"
-    act = B * HW * C * (4 if x3 else 2)          # bf16x3: hi + lo bf16 planes; fp16: one 16-bit plane
+    x3 = a.precision in ("bf16x3", "f16x3")
+    act = B * HW * C * (4 if x3 else 2)          # bf16x3 / f16x3: hi + lo 16-bit planes; fp16: one 16-bit plane
     out = {"kernel": name or a.kernel,
            "workload": f"tools/net_bench.py --game {a.game} --precision {a.precision} --batch {B}: "
                        f"{'C3' if a.game == 'gomoku15' else a.game} net forward, B={B} boards per launch "
@@ -77,7 +77,7 @@ def main():
                     {"activations_in": act, "residual_in_avg": act / 2 if x3 else act * 1.5 / 2,
                      "out_avg": act if x3 else act * 1.25, "weights": 9 * C * C * (4 if x3 else 2)},
                 "algorithmic_note":
-                    (f"g8 bf16 hi + lo activations {B}x{HW}x{C}x4 B = {act / 1e6:.0f} MB in and out per launch; "
+                    (f"g8 hi + lo activations {B}x{HW}x{C}x4 B = {act / 1e6:.0f} MB in and out per launch; "
                      "the 2nd conv of a block also reads the residual (hi + lo); weights hi + lo 2.4 MB") if x3 else
                     (f"g8 activations {B}x{HW}x{C}x2 B = {act / 1e6:.0f} MB in and out per launch; "
                      "the 2nd conv of a block also reads the residual (16-bit + int8) and writes the "

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-4 measurements: the default bench line (C3 + parity_mode + CPU baseline), per-rank shard
 # lines of the 8-GPU configs on one GPU (C3 256 games, C4 128 games, the C5 net at 128 boards),
-# the bf16x3 trunk PMC (conv3x3_v9x3), the tree-kernel PMC at the C3 bench config.
+# (PMC passes: tools/r4_pmc.sh)
 set -o pipefail
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out/r4m
@@ -15,7 +15,3 @@ $T 300 python -u bench.py --config c4 --global-games 128 --steps 3 --warmup 1 --
 for f in bench_c3_g256 bench_c4 bench_c4_g128; do python3 -c "import json,sys;d=json.loads(open('$O/$f.json').read().strip().splitlines()[-1]);print('$f', round(d['value'],2), d['config']['games_per_gpu'], round(d['roofline']['frac'],4), d['roofline']['kernel'])"; done
 for B in 1024 128; do $T 120 python -u tools/net_bench.py --game chess --batch $B --iters 10 2>&1 | tee -a $O/c5_net.txt || exit 1; done
 for B in 1024 128; do $T 120 python -u tools/net_bench.py --game go19 --batch $B --iters 10 2>&1 | tee -a $O/c4_net.txt || exit 1; done
-GAME=gomoku15 BATCH=2048 $T 700 tools/pmc_conv.sh bf16x3 r4_x3 > $O/pmc_x3.log 2>&1 || { tail -5 $O/pmc_x3.log; exit 1; }
-python3 tools/pmc_summary.py gpurun_out/pmc_r4_x3 --kernel conv3x3_v9x3 --precision bf16x3 --out $O/r04_bf16x3_v9x3_trunk_pmc.json || exit 1
-CONFIG=c3 BLOCKS=20 TAG=r4m/tree_c3 PMC_TIMEOUT=300 $T 1000 tools/tree_pmc.sh > $O/tree_c3.log 2>&1 || { tail -5 $O/tree_c3.log; exit 1; }
-tail -30 $O/tree_c3.log
