@@ -803,6 +803,16 @@ __global__ __launch_bounds__(512, 1) void conv3x3_v9x3(ConvBf16Args p) {
     const int n0 = nb * BNT;
     const int nboards = p.m_limit ? *p.m_limit : p.M / HW;
     if (DENSE ? tile * 256 >= nboards * HW : tile >= nboards) return;
+    // First-round stagger: the blocks of a launch run in lockstep rounds (one per CU, identical
+    // work), so every CU reaches its epilogue at once and the epilogues' stores (and the second
+    // conv's residual reads) saturate HBM together (tools/v9_stamps.py: 22 us of a 148 us block).
+    // Offsetting the first round's starts over p.stagger ns keeps the CUs out of phase for the
+    // whole launch, and each epilogue overlaps other CUs' main loops.
+    if (p.stagger > 0 && blockIdx.x < 256) {
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        const uint64_t wait = (uint64_t)(((blockIdx.x * 37u) & 63u) * (uint32_t)p.stagger) / 640u;   // 10 ns ticks
+        while (__builtin_amdgcn_s_memrealtime() - t0 < wait) __builtin_amdgcn_s_sleep(4);
+    }
     V9_STAMP(0);
     const int C = p.C, GI = C / 8, GO = p.N / 8;
     const int NCH = C / 32, NS = 9 * NCH;
@@ -1039,7 +1049,9 @@ __global__ __launch_bounds__(512, 1) void conv3x3_v9x3(ConvBf16Args p) {
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     V9_STAMP(2);
 
-    // epilogue from the accumulators: residual hi + lo joined in fp32, ReLU, split, streaming stores
+    // epilogue from the accumulators: residual hi + lo joined in fp32, ReLU, split, streaming stores.
+    // The residual of row fragments 0-3 is loaded in one burst, then 4-7 once 0-3 are stored (their
+    // accumulators and residual registers free): two memory round trips per wave, not eight.
     const __amdgpu_buffer_rsrc_t rh = __builtin_amdgcn_make_buffer_rsrc((void*)p.Rhi, (short)0, 0x7fffffff, 0x00020000);
     const __amdgpu_buffer_rsrc_t rl = __builtin_amdgcn_make_buffer_rsrc((void*)p.Rlo, (short)0, 0x7fffffff, 0x00020000);
     const int chl = n0 + wn * 64 + 4 * lg;
@@ -1049,63 +1061,79 @@ __global__ __launch_bounds__(512, 1) void conv3x3_v9x3(ConvBf16Args p) {
         for (int j = 0; j < 4; ++j) osc[j] = *reinterpret_cast<const float4*>(p.oscale + chl + j * 16);
     }
     float vmax = 0.0f;                                    // PT 2: fp16 range guard
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
+    auto row_of = [&](int i, int& b, int& pix) -> bool {  // output row of fragment i of this lane
         const int q = wm * 128 + i * 16 + l16;
-        int b, pix;
-        bool live;
         if constexpr (DENSE) {
             const int gq = tile * 256 + q;
             b = gq / HW;
             pix = gq - b * HW;
-            live = b < nboards;
+            return b < nboards;
         } else {
             const int y = q / WG, x = q - y * WG;
             b = tile;
             pix = y * HB + x;
-            live = y < HB && x < HB;
+            return y < HB && x < HB;
         }
-        if (!live) continue;
-        u32x2_t hv[4], lv[4];
-        if (p.Rhi) {
+    };
+    u32x2_t hv[4][4], lv[4][4];
+    auto load_res = [&](auto i0c) {
+        constexpr int i0 = decltype(i0c)::value;
+#pragma unroll
+        for (int ii = 0; ii < 4; ++ii) {
+            int b, pix;
+            if (!row_of(i0 + ii, b, pix)) continue;
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 const int ch = chl + j * 16;
                 const size_t e = (((size_t)b * GO + (ch >> 3)) * HW + pix) * 8 + (ch & 7);
-                hv[j] = __builtin_amdgcn_raw_buffer_load_b64(rh, (int)(e * 2), 0, 2);
-                lv[j] = __builtin_amdgcn_raw_buffer_load_b64(rl, (int)(e * 2), 0, 2);
+                hv[ii][j] = __builtin_amdgcn_raw_buffer_load_b64(rh, (int)(e * 2), 0, 2);
+                lv[ii][j] = __builtin_amdgcn_raw_buffer_load_b64(rl, (int)(e * 2), 0, 2);
             }
         }
+    };
+    auto finish = [&](auto i0c) {
+        constexpr int i0 = decltype(i0c)::value;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int ch = chl + j * 16;
-            const size_t e = (((size_t)b * GO + (ch >> 3)) * HW + pix) * 8 + (ch & 7);
-            float o[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-            if constexpr (PT == 2) {
-                o[0] *= osc[j].x; o[1] *= osc[j].y; o[2] *= osc[j].z; o[3] *= osc[j].w;
-            }
-            if (p.Rhi) {
-                uint16_t hh[4], ll[4];
-                __builtin_memcpy(hh, &hv[j], 8);
-                __builtin_memcpy(ll, &lv[j], 8);
+        for (int ii = 0; ii < 4; ++ii) {
+            const int i = i0 + ii;
+            int b, pix;
+            if (!row_of(i, b, pix)) continue;
 #pragma unroll
-                for (int k = 0; k < 4; ++k) o[k] += H::to_f(hh[k]) + H::to_f(ll[k]);
-            }
-            uint16_t oh[4], ol[4];
+            for (int j = 0; j < 4; ++j) {
+                const int ch = chl + j * 16;
+                const size_t e = (((size_t)b * GO + (ch >> 3)) * HW + pix) * 8 + (ch & 7);
+                float o[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+                if constexpr (PT == 2) {
+                    o[0] *= osc[j].x; o[1] *= osc[j].y; o[2] *= osc[j].z; o[3] *= osc[j].w;
+                }
+                if (p.Rhi) {
+                    uint16_t hh[4], ll[4];
+                    __builtin_memcpy(hh, &hv[ii][j], 8);
+                    __builtin_memcpy(ll, &lv[ii][j], 8);
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                o[k] = __builtin_amdgcn_fmed3f(o[k], 0.0f, 3.0e38f);   // ReLU
-                if constexpr (PT == 2) vmax = fmaxf(vmax, o[k]);
-                oh[k] = H::from_f(o[k]);
-                ol[k] = H::from_f(o[k] - H::to_f(oh[k]));
+                    for (int k = 0; k < 4; ++k) o[k] += H::to_f(hh[k]) + H::to_f(ll[k]);
+                }
+                uint16_t oh[4], ol[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    o[k] = __builtin_amdgcn_fmed3f(o[k], 0.0f, 3.0e38f);   // ReLU
+                    if constexpr (PT == 2) vmax = fmaxf(vmax, o[k]);
+                    oh[k] = H::from_f(o[k]);
+                    ol[k] = H::from_f(o[k] - H::to_f(oh[k]));
+                }
+                u32x2_t hs, ls;
+                __builtin_memcpy(&hs, oh, 8);
+                __builtin_memcpy(&ls, ol, 8);
+                asm volatile("global_store_dwordx2 %0, %1, off nt" ::"v"(p.Chi + e), "v"(hs) : "memory");
+                asm volatile("global_store_dwordx2 %0, %1, off nt" ::"v"(p.Clo + e), "v"(ls) : "memory");
             }
-            u32x2_t hs, ls;
-            __builtin_memcpy(&hs, oh, 8);
-            __builtin_memcpy(&ls, ol, 8);
-            asm volatile("global_store_dwordx2 %0, %1, off nt" ::"v"(p.Chi + e), "v"(hs) : "memory");
-            asm volatile("global_store_dwordx2 %0, %1, off nt" ::"v"(p.Clo + e), "v"(ls) : "memory");
         }
-    }
+    };
+    using I4 = std::integral_constant<int, 4>;
+    if (p.Rhi) load_res(I0{});
+    finish(I0{});
+    if (p.Rhi) load_res(I4{});
+    finish(I4{});
 #ifdef AZ_V9_STAMPS
     V9_STAMP(3);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1179,6 +1207,11 @@ static void v7x3_launch_g(const ConvBf16Args& a, hipStream_t st) {
 }
 
 int az_conv_flags();
+// first-round stagger (ns; az_diag_set_v9_stagger): 32 us measured best of 0 / 8 / 16 / 32 / 64 us,
+// -0.8 % per C3 launch, -0.7 % C4 (profiles/r04_v9x3_stagger.txt); only on launches of >= 1024 blocks
+// (several rounds), where a one-off delay of the last-started CU is amortised
+static int g_v9_stagger = 32000;
+extern "C" int az_diag_set_v9_stagger(int ns) { g_v9_stagger = ns; return 0; }
 // conv3x3_v9x3 variants (A/B measurement, bf16 pieces): flag 0x20000000 puts the tap barrier at the
 // tap start instead of after unit U0, 0x40000000 keeps the SLIM tile's dead 16th fragment in waves
 // 4-7.  fp16 pieces (AZ_PREC_F16X3) run the default variant only.
@@ -1188,15 +1221,17 @@ static void v9x3_launch_g(const ConvBf16Args& a, hipStream_t st) {
     const int tiles = GEO == GEO_DENSE ? (boards * HB * HB + 255) / 256 : boards;
     const int f = az_conv_flags(), var = ((f & 0x20000000) ? 0 : 1) | ((f & 0x40000000) ? 0 : 2);
     const dim3 grid(tiles * (a.N / 256)), block(512);
+    ConvBf16Args b = a;
+    b.stagger = tiles * (a.N / 256) >= 1024 ? g_v9_stagger : 0;
     if (a.pt == 2) {
-        hipLaunchKernelGGL((conv3x3_v9x3<HB, GEO, 3, 2>), grid, block, 0, st, a);
+        hipLaunchKernelGGL((conv3x3_v9x3<HB, GEO, 3, 2>), grid, block, 0, st, b);
         return;
     }
     switch (var) {
-        case 0: hipLaunchKernelGGL((conv3x3_v9x3<HB, GEO, 0, 1>), grid, block, 0, st, a); break;
-        case 1: hipLaunchKernelGGL((conv3x3_v9x3<HB, GEO, 1, 1>), grid, block, 0, st, a); break;
-        case 2: hipLaunchKernelGGL((conv3x3_v9x3<HB, GEO, 2, 1>), grid, block, 0, st, a); break;
-        default: hipLaunchKernelGGL((conv3x3_v9x3<HB, GEO, 3, 1>), grid, block, 0, st, a); break;
+        case 0: hipLaunchKernelGGL((conv3x3_v9x3<HB, GEO, 0, 1>), grid, block, 0, st, b); break;
+        case 1: hipLaunchKernelGGL((conv3x3_v9x3<HB, GEO, 1, 1>), grid, block, 0, st, b); break;
+        case 2: hipLaunchKernelGGL((conv3x3_v9x3<HB, GEO, 2, 1>), grid, block, 0, st, b); break;
+        default: hipLaunchKernelGGL((conv3x3_v9x3<HB, GEO, 3, 1>), grid, block, 0, st, b); break;
     }
 }
 

@@ -964,7 +964,9 @@ int net_heads_fc(az_net* n, int B, const int* nb, float* logits, float* value, h
         // scaled fp16 pieces (~2^-21, as its trunk).  AZ_PREC_BF16X3 and F32 keep exact f32 products
         // (bf16 pieces would add ~2.5e-5 at trained-scale logits).  Conv flag 0x08000000 keeps the f32
         // k_fc_heads (A/B, diagnosis).
-        const bool fx = !(az_conv_flags() & 0x08000000) && n->fcx_hi;
+        // Below 512 boards of capacity the f32 pair is the faster one (C2, 256 boards: k_fc_heads 10.6 us
+        // vs k_fc_heads_x3 12.0 -- both latency-bound chains of L2 round trips at 0.5 GFLOP).
+        const bool fx = !(az_conv_flags() & 0x08000000) && n->fcx_hi && d.max_batch >= 512;
         if (fx && (d.precision == AZ_PREC_FP16 || d.precision == AZ_PREC_BF16)) {
             fa.Wx_hi = n->fcx_hi; fa.Wx_lo = n->fcx_lo; fa.pt = 1;
             fa.S = az_fc_heads_splits_x3(d.max_batch, HK, d.action_size, d.fc_hidden);

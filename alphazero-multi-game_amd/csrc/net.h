@@ -48,6 +48,7 @@ struct ConvBf16Args {
     int* ovf;                                   // fp16 outputs: set to 1 when a value leaves the fp16 range (or null)
     int pt;                                     // x3 kernels (v7x3 / v9x3): pieces 1 = bf16 (0 reads as 1), 2 = fp16
     const float* oscale;                        // pt 2: per-output-channel 2^-s undoing the weights' scale 2^s
+    int stagger;                                // conv3x3_v9x3: first-round start offsets spread over this many ns
 };
 
 // k_smallnet (smallnet.hip): the whole trunk + pool + head 1x1 convs of a 64-filter net, one board per block

@@ -673,14 +673,17 @@ __global__ __launch_bounds__(256) void k_fc_heads_x3(FcHeadArgs p) {
             *reinterpret_cast<f32x4n*>(part + (size_t)(m0 + wm * 32 + 16 * i + l16) * NC + nt * 64 + wn * 32 + 16 * j + 4 * lg) = acc[i][j];
 }
 
-// Finish both heads, one wave per board (4 boards per block): K slices summed in slice order (loads
+// Finish both heads, one 256-thread block per board: K slices summed in slice order (loads
 // unrolled), biases, the value hidden layer (ReLU) and value = tanh(hid . w2 + b2), the dot product
-// reduced across the wave by a fixed xor butterfly (deterministic, no block barrier).
+// reduced by a fixed xor butterfly per wave and the four wave sums added in wave order
+// (deterministic).  (Round 4 tried one wave per board, four boards per block: a quarter of the
+// blocks, 11.0 vs 5.2 us at C2.)
 __global__ __launch_bounds__(256) void k_fc_finish(FcHeadArgs p) {
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int b = blockIdx.x * 4 + wave;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, tid = threadIdx.x;
+    const int b = blockIdx.x;
     const int mlim = p.m_limit ? min(p.B, *p.m_limit) : p.B;
-    if (b >= mlim) return;                             // wave-uniform
+    if (b >= mlim) return;                             // block-uniform
+    __shared__ float wsum[4];
     const int NTP = (p.A + 63) / 64, NTV = (p.H + 63) / 64, NC = (NTP + NTV) * 64, BP = (p.B + 63) / 64 * 64, S = p.S;
     const float* row = p.part + (size_t)b * NC;
     const size_t sstride = (size_t)BP * NC;
@@ -695,9 +698,9 @@ __global__ __launch_bounds__(256) void k_fc_finish(FcHeadArgs p) {
     };
     // k_fc_heads_x3<2>: the rows' 2^s scale undone (exact) before the bias
     auto scl = [&](int col) { return p.rs ? p.rs[col] : 1.0f; };
-    for (int n = lane; n < p.A; n += 64) p.logits[(size_t)b * p.A + n] = sum(n) * scl(n) + p.bp[n];
+    for (int n = tid; n < p.A; n += 256) p.logits[(size_t)b * p.A + n] = sum(n) * scl(n) + p.bp[n];
     float d = 0.0f;
-    for (int h = lane; h < p.H; h += 64) {
+    for (int h = tid; h < p.H; h += 256) {
         float v = sum(NTP * 64 + h) * scl(NTP * 64 + h) + p.bv1[h];
         v = v > 0.0f ? v : 0.0f;
         p.hid[(size_t)b * p.H + h] = v;
@@ -705,15 +708,17 @@ __global__ __launch_bounds__(256) void k_fc_finish(FcHeadArgs p) {
     }
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) d += __shfl_xor(d, off);
-    if (lane == 0) p.value[b] = tanhf(d + p.bv2[0]);
+    if (lane == 0) wsum[wave] = d;
+    __syncthreads();
+    if (tid == 0) p.value[b] = tanhf(((wsum[0] + wsum[1]) + (wsum[2] + wsum[3])) + p.bv2[0]);
 }
 
-// k_fc_heads_x3: its tiles run ~5x faster than the f32 ones, so fewer K slices (less partial
-// traffic for k_fc_finish): enough blocks to cover the CUs once, slices of >= 256 K
+// k_fc_heads_x3: a block's K steps are a dependent chain of global-load round trips, so slices
+// until the blocks cover the CUs once (C2: 32 tiles x 8 slices of 256 K), slices of >= 128 K
 int az_fc_heads_splits_x3(int B, int K, int A, int H) {
     const int tiles = (B + 63) / 64 * ((A + 63) / 64 + (H + 63) / 64);
     int s = 1;
-    while (s < 16 && tiles * s < 256 && K % (2 * s * 32) == 0 && K / (2 * s) >= 256) s *= 2;
+    while (s < 16 && tiles * s < 256 && K % (2 * s * 32) == 0 && K / (2 * s) >= 128) s *= 2;
     return s;
 }
 
@@ -735,7 +740,7 @@ void az_launch_fc_heads(const FcHeadArgs& a, hipStream_t st) {
         hipLaunchKernelGGL(k_fc_heads, dim3(MT * NT, a.S), dim3(256), 0, st, a);
         f.rs = nullptr;                                   // unscaled f32 rows
     }
-    hipLaunchKernelGGL(k_fc_finish, dim3((a.B + 3) / 4), dim3(256), 0, st, f);
+    hipLaunchKernelGGL(k_fc_finish, dim3(a.B), dim3(256), 0, st, f);
 }
 
 // split-K partial sums only (p.part, p.splits): the caller reduces them

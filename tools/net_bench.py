@@ -40,6 +40,9 @@ def main():
     if os.environ.get("AZ_CONV_FLAGS"):
         from az_amd import _lib as _l
         _l.lib().az_diag_set_conv_flags(int(os.environ["AZ_CONV_FLAGS"], 0))
+    if os.environ.get("AZ_V9_STAGGER"):
+        from az_amd import _lib as _l
+        _l.lib().az_diag_set_v9_stagger(int(os.environ["AZ_V9_STAGGER"]))
     eng = az_amd.Engine(int(os.environ.get("LOCAL_RANK", 0)))
     desc = az_amd.NetDesc(bs, planes, a.channels, a.blocks, actions, 32, 8, 256, 1, 0, PREC[a.precision], a.batch)
     net = az_amd.HipNeuralNetwork(eng, desc)
