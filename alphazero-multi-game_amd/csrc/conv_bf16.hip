@@ -1670,6 +1670,7 @@ static void v6_launch(const ConvBf16Args& a, int mode, hipStream_t st) {
 
 bool az_conv_v7_supported(const ConvBf16Args& a);
 int az_conv_v7_launch(const ConvBf16Args& a, int mode, int geo15, hipStream_t st);
+int az_conv_v7_tm(const ConvBf16Args& a);
 
 // Which kernel az_conv_g8_launch takes for a layer (a.flags already set): 0 none (unsupported),
 // 1 conv3x3_v7 (*geo = its 15x15 tile geometry), 2 conv3x3_v6 (*geo = 1 when DENSE), 3 conv3x3_v5.
@@ -1684,6 +1685,16 @@ static int g8_choice(const ConvBf16Args& a, int* geo) {
     if (!(a.flags & 0x100) && (a.H == 15 || !(a.flags & 0x200)) && (boards_g8 >= 1024 || (a.flags & 0x800)) &&
         az_conv_v7_supported(a)) {
         *geo = (a.flags & 8) ? 2 : (a.flags & 0x400) ? 0 : 1;
+        return 1;
+    }
+    // Small batches on the DENSE boards (the per-rank shards of the 8-GPU C4 / C5 configs): v6's
+    // 512-row tiles leave most CUs idle (C5 net, 128 boards: 32 blocks), conv3x3_v7 with 128 / 64-row
+    // tiles (az_conv_v7_tm) fills them -- 128 boards of 8x8: 0.0237 vs 0.0644 ms per launch; 19x19:
+    // faster from 256 boards (0.134 vs 0.140 ms), not at 128 (0.076 vs 0.073;
+    // profiles/r04_small_batch_tiles.txt).  Flag 0x1000 keeps v6 (A/B).
+    if (!(a.flags & (0x100 | 0x1000)) && a.H != 15 && boards_g8 < 1024 && (a.H < 19 || boards_g8 >= 256) &&
+        az_conv_v7_supported(a)) {
+        *geo = 2;
         return 1;
     }
     const size_t HW = (size_t)a.H * a.W;
@@ -1735,7 +1746,12 @@ int az_conv_g8_name(const ConvBf16Args& a_in, int mode, char* out, int len) {
     int geo = 0;
     static const char* g7[3] = {"PAD", "SLIM", "DENSE"};
     switch (g8_choice(a, &geo)) {
-        case 1: snprintf(out, len, "conv3x3_v7<%d, %d, %s>", mode, a.H, g7[a.H == 15 ? geo : 2]); return 0;
+        case 1: {
+            const int g = a.H == 15 ? geo : 2, tm = g == 2 ? az_conv_v7_tm(a) : 256;
+            if (tm != 256) snprintf(out, len, "conv3x3_v7<%d, %d, %s, %d>", mode, a.H, g7[g], tm);
+            else snprintf(out, len, "conv3x3_v7<%d, %d, %s>", mode, a.H, g7[g]);
+            return 0;
+        }
         case 2: snprintf(out, len, "conv3x3_v6<%d, %d%s>", mode, a.H, geo ? ", DENSE" : ""); return 0;
         case 3: snprintf(out, len, "conv3x3_v5<%d, 8>", mode); return 0;
         default: return -1;

@@ -152,31 +152,39 @@ __device__ __forceinline__ void static_for(Fn&& f) {
 //            power-limited chip little -- a branch around them would route every accumulator
 //            through phi copies and spill)
 //  GEO_DENSE 256 consecutive pixels of the batch, taps that leave the board zeroed in the fragments
+//  TM        DENSE only: output rows per tile (256; 128 / 64 for small batches, conv3x3_v7 only)
 enum { GEO_PAD = 0, GEO_SLIM = 1, GEO_DENSE = 2 };
-template <int HB, int GEO>
+template <int HB, int GEO, int TM = 256>
 struct Geom7 {
     static constexpr bool DENSE = GEO == GEO_DENSE, SLIM = GEO == GEO_SLIM;
     static constexpr int WG = DENSE ? HB : SLIM ? HB + 1 : HB + 2;   // grid / halo row width
     static constexpr int HW = HB * HB;
-    static constexpr int GRID = DENSE ? 256 : HB * WG;               // output grid rows of a tile
+    static constexpr int GRID = DENSE ? TM : HB * WG;                // output grid rows of a tile
     static constexpr int NFRAG = (GRID + 15) / 16;                   // 16-row fragments with live rows
-    static constexpr int TROWS = DENSE ? 256 + 2 * HB + 2 : SLIM ? NFRAG * 16 + 2 * WG + 2 : (HB + 2) * (HB + 2);
-    static constexpr int HROWS = 320;                         // 5 DMA pieces of 64 rows per 8-channel group
-    static_assert(TROWS <= HROWS, "halo does not fit 320 rows");
-    static_assert(GRID <= 256 && NFRAG > 8, "grid does not fit a 256-row tile");
+    static constexpr int TROWS = DENSE ? TM + 2 * HB + 2 : SLIM ? NFRAG * 16 + 2 * WG + 2 : (HB + 2) * (HB + 2);
+    // DMA pieces of 64 rows per 8-channel group: 5 (320 rows) for 256-row tiles
+    static constexpr int HROWS = (DENSE && TM < 256) ? (TROWS + 63) / 64 * 64 : 320;
+    static constexpr int NRB = HROWS / 64;
+    static_assert(TROWS <= HROWS, "halo does not fit");
+    static_assert(DENSE ? (TM == 256 || TM == 128 || TM == 64) : (TM == 256 && GRID <= 256 && NFRAG > 8),
+                  "tile geometry");
 };
 
 }  // namespace
 
 // MODE 2: fp16 operands, MODE 1: bf16.  Requires C % 64 == 0 (an even number of 32-channel
 // chunks), N % 128 == 0, a ReLU (every g8 conv has one), no fp32 output.
-template <int MODE, int HB, int GEO>
+// TM < 256 (DENSE, small batches): each wave owns TM / 2 rows = NI fragments (4 or 2) x 64
+// channels, one A register set (no second row half); the halo is NRB pieces per group.
+template <int MODE, int HB, int GEO, int TM = 256>
 __global__ __launch_bounds__(256, 2) void conv3x3_v7(ConvBf16Args p) {
     typedef H16<MODE> H;
-    typedef Geom7<HB, GEO> GM;
+    typedef Geom7<HB, GEO, TM> GM;
     constexpr bool DENSE = GM::DENSE, SLIM = GM::SLIM;
     typedef typename std::conditional<MODE == 2, f16x8, bf16x8>::type frag;
-    constexpr int BNT = 128, WG = GM::WG, HW = GM::HW, HROWS = GM::HROWS;
+    constexpr int BNT = 128, WG = GM::WG, HW = GM::HW, HROWS = GM::HROWS, NRB = GM::NRB;
+    constexpr int NI = TM / 32, NA = NI < 4 ? NI : 4, HALVES = NI / NA;   // fragments per wave / per A set
+    constexpr int WR = TM / 2;                            // rows per wave
     constexpr int A_BUF = 4 * HROWS * 16;                 // one chunk: [4 groups][320 rows][16 B] = 20 KB
     constexpr int B_TAP = 4 * BNT * 16;                   // one tap: [4 groups][128 ch][16 B] = 8 KB
     constexpr int LDS = 2 * A_BUF + 4 * B_TAP;            // 72 KB
@@ -190,7 +198,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_v7(ConvBf16Args p) {
     const int nb = slot % nsplit, tile = (slot / nsplit) * 8 + xcd;   // a tile's channel halves share an XCD
     const int n0 = nb * BNT;
     const int nboards = p.m_limit ? *p.m_limit : p.M / HW;
-    if (DENSE ? tile * 256 >= nboards * HW : tile >= nboards) return;
+    if (DENSE ? tile * TM >= nboards * HW : tile >= nboards) return;
     const int C = p.C, GI = C / 8, GO = p.N / 8;
     const int NCH = C / 32, NS = 9 * NCH;
 
@@ -204,12 +212,12 @@ __global__ __launch_bounds__(256, 2) void conv3x3_v7(ConvBf16Args p) {
     // source offset is recomputed at every issue (a handful of VALU; keeping five offsets live
     // across the main loop would spill)
     auto a_src = [&](int j, int ln) -> uint32_t {
-        const int q = wave + 4 * j, rb = q % 5, g = q / 5;
+        const int q = wave + 4 * j, rb = q % NRB, g = q / NRB;
         const int hr = rb * 64 + ln;
         int Y, X, b;
         bool in;
-        if constexpr (DENSE) {                            // halo row -> pixel tile*256 - HB - 1 + hr
-            const int gpx = tile * 256 - (HB + 1) + hr;
+        if constexpr (DENSE) {                            // halo row -> pixel tile*TM - HB - 1 + hr
+            const int gpx = tile * TM - (HB + 1) + hr;
             b = gpx >= 0 ? gpx / HW : -1;
             const int pix = gpx - b * HW;
             Y = pix / HB + 1; X = pix - (Y - 1) * HB + 1;
@@ -236,7 +244,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_v7(ConvBf16Args p) {
     // voffset = the lane's part (VGPR), soffset = the wave-uniform part (SGPR): keeps the per-tap
     // offsets out of vector registers
     auto issueA = [&](int j, int c, int buf) {            // piece j of chunk c's halo into A buffer `buf`
-        const int q = wave + 4 * j, rb = q % 5, g = q / 5;
+        const int q = wave + 4 * j, rb = q % NRB, g = q / NRB;
         int ln = lane;
         asm volatile("" : "+v"(ln));                      // recompute here, do not hoist
         const uint32_t vo = a_src(j, ln);
@@ -252,24 +260,24 @@ __global__ __launch_bounds__(256, 2) void conv3x3_v7(ConvBf16Args p) {
                                                      (int)lane16, so + b_src[j], 0, 0);
     };
 
-    f32x4v acc[8][4];
+    f32x4v acc[NI][4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {                         // the bias seeds the accumulators
         const float4 bv = *reinterpret_cast<const float4*>(p.bias + n0 + wn * 64 + j * 16 + 4 * (lane >> 4));
 #pragma unroll
-        for (int i = 0; i < 8; ++i) acc[i][j] = f32x4v{bv.x, bv.y, bv.z, bv.w};
+        for (int i = 0; i < NI; ++i) acc[i][j] = f32x4v{bv.x, bv.y, bv.z, bv.w};
     }
 
-    // fragment addresses: activations (MFMA column operand) at halo row wm*128 + 16i + l16 + tap
+    // fragment addresses: activations (MFMA column operand) at halo row wm*WR + 16i + l16 + tap
     // shift, group l >> 4; weights (row operand) at channel wn*64 + 16j + l16, group l >> 4
     const int l16 = lane & 15, lg = lane >> 4;
-    const uint32_t a_lane = lds_addr(abuf) + lg * (HROWS * 16) + (wm * 128 + l16) * 16;
+    const uint32_t a_lane = lds_addr(abuf) + lg * (HROWS * 16) + (wm * WR + l16) * 16;
     const uint32_t b_lane = lds_addr(bbuf) + lg * (BNT * 16) + (wn * 64 + l16) * 16;
-    uint32_t mbits = 0;                                   // DENSE: board-edge bits of the lane's 8 pixels
+    uint32_t mbits = 0;                                   // DENSE: board-edge bits of the lane's NI pixels
     if constexpr (DENSE) {
 #pragma unroll
-        for (int f = 0; f < 8; ++f) {
-            const int gq = tile * 256 + wm * 128 + f * 16 + l16;
+        for (int f = 0; f < NI; ++f) {
+            const int gq = tile * TM + wm * WR + f * 16 + l16;
             const int pix = gq % HW, y = pix / HB, x = pix - y * HB;
             mbits |= ((x == 0 ? 1u : 0u) | (x == HB - 1 ? 2u : 0u) | (y == 0 ? 4u : 0u) | (y == HB - 1 ? 8u : 0u)) << (4 * f);
         }
@@ -277,7 +285,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_v7(ConvBf16Args p) {
 
     // prologue: halo of chunk 0, weights of taps 0..3
 #pragma unroll
-    for (int j = 0; j < 5; ++j) issueA(j, 0, 0);
+    for (int j = 0; j < NRB; ++j) issueA(j, 0, 0);
 #pragma unroll
     for (int s = 0; s < 4; ++s) issueB(s, s);
     wait_vm(6);                                           // A(0), B(0) landed; B(1..3) may fly
@@ -289,7 +297,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_v7(ConvBf16Args p) {
             const uint32_t test = (dy == 0 ? 4u : dy == 2 ? 8u : 0u) | (dx == 0 ? 1u : dx == 2 ? 2u : 0u);
             if (test) {
 #pragma unroll
-                for (int i = 0; i < 4; ++i)
+                for (int i = 0; i < NA; ++i)
                     if (mbits & (test << (4 * (half * 4 + i)))) a[i] = frag{};
             }
         }
@@ -301,7 +309,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_v7(ConvBf16Args p) {
     auto loadA = [&](frag (&a)[4], uint32_t ab, auto tc, auto hc) {
         constexpr int t = decltype(tc)::value, half = decltype(hc)::value;
         constexpr int sh = (t / 3) * WG + (t % 3);
-        static_for<0, 4>([&](auto ic) {
+        static_for<0, NA>([&](auto ic) {
             constexpr int i = decltype(ic)::value;
             if constexpr (SLIM && half == 1 && i == 3) ds_rd<((half * 4 + i) * 16 + sh) * 16>(a[i], ab + z16);
             else ds_rd<((half * 4 + i) * 16 + sh) * 16>(a[i], ab);
@@ -315,7 +323,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_v7(ConvBf16Args p) {
     };
     auto mma = [&](const frag (&a)[4], const frag (&b)[4], int half) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
+        for (int i = 0; i < NA; ++i) {
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 if constexpr (MODE == 2)
@@ -330,7 +338,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_v7(ConvBf16Args p) {
     // tap 0 of chunk 0
     loadB(bw[0], b_lane);
     loadA(alo, a_lane, I0{}, I0{});
-    loadA(ahi, a_lane, I0{}, I1{});
+    if constexpr (HALVES == 2) loadA(ahi, a_lane, I0{}, I1{});
 
     // Two chunks per iteration: 18 taps, the weight registers alternate by tap parity.  Every tap
     // issues the same DMA pieces (a halo piece at taps 0..4, two weight pieces), past the end as
@@ -341,36 +349,39 @@ __global__ __launch_bounds__(256, 2) void conv3x3_v7(ConvBf16Args p) {
         static_for<0, 18>([&](auto tc18) {
             constexpr int T = decltype(tc18)::value;      // tap of the chunk pair
             constexpr int t = T % 9, cur = T & 1, nxt = cur ^ 1;
-            constexpr int allow = (t >= 2 && t - 2 < 5 ? 1 : 0) + (t >= 1 && t - 1 < 5 ? 1 : 0) + 4;
+            constexpr int allow = (t >= 2 && t - 2 < NRB ? 1 : 0) + (t >= 1 && t - 1 < NRB ? 1 : 0) + 4;
+            constexpr int NAF = NA * HALVES;              // activation fragment reads per tap
             const int c = c2 + T / 9;
             const int s = 9 * c + t;
             if constexpr (DENSE) asm volatile("" : "+v"(mbits));   // keep the edge masks inside the loop (no SGPR hoisting)
-            // the 8 youngest LDS reads are this tap's activation fragments: the weights of tap s
+            // the NAF youngest LDS reads are this tap's activation fragments: the weights of tap s
             // (read one tap ago) are in registers -- required before the barrier frees their slot
-            lgkm<8>(bw[cur]);
+            lgkm<NAF>(bw[cur]);
             wait_vm(allow);                               // weights of tap s+1 (and at t == 8 the next halo) landed
             __builtin_amdgcn_s_barrier();
             __builtin_amdgcn_sched_barrier(0);
-            // DMA for later taps: a halo piece of chunk c+1 at taps 0..4 (the last chunk reloads
+            // DMA for later taps: a halo piece of chunk c+1 at taps 0..NRB-1 (the last chunk reloads
             // itself into the free buffer), then the weights of tap s+4 (clamped to the last tap)
-            if constexpr (t < 5) issueA(t, c + 1 < NCH ? c + 1 : c, (c + 1) & 1);
+            if constexpr (t < NRB) issueA(t, c + 1 < NCH ? c + 1 : c, (c + 1) & 1);
             issueB(s + 4 < NS ? s + 4 : NS - 1, (s + 4) & 3);
             // weights of tap s+1 (certified by the barrier above)
             loadB(bw[nxt], b_lane + ((s + 1) & 3) * B_TAP);
             __builtin_amdgcn_sched_barrier(0);
-            lgkm<8>(alo);                                 // activations of tap s, low half
+            lgkm<(HALVES - 1) * NA + 4>(alo);             // activations of tap s, low half
             maskA(alo, 0, t / 3, t % 3);
             mma(alo, bw[cur], 0);
             __builtin_amdgcn_sched_barrier(0);
             const uint32_t an = a_lane + ((t == 8 ? c + 1 : c) & 1) * A_BUF;
             constexpr int tn = (t + 1) % 9;
             loadA(alo, an, std::integral_constant<int, tn>{}, I0{});
-            lgkm<8>(ahi);                                 // activations of tap s, high half
-            maskA(ahi, 1, t / 3, t % 3);
-            __builtin_amdgcn_sched_barrier(0);
-            mma(ahi, bw[cur], 1);
-            __builtin_amdgcn_sched_barrier(0);
-            loadA(ahi, an, std::integral_constant<int, tn>{}, I1{});
+            if constexpr (HALVES == 2) {
+                lgkm<8>(ahi);                             // activations of tap s, high half
+                maskA(ahi, 1, t / 3, t % 3);
+                __builtin_amdgcn_sched_barrier(0);
+                mma(ahi, bw[cur], 1);
+                __builtin_amdgcn_sched_barrier(0);
+                loadA(ahi, an, std::integral_constant<int, tn>{}, I1{});
+            }
             __builtin_amdgcn_sched_barrier(0);
         });
     }
@@ -383,12 +394,12 @@ __global__ __launch_bounds__(256, 2) void conv3x3_v7(ConvBf16Args p) {
     const int chl = n0 + wn * 64 + 4 * lg;                // first channel of the lane in tile j = 0
     float vmax = 0.0f;                                    // fp16: the largest output (the range guard)
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        const int q = wm * 128 + i * 16 + l16;            // output grid row of the tile
+    for (int i = 0; i < NI; ++i) {
+        const int q = wm * WR + i * 16 + l16;             // output grid row of the tile
         int b, pix;
         bool live;
         if constexpr (DENSE) {
-            const int gq = tile * 256 + q;
+            const int gq = tile * TM + q;
             b = gq / HW;
             pix = gq - b * HW;
             live = b < nboards;
@@ -1164,13 +1175,38 @@ extern "C" int az_diag_v9_stamps(int sel, unsigned long long* st, unsigned* hw, 
 #endif
 }
 
-template <int HB, int GEO>
+template <int HB, int GEO, int TM = 256>
 static void v7_launch_g(const ConvBf16Args& a, int mode, hipStream_t st) {
     const int boards = a.M / (HB * HB);
-    const int tiles = GEO == GEO_DENSE ? (boards * HB * HB + 255) / 256 : boards;
+    const int tiles = GEO == GEO_DENSE ? (boards * HB * HB + TM - 1) / TM : boards;
     const int grid = (tiles + 7) / 8 * 8 * (a.N / 128);   // XCD-aware tile/half mapping: whole groups of 8
-    if (mode == 2) hipLaunchKernelGGL((conv3x3_v7<2, HB, GEO>), dim3(grid), dim3(256), 0, st, a);
-    else hipLaunchKernelGGL((conv3x3_v7<1, HB, GEO>), dim3(grid), dim3(256), 0, st, a);
+    if (mode == 2) hipLaunchKernelGGL((conv3x3_v7<2, HB, GEO, TM>), dim3(grid), dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((conv3x3_v7<1, HB, GEO, TM>), dim3(grid), dim3(256), 0, st, a);
+}
+// DENSE boards: the tile rows (256 / 128 / 64) for this launch -- small batches take smaller tiles
+// so one round of blocks covers the CUs (az_conv_v7_tm; flag bits 0x30000 force 256 / 128 / 64)
+int az_conv_v7_tm(const ConvBf16Args& a);
+template <int HB>
+static void v7_launch_dense(const ConvBf16Args& a, int mode, hipStream_t st) {
+    switch (az_conv_v7_tm(a)) {
+        case 64: v7_launch_g<HB, GEO_DENSE, 64>(a, mode, st); break;
+        case 128: v7_launch_g<HB, GEO_DENSE, 128>(a, mode, st); break;
+        default: v7_launch_g<HB, GEO_DENSE, 256>(a, mode, st); break;
+    }
+}
+
+// The DENSE tile rows of a conv3x3_v7 launch: 256 unless the launch is under two rounds of blocks
+// (two blocks per CU), where 128 / 64-row tiles spread the work over more CUs.  Conv flag bits
+// 0x30000 force 256 (1) / 128 (2) / 64 (3) for A/B measurement.
+int az_conv_v7_tm(const ConvBf16Args& a) {
+    const int force = (a.flags >> 16) & 3;
+    if (force) return force == 1 ? 256 : force == 2 ? 128 : 64;
+    const long rows = (long)a.M;
+    const int halves = a.N / 128;
+    auto blocks = [&](int tm) { return ((rows + tm - 1) / tm + 7) / 8 * 8 * halves; };
+    if (blocks(256) >= 1024) return 256;
+    if (blocks(128) >= 512) return 128;
+    return 64;
 }
 
 // true when conv3x3_v7 takes this layer
@@ -1272,12 +1308,12 @@ int az_conv_v7x3_launch(const ConvBf16Args& a, hipStream_t st) {
 int az_conv_v7_launch(const ConvBf16Args& a, int mode, int geo15, hipStream_t st) {
     if (!az_conv_v7_supported(a)) return -1;
     switch (a.H) {
-        case 8: v7_launch_g<8, GEO_DENSE>(a, mode, st); return 0;
-        case 9: v7_launch_g<9, GEO_DENSE>(a, mode, st); return 0;
-        case 13: v7_launch_g<13, GEO_DENSE>(a, mode, st); return 0;
-        case 19: v7_launch_g<19, GEO_DENSE>(a, mode, st); return 0;
+        case 8: v7_launch_dense<8>(a, mode, st); return 0;
+        case 9: v7_launch_dense<9>(a, mode, st); return 0;
+        case 13: v7_launch_dense<13>(a, mode, st); return 0;
+        case 19: v7_launch_dense<19>(a, mode, st); return 0;
         default:
-            if (geo15 == GEO_DENSE) v7_launch_g<15, GEO_DENSE>(a, mode, st);
+            if (geo15 == GEO_DENSE) v7_launch_dense<15>(a, mode, st);
             else if (geo15 == GEO_PAD) v7_launch_g<15, GEO_PAD>(a, mode, st);
             else v7_launch_g<15, GEO_SLIM>(a, mode, st);
             return 0;

@@ -339,8 +339,13 @@ def _same_kernel(profiled, name):
             return None
         args = [x.strip() for x in m.group(2).split(",")]
         # the split-operand kernels (v7x3 / v9x3: <board, geometry[, variant], piece type> in rocprof,
-        # <board, SLIM|DENSE[, f16]> as labelled): the board; the piece type is the precision's
-        return (m.group(1), args[:1] if m.group(1).endswith("x3") else args[:-1])
+        # <board, SLIM|DENSE[, f16]> as labelled): the board; the piece type is the precision's.
+        # conv3x3_v7: <mode, board, geometry[, tile rows]>: all but the geometry
+        if m.group(1).endswith("x3"):
+            return (m.group(1), args[:1])
+        if m.group(1) == "conv3x3_v7":
+            return (m.group(1), args[:2] + args[3:])
+        return (m.group(1), args[:-1])
     p1, p2 = parts(profiled), parts(name)
     return bool(p1 and p2 and p1 == p2)
 

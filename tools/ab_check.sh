@@ -1,3 +1,4 @@
+#!/bin/bash
 # Parity of the trunk paths + same-process A/B of conv flag sets on the C3 / C4 / C5 nets.
 set -o pipefail
 export TMPDIR=/tmp

@@ -1,3 +1,4 @@
+#!/bin/bash
 # Round-2 API additions on the GPU: reference API scripts, callback evaluator, host API, search regression.
 set -o pipefail
 export TMPDIR=/tmp

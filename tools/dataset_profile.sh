@@ -1,3 +1,4 @@
+#!/bin/bash
 # Row f3 measurement: tools/dataset_bench.py (k_dataset_extract, 2048 x 60-ply 15x15 records,
 # 8-fold augmentation, shuffled slots), the same under rocprofv3 kernel trace, and the HBM PMC
 # passes (FETCH_SIZE, WRITE_SIZE in separate runs).  Output: gpurun_out/ds/

@@ -1,3 +1,4 @@
+#!/bin/bash
 # DENSE v6 geometry (conv flag 8) vs the padded geometry: A/B timing per board, and the conv1 split skip.
 set -o pipefail
 export TMPDIR=/tmp

@@ -1,3 +1,4 @@
+#!/bin/bash
 # Round GPU check: dataset tests, the full GPU suite, smoke, default bench line.
 set -o pipefail
 export TMPDIR=/tmp

@@ -1,3 +1,4 @@
+#!/bin/bash
 # Full GPU suite (no -x) + smoke + bench.
 set -o pipefail
 export TMPDIR=/tmp

@@ -1,3 +1,4 @@
+#!/bin/bash
 # The whole GPU suite (stops at the first failure), then smoke().
 set -o pipefail
 export TMPDIR=/tmp

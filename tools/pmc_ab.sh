@@ -1,3 +1,4 @@
+#!/bin/bash
 # SQ/GRBM PMC pass over the C3 trunk (tools/net_bench.py) for each conv flag set in FLAGS (decimal,
 # AZ_CONV_FLAGS), plus a kernel-trace stats pass each.  Output: gpurun_out/pmcab_<flags>/
 set -e

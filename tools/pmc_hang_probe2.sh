@@ -1,3 +1,4 @@
+#!/bin/bash
 # rocprofv3 --pmc progress of searches (tools/pmc_progress.py): CFGS entries are
 # games:capacity-sims:run-sims:mode:profile; each pass is killed at 120 s; the first failure ends
 # the run.  Round 3: --mode sims at 256 games finished at 400 and 800 sims (1-2 s); bench.py itself

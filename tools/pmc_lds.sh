@@ -1,3 +1,4 @@
+#!/bin/bash
 # One SQ counter pass on the C3 trunk: LDS bank conflicts / activity, waits, MFMA busy.
 set -o pipefail
 export TMPDIR=/tmp

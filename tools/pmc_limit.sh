@@ -1,3 +1,4 @@
+#!/bin/bash
 # Does rocprofv3 --pmc stop on the dispatch count?  The 800-sim C3 move hung under --pmc (round 2,
 # twice) while 100- and 400-sim moves finished.  Here the C3 net's forward (≈46 dispatches at
 # batch 16) runs 100 / 170 / 260 times under one SQ counter, each pass killed at 150 s: if the

@@ -1,3 +1,4 @@
+#!/bin/bash
 # SQ counters of k_smallnet (C2 net, 256 boards): MFMA busy, LDS activity / bank conflicts / waits.
 set -o pipefail
 export TMPDIR=/tmp

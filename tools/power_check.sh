@@ -1,3 +1,4 @@
+#!/bin/bash
 # Board power and clocks while the C3 trunk runs (tools/net_bench.py, B = 2048, v7) and while idle:
 # is the trunk conv power-limited?  Read-only rocm-smi / amd-smi queries (no setting is changed).
 set -o pipefail

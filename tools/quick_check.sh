@@ -1,3 +1,4 @@
+#!/bin/bash
 # Net parity + trunk timing per board + the default C3 bench line.
 set -o pipefail
 export TMPDIR=/tmp

@@ -1,3 +1,4 @@
+#!/bin/bash
 # Net parity + per-kernel times of the C3 forward (B = 2048) under rocprofv3 kernel trace.
 set -o pipefail
 export TMPDIR=/tmp

@@ -1,3 +1,4 @@
+#!/bin/bash
 # The whole GPU suite, smoke(), then the C2 and C3 bench lines (no profiler).
 set -o pipefail
 export TMPDIR=/tmp

@@ -1,3 +1,4 @@
+#!/bin/bash
 # k_smallnet: net parity (incl. the C2 replay and trained-scale C2), the 4- vs 8-wave block timing
 # (phase stamps of block 0), then the C2 bench line.
 set -o pipefail

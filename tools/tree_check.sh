@@ -1,3 +1,4 @@
+#!/bin/bash
 # Tree-kernel parity (every search / Go / host-API / callback / self-play replay test), then the C2
 # bench line and a C2 kernel trace under rocprofv3 (per-kernel averages + the inter-kernel gaps).
 set -o pipefail

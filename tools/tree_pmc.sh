@@ -1,3 +1,4 @@
+#!/bin/bash
 # rocprofv3 HBM traffic of the tree kernels (k_select, k_expand_backup, the fused k_expand_select,
 # k_scan) and the record -> g8 input kernel (k_rec_to_g8) over one full C3 move (2048 games, 800
 # sims, BLOCKS residual blocks, default 20 = the bench config): a kernel-trace pass (bench.py's own

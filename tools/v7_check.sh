@@ -1,3 +1,4 @@
+#!/bin/bash
 # conv3x3_v7: bitwise against v6, net parity, trunk timing v7 vs v6 (15x15, C3 net) at the per-GPU
 # batches of 1/2/4/8 GPUs.
 set -o pipefail

@@ -1,3 +1,4 @@
+#!/bin/bash
 # conv3x3_v7x3 (AZ_PREC_BF16X3 on the g8 hi / lo planes): net parity on every geometry + trained
 # scale, then trunk timing at the C3 batch (and the fp16 trunk on the same box for reference).
 set -o pipefail
