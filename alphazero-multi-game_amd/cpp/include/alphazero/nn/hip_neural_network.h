@@ -36,8 +36,9 @@ class HipNeuralNetwork : public NeuralNetwork {
     // The reference's own model file: a TorchScript archive of its plain ResNet (SimplifiedModel /
     // the exporter fallback; torch_neural_network.cpp:90 loads it with torch::jit::load), read
     // without executing it (alphazero/nn/torchscript_reader.h).  precision: AZ_PREC_* of the trunk
-    // (-1: AZ_PREC_BF16X3 where the trunk has 16-bit kernels -- fp32-faithful, the reference's
-    // default fp32 inference -- else AZ_PREC_F32); boardSize <= 0: from the policy size.
+    // (-1: fp32-faithful, the reference's default fp32 inference -- AZ_PREC_F16X3 where its kernels
+    // exist, else AZ_PREC_BF16X3 where the trunk has 16-bit kernels, else AZ_PREC_F32);
+    // boardSize <= 0: from the policy size.
     static std::unique_ptr<HipNeuralNetwork> loadTorchScript(const std::string& path, core::GameType type,
                                                              int boardSize = 0, int precision = -1,
                                                              int maxBatch = 2048, int device = -1);

@@ -102,7 +102,18 @@ std::unique_ptr<HipNeuralNetwork> HipNeuralNetwork::loadTorchScript(const std::s
     s.maxBatch = maxBatch;
     s.precision = precision;
     std::vector<float> blob = torchScriptResNet(path, type, boardSize, s);
-    if (precision < 0) s.precision = s.channels % 32 == 0 ? AZ_PREC_BF16X3 : AZ_PREC_F32;
+    if (precision < 0) {
+        // the fp32-faithful trunk: fp16 pieces where their kernels exist (include/az_engine.h
+        // AZ_PREC_F16X3: conv3x3_v9x3 / v7x3 boards with channels % 128 == 0, the 15x15 64-channel
+        // fused net), else bf16 pieces (channels % 32 == 0), else fp32
+        const int b = s.boardSize;
+        const bool trunk = (b == 8 || b == 9 || b == 13 || b == 15 || b == 19) && s.channels % 128 == 0;
+        const bool small = b == 15 && s.channels == 64 && s.inPlanes <= 16 && s.blocks <= 15 && s.pool <= 8 &&
+                           2 * s.headChannels == 64;
+        s.precision = (trunk || small) && s.blocks > 0 ? AZ_PREC_F16X3
+                      : s.channels % 32 == 0            ? AZ_PREC_BF16X3
+                                                        : AZ_PREC_F32;
+    }
     auto net = std::make_unique<HipNeuralNetwork>(s, device);
     net->loadWeights(blob);
     return net;
@@ -185,11 +196,11 @@ std::string HipNeuralNetwork::getDeviceInfo() const {
 }
 
 std::string HipNeuralNetwork::getModelInfo() const {
-    static const char* prec[] = {"fp32", "bf16x3", "bf16", "fp16"};
+    static const char* prec[] = {"fp32", "bf16x3", "bf16", "fp16", "f16x3"};
     std::ostringstream o;
     o << "ResNet " << shape_.blocks << " blocks x " << shape_.channels << " filters, " << shape_.boardSize << "x"
       << shape_.boardSize << ", " << shape_.inPlanes << " input planes, policy " << shape_.actionSize << ", trunk "
-      << prec[shape_.precision & 3];
+      << (shape_.precision >= 0 && shape_.precision <= 4 ? prec[shape_.precision] : "?");
     return o.str();
 }
 

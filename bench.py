@@ -290,13 +290,14 @@ def run_rank(a, rank, world, dist, make_workload, coll_device):
                "GB_per_s": tree[f"{k}_bytes"] / max(1e-12, 1e-3 * tree[f"{k}_ms"]) / 1e9,
                "frac_of_hbm_peak": tree[f"{k}_bytes"] / max(1e-12, 1e-3 * tree[f"{k}_ms"]) / 8.0e12}
         for name, k in (("k_select", "select"), ("k_expand_backup", "expand"))}
-    out["tree_kernels"]["note"] = ("rank-0 HIP events around each kernel of one simulation step in 16 (those "
+    out["tree_kernels"]["note"] = ("rank-0 device clock stamps around each kernel of one simulation step in 16 (those "
                                    "steps run k_select and k_expand_backup as separate launches; the others "
                                    "fuse step i's expansion with step i+1's selection, k_expand_select); algorithmic "
                                    "bytes counted by the kernels (child records scanned, path VL/backup "
                                    "read-modify-writes, new nodes, leaf planes); latency-bound (one wave per game, "
                                    "dependent tree levels), peak 8 TB/s; rocprofv3 PMC traffic of the same kernels: "
-                                   "profiles/r02h_tree_pmc.json (tools/tree_pmc.sh: C3 games at 400 sims; 800-sim moves hang rocprofv3 --pmc)")
+                                   "profiles/r03h_tree_pmc_c2.json (tools/tree_pmc.sh at the C2 bench config; at the C3 "
+                                   "config rocprofv3 --pmc does not finish a move, DESIGN.md section 7)")
     tr = pmc_traffic(a, kernel, boards_per_launch if launches else 0)
     if tr:
         out["roofline"].update(tr)

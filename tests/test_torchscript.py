@@ -210,7 +210,7 @@ def test_export_azw_accepts_torchscript(tmp_path):
 @pytest.mark.gpu
 @pytest.mark.parametrize("case", LAYOUTS, ids=["simplified8", "fallback15"])
 def test_create_network_from_torchscript(tmp_path, case):
-    """createNeuralNetwork(<the reference's .pt>) -> HipNeuralNetwork (bf16x3 trunk where it has one):
+    """createNeuralNetwork(<the reference's .pt>) -> HipNeuralNetwork (a split-precision trunk where it has one):
     predictBatch on GomokuStates == softmax / value of the traced module within 1e-4."""
     import az_amd
     import net_oracle
