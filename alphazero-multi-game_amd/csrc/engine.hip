@@ -1154,6 +1154,19 @@ int search_step(az_search* s, int mode, bool pre = false, bool fuse_next = false
     return 0;
 }
 
+// diagnostic phase trace of az_selfplay_step on stderr (az_diag_set_step_trace; tools/pmc_progress.py):
+// names the host call a step is blocked in when a profiler stalls it
+static int g_step_trace = 0;
+extern "C" int az_diag_set_step_trace(int on) { g_step_trace = on; return 0; }
+// diagnostic: a host synchronisation after every n simulation steps (0: none, the product default) --
+// bounds the dispatches queued on the engine stream (rocprofv3 --pmc probe)
+static int g_sync_every = 0;
+extern "C" int az_diag_set_sync_every(int n) { g_sync_every = n; return 0; }
+#define STEP_TRACE(...)                                                   \
+    do {                                                                  \
+        if (g_step_trace) { fprintf(stderr, "[step] " __VA_ARGS__); fputc('\n', stderr); fflush(stderr); } \
+    } while (0)
+
 // n simulation steps.  Step i's expansion and step i+1's selection share one launch
 // (k_expand_select) except around the profiled steps (their kernels are timed separately) and
 // with the host evaluator (which runs between the two).
@@ -1166,6 +1179,8 @@ int search_sims(az_search* s, int n) {
         const bool fuse = can_fuse && i + 1 < n && !sampled && !next_sampled;
         if (int r = search_step(s, MODE_SIM, pre, fuse)) return r;
         pre = fuse;
+        if ((i + 1) % 100 == 0) STEP_TRACE("%d sims issued", i + 1);
+        if (g_sync_every > 0 && (i + 1) % g_sync_every == 0) HIPCHK(hipStreamSynchronize(s->e->stream));
     }
     return 0;
 }
@@ -1237,11 +1252,16 @@ int search_noise(az_search* s, float alpha, float eps, const uint8_t* mask) {
 }
 
 int search_run(az_search* s) {
+    STEP_TRACE("search_run: root step");
     if (int r = search_step(s, MODE_ROOT_SEARCH)) return r;
     if (s->c.use_dirichlet_each_search)
         if (int r = search_noise(s, s->c.dirichlet_alpha, s->c.dirichlet_eps, nullptr)) return r;
+    STEP_TRACE("search_run: sims");
     if (int r = search_sims(s, s->c.num_simulations)) return r;
-    return check_err(s);
+    STEP_TRACE("search_run: check_err");
+    const int r = check_err(s);
+    STEP_TRACE("search_run: done");
+    return r;
 }
 
 // (Re)start the listed slots with fresh games.  seed_ids (optional) give each game its own
@@ -2339,9 +2359,11 @@ int az_selfplay_step(az_search* s, const az_selfplay_cfg* cfg, int64_t* moves_do
     const int NA = s->t.NA;
     s->sp_probs.resize((size_t)G * NA); s->sp_cact.resize((size_t)G * NA);
     s->sp_values.resize(G); s->sp_nch.resize(G);
+    STEP_TRACE("select");
     if (int r = search_select(s, 1, temps.data(), 0.0f, actions.data(), s->sp_values.data(), s->sp_probs.data(),
                               s->sp_cact.data(), s->sp_nch.data()))
         return r;
+    STEP_TRACE("apply");
     const int64_t ms = std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::steady_clock::now() - t0).count();
     std::vector<int> term(G), res(G);
     if (int r = search_apply_dev(s, term.data(), res.data())) return r;
@@ -2357,7 +2379,9 @@ int az_selfplay_step(az_search* s, const az_selfplay_cfg* cfg, int64_t* moves_do
                                           s->sp_cact.data() + (size_t)g * NA, ms});
         s->sp_slots.push_back(g);
     }
+    STEP_TRACE("noise");
     if (int r = search_noise(s, s->c.dirichlet_alpha, s->c.dirichlet_eps, noise_mask.data())) return r;
+    STEP_TRACE("restart / counters");
     if (cfg->restart_finished) {
         std::vector<int> fin;
         for (int g = 0; g < G; ++g) if (!s->active[g]) fin.push_back(g);

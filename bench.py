@@ -106,6 +106,10 @@ def parse(argv=None):
                     help="device clock stamps (s_memrealtime, 100 MHz) around sampled trunk / tree launches (the "
                          "roofline); 0 disables (round 3's HIP-event timing hung under rocprofv3 --pmc; the "
                          "stamps do not)")
+    ap.add_argument("--sync-every", type=int, default=0,
+                    help="diagnostic: a host synchronisation after every N simulation steps (0: none). "
+                         "rocprofv3 --pmc stalls on a selfplay step's unsynchronised queue of dispatches "
+                         "(DESIGN.md section 7); tools/tree_pmc.sh passes 100")
     ap.add_argument("--dist-timeout", type=float, default=600.0,
                     help="seconds a rank waits in a collective / barrier before the bench fails (N>1)")
     a = ap.parse_args(argv)
@@ -203,6 +207,9 @@ def run_rank(a, rank, world, dist, make_workload, coll_device):
     sh = azdist.shard_range(rank, world, a.global_games if a.scaling == "strong" else a.global_games * world)
     if sh["games"] < 1:
         raise SystemExit(f"bench.py: rank {rank} got no games ({a.global_games} over {world} ranks)")
+    if getattr(a, "sync_every", 0):
+        from az_amd import _lib
+        _lib.lib().az_diag_set_sync_every(int(a.sync_every))
     wl = make_workload(a, int(os.environ.get("LOCAL_RANK", "0")), sh)
     net = wl.net
     if rank == 0:
@@ -296,8 +303,8 @@ def run_rank(a, rank, world, dist, make_workload, coll_device):
                                    "bytes counted by the kernels (child records scanned, path VL/backup "
                                    "read-modify-writes, new nodes, leaf planes); latency-bound (one wave per game, "
                                    "dependent tree levels), peak 8 TB/s; rocprofv3 PMC traffic of the same kernels: "
-                                   "profiles/r03h_tree_pmc_c2.json (tools/tree_pmc.sh at the C2 bench config; at the C3 "
-                                   "config rocprofv3 --pmc does not finish a move, DESIGN.md section 7)")
+                                   "profiles/r04_tree_pmc_c3.json (tools/tree_pmc.sh: C3's 2048 games x 800 sims, "
+                                   "2-block trunk, --sync-every 100; C2 config: profiles/r03h_tree_pmc_c2.json)")
     tr = pmc_traffic(a, kernel, boards_per_launch if launches else 0)
     if tr:
         out["roofline"].update(tr)

@@ -34,6 +34,12 @@ def say(msg):
     print(f"{time.perf_counter() - t0:8.2f} s  {msg}", flush=True)
 
 
+if os.environ.get("AZ_STEP_TRACE"):          # phase lines of az_selfplay_step on stderr (diag entry point)
+    from az_amd import _lib
+    _lib.lib().az_diag_set_step_trace(1)
+if os.environ.get("AZ_SYNC_EVERY"):          # host sync every n simulation steps (diag entry point)
+    from az_amd import _lib
+    _lib.lib().az_diag_set_sync_every(int(os.environ["AZ_SYNC_EVERY"]))
 eng = az_amd.Engine(0)
 net = az_amd.HipNeuralNetwork(eng, az_amd.gomoku_net_desc(board_size=15, channels=256, blocks=a.blocks,
                                                           precision=az_amd.AZ_PREC_FP16, max_batch=a.games))

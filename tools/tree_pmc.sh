@@ -16,10 +16,13 @@ mkdir -p $O
 # kernel at its own bench config); default c3 with BLOCKS (20: the PMC passes of a full 20-block move
 # crash the profiler's host thread, SIGSEGV, profiles/r03g_tree_pmc_c3_20b_crash.txt -- BLOCKS=2
 # keeps the tree kernels' config, 2048 games x 800 sims, with a shorter trunk)
+# SYNC (default 100): a host sync every SYNC simulation steps -- round 4 found that rocprofv3 --pmc
+# stalls a selfplay step whose thousands of dispatches are queued without a host synchronisation
+# (tools/r4_probe5.sh: sync every 50 / 200 passes in 2 s, none is killed at 120 s)
 if [ "${CONFIG:-c3}" = c2 ]; then
-  CMD="python3 bench.py --config c2 --cpu-baseline 0 --parity-steps 0 --steps 1 --warmup 0"
+  CMD="python3 bench.py --config c2 --cpu-baseline 0 --parity-steps 0 --steps 1 --warmup 0 --sync-every ${SYNC:-100}"
 else
-  CMD="python3 bench.py --cpu-baseline 0 --parity-steps 0 --steps 1 --warmup 0 --sims ${SIMS:-800} --blocks ${BLOCKS:-20}"
+  CMD="python3 bench.py --cpu-baseline 0 --parity-steps 0 --steps 1 --warmup 0 --sims ${SIMS:-800} --blocks ${BLOCKS:-20} --sync-every ${SYNC:-100}"
 fi
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o run -- $CMD > $O/trace.log 2>&1 || { echo FAIL trace; tail -3 $O/trace.log; exit 1; }
 ( while sleep 30; do echo "pmc pass running ($(date +%T))"; done ) &
