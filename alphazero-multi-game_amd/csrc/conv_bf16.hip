@@ -1689,11 +1689,10 @@ static int g8_choice(const ConvBf16Args& a, int* geo) {
     }
     // Small batches on the DENSE boards (the per-rank shards of the 8-GPU C4 / C5 configs): v6's
     // 512-row tiles leave most CUs idle (C5 net, 128 boards: 32 blocks), conv3x3_v7 with 128 / 64-row
-    // tiles (az_conv_v7_tm) fills them -- 128 boards of 8x8: 0.0237 vs 0.0644 ms per launch; 19x19:
-    // faster from 256 boards (0.134 vs 0.140 ms), not at 128 (0.076 vs 0.073;
-    // profiles/r04_small_batch_tiles.txt).  Flag 0x1000 keeps v6 (A/B).
-    if (!(a.flags & (0x100 | 0x1000)) && a.H != 15 && boards_g8 < 1024 && (a.H < 19 || boards_g8 >= 256) &&
-        az_conv_v7_supported(a)) {
+    // tiles (az_conv_v7_tm) fills them -- 128 boards of 8x8: 0.0237 vs 0.0644 ms per launch; 19x19 on
+    // 192-row tiles: 0.0700 vs 0.0747 at 128 boards, 0.1284 vs 0.1375 at 256
+    // (profiles/r04_small_batch_tiles_192.txt).  Flag 0x1000 keeps v6 (A/B).
+    if (!(a.flags & (0x100 | 0x1000)) && a.H != 15 && boards_g8 < 1024 && az_conv_v7_supported(a)) {
         *geo = 2;
         return 1;
     }

@@ -166,7 +166,7 @@ struct Geom7 {
     static constexpr int HROWS = (DENSE && TM < 256) ? (TROWS + 63) / 64 * 64 : 320;
     static constexpr int NRB = HROWS / 64;
     static_assert(TROWS <= HROWS, "halo does not fit");
-    static_assert(DENSE ? (TM == 256 || TM == 128 || TM == 64) : (TM == 256 && GRID <= 256 && NFRAG > 8),
+    static_assert(DENSE ? (TM == 256 || TM == 192 || TM == 128 || TM == 64) : (TM == 256 && GRID <= 256 && NFRAG > 8),
                   "tile geometry");
 };
 
@@ -174,8 +174,8 @@ struct Geom7 {
 
 // MODE 2: fp16 operands, MODE 1: bf16.  Requires C % 64 == 0 (an even number of 32-channel
 // chunks), N % 128 == 0, a ReLU (every g8 conv has one), no fp32 output.
-// TM < 256 (DENSE, small batches): each wave owns TM / 2 rows = NI fragments (4 or 2) x 64
-// channels, one A register set (no second row half); the halo is NRB pieces per group.
+// TM < 256 (DENSE, small batches): each wave owns TM / 2 rows = NI fragments (6, 4 or 2) x 64
+// channels in one or two A register sets of NA fragments; the halo is NRB pieces per group.
 template <int MODE, int HB, int GEO, int TM = 256>
 __global__ __launch_bounds__(256, 2) void conv3x3_v7(ConvBf16Args p) {
     typedef H16<MODE> H;
@@ -183,7 +183,8 @@ __global__ __launch_bounds__(256, 2) void conv3x3_v7(ConvBf16Args p) {
     constexpr bool DENSE = GM::DENSE, SLIM = GM::SLIM;
     typedef typename std::conditional<MODE == 2, f16x8, bf16x8>::type frag;
     constexpr int BNT = 128, WG = GM::WG, HW = GM::HW, HROWS = GM::HROWS, NRB = GM::NRB;
-    constexpr int NI = TM / 32, NA = NI < 4 ? NI : 4, HALVES = NI / NA;   // fragments per wave / per A set
+    constexpr int NI = TM / 32, NA = NI <= 4 ? NI : NI / 2, HALVES = NI / NA;   // fragments per wave / per A set
+    static_assert(NA * HALVES == NI && NA <= 4, "fragment split");
     constexpr int WR = TM / 2;                            // rows per wave
     constexpr int A_BUF = 4 * HROWS * 16;                 // one chunk: [4 groups][320 rows][16 B] = 20 KB
     constexpr int B_TAP = 4 * BNT * 16;                   // one tap: [4 groups][128 ch][16 B] = 8 KB
@@ -298,7 +299,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_v7(ConvBf16Args p) {
             if (test) {
 #pragma unroll
                 for (int i = 0; i < NA; ++i)
-                    if (mbits & (test << (4 * (half * 4 + i)))) a[i] = frag{};
+                    if (mbits & (test << (4 * (half * NA + i)))) a[i] = frag{};
             }
         }
     };
@@ -311,8 +312,8 @@ __global__ __launch_bounds__(256, 2) void conv3x3_v7(ConvBf16Args p) {
         constexpr int sh = (t / 3) * WG + (t % 3);
         static_for<0, NA>([&](auto ic) {
             constexpr int i = decltype(ic)::value;
-            if constexpr (SLIM && half == 1 && i == 3) ds_rd<((half * 4 + i) * 16 + sh) * 16>(a[i], ab + z16);
-            else ds_rd<((half * 4 + i) * 16 + sh) * 16>(a[i], ab);
+            if constexpr (SLIM && half == 1 && i == 3) ds_rd<((half * NA + i) * 16 + sh) * 16>(a[i], ab + z16);
+            else ds_rd<((half * NA + i) * 16 + sh) * 16>(a[i], ab);
         });
     };
     auto loadB = [&](frag (&b)[4], uint32_t bs) {
@@ -327,9 +328,9 @@ __global__ __launch_bounds__(256, 2) void conv3x3_v7(ConvBf16Args p) {
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 if constexpr (MODE == 2)
-                    acc[half * 4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(b[j], a[i], acc[half * 4 + i][j], 0, 0, 0);
+                    acc[half * NA + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(b[j], a[i], acc[half * NA + i][j], 0, 0, 0);
                 else
-                    acc[half * 4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a[i], acc[half * 4 + i][j], 0, 0, 0);
+                    acc[half * NA + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a[i], acc[half * NA + i][j], 0, 0, 0);
             }
         }
     };
@@ -375,7 +376,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_v7(ConvBf16Args p) {
             constexpr int tn = (t + 1) % 9;
             loadA(alo, an, std::integral_constant<int, tn>{}, I0{});
             if constexpr (HALVES == 2) {
-                lgkm<8>(ahi);                             // activations of tap s, high half
+                lgkm<4 + NA>(ahi);                        // activations of tap s, high half
                 maskA(ahi, 1, t / 3, t % 3);
                 __builtin_amdgcn_sched_barrier(0);
                 mma(ahi, bw[cur], 1);
@@ -1184,27 +1185,31 @@ static void v7_launch_g(const ConvBf16Args& a, int mode, hipStream_t st) {
     else hipLaunchKernelGGL((conv3x3_v7<1, HB, GEO, TM>), dim3(grid), dim3(256), 0, st, a);
 }
 // DENSE boards: the tile rows (256 / 128 / 64) for this launch -- small batches take smaller tiles
-// so one round of blocks covers the CUs (az_conv_v7_tm; flag bits 0x30000 force 256 / 128 / 64)
+// so one round of blocks covers the CUs (az_conv_v7_tm; flag bits 0x70000 force 256 / 128 / 64 / 192)
 int az_conv_v7_tm(const ConvBf16Args& a);
 template <int HB>
 static void v7_launch_dense(const ConvBf16Args& a, int mode, hipStream_t st) {
     switch (az_conv_v7_tm(a)) {
         case 64: v7_launch_g<HB, GEO_DENSE, 64>(a, mode, st); break;
         case 128: v7_launch_g<HB, GEO_DENSE, 128>(a, mode, st); break;
+        case 192: v7_launch_g<HB, GEO_DENSE, 192>(a, mode, st); break;
         default: v7_launch_g<HB, GEO_DENSE, 256>(a, mode, st); break;
     }
 }
 
 // The DENSE tile rows of a conv3x3_v7 launch: 256 unless the launch is under two rounds of blocks
-// (two blocks per CU), where 128 / 64-row tiles spread the work over more CUs.  Conv flag bits
-// 0x30000 force 256 (1) / 128 (2) / 64 (3) for A/B measurement.
+// (two blocks per CU), where 192 / 128 / 64-row tiles spread the work over more CUs.  Conv flag bits
+// 0x70000 force 256 (1) / 128 (2) / 64 (3) / 192 (4) for A/B measurement.
 int az_conv_v7_tm(const ConvBf16Args& a) {
-    const int force = (a.flags >> 16) & 3;
-    if (force) return force == 1 ? 256 : force == 2 ? 128 : 64;
+    const int force = (a.flags >> 16) & 7;
+    if (force) return force == 1 ? 256 : force == 2 ? 128 : force == 3 ? 64 : 192;
     const long rows = (long)a.M;
     const int halves = a.N / 128;
     auto blocks = [&](int tm) { return ((rows + tm - 1) / tm + 7) / 8 * 8 * halves; };
     if (blocks(256) >= 1024) return 256;
+    // 19x19: 192-row tiles (128 boards: 0.0700 vs v6 0.0747 ms; 256: 0.1284 vs 0.1375 and 128-row
+    // tiles 0.1378; profiles/r04_small_batch_tiles_192.txt)
+    if (a.H == 19) return 192;
     if (blocks(128) >= 512) return 128;
     return 64;
 }

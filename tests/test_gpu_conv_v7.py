@@ -28,11 +28,13 @@ CASES = [  # board, in_planes, actions, channels, blocks, B, flags selecting v7 
     (9, 11, 81, 128, 2, 29, 0x804),       # DENSE 9x9
     (13, 8, 170, 256, 1, 7, 0x804),       # DENSE 13x13
     (8, 111, 4672, 256, 2, 33, 0x804),    # DENSE 8x8 chess: the 128-channel input conv runs on v7 too
-    # small-batch DENSE tiles (conv flag bits 0x30000 force the tile rows: 1 = 256, 2 = 128, 3 = 64;
-    # without them az_conv_v7_tm picks by the launch's block count -- the cases above take 64)
+    # small-batch DENSE tiles (conv flag bits 0x70000 force the tile rows: 1 = 256, 2 = 128, 3 = 64,
+    # 4 = 192; without them az_conv_v7_tm picks by the board and the launch's block count)
     (19, 8, 362, 256, 2, 13, 0x10804),    # 256-row tiles at a small batch
     (19, 8, 362, 256, 2, 13, 0x20804),    # 128-row tiles
     (19, 8, 362, 256, 2, 13, 0x30804),    # 64-row tiles
+    (19, 8, 362, 256, 2, 13, 0x40804),    # 192-row tiles (two A register sets of 3 fragments)
+    (8, 111, 4672, 256, 2, 33, 0x40804),  # 8x8, 192-row tiles
     (8, 111, 4672, 256, 2, 33, 0x20804),  # 8x8, 128-row tiles: tiles span 2 boards
     (15, 11, 225, 256, 2, 37, 0x20a0c),   # 15x15 DENSE, 128-row tiles
     (13, 8, 170, 256, 1, 7, 0x30804),     # 13x13, 64-row tiles (a tile holds < 1 board)
