@@ -38,7 +38,9 @@ class HipNeuralNetwork : public NeuralNetwork {
     // without executing it (alphazero/nn/torchscript_reader.h).  precision: AZ_PREC_* of the trunk
     // (-1: fp32-faithful, the reference's default fp32 inference -- AZ_PREC_F16X3 where its kernels
     // exist, else AZ_PREC_BF16X3 where the trunk has 16-bit kernels, else AZ_PREC_F32);
-    // boardSize <= 0: from the policy size.
+    // boardSize <= 0: from the policy size.  With precision -1 a net whose activations leave the
+    // fp16 range (AZ_ERR_RANGE from an F16X3 forward) is switched to AZ_PREC_BF16X3 (fp32 range) and
+    // the forward repeated, so predictBatch never fails on it.
     static std::unique_ptr<HipNeuralNetwork> loadTorchScript(const std::string& path, core::GameType type,
                                                              int boardSize = 0, int precision = -1,
                                                              int maxBatch = 2048, int device = -1);
@@ -76,6 +78,7 @@ class HipNeuralNetwork : public NeuralNetwork {
     std::vector<float> blob_;
     float lastMs_ = 0.0f;
     bool debug_ = false;
+    bool autoPrecision_ = false;   // loadTorchScript chose the precision: F16X3 falls back to BF16X3 on AZ_ERR_RANGE
     std::mutex mu_;
 };
 

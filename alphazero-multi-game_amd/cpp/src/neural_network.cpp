@@ -107,7 +107,8 @@ std::unique_ptr<HipNeuralNetwork> HipNeuralNetwork::loadTorchScript(const std::s
         // AZ_PREC_F16X3: conv3x3_v9x3 / v7x3 boards with channels % 128 == 0, the 15x15 64-channel
         // fused net), else bf16 pieces (channels % 32 == 0), else fp32
         const int b = s.boardSize;
-        const bool trunk = (b == 8 || b == 9 || b == 13 || b == 15 || b == 19) && s.channels % 128 == 0;
+        const bool trunk = (b == 8 || b == 9 || b == 13 || b == 15 || b == 19) && s.channels % 128 == 0 &&
+                           (size_t)s.maxBatch * b * b * s.channels * 2 + 524288 < ((size_t)1 << 31);   // check_precision's bound
         const bool small = b == 15 && s.channels == 64 && s.inPlanes <= 16 && s.blocks <= 15 && s.pool <= 8 &&
                            2 * s.headChannels == 64;
         s.precision = (trunk || small) && s.blocks > 0 ? AZ_PREC_F16X3
@@ -116,6 +117,7 @@ std::unique_ptr<HipNeuralNetwork> HipNeuralNetwork::loadTorchScript(const std::s
     }
     auto net = std::make_unique<HipNeuralNetwork>(s, device);
     net->loadWeights(blob);
+    net->autoPrecision_ = precision < 0;
     return net;
 }
 
@@ -169,9 +171,18 @@ void HipNeuralNetwork::predictBatch(const std::vector<std::reference_wrapper<con
     const auto t0 = std::chrono::steady_clock::now();
     for (int b0 = 0; b0 < B; b0 += shape_.maxBatch) {
         const int n = std::min(shape_.maxBatch, B - b0);
-        check(az_net_predict_batch(net_, planes.data() + (size_t)b0 * P, n, pol.data() + (size_t)b0 * A,
-                                   values.data() + b0),
-              "az_net_predict_batch");
+        auto run = [&]() {
+            return az_net_predict_batch(net_, planes.data() + (size_t)b0 * P, n, pol.data() + (size_t)b0 * A,
+                                        values.data() + b0);
+        };
+        int rc = run();
+        if (rc == AZ_ERR_RANGE && autoPrecision_ && shape_.precision == AZ_PREC_F16X3 &&
+            az_net_set_precision(net_, AZ_PREC_BF16X3) == AZ_OK) {
+            // activations beyond fp16's range: the fp32-range split precision from now on
+            shape_.precision = AZ_PREC_BF16X3;
+            rc = run();
+        }
+        check(rc, "az_net_predict_batch");
     }
     lastMs_ = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
     for (int i = 0; i < B; ++i) policies[i].assign(pol.begin() + (size_t)i * A, pol.begin() + (size_t)(i + 1) * A);

@@ -30,11 +30,11 @@
 #include "randwire.h"
 
 // kernels (tree_kernels.hip)
-void az_launch_select(const TreeDev& t, int mode, hipStream_t st);
-void az_launch_expand_select(const TreeDev& te, const TreeDev& ts, hipStream_t st);
-__global__ void k_scan(TreeDev t);
-__global__ void k_expand_backup(TreeDev t, int mode);
-__global__ void k_select_action(TreeDev t, int training, float temperature, const float* temps, int* actions, float* values, float* probs,
+void az_launch_select(const TreeDev* t, int NA, int G, int mode, hipStream_t st);
+void az_launch_expand_select(const TreeDev* ts, const int* eval_slot, int eval_identity, int NA, int G, hipStream_t st);
+__global__ void k_scan(const TreeDev* __restrict__ tp);
+__global__ void k_expand_backup(const TreeDev* __restrict__ tp, int mode);
+__global__ void k_select_action(const TreeDev* __restrict__ tp, int training, float temperature, const float* temps, int* actions, float* values, float* probs,
                                 int* child_actions, int* nchild);
 __global__ void k_apply(TreeDev t, const int* actions, int* terminal, int* result);
 __global__ void k_compact(TreeDev t, Nodes dst, int* src_of);
@@ -197,6 +197,9 @@ struct az_net {
     float* rw_ws = nullptr;           // their split-K partials [rw_splits][rows][F]
     bool loaded = false;
     std::vector<float> host_blob;   // canonical blob of the loaded weights (az_net_get_weights)
+    // every activation / workspace buffer (pointer, bytes before any zeroed tail): the poison
+    // diagnostic (az_diag_set_poison) overwrites them before each forward
+    std::vector<std::pair<void*, size_t>> scratch;
     // profiling: HIP events bracketing the 3x3 trunk of every forward (on the launch stream)
     bool prof = false;
     ProfClock pc;                 // sampled trunk timing (az_net_profile)
@@ -318,7 +321,9 @@ int upload_layer(Layer& L, const std::vector<float>& W, const std::vector<float>
             for (int o = 0; o < N; ++o) {
                 float m = 0.0f;
                 for (size_t k = 0; k < (size_t)9 * C; ++k) m = std::max(m, std::fabs(W[(size_t)o * 9 * C + k]));
-                const int s = m > 0.0f ? 13 - std::ilogb(m) : 0;        // max |W[o]| * 2^s in [2^13, 2^14)
+                // max |W[o]| * 2^s in [2^13, 2^14); s capped at 60 so that a near-zero channel (max |w| below
+                // 2^-47) cannot overflow 2^s or bias * 2^s (its tiny weights keep only fp16's subnormal precision)
+                const int s = m > 0.0f ? std::min(60, 13 - std::ilogb(m)) : 0;
                 const float up = std::ldexp(1.0f, s);
                 bx[o] = b[o] * up;
                 sx[o] = std::ldexp(1.0f, -s);
@@ -399,7 +404,7 @@ int net_load(az_net* n, const float* blob) {
                 float m = 0.0f;
                 for (int t = 0; t < 9; ++t)
                     for (int c = 0; c < F; ++c) m = std::max(m, std::fabs(smf[((l * 9 + t) * F + nn) * F + c]));
-                const int sc = m > 0.0f ? 13 - std::ilogb(m) : 0;
+                const int sc = m > 0.0f ? std::min(60, 13 - std::ilogb(m)) : 0;   // capped as in upload_layer
                 const float up = std::ldexp(1.0f, sc);
                 sbx[l * F + nn] = smb[l * F + nn] * up;
                 ssx[l * F + nn] = std::ldexp(1.0f, -sc);
@@ -497,7 +502,7 @@ int load_heads(az_net* n, ParamCursor& pc) {
             for (int r = 0; r < rows; ++r) {
                 float m = 0.0f;
                 for (int k = 0; k < K; ++k) m = std::max(m, std::fabs(Wm[(size_t)r * K + k]));
-                const int s = m > 0.0f ? 13 - std::ilogb(m) : 0;      // max |row| * 2^s in [2^13, 2^14)
+                const int s = m > 0.0f ? std::min(60, 13 - std::ilogb(m)) : 0;   // max |row| * 2^s in [2^13, 2^14); capped
                 const float up = std::ldexp(1.0f, s);
                 rs[r0 + r] = std::ldexp(1.0f, -s);
                 for (int k = 0; k < K; ++k) {
@@ -736,6 +741,21 @@ float* rw_trunk(az_net* n, int B, const int* nb, hipStream_t st) {
     return x;
 }
 
+// Diagnostic (az_diag_set_poison): with a byte value >= 0, every activation / workspace buffer of a
+// net (not the zeroed tails, not the weights) is filled with that byte before each forward, so a
+// kernel that reads memory its forward never wrote gives a result that depends on the byte
+// (0xff: NaN in every float format) -- the tests compare forwards under two poisons bitwise
+static int g_poison = -1;
+extern "C" int az_diag_set_poison(int byte) { g_poison = byte < 0 ? -1 : (byte & 0xff); return 0; }
+static int poison_net(az_net* n, hipStream_t st, bool inputs) {
+    if (g_poison < 0) return 0;
+    for (const auto& b : n->scratch) {
+        const bool in = b.first == (void*)n->x0 || b.first == (void*)n->in_nchw;
+        if (in == inputs) HIPCHK(hipMemsetAsync(b.first, g_poison, b.second, st));
+    }
+    return 0;
+}
+
 // Forward of B samples (B = capacity; *nb = active samples, device side) from the
 // NHWC16 input x0 -> logits [B][A], value [B].  lr (optional; only where
 // net_input_path != NET_IN_GEMM): the planes come from leaf records instead of x0.
@@ -756,6 +776,7 @@ int net_forward(az_net* n, const float* x0, int B, const int* nb, float* logits,
     int8_t* hq[2] = {reinterpret_cast<int8_t*>(n->hl[0]), reinterpret_cast<int8_t*>(n->hl[1])};
     const int inpath = net_input_path(n);
     if (lr && inpath == NET_IN_GEMM) return az_fail(AZ_ERR_ARG, "net_forward: this net cannot read leaf records");
+    if (int r = poison_net(n, st, false)) return r;
     if (prec == AZ_PREC_F16X3 && !g8x3 && inpath != NET_IN_SMALL)
         return az_fail(AZ_ERR_ARG, "AZ_PREC_F16X3: no fp16-piece trunk for this shape");
     if (inpath == NET_IN_SMALL) {
@@ -1033,10 +1054,41 @@ struct az_search {
     std::vector<float> sp_probs, sp_values;
     std::vector<int> sp_cact, sp_nch, sp_slots;
     std::vector<az_move_rec> sp_moves;
+    // device-resident copies of the TreeDev variants the per-step kernels take (tree_dev()): those
+    // kernels get one 8-byte pointer instead of the ~550-byte struct by value, on ~38k dispatches per
+    // C3 move.  Slot i's host shadow (pinned, the source of its async upload) is h_tree[i].
+    TreeDev* d_tree = nullptr;
+    TreeDev* h_tree = nullptr;
+    int n_tree = 0, next_tree = 0;
     std::mutex mu;
 };
 
 namespace {
+
+constexpr int AZ_TREE_SLOTS = 16;
+// The device copy of TreeDev t (a variant with another arena or batch map is another slot).  A new
+// variant is uploaded on the engine stream, so kernels queued before it still read their slot's old
+// contents; a slot is reused only after a stream synchronisation (no queued kernel reads it then).
+// Variants repeat (2 arenas x {search, identity batch}), so uploads happen at the first moves only.
+const TreeDev* tree_dev(az_search* s, const TreeDev& t) {
+    for (int i = 0; i < s->n_tree; ++i)
+        if (std::memcmp(&s->h_tree[i], &t, sizeof(TreeDev)) == 0) return s->d_tree + i;
+    int k;
+    if (s->n_tree < AZ_TREE_SLOTS) {
+        k = s->n_tree++;
+    } else {
+        if (hipStreamSynchronize(s->e->stream) != hipSuccess) return nullptr;
+        k = s->next_tree;
+        s->next_tree = (k + 1) % AZ_TREE_SLOTS;
+    }
+    std::memcpy(&s->h_tree[k], &t, sizeof(TreeDev));
+    if (hipMemcpyAsync(s->d_tree + k, &s->h_tree[k], sizeof(TreeDev), hipMemcpyHostToDevice, s->e->stream) != hipSuccess)
+        return nullptr;
+    return s->d_tree + k;
+}
+#define TREE_DEV(var, s, t)                                                       \
+    const TreeDev* var = tree_dev(s, t);                                          \
+    if (!var) return az_fail(AZ_ERR_HIP, "TreeDev upload failed")
 
 // The fp16 range guard's flag of a net (sticky on the device until read here): AZ_ERR_RANGE once set.
 int check_ovf(az_net* n, int ovf) {
@@ -1066,7 +1118,8 @@ int check_err(az_search* s) {
 int host_evaluate(az_search* s) {
     hipStream_t st = s->e->stream;
     const int G = s->c.n_games, A = s->t.A, NA = s->t.NA, C = s->t.game == GAME_GO ? 8 : 11;
-    hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, st, s->t);
+    TREE_DEV(dt, s, s->t);
+    hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, st, dt);
     int n = 0;
     HIPCHK(hipMemcpyAsync(&n, s->t.n_eval, 4, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
@@ -1115,7 +1168,8 @@ int search_step(az_search* s, int mode, bool pre = false, bool fuse_next = false
     s->t.nd = s->arena[s->cur];
     const bool prof = s->prof && mode == MODE_SIM && s->prof_steps++ % prof_every() == 0 && s->pc.room(4);
     if (prof) s->pc.stamp(st);
-    if (!pre) az_launch_select(s->t, mode, st);
+    TREE_DEV(dts, s, s->t);
+    if (!pre) az_launch_select(dts, s->t.NA, s->t.G, mode, st);
     if (prof) s->pc.stamp(st);
     if (s->c.eval_kind == AZ_EVAL_CALLBACK) {
         if (int r = host_evaluate(s)) return r;
@@ -1132,7 +1186,7 @@ int search_step(az_search* s, int mode, bool pre = false, bool fuse_next = false
         if (identity) {
             tt.eval_slot = s->d_id; tt.eval_games = s->d_id; tt.n_eval = s->d_id + G; tt.eval_identity = 1;
         } else {
-            hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, st, s->t);
+            hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, st, dts);
         }
         // the net's input stage builds the leaves' planes from their records (record eval_games[b])
         // where it can; otherwise a dense fp32 plane batch is built first
@@ -1147,8 +1201,12 @@ int search_step(az_search* s, int mode, bool pre = false, bool fuse_next = false
         if (r) return r;
     }
     if (prof) s->pc.stamp(st);
-    if (fuse_next) az_launch_expand_select(tt, s->t, st);
-    else hipLaunchKernelGGL(k_expand_backup, dim3(G), dim3(64), 0, st, tt, mode);
+    if (fuse_next) {
+        az_launch_expand_select(dts, tt.eval_slot, tt.eval_identity, s->t.NA, G, st);
+    } else {
+        TREE_DEV(dte, s, tt);
+        hipLaunchKernelGGL(k_expand_backup, dim3(G), dim3(64), 0, st, dte, mode);
+    }
     if (prof) { s->pc.stamp(st); s->prof_sampled += 1; }
     HIPCHK(hipGetLastError());
     return 0;
@@ -1296,7 +1354,8 @@ int search_select(az_search* s, int training, const float* temps_host, float T, 
     const int G = s->c.n_games, A = s->t.NA;     // child-order arrays are [G][NA]
     s->t.nd = s->arena[s->cur];
     if (temps_host) HIPCHK(hipMemcpyAsync(s->d_temps, temps_host, G * 4, hipMemcpyHostToDevice, st));
-    hipLaunchKernelGGL(k_select_action, dim3(G), dim3(64), 0, st, s->t, training, T, temps_host ? s->d_temps : nullptr,
+    TREE_DEV(dt, s, s->t);
+    hipLaunchKernelGGL(k_select_action, dim3(G), dim3(64), 0, st, dt, training, T, temps_host ? s->d_temps : nullptr,
                        s->d_actions, s->d_values, s->d_probs, s->d_cact, s->d_nch);
     HIPCHK(hipGetLastError());
     if (actions) HIPCHK(hipMemcpyAsync(actions, s->d_actions, G * 4, hipMemcpyDeviceToHost, st));
@@ -1379,12 +1438,17 @@ static int check_precision(const az_net_desc& d, int precision) {
         // the fp16-piece kernels: conv3x3_v9x3 / v7x3 (8/9/13/15/19 boards, channels % 128 == 0) or
         // k_smallnet_x3 (15x15, 64 channels)
         const int H = d.board_size;
-        const bool trunk = (H == 8 || H == 9 || H == 13 || H == 15 || H == 19) && d.channels % 128 == 0;
+        // (the shape test of az_conv_v7x3_supported at the capacity, as x3_trunk applies it: the 32-bit
+        // buffer ranges of the activations + their zeroed tail and of the weights)
+        const size_t act_bytes = (size_t)d.max_batch * H * H * d.channels * 2;
+        const bool trunk = (H == 8 || H == 9 || H == 13 || H == 15 || H == 19) && d.channels % 128 == 0 &&
+                           act_bytes + AZ_ACT_TAIL * 2 < ((size_t)1 << 31) &&
+                           (size_t)9 * d.channels * d.channels * 2 < ((size_t)1 << 31);
         const bool small = az_smallnet_supported(H, d.channels, (d.in_planes + 15) / 16 * 16, d.pool, d.head_channels) &&
                            d.blocks <= az_smallnet_max_blocks();
         if (!trunk && !small && d.blocks > 0)
-            return az_fail(AZ_ERR_ARG, "AZ_PREC_F16X3 needs an 8/9/13/15/19 board with channels %% 128 == 0, or the 15x15 "
-                                    "64-channel net; use AZ_PREC_BF16X3 or AZ_PREC_F32");
+            return az_fail(AZ_ERR_ARG, "AZ_PREC_F16X3 needs an 8/9/13/15/19 board with channels %% 128 == 0 (and under 2 GiB "
+                                    "per activation buffer), or the 15x15 64-channel net; use AZ_PREC_BF16X3 or AZ_PREC_F32");
     }
     if (precision != AZ_PREC_F32 && d.channels % 32) return az_fail(AZ_ERR_ARG, "bf16/fp16 trunk needs channels %% 32 == 0");
     if (precision == AZ_PREC_FP16 && !az_conv_v4_supported(d.board_size, d.board_size, d.channels, d.channels) &&
@@ -1429,12 +1493,16 @@ static int net_create(az_engine* e, const az_net_desc* d, az_net** out, bool rw,
     const size_t B = d->max_batch, rows = B * n->HW, F = d->channels;
     n->act_elems = rows * F;
     int r = 0;
-    auto A_ = [&](float** p, size_t cnt) { if (!r) r = dalloc(p, cnt); };
+    auto A_ = [&](float** p, size_t cnt) {
+        if (!r) r = dalloc(p, cnt);
+        if (!r) n->scratch.emplace_back((void*)*p, cnt * 4);
+    };
     // 16-bit activation planes carry a zeroed tail (AZ_ACT_TAIL elements): the v6 conv points the
     // DMA of halo padding rows there
     auto H_ = [&](uint16_t** p, size_t cnt) {
         if (!r) r = dalloc(p, cnt + AZ_ACT_TAIL);
         if (!r && hipMemset(*p + cnt, 0, AZ_ACT_TAIL * 2) != hipSuccess) r = az_fail(AZ_ERR_HIP, "hipMemset");
+        if (!r) n->scratch.emplace_back((void*)*p, cnt * 2);
     };
     A_(&n->x0, rows * n->cin_pad);
     A_(&n->h0, rows * F); A_(&n->h1, rows * F); A_(&n->t, rows * F);
@@ -1486,6 +1554,9 @@ static int net_create(az_engine* e, const az_net_desc* d, az_net** out, bool rw,
     if (!r && hipMemset(n->ovf, 0, 4) != hipSuccess) r = az_fail(AZ_ERR_HIP, "memset");
     if (!r) r = dalloc(&n->zero, 128);
     if (!r && hipMemset(n->zero, 0, 256) != hipSuccess) r = az_fail(AZ_ERR_HIP, "memset");
+    // the memsets above run on the null stream, the forwards on the engine's non-blocking stream,
+    // which does not wait for it: finish them here
+    if (!r && hipDeviceSynchronize() != hipSuccess) r = az_fail(AZ_ERR_HIP, "hipDeviceSynchronize");
     if (r) { az_net_destroy(n); return r; }
     *out = n;
     return 0;
@@ -1639,6 +1710,7 @@ int az_net_load_weights(az_net* n, const float* blob, size_t count) {
     std::lock_guard<std::mutex> lk(n->mu);
     HIPCHK(hipSetDevice(n->e->device));
     if (int r = n->rw ? net_load_rw(n, blob) : net_load(n, blob)) return r;
+    HIPCHK(hipDeviceSynchronize());   // null-stream uploads done before the non-blocking stream reads them
     n->host_blob.assign(blob, blob + count);
     return 0;
 }
@@ -1715,6 +1787,7 @@ static int net_host_forward(az_net* n, const float* planes, int B, float* logits
     HIPCHK(hipSetDevice(n->e->device));
     hipStream_t st = n->e->stream;
     const int A = n->d.action_size;
+    if (int r = poison_net(n, st, true)) return r;
     HIPCHK(hipMemcpyAsync(n->in_nchw, planes, (size_t)B * n->d.in_planes * n->HW * 4, hipMemcpyHostToDevice, st));
     HIPCHK(hipMemcpyAsync(n->d_nb, &B, 4, hipMemcpyHostToDevice, st));
     az_launch_pack_input(n->in_nchw, n->x0, B, n->d.in_planes, n->HW, n->cin_pad, st);
@@ -1905,6 +1978,12 @@ int az_search_create(az_engine* e, az_net* net, const az_search_cfg* c, az_searc
         HIPCHK(hipMemcpy(fo, order.data(), A * 4, hipMemcpyHostToDevice));
     }
     HIPCHK(hipMemset(t.err, 0, 4));
+    if (hipMalloc((void**)&s->d_tree, AZ_TREE_SLOTS * sizeof(TreeDev)) != hipSuccess ||
+        hipHostMalloc((void**)&s->h_tree, AZ_TREE_SLOTS * sizeof(TreeDev), hipHostMallocDefault) != hipSuccess) {
+        az_search_destroy(s);
+        return az_fail(AZ_ERR_OOM, "TreeDev slots");
+    }
+    HIPCHK(hipDeviceSynchronize());   // the null-stream copies / memsets above, before the engine stream runs
     // every slot an idle game with a valid root until k_new_games starts it
     t.nd = s->arena[0];
     hipLaunchKernelGGL(k_init_slots, dim3((G + 255) / 256), dim3(256), 0, e->stream, t, s->arena[1]);
@@ -1943,8 +2022,10 @@ void az_search_destroy(az_search* s) {
                           (const void*)s->d_value, (const void*)s->d_noise, (const void*)s->d_mask, (const void*)s->d_actions,
                           (const void*)s->d_values, (const void*)s->d_probs, (const void*)s->d_cact, (const void*)s->d_nch,
                           (const void*)s->d_term, (const void*)s->d_res, (const void*)s->d_games, (const void*)s->d_seed_ids, (const void*)s->d_temps,
-                          (const void*)s->d_rc, (const void*)s->d_rcf, (const void*)s->d_thr, (const void*)s->d_pruned})
+                          (const void*)s->d_rc, (const void*)s->d_rcf, (const void*)s->d_thr, (const void*)s->d_pruned,
+                          (const void*)s->d_tree})
         F(p);
+    if (s->h_tree) hipHostFree(s->h_tree);
     delete s;
 }
 

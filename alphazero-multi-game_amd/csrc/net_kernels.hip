@@ -475,7 +475,7 @@ static void launch_f32(const GemmArgs& p, hipStream_t st) {
 // Both FC heads in two launches: k_fc_heads computes the split-K partials of the policy FC
 // (K -> A logits) and the value FC1 (K -> H hidden) as one GEMM over 64-column tiles of
 // [policy | value] (f32 MFMA v_mfma_f32_16x16x4_f32: every partial a k-ordered fmaf chain, as
-// gemm_f32); k_fc_finish (one wave per board) sums the slices in order and finishes both heads
+// gemm_f32); k_fc_finish (one 256-thread block per board) sums the slices in order and finishes both heads
 // (bias, ReLU, value FC2, tanh).  Deterministic and batch-position independent.
 typedef float f32x4n __attribute__((ext_vector_type(4)));
 

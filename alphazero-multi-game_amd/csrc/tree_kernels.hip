@@ -544,16 +544,38 @@ struct RootHint {
     int first, cnt, flag;
 };
 
+// LDS of the selection and of the expansion: separate structs so that the fused k_expand_select
+// overlays them (a union: the selection starts after the expansion's last LDS access and a block
+// barrier) and shares one GoLds -- 12.3 KB per block instead of 21.1 KB, so 13 blocks fit a CU and
+// C3's 2048 one-wave blocks (8 per CU) run in one round instead of two (7 per CU fitted at 21.1 KB)
+struct SelLds {
+    uint8_t board[AZ_MAXA];
+    int spath[AZ_DMAX];
+    int sact[AZ_DMAX];
+    int sN[AZ_DMAX], sVL[AZ_DMAX];
+    float sW[AZ_DMAX];
+};
+constexpr int EXP_NPAD = ((AZ_MAXNA + 63) / 64) * 64;   // pol / lp padded with +0.0f for seq_sum_lds
+struct ExpLds {
+    __attribute__((aligned(16))) float pol[EXP_NPAD];
+    __attribute__((aligned(16))) float lp[EXP_NPAD];
+    uint8_t board[AZ_MAXA];
+    int spath[AZ_DMAX];
+    int sact[AZ_DMAX];
+    int legal[AZ_MAXNA];
+    float s_scalar[2];
+};
+
 template <int IT>
-__device__ __forceinline__ void select_game(const TreeDev& t, int mode, const RootHint* hint) {
+__device__ __forceinline__ void select_game(const TreeDev& t, int mode, const RootHint* hint, SelLds& SL, GoLds& gl) {
     const int g = blockIdx.x;
     const int lane = threadIdx.x;
-    __shared__ uint8_t board[AZ_MAXA];
-    __shared__ int spath[AZ_DMAX];
-    __shared__ int sact[AZ_DMAX];
-    __shared__ int sN[AZ_DMAX], sVL[AZ_DMAX];
-    __shared__ float sW[AZ_DMAX];
-    __shared__ GoLds gl;
+    auto& board = SL.board;
+    auto& spath = SL.spath;
+    auto& sact = SL.sact;
+    auto& sN = SL.sN;
+    auto& sVL = SL.sVL;
+    auto& sW = SL.sW;
     const bool go = t.game == GAME_GO;
     if (g >= t.G) return;
     // per-game inputs that do not depend on the tree, loaded before anything waits
@@ -810,16 +832,21 @@ __device__ __forceinline__ void select_game(const TreeDev& t, int mode, const Ro
 }
 
 template <int IT>
-__global__ __launch_bounds__(64) void k_select(TreeDev t, int mode) { select_game<IT>(t, mode, nullptr); }
+__global__ __launch_bounds__(64) void k_select(const TreeDev* __restrict__ tp, int mode) {
+    const TreeDev& t = *tp;                               // device-resident (tree_dev, engine.hip): an 8-byte kernarg
+    __shared__ SelLds SL;
+    __shared__ GoLds gl;
+    select_game<IT>(t, mode, nullptr, SL, gl);
+}
 
 extern "C" int az_diag_tree_stamps(unsigned long long* out, int n) {
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_tree_stamps), sizeof(unsigned long long) * (n < 128 ? n : 128)) == hipSuccess ? 0 : -1;
 }
 
-void az_launch_select(const TreeDev& t, int mode, hipStream_t st) {
-    if (t.NA <= 128) hipLaunchKernelGGL(k_select<2>, dim3(t.G), dim3(64), 0, st, t, mode);
-    else if (t.NA <= 256) hipLaunchKernelGGL(k_select<4>, dim3(t.G), dim3(64), 0, st, t, mode);
-    else hipLaunchKernelGGL(k_select<(AZ_MAXNA + 63) / 64>, dim3(t.G), dim3(64), 0, st, t, mode);
+void az_launch_select(const TreeDev* t, int NA, int G, int mode, hipStream_t st) {
+    if (NA <= 128) hipLaunchKernelGGL(k_select<2>, dim3(G), dim3(64), 0, st, t, mode);
+    else if (NA <= 256) hipLaunchKernelGGL(k_select<4>, dim3(G), dim3(64), 0, st, t, mode);
+    else hipLaunchKernelGGL(k_select<(AZ_MAXNA + 63) / 64>, dim3(G), dim3(64), 0, st, t, mode);
 }
 
 // Host evaluator: the moves from the root to every leaf of the evaluation batch (slot order).
@@ -833,7 +860,8 @@ __global__ void k_leaf_moves(TreeDev t, int* moves, int* len) {
 }
 
 // K2: deterministic compaction of the leaves that need the network (one block).
-__global__ __launch_bounds__(1024) void k_scan(TreeDev t) {
+__global__ __launch_bounds__(1024) void k_scan(const TreeDev* __restrict__ tp) {
+    const TreeDev& t = *tp;
     __shared__ int part[1024];
     const int tid = threadIdx.x;
     const int per = (t.G + 1023) / 1024;
@@ -865,19 +893,18 @@ __global__ __launch_bounds__(1024) void k_scan(TreeDev t) {
 // then the leaf's network outputs and the path nodes' statistics -- the second and last one.
 // The Gomoku leaf board is the root board plus the path moves (no Zobrist work: k_select stored
 // the leaf hash); Go replays its captures on lane 0 (go_build_leaf).
-__device__ __forceinline__ void expand_game(const TreeDev& t, int mode, RootHint* hint = nullptr) {
+__device__ __forceinline__ void expand_game(const TreeDev& t, int mode, ExpLds& EL, GoLds& gl, RootHint* hint = nullptr) {
     const int g = blockIdx.x;
     const int lane = threadIdx.x;
     if (hint && lane == 0) hint->valid = 0;
-    __shared__ uint8_t board[AZ_MAXA];
-    __shared__ int spath[AZ_DMAX];
-    __shared__ int sact[AZ_DMAX];
-    constexpr int NPAD = ((AZ_MAXNA + 63) / 64) * 64;   // pol / lp padded with +0.0f for seq_sum_lds
-    __shared__ __attribute__((aligned(16))) float pol[NPAD];
-    __shared__ int legal[AZ_MAXNA];
-    __shared__ __attribute__((aligned(16))) float lp[NPAD];
-    __shared__ float s_scalar[2];
-    __shared__ GoLds gl;
+    constexpr int NPAD = EXP_NPAD;
+    auto& board = EL.board;
+    auto& spath = EL.spath;
+    auto& sact = EL.sact;
+    auto& pol = EL.pol;
+    auto& legal = EL.legal;
+    auto& lp = EL.lp;
+    auto& s_scalar = EL.s_scalar;
     static_assert(AZ_DMAX <= 128, "two path entries per lane");
     constexpr int BK = (AZ_MAXA + 63) / 64, PK = (AZ_MAXNA + 63) / 64;
     const bool go = t.game == GAME_GO;
@@ -1190,7 +1217,12 @@ __device__ __forceinline__ void expand_game(const TreeDev& t, int mode, RootHint
     tstamp(t, g, 1, 7);
 }
 
-__global__ __launch_bounds__(64) void k_expand_backup(TreeDev t, int mode) { expand_game(t, mode); }
+__global__ __launch_bounds__(64) void k_expand_backup(const TreeDev* __restrict__ tp, int mode) {
+    const TreeDev& t = *tp;
+    __shared__ ExpLds EL;
+    __shared__ GoLds gl;
+    expand_game(t, mode, EL, gl);
+}
 
 // K3 of simulation step i and K1 of step i+1 in one launch: a game's expansion / backup and its
 // next selection are the same wave's consecutive work (no other game is involved), so one
@@ -1199,26 +1231,30 @@ __global__ __launch_bounds__(64) void k_expand_backup(TreeDev t, int mode) { exp
 // One TreeDev argument (the kernel's scalar registers are the tight resource): the expansion's
 // batch map differs from the search's only in eval_slot / eval_identity.
 template <int IT>
-__global__ __launch_bounds__(64) void k_expand_select(TreeDev ts, const int* eval_slot, int eval_identity) {
+__global__ __launch_bounds__(64) void k_expand_select(const TreeDev* __restrict__ tsp, const int* eval_slot, int eval_identity) {
+    const TreeDev& ts = *tsp;
     __shared__ RootHint hint;
+    __shared__ union PhaseLds { SelLds s; ExpLds e; } U;
+    __shared__ GoLds gl;
     TreeDev te = ts;
     te.eval_slot = const_cast<int*>(eval_slot);
     te.eval_identity = eval_identity;
-    expand_game(te, MODE_SIM, &hint);
-    __syncthreads();
-    select_game<IT>(ts, MODE_SIM, &hint);
+    expand_game(te, MODE_SIM, U.e, gl, &hint);
+    __syncthreads();                                      // the expansion's LDS is the selection's from here
+    select_game<IT>(ts, MODE_SIM, &hint, U.s, gl);
 }
 
-void az_launch_expand_select(const TreeDev& te, const TreeDev& ts, hipStream_t st) {
-    if (ts.NA <= 128) hipLaunchKernelGGL(k_expand_select<2>, dim3(ts.G), dim3(64), 0, st, ts, te.eval_slot, te.eval_identity);
-    else if (ts.NA <= 256) hipLaunchKernelGGL(k_expand_select<4>, dim3(ts.G), dim3(64), 0, st, ts, te.eval_slot, te.eval_identity);
-    else hipLaunchKernelGGL(k_expand_select<(AZ_MAXNA + 63) / 64>, dim3(ts.G), dim3(64), 0, st, ts, te.eval_slot, te.eval_identity);
+void az_launch_expand_select(const TreeDev* ts, const int* eval_slot, int eval_identity, int NA, int G, hipStream_t st) {
+    if (NA <= 128) hipLaunchKernelGGL(k_expand_select<2>, dim3(G), dim3(64), 0, st, ts, eval_slot, eval_identity);
+    else if (NA <= 256) hipLaunchKernelGGL(k_expand_select<4>, dim3(G), dim3(64), 0, st, ts, eval_slot, eval_identity);
+    else hipLaunchKernelGGL(k_expand_select<(AZ_MAXNA + 63) / 64>, dim3(G), dim3(64), 0, st, ts, eval_slot, eval_identity);
 }
 
 // K4: visit distribution, action choice and root value per game.
-__global__ __launch_bounds__(64) void k_select_action(TreeDev t, int training, float temperature, const float* temps,
-                                                      int* actions, float* values, float* probs, int* child_actions,
-                                                      int* nchild) {
+__global__ __launch_bounds__(64) void k_select_action(const TreeDev* __restrict__ tp, int training, float temperature,
+                                                      const float* temps, int* actions, float* values, float* probs,
+                                                      int* child_actions, int* nchild) {
+    const TreeDev& t = *tp;
     const int g = blockIdx.x;
     if (temps && g < t.G) temperature = temps[g];         // per-game schedule (self-play driver)
     const int lane = threadIdx.x;

@@ -18,6 +18,13 @@ def _flags(f):
     _lib.lib().az_diag_set_conv_flags(int(f))
 
 
+def _poison(byte):
+    """az_diag_set_poison: every activation / workspace buffer of a net is filled with `byte` before
+    each forward (-1: off), so a read of memory the forward never wrote shows up as a bitwise change"""
+    from az_amd import _lib
+    _lib.lib().az_diag_set_poison(int(byte))
+
+
 CASES = [  # board, in_planes, actions, channels, blocks, B, flags selecting v7 (v6 = flags | 0x100)
     (15, 11, 225, 256, 2, 37, 0xa04),     # SLIM 15x16 tile (the default), ragged batch
     (15, 11, 225, 256, 1, 1, 0xa04),      # a single board
@@ -55,17 +62,26 @@ def test_gpu_v7_bitwise_equals_v6(engine, case, mode):
     net.load_weights(net_oracle.init_blob(desc, seed=31))
     rng = np.random.default_rng(bs * 7 + B)
     x = (rng.random((B, ci, bs, bs)) < (0.05 if ci > 16 else 0.25)).astype(np.float32)
+    # v6 and v7 each run under two poisons (NaN bytes, then 0x55) and v7 once clean: a kernel that
+    # reads activation / remainder / workspace memory its forward never wrote cannot pass
+    outs = {}
     try:
-        _flags(fl | 0x100)
-        l6, v6 = net.forward(x)
-        _flags(fl)
-        l7, v7 = net.forward(x)
+        for name, f, byte in (("v6/ff", fl | 0x100, 0xff), ("v6/55", fl | 0x100, 0x55),
+                              ("v7/ff", fl, 0xff), ("v7/55", fl, 0x55), ("v7", fl, -1)):
+            _flags(f)
+            _poison(byte)
+            outs[name] = net.forward(x)
     finally:
+        _poison(-1)
         _flags(0x204)                     # the library default
-    bad = np.where((l7 != l6).any(axis=1) | (v7 != v6))[0]
-    print(f"{case} {mode}: max|v7 - v6| logits {np.abs(l7 - l6).max():.3e} value {np.abs(v7 - v6).max():.3e}, "
-          f"boards differing {bad.tolist()[:16]} of {B}")
-    assert np.array_equal(l7, l6) and np.array_equal(v7, v6)
+    l6, v6 = outs["v6/ff"]
+    for name, (l7, v7) in outs.items():
+        bad = np.where((l7 != l6).any(axis=1) | (v7 != v6))[0]
+        print(f"{case} {mode} {name}: max|. - v6| logits {np.abs(l7 - l6).max():.3e} value {np.abs(v7 - v6).max():.3e}, "
+              f"boards differing {bad.tolist()[:16]} of {B}")
+    for name, (l7, v7) in outs.items():
+        assert np.isfinite(l7).all() and np.isfinite(v7).all(), name
+        assert np.array_equal(l7, l6) and np.array_equal(v7, v6), name
     net.close()
 
 
@@ -104,15 +120,20 @@ def test_gpu_v9x3_bitwise_equals_v7x3(engine, case, prec):
     x = (rng.random((B, ci, bs, bs)) < (0.05 if ci > 16 else 0.25)).astype(np.float32)
     try:
         _flags(0x10000204)                # conv3x3_v7x3
+        _poison(0xff)
         l7, v7 = net.forward(x)
         outs = {}
         for fl in (V9_VARIANTS if prec == "bf16x3" else V9_VARIANTS[:1]):   # 0x204: the library default
             _flags(fl)
+            _poison(0x55)
             outs[fl] = net.forward(x)
+        _poison(-1)
+        outs["clean"] = net.forward(x)
     finally:
+        _poison(-1)
         _flags(0x204)
     for fl, (l9, v9) in outs.items():
-        print(f"{case} flags {fl:#x}: max|v9x3 - v7x3| logits {np.abs(l9 - l7).max():.3e} value {np.abs(v9 - v7).max():.3e}")
+        print(f"{case} flags {fl}: max|v9x3 - v7x3| logits {np.abs(l9 - l7).max():.3e} value {np.abs(v9 - v7).max():.3e}")
         assert np.isfinite(l9).all() and np.abs(l9).max() > 0
-        assert np.array_equal(l9, l7) and np.array_equal(v9, v7), hex(fl)
+        assert np.array_equal(l9, l7) and np.array_equal(v9, v7), fl
     net.close()

@@ -135,18 +135,30 @@ def test_gpu_go_net_selfplay_matches_oracle_replay(engine, prec):
     net.close()
 
 
+C4_REPLAYS = [  # games per GPU, the logged game, trunk precision, the trunk kernel that batch takes
+    (1024, 777, "fp16", "conv3x3_v6<2, 19, DENSE>"),          # C4 on one GPU
+    (128, 77, "fp16", "conv3x3_v7<2, 19, DENSE, 192>"),       # the per-rank shard of C4 on 8 GPUs
+    (128, 101, "f16x3", "conv3x3_v9x3<19, DENSE, f16>"),      # the same shard in the parity precision
+]
+
+
 @pytest.mark.gpu
-def test_gpu_c4_full_size_replay(engine):
+@pytest.mark.parametrize("G,logged,prec,kernel", C4_REPLAYS, ids=[f"G{c[0]}-{c[2]}" for c in C4_REPLAYS])
+def test_gpu_c4_full_size_replay(engine, G, logged, prec, kernel):
     """C4 at full per-GPU size (BASELINE.json configs[3]: Go 19x19, 1024 games, 800 sims, the 20 x 256
-    net with 8 planes / 362 actions, fp16 trunk on DENSE tiles): the first two moves of every game,
-    game 777 replayed bit for bit through the CPU restatement, sampled network outputs within 1e-4
-    of the fp32 reference network, and every root's probabilities summing to 1."""
+    net with 8 planes / 362 actions, fp16 trunk on DENSE tiles) and at the per-rank shard of its 8-GPU
+    run (128 games: the small-tile trunk; python/scripts/orchestrate_selfplay.py:303-311 shards the
+    games over the GPUs), fp16 and F16X3: the first two moves of every game, one game replayed bit for
+    bit through the CPU restatement, sampled network outputs within 1e-4 of the fp32 reference
+    network, and every root's probabilities summing to 1."""
     import az_amd
     import az_oracle as O
     import net_oracle
-    bs, sims, G, moves, logged = 19, 800, 1024, 2, 777
-    desc = az_amd.NetDesc(bs, 8, 256, 20, bs * bs + 1, 32, 8, 256, 1, 0, az_amd.AZ_PREC_FP16, G)
+    bs, sims, moves = 19, 800, 2
+    p = {"fp16": az_amd.AZ_PREC_FP16, "f16x3": az_amd.AZ_PREC_F16X3}[prec]
+    desc = az_amd.NetDesc(bs, 8, 256, 20, bs * bs + 1, 32, 8, 256, 1, 0, p, G)
     net = az_amd.HipNeuralNetwork(engine, desc)
+    assert net.trunk_kernel() == kernel
     blob = net_oracle.init_blob(desc, seed=1234)
     net.load_weights(blob)
     m = az_amd.ParallelMCTS(engine, n_games=G, board_size=bs, num_simulations=sims, evaluator=az_amd.AZ_EVAL_NET,
@@ -196,6 +208,6 @@ def test_gpu_c4_full_size_replay(engine):
     jdx = np.unique(np.concatenate([[0, G - 1], np.random.default_rng(2).choice(G, 14, replace=False)]))
     jl, jv = net_oracle.forward(desc, blob, xb[jdx])
     el, ev = float(np.abs(lo[jdx] - jl).max()), float(np.abs(v[jdx] - jv).max())
-    print(f"C4 full-size raw outputs: |logit|max {np.abs(jl).max():.3f} max|dlogit|={el:.3e} max|dvalue|={ev:.3e}")
+    print(f"C4 G={G} {prec} raw outputs: |logit|max {np.abs(jl).max():.3f} max|dlogit|={el:.3e} max|dvalue|={ev:.3e}")
     assert el <= 1e-4 and ev <= 1e-4
     net.close()

@@ -191,36 +191,48 @@ def test_gpu_trained_scale_production_batch_x3(engine, shape, B, prec):
     net.close()
 
 
-PROD_B = {"c2": 256, "c3": 2048, "c4": 1024, "c5": 1024}   # the BASELINE configs' batch per forward (one GPU)
+# the BASELINE configs' batch per forward: N = 1 (C2 256, C3 2048, C4 / C5 1024) and the per-rank
+# shards of the multi-GPU configs (python/scripts/orchestrate_selfplay.py:303-311 splits the games over
+# the GPUs): C3 at N = 8 (256 games per GPU), C4 / C5 at N = 8 (128) and C4 at N = 4 (256).  The shard
+# batches take other kernels: fp16 15x15 below 1024 boards conv3x3_v6, 19x19 / 8x8 below 1024 boards the
+# small-tile conv3x3_v7 (192 / 64-row tiles); F16X3 conv3x3_v9x3 with less than one round of blocks.
+PROD_B = [("c2", 256), ("c3", 2048), ("c4", 1024), ("c5", 1024),
+          ("c3", 256), ("c4", 128), ("c4", 256), ("c5", 128)]
+SHARD_KERNEL = {("c3", 256, "fp16"): "conv3x3_v6<2, 15>", ("c4", 128, "fp16"): "conv3x3_v7<2, 19, DENSE, 192>",
+                ("c4", 256, "fp16"): "conv3x3_v7<2, 19, DENSE, 192>", ("c5", 128, "fp16"): "conv3x3_v7<2, 8, DENSE, 64>",
+                ("c3", 256, "f16x3"): "conv3x3_v9x3<15, SLIM, f16>", ("c4", 128, "f16x3"): "conv3x3_v9x3<19, DENSE, f16>",
+                ("c5", 128, "f16x3"): "conv3x3_v9x3<8, DENSE, f16>"}
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("prec", list(PRECS))
-@pytest.mark.parametrize("shape", list(NETS))
-def test_gpu_trunk_scaled_production_batch(engine, shape, prec):
+@pytest.mark.parametrize("shape,B", PROD_B, ids=[f"{s}-B{b}" for s, b in PROD_B])
+def test_gpu_trunk_scaled_production_batch(engine, shape, B, prec):
     """A trained-like TRUNK (trunk_scaled_blob: per-channel BN scales a decade apart, activations
     growing to O(64) through the blocks) plus trained-scale heads, at each config's production batch
-    (C2 256 on k_smallnet_x3, C3 2048, C4 / C5 1024 on conv3x3_v9x3): 16 sampled boards (first, last,
-    14 between) against the fp32 oracle on RAW logits and values.  f16x3 must hold the north-star
+    (C2 256 on k_smallnet_x3, C3 2048, C4 / C5 1024 on conv3x3_v9x3) and at the per-rank shard batches
+    of the multi-GPU configs (C3 256, C4 128 / 256, C5 128): 16 sampled boards (first, last, 14
+    between) against the fp32 oracle on RAW logits and values.  f16x3 must hold the north-star
     1e-4; bf16x3 (16-17 significant bits) is held to BF16X3_REL of the largest logit; fp16's error is
     reported (its 11-bit operands cannot hold 1e-4 at |logit| 8) and bounded relative to the
     largest logit."""
     import az_amd
     import net_oracle
     bs, ci, ch, blocks, A = NETS[shape]
-    B = PROD_B[shape]
     p = PRECS[prec]
     desc = az_amd.NetDesc(bs, ci, ch, blocks, A, 32, 8, 256, 1, 0, p, B)
     x = _planes(shape, B, seed=31)
     pick = np.unique(np.concatenate([[0, B - 1], np.random.default_rng(6).choice(B, 14, replace=False)]))
     blob, amax = trunk_scaled_blob(desc, 2468, x[pick])
     net = az_amd.HipNeuralNetwork(engine, desc)
+    if (shape, B, prec) in SHARD_KERNEL:
+        assert net.trunk_kernel() == SHARD_KERNEL[(shape, B, prec)]
     net.load_weights(blob)
     lo, v = net.forward(x)
     rl, rv = net_oracle.forward(desc, blob, x[pick])
     lmax = float(np.abs(rl).max())
     el, ev = float(np.abs(lo[pick] - rl).max()), float(np.abs(v[pick] - rv).max())
-    print(f"{shape} {prec} B={B} trunk-scaled (max activation {amax:.1f}): |logit|max {lmax:.3f} "
+    print(f"{shape} {prec} B={B} [{net.trunk_kernel()}] trunk-scaled (max activation {amax:.1f}): |logit|max {lmax:.3f} "
           f"max|dlogit|={el:.3e} ({el / lmax:.2e} of |logit|max) max|dvalue|={ev:.3e}")
     assert amax > 30.0 and 7.9 < lmax < 8.1
     if prec == "fp16":
