@@ -356,13 +356,16 @@ class ParallelMCTS:
         check(lib().az_search_profile(self.h, int(enable)))
 
     def profile_read(self):
-        """dict(select_ms, expand_ms, sim_steps, select_bytes, expand_bytes) since profile(True)."""
+        """dict(select_ms, expand_ms, sim_steps, select_bytes, expand_bytes, fused_ms, fused_launches) since
+        profile(True): the split kernels of the sampled steps, the fused k_expand_select of the others."""
         a, b = ctypes.c_double(), ctypes.c_double()
         n, sb, eb = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
         check(lib().az_search_profile_read(self.h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(n), ctypes.byref(sb),
                                            ctypes.byref(eb)))
+        f, fl = ctypes.c_double(), ctypes.c_int64()
+        check(lib().az_search_profile_read_fused(self.h, ctypes.byref(f), ctypes.byref(fl)))
         return {"select_ms": a.value, "expand_ms": b.value, "sim_steps": n.value, "select_bytes": sb.value,
-                "expand_bytes": eb.value}
+                "expand_bytes": eb.value, "fused_ms": f.value, "fused_launches": fl.value}
 
     def selfplayStep(self, temp_drop_move=30, t_init=1.0, t_final=0.0, restart_finished=True):
         cfg = SelfPlayCfg(temp_drop_move, t_init, t_final, int(restart_finished))

@@ -101,6 +101,7 @@ EXPORTS = {
     "az_search_counters": (c_int, [vp, c_int, P(c_int64)]),
     "az_search_profile": (c_int, [vp, c_int]),
     "az_search_profile_read": (c_int, [vp, P(ctypes.c_double), P(ctypes.c_double), P(c_int64), P(c_int64), P(c_int64)]),
+    "az_search_profile_read_fused": (c_int, [vp, P(ctypes.c_double), P(c_int64)]),
     "az_search_enable_eval_log": (c_int, [vp, c_int, c_int]),
     "az_search_read_eval_log": (c_int, [vp, P(c_float), P(c_float), P(c_float), P(c_int)]),
     "az_selfplay_step": (c_int, [vp, P(SelfPlayCfg), P(c_int64), P(c_int64)]),

@@ -45,6 +45,15 @@ class SelfPlayManager {
     void setConcurrentGames(int n) { slots_ = n; }
     void setMaxMoves(int n) { maxMoves_ = n; }
     void setSeeds(unsigned noiseSeed, int noiseSeedStride) { noiseSeed_ = noiseSeed; noiseStride_ = noiseSeedStride; }
+    // Evaluation log (tests: a game replayed through the CPU oracle): every network evaluation of device
+    // slot `slot` (the game id while the games fit the slots) -- post-softmax policy [NA], value, feature
+    // planes [C][A] -- up to `capacity` evaluations, read after generateGames; capacity 0 turns it off.
+    void setEvalLog(int slot, int capacity) { logSlot_ = capacity > 0 ? slot : -1; logCap_ = capacity; }
+    struct EvalLog {
+        int count = 0, policySize = 0, planes = 0, cells = 0;
+        std::vector<float> policy, value, features;   // [count][policySize], [count], [count][planes][cells]
+    };
+    const EvalLog& getEvalLog() const { return log_; }
 
  private:
     nn::NeuralNetwork* nn_;
@@ -63,6 +72,8 @@ class SelfPlayManager {
     bool batchSet_ = false;
     unsigned noiseSeed_ = 42;
     int noiseStride_ = 1;
+    int logSlot_ = -1, logCap_ = 0;
+    EvalLog log_;
 };
 
 }  // namespace selfplay

@@ -455,5 +455,18 @@ PYBIND11_MODULE(_alphazero_cpp, m) {
         .def("getTotalMovesCount", &selfplay::SelfPlayManager::getTotalMovesCount)
         .def("setConcurrentGames", &selfplay::SelfPlayManager::setConcurrentGames)
         .def("setMaxMoves", &selfplay::SelfPlayManager::setMaxMoves)
-        .def("setSeeds", &selfplay::SelfPlayManager::setSeeds);
+        .def("setSeeds", &selfplay::SelfPlayManager::setSeeds)
+        .def("setEvalLog", &selfplay::SelfPlayManager::setEvalLog, py::arg("slot"), py::arg("capacity"))
+        .def("getEvalLog", [](const selfplay::SelfPlayManager& self) {
+            // (policy [n][NA], value [n], planes [n][C][bs][bs]) as numpy arrays
+            const auto& L = self.getEvalLog();
+            const int bs = (int)std::lround(std::sqrt((double)L.cells));
+            py::array_t<float> pol({(py::ssize_t)L.count, (py::ssize_t)L.policySize});
+            py::array_t<float> val((py::ssize_t)L.count);
+            py::array_t<float> pl({(py::ssize_t)L.count, (py::ssize_t)L.planes, (py::ssize_t)bs, (py::ssize_t)bs});
+            std::copy(L.policy.begin(), L.policy.end(), pol.mutable_data());
+            std::copy(L.value.begin(), L.value.end(), val.mutable_data());
+            std::copy(L.features.begin(), L.features.end(), pl.mutable_data());
+            return py::make_tuple(pol, val, pl);
+        });
 }

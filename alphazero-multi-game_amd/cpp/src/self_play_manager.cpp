@@ -144,9 +144,27 @@ std::vector<GameRecord> SelfPlayManager::generateGames(core::GameType type, int 
             az_search_destroy(s);
             throw std::runtime_error(az_last_error());
         }
+        log_ = EvalLog{};
+        if (logSlot_ >= 0 && az_search_enable_eval_log(s, logSlot_, logCap_)) {
+            az_search_destroy(s);
+            throw std::runtime_error(az_last_error());
+        }
         az_selfplay_cfg sc{tempDrop_, tInit_, tFinal_, 0};
         RunCtx ctx{this, &records, type, variant, save_, outDir_, &progress_, &completed_, &totalMoves_, &done};
-        const int rc = az_selfplay_run(s, &sc, numGames_, maxMoves_, sink, progress, &ctx, &abort_);
+        int rc = az_selfplay_run(s, &sc, numGames_, maxMoves_, sink, progress, &ctx, &abort_);
+        if (!rc && logSlot_ >= 0) {
+            EvalLog& L = log_;
+            L.policySize = go ? bs * bs + 1 : bs * bs;
+            L.planes = go ? 8 : 11;
+            L.cells = bs * bs;
+            L.policy.resize((size_t)logCap_ * L.policySize);
+            L.value.resize(logCap_);
+            L.features.resize((size_t)logCap_ * L.planes * L.cells);
+            rc = az_search_read_eval_log(s, L.policy.data(), L.value.data(), L.features.data(), &L.count);
+            L.policy.resize((size_t)L.count * L.policySize);
+            L.value.resize(L.count);
+            L.features.resize((size_t)L.count * L.planes * L.cells);
+        }
         az_search_destroy(s);
         if (rc) throw std::runtime_error(az_last_error());
     } catch (...) {

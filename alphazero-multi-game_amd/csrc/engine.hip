@@ -1047,6 +1047,8 @@ struct az_search {
     bool prof = false;
     ProfClock pc;                 // sampled tree-kernel timing (az_search_profile)
     int64_t prof_steps = 0, prof_sampled = 0;
+    ProfClock pcf;                // sampled timing of the fused k_expand_select (the production tree step)
+    int64_t prof_fused = 0, prof_fused_launches = 0;
     std::vector<long long> prof_cnt0;
     std::vector<std::mt19937> rng;
     std::vector<float> h_noise; std::vector<uint8_t> h_mask;
@@ -1166,6 +1168,7 @@ int search_step(az_search* s, int mode, bool pre = false, bool fuse_next = false
     hipStream_t st = s->e->stream;
     const int G = s->c.n_games;
     s->t.nd = s->arena[s->cur];
+    const int64_t sidx = s->prof_steps;   // this simulation step's index while profiling
     const bool prof = s->prof && mode == MODE_SIM && s->prof_steps++ % prof_every() == 0 && s->pc.room(4);
     if (prof) s->pc.stamp(st);
     TREE_DEV(dts, s, s->t);
@@ -1202,7 +1205,12 @@ int search_step(az_search* s, int mode, bool pre = false, bool fuse_next = false
     }
     if (prof) s->pc.stamp(st);
     if (fuse_next) {
+        // the fused launch is timed on its own cadence, half-way between the split sampled steps
+        const bool fs = s->prof && mode == MODE_SIM && sidx % prof_every() == prof_every() / 2 && s->pcf.room(2);
+        if (s->prof && mode == MODE_SIM) ++s->prof_fused_launches;
+        if (fs) s->pcf.stamp(st);
         az_launch_expand_select(dts, tt.eval_slot, tt.eval_identity, s->t.NA, G, st);
+        if (fs) { s->pcf.stamp(st); ++s->prof_fused; }
     } else {
         TREE_DEV(dte, s, tt);
         hipLaunchKernelGGL(k_expand_backup, dim3(G), dim3(64), 0, st, dte, mode);
@@ -1220,9 +1228,14 @@ extern "C" int az_diag_set_step_trace(int on) { g_step_trace = on; return 0; }
 // bounds the dispatches queued on the engine stream (rocprofv3 --pmc probe)
 static int g_sync_every = 0;
 extern "C" int az_diag_set_sync_every(int n) { g_sync_every = n; return 0; }
-#define STEP_TRACE(...)                                                   \
-    do {                                                                  \
-        if (g_step_trace) { fprintf(stderr, "[step] " __VA_ARGS__); fputc('\n', stderr); fflush(stderr); } \
+// each line carries the host's wall clock (ms, steady_clock) so the phases of a move can be timed
+#define STEP_TRACE(...)                                                                               \
+    do {                                                                                              \
+        if (g_step_trace) {                                                                           \
+            fprintf(stderr, "[step %.3f] ", std::chrono::duration<double, std::milli>(                \
+                                                std::chrono::steady_clock::now().time_since_epoch()).count()); \
+            fprintf(stderr, __VA_ARGS__); fputc('\n', stderr); fflush(stderr);                        \
+        }                                                                                             \
     } while (0)
 
 // n simulation steps.  Step i's expansion and step i+1's selection share one launch
@@ -1260,6 +1273,7 @@ int host_threads() {
 int search_noise(az_search* s, float alpha, float eps, const uint8_t* mask) {
     const int G = s->c.n_games, A = s->t.A, NA = s->t.NA;
     if (int r = search_step(s, MODE_ROOT_NOISE)) return r;
+    STEP_TRACE("noise: root step issued");
     std::vector<int> nroot;
     if (s->t.game == GAME_GO) {        // |children| of each root (legal moves incl. pass and superko)
         nroot.resize(G);
@@ -1296,6 +1310,7 @@ int search_noise(az_search* s, float alpha, float eps, const uint8_t* mask) {
         draw(0, (int)((long)G / nt));
         for (auto& x : th) x.join();
     }
+    STEP_TRACE("noise: gamma draws done");
     bool any = false;
     for (int g = 0; g < G && !any; ++g) any = s->h_mask[g] != 0;
     if (!any) return 0;
@@ -1999,7 +2014,7 @@ int az_search_create(az_engine* e, az_net* net, const az_search_cfg* c, az_searc
 }
 
 void az_search_destroy(az_search* s) {
-    if (s) s->pc.release();
+    if (s) { s->pc.release(); s->pcf.release(); }
     if (!s) return;
     hipSetDevice(s->e->device);
     auto F = [](const void* p) { if (p) hipFree((void*)p); };
@@ -2429,6 +2444,7 @@ int az_selfplay_step(az_search* s, const az_selfplay_cfg* cfg, int64_t* moves_do
     std::vector<long long> c0((size_t)G * AZ_NCNT), c1((size_t)G * AZ_NCNT);
     if (evals_done) HIPCHK(hipMemcpy(c0.data(), s->t.cnt, c0.size() * 8, hipMemcpyDeviceToHost));
     const auto t0 = std::chrono::steady_clock::now();
+    STEP_TRACE("step start");
     if (int r = search_run(s)) return r;
     std::vector<float> temps(G);
     std::vector<int> was_active = s->active;
@@ -2480,6 +2496,7 @@ int az_selfplay_step(az_search* s, const az_selfplay_cfg* cfg, int64_t* moves_do
         for (int g = 0; g < G; ++g) ev += c1[(size_t)g * AZ_NCNT + CNT_EVALS_TOTAL] - c0[(size_t)g * AZ_NCNT + CNT_EVALS_TOTAL];
         *evals_done += ev;
     }
+    STEP_TRACE("step done");
     return 0;
 }
 
@@ -2589,12 +2606,13 @@ int az_search_profile(az_search* s, int enable) {
     HIPCHK(hipSetDevice(s->e->device));
     HIPCHK(hipStreamSynchronize(s->e->stream));
     s->prof = enable != 0;
-    if (s->prof && !s->pc.d && hipMalloc((void**)&s->pc.d, ProfClock::CAP * 8) != hipSuccess) {
-        s->pc.d = nullptr;
-        return az_fail(AZ_ERR_OOM, "profile clock buffer");
-    }
-    s->pc.used = 0;
-    s->prof_steps = 0; s->prof_sampled = 0;
+    for (ProfClock* pc : {&s->pc, &s->pcf})
+        if (s->prof && !pc->d && hipMalloc((void**)&pc->d, ProfClock::CAP * 8) != hipSuccess) {
+            pc->d = nullptr;
+            return az_fail(AZ_ERR_OOM, "profile clock buffer");
+        }
+    s->pc.used = 0; s->pcf.used = 0;
+    s->prof_steps = 0; s->prof_sampled = 0; s->prof_fused = 0; s->prof_fused_launches = 0;
     s->prof_cnt0.assign((size_t)s->c.n_games * AZ_NCNT, 0);
     HIPCHK(hipMemcpy(s->prof_cnt0.data(), s->t.cnt, s->prof_cnt0.size() * 8, hipMemcpyDeviceToHost));
     return 0;
@@ -2628,6 +2646,20 @@ int az_search_profile_read(az_search* s, double* select_ms, double* expand_ms, i
     if (sim_steps) *sim_steps = s->prof_steps;
     if (select_bytes) *select_bytes = bs;
     if (expand_bytes) *expand_bytes = be;
+    return 0;
+}
+
+int az_search_profile_read_fused(az_search* s, double* fused_ms, int64_t* fused_launches) {
+    if (!s) return az_fail(AZ_ERR_ARG, "null search");
+    std::lock_guard<std::mutex> lk(s->mu);
+    HIPCHK(hipSetDevice(s->e->device));
+    HIPCHK(hipStreamSynchronize(s->e->stream));
+    double f = 0.0;
+    const std::vector<double> t = s->pcf.read_ms();
+    for (size_t i = 0; i + 1 < t.size(); i += 2) f += t[i + 1] - t[i];
+    // sampled fused launches' time scaled to every fused launch
+    if (fused_ms) *fused_ms = s->prof_fused ? f * (double)s->prof_fused_launches / (double)s->prof_fused : 0.0;
+    if (fused_launches) *fused_launches = s->prof_fused_launches;
     return 0;
 }
 

@@ -210,6 +210,9 @@ def run_rank(a, rank, world, dist, make_workload, coll_device):
     if getattr(a, "sync_every", 0):
         from az_amd import _lib
         _lib.lib().az_diag_set_sync_every(int(a.sync_every))
+    if os.environ.get("AZ_STEP_TRACE"):      # diagnostic: timestamped phases of every selfplay step on stderr
+        from az_amd import _lib
+        _lib.lib().az_diag_set_step_trace(1)
     wl = make_workload(a, int(os.environ.get("LOCAL_RANK", "0")), sh)
     net = wl.net
     if rank == 0:
@@ -297,14 +300,23 @@ def run_rank(a, rank, world, dist, make_workload, coll_device):
                "GB_per_s": tree[f"{k}_bytes"] / max(1e-12, 1e-3 * tree[f"{k}_ms"]) / 1e9,
                "frac_of_hbm_peak": tree[f"{k}_bytes"] / max(1e-12, 1e-3 * tree[f"{k}_ms"]) / 8.0e12}
         for name, k in (("k_select", "select"), ("k_expand_backup", "expand"))}
-    out["tree_kernels"]["note"] = ("rank-0 device clock stamps around each kernel of one simulation step in 16 (those "
-                                   "steps run k_select and k_expand_backup as separate launches; the others "
-                                   "fuse step i's expansion with step i+1's selection, k_expand_select); algorithmic "
+    if tree.get("fused_launches"):
+        # the production tree step: step i's expansion + step i+1's selection in one launch
+        fb = (tree["select_bytes"] + tree["expand_bytes"]) / steps
+        fus = 1e3 * tree["fused_ms"] / tree["fused_launches"]
+        out["tree_kernels"]["k_expand_select"] = {
+            "avg_launch_us": fus, "launches": tree["fused_launches"], "bytes_per_launch": fb,
+            "GB_per_s": fb / max(1e-12, 1e-6 * fus) / 1e9, "frac_of_hbm_peak": fb / max(1e-12, 1e-6 * fus) / 8.0e12}
+    out["tree_kernels"]["note"] = ("rank-0 device clock stamps: around each kernel of one simulation step in 16 (those "
+                                   "steps run k_select and k_expand_backup as separate launches), and around one "
+                                   "launch in 16 of the fused k_expand_select that every other step runs (step i's "
+                                   "expansion with step i+1's selection: the production tree step; its bytes are "
+                                   "the two kernels' per-step bytes); algorithmic "
                                    "bytes counted by the kernels (child records scanned, path VL/backup "
                                    "read-modify-writes, new nodes, leaf planes); latency-bound (one wave per game, "
                                    "dependent tree levels), peak 8 TB/s; rocprofv3 PMC traffic of the same kernels: "
-                                   "profiles/r04_tree_pmc_c3.json (tools/tree_pmc.sh: C3's 2048 games x 800 sims, "
-                                   "2-block trunk, --sync-every 100; C2 config: profiles/r03h_tree_pmc_c2.json)")
+                                   "profiles/r05_tree_pmc_c3.json (tools/tree_pmc.sh: C3's 2048 games x 800 sims, "
+                                   "20-block trunk, --sync-every 100)")
     tr = pmc_traffic(a, kernel, boards_per_launch if launches else 0)
     if tr:
         out["roofline"].update(tr)

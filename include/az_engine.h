@@ -275,6 +275,11 @@ int az_search_counters(az_search* s, int game, int64_t* out5);
 int az_search_profile(az_search* s, int enable);
 int az_search_profile_read(az_search* s, double* select_ms, double* expand_ms, int64_t* sim_steps,
                            int64_t* select_bytes, int64_t* expand_bytes);
+/* The production tree step: simulation steps other than the sampled ones above run step i's
+ * expansion and step i+1's selection as ONE launch (k_expand_select); its summed GPU time over those
+ * launches since enable (device clock stamps around one launch in AZ_PROF_EVERY, scaled) and their
+ * count.  Measurement only, like az_search_profile_read. */
+int az_search_profile_read_fused(az_search* s, double* fused_ms, int64_t* fused_launches);
 /* Evaluation log (tests): every evaluation of game `game` appends (policy[A] post-softmax,
  * value) in evaluation order; planes too when planes != 0.  Capacity in evaluations. */
 int az_search_enable_eval_log(az_search* s, int game, int capacity);

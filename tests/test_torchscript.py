@@ -23,6 +23,10 @@ import torch
 az = pytest.importorskip("_alphazero_cpp", reason="build the host module: make -C alphazero-multi-game_amd")
 
 
+def bits(a):
+    return np.asarray(a, np.float32).view(np.uint32).tolist()
+
+
 def _module(desc, residual):
     nn = torch.nn
     F, Ci, HC, A, Hd, P = (desc.channels, desc.in_planes, desc.head_channels, desc.action_size, desc.fc_hidden,
@@ -231,3 +235,66 @@ def test_create_network_from_torchscript(tmp_path, case):
         tl, tv = m(torch.from_numpy(x))
     assert np.abs(np.asarray(pol) - net_oracle.softmax_policy(tl.numpy())).max() <= 1e-4
     assert np.abs(np.asarray(val) - tv.numpy().ravel()).max() <= 1e-4
+
+
+@pytest.mark.gpu
+def test_c1_random_model_selfplay_end_to_end(tmp_path):
+    """BASELINE.json configs[0] (C1) end to end through the reference's own entry points: a random
+    model traced to TorchScript at 9x9 (python/scripts/self_play.py:194-246: create_random_model ->
+    export_pytorch_to_libtorch -> az.createNeuralNetwork(model_path, game_type, board_size, use_gpu);
+    src/selfplay/selfplay_main.cpp:240-242 loads it the same way), played by SelfPlayManager for
+    1 game x 100 simulations (src/selfplay/self_play_manager.cpp:47-114, 151-240) with the device's
+    evaluation log on.  The game is replayed bit for bit through the CPU restatement of the
+    reference search fed with the logged network outputs (whose feature planes must equal the
+    oracle's), and the device network's raw logits / values on the logged positions are within the
+    north-star 1e-4 of the traced module itself.  The random model is the reference's plain-ResNet
+    layout (SimplifiedModel, python/simple_export.py:12-66, 128 filters x 4 blocks): the reference's
+    create_random_model builds the Python DDWRandWireResNet, whose graphs need networkx (absent from
+    the image) and whose TorchScript wiring lives in traced code, not in tensors."""
+    import az_amd
+    import az_oracle as O
+    import net_oracle
+    bs, sims = 9, 100
+    desc = az_amd.gomoku_net_desc(board_size=bs, channels=128, blocks=4, residual=1, conv_bias=1, max_batch=2048)
+    m, blob, path = _traced(tmp_path, desc, 1, seed=194, name=f"random_model_gomoku_{bs}x{bs}.pt")
+    net = az.createNeuralNetwork(path, az.GameType.GOMOKU, bs, True)
+    cap = sims * bs * bs + 256
+    mgr = az.SelfPlayManager(net, 1, sims, 1)
+    mgr.setSeeds(42, 1)
+    mgr.setEvalLog(0, cap)
+    recs = mgr.generateGames(az.GameType.GOMOKU, bs, False)
+    pol, val, planes = mgr.getEvalLog()
+    assert len(recs) == 1 and len(pol) > sims and planes.shape[1:] == (11, bs, bs)
+    moves = recs[0].getMoves()
+    k = [0]
+
+    def replay(game, x):
+        i = k[0]
+        k[0] += 1
+        assert np.array_equal(x, planes[i]), f"feature planes differ at evaluation {i}"
+        return pol[i], float(val[i])
+
+    ref = O.play(bs=bs, sims=sims, max_moves=len(moves), eval_kind=O.EVAL_REPLAY, evaluator=replay, noise_seed=42)[0]
+    assert k[0] == len(pol) and len(ref["moves"]) == len(moves)
+    for ply, (mv, r) in enumerate(zip(moves, ref["moves"])):
+        assert (mv.action, bits(mv.policy), bits([mv.value])[0]) == (r["action"], r["probs"], r["value"]), ply
+    assert int(recs[0].getResult()) == (ref["result"] if ref["terminal"] else 0)
+    # the device network (the precision createNeuralNetwork chose) against the traced module: raw outputs
+    shape, eng_blob = az.torchScriptResNet(path, az.GameType.GOMOKU, bs)
+    assert np.array_equal(eng_blob, blob)
+    idx = np.unique(np.concatenate([[0, len(pol) - 1], np.random.default_rng(3).choice(len(pol), 62, replace=False)]))
+    eng = az_amd.Engine(0)
+    d = az_amd.gomoku_net_desc(board_size=bs, channels=128, blocks=4, residual=1, conv_bias=1, max_batch=len(idx),
+                               precision=az_amd.AZ_PREC_F16X3)
+    hn = az_amd.HipNeuralNetwork(eng, d)
+    hn.load_weights(eng_blob)
+    lo, vo = hn.forward(planes[idx])
+    with torch.no_grad():
+        tl, tv = m(torch.from_numpy(np.ascontiguousarray(planes[idx])))
+    el, ev = float(np.abs(lo - tl.numpy()).max()), float(np.abs(vo - tv.numpy().ravel()).max())
+    print(f"C1: {len(moves)} moves, {len(pol)} evaluations replayed; raw outputs vs the traced module "
+          f"max|dlogit| {el:.2e} max|dvalue| {ev:.2e}; logged policy vs module softmax "
+          f"{np.abs(pol[idx] - net_oracle.softmax_policy(tl.numpy())).max():.2e}")
+    assert el <= 1e-4 and ev <= 1e-4
+    assert np.abs(pol[idx] - net_oracle.softmax_policy(tl.numpy())).max() <= 1e-4
+    hn.close()
