@@ -1464,9 +1464,10 @@ __global__ __launch_bounds__(512, 1) void conv3x3_v6(ConvBf16Args p) {
 #undef AZ_SKIP_B
 
 // fp32 NHWC [B*HW][C] -> g8 16-bit + int8 remainder (the first trunk input and residual)
+// Cout >= C (a multiple of 8): groups C/8 .. Cout/8-1 of the output are zero (channel padding)
 template <int MODE>
-__global__ void k_to_g8(const float* in, uint16_t* hi, int8_t* q, int C, int HW, const int* m_limit, int maxB) {
-    const int G = C / 8;
+__global__ void k_to_g8(const float* in, uint16_t* hi, int8_t* q, int C, int HW, const int* m_limit, int maxB, int Cout) {
+    const int G = Cout / 8, GI = C / 8;
     const int B = m_limit ? min(*m_limit, maxB) : maxB;
     const size_t total = (size_t)B * G * HW;
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
@@ -1474,9 +1475,12 @@ __global__ void k_to_g8(const float* in, uint16_t* hi, int8_t* q, int C, int HW,
         const size_t bg = i / HW;
         const int g = (int)(bg % G);
         const size_t b = bg / G;
-        const float* src = in + (b * HW + pix) * C + g * 8;
-        const float4 v0 = *reinterpret_cast<const float4*>(src);
-        const float4 v1 = *reinterpret_cast<const float4*>(src + 4);
+        float4 v0 = {0.0f, 0.0f, 0.0f, 0.0f}, v1 = v0;
+        if (g < GI) {
+            const float* src = in + (b * HW + pix) * C + g * 8;
+            v0 = *reinterpret_cast<const float4*>(src);
+            v1 = *reinterpret_cast<const float4*>(src + 4);
+        }
         const float f[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
         uint16_t h[8];
         int8_t r[8];
@@ -1525,16 +1529,18 @@ void az_launch_to_g8x3(const float* in, uint16_t* hi, uint16_t* lo, int C, int H
 }
 
 void az_launch_to_g8(const float* in, uint16_t* hi, int8_t* q, int C, int HW, const int* m_limit, int maxB, int mode,
-                     hipStream_t st) {
-    if (mode == 2) hipLaunchKernelGGL(k_to_g8<2>, dim3(2048), dim3(256), 0, st, in, hi, q, C, HW, m_limit, maxB);
-    else hipLaunchKernelGGL(k_to_g8<1>, dim3(2048), dim3(256), 0, st, in, hi, q, C, HW, m_limit, maxB);
+                     hipStream_t st, int Cout) {
+    if (Cout < C) Cout = C;
+    if (mode == 2) hipLaunchKernelGGL(k_to_g8<2>, dim3(2048), dim3(256), 0, st, in, hi, q, C, HW, m_limit, maxB, Cout);
+    else hipLaunchKernelGGL(k_to_g8<1>, dim3(2048), dim3(256), 0, st, in, hi, q, C, HW, m_limit, maxB, Cout);
 }
 
 // The search's leaf records -> the g8 16-bit input of the input conv (16 channels = two groups of 8):
 // board b's planes are built from record gidx[b] (leaf_planes.h) and rounded as k_to_g8 rounds them.
+// NG 8-channel groups per board: the 16 planes in groups 0-1, zeros in 2..NG-1 (a 32-channel input conv)
 template <int MODE>
 __global__ void k_rec_to_g8(const uint8_t* rec, const int* gidx, uint16_t* hi, int go, int bs, const int* m_limit,
-                            int maxB) {
+                            int maxB, int NG) {
     const int HW = bs * bs;
     const int B = m_limit ? min(*m_limit, maxB) : maxB;
     const size_t total = (size_t)B * HW;
@@ -1549,15 +1555,16 @@ __global__ void k_rec_to_g8(const uint8_t* rec, const int* gidx, uint16_t* hi, i
             int8_t r[8];
 #pragma unroll
             for (int e = 0; e < 8; ++e) Half16<MODE>::split(c[8 * g + e], h[e], r[e]);
-            *reinterpret_cast<uint4*>(hi + ((b * 2 + g) * HW + pix) * 8) = *reinterpret_cast<const uint4*>(h);
+            *reinterpret_cast<uint4*>(hi + ((b * NG + g) * HW + pix) * 8) = *reinterpret_cast<const uint4*>(h);
         }
+        for (int g = 2; g < NG; ++g) *reinterpret_cast<uint4*>(hi + ((b * NG + g) * HW + pix) * 8) = uint4{0, 0, 0, 0};
     }
 }
 
 void az_launch_rec_to_g8(const uint8_t* rec, const int* gidx, uint16_t* hi, int go, int bs, const int* m_limit, int maxB,
-                         int mode, hipStream_t st) {
-    if (mode == 2) hipLaunchKernelGGL(k_rec_to_g8<2>, dim3(1024), dim3(256), 0, st, rec, gidx, hi, go, bs, m_limit, maxB);
-    else hipLaunchKernelGGL(k_rec_to_g8<1>, dim3(1024), dim3(256), 0, st, rec, gidx, hi, go, bs, m_limit, maxB);
+                         int mode, hipStream_t st, int NG) {
+    if (mode == 2) hipLaunchKernelGGL(k_rec_to_g8<2>, dim3(1024), dim3(256), 0, st, rec, gidx, hi, go, bs, m_limit, maxB, NG);
+    else hipLaunchKernelGGL(k_rec_to_g8<1>, dim3(1024), dim3(256), 0, st, rec, gidx, hi, go, bs, m_limit, maxB, NG);
 }
 
 // adaptive_avg_pool2d(x, (P, P)) of an H x H g8 trunk output (16-bit + int8 remainder) -> fp32 NHWC

@@ -13,6 +13,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <functional>
+#include <future>
 #include <mutex>
 #include <sstream>
 #include <chrono>
@@ -36,7 +37,7 @@ __global__ void k_scan(const TreeDev* __restrict__ tp);
 __global__ void k_expand_backup(const TreeDev* __restrict__ tp, int mode);
 __global__ void k_select_action(const TreeDev* __restrict__ tp, int training, float temperature, const float* temps, int* actions, float* values, float* probs,
                                 int* child_actions, int* nchild);
-__global__ void k_apply(TreeDev t, const int* actions, int* terminal, int* result);
+__global__ void k_apply(TreeDev t, const int* actions, int* terminal, int* result, int* rexp);
 __global__ void k_compact(TreeDev t, Nodes dst, int* src_of);
 __global__ void k_leaf_moves(TreeDev t, int* moves, int* len);
 __global__ void k_prune(TreeDev t, Nodes dst, int* src_of, int thr_all, const int* thr_g, long long* pruned);
@@ -56,9 +57,9 @@ extern "C" int az_diag_set_conv_flags(int flags);
 bool az_conv_g8_supported(int H, int W, int C, int N);
 int az_conv_g8_launch(const ConvBf16Args& a, int mode, hipStream_t st);
 void az_launch_to_g8(const float* in, uint16_t* hi, int8_t* q, int C, int HW, const int* m_limit, int maxB, int mode,
-                     hipStream_t st);
+                     hipStream_t st, int Cout = 0);
 void az_launch_rec_to_g8(const uint8_t* rec, const int* gidx, uint16_t* hi, int go, int bs, const int* m_limit, int maxB,
-                         int mode, hipStream_t st);
+                         int mode, hipStream_t st, int NG = 2);
 void az_launch_rec_planes(const uint8_t* rec, float* dst, const int* eval_games, const int* n_eval, int go, int bs, int maxB,
                           hipStream_t st);
 void az_launch_pool_g8(const uint16_t* hi, const int8_t* q, float* out, int B, int C, int H, int P, const int* m_limit,
@@ -163,6 +164,10 @@ struct az_net {
     size_t act_elems = 0;   // elements of every 16-bit activation buffer before its zeroed tail
     size_t nparams = 0;
     Layer in, pconv, vconv, pfc, vfc1, vfc2;
+    // the input conv with its 16 input channels zero-padded to 32 (16-bit chunk-blocked copies only
+    // used): boards other than 15x15 take it on conv3x3_v6 (32-channel chunks) instead of the f32
+    // GEMM + fp32 -> g8 conversion (C4 Go, 128-board shard: ~98 -> ~15 us per forward)
+    Layer in32;
     Layer hconv;              // [pconv; vconv] as one 1x1 conv (2 HC outputs): both heads in one GEMM
     float* hpv = nullptr;     // its output [B * P * P][2 HC] (policy channels, then value)
     std::vector<Layer> blk;   // 2 per block
@@ -380,6 +385,12 @@ int net_load(az_net* n, const float* blob) {
     };
     fold_conv(pc, F, d.in_planes, 3, n->cin_pad, d.conv_bias, W, b);
     if (int r = upload_layer(n->in, W, b, F, 9 * n->cin_pad, 9, n->cin_pad, F % 32 == 0)) return r;  // 16-bit copies: g8 input conv
+    if (n->cin_pad == 16 && d.board_size != 15 && az_conv_g8_supported(d.board_size, d.board_size, F, F) &&
+        az_conv_g8_supported(d.board_size, d.board_size, 32, F)) {
+        std::vector<float> W32((size_t)F * 9 * 32, 0.0f);   // [F][9][32]: channels 16..31 zero
+        for (size_t ot = 0; ot < (size_t)F * 9; ++ot) std::copy(&W[ot * 16], &W[ot * 16] + 16, &W32[ot * 32]);
+        if (int r = upload_layer(n->in32, W32, b, F, 9 * 32, 9, 32, true)) return r;
+    }
     if (sm) sm_add(W, b, n->cin_pad);
     n->blk.resize(2 * d.blocks);
     for (int i = 0; i < 2 * d.blocks; ++i) {
@@ -645,7 +656,8 @@ int net_input_path(const az_net* n) {
     if (n->sm_W && (prec == AZ_PREC_FP16 || prec == AZ_PREC_BF16X3 || prec == AZ_PREC_F16X3) && d.blocks > 0)
         return NET_IN_SMALL;
     const bool bf = (prec == AZ_PREC_BF16 || prec == AZ_PREC_FP16) && F % 32 == 0;
-    if (bf && az_conv_g8_supported(H, H, F, F) && n->in.Wbk_h != nullptr && az_conv_g8_supported(H, H, n->cin_pad, F))
+    if (bf && az_conv_g8_supported(H, H, F, F) &&
+        ((n->in.Wbk_h != nullptr && az_conv_g8_supported(H, H, n->cin_pad, F)) || n->in32.Wbk_h != nullptr))
         return NET_IN_G8;
     return NET_IN_GEMM;
 }
@@ -810,19 +822,23 @@ int net_forward(az_net* n, const float* x0, int B, const int* nb, float* logits,
         return net_heads_fc(n, B, nb, logits, value, st);
     }
     if (inpath == NET_IN_G8) {
-        // input planes -> g8 16-bit (0/1 planes are exact), then the input conv on the g8 kernel
+        // input planes -> g8 16-bit (0/1 planes are exact), then the input conv on the g8 kernel; 16
+        // planes on a board whose g8 conv needs 32-channel chunks: zero groups 2-3 and in32
+        const bool i32 = !az_conv_g8_supported(H, W, n->cin_pad, F);
+        const Layer& IN = i32 ? n->in32 : n->in;
+        const int cin = i32 ? 32 : n->cin_pad;
         if (lr) {
             if (n->cin_pad != 16) return az_fail(AZ_ERR_ARG, "leaf records carry 16 planes");
-            az_launch_rec_to_g8(lr->rec, lr->gidx, n->th, lr->go, H, nb, B, mode, st);
+            az_launch_rec_to_g8(lr->rec, lr->gidx, n->th, lr->go, H, nb, B, mode, st, cin / 8);
         } else {
-            az_launch_to_g8(x0, n->th, nullptr, n->cin_pad, HW, nb, B, mode, st);
+            az_launch_to_g8(x0, n->th, nullptr, n->cin_pad, HW, nb, B, mode, st, cin);
         }
         ConvBf16Args a{};
         a.Ahi = n->th;
-        a.Bblk = f16 ? n->in.Wbk_h : n->in.Wbk_bf;
+        a.Bblk = f16 ? IN.Wbk_h : IN.Wbk_bf;
         a.Chi = n->hh[0]; a.Cq = hq[0];
-        a.bias = n->in.b;
-        a.M = rows; a.N = F; a.C = n->cin_pad; a.H = H; a.W = W; a.m_limit = nb; a.rows_per_sample = HW; a.relu = 1;
+        a.bias = IN.b;
+        a.M = rows; a.N = F; a.C = cin; a.H = H; a.W = W; a.m_limit = nb; a.rows_per_sample = HW; a.relu = 1;
         a.a_tail = n->act_elems * 2;          // th's zeroed tail sits behind its full capacity
         a.zero = n->zero; a.ovf = n->ovf;
         a.stamp = -1;
@@ -1018,6 +1034,25 @@ int net_heads_fc(az_net* n, int B, const int* nb, float* logits, float* value, h
 }  // namespace
 
 // ===========================================================================
+// A page-locked host buffer: per-move copies to / from it run at DMA speed (a pageable host side
+// goes through the runtime's staging buffer).  get(k) grows it to k elements (null on failure).
+template <class T>
+struct Pinned {
+    T* p = nullptr;
+    size_t n = 0;
+    T* get(size_t k) {
+        if (k > n) {
+            if (p) (void)hipHostFree(p);
+            p = nullptr; n = 0;
+            if (hipHostMalloc((void**)&p, k * sizeof(T), hipHostMallocDefault) != hipSuccess) p = nullptr;
+            else n = k;
+        }
+        return p;
+    }
+    T* data() { return p; }
+    ~Pinned() { if (p) (void)hipHostFree(p); }
+};
+
 struct az_search {
     az_engine* e = nullptr;
     az_net* net = nullptr;
@@ -1038,6 +1073,10 @@ struct az_search {
     float* d_noise = nullptr; uint8_t* d_mask = nullptr;
     int* d_actions = nullptr; float* d_values = nullptr; float* d_probs = nullptr; int* d_cact = nullptr; int* d_nch = nullptr;
     int* d_term = nullptr; int* d_res = nullptr; int* d_games = nullptr; int* d_seed_ids = nullptr;
+    int* d_rexp = nullptr;          // k_apply: per game, its new root needs no root expansion
+    // every playing game's root is expanded (or terminal): the root steps (MODE_ROOT_SEARCH /
+    // MODE_ROOT_NOISE) would select nothing, evaluate nothing and expand nothing -- skipped
+    bool roots_ready = false;
     // scratch allocated once: one game's root-children readback, per-game prune thresholds / counts
     int* d_rc = nullptr; float* d_rcf = nullptr; int* d_thr = nullptr; long long* d_pruned = nullptr;
     float* d_temps = nullptr;
@@ -1051,10 +1090,12 @@ struct az_search {
     int64_t prof_fused = 0, prof_fused_launches = 0;
     std::vector<long long> prof_cnt0;
     std::vector<std::mt19937> rng;
-    std::vector<float> h_noise; std::vector<uint8_t> h_mask;
+    Pinned<float> h_noise; std::vector<uint8_t> h_mask;   // [G][NA] Dirichlet noise (page-locked: its H2D per move)
     // az_selfplay_step's MoveData records of the last step (az_selfplay_step_moves)
-    std::vector<float> sp_probs, sp_values;
-    std::vector<int> sp_cact, sp_nch, sp_slots;
+    // page-locked (Pinned): the per-move D2H of every game's visit distribution and child actions
+    Pinned<float> sp_probs, sp_values;
+    Pinned<int> sp_cact, sp_nch;
+    std::vector<int> sp_slots;
     std::vector<az_move_rec> sp_moves;
     // device-resident copies of the TreeDev variants the per-step kernels take (tree_dev()): those
     // kernels get one 8-byte pointer instead of the ~550-byte struct by value, on ~38k dispatches per
@@ -1062,6 +1103,18 @@ struct az_search {
     TreeDev* d_tree = nullptr;
     TreeDev* h_tree = nullptr;
     int n_tree = 0, next_tree = 0;
+    // Dirichlet draws of the NEXT move, made on a host thread while the device searches this one
+    // (prefetch_noise; Gomoku self-play): per game the child count they were drawn for (-1: none)
+    // and the generator state after them, taken over only when the next noise call asks for exactly
+    // that count; otherwise discarded (the game's own rng was never touched) and drawn inline.
+    struct NoisePrefetch {
+        std::future<void> job;
+        bool on = false;
+        float alpha = 0.0f;
+        std::vector<int> nc;
+        std::vector<std::mt19937> rng;
+        std::vector<float> noise;
+    } pf;
     std::mutex mu;
 };
 
@@ -1167,6 +1220,8 @@ int host_evaluate(az_search* s) {
 int search_step(az_search* s, int mode, bool pre = false, bool fuse_next = false) {
     hipStream_t st = s->e->stream;
     const int G = s->c.n_games;
+    if (mode != MODE_SIM && s->roots_ready) return 0;   // every playing root expanded: a no-op step
+    if (mode != MODE_SIM) s->roots_ready = true;         // after it every playing root is (expanded or terminal)
     s->t.nd = s->arena[s->cur];
     const int64_t sidx = s->prof_steps;   // this simulation step's index while profiling
     const bool prof = s->prof && mode == MODE_SIM && s->prof_steps++ % prof_every() == 0 && s->pc.room(4);
@@ -1270,9 +1325,59 @@ int host_threads() {
     return n;
 }
 
+// addDirichletNoise's draws for one game (parallel_mcts.cpp:1136-1156): nc gammas of a fresh
+// libstdc++ gamma_distribution<float>(alpha) on the game's mt19937, floored and normalised
+void draw_dirichlet(std::mt19937& rng, float alpha, int nc, float* nz) {
+    std::gamma_distribution<float> gamma(alpha, 1.0f);
+    float sum = 0.0f;
+    for (int i = 0; i < nc; ++i) { nz[i] = std::max(1e-10f, gamma(rng)); sum += nz[i]; }
+    if (sum <= 0.0f) { sum = 1.0f; for (int i = 0; i < nc; ++i) nz[i] = 1.0f / (float)nc; }
+    for (int i = 0; i < nc; ++i) nz[i] /= sum;
+}
+
+// the prefetch job done (every accessor of s->rng / s->pf calls this first)
+void pf_wait(az_search* s) {
+    if (s->pf.job.valid()) s->pf.job.get();
+}
+// game g's generator changes outside the noise path (reseed, set, stochastic selectAction): its
+// prefetched draws no longer follow from it
+void pf_drop(az_search* s, int g) {
+    pf_wait(s);
+    if (s->pf.on && g >= 0 && g < (int)s->pf.nc.size()) s->pf.nc[g] = -1;
+}
+
+// Start drawing the next move's noise for the games in `want` on a host thread (Gomoku: a root
+// after one more stone has A - stones - 1 legal children).  The draws use copies of the games'
+// generators; search_noise adopts a game's copy only when it asks for that very draw.
+void prefetch_noise(az_search* s, float alpha, const std::vector<uint8_t>& want) {
+    pf_wait(s);
+    auto& P = s->pf;
+    const int G = s->c.n_games, A = s->t.A, NA = s->t.NA;
+    P.on = false;
+    if (s->t.game != GAME_GOMOKU) return;
+    P.nc.assign(G, -1);
+    P.rng.resize(G);
+    P.noise.resize((size_t)G * NA);
+    bool any = false;
+    for (int g = 0; g < G; ++g)
+        if (want[g] && s->active[g] && A - s->stones[g] - 1 > 0) { P.nc[g] = A - s->stones[g] - 1; any = true; }
+    if (!any) return;
+    P.on = true;
+    P.alpha = alpha;
+    P.job = std::async(std::launch::async, [s, alpha, G, NA] {
+        auto& Q = s->pf;
+        for (int g = 0; g < G; ++g) {
+            if (Q.nc[g] < 0) continue;
+            Q.rng[g] = s->rng[g];
+            draw_dirichlet(Q.rng[g], alpha, Q.nc[g], Q.noise.data() + (size_t)g * NA);
+        }
+    });
+}
+
 int search_noise(az_search* s, float alpha, float eps, const uint8_t* mask) {
     const int G = s->c.n_games, A = s->t.A, NA = s->t.NA;
     if (int r = search_step(s, MODE_ROOT_NOISE)) return r;
+    pf_wait(s);
     STEP_TRACE("noise: root step issued");
     std::vector<int> nroot;
     if (s->t.game == GAME_GO) {        // |children| of each root (legal moves incl. pass and superko)
@@ -1286,6 +1391,14 @@ int search_noise(az_search* s, float alpha, float eps, const uint8_t* mask) {
     // one fresh gamma_distribution per call on the game's mt19937.
     // Every game draws from its own mt19937, so the games split over host threads without changing
     // a single draw (a C2 move's 128 x 225 draws take ~6 ms on one core).
+    auto& P = s->pf;
+    const bool pfo = P.on && P.alpha == alpha;
+    int inline_games = 0;
+    for (int g = 0; g < G; ++g) {
+        if (!s->active[g] || (mask && !mask[g])) continue;
+        const int nc = !nroot.empty() ? nroot[g] : s->fresh[g] ? A : A - s->stones[g];
+        inline_games += !(pfo && nc > 0 && P.nc[g] == nc);
+    }
     auto draw = [&](int g0, int g1) {
         for (int g = g0; g < g1; ++g) {
             s->h_mask[g] = 0;
@@ -1293,15 +1406,17 @@ int search_noise(az_search* s, float alpha, float eps, const uint8_t* mask) {
             const int nc = !nroot.empty() ? nroot[g] : s->fresh[g] ? A : A - s->stones[g];
             if (nc <= 0) continue;
             float* nz = s->h_noise.data() + (size_t)g * NA;
-            std::gamma_distribution<float> gamma(alpha, 1.0f);
-            float sum = 0.0f;
-            for (int i = 0; i < nc; ++i) { nz[i] = std::max(1e-10f, gamma(s->rng[g])); sum += nz[i]; }
-            if (sum <= 0.0f) { sum = 1.0f; for (int i = 0; i < nc; ++i) nz[i] = 1.0f / (float)nc; }
-            for (int i = 0; i < nc; ++i) nz[i] /= sum;
+            if (pfo && P.nc[g] == nc) {               // drawn ahead from a copy of this very generator state
+                std::copy(P.noise.begin() + (size_t)g * NA, P.noise.begin() + (size_t)g * NA + nc, nz);
+                s->rng[g] = P.rng[g];
+            } else {
+                draw_dirichlet(s->rng[g], alpha, nc, nz);
+            }
             s->h_mask[g] = 1;
         }
     };
-    const int nt = std::max(1, std::min({host_threads(), G / 16}));
+    // host threads only for the draws still to be made (none when the prefetch covered the move)
+    const int nt = std::max(1, std::min({host_threads(), inline_games / 16}));
     if (nt == 1) {
         draw(0, G);
     } else {
@@ -1310,7 +1425,8 @@ int search_noise(az_search* s, float alpha, float eps, const uint8_t* mask) {
         draw(0, (int)((long)G / nt));
         for (auto& x : th) x.join();
     }
-    STEP_TRACE("noise: gamma draws done");
+    P.on = false;                                       // consumed (or superseded): each prefetch serves one call
+    STEP_TRACE("noise: gamma draws done (%d inline)", inline_games);
     bool any = false;
     for (int g = 0; g < G && !any; ++g) any = s->h_mask[g] != 0;
     if (!any) return 0;
@@ -1357,7 +1473,9 @@ int search_new_games(az_search* s, const int* games, int n, const int* seed_ids 
         const int g = games[i];
         s->stones[g] = 0; s->active[g] = 1; s->fresh[g] = 1; s->ply[g] = 0;
         s->hist[g].clear();
+        s->roots_ready = false;                          // a fresh root: unexpanded
         const int id = seed_ids ? seed_ids[i] : g;
+        pf_drop(s, g);
         s->rng[g].seed(s->c.noise_seed + (uint32_t)(s->c.noise_seed_stride * id));
     }
     return 0;
@@ -1389,7 +1507,7 @@ int search_apply_dev(az_search* s, int* terminal, int* result) {
     s->t.nd = s->arena[s->cur];
     std::vector<int> acts(G);
     HIPCHK(hipMemcpyAsync(acts.data(), s->d_actions, G * 4, hipMemcpyDeviceToHost, st));
-    hipLaunchKernelGGL(k_apply, dim3(G), dim3(64), 0, st, s->t, s->d_actions, s->d_term, s->d_res);
+    hipLaunchKernelGGL(k_apply, dim3(G), dim3(64), 0, st, s->t, s->d_actions, s->d_term, s->d_res, s->d_rexp);
     hipLaunchKernelGGL(k_compact, dim3(G), dim3(256), 0, st, s->t, s->arena[s->cur ^ 1], s->d_src_of);
     HIPCHK(hipGetLastError());
     s->cur ^= 1;
@@ -1397,14 +1515,19 @@ int search_apply_dev(az_search* s, int* terminal, int* result) {
     std::vector<int> term(G), res(G);
     HIPCHK(hipMemcpyAsync(term.data(), s->d_term, G * 4, hipMemcpyDeviceToHost, st));
     HIPCHK(hipMemcpyAsync(res.data(), s->d_res, G * 4, hipMemcpyDeviceToHost, st));
+    std::vector<int> rexp(G);
+    HIPCHK(hipMemcpyAsync(rexp.data(), s->d_rexp, G * 4, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
+    bool ready = true;
     for (int g = 0; g < G; ++g) {
         if (s->active[g] && acts[g] >= (s->t.game == GAME_GO ? -1 : 0)) {
             s->hist[g].push_back(acts[g]);
             s->stones[g] += 1; s->ply[g] += 1; s->fresh[g] = 0;
             if (term[g]) s->active[g] = 0;
         }
+        ready = ready && rexp[g] != 0;
     }
+    s->roots_ready = ready;
     if (terminal) std::copy(term.begin(), term.end(), terminal);
     if (result) std::copy(res.begin(), res.end(), result);
     return check_err(s);
@@ -1689,7 +1812,7 @@ void az_net_destroy(az_net* n) {
     if (!n) return;
     hipSetDevice(n->e->device);
     auto F = [](void* p) { if (p) hipFree(p); };
-    std::vector<Layer*> ls = {&n->in, &n->pconv, &n->vconv, &n->hconv, &n->pfc, &n->vfc1, &n->vfc2};
+    std::vector<Layer*> ls = {&n->in, &n->in32, &n->pconv, &n->vconv, &n->hconv, &n->pfc, &n->vfc1, &n->vfc2};
     for (auto& l : n->blk) ls.push_back(&l);
     for (auto& blk : n->rwb) {
         ls.push_back(&blk.out_router);
@@ -1952,7 +2075,7 @@ int az_search_create(az_engine* e, az_net* net, const az_search_cfg* c, az_searc
     if (c->eval_kind == AZ_EVAL_NET) SA(s->d_id, G + 1);
     if (c->eval_kind == AZ_EVAL_CALLBACK) { SA(s->d_lmoves, (size_t)G * AZ_DMAX); SA(s->d_llen, G); }
     SA(s->d_noise, (size_t)G * NA); SA(s->d_mask, G); SA(s->d_actions, G); SA(s->d_values, G); SA(s->d_probs, (size_t)G * NA);
-    SA(s->d_cact, (size_t)G * NA); SA(s->d_nch, G); SA(s->d_term, G); SA(s->d_res, G); SA(s->d_games, G); SA(s->d_seed_ids, G); SA(s->d_temps, G);
+    SA(s->d_cact, (size_t)G * NA); SA(s->d_nch, G); SA(s->d_term, G); SA(s->d_res, G); SA(s->d_rexp, G); SA(s->d_games, G); SA(s->d_seed_ids, G); SA(s->d_temps, G);
     SA(s->d_rc, 4 * (size_t)NA + 8); SA(s->d_rcf, 2 * (size_t)NA + 4); SA(s->d_thr, G); SA(s->d_pruned, G);
 #undef SA
     if (r) { az_search_destroy(s); return r; }
@@ -2007,14 +2130,15 @@ int az_search_create(az_engine* e, az_net* net, const az_search_cfg* c, az_searc
     s->stones.assign(G, 0); s->active.assign(G, 0); s->fresh.assign(G, 1); s->ply.assign(G, 0); s->expanded.assign(G, 0);
     s->rng.resize(G);
     s->hist.assign(G, {});
-    s->h_noise.assign((size_t)G * NA, 0.0f);
+    if (!s->h_noise.get((size_t)G * NA)) { az_search_destroy(s); return az_fail(AZ_ERR_OOM, "hipHostMalloc (noise)"); }
+    std::fill(s->h_noise.p, s->h_noise.p + (size_t)G * NA, 0.0f);
     s->h_mask.assign(G, 0);
     *out = s;
     return 0;
 }
 
 void az_search_destroy(az_search* s) {
-    if (s) { s->pc.release(); s->pcf.release(); }
+    if (s) { pf_wait(s); s->pc.release(); s->pcf.release(); }
     if (!s) return;
     hipSetDevice(s->e->device);
     auto F = [](const void* p) { if (p) hipFree((void*)p); };
@@ -2036,7 +2160,7 @@ void az_search_destroy(az_search* s) {
                           (const void*)s->d_src_of, (const void*)s->d_batch, (const void*)s->d_id, (const void*)s->d_logits,
                           (const void*)s->d_value, (const void*)s->d_noise, (const void*)s->d_mask, (const void*)s->d_actions,
                           (const void*)s->d_values, (const void*)s->d_probs, (const void*)s->d_cact, (const void*)s->d_nch,
-                          (const void*)s->d_term, (const void*)s->d_res, (const void*)s->d_games, (const void*)s->d_seed_ids, (const void*)s->d_temps,
+                          (const void*)s->d_term, (const void*)s->d_res, (const void*)s->d_rexp, (const void*)s->d_games, (const void*)s->d_seed_ids, (const void*)s->d_temps,
                           (const void*)s->d_rc, (const void*)s->d_rcf, (const void*)s->d_thr, (const void*)s->d_pruned,
                           (const void*)s->d_tree})
         F(p);
@@ -2138,8 +2262,11 @@ static int with_masked(az_search* s, const uint8_t* mask, const std::function<in
         now[g] = saved[g] && mask[g];
         parked |= now[g] != saved[g];
     }
+    // roots_ready speaks for the games playing when it was set: parked games may have unexpanded roots
+    s->roots_ready = false;
     if (parked) {
         s->active = now;
+        HIPCHK(hipStreamSynchronize(s->e->stream));   // no queued kernel may still read the old flags
         HIPCHK(hipMemcpy(s->t.active, now.data(), (size_t)G * 4, hipMemcpyHostToDevice));
     }
     const int r = fn();
@@ -2149,6 +2276,7 @@ static int with_masked(az_search* s, const uint8_t* mask, const std::function<in
         for (int g = 0; g < G; ++g) back[g] = mask[g] ? s->active[g] : saved[g];
         s->active = back;
         HIPCHK(hipMemcpy(s->t.active, back.data(), (size_t)G * 4, hipMemcpyHostToDevice));
+        s->roots_ready = false;
     }
     return r;
 }
@@ -2190,6 +2318,7 @@ int az_search_select_action(az_search* s, int game, int training, float temperat
     if (int r = search_select(s, training ? 1 : 0, nullptr, temperature, acts.data(), vals.data(), probs.data(), cact.data(),
                               nch.data()))
         return r;
+    pf_drop(s, game);                                // this draw moves the game's generator
     std::mt19937& rng = s->rng[game];
     const int nc = nch[game];
     if (nc == 0) {                                   // no children: a legal move (parallel_mcts.cpp:994-1010)
@@ -2339,6 +2468,7 @@ int az_search_set_params(az_search* s, const az_search_cfg* c) {
 int az_search_seed(az_search* s, int game, uint32_t seed) {
     if (!s || game < 0 || game >= s->c.n_games) return az_fail(AZ_ERR_ARG, "bad argument");
     std::lock_guard<std::mutex> lk(s->mu);
+    pf_drop(s, game);
     s->rng[game].seed(seed);
     return 0;
 }
@@ -2348,6 +2478,7 @@ int az_search_seed(az_search* s, int game, uint32_t seed) {
 int az_search_get_rng(az_search* s, int game, uint32_t* state) {
     if (!s || !state || game < 0 || game >= s->c.n_games) return az_fail(AZ_ERR_ARG, "bad argument");
     std::lock_guard<std::mutex> lk(s->mu);
+    pf_wait(s);
     std::ostringstream os;
     os << s->rng[game];
     std::istringstream is(os.str());
@@ -2364,6 +2495,7 @@ int az_search_set_rng(az_search* s, int game, const uint32_t* state) {
     std::istringstream is(os.str());
     std::mt19937 r;
     if (!(is >> r) || state[AZ_RNG_STATE_WORDS - 1] > 624) return az_fail(AZ_ERR_ARG, "rng state: not an mt19937 state");
+    pf_drop(s, game);
     s->rng[game] = r;
     return 0;
 }
@@ -2372,6 +2504,7 @@ int az_search_root_flags(az_search* s, int game, int* flags) {
     if (!s || !flags || game < 0 || game >= s->c.n_games) return az_fail(AZ_ERR_ARG, "bad argument");
     std::lock_guard<std::mutex> lk(s->mu);
     HIPCHK(hipSetDevice(s->e->device));
+    HIPCHK(hipStreamSynchronize(s->e->stream));   // its queued kernels first: the reads below are null-stream copies
     int root = 0;
     uint8_t f = 0;
     HIPCHK(hipMemcpy(&root, s->t.rnode + game, 4, hipMemcpyDeviceToHost));
@@ -2384,6 +2517,7 @@ int az_search_root_node(az_search* s, int game, int* N, int* VL, float* W) {
     if (!s || game < 0 || game >= s->c.n_games) return az_fail(AZ_ERR_ARG, "bad argument");
     std::lock_guard<std::mutex> lk(s->mu);
     HIPCHK(hipSetDevice(s->e->device));
+    HIPCHK(hipStreamSynchronize(s->e->stream));   // its queued kernels first: the reads below are null-stream copies
     int root = 0;
     HIPCHK(hipMemcpy(&root, s->t.rnode + game, 4, hipMemcpyDeviceToHost));
     const size_t off = (size_t)game * s->t.ncap + root;
@@ -2398,6 +2532,7 @@ int az_search_counters(az_search* s, int game, int64_t* out5) {
     if (!s || game < 0 || game >= s->c.n_games || !out5) return az_fail(AZ_ERR_ARG, "bad argument");
     std::lock_guard<std::mutex> lk(s->mu);
     HIPCHK(hipSetDevice(s->e->device));
+    HIPCHK(hipStreamSynchronize(s->e->stream));   // its queued kernels first: the reads below are null-stream copies
     long long c[AZ_NCNT];
     HIPCHK(hipMemcpy(c, s->t.cnt + (size_t)game * AZ_NCNT, sizeof c, hipMemcpyDeviceToHost));
     for (int i = 0; i < 5; ++i) out5[i] = c[i];
@@ -2423,6 +2558,7 @@ int az_search_read_eval_log(az_search* s, float* policy, float* value, float* pl
     if (!s || !count) return az_fail(AZ_ERR_ARG, "bad argument");
     std::lock_guard<std::mutex> lk(s->mu);
     HIPCHK(hipSetDevice(s->e->device));
+    HIPCHK(hipStreamSynchronize(s->e->stream));   // its queued kernels first: the reads below are null-stream copies
     TreeDev& t = s->t;
     if (!t.log_pol) { *count = 0; return 0; }
     int n = 0;
@@ -2442,7 +2578,12 @@ int az_selfplay_step(az_search* s, const az_selfplay_cfg* cfg, int64_t* moves_do
     HIPCHK(hipSetDevice(s->e->device));
     const int G = s->c.n_games;
     std::vector<long long> c0((size_t)G * AZ_NCNT), c1((size_t)G * AZ_NCNT);
-    if (evals_done) HIPCHK(hipMemcpy(c0.data(), s->t.cnt, c0.size() * 8, hipMemcpyDeviceToHost));
+    hipStream_t st = s->e->stream;
+    // the counters on the engine stream (a null-stream copy would not wait for its queued kernels)
+    if (evals_done) {
+        HIPCHK(hipMemcpyAsync(c0.data(), s->t.cnt, c0.size() * 8, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+    }
     const auto t0 = std::chrono::steady_clock::now();
     STEP_TRACE("step start");
     if (int r = search_run(s)) return r;
@@ -2454,11 +2595,13 @@ int az_selfplay_step(az_search* s, const az_selfplay_cfg* cfg, int64_t* moves_do
     // the same D2H and MoveData assembly as az_selfplay_run (getActionProbabilities + getRootValue
     // per game, self_play_manager.cpp:187-203); read back with az_selfplay_step_moves
     const int NA = s->t.NA;
-    s->sp_probs.resize((size_t)G * NA); s->sp_cact.resize((size_t)G * NA);
-    s->sp_values.resize(G); s->sp_nch.resize(G);
+    float* probs = s->sp_probs.get((size_t)G * NA);
+    int* cact = s->sp_cact.get((size_t)G * NA);
+    float* vals = s->sp_values.get(G);
+    int* nch = s->sp_nch.get(G);
+    if (!probs || !cact || !vals || !nch) return az_fail(AZ_ERR_OOM, "hipHostMalloc (move records)");
     STEP_TRACE("select");
-    if (int r = search_select(s, 1, temps.data(), 0.0f, actions.data(), s->sp_values.data(), s->sp_probs.data(),
-                              s->sp_cact.data(), s->sp_nch.data()))
+    if (int r = search_select(s, 1, temps.data(), 0.0f, actions.data(), vals, probs, cact, nch))
         return r;
     STEP_TRACE("apply");
     const int64_t ms = std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::steady_clock::now() - t0).count();
@@ -2472,8 +2615,7 @@ int az_selfplay_step(az_search* s, const az_selfplay_cfg* cfg, int64_t* moves_do
         if (!was_active[g] || actions[g] == none) continue;
         ++moves;
         if (ply0[g] % 2 == 0) noise_mask[g] = 1;
-        s->sp_moves.push_back(az_move_rec{actions[g], s->sp_values[g], s->sp_nch[g], s->sp_probs.data() + (size_t)g * NA,
-                                          s->sp_cact.data() + (size_t)g * NA, ms});
+        s->sp_moves.push_back(az_move_rec{actions[g], vals[g], nch[g], probs + (size_t)g * NA, cact + (size_t)g * NA, ms});
         s->sp_slots.push_back(g);
     }
     STEP_TRACE("noise");
@@ -2489,9 +2631,17 @@ int az_selfplay_step(az_search* s, const az_selfplay_cfg* cfg, int64_t* moves_do
             if (int r = search_noise(s, s->c.dirichlet_alpha, s->c.dirichlet_eps, m.data())) return r;
         }
     }
+    if (s->t.game == GAME_GOMOKU && !s->c.use_dirichlet_each_search) {
+        // the next move's noise (games whose next ply is even, self_play_manager.cpp:209-211) is drawn
+        // on a host thread while the device searches
+        std::vector<uint8_t> want(G, 0);
+        for (int g = 0; g < G; ++g) want[g] = s->active[g] && s->ply[g] % 2 == 0;
+        prefetch_noise(s, s->c.dirichlet_alpha, want);
+    }
     if (moves_done) *moves_done += moves;
     if (evals_done) {
-        HIPCHK(hipMemcpy(c1.data(), s->t.cnt, c1.size() * 8, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpyAsync(c1.data(), s->t.cnt, c1.size() * 8, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
         long long ev = 0;
         for (int g = 0; g < G; ++g) ev += c1[(size_t)g * AZ_NCNT + CNT_EVALS_TOTAL] - c0[(size_t)g * AZ_NCNT + CNT_EVALS_TOTAL];
         *evals_done += ev;
@@ -2595,7 +2745,13 @@ int az_selfplay_run(az_search* s, const az_selfplay_cfg* cfg, int total_games, i
             if (next + (int)restart.size() < total_games) restart.push_back(g);
         }
         if (int r = start(restart)) return r;
+        if (s->t.game == GAME_GOMOKU && !s->c.use_dirichlet_each_search) {   // as az_selfplay_step
+            std::vector<uint8_t> want(G, 0);
+            for (int g = 0; g < G; ++g) want[g] = s->active[g] && s->ply[g] % 2 == 0;
+            prefetch_noise(s, s->c.dirichlet_alpha, want);
+        }
     }
+    pf_wait(s);
     HIPCHK(hipStreamSynchronize(st));
     return 0;
 }

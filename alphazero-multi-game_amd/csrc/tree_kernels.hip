@@ -1315,7 +1315,8 @@ __global__ __launch_bounds__(64) void k_select_action(const TreeDev* __restrict_
 
 // updateWithMove's subtree reuse (parallel_mcts.cpp:1065-1108): the child that played `a`
 // becomes the root, else a fresh root node.  Lane 0.
-__device__ void reuse_child(const TreeDev& t, int g, const GamePtrs& nd, int a) {
+// returns the flag of the new root (0 for a fresh node)
+__device__ uint8_t reuse_child(const TreeDev& t, int g, const GamePtrs& nd, int a) {
     const int root = t.rnode[g];
     const int fc = nd.first[root], nc = nd.cnt[root];
     int child = -1;
@@ -1326,12 +1327,17 @@ __device__ void reuse_child(const TreeDev& t, int g, const GamePtrs& nd, int a) 
         else t.atop[g] = child + 1;
         nd.N[child] = 0; nd.W[child] = 0.0f; nd.VL[child] = 0; nd.P[child] = 0.0f;
         nd.first[child] = -1; nd.act[child] = -1; nd.cnt[child] = 0; nd.flag[child] = 0;
+        t.rnode[g] = child;
+        return 0;
     }
     t.rnode[g] = child;
+    return nd.flag[child];
 }
 
 // K5: makeMove + updateWithMove; terminal test of the new root (game loop condition).
-__global__ __launch_bounds__(64) void k_apply(TreeDev t, const int* actions, int* terminal, int* result) {
+// rexp[g] (optional): 1 when the game's root after the move needs no root expansion (expanded or
+// terminal, or the game is not playing) -- the host then skips the no-op root steps
+__global__ __launch_bounds__(64) void k_apply(TreeDev t, const int* actions, int* terminal, int* result, int* rexp) {
     const int g = blockIdx.x;
     const int lane = threadIdx.x;
     __shared__ uint8_t board[AZ_MAXA];
@@ -1341,7 +1347,10 @@ __global__ __launch_bounds__(64) void k_apply(TreeDev t, const int* actions, int
     const int A = t.A;
     const bool go = t.game == GAME_GO;
     if (!t.active[g] || a < (go ? -1 : 0) || a >= A) {          // Go: -1 is the pass
-        if (lane == 0) { terminal[g] = t.active[g] ? 0 : 1; result[g] = t.gresult[g]; }
+        if (lane == 0) {
+            terminal[g] = t.active[g] ? 0 : 1; result[g] = t.gresult[g];
+            if (rexp) rexp[g] = t.active[g] ? ((game_nodes(t.nd, (size_t)g * t.ncap).flag[t.rnode[g]] & (FL_EXPANDED | FL_TERMINAL)) != 0) : 1;
+        }
         return;
     }
     GamePtrs nd = game_nodes(t.nd, (size_t)g * t.ncap);
@@ -1372,7 +1381,8 @@ __global__ __launch_bounds__(64) void k_apply(TreeDev t, const int* actions, int
             if (res != R_ONGOING) t.active[g] = 0;
             terminal[g] = res != R_ONGOING;
             result[g] = res;
-            reuse_child(t, g, nd, a);
+            const uint8_t fl = reuse_child(t, g, nd, a);
+            if (rexp) rexp[g] = res != R_ONGOING || (fl & (FL_EXPANDED | FL_TERMINAL)) != 0;
         }
         __syncthreads();
         for (int i = lane; i < A; i += 64) rb[i] = board[i];
@@ -1398,7 +1408,8 @@ __global__ __launch_bounds__(64) void k_apply(TreeDev t, const int* actions, int
         if (res != R_ONGOING) t.active[g] = 0;
         terminal[g] = res != R_ONGOING;
         result[g] = res;
-        reuse_child(t, g, nd, a);
+        const uint8_t fl = reuse_child(t, g, nd, a);
+        if (rexp) rexp[g] = res != R_ONGOING || (fl & (FL_EXPANDED | FL_TERMINAL)) != 0;
     }
 }
 

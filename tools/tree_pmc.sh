@@ -13,16 +13,17 @@ export TMPDIR=/tmp
 O=gpurun_out/${TAG:-tree}
 mkdir -p $O
 # CONFIG=c2: BASELINE configs[1] as the bench runs it (256 games, 400 sims, the 6x64 net: every
-# kernel at its own bench config); default c3 with BLOCKS (20: the PMC passes of a full 20-block move
-# crash the profiler's host thread, SIGSEGV, profiles/r03g_tree_pmc_c3_20b_crash.txt -- BLOCKS=2
-# keeps the tree kernels' config, 2048 games x 800 sims, with a shorter trunk)
-# SYNC (default 100): a host sync every SYNC simulation steps -- round 4 found that rocprofv3 --pmc
-# stalls a selfplay step whose thousands of dispatches are queued without a host synchronisation
-# (tools/r4_probe5.sh: sync every 50 / 200 passes in 2 s, none is killed at 120 s)
+# kernel at its own bench config); default c3 with BLOCKS (default 20, the bench's net)
+# SYNC (default 10): a host sync every SYNC simulation steps.  rocprofv3 --pmc stalls (round 4) or
+# crashes in its own thread (SIGSEGV at a page-aligned address, rounds 3-5) when a selfplay move
+# queues thousands of dispatches without a host synchronisation: BLOCKS=2 passes at SYNC=100 (~600
+# queued dispatches), BLOCKS=20 crashes at SYNC=100 (~4,300: 41 per simulation step) with the 560-byte
+# TreeDev kernargs (r04) and with the round-5 8-byte device-resident TreeDev alike -- so not the
+# kernarg size -- and passes at SYNC=10 (~430; profiles/r05_tree_pmc_c3.json)
 if [ "${CONFIG:-c3}" = c2 ]; then
-  CMD="python3 bench.py --config c2 --cpu-baseline 0 --parity-steps 0 --steps 1 --warmup 0 --sync-every ${SYNC:-100}"
+  CMD="python3 bench.py --config c2 --cpu-baseline 0 --parity-steps 0 --steps 1 --warmup 0 --sync-every ${SYNC:-10}"
 else
-  CMD="python3 bench.py --cpu-baseline 0 --parity-steps 0 --steps 1 --warmup 0 --sims ${SIMS:-800} --blocks ${BLOCKS:-20} --sync-every ${SYNC:-100}"
+  CMD="python3 bench.py --cpu-baseline 0 --parity-steps 0 --steps 1 --warmup 0 --sims ${SIMS:-800} --blocks ${BLOCKS:-20} --sync-every ${SYNC:-10}"
 fi
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o run -- $CMD > $O/trace.log 2>&1 || { echo FAIL trace; tail -3 $O/trace.log; exit 1; }
 ( while sleep 30; do echo "pmc pass running ($(date +%T))"; done ) &
