@@ -120,6 +120,12 @@ __device__ __forceinline__ int lane_bcast(int v, int src) {
 __device__ __forceinline__ float lane_bcast(float v, int src) {
     return __int_as_float(lane_bcast(__float_as_int(v), src));
 }
+// lane src's 64-bit value as a wave-uniform (scalar) value; src wave-uniform
+__device__ __forceinline__ uint64_t lane_read64(uint64_t v, int src) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, src);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), src);
+    return ((uint64_t)hi << 32) | lo;
+}
 
 // inclusive prefix sum across the wave
 __device__ __forceinline__ int wave_incl_scan(int v, int lane) {
@@ -287,10 +293,11 @@ __device__ void write_leafrec(const TreeDev& t, int g, int lane, const uint8_t* 
 struct GoLds {
     int16_t list[AZ_MAXA];       // BFS list / stack
     int16_t mark[AZ_MAXA];       // visit stamps
-    int16_t gid[AZ_MAXA];        // group id of every stone (-1 empty)
-    int16_t glib[AZ_MAXA];       // distinct liberties of group id
+    int16_t gid[AZ_MAXA];        // group label of every stone: the group's smallest point (-1 empty)
+    int glib[AZ_MAXA];           // distinct liberties of the group labelled l
     uint64_t gxor[AZ_MAXA];      // XOR of the group's piece keys
     uint64_t phist[AZ_DMAX];     // position hashes pushed along the selection path
+    uint64_t pkey[AZ_DMAX];      // piece key of the stone path move i places (go_build_leaf prefetch)
     int nph, stamp;
 };
 
@@ -313,12 +320,14 @@ __device__ void go_clear_marks(GoLds& L, int A, int lane) {
 // makeMove (go_state.cpp:192-257) on lane 0: place, remove libertyless opponent groups (only
 // groups adjacent to the new stone can have none), ko point, stones hash.  Returns 1 when the
 // move pushes a position (stone moves), 0 for a pass.
-__device__ int go_play_seq(const TreeDev& t, uint8_t* b, GoLds& L, int a, int p, int& ko, int& passes, uint64_t& bh) {
+// key (optional): the placed stone's piece key, already loaded (go_build_leaf prefetches a path's keys)
+__device__ int go_play_seq(const TreeDev& t, uint8_t* b, GoLds& L, int a, int p, int& ko, int& passes, uint64_t& bh,
+                           const uint64_t* key = nullptr) {
     const int bs = t.bs, A = t.A;
     if (a < 0) { ++passes; ko = -1; return 0; }
     passes = 0;
     b[a] = (uint8_t)p;
-    bh ^= t.zpiece[(size_t)(p - 1) * A + a];
+    bh ^= key ? *key : t.zpiece[(size_t)(p - 1) * A + a];
     const int opp = 3 - p;
     int ngroups = 0, nstones = 0, last = -1;
     int nb[4];
@@ -363,35 +372,50 @@ __device__ __forceinline__ uint64_t go_hash(const TreeDev& t, uint64_t bh, int p
     return h ^ t.zconst;
 }
 
-// Every group of the board: id, distinct liberties, piece-key XOR (lane 0, then visible to all).
-__device__ void go_groups(const TreeDev& t, const uint8_t* b, GoLds& L, int lane) {
+// Every group of the board (visible to all threads after the call): label gid = the group's
+// smallest point index (-1 on empty points), glib[label] its distinct liberties, gxor[label] the XOR
+// of its piece keys.  Thread-parallel over the points (tid of nthr): min-label propagation with
+// pointer jumping over same-colour neighbours until no label moves, then one liberty per (empty
+// point, adjacent group) pair and one key per stone -- integers, so the same results as a
+// sequential flood fill (which held the lane-0 chain of dependent LDS / L2 accesses here).
+__device__ void go_groups(const TreeDev& t, const uint8_t* b, GoLds& L, int tid, int nthr) {
     const int bs = t.bs, A = t.A;
-    for (int a = lane; a < A; a += 64) L.gid[a] = -1;
+    for (int a = tid; a < A; a += nthr) {
+        L.gid[a] = b[a] ? (int16_t)a : (int16_t)-1;
+        L.glib[a] = 0;
+        L.gxor[a] = 0;
+    }
     __syncthreads();
-    if (lane == 0) {
-        int ng = 0;
-        for (int p0 = 0; p0 < A; ++p0) {
-            const int c = b[p0];
-            if (c == 0 || L.gid[p0] >= 0) continue;
-            const int st = ++L.stamp;
-            int n = 0, libs = 0;
-            uint64_t x = 0;
-            L.list[n++] = (int16_t)p0;
-            L.gid[p0] = (int16_t)ng;
-            for (int i = 0; i < n; ++i) {
-                const int s0 = L.list[i];
-                x ^= t.zpiece[(size_t)(c - 1) * A + s0];
-                int nb[4];
-                const int k = go_adj(s0, bs, A, nb);
-                for (int q = 0; q < k; ++q) {
-                    const int e = nb[q];
-                    if (b[e] == 0) { if (L.mark[e] != st) { L.mark[e] = (int16_t)st; ++libs; } }
-                    else if (b[e] == c && L.gid[e] < 0) { L.gid[e] = (int16_t)ng; L.list[n++] = (int16_t)e; }
-                }
-            }
-            L.glib[ng] = (int16_t)libs;
-            L.gxor[ng] = x;
-            ++ng;
+    for (;;) {
+        bool moved = false;
+        for (int a = tid; a < A; a += nthr) {
+            const int c = b[a];
+            if (!c) continue;
+            int m = L.gid[a];
+            int nb[4];
+            const int k = go_adj(a, bs, A, nb);
+            for (int q = 0; q < k; ++q)
+                if (b[nb[q]] == c) m = min(m, (int)L.gid[nb[q]]);
+            m = min(m, (int)L.gid[m]);                    // jump to the label's own label
+            if (m < L.gid[a]) { L.gid[a] = (int16_t)m; moved = true; }
+        }
+        if (!__syncthreads_or(moved)) break;
+    }
+    for (int a = tid; a < A; a += nthr) {
+        const int c = b[a];
+        if (c) {
+            atomicXor(reinterpret_cast<unsigned long long*>(&L.gxor[L.gid[a]]),
+                      (unsigned long long)t.zpiece[(size_t)(c - 1) * A + a]);
+            continue;
+        }
+        int nb[4], seen[4], ns = 0;
+        const int k = go_adj(a, bs, A, nb);
+        for (int q = 0; q < k; ++q) {
+            if (!b[nb[q]]) continue;
+            const int gl = L.gid[nb[q]];
+            bool dup = false;
+            for (int r = 0; r < ns; ++r) dup |= seen[r] == gl;
+            if (!dup) { seen[ns++] = gl; atomicAdd(&L.glib[gl], 1); }
         }
     }
     __syncthreads();
@@ -441,13 +465,22 @@ __device__ void go_build_leaf(const TreeDev& t, int g, int lane, const int* sact
     const uint8_t* rb = t.rboard + (size_t)g * A;
     for (int a = lane; a < A; a += 64) board[a] = rb[a];
     go_clear_marks(L, A, lane);
+    {   // the piece keys of the stones the path places, loaded lane-parallel ahead of the replay
+        const int p0 = t.rplayer[g];
+        for (int i = 1 + lane; i <= depth; i += 64) {
+            const int a = sact[i];
+            const int p = (i & 1) ? p0 : 3 - p0;
+            L.pkey[i] = a >= 0 ? t.zpiece[(size_t)(p - 1) * A + a] : 0ULL;
+        }
+    }
+    __syncthreads();
     if (lane == 0) {
         int p = t.rplayer[g], k = t.rko[g], ps = t.rpass[g];
         uint64_t h = t.rhash[g];
         int nph = 0;
         for (int i = 1; i <= depth; ++i) {
             const int a = sact[i];
-            if (go_play_seq(t, board, L, a, p, k, ps, h)) L.phist[nph++] = go_hash(t, h, p, k);
+            if (go_play_seq(t, board, L, a, p, k, ps, h, &L.pkey[i])) L.phist[nph++] = go_hash(t, h, p, k);
             p = 3 - p;
         }
         L.nph = nph;
@@ -490,9 +523,11 @@ __device__ int go_legal(const TreeDev& t, int g, int lane, const uint8_t* b, con
     const uint64_t tail = t.zplayer[player - 1] ^ (ko >= 0 ? t.zko[ko] : 0ULL) ^ t.zconst;
     if (lane == 0) legal[0] = -1;
     int n = 1;
+    const uint64_t hv0 = lane < nr ? rh[lane] : 0ULL;      // the root history's first 64 positions, one per lane
     for (int c0 = 0; c0 < A; c0 += 64) {
         const int a = c0 + lane;
         bool ok = a < A && b[a] == 0 && a != ko;
+        uint64_t hc = 0;                                    // the candidate's resulting position
         if (ok) {
             int nb[4];
             const int k = go_adj(a, bs, A, nb);
@@ -512,11 +547,18 @@ __device__ int go_legal(const TreeDev& t, int g, int lane, const uint8_t* b, con
                 }
             }
             ok = alive || nc > 0;
-            if (ok) {
-                h ^= tail;
-                for (int r = 0; r < nr && ok; ++r) ok = rh[r] != h;
-                for (int r = 0; r < L.nph && ok; ++r) ok = L.phist[r] != h;
+            hc = h ^ tail;
+        }
+        // positional superko, wave-uniform: every candidate against the root history (64 entries per
+        // coalesced load, broadcast lane by lane -- not one dependent L2 round trip per entry) and
+        // the path's pushes (LDS)
+        if (__ballot(ok)) {
+            for (int r0 = 0; r0 < nr; r0 += 64) {
+                const uint64_t hv = r0 == 0 ? hv0 : (r0 + lane < nr ? rh[r0 + lane] : 0ULL);
+                const int m = min(64, nr - r0);
+                for (int j = 0; j < m; ++j) ok = ok && lane_read64(hv, j) != hc;
             }
+            for (int r = 0; r < L.nph; ++r) ok = ok && L.phist[r] != hc;
         }
         const unsigned long long m = __ballot(ok);
         if (ok) legal[n + __popcll(m & ((1ULL << lane) - 1ULL))] = a;
@@ -794,7 +836,7 @@ __device__ __forceinline__ void select_game(const TreeDev& t, int mode, const Ro
             d_look += (mode == MODE_ROOT_SEARCH ? 1 : 2);
             tstamp(t, g, 0, 5);
             if (go) {
-                go_groups(t, board, gl, lane);
+                go_groups(t, board, gl, lane, 64);
                 go_write_leafrec(t, g, lane, board, gl, player, gko);
             } else {
                 write_leafrec(t, g, lane, board, hist6, player);
@@ -1004,7 +1046,7 @@ __device__ __forceinline__ void expand_game(const TreeDev& t, int mode, ExpLds& 
         int n = 0;
         const bool fresh = !go && (depth == 0) && rfresh;
         if (go) {
-            go_groups(t, board, gl, lane);
+            go_groups(t, board, gl, lane, 64);
             n = go_legal(t, g, lane, board, gl, player, gko, gbh, legal);
         } else if (fresh) {
             for (int i = lane; i < A; i += 64) legal[i] = t.fresh_order[i];
@@ -1692,7 +1734,7 @@ __global__ __launch_bounds__(AZ_DS_THREADS) void k_dataset_extract(DatasetDev d,
         // ---- planes of the position before move m
         if (d.game == GAME_GO) {
             go_clear_marks(L, A, lane);
-            go_groups(t, board, L, lane);
+            go_groups(t, board, L, lane, AZ_DS_THREADS);
             const float half = (float)(bs / 2);
             for (int a = lane; a < A; a += AZ_DS_THREADS) {
                 const int v = board[a];
