@@ -2060,6 +2060,7 @@ int az_search_create(az_engine* e, az_net* net, const az_search_cfg* c, az_searc
     SA(t.path, (size_t)G * AZ_DMAX); SA(t.pact, (size_t)G * AZ_DMAX); SA(t.pstat, (size_t)G * AZ_DMAX); SA(t.rhdr, G); SA(t.plen, G); SA(t.lstatus, G); SA(t.lvalue, G); SA(t.lhash, G); SA(t.ttstore, G);
     SA(t.ttref, G); SA(t.tthslot, G); SA(t.need_eval, G); SA(t.eval_slot, G); SA(t.eval_games, G); SA(t.n_eval, 1);
     SA(t.leafrec, (size_t)G * AZ_REC_BYTES);
+    if (t.game == GAME_GO) SA(t.goleaf, (size_t)G * AZ_GOLEAF_BYTES);
     SA(t.tt_hash, (size_t)G * t.tt_slots); SA(t.tt_visits, (size_t)G * t.tt_slots); SA(t.tt_value, (size_t)G * t.tt_slots);
     SA(t.tt_ref, (size_t)G * t.tt_slots);
     SA(t.ring_buf, (size_t)G * ring); SA(t.ring_cur, G); SA(t.cnt, (size_t)G * AZ_NCNT);
@@ -2150,7 +2151,7 @@ void az_search_destroy(az_search* s) {
                           (const void*)t.pstat, (const void*)t.rhdr,
                           (const void*)t.plen, (const void*)t.lstatus, (const void*)t.lvalue, (const void*)t.lhash,
                           (const void*)t.ttstore, (const void*)t.ttref, (const void*)t.tthslot, (const void*)t.need_eval,
-                          (const void*)t.eval_slot, (const void*)t.eval_games, (const void*)t.n_eval, (const void*)t.leafrec,
+                          (const void*)t.eval_slot, (const void*)t.eval_games, (const void*)t.n_eval, (const void*)t.leafrec, (const void*)t.goleaf,
                           (const void*)t.tt_hash, (const void*)t.tt_visits, (const void*)t.tt_value, (const void*)t.tt_ref,
                           (const void*)t.ring_buf, (const void*)t.ring_cur, (const void*)t.cnt, (const void*)t.zpiece,
                           (const void*)t.zplayer, (const void*)t.fresh_order, (const void*)t.mt, (const void*)t.err,

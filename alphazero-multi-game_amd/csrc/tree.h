@@ -11,6 +11,9 @@
 #define AZ_MAXNA 362         // largest action space (Go 19x19: 361 points + pass)
 #define AZ_DMAX 96           // longest selection path (root + 95 plies); overflow => AZ_ERR_CAPACITY
 #define AZ_NCNT 8            // per-game counters
+// Go leaf state (k_select -> k_expand_backup): [0, 384) board, [384, 416) int32 {player, ko, passes,
+// nph} + u64 stones hash, [416, 416 + 8 * AZ_DMAX) u64 position pushes of the path
+#define AZ_GOLEAF_BYTES (416 + 8 * AZ_DMAX)
 
 // ST_EXPANDED: the leaf is already expanded (a childless node after releaseMemory, or the depth
 // cap): TT lookup, value = getValue() on a miss; ST_EXPVAL: the same with a TT hit (value cached)
@@ -54,6 +57,8 @@ struct TreeDev {
     int* need_eval; int* eval_slot; int* eval_games; int* n_eval;
     int eval_identity;           // 1: the batch maps are the identity (eval_slot[g] == g): no slot load
     uint8_t* leafrec;            // [G][AZ_REC_BYTES] leaf records (leaf_planes.h): the planes' inputs (NET)
+    uint8_t* goleaf;             // Go: [G][AZ_GOLEAF_BYTES] the selected leaf's position (board, side to move,
+                                 // ko, passes, stones hash, the path's position pushes) for its expansion
     uint64_t* tt_hash; int* tt_visits; float* tt_value; uint64_t* tt_ref;   // [G][slots]
     float* ring_buf; uint64_t* ring_cur;                                     // [G][ring], [G]
     long long* cnt;              // [G][AZ_NCNT]

@@ -497,6 +497,44 @@ __device__ void go_build_leaf(const TreeDev& t, int g, int lane, const int* sact
     }
 }
 
+// The selected Go leaf's position for its expansion (AZ_GOLEAF_BYTES per game): the expansion reads
+// it back in one round trip instead of replaying the path's moves, captures and hashes on lane 0 a
+// second time.  go_build_leaf must have run (board, L.phist / L.nph in LDS).
+__device__ void go_store_leaf(const TreeDev& t, int g, int lane, const uint8_t* board, const GoLds& L, int player,
+                              int ko, int passes, uint64_t bh) {
+    uint8_t* dst = t.goleaf + (size_t)g * AZ_GOLEAF_BYTES;
+    for (int a = lane; a < t.A; a += 64) dst[a] = board[a];
+    const int nph = L.nph;
+    uint64_t* ph = reinterpret_cast<uint64_t*>(dst + 416);
+    for (int r = lane; r < nph; r += 64) ph[r] = L.phist[r];
+    if (lane == 0) {
+        int* meta = reinterpret_cast<int*>(dst + 384);
+        meta[0] = player; meta[1] = ko; meta[2] = passes; meta[3] = nph;
+        *reinterpret_cast<uint64_t*>(dst + 400) = bh;
+    }
+}
+// go_build_leaf's results from the stored leaf state (same values: the replay is deterministic)
+__device__ void go_load_leaf(const TreeDev& t, int g, int lane, const int* sact, int depth, uint8_t* board, GoLds& L,
+                             int* hist6, int& player, int& ko, int& passes, uint64_t& bh, uint64_t& hash) {
+    const int A = t.A;
+    const uint8_t* src = t.goleaf + (size_t)g * AZ_GOLEAF_BYTES;
+    const int* meta = reinterpret_cast<const int*>(src + 384);
+    player = meta[0]; ko = meta[1]; passes = meta[2];
+    const int nph = meta[3];
+    bh = *reinterpret_cast<const uint64_t*>(src + 400);
+    for (int a = lane; a < A; a += 64) board[a] = src[a];
+    const uint64_t* ph = reinterpret_cast<const uint64_t*>(src + 416);
+    for (int r = lane; r < nph; r += 64) L.phist[r] = ph[r];
+    go_clear_marks(L, A, lane);
+    if (lane == 0) L.nph = nph;
+    __syncthreads();
+    hash = go_hash(t, bh, player, ko);
+    for (int i = 0; i < 6; ++i) {
+        if (i < depth) hist6[i] = sact[depth - i];
+        else hist6[i] = t.rhist[g * 6 + (i - depth)];
+    }
+}
+
 // The leaf record of a Go leaf (leaf_planes.h; planes of go_state.cpp:338-420): board, side to
 // move, ko point and min(10, group liberties) per stone (go_groups() must have run).
 __device__ void go_write_leafrec(const TreeDev& t, int g, int lane, const uint8_t* b, const GoLds& L, int player, int ko) {
@@ -738,6 +776,7 @@ __device__ __forceinline__ void select_game(const TreeDev& t, int mode, const Ro
     uint64_t gbh = 0;
     if (go) {
         go_build_leaf(t, g, lane, sact, depth, board, gl, hist6, player, gko, gpass, gbh, hash);
+        go_store_leaf(t, g, lane, board, gl, player, gko, gpass, gbh);
     } else {
         // leaf board = root board + path moves (distinct cells, lane-parallel); hash = root hash ^
         // the path's piece keys ^ the side-to-move keys (build_leaf, on registers already loaded)
@@ -934,7 +973,7 @@ __global__ __launch_bounds__(1024) void k_scan(const TreeDev* __restrict__ tp) {
 // board, TT / ring / pool cursors, counters) is loaded before anything waits -- one round trip --
 // then the leaf's network outputs and the path nodes' statistics -- the second and last one.
 // The Gomoku leaf board is the root board plus the path moves (no Zobrist work: k_select stored
-// the leaf hash); Go replays its captures on lane 0 (go_build_leaf).
+// the leaf hash); a Go leaf's position comes back from the state k_select stored (go_load_leaf).
 __device__ __forceinline__ void expand_game(const TreeDev& t, int mode, ExpLds& EL, GoLds& gl, RootHint* hint = nullptr) {
     const int g = blockIdx.x;
     const int lane = threadIdx.x;
@@ -1019,9 +1058,7 @@ __device__ __forceinline__ void expand_game(const TreeDev& t, int mode, ExpLds& 
     uint64_t gbh = 0;
     if (go) {
         __syncthreads();
-        int stones;
-        go_build_leaf(t, g, lane, sact, depth, board, gl, hist6, player, gko, gpass, gbh, hash);
-        (void)stones;
+        go_load_leaf(t, g, lane, sact, depth, board, gl, hist6, player, gko, gpass, gbh, hash);
     } else {
 #pragma unroll
         for (int k = 0; k < BK; ++k) if (lane + 64 * k < A) board[lane + 64 * k] = rb[k];
