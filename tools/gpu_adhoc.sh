@@ -6,6 +6,10 @@ export TMPDIR=/tmp
 R=$PWD
 O=$R/gpurun_out/${TAG:-adhoc}
 mkdir -p $O
-TAG=${TAG:-adhoc}/t LIMIT=1000 FILES="tests/test_gpu_go.py tests/test_gpu_dataset.py tests/test_gpu_host_api.py" bash tools/gpu_tests.sh &&
-timeout -k 10 300 python3 bench.py --config c4 --global-games 128 --steps 3 --warmup 1 --cpu-baseline 0 --parity-steps 2 > $O/bench_c4_g128.json 2> $O/bench_c4_g128.err && cut -c1-200 $O/bench_c4_g128.json &&
-timeout -k 10 400 python3 bench.py --config c4 --steps 2 --warmup 1 --cpu-baseline 0 --parity-steps 1 > $O/bench_c4.json 2> $O/bench_c4.err && cut -c1-200 $O/bench_c4.json
+TAG=${TAG:-adhoc}/t LIMIT=1000 FILES="tests/test_gpu_search.py tests/test_gpu_go.py tests/test_gpu_selfplay_net.py tests/test_gpu_host_api.py tests/test_gpu_api.py tests/test_gpu_callback_eval.py tests/test_torchscript.py tests/test_gpu_randwire.py" bash tools/gpu_tests.sh &&
+for r in 1 2; do
+  for lib in build_head build; do
+    AZ_DIAG_HIP_LIB=$R/alphazero-multi-game_amd/$lib/libaz_hip.so timeout -k 10 200 python3 bench.py --config c2 --steps 4 --warmup 1 --cpu-baseline 0 --parity-steps 1 > $O/c2_$lib.$r.json 2> $O/c2_$lib.$r.err || exit 1
+    echo "$lib $r $(cut -c60-120 $O/c2_$lib.$r.json)"
+  done
+done
