@@ -176,8 +176,11 @@ struct Geom7 {
 // chunks), N % 128 == 0, a ReLU (every g8 conv has one), no fp32 output.
 // TM < 256 (DENSE, small batches): each wave owns TM / 2 rows = NI fragments (6, 4 or 2) x 64
 // channels in one or two A register sets of NA fragments; the halo is NRB pieces per group.
-template <int MODE, int HB, int GEO, int TM = 256>
-__global__ __launch_bounds__(256, 2) void conv3x3_v7(ConvBf16Args p) {
+// RG: weight-tile ring slots (4: tiles land 4 taps ahead, two blocks per CU; 3: 3 taps ahead, and
+// with TM <= 128 (LDS 48 KB, <= 168 VGPRs) THREE blocks per CU -- small batches, more resident waves
+// to hide the per-tap barrier and fragment latencies)
+template <int MODE, int HB, int GEO, int TM = 256, int RG = 4>
+__global__ __launch_bounds__(256, RG == 3 ? 3 : 2) void conv3x3_v7(ConvBf16Args p) {
     typedef H16<MODE> H;
     typedef Geom7<HB, GEO, TM> GM;
     constexpr bool DENSE = GM::DENSE, SLIM = GM::SLIM;
@@ -185,10 +188,11 @@ __global__ __launch_bounds__(256, 2) void conv3x3_v7(ConvBf16Args p) {
     constexpr int BNT = 128, WG = GM::WG, HW = GM::HW, HROWS = GM::HROWS, NRB = GM::NRB;
     constexpr int NI = TM / 32, NA = NI <= 4 ? NI : NI / 2, HALVES = NI / NA;   // fragments per wave / per A set
     static_assert(NA * HALVES == NI && NA <= 4, "fragment split");
+    static_assert(RG == 4 || (RG == 3 && TM <= 128), "ring");
     constexpr int WR = TM / 2;                            // rows per wave
     constexpr int A_BUF = 4 * HROWS * 16;                 // one chunk: [4 groups][320 rows][16 B] = 20 KB
     constexpr int B_TAP = 4 * BNT * 16;                   // one tap: [4 groups][128 ch][16 B] = 8 KB
-    constexpr int LDS = 2 * A_BUF + 4 * B_TAP;            // 72 KB
+    constexpr int LDS = 2 * A_BUF + RG * B_TAP;           // 72 KB (RG 4, TM 256); 48 KB (RG 3, TM 128)
     __shared__ __attribute__((aligned(16))) uint8_t lds[LDS];
 
     const int tid = threadIdx.x, lane = tid & 63;
@@ -284,12 +288,12 @@ __global__ __launch_bounds__(256, 2) void conv3x3_v7(ConvBf16Args p) {
         }
     }
 
-    // prologue: halo of chunk 0, weights of taps 0..3
+    // prologue: halo of chunk 0, weights of taps 0..RG-1
 #pragma unroll
     for (int j = 0; j < NRB; ++j) issueA(j, 0, 0);
 #pragma unroll
-    for (int s = 0; s < 4; ++s) issueB(s, s);
-    wait_vm(6);                                           // A(0), B(0) landed; B(1..3) may fly
+    for (int s = 0; s < RG; ++s) issueB(s, s);
+    wait_vm(2 * (RG - 1));                                // A(0), B(0) landed; B(1..RG-1) may fly
     __builtin_amdgcn_s_barrier();
 
     frag alo[4], ahi[4], bw[2][4];
@@ -344,13 +348,14 @@ __global__ __launch_bounds__(256, 2) void conv3x3_v7(ConvBf16Args p) {
     // Two chunks per iteration: 18 taps, the weight registers alternate by tap parity.  Every tap
     // issues the same DMA pieces (a halo piece at taps 0..4, two weight pieces), past the end as
     // harmless reloads into free buffers, so the vmcnt budget is a compile-time constant: the
-    // weights of tap s+1 were issued in tap s-3 (the prologue for s < 3), followed by the pieces of
-    // taps s-2 and s-1.  Fragments are read one tap ahead, past the end from free buffers.
+    // weights of tap s+1 were issued in tap s-RG+1 (the prologue for s < RG-1), followed by the
+    // pieces of the RG-2 taps after it.  Fragments are read one tap ahead, past the end from free buffers.
     for (int c2 = 0; c2 < NCH; c2 += 2) {
         static_for<0, 18>([&](auto tc18) {
             constexpr int T = decltype(tc18)::value;      // tap of the chunk pair
             constexpr int t = T % 9, cur = T & 1, nxt = cur ^ 1;
-            constexpr int allow = (t >= 2 && t - 2 < NRB ? 1 : 0) + (t >= 1 && t - 1 < NRB ? 1 : 0) + 4;
+            constexpr int allow = RG == 4 ? (t >= 2 && t - 2 < NRB ? 1 : 0) + (t >= 1 && t - 1 < NRB ? 1 : 0) + 4
+                                          : (t >= 1 && t - 1 < NRB ? 1 : 0) + 2;
             constexpr int NAF = NA * HALVES;              // activation fragment reads per tap
             const int c = c2 + T / 9;
             const int s = 9 * c + t;
@@ -362,11 +367,11 @@ __global__ __launch_bounds__(256, 2) void conv3x3_v7(ConvBf16Args p) {
             __builtin_amdgcn_s_barrier();
             __builtin_amdgcn_sched_barrier(0);
             // DMA for later taps: a halo piece of chunk c+1 at taps 0..NRB-1 (the last chunk reloads
-            // itself into the free buffer), then the weights of tap s+4 (clamped to the last tap)
+            // itself into the free buffer), then the weights of tap s+RG (clamped to the last tap)
             if constexpr (t < NRB) issueA(t, c + 1 < NCH ? c + 1 : c, (c + 1) & 1);
-            issueB(s + 4 < NS ? s + 4 : NS - 1, (s + 4) & 3);
+            issueB(s + RG < NS ? s + RG : NS - 1, (s + RG) % RG);
             // weights of tap s+1 (certified by the barrier above)
-            loadB(bw[nxt], b_lane + ((s + 1) & 3) * B_TAP);
+            loadB(bw[nxt], b_lane + ((s + 1) % RG) * B_TAP);
             __builtin_amdgcn_sched_barrier(0);
             lgkm<(HALVES - 1) * NA + 4>(alo);             // activations of tap s, low half
             maskA(alo, 0, t / 3, t % 3);
@@ -1176,22 +1181,24 @@ extern "C" int az_diag_v9_stamps(int sel, unsigned long long* st, unsigned* hw, 
 #endif
 }
 
-template <int HB, int GEO, int TM = 256>
+template <int HB, int GEO, int TM = 256, int RG = 4>
 static void v7_launch_g(const ConvBf16Args& a, int mode, hipStream_t st) {
     const int boards = a.M / (HB * HB);
     const int tiles = GEO == GEO_DENSE ? (boards * HB * HB + TM - 1) / TM : boards;
     const int grid = (tiles + 7) / 8 * 8 * (a.N / 128);   // XCD-aware tile/half mapping: whole groups of 8
-    if (mode == 2) hipLaunchKernelGGL((conv3x3_v7<2, HB, GEO, TM>), dim3(grid), dim3(256), 0, st, a);
-    else hipLaunchKernelGGL((conv3x3_v7<1, HB, GEO, TM>), dim3(grid), dim3(256), 0, st, a);
+    if (mode == 2) hipLaunchKernelGGL((conv3x3_v7<2, HB, GEO, TM, RG>), dim3(grid), dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((conv3x3_v7<1, HB, GEO, TM, RG>), dim3(grid), dim3(256), 0, st, a);
 }
 // DENSE boards: the tile rows (256 / 128 / 64) for this launch -- small batches take smaller tiles
 // so one round of blocks covers the CUs (az_conv_v7_tm; flag bits 0x70000 force 256 / 128 / 64 / 192)
 int az_conv_v7_tm(const ConvBf16Args& a);
 template <int HB>
 static void v7_launch_dense(const ConvBf16Args& a, int mode, hipStream_t st) {
+    // conv flag 0x80000: 128 / 64-row tiles on the 3-slot weight ring, three blocks per CU (A/B)
+    const bool r3 = (a.flags & 0x80000) != 0;
     switch (az_conv_v7_tm(a)) {
-        case 64: v7_launch_g<HB, GEO_DENSE, 64>(a, mode, st); break;
-        case 128: v7_launch_g<HB, GEO_DENSE, 128>(a, mode, st); break;
+        case 64: if (r3) v7_launch_g<HB, GEO_DENSE, 64, 3>(a, mode, st); else v7_launch_g<HB, GEO_DENSE, 64>(a, mode, st); break;
+        case 128: if (r3) v7_launch_g<HB, GEO_DENSE, 128, 3>(a, mode, st); else v7_launch_g<HB, GEO_DENSE, 128>(a, mode, st); break;
         case 192: v7_launch_g<HB, GEO_DENSE, 192>(a, mode, st); break;
         default: v7_launch_g<HB, GEO_DENSE, 256>(a, mode, st); break;
     }

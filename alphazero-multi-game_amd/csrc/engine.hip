@@ -609,33 +609,7 @@ static int fc_splits(int B, int K) {
 }
 
 int net_heads_fc(az_net* n, int B, const int* nb, float* logits, float* value, hipStream_t st,
-                 const float* pp = nullptr, const float* vp = nullptr, int xs = 0, bool finish = true);
-
-// The FC heads net_heads_fc launches for a net: k_fc_heads split-K partials (heads = true; x3 = the
-// split-operand kernel, pt its pieces; S slices) + k_fc_finish, or the generic split-K GEMM path
-struct FcPlan { bool heads = false, x3 = false; int pt = 0, S = 0; };
-FcPlan fc_plan(const az_net* n) {
-    const az_net_desc& d = n->d;
-    const int HK = d.head_channels * n->P2;
-    FcPlan f;
-    if (!(HK % 32 == 0 && HK % 4 == 0)) return f;
-    f.heads = true;
-    f.S = az_fc_heads_splits(d.max_batch, HK, d.action_size, d.fc_hidden);
-    // split-operand FC products at 5x the f32 MFMA rate: the throughput precisions (fp16 / bf16
-    // trunk) in bf16 pieces (~2^-16 per product; their trunk error is 30x larger), AZ_PREC_F16X3 in
-    // scaled fp16 pieces (~2^-21, as its trunk).  AZ_PREC_BF16X3 and F32 keep exact f32 products
-    // (bf16 pieces would add ~2.5e-5 at trained-scale logits).  Conv flag 0x08000000 keeps the f32
-    // k_fc_heads (A/B, diagnosis).  Below 512 boards of capacity the f32 pair is the faster one (C2,
-    // 256 boards: k_fc_heads 10.6 us vs k_fc_heads_x3 12.0 -- both latency-bound chains of L2 round
-    // trips at 0.5 GFLOP).
-    const bool fx = !(az_conv_flags() & 0x08000000) && n->fcx_hi && d.max_batch >= 512;
-    if (fx && (d.precision == AZ_PREC_FP16 || d.precision == AZ_PREC_BF16 || d.precision == AZ_PREC_F16X3)) {
-        f.pt = d.precision == AZ_PREC_F16X3 ? 2 : 1;
-        f.S = az_fc_heads_splits_x3(d.max_batch, HK, d.action_size, d.fc_hidden);
-        f.x3 = d.head_channels % 8 == 0 && (HK / f.S) % 32 == 0;   // az_launch_fc_heads' own test
-    }
-    return f;
-}
+                 const float* pp = nullptr, const float* vp = nullptr, int xs = 0);
 
 // Trunk conv i (0: first conv of a block, 1: second) of an AZ_PREC_BF16X3 / AZ_PREC_F16X3 net on the
 // g8 hi / lo planes (conv3x3_v9x3 / v7x3): input / output / residual plane pairs by ping-pong index `cur`.
@@ -797,10 +771,8 @@ static int poison_net(az_net* n, hipStream_t st, bool inputs) {
 // Forward of B samples (B = capacity; *nb = active samples, device side) from the
 // NHWC16 input x0 -> logits [B][A], value [B].  lr (optional; only where
 // net_input_path != NET_IN_GEMM): the planes come from leaf records instead of x0.
-// fold: the FC heads stop at their split-K partials (only where fc_plan(n).heads; the search's
-// expansion finishes them, TreeDev::fc_part)
 int net_forward(az_net* n, const float* x0, int B, const int* nb, float* logits, float* value, hipStream_t st,
-                const LeafRecs* lr = nullptr, bool fold = false) {
+                const LeafRecs* lr = nullptr) {
     const az_net_desc& d = n->d;
     const int H = d.board_size, W = d.board_size, HW = n->HW, F = d.channels, P = d.pool, PP = n->P2;
     const int rows = B * HW;
@@ -847,7 +819,7 @@ int net_forward(az_net* n, const float* x0, int B, const int* nb, float* logits,
         sa.stamps = az_smallnet_stamps_mode();   // diagnostic phase stamps (az_diag_set_smallnet_stamps)
         if (az_smallnet_launch(sa, B, st)) return az_fail(AZ_ERR_ARG, "smallnet: unsupported shape");
         if (sampled) n->pc.stamp(st);
-        return net_heads_fc(n, B, nb, logits, value, st, nullptr, nullptr, 0, !fold);
+        return net_heads_fc(n, B, nb, logits, value, st);
     }
     if (inpath == NET_IN_G8) {
         // input planes -> g8 16-bit (0/1 planes are exact), then the input conv on the g8 kernel; 16
@@ -1000,37 +972,46 @@ int net_forward(az_net* n, const float* x0, int B, const int* nb, float* logits,
         // both head 1x1 convs as one GEMM (2 HC outputs; every output is the same k-ordered fp32
         // chain as in two launches), read by the FC heads with a 2 HC cell stride
         az_launch_gemm_f32(gemm_args(n->hconv, n->pool, F, n->hpv, 2 * HC, nullptr, B * PP, 1, 1, nb, PP), ACT_RELU, false, st);
-        return net_heads_fc(n, B, nb, logits, value, st, n->hpv, n->hpv + HC, 2 * HC, !fold);
+        return net_heads_fc(n, B, nb, logits, value, st, n->hpv, n->hpv + HC, 2 * HC);
     }
     az_launch_gemm_f32(gemm_args(n->pconv, n->pool, F, n->pp, HC, nullptr, B * PP, 1, 1, nb, PP), ACT_RELU, false, st);
     az_launch_gemm_f32(gemm_args(n->vconv, n->pool, F, n->vp, HC, nullptr, B * PP, 1, 1, nb, PP), ACT_RELU, false, st);
-    return net_heads_fc(n, B, nb, logits, value, st, nullptr, nullptr, 0, !fold);
+    return net_heads_fc(n, B, nb, logits, value, st);
 }
 
 // The FC layers of both heads from the head feature maps pp / vp ([B][P*P][HC]; cell stride xs,
 // default HC: pp / vp may be the two halves of the combined head-conv output).
 int net_heads_fc(az_net* n, int B, const int* nb, float* logits, float* value, hipStream_t st, const float* pp,
-                 const float* vp, int xs, bool finish) {
+                 const float* vp, int xs) {
     const az_net_desc& d = n->d;
     const int PP = n->P2;
     const int HK = d.head_channels * PP;
     if (!pp) { pp = n->pp; vp = n->vp; xs = d.head_channels; }
     // Both FC heads: k_fc_heads (split-K partials of both FCs in one GEMM) + k_fc_finish (per board)
-    const FcPlan plan = fc_plan(n);
-    if (plan.heads) {
+    if (HK % 32 == 0 && HK % 4 == 0) {
         FcHeadArgs fa{};
         fa.pp = pp; fa.vp = vp; fa.hc = d.head_channels; fa.xs = xs;
         fa.Wp = n->pfc.W; fa.bp = n->pfc.b; fa.Wv1 = n->vfc1.W; fa.bv1 = n->vfc1.b; fa.wv2 = n->vfc2.W; fa.bv2 = n->vfc2.b;
         fa.logits = logits; fa.hid = n->v1; fa.value = value;
         fa.part = n->ws; fa.m_limit = nb;
         fa.B = B; fa.K = HK; fa.A = d.action_size; fa.H = d.fc_hidden;
-        fa.S = plan.S;                    // from the capacity: batch-size independent
-        if (plan.pt == 1) {
+        fa.S = az_fc_heads_splits(d.max_batch, HK, d.action_size, d.fc_hidden);   // from the capacity: batch-size independent
+        // split-operand FC products at 5x the f32 MFMA rate: the throughput precisions (fp16 / bf16
+        // trunk) in bf16 pieces (~2^-16 per product; their trunk error is 30x larger), AZ_PREC_F16X3 in
+        // scaled fp16 pieces (~2^-21, as its trunk).  AZ_PREC_BF16X3 and F32 keep exact f32 products
+        // (bf16 pieces would add ~2.5e-5 at trained-scale logits).  Conv flag 0x08000000 keeps the f32
+        // k_fc_heads (A/B, diagnosis).
+        // Below 512 boards of capacity the f32 pair is the faster one (C2, 256 boards: k_fc_heads 10.6 us
+        // vs k_fc_heads_x3 12.0 -- both latency-bound chains of L2 round trips at 0.5 GFLOP).
+        const bool fx = !(az_conv_flags() & 0x08000000) && n->fcx_hi && d.max_batch >= 512;
+        if (fx && (d.precision == AZ_PREC_FP16 || d.precision == AZ_PREC_BF16)) {
             fa.Wx_hi = n->fcx_hi; fa.Wx_lo = n->fcx_lo; fa.pt = 1;
-        } else if (plan.pt == 2) {
+            fa.S = az_fc_heads_splits_x3(d.max_batch, HK, d.action_size, d.fc_hidden);
+        } else if (fx && d.precision == AZ_PREC_F16X3) {
             fa.Wx_hi = n->fcf_hi; fa.Wx_lo = n->fcf_lo; fa.pt = 2; fa.rs = n->fcf_rs; fa.ovf = n->ovf;
+            fa.S = az_fc_heads_splits_x3(d.max_batch, HK, d.action_size, d.fc_hidden);
         }
-        az_launch_fc_heads(fa, st, finish);
+        az_launch_fc_heads(fa, st);
         HIPCHK(hipGetLastError());
         return 0;
     }
@@ -1241,25 +1222,6 @@ int search_step(az_search* s, int mode, bool pre = false, bool fuse_next = false
     const int G = s->c.n_games;
     if (mode != MODE_SIM && s->roots_ready) return 0;   // every playing root expanded: a no-op step
     if (mode != MODE_SIM) s->roots_ready = true;         // after it every playing root is (expanded or terminal)
-    // a device net with k_fc_heads: the expansion finishes the heads from their split-K partials
-    // (the search's batch is G rows; k_fc_finish is not launched)
-    bool fold = false;
-    if (s->c.eval_kind == AZ_EVAL_NET && s->net) {
-        const FcPlan fp = fc_plan(s->net);
-        fold = fp.heads;
-        TreeDev& t = s->t;
-        if (fold) {
-            const az_net_desc& nd = s->net->d;
-            t.fc_part = s->net->ws;
-            t.fc_rs = fp.x3 && fp.pt == 2 ? s->net->fcf_rs : nullptr;
-            t.fc_bp = s->net->pfc.b; t.fc_bv1 = s->net->vfc1.b; t.fc_wv2 = s->net->vfc2.W; t.fc_bv2 = s->net->vfc2.b;
-            t.fc_S = fp.S; t.fc_NTP = (nd.action_size + 63) / 64;
-            t.fc_NC = (t.fc_NTP + (nd.fc_hidden + 63) / 64) * 64;
-            t.fc_BP = (G + 63) / 64 * 64; t.fc_H = nd.fc_hidden;
-        } else {
-            t.fc_part = nullptr;
-        }
-    }
     s->t.nd = s->arena[s->cur];
     const int64_t sidx = s->prof_steps;   // this simulation step's index while profiling
     const bool prof = s->prof && mode == MODE_SIM && s->prof_steps++ % prof_every() == 0 && s->pc.room(4);
@@ -1291,8 +1253,8 @@ int search_step(az_search* s, int mode, bool pre = false, bool fuse_next = false
         if (!in_place) az_launch_rec_planes(tt.leafrec, s->d_batch, tt.eval_games, tt.n_eval, lr.go, tt.bs, G, st);
         const bool prof = s->net->prof;
         if (mode != MODE_SIM) s->net->prof = false;   // time only the simulation batches
-        int r = in_place ? net_forward(s->net, nullptr, G, tt.n_eval, s->d_logits, s->d_value, st, &lr, fold)
-                         : net_forward(s->net, s->d_batch, G, tt.n_eval, s->d_logits, s->d_value, st, nullptr, fold);
+        int r = in_place ? net_forward(s->net, nullptr, G, tt.n_eval, s->d_logits, s->d_value, st, &lr)
+                         : net_forward(s->net, s->d_batch, G, tt.n_eval, s->d_logits, s->d_value, st);
         s->net->prof = prof;
         if (r) return r;
     }

@@ -100,8 +100,7 @@ struct FcHeadArgs {
 };
 int az_fc_heads_splits(int B, int K, int A, int H);
 int az_fc_heads_splits_x3(int B, int K, int A, int H);
-// finish false: the split-K partials only (the search's expansion finishes them, tree_kernels.hip fc_fold)
-void az_launch_fc_heads(const FcHeadArgs& a, hipStream_t st, bool finish = true);
+void az_launch_fc_heads(const FcHeadArgs& a, hipStream_t st);
 void az_launch_value_head(const float* part, int splits, const float* b1, const float* w2, const float* b2, float* hid,
                           float* value, int B, int H, const int* m_limit, hipStream_t st);
 void az_launch_pool(const float* in, float* out, int B, int H, int W, int C, int P, const int* m_limit, hipStream_t st);

@@ -729,7 +729,7 @@ int az_fc_heads_splits(int B, int K, int A, int H) {
     return s;
 }
 
-void az_launch_fc_heads(const FcHeadArgs& a, hipStream_t st, bool finish) {
+void az_launch_fc_heads(const FcHeadArgs& a, hipStream_t st) {
     const int NT = (a.A + 63) / 64 + (a.H + 63) / 64, MT = (a.B + 63) / 64;
     FcHeadArgs f = a;
     if (a.Wx_hi && a.Wx_lo && a.hc % 8 == 0 && (a.K / a.S) % 32 == 0) {
@@ -740,7 +740,7 @@ void az_launch_fc_heads(const FcHeadArgs& a, hipStream_t st, bool finish) {
         hipLaunchKernelGGL(k_fc_heads, dim3(MT * NT, a.S), dim3(256), 0, st, a);
         f.rs = nullptr;                                   // unscaled f32 rows
     }
-    if (finish) hipLaunchKernelGGL(k_fc_finish, dim3(a.B), dim3(256), 0, st, f);
+    hipLaunchKernelGGL(k_fc_finish, dim3(a.B), dim3(256), 0, st, f);
 }
 
 // split-K partial sums only (p.part, p.splits): the caller reduces them

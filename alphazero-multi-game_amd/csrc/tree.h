@@ -69,12 +69,6 @@ struct TreeDev {
     int* err;                    // [1] sticky error bits
     const float* net_logits;     // [B][A] (NET) raw policy logits, by eval slot
     const float* net_value;      // [B]
-    // NET with k_fc_heads split-K heads: the expansion finishes the heads itself (k_fc_finish's
-    // arithmetic, bitwise) from the partials fc_part [S][BP][NC] instead of reading net_logits /
-    // net_value -- one launch less per simulation step (null: read net_logits / net_value)
-    const float* fc_part; const float* fc_rs; const float* fc_bp; const float* fc_bv1; const float* fc_wv2;
-    const float* fc_bv2;
-    int fc_S, fc_NC, fc_NTP, fc_BP, fc_H;
     int log_game, log_cap; float* log_pol; float* log_val; float* log_planes; int* log_n;
     int stamp_game;              // diagnostic: this game's k_select / k_expand_backup write phase stamps (-1 off)
 };

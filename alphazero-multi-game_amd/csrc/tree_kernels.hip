@@ -972,47 +972,6 @@ __global__ __launch_bounds__(1024) void k_scan(const TreeDev* __restrict__ tp) {
 // Latency layout: every per-game input (status, path, cached leaf value / hash / batch slot, root
 // board, TT / ring / pool cursors, counters) is loaded before anything waits -- one round trip --
 // then the leaf's network outputs and the path nodes' statistics -- the second and last one.
-// k_fc_finish (net_kernels.hip) for batch row `row`, folded into the expansion's wave: the policy
-// logits of the lane's columns (lane + 64k) and the value.  The same operations in the same order
-// -- slices summed from 0.0f in slice order, times the row scale (a power of two: exact) plus the
-// bias, ReLU, the value dot as fma chains per hidden index, the xor butterfly within each group of 64
-// hidden indices and the four group sums added in order -- so the outputs are bitwise k_fc_finish's.
-template <int PK>
-__device__ void fc_fold(const TreeDev& t, int row, int lane, int NA, float (&lg)[PK], float& value) {
-    const float* base = t.fc_part + (size_t)row * t.fc_NC;
-    const size_t ss = (size_t)t.fc_BP * t.fc_NC;
-    const int S = t.fc_S;
-    auto sum = [&](int col) {
-        float v[16];
-#pragma unroll
-        for (int s = 0; s < 16; ++s) v[s] = s < S ? base[s * ss + col] : 0.0f;
-        float a = 0.0f;
-#pragma unroll
-        for (int s = 0; s < 16; ++s) if (s < S) a += v[s];
-        return a;
-    };
-#pragma unroll
-    for (int k = 0; k < PK; ++k) {
-        const int n = lane + 64 * k;
-        lg[k] = n < NA ? __builtin_fmaf(sum(n), t.fc_rs ? t.fc_rs[n] : 1.0f, t.fc_bp[n]) : 0.0f;
-    }
-    const int H = t.fc_H, hc0 = t.fc_NTP * 64;
-    float wsum[4];
-#pragma unroll
-    for (int w = 0; w < 4; ++w) {
-        float d = 0.0f;
-        for (int h = 64 * w + lane; h < H; h += 256) {
-            float v = __builtin_fmaf(sum(hc0 + h), t.fc_rs ? t.fc_rs[hc0 + h] : 1.0f, t.fc_bv1[h]);
-            v = v > 0.0f ? v : 0.0f;
-            d = __builtin_fmaf(v, t.fc_wv2[h], d);
-        }
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) d += __shfl_xor(d, off);
-        wsum[w] = d;
-    }
-    value = tanhf(((wsum[0] + wsum[1]) + (wsum[2] + wsum[3])) + t.fc_bv2[0]);
-}
-
 // The Gomoku leaf board is the root board plus the path moves (no Zobrist work: k_select stored
 // the leaf hash); a Go leaf's position comes back from the state k_select stored (go_load_leaf).
 __device__ __forceinline__ void expand_game(const TreeDev& t, int mode, ExpLds& EL, GoLds& gl, RootHint* hint = nullptr) {
@@ -1056,14 +1015,10 @@ __device__ __forceinline__ void expand_game(const TreeDev& t, int mode, ExpLds& 
     float lg[PK];
     float netv = 0.0f;
     if (lg_early) {
-        if (t.fc_part && t.eval_kind == 0) {
-            fc_fold(t, g, lane, NA, lg, netv);
-        } else {
-            const float* src = t.net_logits + (size_t)g * NA;
+        const float* src = t.net_logits + (size_t)g * NA;
 #pragma unroll
-            for (int k = 0; k < PK; ++k) lg[k] = lane + 64 * k < NA ? src[lane + 64 * k] : 0.0f;
-            netv = t.net_value[g];
-        }
+        for (int k = 0; k < PK; ++k) lg[k] = lane + 64 * k < NA ? src[lane + 64 * k] : 0.0f;
+        netv = t.net_value[g];
     }
     uint8_t rb[BK];
 #pragma unroll
@@ -1088,14 +1043,10 @@ __device__ __forceinline__ void expand_game(const TreeDev& t, int mode, ExpLds& 
     // ---- round trip 2 (batches that are not the identity): the leaf's network outputs
     const bool net_in = status == ST_EVAL && (t.eval_kind == 0 || t.eval_kind == 4);
     if (net_in && !lg_early) {
-        if (t.fc_part && t.eval_kind == 0) {
-            fc_fold(t, slot, lane, NA, lg, netv);
-        } else {
-            const float* src = t.net_logits + (size_t)slot * NA;
+        const float* src = t.net_logits + (size_t)slot * NA;
 #pragma unroll
-            for (int k = 0; k < PK; ++k) lg[k] = lane + 64 * k < NA ? src[lane + 64 * k] : 0.0f;
-            netv = t.net_value[slot];
-        }
+        for (int k = 0; k < PK; ++k) lg[k] = lane + 64 * k < NA ? src[lane + 64 * k] : 0.0f;
+        netv = t.net_value[slot];
     }
     const int bN0 = ps0.x, bVL0 = ps0.y, bN1 = ps1.x, bVL1 = ps1.y;
     const float bW0 = __int_as_float(ps0.z), bW1 = __int_as_float(ps1.z);

@@ -46,6 +46,11 @@ CASES = [  # board, in_planes, actions, channels, blocks, B, flags selecting v7 
     (15, 11, 225, 256, 2, 37, 0x20a0c),   # 15x15 DENSE, 128-row tiles
     (13, 8, 170, 256, 1, 7, 0x30804),     # 13x13, 64-row tiles (a tile holds < 1 board)
     (19, 8, 362, 256, 1, 130, 0x804),     # C4 shard-sized batch, the automatic choice
+    # conv flag 0x80000: the 3-slot weight ring with three blocks per CU (128 / 64-row tiles)
+    (19, 8, 362, 256, 2, 13, 0xa0804),    # 128-row tiles, 3-slot ring
+    (8, 111, 4672, 256, 2, 33, 0xb0804),  # 8x8, 64-row tiles, 3-slot ring
+    (13, 8, 170, 256, 1, 7, 0xb0804),     # 13x13, 64-row tiles (a tile holds < 1 board), 3-slot ring
+    (19, 8, 362, 256, 1, 130, 0xa0804),   # C4 shard-sized batch, 128-row tiles, 3-slot ring
 ]
 
 

@@ -6,10 +6,8 @@ export TMPDIR=/tmp
 R=$PWD
 O=$R/gpurun_out/${TAG:-adhoc}
 mkdir -p $O
-TAG=${TAG:-adhoc}/t LIMIT=1000 FILES="tests/test_gpu_search.py tests/test_gpu_go.py tests/test_gpu_selfplay_net.py tests/test_gpu_host_api.py tests/test_gpu_api.py tests/test_gpu_callback_eval.py tests/test_torchscript.py tests/test_gpu_randwire.py" bash tools/gpu_tests.sh &&
-for r in 1 2; do
-  for lib in build_head build; do
-    AZ_DIAG_HIP_LIB=$R/alphazero-multi-game_amd/$lib/libaz_hip.so timeout -k 10 200 python3 bench.py --config c2 --steps 4 --warmup 1 --cpu-baseline 0 --parity-steps 1 > $O/c2_$lib.$r.json 2> $O/c2_$lib.$r.err || exit 1
-    echo "$lib $r $(cut -c60-120 $O/c2_$lib.$r.json)"
-  done
-done
+TAG=${TAG:-adhoc}/t LIMIT=600 FILES="tests/test_gpu_conv_v7.py" K="v7_bitwise" bash tools/gpu_tests.sh &&
+timeout -k 10 200 python3 tools/net_bench.py --game go19 --batch 128 --iters 10 --flags 0x204,0x20204,0xa0204 > $O/go19_128.txt 2>&1 && tail -4 $O/go19_128.txt &&
+timeout -k 10 200 python3 tools/net_bench.py --game go19 --batch 256 --iters 10 --flags 0x204,0x20204,0xa0204 > $O/go19_256.txt 2>&1 && tail -4 $O/go19_256.txt &&
+timeout -k 10 200 python3 tools/net_bench.py --game chess --batch 128 --iters 10 --flags 0x204,0x80204 > $O/chess_128.txt 2>&1 && tail -3 $O/chess_128.txt &&
+AZ_STAMPS_GO=1 AZ_TREE_STAMPS=77 timeout -k 10 200 python3 tools/tree_stamps.py 128 800 3 > $O/go_stamps.txt 2>&1 && cat $O/go_stamps.txt

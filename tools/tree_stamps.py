@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Phase stamps of k_select / k_expand_backup for one game (AZ_TREE_STAMPS=<game>) in the C2 workload
-(256 games, 400 sims, 6x64 fp16 net): the last simulation step of a move, in microseconds and shader
-cycles between consecutive stamps.  usage: tree_stamps.py [games] [sims] [moves]"""
+(256 games, 400 sims, 6x64 fp16 net) or Go 19x19 (AZ_STAMPS_GO=1: the C4 net shape with 2 blocks -- the
+tree phases do not depend on the trunk): the last simulation step of a move, in microseconds and
+shader cycles between consecutive stamps.  usage: tree_stamps.py [games] [sims] [moves]"""
 import ctypes
 import os
 import sys
@@ -16,9 +17,16 @@ sims = int(sys.argv[2]) if len(sys.argv) > 2 else 400
 moves = int(sys.argv[3]) if len(sys.argv) > 3 else 3
 _lib.lib().az_diag_set_tree_stamps(int(os.environ.get("AZ_TREE_STAMPS", "137")))
 eng = az_amd.Engine(0)
-net = az_amd.HipNeuralNetwork(eng, az_amd.gomoku_net_desc(board_size=15, channels=64, blocks=6, max_batch=G))
-net.init_random(1)
-m = az_amd.ParallelMCTS(eng, net=net, n_games=G, board_size=15, num_simulations=sims, evaluator=az_amd.AZ_EVAL_NET)
+if os.environ.get("AZ_STAMPS_GO"):
+    desc = az_amd.NetDesc(19, 8, 256, 2, 362, 32, 8, 256, 1, 0, az_amd.AZ_PREC_FP16, G)
+    net = az_amd.HipNeuralNetwork(eng, desc)
+    net.init_random(1)
+    m = az_amd.ParallelMCTS(eng, net=net, n_games=G, board_size=19, num_simulations=sims, evaluator=az_amd.AZ_EVAL_NET,
+                            game=az_amd.AZ_GAME_GO)
+else:
+    net = az_amd.HipNeuralNetwork(eng, az_amd.gomoku_net_desc(board_size=15, channels=64, blocks=6, max_batch=G))
+    net.init_random(1)
+    m = az_amd.ParallelMCTS(eng, net=net, n_games=G, board_size=15, num_simulations=sims, evaluator=az_amd.AZ_EVAL_NET)
 m.newGames()
 m.addDirichletNoise(0.03, 0.25)
 for _ in range(moves):
