@@ -391,6 +391,14 @@ __global__ __launch_bounds__(256, RG == 3 ? 3 : 2) void conv3x3_v7(ConvBf16Args 
             __builtin_amdgcn_sched_barrier(0);
         });
     }
+    // drain: the last tap's fragment reads (past the end) may still be in flight.  The compiler does
+    // not see them, so without the fragments as operands of the wait it reuses their registers in
+    // the epilogue, and a late LDS return overwrites a live value (seen as wrong outputs under LDS
+    // contention: three blocks per CU, tools/lds_hazards.py)
+    lgkm<0>(alo);
+    if constexpr (HALVES == 2) lgkm<0>(ahi);
+    lgkm<0>(bw[0]);
+    lgkm<0>(bw[1]);
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
 
     // epilogue, straight from the accumulators: lane holds channels 4*(l >> 4) + e of pixel l16
@@ -704,6 +712,11 @@ __global__ __launch_bounds__(256, 1) void conv3x3_v7x3(ConvBf16Args p) {
             __builtin_amdgcn_sched_barrier(0);
         });
     }
+    // drain with every fragment register as an operand (see conv3x3_v7)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) lgkm<0>(a[k >> 2][(k >> 1) & 1][k & 1]);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) lgkm<0>(bw[k >> 1][k & 1]);
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
 
     // epilogue from the accumulators: residual hi + lo joined in fp32, ReLU, split, streaming stores
@@ -1060,6 +1073,12 @@ __global__ __launch_bounds__(512, 1) void conv3x3_v9x3(ConvBf16Args p) {
                 mma_reload(aY, bh, bn, I0{});             // U3, releasing bh to tap s+1
             });
         }
+        // drain with every fragment register as an operand (see conv3x3_v7): the next tap's reads
+        // past the end are in flight, and the two row-half branches' registers merge after this
+        lgkm<0>(aX);
+        lgkm<0>(aY);
+        lgkm<0>(bh);
+        lgkm<0>(bl);
     };
     if (SKIP && wm == 1) main_loop(I1{});
     else main_loop(I0{});
@@ -1186,8 +1205,10 @@ static void v7_launch_g(const ConvBf16Args& a, int mode, hipStream_t st) {
     const int boards = a.M / (HB * HB);
     const int tiles = GEO == GEO_DENSE ? (boards * HB * HB + TM - 1) / TM : boards;
     const int grid = (tiles + 7) / 8 * 8 * (a.N / 128);   // XCD-aware tile/half mapping: whole groups of 8
-    if (mode == 2) hipLaunchKernelGGL((conv3x3_v7<2, HB, GEO, TM, RG>), dim3(grid), dim3(256), 0, st, a);
-    else hipLaunchKernelGGL((conv3x3_v7<1, HB, GEO, TM, RG>), dim3(grid), dim3(256), 0, st, a);
+    // diagnostic conv flag 0x100000: 64 KB of unused dynamic LDS per block (fewer blocks per CU)
+    const unsigned dyn = (a.flags & 0x100000) ? 65536u : 0u;
+    if (mode == 2) hipLaunchKernelGGL((conv3x3_v7<2, HB, GEO, TM, RG>), dim3(grid), dim3(256), dyn, st, a);
+    else hipLaunchKernelGGL((conv3x3_v7<1, HB, GEO, TM, RG>), dim3(grid), dim3(256), dyn, st, a);
 }
 // DENSE boards: the tile rows (256 / 128 / 64) for this launch -- small batches take smaller tiles
 // so one round of blocks covers the CUs (az_conv_v7_tm; flag bits 0x70000 force 256 / 128 / 64 / 192)

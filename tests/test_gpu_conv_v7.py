@@ -51,6 +51,14 @@ CASES = [  # board, in_planes, actions, channels, blocks, B, flags selecting v7 
     (8, 111, 4672, 256, 2, 33, 0xb0804),  # 8x8, 64-row tiles, 3-slot ring
     (13, 8, 170, 256, 1, 7, 0xb0804),     # 13x13, 64-row tiles (a tile holds < 1 board), 3-slot ring
     (19, 8, 362, 256, 1, 130, 0xa0804),   # C4 shard-sized batch, 128-row tiles, 3-slot ring
+    # several blocks per CU over several rounds (LDS contention: a fragment read still in flight at
+    # the loop exit used to land in a reused register -- tools/lds_hazards.py; these gave wrong
+    # boards or an illegal address before the drains)
+    (19, 8, 362, 256, 1, 130, 0x20804),   # 128-row tiles, two blocks per CU
+    (8, 111, 4672, 256, 1, 1024, 0x20804),  # 8x8, 128-row tiles, 1024 boards
+    (13, 8, 170, 256, 1, 400, 0x804),     # 13x13 at 400 boards: the automatic choice (128-row tiles)
+    (9, 11, 81, 256, 1, 700, 0x804),      # 9x9 at 700 boards: the automatic choice (128-row tiles)
+    (19, 8, 362, 256, 1, 400, 0x30804),   # 64-row tiles, three blocks per CU
 ]
 
 
