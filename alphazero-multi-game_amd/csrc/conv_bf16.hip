@@ -1678,6 +1678,7 @@ static void v6_launch(const ConvBf16Args& a, int mode, hipStream_t st) {
 bool az_conv_v7_supported(const ConvBf16Args& a);
 int az_conv_v7_launch(const ConvBf16Args& a, int mode, int geo15, hipStream_t st);
 int az_conv_v7_tm(const ConvBf16Args& a);
+int az_conv_v7_ring(const ConvBf16Args& a);
 
 // Which kernel az_conv_g8_launch takes for a layer (a.flags already set): 0 none (unsupported),
 // 1 conv3x3_v7 (*geo = its 15x15 tile geometry), 2 conv3x3_v6 (*geo = 1 when DENSE), 3 conv3x3_v5.
@@ -1697,8 +1698,8 @@ static int g8_choice(const ConvBf16Args& a, int* geo) {
     // Small batches on the DENSE boards (the per-rank shards of the 8-GPU C4 / C5 configs): v6's
     // 512-row tiles leave most CUs idle (C5 net, 128 boards: 32 blocks), conv3x3_v7 with 128 / 64-row
     // tiles (az_conv_v7_tm) fills them -- 128 boards of 8x8: 0.0237 vs 0.0644 ms per launch; 19x19 on
-    // 192-row tiles: 0.0700 vs 0.0747 at 128 boards, 0.1284 vs 0.1375 at 256
-    // (profiles/r04_small_batch_tiles_192.txt).  Flag 0x1000 keeps v6 (A/B).
+    // 128-row tiles with three blocks per CU: 0.0594 vs v6 0.0747 at 128 boards, 0.1106 vs 0.1375 at
+    // 256 (profiles/r04_small_batch_tiles_192.txt, r05_small_batch_ring3.txt).  Flag 0x1000 keeps v6.
     if (!(a.flags & (0x100 | 0x1000)) && a.H != 15 && boards_g8 < 1024 && az_conv_v7_supported(a)) {
         *geo = 2;
         return 1;
@@ -1754,7 +1755,9 @@ int az_conv_g8_name(const ConvBf16Args& a_in, int mode, char* out, int len) {
     switch (g8_choice(a, &geo)) {
         case 1: {
             const int g = a.H == 15 ? geo : 2, tm = g == 2 ? az_conv_v7_tm(a) : 256;
-            if (tm != 256) snprintf(out, len, "conv3x3_v7<%d, %d, %s, %d>", mode, a.H, g7[g], tm);
+            const int rg = tm != 256 ? az_conv_v7_ring(a) : 4;
+            if (rg != 4) snprintf(out, len, "conv3x3_v7<%d, %d, %s, %d, %d>", mode, a.H, g7[g], tm, rg);
+            else if (tm != 256) snprintf(out, len, "conv3x3_v7<%d, %d, %s, %d>", mode, a.H, g7[g], tm);
             else snprintf(out, len, "conv3x3_v7<%d, %d, %s>", mode, a.H, g7[g]);
             return 0;
         }

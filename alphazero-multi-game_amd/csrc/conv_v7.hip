@@ -1213,10 +1213,10 @@ static void v7_launch_g(const ConvBf16Args& a, int mode, hipStream_t st) {
 // DENSE boards: the tile rows (256 / 128 / 64) for this launch -- small batches take smaller tiles
 // so one round of blocks covers the CUs (az_conv_v7_tm; flag bits 0x70000 force 256 / 128 / 64 / 192)
 int az_conv_v7_tm(const ConvBf16Args& a);
+int az_conv_v7_ring(const ConvBf16Args& a);
 template <int HB>
 static void v7_launch_dense(const ConvBf16Args& a, int mode, hipStream_t st) {
-    // conv flag 0x80000: 128 / 64-row tiles on the 3-slot weight ring, three blocks per CU (A/B)
-    const bool r3 = (a.flags & 0x80000) != 0;
+    const bool r3 = az_conv_v7_ring(a) == 3;
     switch (az_conv_v7_tm(a)) {
         case 64: if (r3) v7_launch_g<HB, GEO_DENSE, 64, 3>(a, mode, st); else v7_launch_g<HB, GEO_DENSE, 64>(a, mode, st); break;
         case 128: if (r3) v7_launch_g<HB, GEO_DENSE, 128, 3>(a, mode, st); else v7_launch_g<HB, GEO_DENSE, 128>(a, mode, st); break;
@@ -1235,11 +1235,21 @@ int az_conv_v7_tm(const ConvBf16Args& a) {
     const int halves = a.N / 128;
     auto blocks = [&](int tm) { return ((rows + tm - 1) / tm + 7) / 8 * 8 * halves; };
     if (blocks(256) >= 1024) return 256;
-    // 19x19: 192-row tiles (128 boards: 0.0700 vs v6 0.0747 ms; 256: 0.1284 vs 0.1375 and 128-row
-    // tiles 0.1378; profiles/r04_small_batch_tiles_192.txt)
-    if (a.H == 19) return 192;
+    // 19x19: 128-row tiles on the 3-slot ring, three blocks per CU (az_conv_v7_ring): 128 boards
+    // 0.0594 ms vs 0.0620 on 192-row tiles (round 4's choice: 0.0700 vs v6 0.0747), 256 boards
+    // 0.1106 vs 0.1160 (profiles/r05_small_batch_ring3.txt)
+    if (a.H == 19) return 128;
     if (blocks(128) >= 512) return 128;
     return 64;
+}
+
+// Weight-ring slots of a DENSE conv3x3_v7 launch with tiles under 256 rows: 3 (three blocks per CU)
+// for 19x19's automatic 128-row tiles or with conv flag 0x80000, else 4 (two blocks per CU)
+int az_conv_v7_ring(const ConvBf16Args& a) {
+    const int tm = az_conv_v7_tm(a);
+    if (tm > 128) return 4;
+    if (a.flags & 0x80000) return 3;
+    return (a.H == 19 && !((a.flags >> 16) & 7)) ? 3 : 4;
 }
 
 // true when conv3x3_v7 takes this layer

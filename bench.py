@@ -95,7 +95,7 @@ def parse(argv=None):
     ap.add_argument("--cpu-window", type=float, default=20.0, help="seconds of the CPU baseline's timed window")
     ap.add_argument("--cpu-workers", type=int, default=0, help="CPU baseline processes (0: the host's CPU share, <=16)")
     ap.add_argument("--seed", type=int, default=1234)
-    ap.add_argument("--parity-steps", type=int, default=1,
+    ap.add_argument("--parity-steps", type=int, default=2,
                     help="N=1: also time this many moves of the same workload with the fp32-faithful f16x3 trunk "
                          "(the parity precision), reported as parity_mode; 0 disables")
     ap.add_argument("--parity-warmup", type=int, default=1)
@@ -316,7 +316,7 @@ def run_rank(a, rank, world, dist, make_workload, coll_device):
                                    "read-modify-writes, new nodes, leaf planes); latency-bound (one wave per game, "
                                    "dependent tree levels), peak 8 TB/s; rocprofv3 PMC traffic of the same kernels: "
                                    "profiles/r05_tree_pmc_c3.json (tools/tree_pmc.sh: C3's 2048 games x 800 sims, "
-                                   "20-block trunk, --sync-every 100)")
+                                   "20-block trunk, --sync-every 10)")
     tr = pmc_traffic(a, kernel, boards_per_launch if launches else 0)
     if tr:
         out["roofline"].update(tr)
@@ -360,11 +360,12 @@ def _same_kernel(profiled, name):
         args = [x.strip() for x in m.group(2).split(",")]
         # the split-operand kernels (v7x3 / v9x3: <board, geometry[, variant], piece type> in rocprof,
         # <board, SLIM|DENSE[, f16]> as labelled): the board; the piece type is the precision's.
-        # conv3x3_v7: <mode, board, geometry[, tile rows]>: all but the geometry
+        # conv3x3_v7: <mode, board, geometry[, tile rows[, ring slots]]> (defaults 256, 4): all but
+        # the geometry
         if m.group(1).endswith("x3"):
             return (m.group(1), args[:1])
         if m.group(1) == "conv3x3_v7":
-            return (m.group(1), args[:2] + args[3:])
+            return (m.group(1), args[:2] + args[3:] + ["256", "4"][len(args[3:]):])
         return (m.group(1), args[:-1])
     p1, p2 = parts(profiled), parts(name)
     return bool(p1 and p2 and p1 == p2)

@@ -223,6 +223,11 @@ def test_pmc_traffic_matches_each_trunk_kernel():
     assert not bench._same_kernel("void conv3x3_v7<1, 15, 1>(ConvBf16Args)", "conv3x3_v7<2, 15, SLIM>")
     assert bench._same_kernel("void conv3x3_v7<2, 8, 2, 64>(ConvBf16Args)", "conv3x3_v7<2, 8, DENSE, 64>")
     assert not bench._same_kernel("void conv3x3_v7<2, 8, 2, 64>(ConvBf16Args)", "conv3x3_v7<2, 8, DENSE, 128>")
+    # the ring-slot argument (default 4) and the tile rows (default 256) as rocprof prints them
+    assert bench._same_kernel("void conv3x3_v7<2, 15, 1, 256, 4>(ConvBf16Args)", "conv3x3_v7<2, 15, SLIM>")
+    assert bench._same_kernel("void conv3x3_v7<2, 19, 2, 128, 3>(ConvBf16Args)", "conv3x3_v7<2, 19, DENSE, 128, 3>")
+    assert not bench._same_kernel("void conv3x3_v7<2, 19, 2, 128, 4>(ConvBf16Args)", "conv3x3_v7<2, 19, DENSE, 128, 3>")
+    assert bench._same_kernel("void conv3x3_v7<2, 8, 2, 64, 4>(ConvBf16Args)", "conv3x3_v7<2, 8, DENSE, 64>")
     # the split-operand kernels: rocprof <board, geometry, variant, piece type> vs the label
     assert bench._same_kernel("void conv3x3_v9x3<15, 1, 3, 2>(ConvBf16Args)", "conv3x3_v9x3<15, SLIM, f16>")
     assert bench._same_kernel("void conv3x3_v9x3<19, 2, 3, 1>(ConvBf16Args)", "conv3x3_v9x3<19, DENSE>")

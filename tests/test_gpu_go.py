@@ -137,7 +137,7 @@ def test_gpu_go_net_selfplay_matches_oracle_replay(engine, prec):
 
 C4_REPLAYS = [  # games per GPU, the logged game, trunk precision, the trunk kernel that batch takes
     (1024, 777, "fp16", "conv3x3_v6<2, 19, DENSE>"),          # C4 on one GPU
-    (128, 77, "fp16", "conv3x3_v7<2, 19, DENSE, 192>"),       # the per-rank shard of C4 on 8 GPUs
+    (128, 77, "fp16", "conv3x3_v7<2, 19, DENSE, 128, 3>"),       # the per-rank shard of C4 on 8 GPUs
     (128, 101, "f16x3", "conv3x3_v9x3<19, DENSE, f16>"),      # the same shard in the parity precision
 ]
 

@@ -323,8 +323,8 @@ def test_gpu_c5_net_full_batch(engine):
     ((19, 8, 256, 20, 362, "bf16x3", 1024), "conv3x3_v9x3<19, DENSE>"),
     ((19, 8, 256, 20, 362, "f16x3", 1024), "conv3x3_v9x3<19, DENSE, f16>"),
     ((19, 8, 256, 20, 362, "fp16", 1024), "conv3x3_v6<2, 19, DENSE>"),   # C4
-    ((19, 8, 256, 20, 362, "fp16", 128), "conv3x3_v7<2, 19, DENSE, 192>"),   # C4 shard at N = 8: small tiles
-    ((19, 8, 256, 20, 362, "fp16", 256), "conv3x3_v7<2, 19, DENSE, 192>"),   # C4 shard at N = 4
+    ((19, 8, 256, 20, 362, "fp16", 128), "conv3x3_v7<2, 19, DENSE, 128, 3>"),   # C4 shard at N = 8: small tiles
+    ((19, 8, 256, 20, 362, "fp16", 256), "conv3x3_v7<2, 19, DENSE, 128, 3>"),   # C4 shard at N = 4
     ((8, 111, 256, 20, 4672, "fp16", 128), "conv3x3_v7<2, 8, DENSE, 64>"),   # C5 shard at N = 8
     ((8, 111, 256, 20, 4672, "fp16", 1024), "conv3x3_v6<2, 8, DENSE>"),      # C5 at N = 1
     ((15, 11, 32, 2, 225, "f32", 4), "gemm_f32"),

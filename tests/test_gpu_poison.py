@@ -21,8 +21,8 @@ CASES = [  # board, in_planes, actions, channels, blocks, B, precision, trunk ke
     (15, 11, 225, 256, 2, 256, "fp16", "conv3x3_v6<2, 15>"),
     (15, 11, 225, 256, 2, 256, "f16x3", "conv3x3_v9x3<15, SLIM, f16>"),
     (19, 8, 362, 256, 2, 1024, "fp16", "conv3x3_v6<2, 19, DENSE>"),
-    (19, 8, 362, 256, 2, 128, "fp16", "conv3x3_v7<2, 19, DENSE, 192>"),
-    (19, 8, 362, 256, 2, 130, "bf16", "conv3x3_v7<1, 19, DENSE, 192>"),
+    (19, 8, 362, 256, 2, 128, "fp16", "conv3x3_v7<2, 19, DENSE, 128, 3>"),
+    (19, 8, 362, 256, 2, 130, "bf16", "conv3x3_v7<1, 19, DENSE, 128, 3>"),
     (19, 8, 362, 256, 2, 128, "f16x3", "conv3x3_v9x3<19, DENSE, f16>"),
     (8, 111, 4672, 256, 2, 128, "fp16", "conv3x3_v7<2, 8, DENSE, 64>"),
     (8, 111, 4672, 256, 2, 128, "f16x3", "conv3x3_v9x3<8, DENSE, f16>"),

@@ -198,8 +198,8 @@ def test_gpu_trained_scale_production_batch_x3(engine, shape, B, prec):
 # small-tile conv3x3_v7 (192 / 64-row tiles); F16X3 conv3x3_v9x3 with less than one round of blocks.
 PROD_B = [("c2", 256), ("c3", 2048), ("c4", 1024), ("c5", 1024),
           ("c3", 256), ("c4", 128), ("c4", 256), ("c5", 128)]
-SHARD_KERNEL = {("c3", 256, "fp16"): "conv3x3_v6<2, 15>", ("c4", 128, "fp16"): "conv3x3_v7<2, 19, DENSE, 192>",
-                ("c4", 256, "fp16"): "conv3x3_v7<2, 19, DENSE, 192>", ("c5", 128, "fp16"): "conv3x3_v7<2, 8, DENSE, 64>",
+SHARD_KERNEL = {("c3", 256, "fp16"): "conv3x3_v6<2, 15>", ("c4", 128, "fp16"): "conv3x3_v7<2, 19, DENSE, 128, 3>",
+                ("c4", 256, "fp16"): "conv3x3_v7<2, 19, DENSE, 128, 3>", ("c5", 128, "fp16"): "conv3x3_v7<2, 8, DENSE, 64>",
                 ("c3", 256, "f16x3"): "conv3x3_v9x3<15, SLIM, f16>", ("c4", 128, "f16x3"): "conv3x3_v9x3<19, DENSE, f16>",
                 ("c5", 128, "f16x3"): "conv3x3_v9x3<8, DENSE, f16>"}
 

@@ -6,9 +6,5 @@ export TMPDIR=/tmp
 R=$PWD
 O=$R/gpurun_out/${TAG:-adhoc}
 mkdir -p $O
-TAG=${TAG:-adhoc}/t LIMIT=700 FILES="tests/test_gpu_conv_v7.py tests/test_gpu_poison.py" bash tools/gpu_tests.sh &&
-AZ_SB_FLAGS="v6=0x904,v7_128=0x20804,v7_128r3=0xa0804,v7_64=0x30804,v7_192=0x40804" \
-  timeout -k 10 120 python3 tools/sb_diag.py 130 > $O/sb19_130.txt 2>&1 &&
-timeout -k 10 200 python3 tools/net_bench.py --game go19 --batch 128 --iters 10 --flags 0x204,0x20204,0xa0204 > $O/go19_128.txt 2>&1 && tail -4 $O/go19_128.txt &&
-timeout -k 10 200 python3 tools/net_bench.py --game go19 --batch 256 --iters 10 --flags 0x204,0x20204,0xa0204 > $O/go19_256.txt 2>&1 && tail -4 $O/go19_256.txt &&
-timeout -k 10 420 python3 bench.py > $O/bench_c3.json 2> $O/bench_c3.err && tail -c 600 $O/bench_c3.json
+TAG=${TAG:-adhoc}/t LIMIT=900 SMOKE=1 bash tools/gpu_tests.sh &&
+timeout -k 10 300 python3 bench.py --config c4 --global-games 128 --cpu-baseline 0 --parity-steps 0 > $O/bench_c4_g128.json 2> $O/bench_c4_g128.err && tail -c 300 $O/bench_c4_g128.json
