@@ -1687,8 +1687,9 @@ static int g8_choice(const ConvBf16Args& a, int* geo) {
     // conv3x3_v7 (conv_v7.hip, two 256-thread blocks per CU, epilogue from registers) takes every
     // layer it supports (trunk convs: C % 64 == 0) unless flag 0x100 selects v6 (A/B measurement);
     // flag 0x200: v7 only on 15x15 boards; 15x15 tile geometry: SLIM (default), flag 8 DENSE, 0x400 PAD.
-    // Below 1024 boards a launch is one or two rounds of blocks and v6 is faster (B = 256: 61 vs 65 us);
-    // flag 0x800 forces v7 at any batch.
+    // 15x15 below 1024 boards: a launch is one or two rounds of blocks and v6 is faster (B = 256: 61
+    // vs 65 us); the other boards take v7's small DENSE tiles there (next branch).  Flag 0x800 forces
+    // v7 at any batch.
     const int boards_g8 = a.M / (a.H * a.W);
     if (!(a.flags & 0x100) && (a.H == 15 || !(a.flags & 0x200)) && (boards_g8 >= 1024 || (a.flags & 0x800)) &&
         az_conv_v7_supported(a)) {

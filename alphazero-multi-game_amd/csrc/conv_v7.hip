@@ -1244,12 +1244,16 @@ int az_conv_v7_tm(const ConvBf16Args& a) {
 }
 
 // Weight-ring slots of a DENSE conv3x3_v7 launch with tiles under 256 rows: 3 (three blocks per CU)
-// for 19x19's automatic 128-row tiles or with conv flag 0x80000, else 4 (two blocks per CU)
+// for the automatic 128-row tiles or with conv flag 0x80000, else 4 (two blocks per CU).  128-row
+// tiles, 4 -> 3 slots: 19x19 128 boards 0.0620 (192-row) -> 0.0594 ms, 13x13 256 0.0709 -> 0.0592,
+// 13x13 512 0.1230 -> 0.1092, 9x9 512 0.0700 -> 0.0578, 8x8 512 0.0444 -> 0.0436; the 64-row tiles
+// measured within +-2 % (8x8 128 0.0217 vs 0.0221, 9x9 256 0.0360 vs 0.0353) and keep 4
+// (profiles/r05_small_batch_ring3.txt)
 int az_conv_v7_ring(const ConvBf16Args& a) {
     const int tm = az_conv_v7_tm(a);
     if (tm > 128) return 4;
     if (a.flags & 0x80000) return 3;
-    return (a.H == 19 && !((a.flags >> 16) & 7)) ? 3 : 4;
+    return (tm == 128 && !((a.flags >> 16) & 7)) ? 3 : 4;
 }
 
 // true when conv3x3_v7 takes this layer
