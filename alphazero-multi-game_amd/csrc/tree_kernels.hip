@@ -372,18 +372,37 @@ __device__ __forceinline__ uint64_t go_hash(const TreeDev& t, uint64_t bh, int p
     return h ^ t.zconst;
 }
 
+// Piece keys of a wave's points (point a = lane + 64 i): of the stone on it (st) and of a stone of
+// `player` on an empty point (pl, the superko candidates) -- all loads issued at once, one L2 round
+// trip ahead of go_groups / go_legal, whose per-point loops otherwise waited for one per chunk.
+constexpr int GO_PTS = (AZ_MAXA + 63) / 64;
+struct GoKeys {
+    uint64_t st[GO_PTS], pl[GO_PTS];
+};
+__device__ __forceinline__ void go_keys(const TreeDev& t, const uint8_t* b, int player, int lane, GoKeys& K) {
+    const int A = t.A;
+#pragma unroll
+    for (int i = 0; i < GO_PTS; ++i) {
+        const int a = lane + 64 * i;
+        const int c = a < A ? b[a] : 0;
+        K.st[i] = c ? t.zpiece[(size_t)(c - 1) * A + a] : 0ULL;
+        K.pl[i] = (a < A && !c) ? t.zpiece[(size_t)(player - 1) * A + a] : 0ULL;
+    }
+}
+
 // Every group of the board (visible to all threads after the call): label gid = the group's
-// smallest point index (-1 on empty points), glib[label] its distinct liberties, gxor[label] the XOR
-// of its piece keys.  Thread-parallel over the points (tid of nthr): min-label propagation with
-// pointer jumping over same-colour neighbours until no label moves, then one liberty per (empty
-// point, adjacent group) pair and one key per stone -- integers, so the same results as a
-// sequential flood fill (which held the lane-0 chain of dependent LDS / L2 accesses here).
-__device__ void go_groups(const TreeDev& t, const uint8_t* b, GoLds& L, int tid, int nthr) {
+// smallest point index (-1 on empty points), glib[label] its distinct liberties and, with keys (one
+// wave: tid = lane, nthr = 64), gxor[label] the XOR of its piece keys.  Thread-parallel over the
+// points (tid of nthr): min-label propagation with pointer jumping over same-colour neighbours until
+// no label moves, then one liberty per (empty point, adjacent group) pair and one key per stone --
+// integers, so the same results as a sequential flood fill (which held the lane-0 chain of dependent
+// LDS / L2 accesses here).  The leaf record and the dataset planes need the liberties only.
+__device__ void go_groups(const TreeDev& t, const uint8_t* b, GoLds& L, int tid, int nthr, const GoKeys* K = nullptr) {
     const int bs = t.bs, A = t.A;
     for (int a = tid; a < A; a += nthr) {
         L.gid[a] = b[a] ? (int16_t)a : (int16_t)-1;
         L.glib[a] = 0;
-        L.gxor[a] = 0;
+        if (K) L.gxor[a] = 0;
     }
     __syncthreads();
     for (;;) {
@@ -401,13 +420,15 @@ __device__ void go_groups(const TreeDev& t, const uint8_t* b, GoLds& L, int tid,
         }
         if (!__syncthreads_or(moved)) break;
     }
-    for (int a = tid; a < A; a += nthr) {
-        const int c = b[a];
-        if (c) {
-            atomicXor(reinterpret_cast<unsigned long long*>(&L.gxor[L.gid[a]]),
-                      (unsigned long long)t.zpiece[(size_t)(c - 1) * A + a]);
-            continue;
+    if (K) {
+#pragma unroll
+        for (int i = 0; i < GO_PTS; ++i) {
+            const int a = tid + 64 * i;
+            if (a < A && b[a]) atomicXor(reinterpret_cast<unsigned long long*>(&L.gxor[L.gid[a]]), K->st[i]);
         }
+    }
+    for (int a = tid; a < A; a += nthr) {
+        if (b[a]) continue;
         int nb[4], seen[4], ns = 0;
         const int k = go_adj(a, bs, A, nb);
         for (int q = 0; q < k; ++q) {
@@ -553,7 +574,7 @@ __device__ void go_write_leafrec(const TreeDev& t, int g, int lane, const uint8_
 // (GoRules::isSuicidalMove) and whose resulting position -- same side to move, the old ko point --
 // is not in position_history_ (root history + the path's pushes).  Needs go_groups().
 __device__ int go_legal(const TreeDev& t, int g, int lane, const uint8_t* b, const GoLds& L, int player, int ko,
-                        uint64_t bh, int* legal) {
+                        uint64_t bh, int* legal, const GoKeys& K) {
     const int A = t.A, bs = t.bs;
     const int opp = 3 - player;
     const uint64_t* rh = t.rposh + (size_t)g * t.hmax;
@@ -562,7 +583,10 @@ __device__ int go_legal(const TreeDev& t, int g, int lane, const uint8_t* b, con
     if (lane == 0) legal[0] = -1;
     int n = 1;
     const uint64_t hv0 = lane < nr ? rh[lane] : 0ULL;      // the root history's first 64 positions, one per lane
-    for (int c0 = 0; c0 < A; c0 += 64) {
+#pragma unroll
+    for (int ci = 0; ci < GO_PTS; ++ci) {
+        const int c0 = 64 * ci;
+        if (c0 >= A) break;
         const int a = c0 + lane;
         bool ok = a < A && b[a] == 0 && a != ko;
         uint64_t hc = 0;                                    // the candidate's resulting position
@@ -571,7 +595,7 @@ __device__ int go_legal(const TreeDev& t, int g, int lane, const uint8_t* b, con
             const int k = go_adj(a, bs, A, nb);
             bool alive = false;
             int capg[4], nc = 0;
-            uint64_t h = bh ^ t.zpiece[(size_t)(player - 1) * A + a];
+            uint64_t h = bh ^ K.pl[ci];
             for (int q = 0; q < k; ++q) {
                 const int e = nb[q];
                 const int v = b[e];
@@ -1083,8 +1107,10 @@ __device__ __forceinline__ void expand_game(const TreeDev& t, int mode, ExpLds& 
         int n = 0;
         const bool fresh = !go && (depth == 0) && rfresh;
         if (go) {
-            go_groups(t, board, gl, lane, 64);
-            n = go_legal(t, g, lane, board, gl, player, gko, gbh, legal);
+            GoKeys gk;
+            go_keys(t, board, player, lane, gk);
+            go_groups(t, board, gl, lane, 64, &gk);
+            n = go_legal(t, g, lane, board, gl, player, gko, gbh, legal, gk);
         } else if (fresh) {
             for (int i = lane; i < A; i += 64) legal[i] = t.fresh_order[i];
             n = A - rstones;   // fresh root is the empty board
