@@ -1639,6 +1639,149 @@ void az_launch_pool_g8(const uint16_t* hi, const int8_t* q, float* out, int B, i
     else hipLaunchKernelGGL(k_pool_g8<1>, dim3(grid), dim3(256), lds, st, hi, q, out, C, H, P, m_limit, B);
 }
 
+// The trunk's tail in one launch: adaptive_avg_pool2d of the g8 trunk output to P x P and both head
+// 1x1 convs ([policy | value], N = 64 outputs, ReLU) -- what k_pool_g8 + gemm_f32<64> computed with
+// an fp32 round trip of the pooled map and a second launch.  One 256-thread block per board walks the
+// channels in 32-channel slices: the slice is joined to fp32 in LDS (as k_pool_g8), pooled into
+// pooled[cell][k] in the same summation order (rows, then columns; / kh / kw), and multiplied into
+// the accumulators with v_mfma_f32_32x32x2_f32 over the slice's k pairs in ascending order -- the
+// products, k pairing and order of gemm_f32's chain, so every output is bitwise the same.  The next
+// slice's global loads are issued before the current slice is pooled.  Wave w owns the 32 x 32 tile
+// (cells 32 (w >> 1).., outputs 32 (w & 1)..).  The slice's weights are prefetched with its
+// activations (a weight load per slice on the critical path cost ~1 us each).
+template <int MODE>
+__global__ __launch_bounds__(256) void k_pool_heads_g8(const uint16_t* hi, const int8_t* q, const float* Wt,
+                                                       const float* bias, float* out, int C, int H, int P,
+                                                       const int* m_limit, int maxB) {
+    constexpr int SL = 36, PL = 33;                     // LDS row strides (floats)
+    extern __shared__ __attribute__((aligned(16))) float f[];
+    const int G = C / 8, HW = H * H, PP = P * P, NS = G / 4;
+    float* pl = f + HW * SL;                            // pooled slice [64 cells][PL]
+    float* ws = pl + 64 * PL;                           // weight slice [64 outputs][PL]
+    const int B = m_limit ? min(*m_limit, maxB) : maxB;
+    const int b = blockIdx.x;
+    if (b >= B) return;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave >> 1, wn = wave & 1, kh = lane >> 5, l32 = lane & 31;
+    constexpr int MAXI = (4 * 361 + 255) / 256;         // slice items per thread (19x19: 6)
+    uint4 rh[MAXI];
+    uint4 rl[MAXI];                                     // MODE 0 / 3: the lo plane (16 B); else .x/.y: int8 remainder
+    float rw[8];                                        // the slice's weights: 64 outputs x 32 k
+    auto load = [&](int sl) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int idx = tid + 256 * i, n = idx >> 5, k = idx & 31;
+            rw[i] = Wt[(size_t)n * C + sl * 32 + k];
+        }
+#pragma unroll
+        for (int i = 0; i < MAXI; ++i) {
+            const int idx = tid + 256 * i;
+            if (idx < 4 * HW) {
+                const int gl = idx / HW, pix = idx - gl * HW;
+                const size_t e = ((size_t)(b * G + sl * 4 + gl) * HW + pix) * 8;
+                rh[i] = *reinterpret_cast<const uint4*>(hi + e);
+                if constexpr (MODE == 0 || MODE == 3) rl[i] = *reinterpret_cast<const uint4*>(reinterpret_cast<const uint16_t*>(q) + e);
+                else { const uint2 r = *reinterpret_cast<const uint2*>(q + e); rl[i] = make_uint4(r.x, r.y, 0u, 0u); }
+            }
+        }
+    };
+    for (int i = tid; i < 64 * PL; i += 256) pl[i] = 0.0f;   // cells >= PP stay zero (their rows are not stored)
+    floatx16 acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
+    load(0);
+    for (int sl = 0; sl < NS; ++sl) {
+        // the slice joined to fp32 (k_pool_g8's values) and its weights [n][32]
+#pragma unroll
+        for (int i = 0; i < MAXI; ++i) {
+            const int idx = tid + 256 * i;
+            if (idx < 4 * HW) {
+                const int gl = idx / HW, pix = idx - gl * HW;
+                uint16_t h[8];
+                float v[8];
+                *reinterpret_cast<uint4*>(h) = rh[i];
+                if constexpr (MODE == 0 || MODE == 3) {
+                    constexpr int PM = MODE == 0 ? 1 : 2;
+                    uint16_t l[8];
+                    *reinterpret_cast<uint4*>(l) = rl[i];
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) v[k] = Half16<PM>::to_f(h[k]) + Half16<PM>::to_f(l[k]);
+                } else {
+                    int8_t r[8];
+                    *reinterpret_cast<uint2*>(r) = make_uint2(rl[i].x, rl[i].y);
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) v[k] = Half16<MODE>::join(h[k], r[k]);
+                }
+                float* d = f + pix * SL + gl * 8;
+                *reinterpret_cast<float4*>(d) = make_float4(v[0], v[1], v[2], v[3]);
+                *reinterpret_cast<float4*>(d + 4) = make_float4(v[4], v[5], v[6], v[7]);
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int idx = tid + 256 * i, n = idx >> 5, k = idx & 31;
+            ws[n * PL + k] = rw[i];
+        }
+        __syncthreads();
+        if (sl + 1 < NS) load(sl + 1);                  // in flight during the pool and the MFMAs
+        {
+            const int c8 = (tid & 3) * 8, o = tid >> 2;
+            if (o < PP) {
+                const int oy = o / P, ox = o - oy * P;
+                const int y0 = (oy * H) / P, y1 = ((oy + 1) * H + P - 1) / P;
+                const int x0 = (ox * H) / P, x1 = ((ox + 1) * H + P - 1) / P;
+                float sm[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+                for (int y = y0; y < y1; ++y)
+                    for (int x = x0; x < x1; ++x) {
+                        const float* src = f + (y * H + x) * SL + c8;
+                        const float4 t0 = *reinterpret_cast<const float4*>(src);
+                        const float4 t1 = *reinterpret_cast<const float4*>(src + 4);
+                        sm[0] += t0.x; sm[1] += t0.y; sm[2] += t0.z; sm[3] += t0.w;
+                        sm[4] += t1.x; sm[5] += t1.y; sm[6] += t1.z; sm[7] += t1.w;
+                    }
+                const float kf = (float)(y1 - y0), kw = (float)(x1 - x0);
+#pragma unroll
+                for (int j = 0; j < 8; ++j) pl[o * PL + c8 + j] = sm[j] / kf / kw;
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int kk = 0; kk < 16; ++kk) {
+            const float a = pl[(32 * wm + l32) * PL + 2 * kk + kh];
+            const float w = ws[(32 * wn + l32) * PL + 2 * kk + kh];
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, w, acc, 0, 0, 0);
+        }
+        __syncthreads();                                // f / pl / ws are rewritten by the next slice
+    }
+    const int n = 32 * wn + l32;
+    const float bn = bias ? bias[n] : 0.0f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int m = 32 * wm + (r & 3) + 8 * (r >> 2) + 4 * kh;
+        if (m < PP) {
+            const float v = acc[r] + bn;
+            out[((size_t)b * PP + m) * 64 + n] = v > 0.0f ? v : 0.0f;
+        }
+    }
+}
+
+// true when k_pool_heads_g8 takes this tail: 32-channel slices, at most 64 cells, both heads' 1x1
+// convs = 64 outputs, the joined slice within the LDS budget
+bool az_pool_heads_supported(int C, int H, int P, int N) {
+    return C % 32 == 0 && P * P <= 64 && N == 64 && H * H <= 361;
+}
+
+int az_launch_pool_heads_g8(const uint16_t* hi, const int8_t* q, const float* Wt, const float* bias, float* out, int B,
+                            int C, int H, int P, int N, const int* m_limit, int mode, hipStream_t st) {
+    if (!az_pool_heads_supported(C, H, P, N)) return -1;
+    const size_t lds = ((size_t)H * H * 36 + 2 * 64 * 33) * sizeof(float);
+    if (mode == 2) hipLaunchKernelGGL(k_pool_heads_g8<2>, dim3(B), dim3(256), lds, st, hi, q, Wt, bias, out, C, H, P, m_limit, B);
+    else if (mode == 0) hipLaunchKernelGGL(k_pool_heads_g8<0>, dim3(B), dim3(256), lds, st, hi, q, Wt, bias, out, C, H, P, m_limit, B);
+    else if (mode == 3) hipLaunchKernelGGL(k_pool_heads_g8<3>, dim3(B), dim3(256), lds, st, hi, q, Wt, bias, out, C, H, P, m_limit, B);
+    else hipLaunchKernelGGL(k_pool_heads_g8<1>, dim3(B), dim3(256), lds, st, hi, q, Wt, bias, out, C, H, P, m_limit, B);
+    return 0;
+}
+
 // true when the g8 trunk (conv3x3_v5 at 15x15 / conv3x3_v6) handles this shape: square boards with a
 // G8Geom instantiation, 128-channel output halves, 16-channel chunks (v5, 15x15) or 32 (v6)
 static bool g8_board(int H) { return H == 8 || H == 9 || H == 13 || H == 15 || H == 19; }

@@ -64,6 +64,9 @@ void az_launch_rec_planes(const uint8_t* rec, float* dst, const int* eval_games,
                           hipStream_t st);
 void az_launch_pool_g8(const uint16_t* hi, const int8_t* q, float* out, int B, int C, int H, int P, const int* m_limit,
                        int mode, hipStream_t st);
+bool az_pool_heads_supported(int C, int H, int P, int N);
+int az_launch_pool_heads_g8(const uint16_t* hi, const int8_t* q, const float* Wt, const float* bias, float* out, int B,
+                            int C, int H, int P, int N, const int* m_limit, int mode, hipStream_t st);
 void az_launch_to_g8x3(const float* in, uint16_t* hi, uint16_t* lo, int C, int HW, const int* m_limit, int maxB,
                        hipStream_t st, int pt, int* ovf);
 bool az_conv_v7x3_supported(const ConvBf16Args& a);
@@ -787,6 +790,10 @@ int net_forward(az_net* n, const float* x0, int B, const int* nb, float* logits,
     const int mode = f16 ? 2 : 1;
     int8_t* hq[2] = {reinterpret_cast<int8_t*>(n->hl[0]), reinterpret_cast<int8_t*>(n->hl[1])};
     const int inpath = net_input_path(n);
+    // the trunk's tail -- pool and both head 1x1 convs -- in one launch on the g8 paths
+    // (k_pool_heads_g8, bitwise what k_pool_g8 + gemm_f32 give; conv flag 0x400000 keeps those for A/B)
+    const bool tail_fused = (g8 || g8x3) && n->hpv && (d.head_channels * PP) % 32 == 0 &&
+                            az_pool_heads_supported(F, H, P, 2 * d.head_channels) && !(az_conv_flags() & 0x400000);
     if (lr && inpath == NET_IN_GEMM) return az_fail(AZ_ERR_ARG, "net_forward: this net cannot read leaf records");
     if (int r = poison_net(n, st, false)) return r;
     if (prec == AZ_PREC_F16X3 && !g8x3 && inpath != NET_IN_SMALL)
@@ -824,6 +831,8 @@ int net_forward(az_net* n, const float* x0, int B, const int* nb, float* logits,
     if (inpath == NET_IN_G8) {
         // input planes -> g8 16-bit (0/1 planes are exact), then the input conv on the g8 kernel; 16
         // planes on a board whose g8 conv needs 32-channel chunks: zero groups 2-3 and in32
+        // (15x15 keeps 16 channels on conv3x3_v5: 126 us per 2048-board launch against 146 us for
+        // conv3x3_v6 on the zero-padded 32, profiles/r05_fused_tail_ab.txt)
         const bool i32 = !az_conv_g8_supported(H, W, n->cin_pad, F);
         const Layer& IN = i32 ? n->in32 : n->in;
         const int cin = i32 ? 32 : n->cin_pad;
@@ -888,8 +897,13 @@ int net_forward(az_net* n, const float* x0, int B, const int* nb, float* logits,
         }
         if (ev1) n->pc.stamp(st);
         ev1 = false;
-        az_launch_pool_g8(n->hh[cur], reinterpret_cast<const int8_t*>(n->hl[cur]), n->pool, B, F, H, P, nb, pt == 2 ? 3 : 0,
-                          st);
+        if (tail_fused) {
+            az_launch_pool_heads_g8(n->hh[cur], reinterpret_cast<const int8_t*>(n->hl[cur]), n->hconv.W, n->hconv.b, n->hpv,
+                                    B, F, H, P, 2 * d.head_channels, nb, pt == 2 ? 3 : 0, st);
+        } else {
+            az_launch_pool_g8(n->hh[cur], reinterpret_cast<const int8_t*>(n->hl[cur]), n->pool, B, F, H, P, nb,
+                              pt == 2 ? 3 : 0, st);
+        }
     } else {
         const bool split = prec == AZ_PREC_BF16X3;
         if (g8) {
@@ -920,7 +934,9 @@ int net_forward(az_net* n, const float* x0, int B, const int* nb, float* logits,
             }
             if (ev1) n->pc.stamp(st);
             ev1 = false;
-            az_launch_pool_g8(n->hh[cur], hq[cur], n->pool, B, F, H, P, nb, mode, st);
+            if (tail_fused) az_launch_pool_heads_g8(n->hh[cur], hq[cur], n->hconv.W, n->hconv.b, n->hpv, B, F, H, P,
+                                                    2 * d.head_channels, nb, mode, st);
+            else az_launch_pool_g8(n->hh[cur], hq[cur], n->pool, B, F, H, P, nb, mode, st);
         } else {
         if (f16) az_launch_to_f16(h, n->hh[0], (size_t)rows * F, nb, HW, F, st, n->ovf);
         else az_launch_split_bf16(h, n->hh[0], split ? n->hl[0] : nullptr, (size_t)rows * F, nb, HW, F, st);
@@ -968,6 +984,7 @@ int net_forward(az_net* n, const float* x0, int B, const int* nb, float* logits,
     if (ev1) n->pc.stamp(st);
     if (!g8 && !g8x3) az_launch_pool(h, n->pool, B, H, W, F, P, nb, st);
     const int HC = d.head_channels, HK = HC * PP;
+    if (tail_fused) return net_heads_fc(n, B, nb, logits, value, st, n->hpv, n->hpv + HC, 2 * HC);
     if (HK % 32 == 0 && n->hpv) {
         // both head 1x1 convs as one GEMM (2 HC outputs; every output is the same k-ordered fp32
         // chain as in two launches), read by the FC heads with a 2 HC cell stride

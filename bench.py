@@ -95,6 +95,8 @@ def parse(argv=None):
     ap.add_argument("--cpu-window", type=float, default=20.0, help="seconds of the CPU baseline's timed window")
     ap.add_argument("--cpu-workers", type=int, default=0, help="CPU baseline processes (0: the host's CPU share, <=16)")
     ap.add_argument("--seed", type=int, default=1234)
+    ap.add_argument("--conv-flags", default=None,
+                    help="diagnostic: conv variant flag set (hex, az_diag_set_conv_flags) for same-box A/B runs")
     ap.add_argument("--parity-steps", type=int, default=2,
                     help="N=1: also time this many moves of the same workload with the fp32-faithful f16x3 trunk "
                          "(the parity precision), reported as parity_mode; 0 disables")
@@ -213,6 +215,9 @@ def run_rank(a, rank, world, dist, make_workload, coll_device):
     if os.environ.get("AZ_STEP_TRACE"):      # diagnostic: timestamped phases of every selfplay step on stderr
         from az_amd import _lib
         _lib.lib().az_diag_set_step_trace(1)
+    if getattr(a, "conv_flags", None):       # diagnostic: a conv variant flag set (same-box A/B)
+        from az_amd import _lib
+        _lib.lib().az_diag_set_conv_flags(int(a.conv_flags, 16))
     wl = make_workload(a, int(os.environ.get("LOCAL_RANK", "0")), sh)
     net = wl.net
     if rank == 0:
