@@ -59,6 +59,8 @@ CASES = [  # board, in_planes, actions, channels, blocks, B, flags selecting v7 
     (13, 8, 170, 256, 1, 400, 0x804),     # 13x13 at 400 boards: the automatic choice (128-row tiles)
     (9, 11, 81, 256, 1, 700, 0x804),      # 9x9 at 700 boards: the automatic choice (128-row tiles)
     (19, 8, 362, 256, 1, 400, 0x30804),   # 64-row tiles, three blocks per CU
+    (8, 111, 4672, 256, 1, 512, 0x804),   # 8x8 at 512 boards: the automatic 128-row tiles on the 3-slot ring
+    (19, 8, 362, 256, 1, 256, 0x804),     # the C4 N = 4 shard: 128-row tiles, 3-slot ring, two rounds
 ]
 
 

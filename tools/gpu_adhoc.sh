@@ -6,10 +6,8 @@ export TMPDIR=/tmp
 R=$PWD
 O=$R/gpurun_out/${TAG:-adhoc}
 mkdir -p $O
-TAG=${TAG:-adhoc}/t LIMIT=900 SMOKE=1 bash tools/gpu_tests.sh &&
-timeout -k 10 560 python3 bench.py > $O/bench_c3.json 2> $O/bench_c3.err && tail -c 200 $O/bench_c3.json && echo &&
-timeout -k 10 300 python3 bench.py --config c2 --cpu-baseline 0 > $O/bench_c2.json 2> $O/bench_c2.err && echo c2 ok &&
-timeout -k 10 400 python3 bench.py --config c4 --cpu-baseline 0 --parity-steps 0 > $O/bench_c4.json 2> $O/bench_c4.err && echo c4 ok &&
-timeout -k 10 400 python3 bench.py --config c4 --global-games 128 --cpu-baseline 0 > $O/bench_c4_g128.json 2> $O/bench_c4_g128.err && echo c4g128 ok &&
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_c3 -o run -- python3 bench.py --steps 1 --warmup 1 --cpu-baseline 0 --parity-steps 0 > $O/prof_c3.log 2>&1 &&
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_c2 -o run -- python3 bench.py --config c2 --steps 1 --warmup 1 --cpu-baseline 0 --parity-steps 0 > $O/prof_c2.log 2>&1 && echo prof ok
+TAG=${TAG:-adhoc}/t LIMIT=400 FILES="tests/test_gpu_conv_v7.py" bash tools/gpu_tests.sh &&
+for B in 256 512 1024; do
+  timeout -k 10 300 python3 tools/net_bench.py --game gomoku15 --batch $B --iters 8 --flags 0x204,0xa04,0xa0a0c,0xb0a0c,0x40a0c,0x10a0c > $O/g15_$B.txt 2>&1 || exit 1
+  echo "B=$B"; grep flags= $O/g15_$B.txt
+done
