@@ -1233,12 +1233,15 @@ int az_conv_v7_tm(const ConvBf16Args& a) {
     if (force) return force == 1 ? 256 : force == 2 ? 128 : force == 3 ? 64 : 192;
     const long rows = (long)a.M;
     const int halves = a.N / 128;
+    const long boards = rows / ((long)a.H * a.W);
     auto blocks = [&](int tm) { return ((rows + tm - 1) / tm + 7) / 8 * 8 * halves; };
+    // below 1024 boards (g8_choice's small-batch branch) 19x19 -- and 13x13 once 128-row tiles fill
+    // the CUs -- take 128-row tiles on the 3-slot ring (az_conv_v7_ring) at every size, including
+    // those whose 256-row tiles would make 1024 blocks: 19x19 128 boards 0.0594 ms (192-row: 0.0620),
+    // 256: 0.1106 (0.1160), 384: 0.1645 (256-row: 0.1887), 512: 0.2111 (0.2268; v6 0.2107), 768:
+    // 0.3085 (0.3392) (profiles/r05_small_batch_ring3.txt)
+    if (boards < 1024 && (a.H == 19 || (a.H == 13 && blocks(128) >= 512))) return 128;
     if (blocks(256) >= 1024) return 256;
-    // 19x19: 128-row tiles on the 3-slot ring, three blocks per CU (az_conv_v7_ring): 128 boards
-    // 0.0594 ms vs 0.0620 on 192-row tiles (round 4's choice: 0.0700 vs v6 0.0747), 256 boards
-    // 0.1106 vs 0.1160 (profiles/r05_small_batch_ring3.txt)
-    if (a.H == 19) return 128;
     if (blocks(128) >= 512) return 128;
     return 64;
 }

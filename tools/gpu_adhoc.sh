@@ -6,8 +6,8 @@ export TMPDIR=/tmp
 R=$PWD
 O=$R/gpurun_out/${TAG:-adhoc}
 mkdir -p $O
-TAG=${TAG:-adhoc}/t LIMIT=400 FILES="tests/test_gpu_conv_v7.py" bash tools/gpu_tests.sh &&
-for B in 256 512 1024; do
-  timeout -k 10 300 python3 tools/net_bench.py --game gomoku15 --batch $B --iters 8 --flags 0x204,0xa04,0xa0a0c,0xb0a0c,0x40a0c,0x10a0c > $O/g15_$B.txt 2>&1 || exit 1
-  echo "B=$B"; grep flags= $O/g15_$B.txt
-done
+TAG=${TAG:-adhoc}/t LIMIT=500 FILES="tests/test_gpu_conv_v7.py tests/test_gpu_poison.py tests/test_gpu_net.py" bash tools/gpu_tests.sh &&
+timeout -k 10 300 python3 tools/net_bench.py --game gomoku15 --batch 1024 --iters 8 --flags 0x204,0x304 > $O/g15_1024.txt 2>&1 && grep flags= $O/g15_1024.txt &&
+timeout -k 10 300 python3 tools/net_bench.py --game go19 --batch 512 --iters 8 --flags 0x204,0x1204 > $O/go19_512.txt 2>&1 && grep flags= $O/go19_512.txt &&
+timeout -k 10 300 python3 bench.py --config c4 --global-games 512 --cpu-baseline 0 --parity-steps 0 > $O/c4_g512.json 2> $O/c4_g512.err &&
+python3 -c "import json; d=json.loads(open('$O/c4_g512.json').read().strip().splitlines()[-1]); r=d['roofline']; print('c4 games 512', round(d['value'],2), r.get('kernel','')[:40], r.get('avg_launch_ms'))"
