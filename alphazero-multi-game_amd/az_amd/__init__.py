@@ -367,6 +367,12 @@ class ParallelMCTS:
         return {"select_ms": a.value, "expand_ms": b.value, "sim_steps": n.value, "select_bytes": sb.value,
                 "expand_bytes": eb.value, "fused_ms": f.value, "fused_launches": fl.value}
 
+    def tree_evictions(self):
+        """Diagnostic: TreeDev slot evictions so far (each one a stream synchronisation)."""
+        f = lib().az_diag_tree_evictions
+        f.restype, f.argtypes = ctypes.c_int64, [ctypes.c_void_p]
+        return int(f(self.h))
+
     def selfplayStep(self, temp_drop_move=30, t_init=1.0, t_final=0.0, restart_finished=True):
         cfg = SelfPlayCfg(temp_drop_move, t_init, t_final, int(restart_finished))
         moves = ctypes.c_int64(0)

@@ -1767,19 +1767,32 @@ __global__ __launch_bounds__(256) void k_pool_heads_g8(const uint16_t* hi, const
 
 // true when k_pool_heads_g8 takes this tail: 32-channel slices, at most 64 cells, both heads' 1x1
 // convs = 64 outputs, the joined slice within the LDS budget
+// k_pool_heads_g8's dynamic LDS: the board's pooled-cell partial sums + two 64 x 33 weight tiles
+static size_t pool_heads_lds(int H) { return ((size_t)H * H * 36 + 2 * 64 * 33) * sizeof(float); }
+// the device's LDS per workgroup (68.9 KB at 19x19 fits gfx950's 160 KB, not a 64 KB part)
+static size_t device_lds_limit() {
+    static const size_t lim = [] {
+        int dev = 0, v = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&v, hipDeviceAttributeMaxSharedMemoryPerBlock, dev) != hipSuccess)
+            return (size_t)0;
+        return (size_t)v;
+    }();
+    return lim;
+}
 bool az_pool_heads_supported(int C, int H, int P, int N) {
-    return C % 32 == 0 && P * P <= 64 && N == 64 && H * H <= 361;
+    return C % 32 == 0 && P * P <= 64 && N == 64 && H * H <= 361 && pool_heads_lds(H) <= device_lds_limit();
 }
 
 int az_launch_pool_heads_g8(const uint16_t* hi, const int8_t* q, const float* Wt, const float* bias, float* out, int B,
                             int C, int H, int P, int N, const int* m_limit, int mode, hipStream_t st) {
     if (!az_pool_heads_supported(C, H, P, N)) return -1;
-    const size_t lds = ((size_t)H * H * 36 + 2 * 64 * 33) * sizeof(float);
+    const size_t lds = pool_heads_lds(H);
     if (mode == 2) hipLaunchKernelGGL(k_pool_heads_g8<2>, dim3(B), dim3(256), lds, st, hi, q, Wt, bias, out, C, H, P, m_limit, B);
     else if (mode == 0) hipLaunchKernelGGL(k_pool_heads_g8<0>, dim3(B), dim3(256), lds, st, hi, q, Wt, bias, out, C, H, P, m_limit, B);
     else if (mode == 3) hipLaunchKernelGGL(k_pool_heads_g8<3>, dim3(B), dim3(256), lds, st, hi, q, Wt, bias, out, C, H, P, m_limit, B);
     else hipLaunchKernelGGL(k_pool_heads_g8<1>, dim3(B), dim3(256), lds, st, hi, q, Wt, bias, out, C, H, P, m_limit, B);
-    return 0;
+    return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
 // true when the g8 trunk (conv3x3_v5 at 15x15 / conv3x3_v6) handles this shape: square boards with a
@@ -1795,6 +1808,7 @@ static int g_conv_flags = 4 | 0x200;   // bit 2: v6 (16x16x32) at 15x15; 0x200: 
 // (a residual L2 prefetch during the main loop measured 0.6% slower and was removed; a cross-row
 // fragment prefetch and a mid-row barrier variant measured 1.5-2% slower)
 extern "C" int az_diag_set_conv_flags(int flags) { g_conv_flags = flags; return 0; }
+extern "C" int az_diag_conv_flags(void) { return g_conv_flags; }   // the current set (bench.py ORs bits into it)
 int az_conv_flags() { return g_conv_flags; }
 
 template <int HB, bool DENSE>

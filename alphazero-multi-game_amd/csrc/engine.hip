@@ -898,8 +898,9 @@ int net_forward(az_net* n, const float* x0, int B, const int* nb, float* logits,
         if (ev1) n->pc.stamp(st);
         ev1 = false;
         if (tail_fused) {
-            az_launch_pool_heads_g8(n->hh[cur], reinterpret_cast<const int8_t*>(n->hl[cur]), n->hconv.W, n->hconv.b, n->hpv,
-                                    B, F, H, P, 2 * d.head_channels, nb, pt == 2 ? 3 : 0, st);
+            if (az_launch_pool_heads_g8(n->hh[cur], reinterpret_cast<const int8_t*>(n->hl[cur]), n->hconv.W, n->hconv.b,
+                                        n->hpv, B, F, H, P, 2 * d.head_channels, nb, pt == 2 ? 3 : 0, st))
+                return az_fail(AZ_ERR_HIP, "k_pool_heads_g8 launch failed");
         } else {
             az_launch_pool_g8(n->hh[cur], reinterpret_cast<const int8_t*>(n->hl[cur]), n->pool, B, F, H, P, nb,
                               pt == 2 ? 3 : 0, st);
@@ -934,9 +935,13 @@ int net_forward(az_net* n, const float* x0, int B, const int* nb, float* logits,
             }
             if (ev1) n->pc.stamp(st);
             ev1 = false;
-            if (tail_fused) az_launch_pool_heads_g8(n->hh[cur], hq[cur], n->hconv.W, n->hconv.b, n->hpv, B, F, H, P,
-                                                    2 * d.head_channels, nb, mode, st);
-            else az_launch_pool_g8(n->hh[cur], hq[cur], n->pool, B, F, H, P, nb, mode, st);
+            if (tail_fused) {
+                if (az_launch_pool_heads_g8(n->hh[cur], hq[cur], n->hconv.W, n->hconv.b, n->hpv, B, F, H, P,
+                                            2 * d.head_channels, nb, mode, st))
+                    return az_fail(AZ_ERR_HIP, "k_pool_heads_g8 launch failed");
+            } else {
+                az_launch_pool_g8(n->hh[cur], hq[cur], n->pool, B, F, H, P, nb, mode, st);
+            }
         } else {
         if (f16) az_launch_to_f16(h, n->hh[0], (size_t)rows * F, nb, HW, F, st, n->ovf);
         else az_launch_split_bf16(h, n->hh[0], split ? n->hl[0] : nullptr, (size_t)rows * F, nb, HW, F, st);
@@ -1114,12 +1119,14 @@ struct az_search {
     Pinned<int> sp_cact, sp_nch;
     std::vector<int> sp_slots;
     std::vector<az_move_rec> sp_moves;
+    int sp_next_id = 0;             // one past the highest game id started on the handle (az_selfplay_step restarts)
     // device-resident copies of the TreeDev variants the per-step kernels take (tree_dev()): those
     // kernels get one 8-byte pointer instead of the ~550-byte struct by value, on ~38k dispatches per
     // C3 move.  Slot i's host shadow (pinned, the source of its async upload) is h_tree[i].
     TreeDev* d_tree = nullptr;
     TreeDev* h_tree = nullptr;
     int n_tree = 0, next_tree = 0;
+    int64_t tree_evictions = 0;     // slot reuses (each a stream synchronisation): az_diag_tree_evictions
     // Dirichlet draws of the NEXT move, made on a host thread while the device searches this one
     // (prefetch_noise; Gomoku self-play): per game the child count they were drawn for (-1: none)
     // and the generator state after them, taken over only when the next noise call asks for exactly
@@ -1150,6 +1157,7 @@ const TreeDev* tree_dev(az_search* s, const TreeDev& t) {
         k = s->n_tree++;
     } else {
         if (hipStreamSynchronize(s->e->stream) != hipSuccess) return nullptr;
+        ++s->tree_evictions;
         k = s->next_tree;
         s->next_tree = (k + 1) % AZ_TREE_SLOTS;
     }
@@ -1238,7 +1246,9 @@ int search_step(az_search* s, int mode, bool pre = false, bool fuse_next = false
     hipStream_t st = s->e->stream;
     const int G = s->c.n_games;
     if (mode != MODE_SIM && s->roots_ready) return 0;   // every playing root expanded: a no-op step
-    if (mode != MODE_SIM) s->roots_ready = true;         // after it every playing root is (expanded or terminal)
+    // a root step that fails part-way (TreeDev upload, the host evaluator, the net forward) leaves
+    // the roots unexpanded: roots_ready is set only once the step is fully issued (below)
+    if (mode != MODE_SIM) s->roots_ready = false;
     s->t.nd = s->arena[s->cur];
     const int64_t sidx = s->prof_steps;   // this simulation step's index while profiling
     const bool prof = s->prof && mode == MODE_SIM && s->prof_steps++ % prof_every() == 0 && s->pc.room(4);
@@ -1289,6 +1299,7 @@ int search_step(az_search* s, int mode, bool pre = false, bool fuse_next = false
     }
     if (prof) { s->pc.stamp(st); s->prof_sampled += 1; }
     HIPCHK(hipGetLastError());
+    if (mode != MODE_SIM) s->roots_ready = true;         // after it every playing root is (expanded or terminal)
     return 0;
 }
 
@@ -1492,6 +1503,7 @@ int search_new_games(az_search* s, const int* games, int n, const int* seed_ids 
         s->hist[g].clear();
         s->roots_ready = false;                          // a fresh root: unexpanded
         const int id = seed_ids ? seed_ids[i] : g;
+        s->sp_next_id = std::max(s->sp_next_id, id + 1);
         pf_drop(s, g);
         s->rng[g].seed(s->c.noise_seed + (uint32_t)(s->c.noise_seed_stride * id));
     }
@@ -2643,7 +2655,11 @@ int az_selfplay_step(az_search* s, const az_selfplay_cfg* cfg, int64_t* moves_do
         std::vector<int> fin;
         for (int g = 0; g < G; ++g) if (!s->active[g]) fin.push_back(g);
         if (!fin.empty()) {
-            if (int r = search_new_games(s, fin.data(), (int)fin.size())) return r;
+            // a restarted slot plays the next game id (slot order), whose evaluator / noise streams
+            // it seeds -- as az_selfplay_run hands out ids -- rather than replaying its slot's seed
+            std::vector<int> ids(fin.size());
+            for (size_t i = 0; i < fin.size(); ++i) ids[i] = s->sp_next_id + (int)i;
+            if (int r = search_new_games(s, fin.data(), (int)fin.size(), ids.data())) return r;
             std::vector<uint8_t> m(G, 0);
             for (int g : fin) m[g] = 1;
             if (int r = search_noise(s, s->c.dirichlet_alpha, s->c.dirichlet_eps, m.data())) return r;
@@ -2773,6 +2789,9 @@ int az_selfplay_run(az_search* s, const az_selfplay_cfg* cfg, int total_games, i
     HIPCHK(hipStreamSynchronize(st));
     return 0;
 }
+
+// diagnostic: TreeDev slot evictions so far (bench.py reports it: a steady-state step should have none)
+int64_t az_diag_tree_evictions(az_search* s) { return s ? s->tree_evictions : -1; }
 
 int az_search_profile(az_search* s, int enable) {
     if (!s) return az_fail(AZ_ERR_ARG, "null search");

@@ -5,6 +5,7 @@
 // transposition-table emulation per game and a prior ring that keeps the children
 // priors of every TT entry alive for later hits.  See DESIGN.md "Data layout in HBM".
 #pragma once
+#include <stddef.h>
 #include <stdint.h>
 
 #define AZ_MAXA 361          // largest board handled on device (19x19)
@@ -46,6 +47,7 @@ struct TreeDev {
     // Go root state (GoState): ko point, consecutive passes, position_history_ (hashes of the
     // positions after every stone move, go_state.cpp:250-252); rhash holds the stones-only hash
     int* rko; int* rpass; uint64_t* rposh; int* rnposh; int hmax;
+    int pad0 = 0;                // explicit padding (zero): tree_dev() compares TreeDev variants bytewise
     const uint64_t* zko;         // [A + 1] "ko_point" feature keys
     uint64_t zconst;             // "rules"[1] ^ "komi"[int(7.5*2) & 15] (Chinese rules, komi 7.5)
     int* gresult;                // [G] GameResult of the root state
@@ -56,6 +58,7 @@ struct TreeDev {
     int4* rhdr;                  // [G] the root's header {first, cnt, flag} as the last simulation's k_select ended
     int* need_eval; int* eval_slot; int* eval_games; int* n_eval;
     int eval_identity;           // 1: the batch maps are the identity (eval_slot[g] == g): no slot load
+    int pad1 = 0;
     uint8_t* leafrec;            // [G][AZ_REC_BYTES] leaf records (leaf_planes.h): the planes' inputs (NET)
     uint8_t* goleaf;             // Go: [G][AZ_GOLEAF_BYTES] the selected leaf's position (board, side to move,
                                  // ko, passes, stones hash, the path's position pushes) for its expansion
@@ -71,7 +74,13 @@ struct TreeDev {
     const float* net_value;      // [B]
     int log_game, log_cap; float* log_pol; float* log_val; float* log_planes; int* log_n;
     int stamp_game;              // diagnostic: this game's k_select / k_expand_backup write phase stamps (-1 off)
+    int pad2 = 0;
 };
+// no implicit padding: every byte of a TreeDev is a member (tree_dev() finds a variant with memcmp)
+static_assert(offsetof(TreeDev, zko) == offsetof(TreeDev, pad0) + sizeof(int), "TreeDev hole after pad0");
+static_assert(offsetof(TreeDev, leafrec) == offsetof(TreeDev, pad1) + sizeof(int), "TreeDev hole after pad1");
+static_assert(sizeof(TreeDev) == offsetof(TreeDev, pad2) + sizeof(int), "TreeDev tail padding");
+static_assert(offsetof(TreeDev, tt_mask) == 10 * sizeof(int), "TreeDev hole before tt_mask");
 
 // Training-example extraction (Dataset::extractExamples + augmentExample).
 // Records are flattened: game g owns moves [move_off[g], move_off[g+1]); move m owns policy

@@ -26,6 +26,7 @@ fp32 PyTorch-CPU network, one game per worker process, one thread each, on the h
 (self_play_manager.cpp:69-89), timed over a fixed window.
 """
 import argparse
+import copy
 import json
 import os
 import socket
@@ -60,6 +61,9 @@ PREC_NOTE = {
 PEAK_TFLOPS = {"f16x3": 2500.0, "bf16x3": 2500.0, "bf16": 2500.0, "fp16": 2500.0, "f32": 157.3}   # dense MFMA peaks, MI355X_MICROARCH.md
 PREC = {"f32": 0, "bf16x3": 1, "bf16": 2, "fp16": 3, "f16x3": 4}
 PARITY_PREC = "f16x3"    # the parity precision parity_mode times
+# f16x3 move time / fp16 move time on C3, measured (profiles/r05_bench_c3_closing.json: 38,640 vs 16,169 ms
+# = 2.39), with margin: the parity moves' time estimate against --time-budget
+PARITY_RATIO = 2.5
 # BASELINE.json configs: game, board, blocks, channels, sims/move, global games
 CONFIGS = {
     "c2": dict(game="gomoku", board=15, blocks=6, channels=64, sims=400, games=256,
@@ -96,11 +100,16 @@ def parse(argv=None):
     ap.add_argument("--cpu-workers", type=int, default=0, help="CPU baseline processes (0: the host's CPU share, <=16)")
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--conv-flags", default=None,
-                    help="diagnostic: conv variant flag set (hex, az_diag_set_conv_flags) for same-box A/B runs")
+                    help="diagnostic: conv variant bits (hex) OR'd into the library's default flag set "
+                         "(az_conv_flags | bits -> az_diag_set_conv_flags) for same-box A/B runs; the trunk "
+                         "kernel the run dispatched is named in roofline.kernel")
     ap.add_argument("--parity-steps", type=int, default=2,
-                    help="N=1: also time this many moves of the same workload with the fp32-faithful f16x3 trunk "
-                         "(the parity precision), reported as parity_mode; 0 disables")
-    ap.add_argument("--parity-warmup", type=int, default=1)
+                    help="N=1: after the timed moves, switch the live net to the fp32-faithful f16x3 trunk (the parity "
+                         "precision) and time this many more moves of the same games, reported as parity_mode; "
+                         "0 disables")
+    ap.add_argument("--parity-warmup", type=int, default=0,
+                    help="untimed parity-precision moves before parity_mode's timed ones (the piece sets are "
+                         "packed at load: none needed)")
     ap.add_argument("--time-budget", type=float, default=560.0,
                     help="seconds: parity_mode is skipped (and says so) when the run so far plus its estimated "
                          "time would exceed this (the driver's run limit is 600 s)")
@@ -202,9 +211,62 @@ class GpuWorkload:
         self.eng.close()
 
 
-def run_rank(a, rank, world, dist, make_workload, coll_device):
+def _timed_moves(a, wl, net, steps, barrier):
+    """`steps` self-play moves of the live workload between barriers, with the trunk / tree
+    kernel clocks on: the raw counters of one timed region."""
+    barrier()
+    if a.kernel_timing:
+        net.profile(True)
+        wl.mcts.profile(True)
+    t0 = time.perf_counter()
+    moves = evals = 0
+    for _ in range(steps):
+        mv, ev = wl.step()
+        moves += mv
+        evals += ev
+    wl.sync()
+    elapsed = time.perf_counter() - t0
+    barrier()
+    trunk_ms, launches, forwards = net.profile_read()
+    ev = getattr(wl.mcts, "tree_evictions", None)
+    return {"elapsed": elapsed, "moves": moves, "evals": evals, "steps": steps, "trunk_ms": trunk_ms,
+            "tree_evictions": ev() if ev else None,
+            "launches": launches, "forwards": forwards, "tree": wl.mcts.profile_read(),
+            "kernel": net.trunk_kernel()}     # the kernel the library dispatches for this net (engine's own choice)
+
+
+def _roofline(a, m, precision):
+    """The dominant kernel's roofline from rank 0's own timed region m: algorithmic conv FLOPs per
+    launch / the launch's average device-clock duration, against the precision's dense MFMA peak."""
+    HW = a.board * a.board
+    conv_flops_per_eval = 2 * a.blocks * 2.0 * 9 * a.channels * a.channels * HW
+    launches = m["launches"]
+    boards_per_launch = m["evals"] * 2 * a.blocks / max(1, launches)        # rank 0's own launches and boards
+    per_launch_flops = boards_per_launch * conv_flops_per_eval / (2 * a.blocks)
+    per_launch_ms = m["trunk_ms"] / max(1, launches)
+    achieved = per_launch_flops / (per_launch_ms * 1e-3) / 1e12 if launches else 0.0
+    peak = PEAK_TFLOPS[precision]
+    rf = {"kernel": f"{m['kernel']} ({precision} trunk, {a.board}x{a.board}, {a.channels} ch)",
+          "bound": "mfma",
+          "achieved": achieved, "peak": peak, "unit": "TFLOP/s", "frac": achieved / peak, "traffic": None,
+          "launches": launches, "avg_launch_ms": per_launch_ms, "boards_per_launch": boards_per_launch,
+          "flops_per_launch": per_launch_flops,
+          # launches are trunk-conv equivalents (2 x blocks per forward); a fused forward (k_smallnet)
+          # is one kernel launch per forward, whose rocprofv3 average is avg_forward_ms
+          "forwards": m["forwards"], "avg_forward_ms": m["trunk_ms"] / max(1, m["forwards"])}
+    b = copy.copy(a)
+    b.precision = precision
+    tr = pmc_traffic(b, m["kernel"], boards_per_launch if launches else 0)
+    if tr:
+        rf.update(tr)
+    return rf
+
+
+def run_rank(a, rank, world, dist, make_workload, coll_device, parity=None):
     """One rank of the bench: shard, weights (rank 0 init + broadcast), warmup, timed steps between
-    barriers, MAX elapsed / SUM counters over ranks.  Returns the JSON dict on rank 0, else None."""
+    barriers, MAX elapsed / SUM counters over ranks.  Returns the JSON dict on rank 0, else None.
+    parity (N=1): parity(ms_per_step) -> number of further moves to time with the parity precision
+    (the live net switched in place, the same games continued), or a string saying why not."""
     from az_amd import dist as azdist
     sh = azdist.shard_range(rank, world, a.global_games if a.scaling == "strong" else a.global_games * world)
     if sh["games"] < 1:
@@ -215,9 +277,10 @@ def run_rank(a, rank, world, dist, make_workload, coll_device):
     if os.environ.get("AZ_STEP_TRACE"):      # diagnostic: timestamped phases of every selfplay step on stderr
         from az_amd import _lib
         _lib.lib().az_diag_set_step_trace(1)
-    if getattr(a, "conv_flags", None):       # diagnostic: a conv variant flag set (same-box A/B)
+    if getattr(a, "conv_flags", None):       # diagnostic: conv variant bits OR'd into the library's defaults
         from az_amd import _lib
-        _lib.lib().az_diag_set_conv_flags(int(a.conv_flags, 16))
+        L = _lib.lib()
+        L.az_diag_set_conv_flags(L.az_diag_conv_flags() | int(a.conv_flags, 16))
     wl = make_workload(a, int(os.environ.get("LOCAL_RANK", "0")), sh)
     net = wl.net
     if rank == 0:
@@ -235,38 +298,26 @@ def run_rank(a, rank, world, dist, make_workload, coll_device):
         wl.sync()
         if dist is not None:
             dist.barrier()
-    barrier()
-    if a.kernel_timing:
-        net.profile(True)
-        wl.mcts.profile(True)
-    t0 = time.perf_counter()
-    moves = evals = 0
-    for _ in range(a.steps):
-        mv, ev = wl.step()
-        moves += mv
-        evals += ev
-    wl.sync()
-    elapsed = time.perf_counter() - t0
-    barrier()
-    trunk_ms, launches, forwards = net.profile_read()
-    tree = wl.mcts.profile_read()
-    kernel = net.trunk_kernel()      # the kernel the library dispatches for this net (engine's own choice)
+    m = _timed_moves(a, wl, net, a.steps, barrier)
+    pm = None
+    if parity is not None and world == 1:
+        n_par = parity(1e3 * m["elapsed"] / a.steps)
+        if isinstance(n_par, str):
+            pm = {"skipped": n_par}
+        else:
+            # the same live games and weights: only the trunk / FC piece set changes (every piece set
+            # is packed at load, az_net_set_precision switches the dispatch)
+            net.set_precision(PREC[PARITY_PREC])
+            for _ in range(a.parity_warmup):
+                wl.step()
+            pm = _timed_moves(a, wl, net, n_par, barrier)
     if hasattr(wl, "close"):
         wl.close()
-    my_evals = evals
-    tot_moves, tot_evals = moves, evals
+    elapsed, tot_moves, tot_evals = m["elapsed"], m["moves"], m["evals"]
     if dist is not None:
-        elapsed, (tot_moves, tot_evals) = azdist.reduce_counters(dist, elapsed, [moves, evals], coll_device)
+        elapsed, (tot_moves, tot_evals) = azdist.reduce_counters(dist, elapsed, [m["moves"], m["evals"]], coll_device)
     if rank != 0:
         return None
-
-    HW = a.board * a.board
-    conv_flops_per_eval = 2 * a.blocks * 2.0 * 9 * a.channels * a.channels * HW
-    boards_per_launch = my_evals * 2 * a.blocks / max(1, launches)        # rank 0's own launches and boards
-    per_launch_flops = boards_per_launch * conv_flops_per_eval / (2 * a.blocks)
-    per_launch_ms = trunk_ms / max(1, launches)
-    achieved = per_launch_flops / (per_launch_ms * 1e-3) / 1e12 if launches else 0.0
-    peak = PEAK_TFLOPS[a.precision]
     strong = a.scaling == "strong"
     out = {
         "metric": METRIC,
@@ -289,15 +340,9 @@ def run_rank(a, rank, world, dist, make_workload, coll_device):
                    "blocks": a.blocks, "channels": a.channels, "parallelism": f"game-shard x{world}"},
         "nn_evals_per_s": tot_evals / elapsed,
         "evals_per_move": tot_evals / max(1, tot_moves),
-        "roofline": {"kernel": f"{kernel} ({a.precision} trunk, {a.board}x{a.board}, {a.channels} ch)",
-                     "bound": "mfma",
-                     "achieved": achieved, "peak": peak, "unit": "TFLOP/s", "frac": achieved / peak, "traffic": None,
-                     "launches": launches, "avg_launch_ms": per_launch_ms, "boards_per_launch": boards_per_launch,
-                     "flops_per_launch": per_launch_flops,
-                     # launches are trunk-conv equivalents (2 x blocks per forward); a fused forward (k_smallnet)
-                     # is one kernel launch per forward, whose rocprofv3 average is avg_forward_ms
-                     "forwards": forwards, "avg_forward_ms": trunk_ms / max(1, forwards)},
+        "roofline": _roofline(a, m, a.precision),
     }
+    tree = m["tree"]
     steps = max(1, tree["sim_steps"])
     out["tree_kernels"] = {
         name: {"avg_launch_us": 1e3 * tree[f"{k}_ms"] / steps,
@@ -312,6 +357,8 @@ def run_rank(a, rank, world, dist, make_workload, coll_device):
         out["tree_kernels"]["k_expand_select"] = {
             "avg_launch_us": fus, "launches": tree["fused_launches"], "bytes_per_launch": fb,
             "GB_per_s": fb / max(1e-12, 1e-6 * fus) / 1e9, "frac_of_hbm_peak": fb / max(1e-12, 1e-6 * fus) / 8.0e12}
+    # TreeDev variants re-uploaded over a full slot cache (each a host sync), since the handle was made
+    out["tree_kernels"]["tree_dev_evictions"] = m["tree_evictions"]
     out["tree_kernels"]["note"] = ("rank-0 device clock stamps: around each kernel of one simulation step in 16 (those "
                                    "steps run k_select and k_expand_backup as separate launches), and around one "
                                    "launch in 16 of the fused k_expand_select that every other step runs (step i's "
@@ -322,9 +369,8 @@ def run_rank(a, rank, world, dist, make_workload, coll_device):
                                    "dependent tree levels), peak 8 TB/s; rocprofv3 PMC traffic of the same kernels: "
                                    "profiles/r05_tree_pmc_c3.json (tools/tree_pmc.sh: C3's 2048 games x 800 sims, "
                                    "20-block trunk, --sync-every 10)")
-    tr = pmc_traffic(a, kernel, boards_per_launch if launches else 0)
-    if tr:
-        out["roofline"].update(tr)
+    if pm is not None:
+        out["parity_mode"] = pm if "skipped" in pm else parity_line(a, pm, m)
     return out
 
 
@@ -467,21 +513,36 @@ def cpu_baseline_line(a, raw, evals_per_move):
                       f"{evals_per_move:.1f} evaluations per move (measured on the GPU run of the same workload)"}
 
 
-def parity_mode(a, make_workload, dev):
-    """The same workload with the fp32-faithful trunk (f16x3), a short timed run in the same process
-    (N=1, after the headline run has freed its device memory): positions/s and its own roofline."""
-    import copy
-    b = copy.copy(a)
-    b.precision, b.steps, b.warmup = PARITY_PREC, a.parity_steps, a.parity_warmup
-    out = run_rank(b, 0, 1, None, make_workload, dev)
-    keys = ("value", "unit", "steps", "warmup", "ms_per_step", "dtype", "dtype_note", "nn_evals_per_s",
-            "evals_per_move", "roofline")
-    pm = {k: out[k] for k in keys}
-    rf = pm["roofline"]
+def parity_line(a, pm, m):
+    """parity_mode: the fp32-faithful trunk (f16x3) timed on the same live workload right after the
+    headline moves (same games continued, same weights): positions/s and its own roofline."""
+    out = {"value": pm["moves"] / pm["elapsed"], "unit": "positions/s", "steps": pm["steps"],
+           "warmup": a.parity_warmup, "ms_per_step": 1e3 * pm["elapsed"] / pm["steps"], "dtype": PARITY_PREC,
+           "dtype_note": PREC_NOTE[PARITY_PREC], "nn_evals_per_s": pm["evals"] / pm["elapsed"],
+           "evals_per_move": pm["evals"] / max(1, pm["moves"]),
+           "ratio_to_headline_ms_per_step": (pm["elapsed"] / pm["steps"]) / (m["elapsed"] / m["steps"]),
+           "roofline": _roofline(a, pm, PARITY_PREC)}
+    rf = out["roofline"]
     rf["mfma_issue_frac"] = 3 * rf["frac"]      # three MFMAs per algorithmic product
-    pm["note"] = ("same workload and weights, trunk in the parity precision; roofline FLOPs counted once "
-                  "(algorithmic), so frac <= 1/3 and mfma_issue_frac = 3 x frac")
-    return pm
+    out["note"] = (f"the same {a.global_games} live games continued for {pm['steps']} more moves (moves "
+                   f"{a.warmup + a.steps + a.parity_warmup + 1}..{a.warmup + a.steps + a.parity_warmup + pm['steps']} of "
+                   "every game) with the net switched in place to the parity precision (az_net_set_precision; every "
+                   "piece set is packed at load); roofline FLOPs counted once (algorithmic), so frac <= 1/3 and "
+                   "mfma_issue_frac = 3 x frac")
+    return out
+
+
+def parity_budget(a):
+    """parity(ms_per_step) for run_rank: the parity moves to time, or why none are -- the run so far
+    plus their estimate (PARITY_RATIO x the headline move, measured) must stay inside --time-budget."""
+    def decide(ms_per_step):
+        n = a.parity_steps + a.parity_warmup
+        est = n * ms_per_step / 1e3 * PARITY_RATIO + 5.0
+        spent = time.perf_counter() - T_START
+        if spent + est <= a.time_budget:
+            return a.parity_steps
+        return f"time budget: {spent:.0f} s spent + ~{est:.0f} s estimated > {a.time_budget:.0f} s"
+    return decide
 
 
 def split_affinity(local, local_world):
@@ -533,18 +594,12 @@ def main(argv=None, make_workload=None, backend=None):
         dist.init_process_group(backend or "nccl", init_method="env://",
                                 timeout=datetime.timedelta(seconds=a.dist_timeout))
     try:
-        out = run_rank(a, rank, world, dist, make_workload, dev)
+        parity = None
+        if world == 1 and a.parity_steps > 0 and a.precision not in ("f16x3", "bf16x3") and a.channels % 64 == 0:
+            parity = parity_budget(a)
+        out = run_rank(a, rank, world, dist, make_workload, dev, parity=parity)
         if out is not None:
             out["cpu_baseline"] = cpu_baseline_line(a, raw_cpu, out["evals_per_move"]) if raw_cpu else None
-            if world == 1 and a.parity_steps > 0 and a.precision not in ("f16x3", "bf16x3") and a.channels % 64 == 0:
-                # f16x3 moves take ~2.5x the fp16 trunk's (1.19 vs 0.485 ms per launch), plus setup
-                est = (a.parity_steps + a.parity_warmup) * out["ms_per_step"] / 1e3 * 2.8 + 20.0
-                spent = time.perf_counter() - T_START
-                if spent + est <= a.time_budget:
-                    out["parity_mode"] = parity_mode(a, make_workload, dev)
-                else:
-                    out["parity_mode"] = {"skipped": f"time budget: {spent:.0f} s spent + ~{est:.0f} s estimated > "
-                                                     f"{a.time_budget:.0f} s"}
             print(json.dumps(out), flush=True)
     finally:
         if dist is not None:

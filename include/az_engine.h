@@ -289,7 +289,10 @@ int az_search_read_eval_log(az_search* s, float* policy, float* value, float* pl
 /* One SelfPlayManager::playSingleGame move for every active game: search, temperature
  * schedule (T = ply < temp_drop ? t_init : t_final), selectAction(true, T), record,
  * makeMove/updateWithMove, noise after even plies.  Finished games restart when
- * restart != 0.  moves_done/evals_done accumulate the positions and NN evaluations. */
+ * restart != 0, in slot order, as the next game ids (one past the highest id started on the
+ * handle; az_search_new_games' slots are ids 0..n-1), each seeding its evaluator / noise streams
+ * by its id as az_selfplay_run does.  moves_done/evals_done accumulate the positions and NN
+ * evaluations. */
 typedef struct az_selfplay_cfg {
     int temp_drop_move;   /* 30 */
     float t_init;         /* 1.0 */

@@ -31,6 +31,10 @@ class _Net:
         self.blob = None
         self.loaded = None
         self.prof = False
+        self.precision = None
+
+    def set_precision(self, p):
+        self.precision = p
 
     def init_random(self, seed):
         self.blob = (np.arange(self.num_params, dtype=np.float32) + seed) * 0.25
@@ -49,7 +53,7 @@ class _Net:
         return 4.0, 40 * 2, 2      # 4 ms over 80 trunk launches
 
     def trunk_kernel(self):
-        return "conv3x3_v7<2, 15, SLIM>"
+        return "conv3x3_v9x3<15, SLIM, f16>" if self.precision == 4 else "conv3x3_v7<2, 15, SLIM>"
 
 
 class _Mcts:
@@ -240,3 +244,31 @@ def test_pmc_traffic_matches_each_trunk_kernel():
     assert x3["traffic"] > fp16["traffic"] > 0
     half = bench.pmc_traffic(types.SimpleNamespace(precision="fp16", **net), "conv3x3_v7<2, 15, SLIM>", 1024.0)
     assert half["traffic"] == pytest.approx(fp16["traffic"] / 2)
+
+
+def test_bench_parity_mode_in_place_world1():
+    """N=1: after the timed headline moves the live net switches to the parity precision (f16x3) in
+    place and the same workload is timed for --parity-steps more moves (no second setup / warm-up);
+    the budget rule skips it, and says so, when the estimate would overrun --time-budget."""
+    import bench
+    a = bench.parse(["--steps", "3", "--warmup", "2", "--parity-steps", "2"])
+    wls = []
+
+    def make(a_, local, shard):
+        wls.append(_Workload(a_, local, shard))
+        return wls[-1]
+    out = bench.run_rank(a, 0, 1, None, make, "cpu", parity=bench.parity_budget(a))
+    w = wls[0]
+    assert len(wls) == 1 and w.steps == 2 + 3 + 2          # one workload: warmup, headline, parity moves
+    assert w.net.precision == bench.PREC["f16x3"]
+    pm = out["parity_mode"]
+    assert pm["dtype"] == "f16x3" and pm["steps"] == 2 and pm["value"] > 0
+    assert "v9x3" in pm["roofline"]["kernel"] and "v7<" in out["roofline"]["kernel"]
+    assert pm["roofline"]["mfma_issue_frac"] == pytest.approx(3 * pm["roofline"]["frac"])
+    assert "moves 6..7" in pm["note"]
+    # the budget: an estimate past --time-budget skips the parity moves and names the numbers
+    b = bench.parse(["--steps", "3", "--warmup", "2", "--parity-steps", "2", "--time-budget", "1"])
+    wls.clear()
+    out = bench.run_rank(b, 0, 1, None, make, "cpu", parity=bench.parity_budget(b))
+    assert "skipped" in out["parity_mode"] and "time budget" in out["parity_mode"]["skipped"]
+    assert wls[0].steps == 5 and wls[0].net.precision is None

@@ -187,3 +187,42 @@ def test_gpu_selfplay_manager_python_network_matches_oracle():
         for ply, (m, r) in enumerate(zip(mv, ref["moves"])):
             assert (m.action, bits(m.policy), bits([m.value])[0]) == (r["action"], r["probs"], r["value"]), (g, ply)
     assert max(net.batches) == 2
+
+
+@pytest.mark.gpu
+def test_gpu_callback_failure_then_retry_matches_oracle(engine):
+    """A host evaluator that raises once, in the root expansion of the first addDirichletNoise: the
+    call fails with AzError and leaves the roots unexpanded (roots_ready is set only after a root
+    step completes), so the retried call expands the roots, then draws and mixes the noise exactly
+    as the reference's addDirichletNoise -> expandNode does; the game then matches the oracle bit
+    for bit (the failed attempt's TT lookup is not in the oracle's counters, so those are skipped)."""
+    import az_amd
+    import az_oracle as O
+    bs, sims, n = 9, 60, 2
+    refs = O.play(seed_stride=1, bs=bs, sims=sims, max_moves=4, eval_kind=O.EVAL_REPLAY, n_games=n,
+                  evaluator=lambda g, planes: plane_eval(planes))
+    state = {"fail": 1, "calls": 0}
+
+    def cb(games, moves, planes):
+        state["calls"] += 1
+        if state["fail"]:
+            state["fail"] -= 1
+            raise RuntimeError("evaluator unavailable (once)")
+        out = [plane_eval(planes[i]) for i in range(len(games))]
+        return np.stack([o[0] for o in out]), np.array([o[1] for o in out], np.float32)
+
+    m = az_amd.ParallelMCTS(engine, n_games=n, board_size=bs, num_simulations=sims, evaluator=az_amd.AZ_EVAL_CALLBACK,
+                            callback=cb, noise_seed_stride=1)
+    try:
+        m.newGames()
+        with pytest.raises(az_amd.AzError):
+            m.addDirichletNoise(0.03, 0.25)
+        assert state["calls"] == 1
+        m.addDirichletNoise(0.03, 0.25)                  # the retry: root expansion, then the noise
+        assert state["calls"] == 2
+        from test_gpu_search import children_rows
+        for g in range(n):
+            assert children_rows(m, g) == refs[g]["init_root"], g
+        play_and_compare(m, refs, n, max_moves=4, start=False, counters=False)
+    finally:
+        m.close()

@@ -36,10 +36,13 @@ def children_rows(m, g):
     return [[int(a), int(n), int(v), w, p] for a, n, v, w, p in zip(act, N, VL, bits(W), bits(P))]
 
 
-def play_and_compare(m, refs, n_games, max_moves=None):
-    """Drive the engine with the playSingleGame loop and compare to per-game reference dicts."""
-    m.newGames()
-    m.addDirichletNoise(0.03, 0.25)
+def play_and_compare(m, refs, n_games, max_moves=None, start=True, counters=True):
+    """Drive the engine with the playSingleGame loop and compare to per-game reference dicts.
+    start=False: the caller already ran newGames + the initial noise; counters=False skips the
+    TT lookup / hit / evaluation counters."""
+    if start:
+        m.newGames()
+        m.addDirichletNoise(0.03, 0.25)
     for g in range(n_games):
         assert children_rows(m, g) == refs[g]["init_root"], f"init_root game {g}"
     nmoves = max(len(r["moves"]) for r in refs)
@@ -61,7 +64,9 @@ def play_and_compare(m, refs, n_games, max_moves=None):
             assert int(act[g]) == r["action"], (g, ply, "action")
             assert bits([val[g]])[0] == r["value"], (g, ply, "value")
             c = m.counters(g)
-            assert (c["tt_lookups"], c["tt_hits"], c["evals"]) == (r["tt_lookups"], r["tt_hits"], r["evals"]), (g, ply)
+            if counters:
+                assert (c["tt_lookups"], c["tt_hits"], c["evals"]) == (r["tt_lookups"], r["tt_hits"], r["evals"]), \
+                    (g, ply)
         act = np.array([act[g] if live[g] else m.none for g in range(n_games)], np.int32)
         term, res = m.updateWithMove(act)
         for g in range(n_games):
@@ -178,3 +183,52 @@ def test_gpu_sharded_selfplay_independent_of_rank_count(engine):
         assert [(m.action, bits(m.policy), bits([m.value])[0]) for m in a.moves] == \
                [(m.action, bits(m.policy), bits([m.value])[0]) for m in b.moves], g
         assert a.result == b.result
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ev,slots", [("random", 4), ("hash", 3)])
+def test_gpu_selfplay_step_matches_oracle(engine, ev, slots):
+    """az_selfplay_step + az_selfplay_step_moves -- the entry point bench.py times -- against the
+    oracle's playSingleGame records (self_play_manager.cpp:187-216): `slots` games stepped one move
+    at a time for 70 moves with restart_finished (6x6 games end after 25-36 plies, past the T = 0
+    drop at 30), every MoveData compared (action, child-order
+    visit distribution bits incl. the T = 0 NaNs, root value bits, child actions) with the record
+    of the game id its slot plays; a finished slot restarts as the next game id in slot order
+    (seeding its noise / evaluator streams by that id), with the noise prefetch on this path."""
+    import az_amd
+    import az_oracle as O
+    bs, sims, steps, total = 6, 48, 70, 24
+    kind = O.EVAL_RANDOM if ev == "random" else O.EVAL_HASH
+    dev = az_amd.AZ_EVAL_RANDOM if ev == "random" else az_amd.AZ_EVAL_HASH
+    refs = O.play(seed_stride=1, bs=bs, sims=sims, eval_kind=kind, eval_seed=5, n_games=total)
+    m = az_amd.ParallelMCTS(engine, n_games=slots, board_size=bs, num_simulations=sims, evaluator=dev, eval_seed=5,
+                            noise_seed=42, noise_seed_stride=1)
+    gid = list(range(slots))            # the game id each slot plays
+    ply = [0] * slots
+    nxt = slots
+    restarts = 0
+    try:
+        m.newGames()
+        m.addDirichletNoise(0.03, 0.25)
+        for step in range(steps):
+            mv, _ = m.selfplayStep()
+            recs = m.stepMoves(materialize=True)
+            assert mv == len(recs) == slots, step            # every slot moves (finished slots restarted)
+            assert [s for s, _ in recs] == list(range(slots))
+            for s, md in recs:
+                assert gid[s] < total, "more games than the oracle played"
+                rm = refs[gid[s]]["moves"][ply[s]]
+                where = (step, s, gid[s], ply[s])
+                assert md.action == rm["action"], where
+                assert bits(md.policy) == rm["probs"], where
+                assert bits([md.value])[0] == rm["value"], where
+                assert list(md.child_actions) == [r[0] for r in rm["children"]], where
+                ply[s] += 1
+            for s in range(slots):                           # finished: the slot takes the next id
+                if ply[s] == len(refs[gid[s]]["moves"]):
+                    assert refs[gid[s]]["terminal"], gid[s]
+                    gid[s], ply[s], nxt = nxt, 0, nxt + 1
+                    restarts += 1
+    finally:
+        m.close()
+    assert restarts >= 2 * slots                             # every slot restarted at least twice

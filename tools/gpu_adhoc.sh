@@ -6,5 +6,5 @@ export TMPDIR=/tmp
 R=$PWD
 O=$R/gpurun_out/${TAG:-adhoc}
 mkdir -p $O
-TAG=${TAG:-adhoc}/t LIMIT=900 SMOKE=1 bash tools/gpu_tests.sh &&
-timeout -k 10 560 python3 bench.py > $O/bench_c3.json 2> $O/bench_c3.err && tail -c 300 $O/bench_c3.json
+TAG=${TAG:-adhoc}/t LIMIT=600 FILES="${FILES:-tests/test_gpu_search.py tests/test_gpu_callback_eval.py}" bash tools/gpu_tests.sh &&
+timeout -k 10 590 python3 bench.py --steps ${STEPS:-20} --warmup ${WARMUP:-5} > $O/bench_c3.json 2> $O/bench_c3.err && tail -c 600 $O/bench_c3.json
