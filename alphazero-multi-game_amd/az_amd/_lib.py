@@ -118,7 +118,16 @@ EXPORTS = {
     "az_dataset_permute": (c_int, [vp, P(c_int64)]),
     "az_dataset_gather": (c_int, [vp, P(c_int64), c_int, P(c_float), P(c_float), P(c_int), P(c_float)]),
     "az_dataset_profile_read": (c_int, [vp, P(ctypes.c_double), P(ctypes.c_double)]),
+    "az_dist_unique_id": (c_int, [P(ctypes.c_ubyte)]),
+    "az_dist_init": (c_int, [vp, c_int, c_int, P(ctypes.c_ubyte), c_int, P(vp)]),
+    "az_dist_destroy": (None, [vp]),
+    "az_dist_info": (c_int, [vp, P(c_int), P(c_int)]),
+    "az_dist_barrier": (c_int, [vp]),
+    "az_counters_allreduce": (c_int, [vp, P(ctypes.c_double), P(ctypes.c_double), c_int, c_int]),
+    "az_net_broadcast_weights": (c_int, [vp, vp, c_int]),
 }
+AZ_DIST_ID_BYTES = 128
+AZ_DIST_SUM, AZ_DIST_MAX = 0, 1
 
 _lib = None
 

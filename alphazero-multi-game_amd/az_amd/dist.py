@@ -1,12 +1,16 @@
 """Multi-GPU plumbing of the self-play path: one process per GPU,
-games sharded by contiguous global id ranges, no collective in the inner loop.  RCCL (backend
-"nccl") on the GPU box; the same functions run over gloo on CPU tensors in the tests.
+games sharded by contiguous global id ranges, no collective in the inner loop.
 
   shard(rank, games_per_rank)      -> global game ids and the seeds that make every game's
                                       record independent of the rank count
-  broadcast_weights(...)            -> rank 0's weight blob on every rank (one broadcast)
-  reduce_counters(...)              -> (max elapsed, summed counters) for the bench line
+  Dist                              -> the engine's own RCCL communicator (az_dist_*, csrc/dist.hip):
+                                      weights broadcast straight into the nets' device buffers,
+                                      counter reductions, barriers -- the product path
+  broadcast_weights / reduce_counters -> the same two collectives over a torch.distributed group
+                                      (gloo on CPU tensors: the rank-logic tests without a GPU)
 """
+import ctypes
+
 import numpy as np
 
 NOISE_SEED = 42     # ParallelMCTS setDeterministicMode seed (parallel_mcts.cpp:1268)
@@ -51,3 +55,50 @@ def reduce_counters(dist, elapsed, counters, device="cpu"):
     c = torch.tensor([float(v) for v in counters], dtype=torch.float64, device=device)
     dist.all_reduce(c, op=dist.ReduceOp.SUM)
     return float(x.item()), [int(v) for v in c.tolist()]
+
+
+class Dist:
+    """The engine's RCCL communicator over the ranks' engines (include/az_engine.h az_dist_*).
+    Rank 0 makes the id (unique_id()); every rank passes the same id.  Collectives wait with a
+    deadline (timeout_s): a dead rank makes the others raise AzError, not hang."""
+
+    def __init__(self, engine, rank, world, uid, timeout_s=600.0):
+        from ._lib import AZ_DIST_ID_BYTES, check, lib
+        if len(uid) != AZ_DIST_ID_BYTES:
+            raise ValueError(f"dist id must be {AZ_DIST_ID_BYTES} bytes")
+        buf = (ctypes.c_ubyte * AZ_DIST_ID_BYTES).from_buffer_copy(uid)
+        h = ctypes.c_void_p()
+        check(lib().az_dist_init(engine.h, int(rank), int(world), buf, int(timeout_s * 1000), ctypes.byref(h)))
+        self.h, self.rank, self.world = h, int(rank), int(world)
+
+    @staticmethod
+    def unique_id():
+        from ._lib import AZ_DIST_ID_BYTES, check, lib
+        buf = (ctypes.c_ubyte * AZ_DIST_ID_BYTES)()
+        check(lib().az_dist_unique_id(buf))
+        return bytes(buf)
+
+    def barrier(self):
+        from ._lib import check, lib
+        check(lib().az_dist_barrier(self.h))
+
+    def allreduce(self, values, op="sum"):
+        """SUM ("sum") or MAX ("max") over the ranks of a list of numbers (float64)."""
+        from ._lib import AZ_DIST_MAX, AZ_DIST_SUM, check, lib
+        x = np.ascontiguousarray(values, np.float64).reshape(-1)
+        out = np.empty_like(x)
+        dp = ctypes.POINTER(ctypes.c_double)
+        check(lib().az_counters_allreduce(self.h, x.ctypes.data_as(dp), out.ctypes.data_as(dp), x.size,
+                                          AZ_DIST_SUM if op == "sum" else AZ_DIST_MAX))
+        return out.tolist()
+
+    def broadcast_weights(self, net, root=0):
+        """Rank root's weights into `net` on every rank, device to device (az_net_broadcast_weights)."""
+        from ._lib import check, lib
+        check(lib().az_net_broadcast_weights(self.h, net.h, int(root)))
+
+    def close(self):
+        from ._lib import lib
+        if self.h:
+            lib().az_dist_destroy(self.h)
+            self.h = None

@@ -66,6 +66,13 @@ class HipNeuralNetwork : public NeuralNetwork {
     void enableDebugMode(bool enable) override { debug_ = enable; }
     void printModelSummary() const override;
 
+    // after a weight broadcast into this net (selfplay::Distributed): the host copy of the blob
+    void refreshHostWeights();
+    // the precision was chosen at load (loadTorchScript, precision -1) and the trunk is F16X3:
+    // switch to AZ_PREC_BF16X3 (the fp32 range) and return true -- what predictBatch does on
+    // AZ_ERR_RANGE, for callers that run the net inside the engine (SelfPlayManager::generateGames)
+    bool fallbackToFp32Range();
+
     az_net* handle() const { return net_; }
     az_engine* engine() const { return eng_; }
     const NetShape& shape() const { return shape_; }

@@ -15,6 +15,22 @@
 namespace alphazero {
 namespace selfplay {
 
+class Distributed;
+
+// Contiguous global game ids of one rank of a per-GPU job (the first total % world ranks take one
+// more) and the noise seed that keeps every game's record independent of the rank count (seed +
+// global id): shardGames() in distributed.h, SelfPlayManager::setShard.
+struct GameShard {
+    int firstGame = 0, numGames = 0;
+    unsigned noiseSeed = 42;
+};
+
+// Job-wide counters of a sharded run, reduced over the ranks (RCCL) after generateGames.
+struct JobStats {
+    long long gamesCompleted = 0, totalMoves = 0;
+    double seconds = 0.0;          // the slowest rank's generateGames time
+};
+
 class SelfPlayManager {
  public:
     // numThreads is kept for the signature; concurrency is the device slot count
@@ -42,6 +58,16 @@ class SelfPlayManager {
     float getTemperature(int moveNum) const { return moveNum >= tempDrop_ ? tFinal_ : tInit_; }
 
     // engine extensions
+    // one rank's share of a per-GPU job: its games are the global ids [firstGame, firstGame +
+    // numGames) (record file names, noise / evaluator seeds); numGames replaces the constructor's
+    void setShard(const GameShard& s) {
+        numGames_ = s.numGames; firstGame_ = s.firstGame; noiseSeed_ = s.noiseSeed; noiseStride_ = 1;
+    }
+    int getFirstGameId() const { return firstGame_; }
+    // with a communicator, generateGames ends by reducing the job's counters over the ranks
+    // (every rank must call generateGames); getJobStats() then holds them
+    void setDistributed(Distributed* d) { dist_ = d; }
+    const JobStats& getJobStats() const { return job_; }
     void setConcurrentGames(int n) { slots_ = n; }
     void setMaxMoves(int n) { maxMoves_ = n; }
     void setSeeds(unsigned noiseSeed, int noiseSeedStride) { noiseSeed_ = noiseSeed; noiseStride_ = noiseSeedStride; }
@@ -56,6 +82,9 @@ class SelfPlayManager {
     const EvalLog& getEvalLog() const { return log_; }
 
  private:
+    int runGames(core::GameType type, int bs, bool variant, std::vector<GameRecord>& records, std::vector<char>& done,
+                 std::vector<std::string>& written);
+
     nn::NeuralNetwork* nn_;
     int numGames_, numSimulations_, numThreads_;
     float alpha_ = 0.03f, eps_ = 0.25f, tInit_ = 1.0f, tFinal_ = 0.0f;
@@ -74,6 +103,9 @@ class SelfPlayManager {
     int noiseStride_ = 1;
     int logSlot_ = -1, logCap_ = 0;
     EvalLog log_;
+    int firstGame_ = 0;
+    Distributed* dist_ = nullptr;
+    JobStats job_;
 };
 
 }  // namespace selfplay

@@ -15,6 +15,8 @@
 #include "alphazero/nn/random_policy_network.h"
 #include "alphazero/selfplay/dataset.h"
 #include "alphazero/selfplay/game_record.h"
+#include "alphazero/selfplay/distributed.h"
+#include "alphazero/selfplay/run_metadata.h"
 #include "alphazero/selfplay/self_play_manager.h"
 
 namespace py = pybind11;
@@ -428,6 +430,53 @@ PYBIND11_MODULE(_alphazero_cpp, m) {
         .def("getExamples", &selfplay::Dataset::getExamples)
         .def("lastExtractMs", &selfplay::Dataset::lastExtractMs);
 
+    py::class_<selfplay::RunMetadata>(m, "RunMetadata")
+        .def(py::init<>())
+        .def_readwrite("game", &selfplay::RunMetadata::game)
+        .def_readwrite("boardSize", &selfplay::RunMetadata::boardSize)
+        .def_readwrite("numGamesRequested", &selfplay::RunMetadata::numGamesRequested)
+        .def_readwrite("numGamesCompleted", &selfplay::RunMetadata::numGamesCompleted)
+        .def_readwrite("simulations", &selfplay::RunMetadata::simulations)
+        .def_readwrite("threads", &selfplay::RunMetadata::threads)
+        .def_readwrite("temperature", &selfplay::RunMetadata::temperature)
+        .def_readwrite("tempDrop", &selfplay::RunMetadata::tempDrop)
+        .def_readwrite("finalTemp", &selfplay::RunMetadata::finalTemp)
+        .def_readwrite("dirichletAlpha", &selfplay::RunMetadata::dirichletAlpha)
+        .def_readwrite("dirichletEpsilon", &selfplay::RunMetadata::dirichletEpsilon)
+        .def_readwrite("variant", &selfplay::RunMetadata::variant)
+        .def_readwrite("modelPath", &selfplay::RunMetadata::modelPath)
+        .def_readwrite("totalMoves", &selfplay::RunMetadata::totalMoves)
+        .def_readwrite("avgMovesPerGame", &selfplay::RunMetadata::avgMovesPerGame)
+        .def_readwrite("totalTimeSeconds", &selfplay::RunMetadata::totalTimeSeconds)
+        .def_readwrite("avgMovesPerSecond", &selfplay::RunMetadata::avgMovesPerSecond)
+        .def_readwrite("useGpu", &selfplay::RunMetadata::useGpu)
+        .def_readwrite("batchSize", &selfplay::RunMetadata::batchSize)
+        .def_readwrite("batchTimeout", &selfplay::RunMetadata::batchTimeout)
+        .def_readwrite("fp16Used", &selfplay::RunMetadata::fp16Used)
+        .def_readwrite("cPuct", &selfplay::RunMetadata::cPuct)
+        .def_readwrite("fpuReduction", &selfplay::RunMetadata::fpuReduction)
+        .def_readwrite("virtualLoss", &selfplay::RunMetadata::virtualLoss)
+        .def_readwrite("useTranspositionTable", &selfplay::RunMetadata::useTranspositionTable)
+        .def_readwrite("progressiveWidening", &selfplay::RunMetadata::progressiveWidening)
+        .def_readwrite("rank", &selfplay::RunMetadata::rank)
+        .def_readwrite("world", &selfplay::RunMetadata::world)
+        .def_readwrite("firstGameId", &selfplay::RunMetadata::firstGameId)
+        .def_readwrite("precision", &selfplay::RunMetadata::precision)
+        .def_readwrite("device", &selfplay::RunMetadata::device)
+        .def_readwrite("jobGamesCompleted", &selfplay::RunMetadata::jobGamesCompleted)
+        .def_readwrite("jobTotalMoves", &selfplay::RunMetadata::jobTotalMoves)
+        .def_readwrite("jobSeconds", &selfplay::RunMetadata::jobSeconds)
+        .def_readwrite("jobMovesPerSecond", &selfplay::RunMetadata::jobMovesPerSecond);
+    m.def("runMetadataJson", &selfplay::runMetadataJson);
+    m.def("writeRunMetadata", &selfplay::writeRunMetadata, py::arg("metadata"), py::arg("outputDir"));
+    py::class_<selfplay::GameShard>(m, "GameShard")
+        .def(py::init<>())
+        .def_readwrite("firstGame", &selfplay::GameShard::firstGame)
+        .def_readwrite("numGames", &selfplay::GameShard::numGames)
+        .def_readwrite("noiseSeed", &selfplay::GameShard::noiseSeed);
+    m.def("shardGames", &selfplay::shardGames, py::arg("rank"), py::arg("world"), py::arg("totalGames"),
+          py::arg("noiseSeed") = 42u);
+
     py::class_<selfplay::SelfPlayManager>(m, "SelfPlayManager")
         .def(py::init<nn::NeuralNetwork*, int, int, int>(), py::arg("neuralNetwork"), py::arg("numGames") = 100,
              py::arg("numSimulations") = 800, py::arg("numThreads") = 4, py::keep_alive<1, 2>())
@@ -456,6 +505,8 @@ PYBIND11_MODULE(_alphazero_cpp, m) {
         .def("setConcurrentGames", &selfplay::SelfPlayManager::setConcurrentGames)
         .def("setMaxMoves", &selfplay::SelfPlayManager::setMaxMoves)
         .def("setSeeds", &selfplay::SelfPlayManager::setSeeds)
+        .def("setShard", &selfplay::SelfPlayManager::setShard)
+        .def("getFirstGameId", &selfplay::SelfPlayManager::getFirstGameId)
         .def("setEvalLog", &selfplay::SelfPlayManager::setEvalLog, py::arg("slot"), py::arg("capacity"))
         .def("getEvalLog", [](const selfplay::SelfPlayManager& self) {
             // (policy [n][NA], value [n], planes [n][C][bs][bs]) as numpy arrays

@@ -57,6 +57,20 @@ HipNeuralNetwork::~HipNeuralNetwork() {
     if (net_) az_net_destroy(net_);
 }
 
+void HipNeuralNetwork::refreshHostWeights() {
+    std::lock_guard<std::mutex> lk(mu_);
+    blob_.resize(params_);
+    check(az_net_get_weights(net_, blob_.data(), blob_.size()), "az_net_get_weights");
+}
+
+bool HipNeuralNetwork::fallbackToFp32Range() {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (!autoPrecision_ || shape_.precision != AZ_PREC_F16X3) return false;
+    check(az_net_set_precision(net_, AZ_PREC_BF16X3), "az_net_set_precision");
+    shape_.precision = AZ_PREC_BF16X3;
+    return true;
+}
+
 void HipNeuralNetwork::loadWeights(const std::vector<float>& blob) {
     std::lock_guard<std::mutex> lk(mu_);
     check(az_net_load_weights(net_, blob.data(), blob.size()), "az_net_load_weights");

@@ -2,6 +2,7 @@
 #include "alphazero/selfplay/self_play_manager.h"
 
 #include <chrono>
+#include <cstdio>
 #include <ctime>
 #include <filesystem>
 #include <iomanip>
@@ -9,6 +10,8 @@
 #include <sstream>
 
 #include "alphazero/games/gomoku/gomoku_state.h"
+#include "alphazero/nn/hip_neural_network.h"
+#include "alphazero/selfplay/distributed.h"
 
 namespace alphazero {
 namespace selfplay {
@@ -32,6 +35,8 @@ void SelfPlayManager::setMctsConfig(const mcts::MCTSConfig& c) {
 namespace {
 struct RunCtx {
     SelfPlayManager* self;
+    int firstGame;                  // global id of local game 0 (setShard)
+    std::vector<std::string> files; // record files written by this attempt
     std::vector<GameRecord>* records;
     core::GameType type;
     bool variant;
@@ -55,9 +60,9 @@ void sink(void* user, int gid, int bs, int n, const az_move_rec* moves, int resu
         std::tm tm{};
         localtime_r(&t, &tm);
         std::ostringstream f;
-        f << c->dir << "/" << std::setfill('0') << std::setw(3) << gid << "_" << std::put_time(&tm, "%Y%m%d_%H%M%S")
-          << ".json";
-        rec.saveToFile(f.str());
+        f << c->dir << "/" << std::setfill('0') << std::setw(3) << gid + c->firstGame << "_"
+          << std::put_time(&tm, "%Y%m%d_%H%M%S") << ".json";
+        if (rec.saveToFile(f.str())) c->files.push_back(f.str());
     }
     (*c->records)[gid] = std::move(rec);
     (*c->done)[gid] = 1;
@@ -105,73 +110,106 @@ void progress(void* user, int gid, int move, int total_games, int64_t /*total_mo
 }
 }  // namespace
 
+// One az_selfplay_run over numGames_ games: the records of the finished games, the record files
+// written; returns the engine's status.
+int SelfPlayManager::runGames(core::GameType type, int bs, bool variant, std::vector<GameRecord>& records,
+                              std::vector<char>& done, std::vector<std::string>& written) {
+    const bool go = type == core::GameType::GO;
+    const mcts::DeviceEvaluator ev = mcts::deviceEvaluator(nn_);
+    az_search_cfg c{};
+    c.game = go ? AZ_GAME_GO : AZ_GAME_GOMOKU;
+    c.n_games = slots_ > 0 ? slots_ : std::min(std::max(numGames_, 1), 2048);
+    if (batchSet_ && batchSize_ > 0) c.n_games = std::min(c.n_games, batchSize_);   // network batch per step
+    c.board_size = bs;
+    c.num_simulations = numSimulations_;
+    c.c_puct = mcts_.cPuct > 0.0f ? mcts_.cPuct : 1.5f;       // :177-178
+    c.fpu_reduction = mcts_.fpuReduction >= 0.0f ? mcts_.fpuReduction : 0.1f;
+    c.virtual_loss = mcts_.virtualLoss;
+    c.eval_kind = ev.kind;
+    c.eval_seed = ev.seed + (uint32_t)firstGame_;           // per-game evaluator streams by global id
+    c.zobrist_seed = 12345u;
+    c.noise_seed = noiseSeed_;
+    c.noise_seed_stride = noiseStride_;
+    c.use_dirichlet_each_search = mcts_.useDirichletNoise ? 1 : 0;
+    c.dirichlet_alpha = alpha_;
+    c.dirichlet_eps = eps_;
+    c.tt_log2 = 20;                                            // TranspositionTable tt(1048576), :159
+    az_search* s = nullptr;
+    if (az_search_create(ev.engine, ev.net, &c, &s)) throw std::runtime_error(az_last_error());
+    EvalCtx ectx{nn_, type, bs};
+    if (ev.kind == AZ_EVAL_CALLBACK && az_search_set_evaluator(s, host_eval, &ectx)) {
+        az_search_destroy(s);
+        throw std::runtime_error(az_last_error());
+    }
+    log_ = EvalLog{};
+    if (logSlot_ >= 0 && az_search_enable_eval_log(s, logSlot_, logCap_)) {
+        az_search_destroy(s);
+        throw std::runtime_error(az_last_error());
+    }
+    az_selfplay_cfg sc{tempDrop_, tInit_, tFinal_, 0};
+    RunCtx ctx{this, firstGame_, {}, &records, type, variant, save_, outDir_, &progress_, &completed_, &totalMoves_,
+               &done};
+    int rc = az_selfplay_run(s, &sc, numGames_, maxMoves_, sink, progress, &ctx, &abort_);
+    written = ctx.files;
+    if (!rc && logSlot_ >= 0) {
+        EvalLog& L = log_;
+        L.policySize = go ? bs * bs + 1 : bs * bs;
+        L.planes = go ? 8 : 11;
+        L.cells = bs * bs;
+        L.policy.resize((size_t)logCap_ * L.policySize);
+        L.value.resize(logCap_);
+        L.features.resize((size_t)logCap_ * L.planes * L.cells);
+        rc = az_search_read_eval_log(s, L.policy.data(), L.value.data(), L.features.data(), &L.count);
+        L.policy.resize((size_t)L.count * L.policySize);
+        L.value.resize(L.count);
+        L.features.resize((size_t)L.count * L.planes * L.cells);
+    }
+    az_search_destroy(s);
+    return rc;
+}
+
 std::vector<GameRecord> SelfPlayManager::generateGames(core::GameType type, int boardSize, bool variant) {
     const bool go = type == core::GameType::GO;
     if (!go && type != core::GameType::GOMOKU) throw std::invalid_argument("generateGames: Gomoku or Go (no Chess rules)");
     if (variant) throw std::invalid_argument("generateGames: variant rules are not supported");
     running_ = true;
     abort_ = 0;
-    completed_ = 0;
-    totalMoves_ = 0;
     const int bs = boardSize > 0 ? boardSize : go ? 19 : 15;
     if (save_) std::filesystem::create_directories(outDir_);
-    std::vector<GameRecord> records(numGames_, GameRecord(type, bs, variant));
-    std::vector<char> done(numGames_, 0);
+    std::vector<GameRecord> records;
+    std::vector<char> done;
+    const auto t0 = std::chrono::steady_clock::now();
     try {
-        const mcts::DeviceEvaluator ev = mcts::deviceEvaluator(nn_);
-        az_search_cfg c{};
-        c.game = go ? AZ_GAME_GO : AZ_GAME_GOMOKU;
-        c.n_games = slots_ > 0 ? slots_ : std::min(std::max(numGames_, 1), 2048);
-        if (batchSet_ && batchSize_ > 0) c.n_games = std::min(c.n_games, batchSize_);   // network batch per step
-        c.board_size = bs;
-        c.num_simulations = numSimulations_;
-        c.c_puct = mcts_.cPuct > 0.0f ? mcts_.cPuct : 1.5f;       // :177-178
-        c.fpu_reduction = mcts_.fpuReduction >= 0.0f ? mcts_.fpuReduction : 0.1f;
-        c.virtual_loss = mcts_.virtualLoss;
-        c.eval_kind = ev.kind;
-        c.eval_seed = ev.seed;
-        c.zobrist_seed = 12345u;
-        c.noise_seed = noiseSeed_;
-        c.noise_seed_stride = noiseStride_;
-        c.use_dirichlet_each_search = mcts_.useDirichletNoise ? 1 : 0;
-        c.dirichlet_alpha = alpha_;
-        c.dirichlet_eps = eps_;
-        c.tt_log2 = 20;                                            // TranspositionTable tt(1048576), :159
-        az_search* s = nullptr;
-        if (az_search_create(ev.engine, ev.net, &c, &s)) throw std::runtime_error(az_last_error());
-        EvalCtx ectx{nn_, type, bs};
-        if (ev.kind == AZ_EVAL_CALLBACK && az_search_set_evaluator(s, host_eval, &ectx)) {
-            az_search_destroy(s);
-            throw std::runtime_error(az_last_error());
+        // a load-time-chosen F16X3 net whose activations leave the fp16 range (AZ_ERR_RANGE) switches
+        // to BF16X3 and the whole run repeats (its record files removed), as predictBatch does for a batch
+        for (int attempt = 0;; ++attempt) {
+            records.assign(numGames_, GameRecord(type, bs, variant));
+            done.assign(numGames_, 0);
+            completed_ = 0;
+            totalMoves_ = 0;
+            std::vector<std::string> written;
+            const int rc = runGames(type, bs, variant, records, done, written);
+            auto* hip = dynamic_cast<nn::HipNeuralNetwork*>(nn_);
+            if (rc == AZ_ERR_RANGE && attempt == 0 && hip && hip->fallbackToFp32Range()) {
+                for (const std::string& f : written) std::remove(f.c_str());
+                continue;
+            }
+            if (rc) throw std::runtime_error(az_last_error());
+            break;
         }
-        log_ = EvalLog{};
-        if (logSlot_ >= 0 && az_search_enable_eval_log(s, logSlot_, logCap_)) {
-            az_search_destroy(s);
-            throw std::runtime_error(az_last_error());
-        }
-        az_selfplay_cfg sc{tempDrop_, tInit_, tFinal_, 0};
-        RunCtx ctx{this, &records, type, variant, save_, outDir_, &progress_, &completed_, &totalMoves_, &done};
-        int rc = az_selfplay_run(s, &sc, numGames_, maxMoves_, sink, progress, &ctx, &abort_);
-        if (!rc && logSlot_ >= 0) {
-            EvalLog& L = log_;
-            L.policySize = go ? bs * bs + 1 : bs * bs;
-            L.planes = go ? 8 : 11;
-            L.cells = bs * bs;
-            L.policy.resize((size_t)logCap_ * L.policySize);
-            L.value.resize(logCap_);
-            L.features.resize((size_t)logCap_ * L.planes * L.cells);
-            rc = az_search_read_eval_log(s, L.policy.data(), L.value.data(), L.features.data(), &L.count);
-            L.policy.resize((size_t)L.count * L.policySize);
-            L.value.resize(L.count);
-            L.features.resize((size_t)L.count * L.planes * L.cells);
-        }
-        az_search_destroy(s);
-        if (rc) throw std::runtime_error(az_last_error());
     } catch (...) {
         running_ = false;
         throw;
     }
     running_ = false;
+    const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    job_ = JobStats{completed_.load(), totalMoves_.load(), secs};
+    if (dist_) {   // the job's counters over the ranks (every rank reaches this point)
+        const std::vector<double> sum = dist_->allreduceSum({(double)job_.gamesCompleted, (double)job_.totalMoves});
+        job_.gamesCompleted = (long long)sum[0];
+        job_.totalMoves = (long long)sum[1];
+        job_.seconds = dist_->allreduceMax({secs})[0];
+    }
     std::vector<GameRecord> out;   // finished games in game-id order (all of them unless aborted)
     for (int g = 0; g < numGames_; ++g)
         if (done[g]) out.push_back(std::move(records[g]));

@@ -4,6 +4,7 @@
 // The product path never falls back to the CPU: without a HIP device every entry
 // point fails with AZ_ERR_HIP.
 #include <hip/hip_runtime.h>
+#include <pthread.h>
 #include <sched.h>
 
 #include <algorithm>
@@ -205,6 +206,9 @@ struct az_net {
     float* rw_ws = nullptr;           // their split-K partials [rw_splits][rows][F]
     bool loaded = false;
     std::vector<float> host_blob;   // canonical blob of the loaded weights (az_net_get_weights)
+    // the device buffers of the loaded weights, in allocation order (recorded at the first load;
+    // later loads rewrite the same buffers): what az_net_broadcast_weights sends
+    std::vector<std::pair<void*, size_t>> wbufs;
     // every activation / workspace buffer (pointer, bytes before any zeroed tail): the poison
     // diagnostic (az_diag_set_poison) overwrites them before each forward
     std::vector<std::pair<void*, size_t>> scratch;
@@ -1393,6 +1397,7 @@ void prefetch_noise(az_search* s, float alpha, const std::vector<uint8_t>& want)
     P.on = true;
     P.alpha = alpha;
     P.job = std::async(std::launch::async, [s, alpha, G, NA] {
+        pthread_setname_np(pthread_self(), "az-noise-pf");   // named in crash reports (az_diag_crash_report)
         auto& Q = s->pf;
         for (int g = 0; g < G; ++g) {
             if (Q.nc[g] < 0) continue;
@@ -1428,6 +1433,7 @@ int search_noise(az_search* s, float alpha, float eps, const uint8_t* mask) {
         inline_games += !(pfo && nc > 0 && P.nc[g] == nc);
     }
     auto draw = [&](int g0, int g1) {
+        if (g0 > 0) pthread_setname_np(pthread_self(), "az-gamma");   // the workers (g0 = 0: the caller)
         for (int g = g0; g < g1; ++g) {
             s->h_mask[g] = 0;
             if (!s->active[g] || (mask && !mask[g])) continue;
@@ -1876,11 +1882,40 @@ int az_net_load_weights(az_net* n, const float* blob, size_t count) {
     if (count != n->nparams) return az_fail(AZ_ERR_ARG, "expected %zu parameters, got %zu", n->nparams, count);
     std::lock_guard<std::mutex> lk(n->mu);
     HIPCHK(hipSetDevice(n->e->device));
-    if (int r = n->rw ? net_load_rw(n, blob) : net_load(n, blob)) return r;
+    {
+        // the first load allocates the weight buffers: record them (net_weight_buffers)
+        WeightRegistry reg(n->wbufs.empty() ? &n->wbufs : nullptr);
+        if (int r = n->rw ? net_load_rw(n, blob) : net_load(n, blob)) return r;
+    }
     HIPCHK(hipDeviceSynchronize());   // null-stream uploads done before the non-blocking stream reads them
     n->host_blob.assign(blob, blob + count);
     return 0;
 }
+
+}  // extern "C"
+// ---- net internals for dist.hip (engine_internal.h), C++ linkage
+int net_weight_buffers(az_net* n, std::vector<std::pair<void*, size_t>>& out) {
+    if (n->wbufs.empty()) {
+        // never loaded: a load of zero weights allocates (and records) every weight buffer, which a
+        // broadcast then overwrites (host work once per net, no device traffic beyond the uploads)
+        std::vector<float> zero(n->nparams, 0.0f);
+        WeightRegistry reg(&n->wbufs);
+        if (int r = n->rw ? net_load_rw(n, zero.data()) : net_load(n, zero.data())) return r;
+        HIPCHK(hipDeviceSynchronize());
+        n->loaded = false;
+    }
+    out = n->wbufs;
+    return 0;
+}
+const std::vector<float>& net_host_blob(az_net* n) { return n->host_blob; }
+size_t net_param_count(az_net* n) { return n->nparams; }
+az_engine* net_engine(az_net* n) { return n->e; }
+std::mutex& net_mutex(az_net* n) { return n->mu; }
+void net_adopt_blob(az_net* n, const float* blob) {
+    n->host_blob.assign(blob, blob + n->nparams);
+    n->loaded = true;
+}
+extern "C" {
 
 int az_net_get_weights(az_net* n, float* blob, size_t count) {
     if (!n || !blob) return az_fail(AZ_ERR_ARG, "null argument");

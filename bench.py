@@ -7,8 +7,9 @@ contiguous global game ids), 800 simulations per move, the reference's playSingl
 (Dirichlet noise, temperature schedule, subtree reuse, per-game transposition table).  One step
 = one committed move of every game (800 batched simulations: PUCT select -> leaf batch through
 the ConvNet -> expand / backup), with the MoveData records of every move assembled on the host.
-Games shard across ranks with no data-path collective; RCCL only broadcasts rank 0's weights
-and reduces the counters.  `--scaling weak` keeps 2048 games per GPU instead.
+Games shard across ranks with no data-path collective; RCCL -- the engine's own communicator
+(az_dist_*, csrc/dist.hip) -- only broadcasts rank 0's weights into every rank's device weight
+buffers, reduces the counters and runs the timing barriers.  `--scaling weak` keeps 2048 games per GPU instead.
 
   --config c2   BASELINE.json configs[1]: 15x15, 6b x 64f, 256 games, 400 sims, 1 GPU
   --config c4   BASELINE.json configs[3]: Go 19x19 (GoState on device), 8 planes, 362 actions,
@@ -121,6 +122,9 @@ def parse(argv=None):
                     help="diagnostic: a host synchronisation after every N simulation steps (0: none). "
                          "rocprofv3 --pmc stalls on a selfplay step's unsynchronised queue of dispatches "
                          "(DESIGN.md section 7); tools/tree_pmc.sh passes 100")
+    ap.add_argument("--crash-report", default=None,
+                    help="diagnostic: on a fault in any thread, append the thread's name, the fault address, the PC "
+                         "and /proc/self/maps to this file (az_diag_crash_report), then the previous handler runs")
     ap.add_argument("--dist-timeout", type=float, default=600.0,
                     help="seconds a rank waits in a collective / barrier before the bench fails (N>1)")
     a = ap.parse_args(argv)
@@ -203,7 +207,7 @@ class GpuWorkload:
         pass                           # selfplayStep returns after a stream synchronize
 
     def close(self):
-        """Free the device search and net (the parity-mode run allocates a workload of the same size)."""
+        """Free the device search, the net and the engine."""
         if self.mcts is not None:
             self.mcts.close()
             self.mcts = None
@@ -262,15 +266,71 @@ def _roofline(a, m, precision):
     return rf
 
 
-def run_rank(a, rank, world, dist, make_workload, coll_device, parity=None):
+class EngineColl:
+    """The product collectives (N>1): the engine's own RCCL communicator (az_dist_*) over the
+    ranks' engines -- rank 0's weights broadcast straight into every rank's device weight buffers,
+    device-level barriers, counter reductions.  torch.distributed (gloo) only hands out the id."""
+
+    def __init__(self, engine, rank, world, pg, timeout_s):
+        from az_amd import dist as azdist
+        box = [azdist.Dist.unique_id() if rank == 0 else None]
+        pg.broadcast_object_list(box, src=0)
+        self.d = azdist.Dist(engine, rank, world, box[0], timeout_s)
+        self.kind = "rccl (engine az_dist_*)"
+
+    def broadcast_weights(self, net):
+        self.d.broadcast_weights(net, 0)
+
+    def barrier(self):
+        self.d.barrier()
+
+    def reduce(self, elapsed, counters):
+        mx = self.d.allreduce([elapsed], "max")[0]
+        return mx, [int(round(v)) for v in self.d.allreduce(counters, "sum")]
+
+    def close(self):
+        self.d.close()
+
+
+class TorchColl:
+    """The same collectives over a torch.distributed group (gloo on CPU: the rank-logic tests)."""
+
+    def __init__(self, pg, device="cpu"):
+        self.pg, self.device = pg, device
+        self.kind = f"torch.distributed {pg.get_backend()}"
+
+    def broadcast_weights(self, net):
+        from az_amd import dist as azdist
+        blob = net.get_weights() if self.pg.get_rank() == 0 else None
+        blob = azdist.broadcast_weights(self.pg, blob, net.num_params, self.device)
+        if self.pg.get_rank() != 0:
+            net.load_weights(blob)
+
+    def barrier(self):
+        self.pg.barrier()
+
+    def reduce(self, elapsed, counters):
+        from az_amd import dist as azdist
+        return azdist.reduce_counters(self.pg, elapsed, counters, self.device)
+
+    def close(self):
+        pass
+
+
+def run_rank(a, rank, world, make_workload, make_coll=None, parity=None):
     """One rank of the bench: shard, weights (rank 0 init + broadcast), warmup, timed steps between
     barriers, MAX elapsed / SUM counters over ranks.  Returns the JSON dict on rank 0, else None.
+    make_coll(workload) (N>1): the collectives (EngineColl on the GPUs, TorchColl in the CPU tests).
     parity (N=1): parity(ms_per_step) -> number of further moves to time with the parity precision
     (the live net switched in place, the same games continued), or a string saying why not."""
     from az_amd import dist as azdist
     sh = azdist.shard_range(rank, world, a.global_games if a.scaling == "strong" else a.global_games * world)
     if sh["games"] < 1:
         raise SystemExit(f"bench.py: rank {rank} got no games ({a.global_games} over {world} ranks)")
+    if getattr(a, "crash_report", None):     # diagnostic: symbolisable crash reports (profiler runs)
+        from az_amd import _lib
+        if _lib.lib().az_diag_crash_report(a.crash_report.encode()) != 0:
+            raise RuntimeError("az_diag_crash_report failed")
     if getattr(a, "sync_every", 0):
         from az_amd import _lib
         _lib.lib().az_diag_set_sync_every(int(a.sync_every))
@@ -283,21 +343,29 @@ def run_rank(a, rank, world, dist, make_workload, coll_device, parity=None):
         L.az_diag_set_conv_flags(L.az_diag_conv_flags() | int(a.conv_flags, 16))
     wl = make_workload(a, int(os.environ.get("LOCAL_RANK", "0")), sh)
     net = wl.net
+    coll = make_coll(wl) if world > 1 else None
+    try:
+        return _run_rank(a, rank, world, sh, wl, net, coll, parity)
+    finally:
+        if coll is not None:
+            coll.close()
+        if hasattr(wl, "close"):         # the device search, net and engine (after the communicator)
+            wl.close()
+
+
+def _run_rank(a, rank, world, sh, wl, net, coll, parity):
     if rank == 0:
         net.init_random(a.seed)
-    if world > 1:
-        blob = net.get_weights() if rank == 0 else None
-        blob = azdist.broadcast_weights(dist, blob, net.num_params, coll_device)   # RCCL over xGMI, once
-        if rank != 0:
-            net.load_weights(blob)
+    if coll is not None:
+        coll.broadcast_weights(net)          # rank 0's weights on every rank, once (RCCL over xGMI)
     wl.start()
     for _ in range(a.warmup):
         wl.step()
 
     def barrier():
         wl.sync()
-        if dist is not None:
-            dist.barrier()
+        if coll is not None:
+            coll.barrier()
     m = _timed_moves(a, wl, net, a.steps, barrier)
     pm = None
     if parity is not None and world == 1:
@@ -311,11 +379,9 @@ def run_rank(a, rank, world, dist, make_workload, coll_device, parity=None):
             for _ in range(a.parity_warmup):
                 wl.step()
             pm = _timed_moves(a, wl, net, n_par, barrier)
-    if hasattr(wl, "close"):
-        wl.close()
     elapsed, tot_moves, tot_evals = m["elapsed"], m["moves"], m["evals"]
-    if dist is not None:
-        elapsed, (tot_moves, tot_evals) = azdist.reduce_counters(dist, elapsed, [m["moves"], m["evals"]], coll_device)
+    if coll is not None:
+        elapsed, (tot_moves, tot_evals) = coll.reduce(elapsed, [m["moves"], m["evals"]])
     if rank != 0:
         return None
     strong = a.scaling == "strong"
@@ -337,7 +403,8 @@ def run_rank(a, rank, world, dist, make_workload, coll_device, parity=None):
                                f"{' sharded' if strong else ''} over {world} GPU(s), {a.sims} sims/move",
                    "baseline_config": a.config, "game": a.game, "global_games": a.global_games if strong else
                    a.global_games * world, "games_per_gpu": sh["games"], "sims_per_move": a.sims, "board": a.board,
-                   "blocks": a.blocks, "channels": a.channels, "parallelism": f"game-shard x{world}"},
+                   "blocks": a.blocks, "channels": a.channels, "parallelism": f"game-shard x{world}",
+                   "collectives": coll.kind if coll is not None else None},
         "nn_evals_per_s": tot_evals / elapsed,
         "evals_per_move": tot_evals / max(1, tot_moves),
         "roofline": _roofline(a, m, a.precision),
@@ -578,26 +645,29 @@ def main(argv=None, make_workload=None, backend=None):
         raw_cpu = cpu_baseline(a, a.cpu_workers or cpu_share(), a.cpu_window)
     make_workload = make_workload or GpuWorkload
     dist = None
-    dev = "cpu"
+    make_coll = None
     if world > 1:
         import datetime
         import torch
         import torch.distributed as dist
         split_affinity(local, int(os.environ.get("LOCAL_WORLD_SIZE", str(world))))
-        if backend is None:
-            if torch.cuda.device_count() <= local:
-                print(f"bench.py: LOCAL_RANK {local} but {torch.cuda.device_count()} GPU(s) visible", file=sys.stderr)
-                return 2
-            torch.cuda.set_device(local)
-            dev = f"cuda:{local}"
-        # a rank that dies leaves the others in a collective: they fail after dist_timeout, not hang
-        dist.init_process_group(backend or "nccl", init_method="env://",
+        if backend is None and torch.cuda.device_count() <= local:
+            print(f"bench.py: LOCAL_RANK {local} but {torch.cuda.device_count()} GPU(s) visible", file=sys.stderr)
+            return 2
+        # gloo: the bootstrap group (hands out the engine communicator's id) -- or, with a test
+        # backend, the collectives themselves.  A rank that dies leaves the others in a collective:
+        # they fail after dist_timeout (gloo's timeout, the engine's RCCL deadline), not hang.
+        dist.init_process_group(backend or "gloo", init_method="env://",
                                 timeout=datetime.timedelta(seconds=a.dist_timeout))
+        if backend is None:
+            make_coll = lambda wl: EngineColl(wl.eng, rank, world, dist, a.dist_timeout)   # noqa: E731
+        else:
+            make_coll = lambda wl: TorchColl(dist, "cpu")                                 # noqa: E731
     try:
         parity = None
         if world == 1 and a.parity_steps > 0 and a.precision not in ("f16x3", "bf16x3") and a.channels % 64 == 0:
             parity = parity_budget(a)
-        out = run_rank(a, rank, world, dist, make_workload, dev, parity=parity)
+        out = run_rank(a, rank, world, make_workload, make_coll, parity=parity)
         if out is not None:
             out["cpu_baseline"] = cpu_baseline_line(a, raw_cpu, out["evals_per_move"]) if raw_cpu else None
             print(json.dumps(out), flush=True)

@@ -17,6 +17,8 @@
  *                 (include/alphazero/mcts/parallel_mcts.h:131-201)
  *   az_selfplay_* alphazero::selfplay::SelfPlayManager::generateGames / playSingleGame
  *                 (src/selfplay/self_play_manager.cpp:47-234)
+ *   az_dist_*     the per-GPU process sharding of python/scripts/orchestrate_selfplay.py:303-311,
+ *                 741-749, with RCCL for the weights and the counters
  */
 #ifndef AZ_ENGINE_H
 #define AZ_ENGINE_H
@@ -372,6 +374,32 @@ int az_dataset_gather(az_dataset* d, const int64_t* idx, int n, float* states, f
 /* Measurement: time (HIP events on the engine stream) and algorithmic HBM bytes of the last
  * extraction kernel. */
 int az_dataset_profile_read(az_dataset* d, double* extract_ms, double* bytes);
+
+/* ------------------------------------------------------------ multi-GPU */
+/* One process per GPU (the reference's per-GPU self_play processes,
+ * python/scripts/orchestrate_selfplay.py:303-311,741-749), games sharded by contiguous global id
+ * ranges with no data-path collective; RCCL over xGMI only to broadcast the weights and to reduce
+ * the counters.  Rank 0 makes the id (az_dist_unique_id) and hands it to
+ * every rank out of band (a file, a launcher's store); each rank calls az_dist_init with its own
+ * engine.  Collectives run on the engine's stream and wait with a deadline: after timeout_ms
+ * (<= 0: 600 s) without completion -- a rank died or never joined -- the communicator is aborted
+ * and the call returns AZ_ERR_STATE, as does every later call on the handle. */
+#define AZ_DIST_ID_BYTES 128
+typedef struct az_dist az_dist;
+enum az_dist_op { AZ_DIST_SUM = 0, AZ_DIST_MAX = 1 };
+int az_dist_unique_id(unsigned char* id);   /* id[AZ_DIST_ID_BYTES] */
+int az_dist_init(az_engine* e, int rank, int world, const unsigned char* id, int timeout_ms, az_dist** out);
+void az_dist_destroy(az_dist* d);
+int az_dist_info(az_dist* d, int* rank, int* world);
+/* Every rank's engine stream drained and every rank arrived. */
+int az_dist_barrier(az_dist* d);
+/* out[i] = SUM or MAX over the ranks of in[i], i < count (1..64); host buffers (out may be in). */
+int az_counters_allreduce(az_dist* d, const double* in, double* out, int count, int op);
+/* Rank root's loaded weights into net n on every rank: ncclBroadcast straight into the net's
+ * packed device weight buffers (every precision's piece set) and the canonical fp32 blob
+ * (az_net_get_weights); no host hop on the device path.  The nets must share one az_net_desc
+ * (checked); a never-loaded net on a non-root rank is allocated first. */
+int az_net_broadcast_weights(az_dist* d, az_net* n, int root);
 
 #ifdef __cplusplus
 }

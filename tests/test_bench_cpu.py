@@ -95,7 +95,7 @@ def _rank(rank, world, port, q):
         def make(a_, local, shard):
             wls.append(_Workload(a_, local, shard))
             return wls[-1]
-        out = bench.run_rank(a, rank, world, dist, make, "cpu")
+        out = bench.run_rank(a, rank, world, make, lambda wl: bench.TorchColl(dist, "cpu"))
         w = wls[0]
         q.put((rank, out, w.shard, None if w.net.loaded is None else float(w.net.loaded.sum()), w.steps))
     finally:
@@ -257,7 +257,7 @@ def test_bench_parity_mode_in_place_world1():
     def make(a_, local, shard):
         wls.append(_Workload(a_, local, shard))
         return wls[-1]
-    out = bench.run_rank(a, 0, 1, None, make, "cpu", parity=bench.parity_budget(a))
+    out = bench.run_rank(a, 0, 1, make, parity=bench.parity_budget(a))
     w = wls[0]
     assert len(wls) == 1 and w.steps == 2 + 3 + 2          # one workload: warmup, headline, parity moves
     assert w.net.precision == bench.PREC["f16x3"]
@@ -269,6 +269,6 @@ def test_bench_parity_mode_in_place_world1():
     # the budget: an estimate past --time-budget skips the parity moves and names the numbers
     b = bench.parse(["--steps", "3", "--warmup", "2", "--parity-steps", "2", "--time-budget", "1"])
     wls.clear()
-    out = bench.run_rank(b, 0, 1, None, make, "cpu", parity=bench.parity_budget(b))
+    out = bench.run_rank(b, 0, 1, make, parity=bench.parity_budget(b))
     assert "skipped" in out["parity_mode"] and "time budget" in out["parity_mode"]["skipped"]
     assert wls[0].steps == 5 and wls[0].net.precision is None

@@ -19,7 +19,8 @@ mkdir -p $O
 # queues thousands of dispatches without a host synchronisation: BLOCKS=2 passes at SYNC=100 (~600
 # queued dispatches), BLOCKS=20 crashes at SYNC=100 (~4,300: 41 per simulation step) with the 560-byte
 # TreeDev kernargs (r04) and with the round-5 8-byte device-resident TreeDev alike -- so not the
-# kernarg size -- and passes at SYNC=10 (~430; profiles/r05_tree_pmc_c3.json)
+# kernarg size -- and passes at SYNC=10 (~430; profiles/r05_tree_pmc_c3.json).  The counter passes
+# run with --crash-report: a crash leaves $O/crash_<pass>.txt (thread name, PC, /proc/self/maps)
 if [ "${CONFIG:-c3}" = c2 ]; then
   CMD="python3 bench.py --config c2 --cpu-baseline 0 --parity-steps 0 --steps 1 --warmup 0 --sync-every ${SYNC:-10}"
 else
@@ -29,8 +30,8 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/tra
 ( while sleep 30; do echo "pmc pass running ($(date +%T))"; done ) &
 HB=$!
 trap "kill $HB 2>/dev/null" EXIT
-timeout -s KILL ${PMC_TIMEOUT:-240} rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/fetch -o run -- $CMD --kernel-timing ${KT:-1} > $O/fetch.log 2>&1 || { echo FAIL fetch; tail -3 $O/fetch.log; exit 1; }
-timeout -s KILL ${PMC_TIMEOUT:-240} rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/write -o run -- $CMD --kernel-timing ${KT:-1} > $O/write.log 2>&1 || { echo FAIL write; tail -3 $O/write.log; exit 1; }
+timeout -s KILL ${PMC_TIMEOUT:-240} rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/fetch -o run -- $CMD --kernel-timing ${KT:-1} --crash-report $O/crash_fetch.txt > $O/fetch.log 2>&1 || { echo FAIL fetch; tail -3 $O/fetch.log; exit 1; }
+timeout -s KILL ${PMC_TIMEOUT:-240} rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/write -o run -- $CMD --kernel-timing ${KT:-1} --crash-report $O/crash_write.txt > $O/write.log 2>&1 || { echo FAIL write; tail -3 $O/write.log; exit 1; }
 kill $HB 2>/dev/null
 O=$O SIMS=${SIMS:-800} BLOCKS=${BLOCKS:-20} CONFIG=${CONFIG:-c3} python3 - <<'PY'
 import collections, csv, glob, json, os, re
