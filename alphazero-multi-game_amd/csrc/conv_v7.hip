@@ -187,6 +187,11 @@ __global__ __launch_bounds__(256, RG == 3 ? 3 : 2) void conv3x3_v7(ConvBf16Args 
     typedef typename std::conditional<MODE == 2, f16x8, bf16x8>::type frag;
     constexpr int BNT = 128, WG = GM::WG, HW = GM::HW, HROWS = GM::HROWS, NRB = GM::NRB;
     constexpr int NI = TM / 32, NA = NI <= 4 ? NI : NI / 2, HALVES = NI / NA;   // fragments per wave / per A set
+#ifdef AZ_V7_NOSKIP
+    constexpr bool SKIP = false;
+#else
+    constexpr bool SKIP = SLIM && HALVES == 2;            // waves wm = 1 skip the SLIM tile's dead 16th fragment
+#endif
     static_assert(NA * HALVES == NI && NA <= 4, "fragment split");
     static_assert(RG == 4 || (RG == 3 && TM <= 128), "ring");
     constexpr int WR = TM / 2;                            // rows per wave
@@ -296,7 +301,6 @@ __global__ __launch_bounds__(256, RG == 3 ? 3 : 2) void conv3x3_v7(ConvBf16Args 
     wait_vm(2 * (RG - 1));                                // A(0), B(0) landed; B(1..RG-1) may fly
     __builtin_amdgcn_s_barrier();
 
-    frag alo[4], ahi[4], bw[2][4];
     auto maskA = [&](frag (&a)[4], int half, int dy, int dx) {
         if constexpr (DENSE) {
             const uint32_t test = (dy == 0 ? 4u : dy == 2 ? 8u : 0u) | (dx == 0 ? 1u : dx == 2 ? 2u : 0u);
@@ -307,99 +311,117 @@ __global__ __launch_bounds__(256, RG == 3 ? 3 : 2) void conv3x3_v7(ConvBf16Args 
             }
         }
     };
-    // fragments of tap t (compile time) of the chunk in A buffer `ab`, weights in slot `bs`
-    // SLIM: the 16th fragment (rows 240..255, no live outputs) of the second row half reads 16 rows
-    // further on, where every halo row of every tap is zero (rows >= 256: halo row Y >= 16)
-    const uint32_t z16 = (SLIM && wm == 1) ? 16 * 16 : 0;
-    auto loadA = [&](frag (&a)[4], uint32_t ab, auto tc, auto hc) {
-        constexpr int t = decltype(tc)::value, half = decltype(hc)::value;
-        constexpr int sh = (t / 3) * WG + (t % 3);
-        static_for<0, NA>([&](auto ic) {
-            constexpr int i = decltype(ic)::value;
-            if constexpr (SLIM && half == 1 && i == 3) ds_rd<((half * NA + i) * 16 + sh) * 16>(a[i], ab + z16);
-            else ds_rd<((half * NA + i) * 16 + sh) * 16>(a[i], ab);
-        });
-    };
-    auto loadB = [&](frag (&b)[4], uint32_t bs) {
-        static_for<0, 4>([&](auto jc) {
-            constexpr int j = decltype(jc)::value;
-            ds_rd<j * 256>(b[j], bs);
-        });
-    };
-    auto mma = [&](const frag (&a)[4], const frag (&b)[4], int half) {
-#pragma unroll
-        for (int i = 0; i < NA; ++i) {
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                if constexpr (MODE == 2)
-                    acc[half * NA + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(b[j], a[i], acc[half * NA + i][j], 0, 0, 0);
-                else
-                    acc[half * NA + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a[i], acc[half * NA + i][j], 0, 0, 0);
-            }
-        }
-    };
     using I0 = std::integral_constant<int, 0>;
     using I1 = std::integral_constant<int, 1>;
-    // tap 0 of chunk 0
-    loadB(bw[0], b_lane);
-    loadA(alo, a_lane, I0{}, I0{});
-    if constexpr (HALVES == 2) loadA(ahi, a_lane, I0{}, I1{});
-
-    // Two chunks per iteration: 18 taps, the weight registers alternate by tap parity.  Every tap
-    // issues the same DMA pieces (a halo piece at taps 0..4, two weight pieces), past the end as
-    // harmless reloads into free buffers, so the vmcnt budget is a compile-time constant: the
-    // weights of tap s+1 were issued in tap s-RG+1 (the prologue for s < RG-1), followed by the
-    // pieces of the RG-2 taps after it.  Fragments are read one tap ahead, past the end from free buffers.
-    for (int c2 = 0; c2 < NCH; c2 += 2) {
-        static_for<0, 18>([&](auto tc18) {
-            constexpr int T = decltype(tc18)::value;      // tap of the chunk pair
-            constexpr int t = T % 9, cur = T & 1, nxt = cur ^ 1;
-            constexpr int allow = RG == 4 ? (t >= 2 && t - 2 < NRB ? 1 : 0) + (t >= 1 && t - 1 < NRB ? 1 : 0) + 4
-                                          : (t >= 1 && t - 1 < NRB ? 1 : 0) + 2;
-            constexpr int NAF = NA * HALVES;              // activation fragment reads per tap
-            const int c = c2 + T / 9;
-            const int s = 9 * c + t;
-            if constexpr (DENSE) asm volatile("" : "+v"(mbits));   // keep the edge masks inside the loop (no SGPR hoisting)
-            // the NAF youngest LDS reads are this tap's activation fragments: the weights of tap s
-            // (read one tap ago) are in registers -- required before the barrier frees their slot
-            lgkm<NAF>(bw[cur]);
-            wait_vm(allow);                               // weights of tap s+1 (and at t == 8 the next halo) landed
-            __builtin_amdgcn_s_barrier();
-            __builtin_amdgcn_sched_barrier(0);
-            // DMA for later taps: a halo piece of chunk c+1 at taps 0..NRB-1 (the last chunk reloads
-            // itself into the free buffer), then the weights of tap s+RG (clamped to the last tap)
-            if constexpr (t < NRB) issueA(t, c + 1 < NCH ? c + 1 : c, (c + 1) & 1);
-            issueB(s + RG < NS ? s + RG : NS - 1, (s + RG) % RG);
-            // weights of tap s+1 (certified by the barrier above)
-            loadB(bw[nxt], b_lane + ((s + 1) % RG) * B_TAP);
-            __builtin_amdgcn_sched_barrier(0);
-            lgkm<(HALVES - 1) * NA + 4>(alo);             // activations of tap s, low half
-            maskA(alo, 0, t / 3, t % 3);
-            mma(alo, bw[cur], 0);
-            __builtin_amdgcn_sched_barrier(0);
-            const uint32_t an = a_lane + ((t == 8 ? c + 1 : c) & 1) * A_BUF;
-            constexpr int tn = (t + 1) % 9;
-            loadA(alo, an, std::integral_constant<int, tn>{}, I0{});
-            if constexpr (HALVES == 2) {
-                lgkm<4 + NA>(ahi);                        // activations of tap s, high half
-                maskA(ahi, 1, t / 3, t % 3);
-                __builtin_amdgcn_sched_barrier(0);
-                mma(ahi, bw[cur], 1);
-                __builtin_amdgcn_sched_barrier(0);
-                loadA(ahi, an, std::integral_constant<int, tn>{}, I1{});
+    // The main loop, compiled once per row half of the tile (WMC = wm, a wave-uniform branch): on the
+    // SLIM grid the second half's 16th fragment (grid rows 240..255) holds no live output, so with
+    // SKIP waves wm = 1 neither read nor multiply it -- 1/16 of the tile's MFMAs and fragment reads
+    // (as conv3x3_v9x3's SKIP variant).  -DAZ_V7_NOSKIP builds the round-5 kernel (A/B measurement),
+    // where those MFMAs run on all-zero halo rows.
+    auto main_loop = [&](auto wmc) {
+        constexpr int WMC = decltype(wmc)::value;
+        constexpr int NI1 = (SKIP && WMC == 1) ? NA - 1 : NA;   // fragments of the second A set this wave computes
+        frag alo[4], ahi[4], bw[2][4];
+        // fragments of tap t (compile time) of the chunk in A buffer `ab`, weights in slot `bs`
+        // SLIM without SKIP: the 16th fragment (rows 240..255, no live outputs) of the second row half
+        // reads 16 rows further on, where every halo row of every tap is zero (rows >= 256: halo row Y >= 16)
+        const uint32_t z16 = (SLIM && wm == 1) ? 16 * 16 : 0;
+        auto loadA = [&](frag (&a)[4], uint32_t ab, auto tc, auto hc) {
+            constexpr int t = decltype(tc)::value, half = decltype(hc)::value;
+            constexpr int sh = (t / 3) * WG + (t % 3);
+            static_for<0, NA>([&](auto ic) {
+                constexpr int i = decltype(ic)::value;
+                if constexpr (half == 1 && i >= NI1) return;
+                else if constexpr (SLIM && half == 1 && i == 3) ds_rd<((half * NA + i) * 16 + sh) * 16>(a[i], ab + z16);
+                else ds_rd<((half * NA + i) * 16 + sh) * 16>(a[i], ab);
+            });
+        };
+        auto loadB = [&](frag (&b)[4], uint32_t bs) {
+            static_for<0, 4>([&](auto jc) {
+                constexpr int j = decltype(jc)::value;
+                ds_rd<j * 256>(b[j], bs);
+            });
+        };
+        auto mma = [&](const frag (&a)[4], const frag (&b)[4], auto hc) {
+            constexpr int half = decltype(hc)::value, NIH = half == 1 ? NI1 : NA;
+#pragma unroll
+            for (int i = 0; i < NIH; ++i) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    if constexpr (MODE == 2)
+                        acc[half * NA + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(b[j], a[i], acc[half * NA + i][j], 0, 0, 0);
+                    else
+                        acc[half * NA + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a[i], acc[half * NA + i][j], 0, 0, 0);
+                }
             }
-            __builtin_amdgcn_sched_barrier(0);
-        });
+        };
+        // tap 0 of chunk 0
+        loadB(bw[0], b_lane);
+        loadA(alo, a_lane, I0{}, I0{});
+        if constexpr (HALVES == 2) loadA(ahi, a_lane, I0{}, I1{});
+
+        // Two chunks per iteration: 18 taps, the weight registers alternate by tap parity.  Every tap
+        // issues the same DMA pieces (a halo piece at taps 0..4, two weight pieces), past the end as
+        // harmless reloads into free buffers, so the vmcnt budget is a compile-time constant: the
+        // weights of tap s+1 were issued in tap s-RG+1 (the prologue for s < RG-1), followed by the
+        // pieces of the RG-2 taps after it.  Fragments are read one tap ahead, past the end from free buffers.
+        for (int c2 = 0; c2 < NCH; c2 += 2) {
+            static_for<0, 18>([&](auto tc18) {
+                constexpr int T = decltype(tc18)::value;      // tap of the chunk pair
+                constexpr int t = T % 9, cur = T & 1, nxt = cur ^ 1;
+                constexpr int allow = RG == 4 ? (t >= 2 && t - 2 < NRB ? 1 : 0) + (t >= 1 && t - 1 < NRB ? 1 : 0) + 4
+                                              : (t >= 1 && t - 1 < NRB ? 1 : 0) + 2;
+                constexpr int NAF = NA + (HALVES - 1) * NI1;  // activation fragment reads per tap
+                const int c = c2 + T / 9;
+                const int s = 9 * c + t;
+                if constexpr (DENSE) asm volatile("" : "+v"(mbits));   // keep the edge masks inside the loop (no SGPR hoisting)
+                // the NAF youngest LDS reads are this tap's activation fragments: the weights of tap s
+                // (read one tap ago) are in registers -- required before the barrier frees their slot
+                lgkm<NAF>(bw[cur]);
+                wait_vm(allow);                               // weights of tap s+1 (and at t == 8 the next halo) landed
+                __builtin_amdgcn_s_barrier();
+                __builtin_amdgcn_sched_barrier(0);
+                // DMA for later taps: a halo piece of chunk c+1 at taps 0..NRB-1 (the last chunk reloads
+                // itself into the free buffer), then the weights of tap s+RG (clamped to the last tap)
+                if constexpr (t < NRB) issueA(t, c + 1 < NCH ? c + 1 : c, (c + 1) & 1);
+                issueB(s + RG < NS ? s + RG : NS - 1, (s + RG) % RG);
+                // weights of tap s+1 (certified by the barrier above)
+                loadB(bw[nxt], b_lane + ((s + 1) % RG) * B_TAP);
+                __builtin_amdgcn_sched_barrier(0);
+                lgkm<(HALVES - 1) * NI1 + 4>(alo);            // activations of tap s, low half
+                maskA(alo, 0, t / 3, t % 3);
+                mma(alo, bw[cur], I0{});
+                __builtin_amdgcn_sched_barrier(0);
+                const uint32_t an = a_lane + ((t == 8 ? c + 1 : c) & 1) * A_BUF;
+                constexpr int tn = (t + 1) % 9;
+                loadA(alo, an, std::integral_constant<int, tn>{}, I0{});
+                if constexpr (HALVES == 2) {
+                    lgkm<4 + NA>(ahi);                        // activations of tap s, high half
+                    maskA(ahi, 1, t / 3, t % 3);
+                    __builtin_amdgcn_sched_barrier(0);
+                    mma(ahi, bw[cur], I1{});
+                    __builtin_amdgcn_sched_barrier(0);
+                    loadA(ahi, an, std::integral_constant<int, tn>{}, I1{});
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            });
+        }
+        // drain: the last tap's fragment reads (past the end) may still be in flight.  The compiler does
+        // not see them, so without the fragments as operands of the wait it reuses their registers in
+        // the epilogue, and a late LDS return overwrites a live value (seen as wrong outputs under LDS
+        // contention: three blocks per CU, tools/lds_hazards.py)
+        lgkm<0>(alo);
+        if constexpr (HALVES == 2) lgkm<0>(ahi);
+        lgkm<0>(bw[0]);
+        lgkm<0>(bw[1]);
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    };
+    if constexpr (SKIP) {
+        if (wm == 0) main_loop(I0{});
+        else main_loop(I1{});
+    } else {
+        main_loop(I0{});
     }
-    // drain: the last tap's fragment reads (past the end) may still be in flight.  The compiler does
-    // not see them, so without the fragments as operands of the wait it reuses their registers in
-    // the epilogue, and a late LDS return overwrites a live value (seen as wrong outputs under LDS
-    // contention: three blocks per CU, tools/lds_hazards.py)
-    lgkm<0>(alo);
-    if constexpr (HALVES == 2) lgkm<0>(ahi);
-    lgkm<0>(bw[0]);
-    lgkm<0>(bw[1]);
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
 
     // epilogue, straight from the accumulators: lane holds channels 4*(l >> 4) + e of pixel l16
     // of every 16 x 16 tile; residual join, ReLU, 16-bit + int8 split, streaming stores
