@@ -215,6 +215,11 @@ class GpuWorkload:
         self.eng.close()
 
 
+def _progress(msg):
+    """A progress line on stderr (the JSON line is the only stdout output)."""
+    print(f"[bench {time.perf_counter() - T_START:7.1f} s] {msg}", file=sys.stderr, flush=True)
+
+
 def _timed_moves(a, wl, net, steps, barrier):
     """`steps` self-play moves of the live workload between barriers, with the trunk / tree
     kernel clocks on: the raw counters of one timed region."""
@@ -224,10 +229,11 @@ def _timed_moves(a, wl, net, steps, barrier):
         wl.mcts.profile(True)
     t0 = time.perf_counter()
     moves = evals = 0
-    for _ in range(steps):
+    for k in range(steps):
         mv, ev = wl.step()
         moves += mv
         evals += ev
+        _progress(f"timed step {k + 1}/{steps}: {mv} moves, {time.perf_counter() - t0:.1f} s")
     wl.sync()
     elapsed = time.perf_counter() - t0
     barrier()
@@ -359,8 +365,9 @@ def _run_rank(a, rank, world, sh, wl, net, coll, parity):
     if coll is not None:
         coll.broadcast_weights(net)          # rank 0's weights on every rank, once (RCCL over xGMI)
     wl.start()
-    for _ in range(a.warmup):
+    for k in range(a.warmup):
         wl.step()
+        _progress(f"warmup step {k + 1}/{a.warmup}")
 
     def barrier():
         wl.sync()
@@ -643,6 +650,7 @@ def main(argv=None, make_workload=None, backend=None):
     raw_cpu = None
     if a.cpu_baseline and world == 1:
         raw_cpu = cpu_baseline(a, a.cpu_workers or cpu_share(), a.cpu_window)
+        _progress(f"cpu baseline: {raw_cpu['evals_per_s']:.1f} evals/s on {raw_cpu['cores']} cores")
     make_workload = make_workload or GpuWorkload
     dist = None
     make_coll = None

