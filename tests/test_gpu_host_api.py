@@ -98,6 +98,30 @@ def test_host_selfplay_manager_matches_oracle(tmp_path):
 
 
 @pytest.mark.gpu
+def test_host_selfplay_manager_shard_matches_oracle(tmp_path):
+    """SelfPlayManager.setShard (one rank's share of a per-GPU job, shardGames): rank 1 of 2 over 7
+    global games plays ids 4..6 -- the oracle's records of those ids (noise / evaluator streams by
+    global id), its record files named by the global id."""
+    import az_oracle as O
+    total, bs, sims, max_moves = 7, 7, 48, 20
+    refs = O.play(seed_stride=1, bs=bs, sims=sims, max_moves=max_moves, eval_kind=O.EVAL_RANDOM, eval_seed=5,
+                  n_games=total)
+    sh = az.shardGames(1, 2, total)
+    assert (sh.firstGame, sh.numGames, sh.noiseSeed) == (4, 3, 46)
+    mgr = az.SelfPlayManager(az.RandomPolicyNetwork(az.GameType.GOMOKU, bs, 5), 100, sims, 4)
+    mgr.setShard(sh)
+    mgr.setMaxMoves(max_moves)
+    mgr.setSaveGames(True, str(tmp_path))
+    recs = mgr.generateGames(az.GameType.GOMOKU, bs, False)
+    assert len(recs) == 3 and mgr.getFirstGameId() == 4
+    for k, rec in enumerate(recs):
+        ref = refs[4 + k]
+        got = [(m.action, bits(m.policy), bits([m.value])[0]) for m in rec.getMoves()]
+        assert got == [(r["action"], r["probs"], r["value"]) for r in ref["moves"]], 4 + k
+    assert sorted(f[:3] for f in os.listdir(tmp_path)) == ["004", "005", "006"]
+
+
+@pytest.mark.gpu
 def test_host_hip_network_predict_batch_matches_torch():
     """HipNeuralNetwork.predictBatch (planes built from GomokuState) == softmax of the fp32
     restatement, <= 1e-4 (north_star tolerance) at f32 precision."""
