@@ -13,6 +13,7 @@
 // they fail with AZ_ERR_STATE after the communicator's timeout (ncclCommAbort) instead of hanging.
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cstring>
 #include <thread>
@@ -190,13 +191,19 @@ int az_net_broadcast_weights(az_dist* d, az_net* n, int root) {
         d->blob_cap = np;
     }
     if (d->rank == root) HIPCHK(hipMemcpyAsync(d->blob, net_host_blob(n).data(), np * 4, hipMemcpyHostToDevice, st));
-    NCCLCHK(ncclGroupStart());
-    ncclResult_t gr = ncclBroadcast(d->blob, d->blob, np, ncclFloat32, root, d->comm, st);
-    for (size_t i = 0; gr == ncclSuccess && i < bufs.size(); ++i)
-        gr = ncclBroadcast(bufs[i].first, bufs[i].first, bufs[i].second, ncclUint8, root, d->comm, st);
-    const ncclResult_t ge = ncclGroupEnd();
-    if (gr != ncclSuccess) return nccl_fail(gr, "ncclBroadcast");
-    if (ge != ncclSuccess) return nccl_fail(ge, "ncclGroupEnd");
+    NCCLCHK(ncclBroadcast(d->blob, d->blob, np, ncclFloat32, root, d->comm, st));
+    // the packed buffers (~550 for a 20-block net) in groups of 64 broadcasts: one fused launch
+    // per group, well inside RCCL's per-group work limits
+    constexpr size_t GROUP = 64;
+    for (size_t g0 = 0; g0 < bufs.size(); g0 += GROUP) {
+        NCCLCHK(ncclGroupStart());
+        ncclResult_t gr = ncclSuccess;
+        for (size_t i = g0; gr == ncclSuccess && i < std::min(bufs.size(), g0 + GROUP); ++i)
+            gr = ncclBroadcast(bufs[i].first, bufs[i].first, bufs[i].second, ncclUint8, root, d->comm, st);
+        const ncclResult_t ge = ncclGroupEnd();
+        if (gr != ncclSuccess) return nccl_fail(gr, "ncclBroadcast");
+        if (ge != ncclSuccess) return nccl_fail(ge, "ncclGroupEnd");
+    }
     std::vector<float> host;
     if (d->rank != root) {
         host.resize(np);
