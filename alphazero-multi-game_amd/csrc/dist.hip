@@ -13,9 +13,13 @@
 // they fail with AZ_ERR_STATE after the communicator's timeout (ncclCommAbort) instead of hanging.
 #include <rccl/rccl.h>
 
+#include <pthread.h>
+
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstring>
+#include <memory>
 #include <thread>
 
 #include "engine_internal.h"
@@ -112,12 +116,36 @@ int az_dist_init(az_engine* e, int rank, int world, const unsigned char* id, int
     if (int r = dalloc(&d->dbuf, AZ_DIST_MAX_COUNTERS)) { delete d; return r; }
     ncclUniqueId u;
     std::memcpy(&u, id, AZ_DIST_ID_BYTES);
-    const ncclResult_t r = ncclCommInitRank(&d->comm, world, u, rank);
-    if (r != ncclSuccess) {
+    // ncclCommInitRank blocks until every rank joined: it runs on a helper thread, awaited with the
+    // communicator's deadline (a rank that never starts fails the others instead of hanging them;
+    // on a timeout the helper is left behind, blocked in RCCL, and the process is expected to exit)
+    struct Init {
+        ncclComm_t comm = nullptr;
+        ncclResult_t r = ncclInternalError;
+        std::atomic<bool> done{false};
+    };
+    auto job = std::make_shared<Init>();
+    const int dev = e->device;
+    std::thread([job, world, u, rank, dev] {
+        pthread_setname_np(pthread_self(), "az-rccl-init");
+        if (hipSetDevice(dev) == hipSuccess) job->r = ncclCommInitRank(&job->comm, world, u, rank);
+        job->done = true;
+    }).detach();
+    const auto t0 = std::chrono::steady_clock::now();
+    while (!job->done) {
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(d->timeout_ms)) {
+            (void)hipFree(d->dbuf);
+            delete d;
+            return az_fail(AZ_ERR_STATE, "ncclCommInitRank: not every rank joined within %d ms", timeout_ms > 0 ? timeout_ms : 600000);
+        }
+        std::this_thread::sleep_for(std::chrono::milliseconds(1));
+    }
+    if (job->r != ncclSuccess) {
         (void)hipFree(d->dbuf);
         delete d;
-        return nccl_fail(r, "ncclCommInitRank");
+        return nccl_fail(job->r, "ncclCommInitRank");
     }
+    d->comm = job->comm;
     *out = d;
     return 0;
 }

@@ -668,7 +668,17 @@ def main(argv=None, make_workload=None, backend=None):
         dist.init_process_group(backend or "gloo", init_method="env://",
                                 timeout=datetime.timedelta(seconds=a.dist_timeout))
         if backend is None:
-            make_coll = lambda wl: EngineColl(wl.eng, rank, world, dist, a.dist_timeout)   # noqa: E731
+            def make_coll(wl):
+                try:
+                    return EngineColl(wl.eng, rank, world, dist, a.dist_timeout)
+                except Exception as e:  # noqa: BLE001 -- said in the line (config.collectives) and on stderr
+                    # every rank fails the same way (the communicator's init is collective, with a
+                    # deadline): the run goes on over the gloo group rather than losing the measurement
+                    print(f"bench.py: rank {rank}: engine communicator failed ({e}); collectives over gloo",
+                          file=sys.stderr, flush=True)
+                    c = TorchColl(dist, "cpu")
+                    c.kind += f" (engine RCCL init failed: {e})"
+                    return c
         else:
             make_coll = lambda wl: TorchColl(dist, "cpu")                                 # noqa: E731
     try:
