@@ -662,6 +662,8 @@ def main(argv=None, make_workload=None, backend=None):
         if backend is None and torch.cuda.device_count() <= local:
             print(f"bench.py: LOCAL_RANK {local} but {torch.cuda.device_count()} GPU(s) visible", file=sys.stderr)
             return 2
+        # one node (the driver runs --nnodes=1): gloo's pairs over loopback, whatever the hostname resolves to
+        os.environ.setdefault("GLOO_SOCKET_IFNAME", "lo")
         # gloo: the bootstrap group (hands out the engine communicator's id) -- or, with a test
         # backend, the collectives themselves.  A rank that dies leaves the others in a collective:
         # they fail after dist_timeout (gloo's timeout, the engine's RCCL deadline), not hang.
