@@ -122,6 +122,9 @@ def parse(argv=None):
                     help="diagnostic: a host synchronisation after every N simulation steps (0: none). "
                          "rocprofv3 --pmc stalls on a selfplay step's unsynchronised queue of dispatches "
                          "(DESIGN.md section 7); tools/tree_pmc.sh passes 100")
+    ap.add_argument("--streams", type=int, default=1,
+                    help="N=1: split the games into this many device handles (own engine / HIP stream / net "
+                         "each) stepped concurrently by host threads (StreamWorkload)")
     ap.add_argument("--crash-report", default=None,
                     help="diagnostic: on a fault in any thread, append the thread's name, the fault address, the PC "
                          "and /proc/self/maps to this file (az_diag_crash_report), then the previous handler runs")
@@ -215,6 +218,100 @@ class GpuWorkload:
         self.eng.close()
 
 
+class _NetGroup:
+    """The nets of a StreamWorkload seen as one (rank 0's init on the first, copied to the others)."""
+
+    def __init__(self, nets):
+        self.nets = nets
+        self.num_params = nets[0].num_params
+
+    def init_random(self, seed):
+        self.nets[0].init_random(seed)
+        blob = self.nets[0].get_weights()
+        for n in self.nets[1:]:
+            n.load_weights(blob)
+
+    def get_weights(self):
+        return self.nets[0].get_weights()
+
+    def load_weights(self, blob):
+        for n in self.nets:
+            n.load_weights(blob)
+
+    def set_precision(self, p):
+        for n in self.nets:
+            n.set_precision(p)
+
+    def profile(self, on):
+        for n in self.nets:
+            n.profile(on)
+
+    def profile_read(self):
+        r = [n.profile_read() for n in self.nets]
+        return sum(x[0] for x in r), sum(x[1] for x in r), sum(x[2] for x in r)
+
+    def trunk_kernel(self):
+        return self.nets[0].trunk_kernel()
+
+
+class _MctsGroup:
+    def __init__(self, subs):
+        self.subs = subs
+
+    def profile(self, on):
+        for w in self.subs:
+            w.mcts.profile(on)
+
+    def profile_read(self):
+        out = {}
+        for w in self.subs:
+            for k, v in w.mcts.profile_read().items():
+                out[k] = out.get(k, 0) + v
+        return out
+
+    def tree_evictions(self):
+        return sum(w.mcts.tree_evictions() for w in self.subs)
+
+
+class StreamWorkload:
+    """`--streams K` (N = 1): the rank's games split into K independent device handles, each with its
+    own engine (HIP stream), net and search, stepped by K host threads at once -- so one handle's
+    tree kernels and small launches run beside another's network (the games are independent; each
+    keeps its global id's seeds, as a K-way shard).  For latency-bound configs (C2's 256 games, the
+    per-rank shards of the 8-GPU configs), where one handle's dependent chain of short launches
+    leaves CUs idle."""
+
+    def __init__(self, a, local, shard, k):
+        from az_amd import dist as azdist
+        self.subs = []
+        for i in range(k):
+            sub = azdist.shard_range(i, k, shard["games"])
+            sh = dict(shard, games=sub["games"], noise_seed=shard["noise_seed"] + sub["first_game"])
+            self.subs.append(GpuWorkload(a, local, sh))
+        self.eng = self.subs[0].eng
+        self.net = _NetGroup([w.net for w in self.subs])
+        self.mcts = None
+        import concurrent.futures
+        self.pool = concurrent.futures.ThreadPoolExecutor(k)
+
+    def start(self):
+        for w in self.subs:
+            w.start()
+        self.mcts = _MctsGroup(self.subs)
+
+    def step(self):
+        r = list(self.pool.map(lambda w: w.step(), self.subs))
+        return sum(x[0] for x in r), sum(x[1] for x in r)
+
+    def sync(self):
+        pass
+
+    def close(self):
+        self.pool.shutdown()
+        for w in self.subs:
+            w.close()
+
+
 def _progress(msg):
     """A progress line on stderr (the JSON line is the only stdout output)."""
     print(f"[bench {time.perf_counter() - T_START:7.1f} s] {msg}", file=sys.stderr, flush=True)
@@ -264,6 +361,9 @@ def _roofline(a, m, precision):
           # launches are trunk-conv equivalents (2 x blocks per forward); a fused forward (k_smallnet)
           # is one kernel launch per forward, whose rocprofv3 average is avg_forward_ms
           "forwards": m["forwards"], "avg_forward_ms": m["trunk_ms"] / max(1, m["forwards"])}
+    if getattr(a, "streams", 1) > 1:
+        rf["note"] = (f"{a.streams} streams: the handles' trunk launches overlap in time, so avg_launch_ms includes "
+                      "the other streams' share of the CUs and achieved / frac understate the chip's rate")
     b = copy.copy(a)
     b.precision = precision
     tr = pmc_traffic(b, m["kernel"], boards_per_launch if launches else 0)
@@ -410,7 +510,8 @@ def _run_rank(a, rank, world, sh, wl, net, coll, parity):
                                f"{' sharded' if strong else ''} over {world} GPU(s), {a.sims} sims/move",
                    "baseline_config": a.config, "game": a.game, "global_games": a.global_games if strong else
                    a.global_games * world, "games_per_gpu": sh["games"], "sims_per_move": a.sims, "board": a.board,
-                   "blocks": a.blocks, "channels": a.channels, "parallelism": f"game-shard x{world}",
+                   "blocks": a.blocks, "channels": a.channels, "parallelism": f"game-shard x{world}" +
+                   (f", {a.streams} streams" if getattr(a, "streams", 1) > 1 else ""),
                    "collectives": coll.kind if coll is not None else None},
         "nn_evals_per_s": tot_evals / elapsed,
         "evals_per_move": tot_evals / max(1, tot_moves),
@@ -651,6 +752,11 @@ def main(argv=None, make_workload=None, backend=None):
     if a.cpu_baseline and world == 1:
         raw_cpu = cpu_baseline(a, a.cpu_workers or cpu_share(), a.cpu_window)
         _progress(f"cpu baseline: {raw_cpu['evals_per_s']:.1f} evals/s on {raw_cpu['cores']} cores")
+    if make_workload is None and a.streams > 1:
+        if world > 1:
+            print("bench.py: --streams > 1 is an N = 1 option", file=sys.stderr)
+            return 2
+        make_workload = lambda a_, local, shard: StreamWorkload(a_, local, shard, a.streams)   # noqa: E731
     make_workload = make_workload or GpuWorkload
     dist = None
     make_coll = None

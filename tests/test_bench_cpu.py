@@ -352,3 +352,32 @@ def test_bench_engine_collectives_bootstrap_gloo_world2():
     assert ld0 is None and ld1 == float(((np.arange(777, dtype=np.float32) + 1234) * 0.25).sum())
     assert out1 is None and out0["config"]["collectives"] == "rccl (engine az_dist_*)"
     assert abs(out0["value"] - 2 * 2 * 1024 / (out0["ms_per_step"] * 2 / 1e3)) < 1e-6 * out0["value"]
+
+
+def test_bench_stream_workload_splits_games(monkeypatch):
+    """--streams K: the rank's games split into K handles with the K-way shard's seeds (game ids and
+    noise streams as a K-rank run), rank 0's weights copied into every handle's net, and a step's
+    moves / evaluations summed over the handles."""
+    import bench
+    made = []
+
+    class _W(_Workload):
+        def __init__(self, a, local, shard):
+            super().__init__(a, local, shard)
+            self.eng = object()
+            made.append(self)
+
+    monkeypatch.setattr(bench, "GpuWorkload", _W)
+    a = bench.parse(["--streams", "3", "--config", "c2"])
+    sh = {"first_game": 0, "games": 256, "noise_seed": 42, "noise_seed_stride": 1, "eval_seed": 0}
+    wl = bench.StreamWorkload(a, 0, sh, 3)
+    assert [w.shard["games"] for w in made] == [86, 85, 85]
+    assert [w.shard["noise_seed"] for w in made] == [42, 42 + 86, 42 + 171]
+    wl.net.init_random(5)
+    assert all(np.array_equal(w.net.loaded, made[0].net.blob) for w in made[1:])
+    wl.start()
+    assert wl.step() == (256, 256 * 800)
+    wl.net.set_precision(4)
+    assert all(w.net.precision == 4 for w in made)
+    assert wl.net.profile_read() == (12.0, 240, 6)
+    wl.pool.shutdown()
