@@ -423,7 +423,7 @@ class TorchColl:
         pass
 
 
-def run_rank(a, rank, world, make_workload, make_coll=None, parity=None):
+def run_rank(a, rank, world, make_workload, make_coll=None, parity=None, before_timed=None):
     """One rank of the bench: shard, weights (rank 0 init + broadcast), warmup, timed steps between
     barriers, MAX elapsed / SUM counters over ranks.  Returns the JSON dict on rank 0, else None.
     make_coll(workload) (N>1): the collectives (EngineColl on the GPUs, TorchColl in the CPU tests).
@@ -451,7 +451,7 @@ def run_rank(a, rank, world, make_workload, make_coll=None, parity=None):
     net = wl.net
     coll = make_coll(wl) if world > 1 else None
     try:
-        return _run_rank(a, rank, world, sh, wl, net, coll, parity)
+        return _run_rank(a, rank, world, sh, wl, net, coll, parity, before_timed)
     finally:
         if coll is not None:
             coll.close()
@@ -459,7 +459,7 @@ def run_rank(a, rank, world, make_workload, make_coll=None, parity=None):
             wl.close()
 
 
-def _run_rank(a, rank, world, sh, wl, net, coll, parity):
+def _run_rank(a, rank, world, sh, wl, net, coll, parity, before_timed=None):
     if rank == 0:
         net.init_random(a.seed)
     if coll is not None:
@@ -468,6 +468,8 @@ def _run_rank(a, rank, world, sh, wl, net, coll, parity):
     for k in range(a.warmup):
         wl.step()
         _progress(f"warmup step {k + 1}/{a.warmup}")
+    if before_timed is not None:
+        before_timed()                   # e.g. the CPU baseline that ran beside the setup and warm-up
 
     def barrier():
         wl.sync()
@@ -685,7 +687,8 @@ def cpu_baseline_line(a, raw, evals_per_move):
                       f"game each from the empty board (oracle/ Mode S search, {a.sims} sims/move, fp32 "
                       f"{a.blocks}b x {a.channels}f net on PyTorch-CPU, B=1 per evaluation), {raw['evals']} "
                       f"evaluations in a {raw['window_s']:.1f} s window; positions/s = evaluations/s / "
-                      f"{evals_per_move:.1f} evaluations per move (measured on the GPU run of the same workload)"}
+                      f"{evals_per_move:.1f} evaluations per move (measured on the GPU run of the same workload); "
+                      f"run beside the GPU run's setup and warm-up, joined before its timed moves"}
 
 
 def parity_line(a, pm, m):
@@ -748,10 +751,31 @@ def main(argv=None, make_workload=None, backend=None):
         return 2
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    raw_cpu = None
+    # the CPU baseline (rank 0, N = 1) runs in its own worker processes BESIDE the GPU setup and
+    # warm-up -- its 16 cores are a sixteenth of a GPU box's host, and the GPU process's host threads
+    # mostly wait on the device -- and is joined before the timed moves, which run alone
+    cpu = {}
+    cpu_thread = None
     if a.cpu_baseline and world == 1:
-        raw_cpu = cpu_baseline(a, a.cpu_workers or cpu_share(), a.cpu_window)
-        _progress(f"cpu baseline: {raw_cpu['evals_per_s']:.1f} evals/s on {raw_cpu['cores']} cores")
+        import threading
+
+        def _cpu():
+            try:
+                cpu["raw"] = cpu_baseline(a, a.cpu_workers or cpu_share(), a.cpu_window)
+            except Exception as e:  # noqa: BLE001 -- reported in the line, the GPU run goes on
+                cpu["error"] = repr(e)
+        cpu_thread = threading.Thread(target=_cpu, name="cpu-baseline")
+        cpu_thread.start()
+
+    def join_cpu():
+        nonlocal cpu_thread
+        if cpu_thread is not None:
+            cpu_thread.join()
+            cpu_thread = None
+            if "raw" in cpu:
+                _progress(f"cpu baseline: {cpu['raw']['evals_per_s']:.1f} evals/s on {cpu['raw']['cores']} cores")
+            else:
+                _progress(f"cpu baseline failed: {cpu.get('error')}")
     if make_workload is None and a.streams > 1:
         if world > 1:
             print("bench.py: --streams > 1 is an N = 1 option", file=sys.stderr)
@@ -793,9 +817,13 @@ def main(argv=None, make_workload=None, backend=None):
         parity = None
         if world == 1 and a.parity_steps > 0 and a.precision not in ("f16x3", "bf16x3") and a.channels % 64 == 0:
             parity = parity_budget(a)
-        out = run_rank(a, rank, world, make_workload, make_coll, parity=parity)
+        out = run_rank(a, rank, world, make_workload, make_coll, parity=parity, before_timed=join_cpu)
+        join_cpu()
         if out is not None:
-            out["cpu_baseline"] = cpu_baseline_line(a, raw_cpu, out["evals_per_move"]) if raw_cpu else None
+            if "raw" in cpu:
+                out["cpu_baseline"] = cpu_baseline_line(a, cpu["raw"], out["evals_per_move"])
+            else:
+                out["cpu_baseline"] = {"error": cpu["error"]} if "error" in cpu else None
             print(json.dumps(out), flush=True)
     finally:
         if dist is not None:
