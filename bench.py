@@ -123,7 +123,7 @@ def parse(argv=None):
                          "rocprofv3 --pmc stalls on a selfplay step's unsynchronised queue of dispatches "
                          "(DESIGN.md section 7); tools/tree_pmc.sh passes 100")
     ap.add_argument("--streams", type=int, default=1,
-                    help="N=1: split the games into this many device handles (own engine / HIP stream / net "
+                    help="split each rank's games into this many device handles (own engine / HIP stream / net "
                          "each) stepped concurrently by host threads (StreamWorkload)")
     ap.add_argument("--crash-report", default=None,
                     help="diagnostic: on a fault in any thread, append the thread's name, the fault address, the PC "
@@ -270,11 +270,12 @@ class _MctsGroup:
         return out
 
     def tree_evictions(self):
-        return sum(w.mcts.tree_evictions() for w in self.subs)
+        ev = [getattr(w.mcts, "tree_evictions", None) for w in self.subs]
+        return sum(f() for f in ev) if all(ev) else None
 
 
 class StreamWorkload:
-    """`--streams K` (N = 1): the rank's games split into K independent device handles, each with its
+    """`--streams K`: the rank's games split into K independent device handles, each with its
     own engine (HIP stream), net and search, stepped by K host threads at once -- so one handle's
     tree kernels and small launches run beside another's network (the games are independent; each
     keeps its global id's seeds, as a K-way shard).  For latency-bound configs (C2's 256 games, the
@@ -309,7 +310,8 @@ class StreamWorkload:
     def close(self):
         self.pool.shutdown()
         for w in self.subs:
-            w.close()
+            if hasattr(w, "close"):
+                w.close()
 
 
 def _progress(msg):
@@ -385,7 +387,12 @@ class EngineColl:
         self.kind = "rccl (engine az_dist_*)"
 
     def broadcast_weights(self, net):
-        self.d.broadcast_weights(net, 0)
+        nets = getattr(net, "nets", [net])           # a StreamWorkload's nets: into the first, then copied
+        self.d.broadcast_weights(nets[0], 0)
+        if len(nets) > 1:
+            blob = nets[0].get_weights()
+            for n in nets[1:]:
+                n.load_weights(blob)
 
     def barrier(self):
         self.d.barrier()
@@ -777,9 +784,6 @@ def main(argv=None, make_workload=None, backend=None):
             else:
                 _progress(f"cpu baseline failed: {cpu.get('error')}")
     if make_workload is None and a.streams > 1:
-        if world > 1:
-            print("bench.py: --streams > 1 is an N = 1 option", file=sys.stderr)
-            return 2
         make_workload = lambda a_, local, shard: StreamWorkload(a_, local, shard, a.streams)   # noqa: E731
     make_workload = make_workload or GpuWorkload
     dist = None

@@ -381,3 +381,51 @@ def test_bench_stream_workload_splits_games(monkeypatch):
     assert all(w.net.precision == 4 for w in made)
     assert wl.net.profile_read() == (12.0, 240, 6)
     wl.pool.shutdown()
+
+
+def _rank_streams(rank, world, port, q):
+    import torch.distributed as dist
+    import bench
+    from az_amd import dist as azdist
+    azdist.Dist = _FakeDist
+
+    class _W(_Workload):
+        def __init__(self, a, local, shard):
+            super().__init__(a, local, shard)
+            self.eng = object()
+    bench.GpuWorkload = _W
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), LOCAL_RANK=str(rank))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        a = bench.parse(["--gpus", str(world), "--steps", "2", "--warmup", "1", "--streams", "2"])
+        wls = []
+
+        def make(a_, local, shard):
+            wls.append(bench.StreamWorkload(a_, local, shard, 2))
+            return wls[-1]
+        out = bench.run_rank(a, rank, world, make, lambda wl: bench.EngineColl(wl.eng, rank, world, dist, 30.0))
+        nets = wls[0].net.nets
+        q.put((rank, out, [None if n.loaded is None else float(n.loaded.sum()) for n in nets],
+               [w.shard for w in wls[0].subs]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bench_streams_at_world2_gloo():
+    """--streams 2 on every rank of a 2-rank run: the rank's 1024 games split 512 + 512 with the
+    global ids' seeds, rank 0's weights broadcast into rank 1's first net and copied into its second."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank_streams, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted((q.get(timeout=180) for _ in procs), key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    (_, out0, ld0, sh0), (_, out1, ld1, sh1) = res
+    want = float(((np.arange(777, dtype=np.float32) + 1234) * 0.25).sum())
+    assert ld1 == [want, want] and ld0[0] is None and ld0[1] == want     # rank 0: init on net 0, copied to net 1
+    assert [s["noise_seed"] for s in sh1] == [42 + 1024, 42 + 1024 + 512] and [s["games"] for s in sh0] == [512, 512]
+    assert out0["config"]["parallelism"] == "game-shard x2, 2 streams"
