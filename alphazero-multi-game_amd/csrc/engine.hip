@@ -1593,8 +1593,8 @@ int az_engine_create(int device, az_engine** out) {
 
 void az_engine_destroy(az_engine* e) {
     if (!e) return;
-    hipSetDevice(e->device);
-    if (e->stream) hipStreamDestroy(e->stream);
+    (void)hipSetDevice(e->device);
+    if (e->stream) (void)hipStreamDestroy(e->stream);
     delete e;
 }
 
@@ -1845,8 +1845,8 @@ int az_randwire_graph(int block, int* order, int* topo, int* inputs, int* n_inpu
 
 void az_net_destroy(az_net* n) {
     if (!n) return;
-    hipSetDevice(n->e->device);
-    auto F = [](void* p) { if (p) hipFree(p); };
+    (void)hipSetDevice(n->e->device);
+    auto F = [](void* p) { if (p) (void)hipFree(p); };
     std::vector<Layer*> ls = {&n->in, &n->in32, &n->pconv, &n->vconv, &n->hconv, &n->pfc, &n->vfc1, &n->vfc2};
     for (auto& l : n->blk) ls.push_back(&l);
     for (auto& blk : n->rwb) {
@@ -2205,8 +2205,8 @@ int az_search_create(az_engine* e, az_net* net, const az_search_cfg* c, az_searc
 void az_search_destroy(az_search* s) {
     if (s) { pf_wait(s); s->pc.release(); s->pcf.release(); }
     if (!s) return;
-    hipSetDevice(s->e->device);
-    auto F = [](const void* p) { if (p) hipFree((void*)p); };
+    (void)hipSetDevice(s->e->device);
+    auto F = [](const void* p) { if (p) (void)hipFree((void*)p); };
     for (auto& nd : s->arena) { F(nd.N); F(nd.W); F(nd.VL); F(nd.P); F(nd.first); F(nd.act); F(nd.cnt); F(nd.flag); }
     TreeDev& t = s->t;
     for (const void* p : {(const void*)t.atop, (const void*)t.rboard, (const void*)t.rhist, (const void*)t.rplayer,
@@ -2229,7 +2229,7 @@ void az_search_destroy(az_search* s) {
                           (const void*)s->d_rc, (const void*)s->d_rcf, (const void*)s->d_thr, (const void*)s->d_pruned,
                           (const void*)s->d_tree})
         F(p);
-    if (s->h_tree) hipHostFree(s->h_tree);
+    if (s->h_tree) (void)hipHostFree(s->h_tree);
     delete s;
 }
 
@@ -2459,7 +2459,7 @@ int az_search_root_children(az_search* s, int game, int* actions, int* N, int* V
     if (W) HIPCHK(hipMemcpy(W, dW, n * 4, hipMemcpyDeviceToHost));
     if (P) HIPCHK(hipMemcpy(P, dP, n * 4, hipMemcpyDeviceToHost));
     *n_children = n;
-    for (void* p : {(void*)da, (void*)dN, (void*)dVL, (void*)dn, (void*)dri, (void*)dW, (void*)dP, (void*)drw}) hipFree(p);
+    for (void* p : {(void*)da, (void*)dN, (void*)dVL, (void*)dn, (void*)dri, (void*)dW, (void*)dP, (void*)drw}) (void)hipFree(p);
     return 0;
 }
 
@@ -2609,7 +2609,7 @@ int az_search_enable_eval_log(az_search* s, int game, int capacity) {
     std::lock_guard<std::mutex> lk(s->mu);
     HIPCHK(hipSetDevice(s->e->device));
     TreeDev& t = s->t;
-    if (t.log_pol) { hipFree(t.log_pol); hipFree(t.log_val); hipFree(t.log_planes); hipFree(t.log_n); }
+    if (t.log_pol) { (void)hipFree(t.log_pol); (void)hipFree(t.log_val); (void)hipFree(t.log_planes); (void)hipFree(t.log_n); }
     t.log_pol = nullptr; t.log_val = nullptr; t.log_planes = nullptr; t.log_n = nullptr;
     const int npl = t.game == GAME_GO ? 8 : 11;
     DALLOC(t.log_pol, (size_t)capacity * t.NA); DALLOC(t.log_val, capacity); DALLOC(t.log_planes, (size_t)capacity * npl * t.A);
