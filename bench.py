@@ -617,10 +617,12 @@ def cpu_share():
     return max(1, min(16, n))
 
 
-def _cpu_worker(i, desc_fields, blob_path, game, board, sims, window, barrier, q):
+def _cpu_worker(i, desc_fields, blob_path, game, board, sims, window, barrier, q, cpu=None):
     """One game on one core: oracle Mode S search, fp32 PyTorch-CPU net at B=1 per evaluation (as
     ParallelMCTS::evaluateState calls NeuralNetwork::predict), evaluations counted in the window."""
     import torch
+    if cpu is not None and hasattr(os, "sched_setaffinity"):
+        os.sched_setaffinity(0, {cpu})           # its own core, apart from the GPU process's
     torch.set_num_threads(1)
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import types
@@ -649,7 +651,7 @@ def _cpu_worker(i, desc_fields, blob_path, game, board, sims, window, barrier, q
     q.put((i, st["n"], time.perf_counter() - t0))
 
 
-def cpu_baseline(a, workers, window):
+def cpu_baseline(a, workers, window, cpus=None):
     """Raw CPU sample: {evals_per_s, cores, window, workers}; positions/s is derived after the GPU run
     from its measured evaluations per move.  Runs before anything touches the GPU."""
     import multiprocessing as mp
@@ -668,7 +670,8 @@ def cpu_baseline(a, workers, window):
         ctx = mp.get_context("spawn")
         barrier = ctx.Barrier(workers + 1)
         q = ctx.Queue()
-        procs = [ctx.Process(target=_cpu_worker, args=(i, fields, path, a.game, a.board, a.sims, window, barrier, q))
+        procs = [ctx.Process(target=_cpu_worker, args=(i, fields, path, a.game, a.board, a.sims, window, barrier, q,
+                                                         cpus[i] if cpus else None))
                  for i in range(workers)]
         for p in procs:
             p.start()
@@ -689,13 +692,14 @@ def cpu_baseline_line(a, raw, evals_per_move):
     return {"value": raw["evals_per_s"] / evals_per_move, "unit": "positions/s", "cores": raw["cores"],
             "cores_from": f"min(16, affinity {aff}, OMP_NUM_THREADS {os.environ.get('OMP_NUM_THREADS')}); "
                           f"nproc {os.cpu_count()}",
-            "kind": "port", "evals_per_s": raw["evals_per_s"],
+            "kind": "port", "evals_per_s": raw["evals_per_s"], "cpus": raw.get("cpus", "shared"),
             "sample": f"{raw['cores']} worker processes x 1 thread, one {'Go' if go else 'Gomoku'} {a.board}x{a.board} "
                       f"game each from the empty board (oracle/ Mode S search, {a.sims} sims/move, fp32 "
                       f"{a.blocks}b x {a.channels}f net on PyTorch-CPU, B=1 per evaluation), {raw['evals']} "
                       f"evaluations in a {raw['window_s']:.1f} s window; positions/s = evaluations/s / "
-                      f"{evals_per_move:.1f} evaluations per move (measured on the GPU run of the same workload); "
-                      f"run beside the GPU run's setup and warm-up, joined before its timed moves"}
+                      f"{evals_per_move:.1f} evaluations per move (measured on the GPU run of the same workload)" +
+                      ("; run on its own cores beside the GPU run's setup and warm-up, joined before its timed moves"
+                       if raw.get("cpus", "shared") != "shared" else "")}
 
 
 def parity_line(a, pm, m):
@@ -765,14 +769,28 @@ def main(argv=None, make_workload=None, backend=None):
     cpu_thread = None
     if a.cpu_baseline and world == 1:
         import threading
+        workers = a.cpu_workers or cpu_share()
+        mine = sorted(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else []
+        cpus = None
+        if len(mine) >= 4 * workers:
+            # a GPU box (256 host CPUs): the workers on the last `workers` CPUs, one each, the GPU process
+            # (every thread it starts from here on) on the first quarter -- disjoint cores, SMT siblings
+            # included whether they are numbered adjacently or half the machine apart, so neither run
+            # takes the other's; otherwise the baseline runs alone, before the GPU work
+            cpus = mine[-workers:]
+            os.sched_setaffinity(0, set(mine[:len(mine) // 4]))
 
         def _cpu():
             try:
-                cpu["raw"] = cpu_baseline(a, a.cpu_workers or cpu_share(), a.cpu_window)
+                cpu["raw"] = cpu_baseline(a, workers, a.cpu_window, cpus)
+                cpu["raw"]["cpus"] = f"{cpus[0]}..{cpus[-1]} (GPU process on {mine[0]}..{mine[len(mine) // 4 - 1]})" \
+                    if cpus else "shared"
             except Exception as e:  # noqa: BLE001 -- reported in the line, the GPU run goes on
                 cpu["error"] = repr(e)
         cpu_thread = threading.Thread(target=_cpu, name="cpu-baseline")
         cpu_thread.start()
+        if cpus is None:
+            cpu_thread.join()
 
     def join_cpu():
         nonlocal cpu_thread
