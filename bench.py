@@ -99,6 +99,9 @@ def parse(argv=None):
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU restatement on rank 0 at N=1")
     ap.add_argument("--cpu-window", type=float, default=20.0, help="seconds of the CPU baseline's timed window")
     ap.add_argument("--cpu-workers", type=int, default=0, help="CPU baseline processes (0: the host's CPU share, <=16)")
+    ap.add_argument("--cpu-beside", type=int, default=0,
+                    help="1: run the CPU baseline on its own cores beside the GPU warm-up (saves ~30 s; a GPU "
+                         "box's CPU share is a quota, so the baseline then reads 0.74-0.89x its value alone)")
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--conv-flags", default=None,
                     help="diagnostic: conv variant bits (hex) OR'd into the library's default flag set "
@@ -692,14 +695,14 @@ def cpu_baseline_line(a, raw, evals_per_move):
     return {"value": raw["evals_per_s"] / evals_per_move, "unit": "positions/s", "cores": raw["cores"],
             "cores_from": f"min(16, affinity {aff}, OMP_NUM_THREADS {os.environ.get('OMP_NUM_THREADS')}); "
                           f"nproc {os.cpu_count()}",
-            "kind": "port", "evals_per_s": raw["evals_per_s"], "cpus": raw.get("cpus", "shared"),
+            "kind": "port", "evals_per_s": raw["evals_per_s"], "cpus": raw.get("cpus", "alone"),
             "sample": f"{raw['cores']} worker processes x 1 thread, one {'Go' if go else 'Gomoku'} {a.board}x{a.board} "
                       f"game each from the empty board (oracle/ Mode S search, {a.sims} sims/move, fp32 "
                       f"{a.blocks}b x {a.channels}f net on PyTorch-CPU, B=1 per evaluation), {raw['evals']} "
                       f"evaluations in a {raw['window_s']:.1f} s window; positions/s = evaluations/s / "
                       f"{evals_per_move:.1f} evaluations per move (measured on the GPU run of the same workload)" +
                       ("; run on its own cores beside the GPU run's setup and warm-up, joined before its timed moves"
-                       if raw.get("cpus", "shared") != "shared" else "")}
+                       if raw.get("cpus", "alone") != "alone" else "; run alone, before the GPU work")}
 
 
 def parity_line(a, pm, m):
@@ -762,9 +765,10 @@ def main(argv=None, make_workload=None, backend=None):
         return 2
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    # the CPU baseline (rank 0, N = 1) runs in its own worker processes BESIDE the GPU setup and
-    # warm-up -- its 16 cores are a sixteenth of a GPU box's host, and the GPU process's host threads
-    # mostly wait on the device -- and is joined before the timed moves, which run alone
+    # the CPU baseline (rank 0, N = 1) runs in its own worker processes, alone, before the GPU work.
+    # --cpu-beside 1 runs it beside the GPU setup and warm-up instead (joined before the timed moves),
+    # but a GPU box's 16-CPU share is a quota that both then draw on: measured 310 evals/s unpinned and
+    # 259 pinned to CPUs of their own, against 349 alone (profiles/r06_bench_c3_cpu_pinned.json)
     cpu = {}
     cpu_thread = None
     if a.cpu_baseline and world == 1:
@@ -772,11 +776,11 @@ def main(argv=None, make_workload=None, backend=None):
         workers = a.cpu_workers or cpu_share()
         mine = sorted(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else []
         cpus = None
-        if len(mine) >= 4 * workers:
+        if a.cpu_beside and len(mine) >= 4 * workers:
             # a GPU box (256 host CPUs): the workers on the last `workers` CPUs, one each, the GPU process
             # (every thread it starts from here on) on the first quarter -- disjoint cores, SMT siblings
             # included whether they are numbered adjacently or half the machine apart, so neither run
-            # takes the other's; otherwise the baseline runs alone, before the GPU work
+            # takes the other's CPUs (though both draw on the same quota)
             cpus = mine[-workers:]
             os.sched_setaffinity(0, set(mine[:len(mine) // 4]))
 
@@ -784,7 +788,7 @@ def main(argv=None, make_workload=None, backend=None):
             try:
                 cpu["raw"] = cpu_baseline(a, workers, a.cpu_window, cpus)
                 cpu["raw"]["cpus"] = f"{cpus[0]}..{cpus[-1]} (GPU process on {mine[0]}..{mine[len(mine) // 4 - 1]})" \
-                    if cpus else "shared"
+                    if cpus else "alone"
             except Exception as e:  # noqa: BLE001 -- reported in the line, the GPU run goes on
                 cpu["error"] = repr(e)
         cpu_thread = threading.Thread(target=_cpu, name="cpu-baseline")
