@@ -1371,8 +1371,8 @@ __global__ __launch_bounds__(512, 1) void conv3x3_v6(ConvBf16Args p) {
             // streaming (nt) loads: the residual is read once (-2% trunk time at C3)
             const __amdgpu_buffer_rsrc_t rh = __builtin_amdgcn_make_buffer_rsrc((void*)p.Rhi, (short)0, 0x7fffffff, 0x00020000);
             const __amdgpu_buffer_rsrc_t rqq = __builtin_amdgcn_make_buffer_rsrc((void*)p.Rq, (short)0, 0x7fffffff, 0x00020000);
-            const u32x4_t h = __builtin_amdgcn_raw_buffer_load_b128(rh, (int)(e * 2), 0, 2);
-            const u32x2_t q = __builtin_amdgcn_raw_buffer_load_b64(rqq, (int)e, 0, 2);
+            const u32x4_t h = __builtin_amdgcn_raw_buffer_load_b128(rh, (int)(e * 2), 0, AZ_RES_AUX);
+            const u32x2_t q = __builtin_amdgcn_raw_buffer_load_b64(rqq, (int)e, 0, AZ_RES_AUX);
             __builtin_memcpy(&rr.h, &h, 16);
             __builtin_memcpy(&rr.q, &q, 8);
         }

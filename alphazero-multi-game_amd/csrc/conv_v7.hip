@@ -429,34 +429,51 @@ __global__ __launch_bounds__(256, RG == 3 ? 3 : 2) void conv3x3_v7(ConvBf16Args 
     const __amdgpu_buffer_rsrc_t rq = __builtin_amdgcn_make_buffer_rsrc((void*)p.Rq, (short)0, 0x7fffffff, 0x00020000);
     const int chl = n0 + wn * 64 + 4 * lg;                // first channel of the lane in tile j = 0
     float vmax = 0.0f;                                    // fp16: the largest output (the range guard)
-#pragma unroll
-    for (int i = 0; i < NI; ++i) {
+    auto locate = [&](int i, int& b, int& pix) -> bool {  // fragment row i of the lane: board, pixel, live
         const int q = wm * WR + i * 16 + l16;             // output grid row of the tile
-        int b, pix;
-        bool live;
         if constexpr (DENSE) {
             const int gq = tile * TM + q;
             b = gq / HW;
             pix = gq - b * HW;
-            live = b < nboards;
+            return b < nboards;
         } else {
             const int y = q / WG, x = q - y * WG;
             b = tile;
             pix = y * HB + x;
-            live = y < HB && x < HB;
+            return y < HB && x < HB;
         }
-        if (!live) continue;
-        u32x2_t hv[4];
-        uint32_t qv[4];
-        if (p.Rhi) {
+    };
+    // The residual join's loads go out EB fragment rows at a time (one memory round trip per burst,
+    // two per wave at NI = 8), not one round trip per row: each row's loads would otherwise wait
+    // behind the previous row's stores (the asm stores are memory barriers to the compiler), and a
+    // 2nd conv's epilogue was eight serial HBM round trips per wave (conv2 498 us vs conv1 423 us per
+    // C3 launch under PMC, profiles/r06_c3_fp16_pmc_calib.json).  <= 48 VGPRs per burst; the
+    // arithmetic and the stored values are unchanged.
+    constexpr int EB = NI <= 4 ? NI : NI % 4 == 0 ? 4 : NI % 3 == 0 ? 3 : NI % 2 == 0 ? 2 : 1;
+    static_assert(NI % EB == 0, "bursts");
+#pragma unroll
+    for (int i0 = 0; i0 < NI; i0 += EB) {
+    u32x2_t hv[EB][4];
+    uint32_t qv[EB][4];
+    if (p.Rhi) {
+#pragma unroll
+        for (int ii = 0; ii < EB; ++ii) {
+            int b, pix;
+            if (!locate(i0 + ii, b, pix)) continue;
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 const int ch = chl + j * 16;
                 const size_t e = (((size_t)b * GO + (ch >> 3)) * HW + pix) * 8 + (ch & 7);
-                hv[j] = __builtin_amdgcn_raw_buffer_load_b64(rh, (int)(e * 2), 0, 2);
-                qv[j] = __builtin_amdgcn_raw_buffer_load_b32(rq, (int)e, 0, 2);
+                hv[ii][j] = __builtin_amdgcn_raw_buffer_load_b64(rh, (int)(e * 2), 0, AZ_RES_AUX);
+                qv[ii][j] = __builtin_amdgcn_raw_buffer_load_b32(rq, (int)e, 0, AZ_RES_AUX);
             }
         }
+    }
+#pragma unroll
+    for (int ii = 0; ii < EB; ++ii) {
+        const int i = i0 + ii;
+        int b, pix;
+        if (!locate(i, b, pix)) continue;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const int ch = chl + j * 16;
@@ -465,8 +482,8 @@ __global__ __launch_bounds__(256, RG == 3 ? 3 : 2) void conv3x3_v7(ConvBf16Args 
             if (p.Rhi) {
                 uint16_t hh[4];
                 int8_t qq[4];
-                __builtin_memcpy(hh, &hv[j], 8);
-                __builtin_memcpy(qq, &qv[j], 4);
+                __builtin_memcpy(hh, &hv[ii][j], 8);
+                __builtin_memcpy(qq, &qv[ii][j], 4);
 #pragma unroll
                 for (int k = 0; k < 4; ++k) o[k] += H::join(hh[k], qq[k]);
             }
@@ -488,6 +505,7 @@ __global__ __launch_bounds__(256, RG == 3 ? 3 : 2) void conv3x3_v7(ConvBf16Args 
                 asm volatile("global_store_dword %0, %1, off nt" ::"v"(p.Cq + e), "v"(qs) : "memory");
             }
         }
+    }
     }
     if (MODE == 2 && !(vmax <= 65504.0f) && p.ovf) atomicOr(p.ovf, 1);   // fp16 overflow: the engine fails the forward
 }
@@ -774,8 +792,8 @@ __global__ __launch_bounds__(256, 1) void conv3x3_v7x3(ConvBf16Args p) {
             for (int j = 0; j < 4; ++j) {
                 const int ch = chl + j * 16;
                 const size_t e = (((size_t)b * GO + (ch >> 3)) * HW + pix) * 8 + (ch & 7);
-                hv[j] = __builtin_amdgcn_raw_buffer_load_b64(rh, (int)(e * 2), 0, 2);
-                lv[j] = __builtin_amdgcn_raw_buffer_load_b64(rl, (int)(e * 2), 0, 2);
+                hv[j] = __builtin_amdgcn_raw_buffer_load_b64(rh, (int)(e * 2), 0, AZ_RES_AUX);
+                lv[j] = __builtin_amdgcn_raw_buffer_load_b64(rl, (int)(e * 2), 0, AZ_RES_AUX);
             }
         }
 #pragma unroll
@@ -1144,8 +1162,8 @@ __global__ __launch_bounds__(512, 1) void conv3x3_v9x3(ConvBf16Args p) {
             for (int j = 0; j < 4; ++j) {
                 const int ch = chl + j * 16;
                 const size_t e = (((size_t)b * GO + (ch >> 3)) * HW + pix) * 8 + (ch & 7);
-                hv[ii][j] = __builtin_amdgcn_raw_buffer_load_b64(rh, (int)(e * 2), 0, 2);
-                lv[ii][j] = __builtin_amdgcn_raw_buffer_load_b64(rl, (int)(e * 2), 0, 2);
+                hv[ii][j] = __builtin_amdgcn_raw_buffer_load_b64(rh, (int)(e * 2), 0, AZ_RES_AUX);
+                lv[ii][j] = __builtin_amdgcn_raw_buffer_load_b64(rl, (int)(e * 2), 0, AZ_RES_AUX);
             }
         }
     };

@@ -5,6 +5,12 @@
 
 enum { ACT_NONE = 0, ACT_RELU = 1, ACT_TANH = 2 };
 
+// cache-policy bits of the trunk convs' residual-join loads (raw buffer loads of the g8 planes in the
+// epilogue; gfx950 CPol: 1 sc0, 2 nt, 16 sc1)
+#ifndef AZ_RES_AUX
+#define AZ_RES_AUX 2
+#endif
+
 // out[m][n] = act( sum_k A(m,k) * B[n][k] + bias[n] (+ res[m][n]) ),  k = tap*C + c
 struct GemmArgs {
     const float* A; int lda;        // activations, row-major [rows][lda] (NHWC for convs)
