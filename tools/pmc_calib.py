@@ -46,7 +46,7 @@ def main():
     a = ap.parse_args()
     res = {"kernel": a.kernel, "workload": "tools/net_bench.py --game gomoku15 --batch 2048 --precision fp16",
            "algorithmic_bytes": ALG, "classes": {}}
-    for sub in ("fetch", "req", "hit", "write"):
+    for sub in ("fetch", "req", "hit", "write", "wrreq"):
         d = dispatches(os.path.join(a.dir, sub), a.kernel)
         if not d:
             continue
@@ -70,6 +70,10 @@ def main():
         if "TCC_EA0_RDREQ_64B_sum" in c and "TCC_EA0_RDREQ_128B_sum" in c:
             c["rdreq_bytes"] = 64 * c["TCC_EA0_RDREQ_64B_sum"] + 128 * c["TCC_EA0_RDREQ_128B_sum"]
             c["rdreq_bytes_over_alg"] = c["rdreq_bytes"] / alg["read"]
+        if "TCC_EA0_WRREQ_sum" in c and "TCC_EA0_WRREQ_64B_sum" in c:   # 32-B and 64-B write requests
+            n, n64 = c["TCC_EA0_WRREQ_sum"], c["TCC_EA0_WRREQ_64B_sum"]
+            c["wrreq_bytes"] = 64 * n64 + 32 * (n - n64)
+            c["wrreq_bytes_over_alg"] = c["wrreq_bytes"] / alg["write"]
         if "TCC_HIT_sum" in c and "TCC_MISS_sum" in c:
             c["l2_hit_rate"] = c["TCC_HIT_sum"] / max(1.0, c["TCC_HIT_sum"] + c["TCC_MISS_sum"])
     k1, k2 = res["classes"].get("conv1", {}), res["classes"].get("conv2", {})
