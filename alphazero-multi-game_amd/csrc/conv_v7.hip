@@ -31,6 +31,14 @@
 
 #include "net.h"
 
+// conv3x3_v7's output stores: streaming (nt) by default; AZ_V7_ST_PLAIN=1 builds plain stores (A/B of
+// the row-boundary partial writes)
+#if defined(AZ_V7_ST_PLAIN) && AZ_V7_ST_PLAIN
+#define AZ_V7_ST ""
+#else
+#define AZ_V7_ST " nt"
+#endif
+
 namespace {
 
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
@@ -498,11 +506,11 @@ __global__ __launch_bounds__(256, RG == 3 ? 3 : 2) void conv3x3_v7(ConvBf16Args 
             }
             u32x2_t hs;
             __builtin_memcpy(&hs, oh, 8);
-            asm volatile("global_store_dwordx2 %0, %1, off nt" ::"v"(p.Chi + e), "v"(hs) : "memory");
+            asm volatile("global_store_dwordx2 %0, %1, off" AZ_V7_ST ::"v"(p.Chi + e), "v"(hs) : "memory");
             if (p.Cq) {
                 uint32_t qs;
                 __builtin_memcpy(&qs, oq, 4);
-                asm volatile("global_store_dword %0, %1, off nt" ::"v"(p.Cq + e), "v"(qs) : "memory");
+                asm volatile("global_store_dword %0, %1, off" AZ_V7_ST ::"v"(p.Cq + e), "v"(qs) : "memory");
             }
         }
     }
